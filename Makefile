@@ -1,0 +1,41 @@
+# Build recipe (no cmake): hipcc for the product library, gcc for the oracle.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+CXXFLAGS = -O3 -std=c++17 -fPIC -Wall -Wno-unused-function
+LIB = regex_amd/lib/librure_amd.so
+HOST_SRC = regex_amd/csrc/host/syntax.cpp regex_amd/csrc/host/compile.cpp regex_amd/csrc/host/dfa_build.cpp
+RT_SRC = regex_amd/csrc/rure_amd.cpp
+KERNEL_SRC = regex_amd/csrc/kernels/dfa_scan.hip
+HDRS = $(wildcard regex_amd/csrc/host/*.hpp regex_amd/csrc/host/*.h regex_amd/csrc/kernels/*.hpp include/*.h)
+OBJDIR = regex_amd/build
+HOST_OBJ = $(patsubst regex_amd/csrc/host/%.cpp,$(OBJDIR)/%.o,$(HOST_SRC))
+
+ORACLE_LIB = oracle/build/liboracle.so
+ORACLE_SRC = $(wildcard oracle/*.c)
+
+all: $(LIB) $(ORACLE_LIB)
+
+$(OBJDIR)/%.o: regex_amd/csrc/host/%.cpp $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(CXXFLAGS) -c $< -o $@
+
+$(OBJDIR)/rure_amd.o: $(RT_SRC) $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(CXXFLAGS) -c $< -o $@
+
+$(OBJDIR)/dfa_scan.o: $(KERNEL_SRC) $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(CXXFLAGS) --offload-arch=$(ARCH) -c $< -o $@
+
+$(LIB): $(HOST_OBJ) $(OBJDIR)/rure_amd.o $(OBJDIR)/dfa_scan.o
+	@mkdir -p regex_amd/lib
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^
+
+$(ORACLE_LIB): $(ORACLE_SRC) $(wildcard oracle/*.h)
+	@mkdir -p oracle/build
+	gcc -O2 -std=c11 -fPIC -shared -Wall -o $@ $(ORACLE_SRC) -lpthread
+
+clean:
+	rm -rf regex_amd/build regex_amd/lib oracle/build
+
+.PHONY: all clean

@@ -1,0 +1,165 @@
+/*
+ * rure_amd.h — MI355X drop-in for the batched byte-regex scan path of the
+ * reference `rure` C API (regex 0.2.5, regex-capi/include/rure.h).
+ *
+ * Part 1 re-declares the `rure` entry points a C caller of the reference
+ * binds, with the same names, argument meaning, flag values and ownership
+ * rules; each cites the reference declaration it replaces.  Every search
+ * entry point runs on the GPU (HIP kernels for gfx950); there is no CPU
+ * matching path inside this library.
+ *
+ * Part 2 adds the batched device-pointer entry points the hot path needs
+ * (one call scans many haystacks resident in HBM).  Plain pointers and sizes
+ * only; `stream` is a `hipStream_t` passed as `void *` (NULL = the null
+ * stream).
+ */
+#ifndef RURE_AMD_H
+#define RURE_AMD_H
+
+#include <stdbool.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------- Part 1 */
+
+typedef struct rure rure;                  /* rure.h:29 */
+typedef struct rure_set rure_set;          /* rure.h:36 */
+typedef struct rure_options rure_options;  /* rure.h:47 */
+typedef struct rure_iter rure_iter;        /* rure.h:106 */
+typedef struct rure_error rure_error;      /* rure.h:127 */
+
+/* rure.h:56-68 */
+#define RURE_FLAG_CASEI (1 << 0)
+#define RURE_FLAG_MULTI (1 << 1)
+#define RURE_FLAG_DOTNL (1 << 2)
+#define RURE_FLAG_SWAP_GREED (1 << 3)
+#define RURE_FLAG_SPACE (1 << 4)
+#define RURE_FLAG_UNICODE (1 << 5)
+#define RURE_DEFAULT_FLAGS RURE_FLAG_UNICODE
+
+/* rure.h:73-78 */
+typedef struct rure_match {
+  size_t start;
+  size_t end;
+} rure_match;
+
+/* rure.h:147 — aborts (after printing the error) if the pattern is invalid. */
+rure *rure_compile_must(const char *pattern);
+/* rure.h:168-170 — NULL on error (error filled if non-NULL). */
+rure *rure_compile(const uint8_t *pattern, size_t length, uint32_t flags,
+                   rure_options *options, rure_error *error);
+/* rure.h:175 */
+void rure_free(rure *re);
+/* rure.h:197-198 */
+bool rure_is_match(rure *re, const uint8_t *haystack, size_t length, size_t start);
+/* rure.h:217-218 — `match` may be NULL. */
+bool rure_find(rure *re, const uint8_t *haystack, size_t length, size_t start,
+               rure_match *match);
+/* rure.h:264-265 */
+bool rure_shortest_match(rure *re, const uint8_t *haystack, size_t length,
+                         size_t start, size_t *end);
+/* rure.h:317-330 — iterator over successive non-overlapping matches. */
+rure_iter *rure_iter_new(rure *re);
+void rure_iter_free(rure_iter *it);
+bool rure_iter_next(rure_iter *it, const uint8_t *haystack, size_t length,
+                    rure_match *match);
+/* rure.h:423-454 */
+rure_options *rure_options_new(void);
+void rure_options_free(rure_options *options);
+void rure_options_size_limit(rure_options *options, size_t limit);
+void rure_options_dfa_size_limit(rure_options *options, size_t limit);
+/* rure.h:476-538 */
+rure_set *rure_compile_set(const uint8_t **patterns, const size_t *patterns_lengths,
+                           size_t patterns_count, uint32_t flags,
+                           rure_options *options, rure_error *error);
+void rure_set_free(rure_set *re);
+bool rure_set_is_match(rure_set *re, const uint8_t *haystack, size_t length, size_t start);
+bool rure_set_matches(rure_set *re, const uint8_t *haystack, size_t length, size_t start,
+                      bool *matches);
+size_t rure_set_len(rure_set *re);
+/* rure.h:551-568 */
+rure_error *rure_error_new(void);
+void rure_error_free(rure_error *err);
+const char *rure_error_message(rure_error *err);
+
+/* ---------------------------------------------------------------- Part 2 */
+
+/* Status codes of the batched calls. */
+#define RURE_AMD_OK 0
+#define RURE_AMD_ERR_ARG (-1)        /* bad argument */
+#define RURE_AMD_ERR_HIP (-2)        /* HIP runtime error (no device, launch failure) */
+#define RURE_AMD_ERR_DFA (-3)        /* automaton could not be materialized */
+
+/* A batch of haystacks resident in device memory.  Haystack i is
+ *   bytes [offsets[i], offsets[i+1])            when offsets != NULL, else
+ *   bytes [i*stride, i*stride + length)         (fixed stride).
+ * The search in every haystack starts at `start` (with look-behind context,
+ * like rure_find's `start`, rure.h:186-192).  Offsets in results are relative
+ * to the haystack's first byte. */
+typedef struct rure_amd_batch {
+  const uint8_t *haystack;
+  const uint64_t *offsets;
+  size_t stride;
+  size_t length;
+  size_t count;
+  size_t start;
+} rure_amd_batch;
+
+/* Batched rure_find: out[i] = leftmost-first match, or {SIZE_MAX, SIZE_MAX}. */
+int rure_amd_find_batch(rure *re, const rure_amd_batch *batch, rure_match *out, void *stream);
+/* Batched rure_is_match: out[i] in {0, 1}. */
+int rure_amd_is_match_batch(rure *re, const rure_amd_batch *batch, uint8_t *out, void *stream);
+/* Batched rure_shortest_match: end[i] or SIZE_MAX. */
+int rure_amd_shortest_match_batch(rure *re, const rure_amd_batch *batch, size_t *end, void *stream);
+/* Batched rure_set_matches: bit j of mask[i] set iff pattern j matches (<= 64 patterns). */
+int rure_amd_set_matches_batch(rure_set *re, const rure_amd_batch *batch, uint64_t *mask,
+                               void *stream);
+
+/* Diagnostics (host only, no GPU needed). */
+typedef struct rure_amd_dfa_info {
+  int32_t ok;            /* 1 if the automaton was materialized */
+  int32_t states;        /* minimised states incl. dead/quit */
+  int32_t raw_states;    /* lazy-DFA states before minimisation */
+  int32_t normal;        /* [0, normal) carry no match flag */
+  int32_t match_end;     /* [normal, match_end) carry the match flag */
+  int32_t dead;
+  int32_t quit;          /* -1 if none */
+  int32_t hot;           /* states held in the LDS fast table */
+  int32_t byte_classes;
+  int32_t insts;
+} rure_amd_dfa_info;
+/* which: 0 = forward DFA program, 1 = reverse DFA program. */
+int rure_amd_dfa_info_get(rure *re, int which, rure_amd_dfa_info *info);
+int rure_amd_set_dfa_info_get(rure_set *re, rure_amd_dfa_info *info);
+
+/* Export of the compiled byte programs (the reference's Program/Inst
+ * contract, prog.rs:18-75, 261-425) as flat 12-byte records, for the CPU
+ * oracle and tests.  which: 0 = forward DFA program (with `.*?`),
+ * 1 = reverse DFA program, 2 = NFA program (with capture saves).
+ * Returns the number of instructions; copies at most `cap` records. */
+typedef struct rure_amd_inst {
+  uint8_t op, look, lo, hi;
+  uint32_t x, y;
+} rure_amd_inst;
+typedef struct rure_amd_prog_info {
+  uint32_t ninsts, start, nmatches, ncaptures;
+  uint8_t anchored_start, anchored_end, has_unicode_word_boundary, is_reverse;
+  uint8_t byte_classes[256];
+} rure_amd_prog_info;
+int64_t rure_amd_program_export(rure *re, int which, rure_amd_prog_info *info,
+                                rure_amd_inst *insts, size_t cap);
+int64_t rure_amd_set_program_export(rure_set *re, int which, rure_amd_prog_info *info,
+                                    rure_amd_inst *insts, size_t cap);
+/* Export of a materialized DFA: trans = states*256 u32, eof_match = states
+ * bytes, start = 128 u32. */
+int rure_amd_dfa_export(rure *re, int which, uint32_t *trans, uint8_t *eof_match,
+                        uint32_t *start);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RURE_AMD_H */

@@ -1,0 +1,285 @@
+/*
+ * TEST INFRASTRUCTURE ONLY.  Restatement of the reference dispatcher for
+ * the DFA match types, src/exec.rs:
+ *   shortest_match_at  382-420   (Dfa arm; Quit -> shortest_nfa)
+ *   is_match_at        427-468   (Dfa arm; Quit -> match_nfa)
+ *   find_at            473-514   (Dfa arm; Quit -> find_nfa)
+ *   find_dfa_forward   632-662
+ *   many_matches_at    998-1038  (DfaMany arm; Quit -> exec_nfa)
+ * and the iteration rule of src/re_trait.rs:197-221 (Matches::next).
+ * Engine choice (literal / DFA / NFA) is result-neutral in the reference
+ * (HACKING.md:60-61), so the DFA arms stand for every match type.
+ */
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "oracle_int.h"
+
+#define R_MATCH 0
+#define R_NOMATCH 1
+#define R_QUIT 2
+
+orc_prog *orc_prog_new(const orc_inst *insts, uint32_t n, uint32_t start, const uint8_t *byte_classes,
+                       int is_reverse, int anchored_start, int anchored_end, int has_uwb, uint32_t ncaps,
+                       size_t dfa_size_limit) {
+  orc_prog *p = (orc_prog *)calloc(1, sizeof(orc_prog));
+  p->insts = (orc_inst *)malloc((n ? n : 1) * sizeof(orc_inst));
+  memcpy(p->insts, insts, n * sizeof(orc_inst));
+  p->n = n;
+  p->start = start;
+  memcpy(p->byte_classes, byte_classes, 256);
+  p->is_reverse = is_reverse;
+  p->anchored_start = anchored_start;
+  p->anchored_end = anchored_end;
+  p->has_uwb = has_uwb;
+  p->ncaps = ncaps;
+  p->dfa_size_limit = dfa_size_limit;
+  for (uint32_t i = 0; i < n; ++i) if (insts[i].op == OP_MATCH) p->nmatches++;
+  return p;
+}
+
+void orc_prog_free(orc_prog *p) {
+  if (!p) return;
+  free(p->insts);
+  free(p);
+}
+
+orc_regex *orc_regex_new(orc_prog *nfa, orc_prog *fwd, orc_prog *rev) {
+  orc_regex *r = (orc_regex *)calloc(1, sizeof(orc_regex));
+  r->nfa = nfa;
+  r->fwd = fwd;
+  r->rev = rev;
+  return r;
+}
+
+void orc_regex_free(orc_regex *r) {
+  if (!r) return;
+  orc_prog_free(r->nfa);
+  orc_prog_free(r->fwd);
+  orc_prog_free(r->rev);
+  free(r);
+}
+
+orc_cache *orc_cache_new(const orc_regex *r) {
+  orc_cache *c = (orc_cache *)calloc(1, sizeof(orc_cache));
+  if (r->fwd) c->fwd = orc_dfa_cache_new(r->fwd);
+  if (r->rev) c->rev = orc_dfa_cache_new(r->rev);
+  if (r->nfa) c->pike = orc_pike_cache_new(r->nfa);
+  return c;
+}
+
+void orc_cache_free(orc_cache *c) {
+  if (!c) return;
+  orc_dfa_cache_free(c->fwd);
+  orc_dfa_cache_free(c->rev);
+  orc_pike_cache_free(c->pike);
+  free(c);
+}
+
+void orc_cache_stats(const orc_cache *c, orc_stats *out) {
+  *out = c->st;
+  out->flushes = (c->fwd ? c->fwd->stat_flushes : 0) + (c->rev ? c->rev->stat_flushes : 0);
+  out->states = c->fwd ? orc_dfa_cache_nstates(c->fwd) : 0;
+}
+
+void orc_cache_reset_stats(orc_cache *c) { memset(&c->st, 0, sizeof(c->st)); }
+
+/* exec.rs:840-855 find_nfa (Pike VM, slots [None, None]) */
+int orc_find_nfa(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t len, size_t start, size_t *ms,
+                 size_t *me) {
+  uint8_t m[1] = {0};
+  size_t slots[2] = {SIZE_MAX, SIZE_MAX};
+  if (!orc_pike_exec(r->nfa, c->pike, m, 1, slots, 2, 0, text, len, start)) return 0;
+  if (slots[0] == SIZE_MAX || slots[1] == SIZE_MAX) return 0;
+  *ms = slots[0];
+  *me = slots[1];
+  return 1;
+}
+
+int orc_captures_nfa(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t len, size_t start, size_t *slots,
+                     size_t nslots) {
+  uint8_t m[1] = {0};
+  for (size_t i = 0; i < nslots; ++i) slots[i] = SIZE_MAX;
+  return orc_pike_exec(r->nfa, c->pike, m, 1, slots, nslots, 0, text, len, start);
+}
+
+/* exec.rs:632-662 find_dfa_forward */
+static int find_dfa_forward(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t len, size_t start,
+                            size_t *ms, size_t *me) {
+  size_t end, stop;
+  int k = orc_dfa_forward(r->fwd, c->fwd, 0, text, len, start, &end, &stop);
+  c->st.fwd_bytes += stop - start;
+  if (k != R_MATCH) return k;
+  if (end == start) { *ms = start; *me = start; return R_MATCH; }
+  size_t s, consumed;
+  int k2 = orc_dfa_reverse(r->rev, c->rev, 0, text + start, len - start, end - start, &s, &consumed);
+  c->st.rev_bytes += consumed;
+  if (k2 != R_MATCH) return k2;
+  *ms = start + s;
+  *me = end;
+  return R_MATCH;
+}
+
+int orc_find_at(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t len, size_t start, size_t *ms,
+                size_t *me) {
+  if (start > len) return 0;
+  int k = find_dfa_forward(r, c, text, len, start, ms, me);
+  if (k == R_MATCH) return 1;
+  if (k == R_NOMATCH) return 0;
+  c->st.quits++;
+  return orc_find_nfa(r, c, text, len, start, ms, me);
+}
+
+int orc_shortest_match_at(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t len, size_t start,
+                          size_t *end) {
+  if (start > len) return 0;
+  size_t e, stop;
+  int k = orc_dfa_forward(r->fwd, c->fwd, 1, text, len, start, &e, &stop);
+  c->st.fwd_bytes += stop - start;
+  if (k == R_MATCH) { *end = e; return 1; }
+  if (k == R_NOMATCH) return 0;
+  c->st.quits++;
+  /* exec.rs:825-837 shortest_nfa: quit_after_match Pike VM, slots[1] */
+  uint8_t m[1] = {0};
+  size_t slots[2] = {SIZE_MAX, SIZE_MAX};
+  if (!orc_pike_exec(r->nfa, c->pike, m, 1, slots, 2, 1, text, len, start)) return 0;
+  if (slots[1] == SIZE_MAX) return 0;
+  *end = slots[1];
+  return 1;
+}
+
+int orc_is_match_at(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t len, size_t start) {
+  if (start > len) return 0;
+  size_t e, stop;
+  int k = orc_dfa_forward(r->fwd, c->fwd, 1, text, len, start, &e, &stop);
+  c->st.fwd_bytes += stop - start;
+  if (k == R_MATCH) return 1;
+  if (k == R_NOMATCH) return 0;
+  c->st.quits++;
+  uint8_t m[1] = {0};
+  return orc_pike_exec(r->nfa, c->pike, m, 1, NULL, 0, 1, text, len, start);
+}
+
+int orc_many_matches_nfa(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t len, size_t start,
+                         uint8_t *matches) {
+  return orc_pike_exec(r->nfa, c->pike, matches, r->nfa->nmatches, NULL, 0, 0, text, len, start);
+}
+
+int orc_many_matches_at(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t len, size_t start,
+                        uint8_t *matches) {
+  if (start > len) return 0;
+  size_t pos, stop;
+  int k = orc_dfa_forward_many(r->fwd, c->fwd, matches, text, len, start, &pos, &stop);
+  c->st.fwd_bytes += stop - start;
+  if (k == R_MATCH) return 1;
+  if (k == R_NOMATCH) return 0;
+  c->st.quits++;
+  return orc_many_matches_nfa(r, c, text, len, start, matches);
+}
+
+int64_t orc_find_iter(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t len, size_t *pairs,
+                      size_t cap) {  /* re_trait.rs:197-221 */
+  size_t last_end = 0;
+  int has_last = 0;
+  size_t last_match = 0;
+  int64_t count = 0;
+  for (;;) {
+    if (last_end > len) break;
+    size_t s, e;
+    if (!orc_find_at(r, c, text, len, last_end, &s, &e)) break;
+    if (s == e) {
+      last_end = e + 1;  /* next_after_empty for bytes (exec.rs:375-377) */
+      if (has_last && last_match == e) continue;
+    } else {
+      last_end = e;
+    }
+    has_last = 1;
+    last_match = e;
+    if ((size_t)count < cap) { pairs[2 * count] = s; pairs[2 * count + 1] = e; }
+    count++;
+  }
+  return count;
+}
+
+/* ---------------------------------------------------------- batch baseline */
+typedef struct {
+  const orc_regex *r;
+  const uint8_t *buf;
+  const uint64_t *offs;
+  size_t stride, length, lo, hi;
+  int mode;  /* 0 find, 1 is_match, 2 set */
+  uint64_t *out;
+  uint8_t *out8;
+  orc_stats st;
+} Job;
+
+static void *worker(void *arg) {
+  Job *j = (Job *)arg;
+  orc_cache *c = orc_cache_new(j->r);
+  uint8_t matches[64];
+  for (size_t i = j->lo; i < j->hi; ++i) {
+    const uint8_t *t;
+    size_t len;
+    if (j->offs) { t = j->buf + j->offs[i]; len = (size_t)(j->offs[i + 1] - j->offs[i]); }
+    else { t = j->buf + i * j->stride; len = j->length; }
+    if (j->mode == 0) {
+      size_t s, e;
+      if (orc_find_at(j->r, c, t, len, 0, &s, &e)) { j->out[2 * i] = s; j->out[2 * i + 1] = e; }
+      else { j->out[2 * i] = UINT64_MAX; j->out[2 * i + 1] = UINT64_MAX; }
+    } else if (j->mode == 1) {
+      j->out8[i] = (uint8_t)orc_is_match_at(j->r, c, t, len, 0);
+    } else {
+      uint32_t nm = j->r->fwd->nmatches;
+      memset(matches, 0, sizeof(matches));
+      orc_many_matches_at(j->r, c, t, len, 0, matches);
+      uint64_t m = 0;
+      for (uint32_t k = 0; k < nm && k < 64; ++k) if (matches[k]) m |= 1ull << k;
+      j->out[i] = m;
+    }
+  }
+  j->st = c->st;
+  orc_cache_free(c);
+  return NULL;
+}
+
+static int run_batch(const orc_regex *r, const uint8_t *buf, const uint64_t *offs, size_t stride, size_t length,
+                     size_t n, int nthreads, int mode, uint64_t *out, uint8_t *out8, orc_stats *stats) {
+  if (nthreads < 1) nthreads = 1;
+  if ((size_t)nthreads > n && n > 0) nthreads = (int)n;
+  Job *jobs = (Job *)calloc((size_t)nthreads, sizeof(Job));
+  pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+  size_t per = (n + nthreads - 1) / (nthreads ? nthreads : 1);
+  for (int k = 0; k < nthreads; ++k) {
+    Job *j = &jobs[k];
+    j->r = r; j->buf = buf; j->offs = offs; j->stride = stride; j->length = length;
+    j->lo = (size_t)k * per; j->hi = j->lo + per; if (j->hi > n) j->hi = n; if (j->lo > n) j->lo = n;
+    j->mode = mode; j->out = out; j->out8 = out8;
+    if (nthreads == 1) worker(j); else pthread_create(&th[k], NULL, worker, j);
+  }
+  if (stats) memset(stats, 0, sizeof(*stats));
+  for (int k = 0; k < nthreads; ++k) {
+    if (nthreads > 1) pthread_join(th[k], NULL);
+    if (stats) {
+      stats->fwd_bytes += jobs[k].st.fwd_bytes;
+      stats->rev_bytes += jobs[k].st.rev_bytes;
+      stats->quits += jobs[k].st.quits;
+    }
+  }
+  free(jobs);
+  free(th);
+  return 0;
+}
+
+int orc_find_batch(const orc_regex *r, const uint8_t *buf, const uint64_t *offs, size_t stride, size_t length,
+                   size_t n, int nthreads, uint64_t *out_pairs, orc_stats *stats) {
+  return run_batch(r, buf, offs, stride, length, n, nthreads, 0, out_pairs, NULL, stats);
+}
+int orc_is_match_batch(const orc_regex *r, const uint8_t *buf, const uint64_t *offs, size_t stride, size_t length,
+                       size_t n, int nthreads, uint8_t *out) {
+  return run_batch(r, buf, offs, stride, length, n, nthreads, 1, NULL, out, NULL);
+}
+int orc_set_batch(const orc_regex *r, const uint8_t *buf, const uint64_t *offs, size_t stride, size_t length,
+                  size_t n, int nthreads, uint64_t *masks) {
+  return run_batch(r, buf, offs, stride, length, n, nthreads, 2, masks, NULL, NULL);
+}

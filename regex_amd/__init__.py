@@ -1,0 +1,275 @@
+"""regex_amd — MI355X drop-in for the batched `regex::bytes::Regex` scan path.
+
+Python mirror of the reference's operator interface for this path
+(`regex::bytes::Regex` / `RegexSet`, src/re_bytes.rs:114-623,
+src/re_set.rs:86-254) over the C ABI in include/rure_amd.h.  Every search
+runs on the GPU through librure_amd.so; single-haystack calls stage the
+bytes to HBM, batch calls take device tensors (torch) that are already
+resident.
+
+    re = regex_amd.Regex(r"\\d{4}-\\d{2}-\\d{2}")
+    re.find(b"on 2017-12-30")                     # -> (3, 13)
+    starts, ends = re.find_batch(buf, stride=4096, length=4096, count=n)
+"""
+import ctypes
+
+from . import _native as N
+
+__all__ = ["Regex", "RegexSet", "Error", "NONE"]
+
+NONE = N.NONE
+
+
+class Error(Exception):
+    """Invalid pattern (regex-capi/src/error.rs:8-77)."""
+
+
+def _flags(case_insensitive=False, multi_line=False, dot_matches_new_line=False,
+           swap_greed=False, ignore_whitespace=False, unicode=True):
+    f = 0
+    if case_insensitive: f |= N.FLAG_CASEI
+    if multi_line: f |= N.FLAG_MULTI
+    if dot_matches_new_line: f |= N.FLAG_DOTNL
+    if swap_greed: f |= N.FLAG_SWAP_GREED
+    if ignore_whitespace: f |= N.FLAG_SPACE
+    if unicode: f |= N.FLAG_UNICODE
+    return f
+
+
+def _options(size_limit, dfa_size_limit):
+    if size_limit is None and dfa_size_limit is None:
+        return None
+    o = N.rure_options_new()
+    if size_limit is not None:
+        N.rure_options_size_limit(o, size_limit)
+    if dfa_size_limit is not None:
+        N.rure_options_dfa_size_limit(o, dfa_size_limit)
+    return o
+
+
+def _check(rc, what):
+    if rc == N.OK:
+        return
+    names = {N.ERR_ARG: "bad argument", N.ERR_HIP: "HIP runtime error",
+             N.ERR_DFA: "automaton could not be materialized"}
+    raise RuntimeError("%s failed: %s (%d)" % (what, names.get(rc, "error"), rc))
+
+
+def _batch(haystack, offsets=None, stride=None, length=None, count=None, start=0):
+    """Describes a batch of device-resident haystacks (torch uint8 tensor)."""
+    import torch
+    if not isinstance(haystack, torch.Tensor) or not haystack.is_cuda:
+        raise TypeError("haystack must be a torch CUDA (HIP) uint8 tensor")
+    if haystack.dtype != torch.uint8 or not haystack.is_contiguous():
+        raise TypeError("haystack must be a contiguous uint8 tensor")
+    b = N.RureBatch()
+    b.haystack = haystack.data_ptr()
+    b.start = start
+    if offsets is not None:
+        if offsets.dtype != torch.int64 or not offsets.is_cuda or not offsets.is_contiguous():
+            raise TypeError("offsets must be a contiguous int64 CUDA tensor of n+1 entries")
+        b.offsets = offsets.data_ptr()
+        b.count = offsets.numel() - 1
+        b.stride = 0
+        b.length = 0
+    else:
+        if stride is None or length is None:
+            raise TypeError("give offsets, or stride and length")
+        n = count if count is not None else (haystack.numel() // stride if stride else 0)
+        if n and (n - 1) * stride + length > haystack.numel():
+            raise ValueError("batch exceeds the haystack buffer")
+        b.offsets = None
+        b.stride = stride
+        b.length = length
+        b.count = n
+    return b
+
+
+def _stream_ptr(stream):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+class Regex(object):
+    """`regex::bytes::Regex` (re_bytes.rs:78-605): Unicode on by default."""
+
+    def __init__(self, pattern, case_insensitive=False, multi_line=False,
+                 dot_matches_new_line=False, swap_greed=False, ignore_whitespace=False,
+                 unicode=True, size_limit=None, dfa_size_limit=None):
+        if isinstance(pattern, str):
+            pattern = pattern.encode("utf-8")
+        self.pattern = pattern
+        flags = _flags(case_insensitive, multi_line, dot_matches_new_line, swap_greed,
+                       ignore_whitespace, unicode)
+        err = N.rure_error_new()
+        opts = _options(size_limit, dfa_size_limit)
+        try:
+            self._re = N.rure_compile(pattern, len(pattern), flags, opts, err)
+            if not self._re:
+                raise Error(N.rure_error_message(err).decode("utf-8", "replace"))
+        finally:
+            N.rure_error_free(err)
+            if opts:
+                N.rure_options_free(opts)
+
+    def __del__(self):
+        re_ = getattr(self, "_re", None)
+        if re_:
+            N.rure_free(re_)
+            self._re = None
+
+    # ------------------------------------------------ single haystack (rure_*)
+    def is_match(self, text, start=0):
+        return bool(N.rure_is_match(self._re, text, len(text), start))
+
+    def find(self, text, start=0):
+        m = N.RureMatch()
+        if N.rure_find(self._re, text, len(text), start, ctypes.byref(m)):
+            return (m.start, m.end)
+        return None
+
+    def shortest_match(self, text, start=0):
+        e = N.c_size()
+        if N.rure_shortest_match(self._re, text, len(text), start, ctypes.byref(e)):
+            return e.value
+        return None
+
+    def find_iter(self, text):
+        it = N.rure_iter_new(self._re)
+        out = []
+        try:
+            m = N.RureMatch()
+            while N.rure_iter_next(it, text, len(text), ctypes.byref(m)):
+                out.append((m.start, m.end))
+        finally:
+            N.rure_iter_free(it)
+        return out
+
+    # -------------------------------------------- batches (device tensors)
+    def find_batch(self, haystack, offsets=None, stride=None, length=None, count=None,
+                   start=0, out=None, stream=None):
+        """Leftmost-first match per haystack.  Returns an (n, 2) int64 tensor of
+        (start, end); -1 (== SIZE_MAX) marks no match."""
+        import torch
+        b = _batch(haystack, offsets, stride, length, count, start)
+        if out is None:
+            out = torch.empty((b.count, 2), dtype=torch.int64, device=haystack.device)
+        _check(N.rure_amd_find_batch(self._re, ctypes.byref(b), ctypes.c_void_p(out.data_ptr()),
+                                     _stream_ptr(stream)), "find_batch")
+        return out
+
+    def is_match_batch(self, haystack, offsets=None, stride=None, length=None, count=None,
+                       start=0, out=None, stream=None):
+        import torch
+        b = _batch(haystack, offsets, stride, length, count, start)
+        if out is None:
+            out = torch.empty((b.count,), dtype=torch.uint8, device=haystack.device)
+        _check(N.rure_amd_is_match_batch(self._re, ctypes.byref(b), ctypes.c_void_p(out.data_ptr()),
+                                         _stream_ptr(stream)), "is_match_batch")
+        return out
+
+    def shortest_match_batch(self, haystack, offsets=None, stride=None, length=None, count=None,
+                             start=0, out=None, stream=None):
+        import torch
+        b = _batch(haystack, offsets, stride, length, count, start)
+        if out is None:
+            out = torch.empty((b.count,), dtype=torch.int64, device=haystack.device)
+        _check(N.rure_amd_shortest_match_batch(self._re, ctypes.byref(b), ctypes.c_void_p(out.data_ptr()),
+                                               _stream_ptr(stream)), "shortest_match_batch")
+        return out
+
+    # ----------------------------------------------------------- diagnostics
+    def dfa_info(self, which=0):
+        info = N.DfaInfo()
+        rc = N.rure_amd_dfa_info_get(self._re, which, ctypes.byref(info))
+        return {k: getattr(info, k) for k, _ in N.DfaInfo._fields_} if rc == N.OK else None
+
+    def program(self, which):
+        """Compiled byte program (0 fwd DFA, 1 reverse DFA, 2 NFA): (info, insts)."""
+        return _export(N.rure_amd_program_export, self._re, which)
+
+    def dfa_tables(self, which=0):
+        import numpy as np
+        info = self.dfa_info(which)
+        if info is None:
+            return None
+        n = info["states"]
+        trans = np.zeros(n * 256, dtype=np.uint32)
+        eof = np.zeros(n, dtype=np.uint8)
+        start = np.zeros(128, dtype=np.uint32)
+        _check(N.rure_amd_dfa_export(self._re, which, trans.ctypes.data, eof.ctypes.data, start.ctypes.data),
+               "dfa_export")
+        return info, trans.reshape(n, 256), eof, start
+
+
+def _export(fn, handle, which):
+    import numpy as np
+    info = N.ProgInfo()
+    n = fn(handle, which, ctypes.byref(info), None, 0)
+    if n < 0:
+        raise ValueError("no such program")
+    arr = np.zeros(max(n, 1) * 12, dtype=np.uint8)
+    fn(handle, which, ctypes.byref(info), arr.ctypes.data, n)
+    return info, arr[: n * 12]
+
+
+class RegexSet(object):
+    """`regex::bytes::RegexSet` (re_set.rs:86-254)."""
+
+    def __init__(self, patterns, case_insensitive=False, multi_line=False,
+                 dot_matches_new_line=False, swap_greed=False, ignore_whitespace=False,
+                 unicode=True, size_limit=None, dfa_size_limit=None):
+        pats = [p.encode("utf-8") if isinstance(p, str) else p for p in patterns]
+        self.patterns = pats
+        arr = (ctypes.c_char_p * max(len(pats), 1))(*pats)
+        lens = (N.c_size * max(len(pats), 1))(*[len(p) for p in pats])
+        flags = _flags(case_insensitive, multi_line, dot_matches_new_line, swap_greed,
+                       ignore_whitespace, unicode)
+        err = N.rure_error_new()
+        opts = _options(size_limit, dfa_size_limit)
+        try:
+            self._set = N.rure_compile_set(arr, lens, len(pats), flags, opts, err)
+            if not self._set:
+                raise Error(N.rure_error_message(err).decode("utf-8", "replace"))
+        finally:
+            N.rure_error_free(err)
+            if opts:
+                N.rure_options_free(opts)
+
+    def __del__(self):
+        s = getattr(self, "_set", None)
+        if s:
+            N.rure_set_free(s)
+            self._set = None
+
+    def __len__(self):
+        return N.rure_set_len(self._set)
+
+    def is_match(self, text, start=0):
+        return bool(N.rure_set_is_match(self._set, text, len(text), start))
+
+    def matches(self, text, start=0):
+        n = len(self)
+        buf = (ctypes.c_bool * max(n, 1))()
+        N.rure_set_matches(self._set, text, len(text), start, buf)
+        return [i for i in range(n) if buf[i]]
+
+    def matches_batch(self, haystack, offsets=None, stride=None, length=None, count=None,
+                      start=0, out=None, stream=None):
+        """One int64 bit mask per haystack (bit j <=> pattern j matched)."""
+        import torch
+        b = _batch(haystack, offsets, stride, length, count, start)
+        if out is None:
+            out = torch.empty((b.count,), dtype=torch.int64, device=haystack.device)
+        _check(N.rure_amd_set_matches_batch(self._set, ctypes.byref(b), ctypes.c_void_p(out.data_ptr()),
+                                            _stream_ptr(stream)), "matches_batch")
+        return out
+
+    def program(self, which):
+        return _export(N.rure_amd_set_program_export, self._set, which)
+
+    def dfa_info(self):
+        info = N.DfaInfo()
+        rc = N.rure_amd_set_dfa_info_get(self._set, ctypes.byref(info))
+        return {k: getattr(info, k) for k, _ in N.DfaInfo._fields_} if rc == N.OK else None

@@ -1,0 +1,121 @@
+"""ctypes binding of the C ABI in include/rure_amd.h (librure_amd.so).
+
+The library is built in-tree (`make` / `__graft_entry__.build()`) into
+regex_amd/lib/.  There is no fallback: if the shared object is missing the
+import fails loudly.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "librure_amd.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        "regex_amd: native library %s is missing; build it with `make` or "
+        "`python -c 'import __graft_entry__ as g; g.build()'`" % LIB_PATH)
+
+# Share the HIP runtime with PyTorch (the device-memory / stream plumbing):
+# torch bundles its own libamdhip64.so.7; loading it first makes our library
+# bind to the same runtime instead of pulling in a second copy from /opt/rocm.
+try:
+    import torch  # noqa: F401
+except ImportError:  # pure C-ABI use without torch
+    pass
+
+lib = ctypes.CDLL(LIB_PATH)
+
+c_u8p = ctypes.POINTER(ctypes.c_uint8)
+c_size = ctypes.c_size_t
+
+
+class RureMatch(ctypes.Structure):
+    _fields_ = [("start", c_size), ("end", c_size)]
+
+
+class RureBatch(ctypes.Structure):
+    _fields_ = [("haystack", ctypes.c_void_p), ("offsets", ctypes.c_void_p),
+                ("stride", c_size), ("length", c_size), ("count", c_size),
+                ("start", c_size)]
+
+
+class DfaInfo(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "ok", "states", "raw_states", "normal", "match_end", "dead", "quit",
+        "hot", "byte_classes", "insts")]
+
+
+class ProgInfo(ctypes.Structure):
+    _fields_ = [("ninsts", ctypes.c_uint32), ("start", ctypes.c_uint32),
+                ("nmatches", ctypes.c_uint32), ("ncaptures", ctypes.c_uint32),
+                ("anchored_start", ctypes.c_uint8), ("anchored_end", ctypes.c_uint8),
+                ("has_unicode_word_boundary", ctypes.c_uint8), ("is_reverse", ctypes.c_uint8),
+                ("byte_classes", ctypes.c_uint8 * 256)]
+
+
+class Inst(ctypes.Structure):
+    _fields_ = [("op", ctypes.c_uint8), ("look", ctypes.c_uint8), ("lo", ctypes.c_uint8),
+                ("hi", ctypes.c_uint8), ("x", ctypes.c_uint32), ("y", ctypes.c_uint32)]
+
+
+def _sig(name, res, *args):
+    f = getattr(lib, name)
+    f.restype = res
+    f.argtypes = list(args)
+    return f
+
+
+VP = ctypes.c_void_p
+rure_error_new = _sig("rure_error_new", VP)
+rure_error_free = _sig("rure_error_free", None, VP)
+rure_error_message = _sig("rure_error_message", ctypes.c_char_p, VP)
+rure_options_new = _sig("rure_options_new", VP)
+rure_options_free = _sig("rure_options_free", None, VP)
+rure_options_size_limit = _sig("rure_options_size_limit", None, VP, c_size)
+rure_options_dfa_size_limit = _sig("rure_options_dfa_size_limit", None, VP, c_size)
+rure_compile = _sig("rure_compile", VP, ctypes.c_char_p, c_size, ctypes.c_uint32, VP, VP)
+rure_free = _sig("rure_free", None, VP)
+rure_is_match = _sig("rure_is_match", ctypes.c_bool, VP, ctypes.c_char_p, c_size, c_size)
+rure_find = _sig("rure_find", ctypes.c_bool, VP, ctypes.c_char_p, c_size, c_size,
+                 ctypes.POINTER(RureMatch))
+rure_shortest_match = _sig("rure_shortest_match", ctypes.c_bool, VP, ctypes.c_char_p, c_size, c_size,
+                           ctypes.POINTER(c_size))
+rure_iter_new = _sig("rure_iter_new", VP, VP)
+rure_iter_free = _sig("rure_iter_free", None, VP)
+rure_iter_next = _sig("rure_iter_next", ctypes.c_bool, VP, ctypes.c_char_p, c_size,
+                      ctypes.POINTER(RureMatch))
+rure_compile_set = _sig("rure_compile_set", VP, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(c_size),
+                        c_size, ctypes.c_uint32, VP, VP)
+rure_set_free = _sig("rure_set_free", None, VP)
+rure_set_is_match = _sig("rure_set_is_match", ctypes.c_bool, VP, ctypes.c_char_p, c_size, c_size)
+rure_set_matches = _sig("rure_set_matches", ctypes.c_bool, VP, ctypes.c_char_p, c_size, c_size,
+                        ctypes.POINTER(ctypes.c_bool))
+rure_set_len = _sig("rure_set_len", c_size, VP)
+rure_amd_find_batch = _sig("rure_amd_find_batch", ctypes.c_int, VP, ctypes.POINTER(RureBatch), VP, VP)
+rure_amd_is_match_batch = _sig("rure_amd_is_match_batch", ctypes.c_int, VP, ctypes.POINTER(RureBatch), VP, VP)
+rure_amd_shortest_match_batch = _sig("rure_amd_shortest_match_batch", ctypes.c_int, VP,
+                                     ctypes.POINTER(RureBatch), VP, VP)
+rure_amd_set_matches_batch = _sig("rure_amd_set_matches_batch", ctypes.c_int, VP, ctypes.POINTER(RureBatch),
+                                  VP, VP)
+rure_amd_dfa_info_get = _sig("rure_amd_dfa_info_get", ctypes.c_int, VP, ctypes.c_int, ctypes.POINTER(DfaInfo))
+rure_amd_set_dfa_info_get = _sig("rure_amd_set_dfa_info_get", ctypes.c_int, VP, ctypes.POINTER(DfaInfo))
+rure_amd_program_export = _sig("rure_amd_program_export", ctypes.c_int64, VP, ctypes.c_int,
+                               ctypes.POINTER(ProgInfo), VP, c_size)
+rure_amd_set_program_export = _sig("rure_amd_set_program_export", ctypes.c_int64, VP, ctypes.c_int,
+                                   ctypes.POINTER(ProgInfo), VP, c_size)
+rure_amd_dfa_export = _sig("rure_amd_dfa_export", ctypes.c_int, VP, ctypes.c_int, VP, VP, VP)
+
+FLAG_CASEI = 1 << 0
+FLAG_MULTI = 1 << 1
+FLAG_DOTNL = 1 << 2
+FLAG_SWAP_GREED = 1 << 3
+FLAG_SPACE = 1 << 4
+FLAG_UNICODE = 1 << 5
+DEFAULT_FLAGS = FLAG_UNICODE
+
+OK = 0
+ERR_ARG = -1
+ERR_HIP = -2
+ERR_DFA = -3
+NONE = (1 << 64) - 1
+QUIT = (1 << 64) - 2

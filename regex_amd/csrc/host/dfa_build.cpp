@@ -1,0 +1,420 @@
+// Eager DFA materialization + minimisation.  See dfa_build.hpp.
+#include "dfa_build.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <deque>
+#include <unordered_map>
+
+namespace rure_amd {
+namespace {
+
+struct EmptyFlags {  // dfa.rs:408-416
+  bool start = false, end = false, start_line = false, end_line = false;
+  bool wb = false, nwb = false;
+};
+
+enum : uint8_t { SF_MATCH = 1, SF_WORD = 2, SF_EMPTY = 4 };  // dfa.rs:1648-1672
+
+// Ordered sparse set of instruction pointers (src/sparse.rs:15-64).
+struct SparseSet {
+  std::vector<uint32_t> dense, sparse;
+  size_t n = 0;
+  explicit SparseSet(size_t cap) : dense(cap), sparse(cap) {}
+  bool contains(uint32_t v) const { uint32_t i = sparse[v]; return i < n && dense[i] == v; }
+  void insert(uint32_t v) { dense[n] = v; sparse[v] = (uint32_t)n; ++n; }
+  void clear() { n = 0; }
+};
+
+class Builder {
+ public:
+  Builder(const Program &p, const DfaBuildLimits &lim)
+      : p_(p), lim_(lim), qa_(p.insts.size() + 1), qb_(p.insts.size() + 1) {
+    is_set_ = p.matches.size() > 1;
+    cont_ = p.is_reverse || is_set_;  // dfa.rs:1557-1559
+    word_matters_ = false;
+    for (const Inst &i : p.insts)
+      if (i.op == OP_EMPTY && i.look >= LOOK_WORD_BOUNDARY) word_matters_ = true;
+    quit_ = p.has_unicode_word_boundary;
+    stack_.reserve(p.insts.size() + 1);
+  }
+
+  bool build(DenseDfa *out, std::string *err) {
+    // raw state 0 = DEAD, raw state 1 = QUIT (always allocated, maybe unused)
+    keys_.push_back(std::string());
+    keys_.push_back(std::string());
+    compute_starts();
+    const int ncls = p_.num_byte_classes();
+    uint8_t rep[256];
+    {
+      int seen = -1;
+      for (int b = 0; b < 256; ++b)
+        if (p_.byte_classes[b] != seen) { seen = p_.byte_classes[b]; rep[seen] = (uint8_t)b; }
+    }
+    // Transitions of DEAD and QUIT: absorbing.
+    trans_cls_.assign((size_t)2 * ncls, 0);
+    for (int c = 0; c < ncls; ++c) { trans_cls_[c] = 0; trans_cls_[ncls + c] = 1; }
+    eof_match_ = {0, 0};
+    eof_mask_ = {0, 0};
+    for (size_t s = 2; s < keys_.size(); ++s) {
+      if ((int)keys_.size() > lim_.max_raw_states) {
+        if (err) *err = "DFA state budget exceeded (" + std::to_string(lim_.max_raw_states) + " states)";
+        return false;
+      }
+      std::string key = keys_[s];  // copy: keys_ may grow
+      trans_cls_.resize((s + 1) * ncls);
+      for (int c = 0; c < ncls; ++c) trans_cls_[s * ncls + c] = step(key, rep[c]);
+      uint64_t mask = 0;
+      bool m = step_eof(key, &mask);
+      eof_match_.push_back(m ? 1 : 0);
+      eof_mask_.push_back(mask);
+    }
+    const int nraw = (int)keys_.size();
+    // Expand to 256 columns (QUIT override for non-ASCII bytes when the
+    // program has a Unicode word boundary, dfa.rs:1487-1496).
+    std::vector<uint32_t> t256((size_t)nraw * 256);
+    for (int s = 0; s < nraw; ++s)
+      for (int b = 0; b < 256; ++b)
+        t256[(size_t)s * 256 + b] =
+            (quit_ && b >= 0x80 && s != 0) ? 1u : trans_cls_[(size_t)s * ncls + p_.byte_classes[b]];
+    minimise(nraw, t256, out);
+    out->raw_states = nraw;
+    return true;
+  }
+
+ private:
+  const Program &p_;
+  DfaBuildLimits lim_;
+  SparseSet qa_, qb_;
+  std::vector<uint32_t> stack_;
+  bool is_set_, cont_, word_matters_, quit_;
+  std::vector<std::string> keys_;
+  std::unordered_map<std::string, uint32_t> ids_;
+  std::vector<uint32_t> trans_cls_;
+  std::vector<uint8_t> eof_match_;
+  std::vector<uint64_t> eof_mask_;
+  uint32_t start_raw_[128];
+  bool start_used_[128];
+
+  // dfa.rs:1073-1134
+  void follow(uint32_t ip0, SparseSet &q, const EmptyFlags &f) {
+    stack_.push_back(ip0);
+    while (!stack_.empty()) {
+      uint32_t ip = stack_.back();
+      stack_.pop_back();
+      if (q.contains(ip)) continue;
+      q.insert(ip);
+      const Inst &in = p_.insts[ip];
+      switch (in.op) {
+        case OP_MATCH: case OP_BYTES: break;
+        case OP_EMPTY: {
+          bool ok = false;
+          switch (in.look) {
+            case LOOK_START_LINE: ok = f.start_line; break;
+            case LOOK_END_LINE: ok = f.end_line; break;
+            case LOOK_START_TEXT: ok = f.start; break;
+            case LOOK_END_TEXT: ok = f.end; break;
+            case LOOK_WORD_BOUNDARY_ASCII: case LOOK_WORD_BOUNDARY: ok = f.wb; break;
+            case LOOK_NOT_WORD_BOUNDARY_ASCII: case LOOK_NOT_WORD_BOUNDARY: ok = f.nwb; break;
+          }
+          if (ok) stack_.push_back(in.x);
+          break;
+        }
+        case OP_SAVE: stack_.push_back(in.x); break;
+        case OP_SPLIT: stack_.push_back(in.y); stack_.push_back(in.x); break;
+      }
+    }
+  }
+
+  // dfa.rs:1196-1244 plus interning; returns raw id (0 = DEAD).
+  uint32_t intern(const SparseSet &q, uint8_t sflags) {
+    std::string key(1, '\0');
+    for (size_t k = 0; k < q.n; ++k) {
+      uint32_t ip = q.dense[k];
+      const Inst &in = p_.insts[ip];
+      bool push = false, stop = false;
+      switch (in.op) {
+        case OP_SAVE: case OP_SPLIT: break;
+        case OP_BYTES: push = true; break;
+        case OP_EMPTY: sflags |= SF_EMPTY; push = true; break;
+        case OP_MATCH: push = true; stop = !cont_; break;
+      }
+      if (push) key.append((const char *)&ip, 4);
+      if (stop) break;
+    }
+    if (key.size() == 1 && !(sflags & SF_MATCH)) return 0;
+    key[0] = (char)sflags;
+    auto it = ids_.find(key);
+    if (it != ids_.end()) return it->second;
+    uint32_t id = (uint32_t)keys_.size();
+    ids_.emplace(key, id);
+    keys_.push_back(std::move(key));
+    return id;
+  }
+
+  void load(const std::string &key, SparseSet &q) {
+    q.clear();
+    for (size_t k = 1; k + 4 <= key.size(); k += 4) {
+      uint32_t ip;
+      memcpy(&ip, key.data() + k, 4);
+      q.insert(ip);
+    }
+  }
+
+  // Shared body of exec_byte (dfa.rs:910-1048) for a real byte (b < 256) or
+  // EOF (b == 256).  Leaves the resulting ordered set in *res and flags in *sf.
+  void exec(const std::string &key, int b, SparseSet **res, uint8_t *sf) {
+    SparseSet *qcur = &qa_, *qnext = &qb_;
+    load(key, *qcur);
+    uint8_t flags = (uint8_t)key[0];
+    bool is_word_last = (flags & SF_WORD) != 0;
+    bool is_word = b < 256 && is_word_byte((uint8_t)b);
+    if (flags & SF_EMPTY) {
+      EmptyFlags ef;
+      if (b == 256) { ef.end = true; ef.end_line = true; }
+      else if (b == '\n') ef.end_line = true;
+      if (is_word_last == is_word) ef.nwb = true; else ef.wb = true;
+      qnext->clear();
+      for (size_t k = 0; k < qcur->n; ++k) follow(qcur->dense[k], *qnext, ef);
+      std::swap(qcur, qnext);
+    }
+    EmptyFlags ef2;
+    ef2.start_line = (b == '\n');
+    uint8_t sflags = 0;
+    if (is_word && word_matters_) sflags |= SF_WORD;
+    qnext->clear();
+    for (size_t k = 0; k < qcur->n; ++k) {
+      uint32_t ip = qcur->dense[k];
+      const Inst &in = p_.insts[ip];
+      if (in.op == OP_MATCH) {
+        sflags |= SF_MATCH;
+        if (!cont_) break;
+        if (is_set_ && !qnext->contains(ip)) qnext->insert(ip);
+      } else if (in.op == OP_BYTES) {
+        if (b < 256 && in.lo <= b && b <= in.hi) follow(in.x, *qnext, ef2);
+      }
+    }
+    if (b == 256 && is_set_) std::swap(qcur, qnext);  // dfa.rs:1004-1015
+    *res = qnext;
+    *sf = sflags;
+  }
+
+  uint32_t step(const std::string &key, uint8_t b) {
+    SparseSet *q; uint8_t sf;
+    exec(key, b, &q, &sf);
+    return intern(*q, sf);
+  }
+
+  bool step_eof(const std::string &key, uint64_t *mask) {
+    SparseSet *q; uint8_t sf;
+    exec(key, 256, &q, &sf);
+    uint64_t m = 0;
+    if (is_set_) {
+      for (size_t k = 0; k < q->n; ++k) {
+        const Inst &in = p_.insts[q->dense[k]];
+        if (in.op == OP_MATCH && in.x < 64) m |= 1ull << in.x;
+      }
+    }
+    *mask = m;
+    return (sf & SF_MATCH) != 0;
+  }
+
+  uint32_t start_for(const EmptyFlags &ef, bool word_last) {  // dfa.rs:1370-1409
+    qa_.clear();
+    follow(p_.start, qa_, ef);
+    uint8_t sf = (word_last && word_matters_) ? SF_WORD : 0;
+    return intern(qa_, sf);
+  }
+
+  static int flag_index(const EmptyFlags &e, bool word) {
+    return (e.start ? 1 : 0) | (e.end ? 2 : 0) | (e.start_line ? 4 : 0) | (e.end_line ? 8 : 0) |
+           (e.wb ? 16 : 0) | (e.nwb ? 32 : 0) | (word ? 64 : 0);
+  }
+
+  void compute_starts() {
+    for (int i = 0; i < 128; ++i) { start_raw_[i] = 0; start_used_[i] = false; }
+    // ctx: edge = at the text edge the search starts from (at==0 fwd, at==len rev);
+    // empty = whole text empty; near: byte before (fwd) / at (rev) the start:
+    // 0 none, 1 '\n', 2 word byte, 3 other; far_word: the other neighbour is a word byte.
+    for (int edge = 0; edge < 2; ++edge)
+      for (int empty = 0; empty < 2; ++empty)
+        for (int near = 0; near < 4; ++near)
+          for (int far_word = 0; far_word < 2; ++far_word) {
+            if (empty && !edge) continue;
+            if (edge && near != 0) continue;
+            if (!edge && near == 0) continue;
+            if (empty && far_word) continue;
+            EmptyFlags ef;
+            ef.start = edge;
+            ef.end = empty;
+            ef.start_line = edge || near == 1;
+            ef.end_line = empty;
+            bool word_last = near == 2;
+            bool word_next = far_word;
+            if (word_last == word_next) ef.nwb = true; else ef.wb = true;
+            int fi = flag_index(ef, word_last);
+            if (start_used_[fi]) continue;
+            start_used_[fi] = true;
+            start_raw_[fi] = start_for(ef, word_last);
+          }
+  }
+
+  // Moore partition refinement over byte columns; outputs preserved:
+  // single: (match flag, EOF match, dead, quit); set: (EOF match mask, dead, quit).
+  void minimise(int n, const std::vector<uint32_t> &t, DenseDfa *out) {
+    // distinct byte columns: transitions depend on the byte only through its
+    // class (plus the QUIT split for non-ASCII bytes)
+    std::vector<int> colrep;
+    {
+      std::vector<int> seen(512, -1);
+      for (int b = 0; b < 256; ++b) {
+        int key = p_.byte_classes[b] * 2 + ((quit_ && b >= 0x80) ? 1 : 0);
+        if (seen[key] < 0) { seen[key] = b; colrep.push_back(b); }
+      }
+    }
+    std::vector<uint32_t> block(n), nb(n);
+    auto out_key = [&](int s) {
+      std::string k;
+      uint8_t tag = (s == 0 || (s == 1 && !quit_)) ? 1 : s == 1 ? 2 : 0;
+      k.push_back((char)tag);
+      if (s >= 2) {
+        if (is_set_) k.append((const char *)&eof_mask_[s], 8);
+        else {
+          uint8_t m = (keys_[s][0] & SF_MATCH) ? 1 : 0;
+          k.push_back((char)m);
+          k.push_back((char)eof_match_[s]);
+        }
+      }
+      return k;
+    };
+    size_t nblocks;
+    {
+      std::unordered_map<std::string, uint32_t> m;
+      for (int s = 0; s < n; ++s) {
+        auto it = m.emplace(out_key(s), (uint32_t)m.size()).first;
+        block[s] = it->second;
+      }
+      nblocks = m.size();
+    }
+    while (true) {
+      std::unordered_map<std::string, uint32_t> m;
+      m.reserve(n * 2);
+      for (int s = 0; s < n; ++s) {
+        std::string sig((const char *)&block[s], 4);
+        for (int b : colrep) sig.append((const char *)&block[t[(size_t)s * 256 + b]], 4);
+        auto it = m.emplace(sig, (uint32_t)m.size()).first;
+        nb[s] = it->second;
+      }
+      bool done = m.size() == nblocks;
+      nblocks = m.size();
+      block.swap(nb);
+      if (done) break;
+    }
+    // representative per block and categories
+    std::vector<int> rep(nblocks, -1);
+    for (int s = 0; s < n; ++s) if (rep[block[s]] < 0) rep[block[s]] = s;
+    const uint32_t dead_b = block[0];
+    const bool quit_used = quit_ && true;
+    const uint32_t quit_b = block[1];
+    auto is_special = [&](uint32_t b) {
+      int s = rep[b];
+      if (b == dead_b || (quit_used && b == quit_b)) return false;
+      if (is_set_) {  // absorbing: result can no longer change
+        for (int c : colrep) if (block[t[(size_t)s * 256 + c]] != b) return false;
+        return true;
+      }
+      return (keys_[s][0] & SF_MATCH) != 0;
+    };
+    // order: normal states reachable from the start states through ASCII
+    // bytes first (the LDS-resident "hot" set of the kernels), then the
+    // remaining normal states, all in BFS order.
+    std::vector<int32_t> newid(nblocks, -1);
+    std::vector<uint32_t> order_normal, order_special;
+    auto is_ordinary = [&](uint32_t b) {
+      return b != dead_b && !(quit_used && b == quit_b) && !is_special(b);
+    };
+    {
+      std::vector<char> seen(nblocks, 0);
+      std::deque<uint32_t> dq;
+      for (int i = 0; i < 128; ++i) {
+        uint32_t b = block[start_raw_[i]];
+        if (start_used_[i] && !seen[b] && is_ordinary(b)) { seen[b] = 1; dq.push_back(b); }
+      }
+      while (!dq.empty()) {
+        uint32_t b = dq.front(); dq.pop_front();
+        order_normal.push_back(b);
+        int s = rep[b];
+        for (int c : colrep) {
+          if (c >= 0x80) continue;
+          uint32_t nb2 = block[t[(size_t)s * 256 + c]];
+          if (!seen[nb2] && is_ordinary(nb2)) { seen[nb2] = 1; dq.push_back(nb2); }
+        }
+      }
+      out->n_ascii = (int)order_normal.size();
+      std::vector<char> seen2(nblocks, 0);
+      auto push = [&](uint32_t b) { if (!seen2[b]) { seen2[b] = 1; dq.push_back(b); } };
+      for (int i = 0; i < 128; ++i) if (start_used_[i]) push(block[start_raw_[i]]);
+      for (uint32_t b = 0; b < nblocks; ++b) push(b);  // unreachable blocks last
+      while (!dq.empty()) {
+        uint32_t b = dq.front(); dq.pop_front();
+        if (b != dead_b && !(quit_used && b == quit_b)) {
+          if (is_special(b)) order_special.push_back(b);
+          else if (!seen[b]) order_normal.push_back(b);
+        }
+        int s = rep[b];
+        for (int c : colrep) push(block[t[(size_t)s * 256 + c]]);
+      }
+    }
+    int next = 0;
+    for (uint32_t b : order_normal) newid[b] = next++;
+    out->n_normal = next;
+    for (uint32_t b : order_special) newid[b] = next++;
+    out->n_match_end = next;
+    out->dead = next;
+    newid[dead_b] = next++;
+    out->quit = -1;
+    if (quit_used && quit_b != dead_b) { out->quit = next; newid[quit_b] = next++; }
+    out->nstates = next;
+    out->is_set = is_set_;
+    out->reverse = p_.is_reverse;
+    out->trans.assign((size_t)next * 256, 0);
+    out->eof_match.assign(next, 0);
+    out->eof_mask.assign(next, 0);
+    for (uint32_t b = 0; b < nblocks; ++b) {
+      int s = rep[b], id = newid[b];
+      for (int c = 0; c < 256; ++c) out->trans[(size_t)id * 256 + c] = newid[block[t[(size_t)s * 256 + c]]];
+      out->eof_match[id] = eof_match_[s];
+      out->eof_mask[id] = eof_mask_[s];
+    }
+    for (int i = 0; i < 128; ++i) out->start[i] = (uint32_t)(start_used_[i] ? newid[block[start_raw_[i]]] : out->dead);
+  }
+};
+
+}  // namespace
+
+bool build_dense_dfa(const Program &prog, const DfaBuildLimits &lim, DenseDfa *out, std::string *err) {
+  Builder b(prog, lim);
+  return b.build(out, err);
+}
+
+int start_flag_index_fwd(const uint8_t *text, size_t len, size_t at) {  // dfa.rs:1415-1434
+  bool start = at == 0, end = len == 0;
+  bool start_line = at == 0 || text[at - 1] == '\n';
+  bool word_last = at > 0 && is_word_byte(text[at - 1]);
+  bool word = at < len && is_word_byte(text[at]);
+  bool wb = word_last != word;
+  return (start ? 1 : 0) | (end ? 2 : 0) | (start_line ? 4 : 0) | (end ? 8 : 0) |
+         (wb ? 16 : 32) | (word_last ? 64 : 0);
+}
+
+int start_flag_index_rev(const uint8_t *text, size_t len, size_t at) {  // dfa.rs:1440-1464
+  bool start = at == len, end = len == 0;
+  bool start_line = at == len || text[at] == '\n';
+  bool word_last = at < len && is_word_byte(text[at]);
+  bool word = at > 0 && is_word_byte(text[at - 1]);
+  bool wb = word_last != word;
+  return (start ? 1 : 0) | (end ? 2 : 0) | (start_line ? 4 : 0) | (end ? 8 : 0) |
+         (wb ? 16 : 32) | (word_last ? 64 : 0);
+}
+
+}  // namespace rure_amd

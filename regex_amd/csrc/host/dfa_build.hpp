@@ -1,0 +1,56 @@
+// Offline (eager) DFA materialization of a byte Program.
+//
+// The reference builds its DFA lazily during search (src/dfa.rs: exec_byte
+// 910-1048, follow_epsilons 1073-1134, cached_state_key 1196-1244,
+// start_state 1370-1409, start_flags 1415-1464).  A GPU cannot build states
+// on the fly, so we run the very same subset construction eagerly over every
+// state reachable from every start-flag combination, then minimise it
+// (Moore partition refinement).  Laziness, cache flushes and state numbering
+// only change *when* states are built, never which language they accept
+// (dfa.rs:1176-1183, prog.rs:63-68), so offsets stay bit-identical.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "program.hpp"
+
+namespace rure_amd {
+
+// One materialized + minimised DFA.  State numbering (kernel contract):
+//   [0, n_normal)            ordinary states (no match flag)
+//   [n_normal, n_match_end)  states carrying the (one-byte delayed) match flag
+//   dead                     == n_match_end      (absorbing, never matches)
+//   quit                     == n_match_end + 1  (only if has_quit)
+struct DenseDfa {
+  int nstates = 0;
+  int n_normal = 0;
+  int n_match_end = 0;
+  int dead = 0;
+  int quit = -1;
+  bool is_set = false;
+  bool reverse = false;
+  std::vector<uint32_t> trans;     // nstates * 256, next state per byte
+  std::vector<uint8_t> eof_match;  // per state: EOF transition yields a match flag
+  std::vector<uint64_t> eof_mask;  // sets: Match slots visible after the EOF step
+  uint32_t start[128];             // start state per 7-bit start-flag index (dfa.rs:1381-1390)
+  int raw_states = 0;              // states before minimisation (diagnostics)
+  int n_ascii = 0;                 // normal states reachable through ASCII bytes (numbered first)
+};
+
+struct DfaBuildLimits {
+  int max_raw_states = 1 << 16;
+};
+
+// Builds the DFA for `prog` (a forward DFA program with `.*?` unless anchored,
+// or a reverse program).  Returns false (with `err`) if the state budget is
+// exceeded.
+bool build_dense_dfa(const Program &prog, const DfaBuildLimits &lim, DenseDfa *out,
+                     std::string *err);
+
+// Start-flag index for a forward search starting at `at` (dfa.rs:1415-1434).
+int start_flag_index_fwd(const uint8_t *text, size_t len, size_t at);
+// Start-flag index for a reverse search ending at `at` (dfa.rs:1440-1464).
+int start_flag_index_rev(const uint8_t *text, size_t len, size_t at);
+
+}  // namespace rure_amd

@@ -1,0 +1,56 @@
+// Byte-program IR: the same Program/Inst contract as the reference
+// (src/prog.rs:18-75 Program, prog.rs:261-425 Inst).  Only byte programs
+// are produced (Char/Ranges never appear): the DFA programs always use bytes
+// (prog.rs:134-136) and the NFA program is compiled with `bytes(true)`, the
+// configuration the reference's `nfa-bytes` test target exercises
+// (tests/test_nfa_bytes.rs).
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "syntax.hpp"
+
+namespace rure_amd {
+
+enum InstOp : uint8_t { OP_MATCH = 0, OP_SAVE = 1, OP_SPLIT = 2, OP_EMPTY = 3, OP_BYTES = 4 };
+
+// prog.rs:334-351
+enum Look : uint8_t {
+  LOOK_START_LINE = 0, LOOK_END_LINE = 1, LOOK_START_TEXT = 2, LOOK_END_TEXT = 3,
+  LOOK_WORD_BOUNDARY = 4, LOOK_NOT_WORD_BOUNDARY = 5,
+  LOOK_WORD_BOUNDARY_ASCII = 6, LOOK_NOT_WORD_BOUNDARY_ASCII = 7,
+};
+
+// Flat 12-byte instruction.  MATCH: x = match slot.  SAVE: x = goto, y = slot.
+// SPLIT: x = goto1, y = goto2.  EMPTY: x = goto, look.  BYTES: x = goto, [lo, hi].
+struct Inst {
+  uint8_t op, look, lo, hi;
+  uint32_t x, y;
+};
+
+struct Program {
+  std::vector<Inst> insts;
+  std::vector<uint32_t> matches;     // pcs of Match insts (prog.rs:24)
+  uint32_t start = 0;
+  uint8_t byte_classes[256] = {0};
+  bool is_dfa = false, is_reverse = false;
+  bool anchored_start = false, anchored_end = false;
+  bool has_unicode_word_boundary = false;
+  bool only_utf8 = false;
+  std::vector<std::string> capture_names;   // index 0 = whole match ("")
+  std::vector<bool> capture_has_name;
+  size_t dfa_size_limit = 2u << 20;
+  int num_byte_classes() const { return (int)byte_classes[255] + 1; }
+};
+
+struct CompileOptions {
+  bool dfa = false, reverse = false, only_utf8 = false;
+  size_t size_limit = 10u << 20;
+};
+
+// compile.rs:124-206.  `exprs` has >= 1 element.
+bool compile_program(const std::vector<Expr> &exprs, const CompileOptions &opt,
+                     Program *out, std::string *err);
+
+}  // namespace rure_amd

@@ -1,0 +1,51 @@
+// Device-side descriptors shared by the HIP kernels and the host runtime.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rure_amd {
+
+enum { MODE_FIND = 0, MODE_ISMATCH = 1, MODE_SHORTEST = 2 };
+
+struct BatchDev {
+  const uint8_t *hay;
+  const uint64_t *offs;   // n+1 offsets or nullptr (fixed stride)
+  uint64_t stride, length, count, start;
+};
+
+// Forward DFA on the device.  State ids: [0, hot) are in the LDS fast table
+// (u8, 256 columns, row `hot` = absorbing sentinel); [0, n_normal) carry no
+// match flag; [n_normal, n_match_end) carry the match flag; `dead`, `quit`.
+struct FwdDfaDev {
+  const uint8_t *lds_image;   // (hot + 1) * 256 bytes, padded to 16
+  uint32_t lds_bytes;
+  uint32_t hot;
+  const uint16_t *full;       // nstates * 256
+  const uint8_t *eof;         // nstates: EOF step yields a match flag
+  const uint16_t *start;      // 128 start states by flag index
+  uint32_t n_normal, n_match_end, dead, quit;
+};
+
+struct RevDfaDev {
+  const uint16_t *full;
+  const uint8_t *eof;
+  const uint16_t *start;
+  uint32_t n_normal, n_match_end, dead, quit;
+};
+
+// Set DFA: final answer is eof_mask[state after the last byte].
+struct SetDfaDev {
+  const uint8_t *lds_image;
+  uint32_t lds_bytes;
+  uint32_t hot;
+  const uint16_t *full;
+  const uint64_t *eof_mask;
+  const uint16_t *start;
+  uint32_t n_normal, n_match_end, dead, quit;
+};
+
+hipError_t launch_dfa_fwd(int mode, const BatchDev &b, const FwdDfaDev &f, const RevDfaDev &r, void *out,
+                          hipStream_t st, int grid);
+hipError_t launch_dfa_set(const BatchDev &b, const SetDfaDev &f, uint64_t *out, hipStream_t st, int grid);
+
+}  // namespace rure_amd

@@ -1,0 +1,718 @@
+// rure_amd: C ABI (include/rure_amd.h) over the host compiler + HIP kernels.
+//
+// Mirrors the reference C API regex-capi/src/rure.rs (compile 95-150,
+// is_match 158-168, find 170-187, shortest_match 207-224, iter 308-360,
+// options 13-19/67-74, set 470-572, errors regex-capi/src/error.rs) and the
+// engine construction of src/exec.rs:273-327 (three programs per regex: NFA,
+// forward DFA with `.*?`, reverse DFA).  All matching runs on the GPU.
+#include "../../include/rure_amd.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "host/dfa_build.hpp"
+#include "host/program.hpp"
+#include "host/syntax.hpp"
+#include "kernels/dfa_scan.hpp"
+
+using namespace rure_amd;
+
+struct rure_error {
+  std::string msg;
+};
+
+struct rure_options {
+  size_t size_limit = 10u << 20;       // rure.rs:67-74, re_builder.rs:30-31
+  size_t dfa_size_limit = 2u << 20;
+};
+
+namespace {
+
+[[noreturn]] void die(const std::string &m) {
+  fprintf(stderr, "rure_amd: %s\n", m.c_str());
+  fprintf(stderr, "aborting\n");
+  abort();
+}
+
+bool hip_ok(hipError_t e, std::string *err) {
+  if (e == hipSuccess) return true;
+  if (err) *err = std::string("HIP error: ") + hipGetErrorString(e);
+  return false;
+}
+
+// Device copy of the automata of one regex on one device.
+struct DevTables {
+  void *blob = nullptr;
+  FwdDfaDev f{};
+  RevDfaDev r{};
+  SetDfaDev s{};
+  int cus = 256;
+};
+
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// Packs a materialized forward (or set) DFA into the LDS image / full table.
+struct PackedFwd {
+  std::vector<uint8_t> lds;
+  std::vector<uint16_t> full;
+  std::vector<uint8_t> eof;
+  std::vector<uint64_t> eof_mask;
+  std::vector<uint16_t> start;
+  uint32_t hot = 0;
+};
+
+bool pack_forward(const DenseDfa &d, PackedFwd *p, std::string *err) {
+  if (d.nstates > 65535) {
+    if (err) *err = "DFA has too many states for u16 tables";
+    return false;
+  }
+  uint32_t hot = (uint32_t)std::min(d.n_normal, 255);
+  p->hot = hot;
+  size_t lds_bytes = ((size_t)(hot + 1) * 256 + 15) & ~(size_t)15;
+  p->lds.assign(lds_bytes, 0);
+  for (uint32_t s = 0; s <= hot; ++s)
+    for (int b = 0; b < 256; ++b) {
+      uint32_t t = (s < hot) ? d.trans[(size_t)s * 256 + b] : hot;
+      p->lds[(size_t)s * 256 + b] = (uint8_t)(t < hot ? t : hot);
+    }
+  p->full.resize((size_t)d.nstates * 256);
+  for (size_t i = 0; i < p->full.size(); ++i) p->full[i] = (uint16_t)d.trans[i];
+  p->eof.assign(d.eof_match.begin(), d.eof_match.end());
+  p->eof_mask.assign(d.eof_mask.begin(), d.eof_mask.end());
+  p->start.resize(128);
+  for (int i = 0; i < 128; ++i) p->start[i] = (uint16_t)d.start[i];
+  return true;
+}
+
+struct Blob {
+  std::vector<uint8_t> bytes;
+  size_t add(const void *src, size_t n) {
+    size_t off = align256(bytes.size());
+    bytes.resize(off + align256(n));
+    if (n) memcpy(bytes.data() + off, src, n);
+    return off;
+  }
+};
+
+int device_cus(int dev) {
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return 256;
+  return prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+}
+
+int grid_for(size_t count, uint32_t lds_bytes, int cus) {
+  size_t blocks = (count + 255) / 256;
+  uint32_t per_cu = 8;
+  if (lds_bytes > 0) per_cu = std::max<uint32_t>(1, std::min<uint32_t>(8, (160u * 1024u) / lds_bytes));
+  size_t cap = (size_t)cus * per_cu;
+  if (blocks > cap) blocks = cap;
+  if (blocks == 0) blocks = 1;
+  return (int)blocks;
+}
+
+// A reusable host->device staging area for the single-haystack entry points.
+struct Staging {
+  int dev = -1;
+  hipStream_t stream = nullptr;
+  uint8_t *hay = nullptr;
+  size_t cap = 0;
+  uint64_t *res = nullptr;
+  ~Staging() {
+    if (hay) (void)hipFree(hay);
+    if (res) (void)hipFree(res);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+  bool ensure(int d, size_t n, std::string *err) {
+    if (dev != d) {
+      if (hay) (void)hipFree(hay);
+      if (res) (void)hipFree(res);
+      if (stream) (void)hipStreamDestroy(stream);
+      hay = nullptr; res = nullptr; stream = nullptr; cap = 0;
+      dev = d;
+      if (!hip_ok(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), err)) return false;
+      if (!hip_ok(hipMalloc(&res, 64 * sizeof(uint64_t)), err)) return false;
+    }
+    if (n + 16 > cap) {
+      if (hay) (void)hipFree(hay);
+      hay = nullptr;
+      size_t c = std::max<size_t>(n + 16, 1 << 16);
+      if (!hip_ok(hipMalloc(&hay, c), err)) return false;
+      cap = c;
+    }
+    return true;
+  }
+};
+
+}  // namespace
+
+struct rure {
+  std::string pattern;
+  uint32_t flags = 0;
+  rure_options opts;
+  Expr expr;
+  Program nfa, fwd, rev;
+  std::mutex mu;
+  bool built = false, dfa_ok = false;
+  std::string dfa_err;
+  DenseDfa dfwd, drev;
+  PackedFwd pf;
+  std::map<int, DevTables> dev;
+  Staging stage;
+};
+
+struct rure_set {
+  std::vector<std::string> patterns;
+  uint32_t flags = 0;
+  rure_options opts;
+  std::vector<Expr> exprs;
+  Program fwd;      // compile_many DFA program (compile.rs:162-198)
+  Program nfa;      // compile_many NFA program (no `.*?`, no saves)
+  std::mutex mu;
+  bool built = false, dfa_ok = false;
+  std::string dfa_err;
+  DenseDfa dfa;
+  PackedFwd pf;
+  std::map<int, DevTables> dev;
+  Staging stage;
+  rure *single = nullptr;   // one-pattern sets compile with compile_one
+};
+
+struct rure_iter {
+  rure *re;
+  size_t last_end = 0;
+  bool has_last_match = false;
+  size_t last_match = 0;
+};
+
+namespace {
+
+SyntaxFlags syntax_flags(uint32_t flags) {  // rure.rs:119-124
+  SyntaxFlags f;
+  f.casei = (flags & RURE_FLAG_CASEI) != 0;
+  f.multi = (flags & RURE_FLAG_MULTI) != 0;
+  f.dotnl = (flags & RURE_FLAG_DOTNL) != 0;
+  f.swap_greed = (flags & RURE_FLAG_SWAP_GREED) != 0;
+  f.ignore_space = (flags & RURE_FLAG_SPACE) != 0;
+  f.unicode = (flags & RURE_FLAG_UNICODE) != 0;
+  f.allow_bytes = true;  // bytes::RegexBuilder (re_builder.rs:171, exec.rs:225)
+  return f;
+}
+
+bool build_regex_dfas(rure *re) {
+  std::lock_guard<std::mutex> g(re->mu);
+  if (re->built) return re->dfa_ok;
+  re->built = true;
+  DfaBuildLimits lim;
+  std::string err;
+  if (!build_dense_dfa(re->fwd, lim, &re->dfwd, &err) || !build_dense_dfa(re->rev, lim, &re->drev, &err) ||
+      !pack_forward(re->dfwd, &re->pf, &err) || re->drev.nstates > 65535) {
+    re->dfa_err = err.empty() ? "reverse DFA too large" : err;
+    re->dfa_ok = false;
+    return false;
+  }
+  re->dfa_ok = true;
+  return true;
+}
+
+bool build_set_dfa(rure_set *rs) {
+  std::lock_guard<std::mutex> g(rs->mu);
+  if (rs->built) return rs->dfa_ok;
+  rs->built = true;
+  if (rs->exprs.empty()) { rs->dfa_ok = true; return true; }
+  DfaBuildLimits lim;
+  std::string err;
+  if (!build_dense_dfa(rs->fwd, lim, &rs->dfa, &err) || !pack_forward(rs->dfa, &rs->pf, &err)) {
+    rs->dfa_err = err;
+    rs->dfa_ok = false;
+    return false;
+  }
+  rs->dfa_ok = true;
+  return true;
+}
+
+// Upload (once per device) and return device descriptors.
+DevTables *regex_device(rure *re, std::string *err) {
+  if (!build_regex_dfas(re)) { if (err) *err = re->dfa_err; return nullptr; }
+  int d = 0;
+  if (!hip_ok(hipGetDevice(&d), err)) return nullptr;
+  std::lock_guard<std::mutex> g(re->mu);
+  auto it = re->dev.find(d);
+  if (it != re->dev.end()) return &it->second;
+  const PackedFwd &pf = re->pf;
+  const DenseDfa &rv = re->drev;
+  std::vector<uint16_t> rfull(rv.trans.size()), rstart(128);
+  for (size_t i = 0; i < rv.trans.size(); ++i) rfull[i] = (uint16_t)rv.trans[i];
+  for (int i = 0; i < 128; ++i) rstart[i] = (uint16_t)rv.start[i];
+  Blob b;
+  size_t o_lds = b.add(pf.lds.data(), pf.lds.size());
+  size_t o_full = b.add(pf.full.data(), pf.full.size() * 2);
+  size_t o_eof = b.add(pf.eof.data(), pf.eof.size());
+  size_t o_start = b.add(pf.start.data(), 256);
+  size_t o_rfull = b.add(rfull.data(), rfull.size() * 2);
+  size_t o_reof = b.add(rv.eof_match.data(), rv.eof_match.size());
+  size_t o_rstart = b.add(rstart.data(), 256);
+  DevTables t;
+  if (!hip_ok(hipMalloc(&t.blob, b.bytes.size()), err)) return nullptr;
+  if (!hip_ok(hipMemcpy(t.blob, b.bytes.data(), b.bytes.size(), hipMemcpyHostToDevice), err)) {
+    (void)hipFree(t.blob);
+    return nullptr;
+  }
+  uint8_t *base = (uint8_t *)t.blob;
+  const DenseDfa &fw = re->dfwd;
+  t.f.lds_image = base + o_lds;
+  t.f.lds_bytes = (uint32_t)pf.lds.size();
+  t.f.hot = pf.hot;
+  t.f.full = (const uint16_t *)(base + o_full);
+  t.f.eof = base + o_eof;
+  t.f.start = (const uint16_t *)(base + o_start);
+  t.f.n_normal = fw.n_normal;
+  t.f.n_match_end = fw.n_match_end;
+  t.f.dead = fw.dead;
+  t.f.quit = fw.quit < 0 ? 0xFFFFFFFFu : (uint32_t)fw.quit;
+  t.r.full = (const uint16_t *)(base + o_rfull);
+  t.r.eof = base + o_reof;
+  t.r.start = (const uint16_t *)(base + o_rstart);
+  t.r.n_normal = rv.n_normal;
+  t.r.n_match_end = rv.n_match_end;
+  t.r.dead = rv.dead;
+  t.r.quit = rv.quit < 0 ? 0xFFFFFFFFu : (uint32_t)rv.quit;
+  t.cus = device_cus(d);
+  return &(re->dev[d] = t);
+}
+
+DevTables *set_device(rure_set *rs, std::string *err) {
+  if (!build_set_dfa(rs)) { if (err) *err = rs->dfa_err; return nullptr; }
+  int d = 0;
+  if (!hip_ok(hipGetDevice(&d), err)) return nullptr;
+  std::lock_guard<std::mutex> g(rs->mu);
+  auto it = rs->dev.find(d);
+  if (it != rs->dev.end()) return &it->second;
+  const PackedFwd &pf = rs->pf;
+  const std::vector<uint64_t> &mask = pf.eof_mask;
+  Blob b;
+  size_t o_lds = b.add(pf.lds.data(), pf.lds.size());
+  size_t o_full = b.add(pf.full.data(), pf.full.size() * 2);
+  size_t o_mask = b.add(mask.data(), mask.size() * 8);
+  size_t o_start = b.add(pf.start.data(), 256);
+  DevTables t;
+  if (!hip_ok(hipMalloc(&t.blob, b.bytes.size()), err)) return nullptr;
+  if (!hip_ok(hipMemcpy(t.blob, b.bytes.data(), b.bytes.size(), hipMemcpyHostToDevice), err)) {
+    (void)hipFree(t.blob);
+    return nullptr;
+  }
+  uint8_t *base = (uint8_t *)t.blob;
+  const DenseDfa &fw = rs->dfa;
+  t.s.lds_image = base + o_lds;
+  t.s.lds_bytes = (uint32_t)pf.lds.size();
+  t.s.hot = pf.hot;
+  t.s.full = (const uint16_t *)(base + o_full);
+  t.s.eof_mask = (const uint64_t *)(base + o_mask);
+  t.s.start = (const uint16_t *)(base + o_start);
+  t.s.n_normal = fw.n_normal;
+  t.s.n_match_end = fw.n_match_end;
+  t.s.dead = fw.dead;
+  t.s.quit = fw.quit < 0 ? 0xFFFFFFFFu : (uint32_t)fw.quit;
+  t.cus = device_cus(d);
+  return &(rs->dev[d] = t);
+}
+
+bool to_batch(const rure_amd_batch *b, BatchDev *o) {
+  if (!b || (!b->haystack && b->count > 0)) return false;
+  o->hay = b->haystack;
+  o->offs = b->offsets;
+  o->stride = b->stride;
+  o->length = b->length;
+  o->count = b->count;
+  o->start = b->start;
+  return true;
+}
+
+const uint64_t kQuit = ~0ull - 1;
+
+// Runs one regex over one host haystack on the GPU (single-call entry points).
+// mode: MODE_FIND / MODE_ISMATCH / MODE_SHORTEST.  Returns false if no match.
+bool single_call(rure *re, int mode, const uint8_t *hay, size_t len, size_t start, uint64_t *r0, uint64_t *r1) {
+  std::string err;
+  DevTables *t = regex_device(re, &err);
+  if (!t) die(err);
+  std::lock_guard<std::mutex> g(re->mu);
+  int d = 0;
+  if (!hip_ok(hipGetDevice(&d), &err)) die(err);
+  if (!re->stage.ensure(d, len, &err)) die(err);
+  hipStream_t st = re->stage.stream;
+  if (len && !hip_ok(hipMemcpyAsync(re->stage.hay, hay, len, hipMemcpyHostToDevice, st), &err)) die(err);
+  BatchDev b{re->stage.hay, nullptr, 0, len, 1, start};
+  if (!hip_ok(launch_dfa_fwd(mode, b, t->f, t->r, re->stage.res, st, 1), &err)) die(err);
+  uint64_t out[2] = {~0ull, ~0ull};
+  size_t nbytes = mode == MODE_FIND ? 16 : mode == MODE_SHORTEST ? 8 : 1;
+  if (!hip_ok(hipMemcpyAsync(out, re->stage.res, nbytes, hipMemcpyDeviceToHost, st), &err)) die(err);
+  if (!hip_ok(hipStreamSynchronize(st), &err)) die(err);
+  if (mode == MODE_ISMATCH) {
+    uint8_t v = (uint8_t)(out[0] & 0xFF);
+    if (v == 2) die("Unicode word boundary on non-ASCII input needs the NFA kernel (not available)");
+    return v == 1;
+  }
+  if (out[0] == kQuit || (mode == MODE_FIND && out[1] == kQuit))
+    die("Unicode word boundary on non-ASCII input needs the NFA kernel (not available)");
+  if (out[0] == ~0ull) return false;
+  *r0 = out[0];
+  if (r1) *r1 = out[1];
+  return true;
+}
+
+uint64_t set_single_call(rure_set *rs, const uint8_t *hay, size_t len, size_t start) {
+  std::string err;
+  DevTables *t = set_device(rs, &err);
+  if (!t) die(err);
+  std::lock_guard<std::mutex> g(rs->mu);
+  int d = 0;
+  if (!hip_ok(hipGetDevice(&d), &err)) die(err);
+  if (!rs->stage.ensure(d, len, &err)) die(err);
+  hipStream_t st = rs->stage.stream;
+  if (len && !hip_ok(hipMemcpyAsync(rs->stage.hay, hay, len, hipMemcpyHostToDevice, st), &err)) die(err);
+  BatchDev b{rs->stage.hay, nullptr, 0, len, 1, start};
+  if (!hip_ok(launch_dfa_set(b, t->s, rs->stage.res, st, 1), &err)) die(err);
+  uint64_t out = 0;
+  if (!hip_ok(hipMemcpyAsync(&out, rs->stage.res, 8, hipMemcpyDeviceToHost, st), &err)) die(err);
+  if (!hip_ok(hipStreamSynchronize(st), &err)) die(err);
+  if (out == kQuit) die("Unicode word boundary on non-ASCII input needs the NFA kernel (not available)");
+  return out;
+}
+
+void fill_prog_info(const Program &p, rure_amd_prog_info *info) {
+  info->ninsts = (uint32_t)p.insts.size();
+  info->start = p.start;
+  info->nmatches = (uint32_t)p.matches.size();
+  info->ncaptures = (uint32_t)p.capture_names.size();
+  info->anchored_start = p.anchored_start;
+  info->anchored_end = p.anchored_end;
+  info->has_unicode_word_boundary = p.has_unicode_word_boundary;
+  info->is_reverse = p.is_reverse;
+  memcpy(info->byte_classes, p.byte_classes, 256);
+}
+
+int64_t export_prog(const Program &p, rure_amd_prog_info *info, rure_amd_inst *insts, size_t cap) {
+  if (info) fill_prog_info(p, info);
+  if (insts) {
+    size_t n = std::min(cap, p.insts.size());
+    for (size_t i = 0; i < n; ++i) {
+      const Inst &in = p.insts[i];
+      insts[i] = rure_amd_inst{in.op, in.look, in.lo, in.hi, in.x, in.y};
+    }
+  }
+  return (int64_t)p.insts.size();
+}
+
+void fill_info(const DenseDfa &d, const Program &p, uint32_t hot, rure_amd_dfa_info *info) {
+  info->ok = 1;
+  info->states = d.nstates;
+  info->raw_states = d.raw_states;
+  info->normal = d.n_normal;
+  info->match_end = d.n_match_end;
+  info->dead = d.dead;
+  info->quit = d.quit;
+  info->hot = (int32_t)hot;
+  info->byte_classes = p.num_byte_classes();
+  info->insts = (int32_t)p.insts.size();
+}
+
+}  // namespace
+
+extern "C" {
+
+// ------------------------------------------------------------------ errors
+rure_error *rure_error_new(void) { return new rure_error(); }
+void rure_error_free(rure_error *err) { delete err; }
+const char *rure_error_message(rure_error *err) { return err ? err->msg.c_str() : ""; }
+
+// ----------------------------------------------------------------- options
+rure_options *rure_options_new(void) { return new rure_options(); }
+void rure_options_free(rure_options *o) { delete o; }
+void rure_options_size_limit(rure_options *o, size_t limit) { if (o) o->size_limit = limit; }
+void rure_options_dfa_size_limit(rure_options *o, size_t limit) { if (o) o->dfa_size_limit = limit; }
+
+// ----------------------------------------------------------------- compile
+rure *rure_compile(const uint8_t *pattern, size_t length, uint32_t flags, rure_options *options,
+                   rure_error *error) {
+  std::string pat((const char *)pattern, length);
+  {
+    size_t i = 0;
+    while (i < length) {  // rure.rs:101-112: the pattern must be UTF-8
+      uint32_t cp; size_t l;
+      if (!decode_utf8(pattern + i, length - i, &cp, &l)) {
+        if (error) error->msg = "pattern is not valid UTF-8 (invalid byte at offset " + std::to_string(i) + ")";
+        return nullptr;
+      }
+      i += l;
+    }
+  }
+  std::unique_ptr<rure> re(new rure());
+  re->pattern = pat;
+  re->flags = flags;
+  if (options) re->opts = *options;
+  std::string err;
+  if (!parse_regex(pat, syntax_flags(flags), &re->expr, &err)) {
+    if (error) error->msg = err;
+    return nullptr;
+  }
+  std::vector<Expr> es{re->expr};
+  CompileOptions o;
+  o.size_limit = re->opts.size_limit;
+  // exec.rs:288-306: nfa (bytes), dfa (.*? prefixed), dfa_reverse
+  if (!compile_program(es, o, &re->nfa, &err)) { if (error) error->msg = err; return nullptr; }
+  o.dfa = true;
+  if (!compile_program(es, o, &re->fwd, &err)) { if (error) error->msg = err; return nullptr; }
+  o.reverse = true;
+  if (!compile_program(es, o, &re->rev, &err)) { if (error) error->msg = err; return nullptr; }
+  re->fwd.dfa_size_limit = re->rev.dfa_size_limit = re->opts.dfa_size_limit;
+  return re.release();
+}
+
+rure *rure_compile_must(const char *pattern) {  // rure.rs:76-91
+  rure_error err;
+  rure *re = rure_compile((const uint8_t *)pattern, strlen(pattern), RURE_DEFAULT_FLAGS, nullptr, &err);
+  if (!re) {
+    fprintf(stderr, "%s\naborting from rure_compile_must\n", err.msg.c_str());
+    abort();
+  }
+  return re;
+}
+
+void rure_free(rure *re) {
+  if (!re) return;
+  for (auto &kv : re->dev) {
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(kv.first);
+    (void)hipFree(kv.second.blob);
+    (void)hipSetDevice(cur);
+  }
+  delete re;
+}
+
+// ---------------------------------------------------------------- searches
+bool rure_is_match(rure *re, const uint8_t *hay, size_t len, size_t start) {
+  uint64_t a;
+  return single_call(re, MODE_ISMATCH, hay, len, start, &a, nullptr);
+}
+
+bool rure_find(rure *re, const uint8_t *hay, size_t len, size_t start, rure_match *m) {
+  uint64_t s, e;
+  if (!single_call(re, MODE_FIND, hay, len, start, &s, &e)) return false;
+  if (m) { m->start = (size_t)s; m->end = (size_t)e; }
+  return true;
+}
+
+bool rure_shortest_match(rure *re, const uint8_t *hay, size_t len, size_t start, size_t *end) {
+  uint64_t e;
+  if (!single_call(re, MODE_SHORTEST, hay, len, start, &e, nullptr)) return false;
+  if (end) *end = (size_t)e;
+  return true;
+}
+
+rure_iter *rure_iter_new(rure *re) {
+  rure_iter *it = new rure_iter();
+  it->re = re;
+  return it;
+}
+void rure_iter_free(rure_iter *it) { delete it; }
+
+bool rure_iter_next(rure_iter *it, const uint8_t *hay, size_t len, rure_match *m) {  // rure.rs:322-360
+  while (true) {
+    if (it->last_end > len) return false;
+    uint64_t s, e;
+    if (!single_call(it->re, MODE_FIND, hay, len, it->last_end, &s, &e)) return false;
+    if (s == e) {
+      it->last_end += 1;
+      if (it->has_last_match && it->last_match == e) continue;
+    } else {
+      it->last_end = e;
+    }
+    it->has_last_match = true;
+    it->last_match = e;
+    if (m) { m->start = (size_t)s; m->end = (size_t)e; }
+    return true;
+  }
+}
+
+// --------------------------------------------------------------------- sets
+rure_set *rure_compile_set(const uint8_t **patterns, const size_t *lens, size_t count, uint32_t flags,
+                           rure_options *options, rure_error *error) {
+  std::unique_ptr<rure_set> rs(new rure_set());
+  rs->flags = flags;
+  if (options) rs->opts = *options;
+  for (size_t i = 0; i < count; ++i) {
+    std::string pat((const char *)patterns[i], lens[i]);
+    size_t k = 0;
+    while (k < pat.size()) {
+      uint32_t cp; size_t l;
+      if (!decode_utf8((const uint8_t *)pat.data() + k, pat.size() - k, &cp, &l)) {
+        if (error) error->msg = "pattern is not valid UTF-8";
+        return nullptr;
+      }
+      k += l;
+    }
+    Expr e;
+    std::string err;
+    if (!parse_regex(pat, syntax_flags(flags), &e, &err)) { if (error) error->msg = err; return nullptr; }
+    rs->patterns.push_back(pat);
+    rs->exprs.push_back(std::move(e));
+  }
+  if (rs->exprs.size() > 64) {
+    if (error) error->msg = "rure_amd: sets of more than 64 patterns are not supported yet";
+    return nullptr;
+  }
+  if (rs->exprs.size() == 1) {
+    rs->single = rure_compile((const uint8_t *)rs->patterns[0].data(), rs->patterns[0].size(), flags,
+                              options, error);
+    if (!rs->single) return nullptr;
+  } else if (!rs->exprs.empty()) {
+    CompileOptions o;
+    o.size_limit = rs->opts.size_limit;
+    o.dfa = true;
+    std::string err;
+    if (!compile_program(rs->exprs, o, &rs->fwd, &err)) { if (error) error->msg = err; return nullptr; }
+    o.dfa = false;
+    if (!compile_program(rs->exprs, o, &rs->nfa, &err)) { if (error) error->msg = err; return nullptr; }
+  }
+  return rs.release();
+}
+
+void rure_set_free(rure_set *rs) {
+  if (!rs) return;
+  if (rs->single) rure_free(rs->single);
+  for (auto &kv : rs->dev) {
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(kv.first);
+    (void)hipFree(kv.second.blob);
+    (void)hipSetDevice(cur);
+  }
+  delete rs;
+}
+
+size_t rure_set_len(rure_set *rs) { return rs->exprs.size(); }
+
+static uint64_t set_mask_single(rure_set *rs, const uint8_t *hay, size_t len, size_t start) {
+  if (rs->exprs.empty()) return 0;  // MatchType::Nothing (exec.rs:276-286)
+  if (rs->single) return rure_is_match(rs->single, hay, len, start) ? 1 : 0;  // dfa.rs:556-558
+  return set_single_call(rs, hay, len, start);
+}
+
+bool rure_set_is_match(rure_set *rs, const uint8_t *hay, size_t len, size_t start) {
+  return set_mask_single(rs, hay, len, start) != 0;
+}
+
+bool rure_set_matches(rure_set *rs, const uint8_t *hay, size_t len, size_t start, bool *matches) {
+  size_t n = rs->exprs.size();
+  for (size_t i = 0; i < n; ++i) matches[i] = false;  // rure.rs:557-562
+  uint64_t m = set_mask_single(rs, hay, len, start);
+  for (size_t i = 0; i < n; ++i) matches[i] = (m >> i) & 1;
+  return m != 0;
+}
+
+// ------------------------------------------------------------------ batches
+int rure_amd_find_batch(rure *re, const rure_amd_batch *batch, rure_match *out, void *stream) {
+  static_assert(sizeof(rure_match) == 16, "rure_match layout");
+  BatchDev b;
+  if (!re || !to_batch(batch, &b) || (!out && b.count)) return RURE_AMD_ERR_ARG;
+  if (b.count == 0) return RURE_AMD_OK;
+  std::string err;
+  DevTables *t = regex_device(re, &err);
+  if (!t) return err.rfind("HIP", 0) == 0 ? RURE_AMD_ERR_HIP : RURE_AMD_ERR_DFA;
+  int grid = grid_for(b.count, t->f.lds_bytes, t->cus);
+  if (launch_dfa_fwd(MODE_FIND, b, t->f, t->r, out, (hipStream_t)stream, grid) != hipSuccess) return RURE_AMD_ERR_HIP;
+  return RURE_AMD_OK;
+}
+
+int rure_amd_is_match_batch(rure *re, const rure_amd_batch *batch, uint8_t *out, void *stream) {
+  BatchDev b;
+  if (!re || !to_batch(batch, &b) || (!out && b.count)) return RURE_AMD_ERR_ARG;
+  if (b.count == 0) return RURE_AMD_OK;
+  std::string err;
+  DevTables *t = regex_device(re, &err);
+  if (!t) return err.rfind("HIP", 0) == 0 ? RURE_AMD_ERR_HIP : RURE_AMD_ERR_DFA;
+  int grid = grid_for(b.count, t->f.lds_bytes, t->cus);
+  if (launch_dfa_fwd(MODE_ISMATCH, b, t->f, t->r, out, (hipStream_t)stream, grid) != hipSuccess) return RURE_AMD_ERR_HIP;
+  return RURE_AMD_OK;
+}
+
+int rure_amd_shortest_match_batch(rure *re, const rure_amd_batch *batch, size_t *end, void *stream) {
+  BatchDev b;
+  if (!re || !to_batch(batch, &b) || (!end && b.count)) return RURE_AMD_ERR_ARG;
+  if (b.count == 0) return RURE_AMD_OK;
+  std::string err;
+  DevTables *t = regex_device(re, &err);
+  if (!t) return err.rfind("HIP", 0) == 0 ? RURE_AMD_ERR_HIP : RURE_AMD_ERR_DFA;
+  int grid = grid_for(b.count, t->f.lds_bytes, t->cus);
+  if (launch_dfa_fwd(MODE_SHORTEST, b, t->f, t->r, end, (hipStream_t)stream, grid) != hipSuccess) return RURE_AMD_ERR_HIP;
+  return RURE_AMD_OK;
+}
+
+int rure_amd_set_matches_batch(rure_set *rs, const rure_amd_batch *batch, uint64_t *mask, void *stream) {
+  BatchDev b;
+  if (!rs || !to_batch(batch, &b) || (!mask && b.count)) return RURE_AMD_ERR_ARG;
+  if (b.count == 0) return RURE_AMD_OK;
+  if (rs->exprs.size() < 2) return RURE_AMD_ERR_ARG;  // see rure_set_matches
+  std::string err;
+  DevTables *t = set_device(rs, &err);
+  if (!t) return err.rfind("HIP", 0) == 0 ? RURE_AMD_ERR_HIP : RURE_AMD_ERR_DFA;
+  int grid = grid_for(b.count, t->s.lds_bytes, t->cus);
+  if (launch_dfa_set(b, t->s, mask, (hipStream_t)stream, grid) != hipSuccess) return RURE_AMD_ERR_HIP;
+  return RURE_AMD_OK;
+}
+
+// ------------------------------------------------------------- diagnostics
+int rure_amd_dfa_info_get(rure *re, int which, rure_amd_dfa_info *info) {
+  if (!re || !info) return RURE_AMD_ERR_ARG;
+  memset(info, 0, sizeof(*info));
+  if (!build_regex_dfas(re)) { info->ok = 0; return RURE_AMD_ERR_DFA; }
+  if (which == 0) fill_info(re->dfwd, re->fwd, re->pf.hot, info);
+  else fill_info(re->drev, re->rev, 0, info);
+  return RURE_AMD_OK;
+}
+
+int rure_amd_set_dfa_info_get(rure_set *rs, rure_amd_dfa_info *info) {
+  if (!rs || !info) return RURE_AMD_ERR_ARG;
+  memset(info, 0, sizeof(*info));
+  if (!build_set_dfa(rs)) { info->ok = 0; return RURE_AMD_ERR_DFA; }
+  if (rs->exprs.empty()) return RURE_AMD_OK;
+  fill_info(rs->dfa, rs->fwd, rs->pf.hot, info);
+  return RURE_AMD_OK;
+}
+
+int64_t rure_amd_program_export(rure *re, int which, rure_amd_prog_info *info, rure_amd_inst *insts,
+                                size_t cap) {
+  if (!re) return RURE_AMD_ERR_ARG;
+  const Program &p = which == 0 ? re->fwd : which == 1 ? re->rev : re->nfa;
+  return export_prog(p, info, insts, cap);
+}
+
+int64_t rure_amd_set_program_export(rure_set *rs, int which, rure_amd_prog_info *info, rure_amd_inst *insts,
+                                    size_t cap) {
+  if (!rs) return RURE_AMD_ERR_ARG;
+  if (rs->single) return rure_amd_program_export(rs->single, which, info, insts, cap);
+  if (which == 1) return RURE_AMD_ERR_ARG;
+  return export_prog(which == 0 ? rs->fwd : rs->nfa, info, insts, cap);
+}
+
+int rure_amd_dfa_export(rure *re, int which, uint32_t *trans, uint8_t *eof_match, uint32_t *start) {
+  if (!re) return RURE_AMD_ERR_ARG;
+  if (!build_regex_dfas(re)) return RURE_AMD_ERR_DFA;
+  const DenseDfa &d = which == 0 ? re->dfwd : re->drev;
+  if (trans) memcpy(trans, d.trans.data(), d.trans.size() * 4);
+  if (eof_match) memcpy(eof_match, d.eof_match.data(), d.eof_match.size());
+  if (start) memcpy(start, d.start, sizeof(d.start));
+  return RURE_AMD_OK;
+}
+
+}  // extern "C"
