@@ -1,0 +1,82 @@
+"""Host-side simulation of the exported dense DFA tables, mirroring the
+kernel's algorithm (regex_amd/csrc/kernels/dfa_scan.hip) step for step.
+TEST INFRASTRUCTURE: validates the eager materializer + minimiser on CPU."""
+
+
+def word(b):
+    return b == 0x5F or 0x30 <= b <= 0x39 or 0x41 <= b <= 0x5A or 0x61 <= b <= 0x7A
+
+
+def fwd_flag(t, at):
+    start, end = at == 0, len(t) == 0
+    sl = at == 0 or t[at - 1] == 0x0A
+    wl = at > 0 and word(t[at - 1])
+    wn = at < len(t) and word(t[at])
+    return (1 if start else 0) | (2 if end else 0) | (4 if sl else 0) | (8 if end else 0) | \
+        (16 if wl != wn else 32) | (64 if wl else 0)
+
+
+def rev_flag(t, lo, at):
+    start, end = at == len(t), lo == len(t)
+    sl = at == len(t) or t[at] == 0x0A
+    wl = at < len(t) and word(t[at])
+    wn = at > lo and word(t[at - 1])
+    return (1 if start else 0) | (2 if end else 0) | (4 if sl else 0) | (8 if end else 0) | \
+        (16 if wl != wn else 32) | (64 if wl else 0)
+
+
+class QuitError(Exception):
+    pass
+
+
+def find(fwd, rev, t, start=0, mode="find"):
+    info, tr, eof, st = fwd
+    s = int(st[fwd_flag(t, start)])
+    last = None
+    if s >= info["normal"]:
+        return None
+    at = start
+    done = False
+    while at < len(t):
+        s = int(tr[s, t[at]])
+        if s >= info["normal"]:
+            if s < info["match_end"]:
+                last = at
+                if mode != "find":
+                    done = True
+                    break
+            elif s == info["dead"]:
+                done = True
+                break
+            else:
+                raise QuitError()
+        at += 1
+    if not done and eof[s]:
+        last = len(t)
+    if mode == "shortest":
+        return last
+    if mode == "is_match":
+        return last is not None
+    if last is None:
+        return None
+    if last == start:
+        return (start, start)
+    rinfo, rtr, reof, rst = rev
+    s = int(rst[rev_flag(t, start, last)])
+    rs = None
+    a = last
+    dead = False
+    while a > start:
+        a -= 1
+        s = int(rtr[s, t[a]])
+        if s >= rinfo["normal"]:
+            if s < rinfo["match_end"]:
+                rs = a + 1
+            elif s == rinfo["dead"]:
+                dead = True
+                break
+            else:
+                raise QuitError()
+    if not dead and reof[s]:
+        rs = start
+    return (rs, last)

@@ -1,0 +1,22 @@
+"""Loaders for the committed golden fixtures (tests/golden/)."""
+import gzip
+import json
+import os
+
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def vectors():
+    with open(os.path.join(G, "reference_vectors.json"), encoding="utf-8") as f:
+        return json.load(f)
+
+
+def known_counts():
+    with open(os.path.join(G, "known_counts.json")) as f:
+        return json.load(f)
+
+
+def corpus(name):
+    fn = {"sherlock": "sherlock.txt.gz", "regexdna": "regexdna-input.txt.gz"}[name]
+    with gzip.open(os.path.join(G, fn), "rb") as f:
+        return f.read()
