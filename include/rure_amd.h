@@ -131,6 +131,8 @@ typedef struct rure_amd_dfa_info {
   int32_t hot;           /* states held in the LDS fast table */
   int32_t byte_classes;
   int32_t insts;
+  int32_t fast_stride;   /* bytes per dependent LDS lookup in the tile kernel (1, 2, 4) */
+  int32_t fast_classes;  /* local byte classes of the multi-byte table (K) */
 } rure_amd_dfa_info;
 /* which: 0 = forward DFA program, 1 = reverse DFA program. */
 int rure_amd_dfa_info_get(rure *re, int which, rure_amd_dfa_info *info);

@@ -42,7 +42,7 @@ class RureBatch(ctypes.Structure):
 class DfaInfo(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in (
         "ok", "states", "raw_states", "normal", "match_end", "dead", "quit",
-        "hot", "byte_classes", "insts")]
+        "hot", "byte_classes", "insts", "fast_stride", "fast_classes")]
 
 
 class ProgInfo(ctypes.Structure):

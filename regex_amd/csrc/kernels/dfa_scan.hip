@@ -23,6 +23,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "dfa_scan.hpp"
 
 namespace rure_amd {
@@ -57,6 +59,8 @@ struct LaneState {
   uint64_t last;   // last match end (NONE if none)
   bool done;
   bool quit;
+  bool fast;       // multi-byte path: t holds s * P and s may be stale
+  uint32_t t;
 };
 
 static constexpr uint64_t NONE = ~0ull;
@@ -120,6 +124,87 @@ __device__ __forceinline__ void chunk16(LaneState &L, const FwdDfaDev &f, const 
   }
 }
 
+// Multi-byte fast path (STRIDE = 2 or 4 bytes per dependent LDS lookup).
+// The class lookups do not depend on the state, so only one LDS round trip
+// per STRIDE bytes sits on the critical path.
+template <int STRIDE>
+__device__ __forceinline__ uint32_t fastS(uint32_t t, uint32_t w, const uint8_t *cls, const uint16_t *tab) {
+  if (STRIDE == 4) {
+    uint32_t a = cls[w & 0xFF] + cls[256 + ((w >> 8) & 0xFF)] + cls[512 + ((w >> 16) & 0xFF)] + cls[768 + (w >> 24)];
+    return tab[t + a];
+  } else {
+    uint32_t a0 = cls[w & 0xFF] + cls[256 + ((w >> 8) & 0xFF)];
+    uint32_t a1 = cls[(w >> 16) & 0xFF] + cls[256 + (w >> 24)];
+    t = tab[t + a0];
+    return tab[t + a1];
+  }
+}
+
+template <int MODE, int STRIDE>
+__device__ __forceinline__ void chunk16s(LaneState &L, const FwdDfaDev &f, const uint8_t *cls, const uint16_t *tab,
+                                         uint4 v, uint64_t pos) {
+  if (L.fast) {
+    uint32_t t = L.t;
+    t = fastS<STRIDE>(t, v.x, cls, tab);
+    t = fastS<STRIDE>(t, v.y, cls, tab);
+    t = fastS<STRIDE>(t, v.z, cls, tab);
+    t = fastS<STRIDE>(t, v.w, cls, tab);
+    if (t != f.sent) { L.t = t; return; }
+    L.s = L.t / f.P;  // real state at the chunk start (rare path)
+    L.fast = false;
+  }
+  uint32_t words[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll 1
+  for (int j = 0; j < 16; ++j) {
+    careful_step<MODE>(L, f, (words[j >> 2] >> ((j & 3) * 8)) & 0xFF, pos + j);
+    if (L.done) return;
+  }
+  if (L.s < f.hot_s) { L.t = L.s * f.P; L.fast = true; }
+}
+
+template <int MODE>
+__device__ __forceinline__ void finish_lane(const LaneState &L, const RevDfaDev &r, const uint8_t *base,
+                                            uint64_t len, uint64_t lo, uint64_t h, void *out) {
+  if (MODE == MODE_ISMATCH) {
+    ((uint8_t *)out)[h] = L.quit ? 2 : (L.last != NONE ? 1 : 0);
+    return;
+  }
+  if (MODE == MODE_SHORTEST) {
+    ((uint64_t *)out)[h] = L.quit ? QUITMARK : L.last;
+    return;
+  }
+  uint64_t ms = NONE, me = NONE;
+  if (L.quit) {
+    ms = me = QUITMARK;
+  } else if (L.last != NONE) {
+    me = L.last;
+    if (me == lo) {
+      ms = lo;                              // exec.rs:647
+    } else {
+      // reverse scan over text[lo..me] (exec.rs:651-661, dfa.rs:768-866)
+      uint32_t s = r.start[rev_flag_index(base, lo, len, me)];
+      uint64_t rs = NONE;
+      bool dead = s == r.dead;
+      bool rq = false;
+      uint64_t a = me;
+      while (!dead && a > lo) {
+        --a;
+        s = r.full[(size_t)s * 256 + base[a]];
+        if (s >= r.n_normal) {
+          if (s < r.n_match_end) rs = a + 1;
+          else if (s == r.dead) dead = true;
+          else { rq = true; dead = true; }
+        }
+      }
+      if (!dead && r.eof[s]) rs = lo;
+      if (rq) { ms = me = QUITMARK; }
+      else ms = rs;
+    }
+  }
+  ((uint64_t *)out)[2 * h] = ms;
+  ((uint64_t *)out)[2 * h + 1] = me;
+}
+
 template <int MODE, bool STRIDED>
 __global__ __launch_bounds__(256) void dfa_fwd_kernel(BatchDev bt, FwdDfaDev f, RevDfaDev r, void *out) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -156,15 +241,17 @@ __global__ __launch_bounds__(256) void dfa_fwd_kernel(BatchDev bt, FwdDfaDev f, 
       step1<MODE>(L, f, lds, base[at], at);
       ++at;
     }
-    // body: 64-byte bursts per lane
-    while (!L.done && at + 64 <= len) {
+    // body: 128-byte bursts per lane (one whole cache line per burst, so no
+    // line is fetched twice even when the L2 is under pressure)
+    while (!L.done && at + 128 <= len) {
       const uint4 *p = (const uint4 *)(base + at);
-      uint4 v0 = p[0], v1 = p[1], v2 = p[2], v3 = p[3];
-      chunk16<MODE>(L, f, lds, v0, at);
-      if (!L.done) chunk16<MODE>(L, f, lds, v1, at + 16);
-      if (!L.done) chunk16<MODE>(L, f, lds, v2, at + 32);
-      if (!L.done) chunk16<MODE>(L, f, lds, v3, at + 48);
-      at += 64;
+      uint4 v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = p[k];
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (!L.done) chunk16<MODE>(L, f, lds, v[k], at + 16 * k);
+      at += 128;
     }
     while (!L.done && at + 16 <= len) {
       uint4 v = *(const uint4 *)(base + at);
@@ -178,45 +265,104 @@ __global__ __launch_bounds__(256) void dfa_fwd_kernel(BatchDev bt, FwdDfaDev f, 
     // EOF sentinel step (dfa.rs:748-763)
     if (!L.done && f.eof[L.s]) L.last = len;
 
-    if (MODE == MODE_ISMATCH) {
-      ((uint8_t *)out)[h] = L.quit ? 2 : (L.last != NONE ? 1 : 0);
-      continue;
-    }
-    if (MODE == MODE_SHORTEST) {
-      ((uint64_t *)out)[h] = L.quit ? QUITMARK : L.last;
-      continue;
-    }
-    uint64_t ms = NONE, me = NONE;
-    if (L.quit) {
-      ms = me = QUITMARK;
-    } else if (L.last != NONE) {
-      me = L.last;
-      const uint64_t lo = bt.start;
-      if (me == lo) {
-        ms = lo;                              // exec.rs:647
-      } else {
-        // reverse scan over text[lo..me] (exec.rs:651-661, dfa.rs:768-866)
-        uint32_t s = r.start[rev_flag_index(base, lo, len, me)];
-        uint64_t rs = NONE;
-        bool dead = s >= r.n_normal && s == r.dead;
-        bool rq = false;
-        uint64_t a = me;
-        while (!dead && a > lo) {
-          --a;
-          s = r.full[(size_t)s * 256 + base[a]];
-          if (s >= r.n_normal) {
-            if (s < r.n_match_end) rs = a + 1;
-            else if (s == r.dead) dead = true;
-            else { rq = true; dead = true; }
-          }
+    finish_lane<MODE>(L, r, base, len, bt.start, h, out);
+  }
+}
+
+// ------------------------------------------------------- coalesced tiles
+// Fixed-stride batches (stride % 16 == 0, search start 0, hot set <= 63
+// states): a wave owns 64 consecutive haystacks and walks them in lockstep
+// 128 bytes at a time.  The 8 KiB tile is fetched with coalesced loads (one
+// wave-instruction = 8 haystacks x one whole 128-byte line, instead of 64
+// scattered lines), transposed through a per-wave LDS buffer (rows XOR-
+// swizzled so the ds_read_b128 of 16 lanes hit 16 distinct bank groups), and
+// each lane then steps its own row through the DFA.  The next tile's loads
+// are in flight while the current one is scanned.
+static constexpr int kTileTab = 16384;   // largest LDS fast table of the tile path (hot + 1 <= 64 rows)
+
+template <int MODE, int TAB, int STRIDE>
+__global__ __launch_bounds__(256) void dfa_fwd_tile_kernel(BatchDev bt, FwdDfaDev f, RevDfaDev r, void *out) {
+  __shared__ __attribute__((aligned(16))) uint8_t tab[TAB];
+  const uint8_t *img = STRIDE == 1 ? f.lds_image : f.lds_image_s;
+  const uint32_t img_bytes = STRIDE == 1 ? f.lds_bytes : f.lds_bytes_s;
+  __shared__ __attribute__((aligned(16))) uint4 stage[4][64 * 8];
+  for (uint32_t i = threadIdx.x * 16; i < img_bytes; i += blockDim.x * 16)
+    *(uint4 *)(tab + i) = *(const uint4 *)(img + i);
+  __syncthreads();
+  const uint16_t *tab16 = (const uint16_t *)(tab + 1024);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint4 *buf = stage[w];
+  const uint64_t L = bt.length, S = bt.stride, n = bt.count;
+  const uint64_t L128 = L & ~(uint64_t)127;
+  const uint64_t nwaves = (uint64_t)gridDim.x * 4;
+  const int src_h = lane >> 3, src_seg = lane & 7;
+  for (uint64_t g = (uint64_t)blockIdx.x * 4 + w; g * 64 < n; g += nwaves) {
+    const uint64_t h = g * 64 + lane;
+    const bool valid = h < n;
+    const uint8_t *base = bt.hay + (valid ? h : 0) * S;
+    LaneState L_;
+    L_.last = NONE;
+    L_.quit = false;
+    L_.done = !valid;
+    L_.s = valid ? f.start[fwd_flag_index(base, L, 0)] : f.dead;
+    if (L_.s >= f.n_normal) L_.done = true;
+    L_.fast = STRIDE > 1 && !L_.done && L_.s < f.hot_s;
+    L_.t = L_.fast ? L_.s * f.P : 0;
+    // this lane's share of each coalesced tile load: haystack g*64 + 8k + src_h,
+    // 16-byte segment src_seg (rows past the batch end re-read row n-1; unused)
+    uint64_t hh0 = g * 64 + src_h;
+    const uint8_t *src0 = bt.hay + (hh0 < n ? hh0 : n - 1) * S + 16 * src_seg;
+    const uint64_t kstep = 8 * S;                     // wave-uniform
+    const uint64_t klast = (n - 1) * S + 16 * src_seg;  // clamp rows past the batch end
+    uint4 n0, n1, n2, n3, n4, n5, n6, n7;
+    uint64_t at = 0;
+#define RURE_SRC(k) ((g * 64 + 8 * (k) + src_h < n) ? src0 + (k) * kstep : bt.hay + klast)
+#define RURE_LOAD_TILE(a)                                                          \
+  n0 = *(const uint4 *)(RURE_SRC(0) + (a)); n1 = *(const uint4 *)(RURE_SRC(1) + (a));  \
+  n2 = *(const uint4 *)(RURE_SRC(2) + (a)); n3 = *(const uint4 *)(RURE_SRC(3) + (a));  \
+  n4 = *(const uint4 *)(RURE_SRC(4) + (a)); n5 = *(const uint4 *)(RURE_SRC(5) + (a));  \
+  n6 = *(const uint4 *)(RURE_SRC(6) + (a)); n7 = *(const uint4 *)(RURE_SRC(7) + (a));
+#define RURE_STAGE(k, v) buf[(8 * (k) + src_h) * 8 + (src_seg ^ (((8 * (k) + src_h) >> 1) & 7))] = (v);
+    if (L128) { RURE_LOAD_TILE(0) }
+    const int sw = (lane >> 1) & 7;
+    for (; at < L128; at += 128) {
+      if (!__any(!L_.done)) break;
+      // stage the tile (rows XOR-swizzled), then prefetch the next one
+      RURE_STAGE(0, n0) RURE_STAGE(1, n1) RURE_STAGE(2, n2) RURE_STAGE(3, n3)
+      RURE_STAGE(4, n4) RURE_STAGE(5, n5) RURE_STAGE(6, n6) RURE_STAGE(7, n7)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const uint64_t an = (at + 128 < L128) ? at + 128 : at;
+      RURE_LOAD_TILE(an)
+      uint4 cur = buf[lane * 8 + sw];
+#pragma unroll 1
+      for (int m = 0; m < 8; ++m) {
+        uint4 nx = buf[lane * 8 + ((m + 1 < 8 ? m + 1 : 7) ^ sw)];
+        if (!L_.done) {
+          if (STRIDE == 1) chunk16<MODE>(L_, f, tab, cur, at + 16 * m);
+          else chunk16s<MODE, STRIDE>(L_, f, tab, tab16, cur, at + 16 * m);
         }
-        if (!dead && r.eof[s]) rs = lo;
-        if (rq) { ms = me = QUITMARK; }
-        else ms = rs;
+        cur = nx;
       }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    ((uint64_t *)out)[2 * h] = ms;
-    ((uint64_t *)out)[2 * h + 1] = me;
+#undef RURE_LOAD_TILE
+#undef RURE_SRC
+#undef RURE_STAGE
+    if (valid) {
+      if (STRIDE > 1 && L_.fast) { L_.s = L_.t / f.P; L_.fast = false; }
+      at = L128;
+      while (!L_.done && at < L) {
+        if (STRIDE == 1) step1<MODE>(L_, f, tab, base[at], at);
+        else careful_step<MODE>(L_, f, base[at], at);
+        ++at;
+      }
+      if (!L_.done && f.eof[L_.s]) L_.last = L;
+      finish_lane<MODE>(L_, r, base, L, 0, h, out);
+    }
   }
 }
 
@@ -299,9 +445,48 @@ static hipError_t launch_fwd(const BatchDev &b, const FwdDfaDev &f, const RevDfa
   return hipGetLastError();
 }
 
+template <int MODE, int STRIDE>
+static hipError_t launch_tile_s(const BatchDev &b, const FwdDfaDev &f, const RevDfaDev &r, void *out, hipStream_t st,
+                                int grid) {
+  const uint32_t bytes = STRIDE == 1 ? f.lds_bytes : f.lds_bytes_s;
+  if (bytes <= 4096)
+    hipLaunchKernelGGL((dfa_fwd_tile_kernel<MODE, 4096, STRIDE>), dim3(grid), dim3(256), 0, st, b, f, r, out);
+  else
+    hipLaunchKernelGGL((dfa_fwd_tile_kernel<MODE, kTileTab, STRIDE>), dim3(grid), dim3(256), 0, st, b, f, r, out);
+  return hipGetLastError();
+}
+
+template <int MODE>
+static hipError_t launch_tile(const BatchDev &b, const FwdDfaDev &f, const RevDfaDev &r, void *out, hipStream_t st,
+                              int grid) {
+  // Latency-bound regime (few lanes per CU): fewer dependent LDS lookups per
+  // byte win (multi-byte table).  Throughput regime (many lanes): fewer LDS
+  // operations per byte win (byte table, one ds_read_u8 per byte).
+  const bool latency_bound = b.count <= (uint64_t)f.cus * 16 * 64 / 2;  // < half the resident lanes
+  if (latency_bound && f.stride == 4 && f.lds_bytes_s <= (uint32_t)kTileTab) return launch_tile_s<MODE, 4>(b, f, r, out, st, grid);
+  if (latency_bound && f.stride == 2 && f.lds_bytes_s <= (uint32_t)kTileTab) return launch_tile_s<MODE, 2>(b, f, r, out, st, grid);
+  return launch_tile_s<MODE, 1>(b, f, r, out, st, grid);
+}
+
+bool tile_path_ok(const BatchDev &b, const FwdDfaDev &f) {
+  return b.offs == nullptr && b.start == 0 && (b.stride % 16) == 0 && (((uintptr_t)b.hay) & 15) == 0 &&
+         b.length <= b.stride && b.length >= 128 &&
+         f.lds_bytes <= (uint32_t)kTileTab;
+}
+
 hipError_t launch_dfa_fwd(int mode, const BatchDev &b, const FwdDfaDev &f, const RevDfaDev &r, void *out,
                           hipStream_t st, int grid) {
   const bool strided = b.offs == nullptr;
+  if (tile_path_ok(b, f)) {
+    int waves = (int)((b.count + 63) / 64);
+    int tgrid = std::min(grid, (waves + 3) / 4);
+    if (tgrid < 1) tgrid = 1;
+    switch (mode) {
+      case MODE_FIND: return launch_tile<MODE_FIND>(b, f, r, out, st, tgrid);
+      case MODE_ISMATCH: return launch_tile<MODE_ISMATCH>(b, f, r, out, st, tgrid);
+      default: return launch_tile<MODE_SHORTEST>(b, f, r, out, st, tgrid);
+    }
+  }
   switch (mode) {
     case MODE_FIND: return strided ? launch_fwd<MODE_FIND, true>(b, f, r, out, st, grid)
                                    : launch_fwd<MODE_FIND, false>(b, f, r, out, st, grid);

@@ -20,6 +20,15 @@ struct FwdDfaDev {
   const uint8_t *lds_image;   // (hot + 1) * 256 bytes, padded to 16
   uint32_t lds_bytes;
   uint32_t hot;
+  // Multi-byte fast table for the coalesced-tile kernel (stride 2 or 4 bytes
+  // per LDS lookup over local byte classes of the ASCII-hot sub-DFA);
+  // stride == 1 means "use lds_image".  Image: 4 x 256 u8 class tables
+  // (class * K^(stride-1-p) for byte position p) then (hot_s + 1) * P u16
+  // entries holding next_state * P; sentinel = hot_s * P.
+  const uint8_t *lds_image_s;
+  uint32_t lds_bytes_s;
+  uint32_t stride, hot_s, P, sent;
+  uint32_t cus;               // compute units of the device (launch heuristics)
   const uint16_t *full;       // nstates * 256
   const uint8_t *eof;         // nstates: EOF step yields a match flag
   const uint16_t *start;      // 128 start states by flag index

@@ -63,6 +63,8 @@ size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 // Packs a materialized forward (or set) DFA into the LDS image / full table.
 struct PackedFwd {
   std::vector<uint8_t> lds;
+  std::vector<uint8_t> lds_s;   // multi-byte (stride 2/4) fast table image, empty if stride 1
+  uint32_t stride = 1, hot_s = 0, P = 1, sent = 0;
   std::vector<uint16_t> full;
   std::vector<uint8_t> eof;
   std::vector<uint64_t> eof_mask;
@@ -70,12 +72,81 @@ struct PackedFwd {
   uint32_t hot = 0;
 };
 
+// Multi-byte fast table over the ASCII-hot sub-DFA (states [0, A)): bytes
+// are grouped into K local classes (identical columns over the hot states,
+// non-hot targets folded into the sentinel A); if K^stride is small the
+// table maps (state, class_1..class_stride) -> next state in one lookup.
+void build_stride_image(const DenseDfa &d, PackedFwd *p) {
+  const int A = std::min(std::min(d.n_ascii, d.n_normal), 255);
+  p->stride = 1;
+  if (A <= 0) return;
+  std::vector<int> cls(256, -1);
+  std::vector<int> rep;
+  std::map<std::vector<uint16_t>, int> seen;
+  for (int b = 0; b < 256; ++b) {
+    std::vector<uint16_t> col(A);
+    for (int s = 0; s < A; ++s) {
+      uint32_t t = d.trans[(size_t)s * 256 + b];
+      col[s] = (uint16_t)(t < (uint32_t)A ? t : A);
+    }
+    auto it = seen.find(col);
+    if (it == seen.end()) { it = seen.emplace(col, (int)rep.size()).first; rep.push_back(b); }
+    cls[b] = it->second;
+  }
+  const int K = (int)rep.size();
+  int stride = 1;
+  const long budget = (16384 - 1024) / 2;  // u16 entries after the 1 KiB class tables
+  if (K <= 4 && (long)(A + 1) * K * K * K * K <= budget) stride = 4;
+  else if (K <= 16 && (long)(A + 1) * K * K <= budget) stride = 2;
+  if (stride == 1) return;
+  uint32_t P = 1;
+  for (int i = 0; i < stride; ++i) P *= (uint32_t)K;
+  std::vector<uint8_t> img(1024, 0);
+  for (int pos = 0; pos < stride; ++pos) {
+    uint32_t mul = 1;
+    for (int i = pos + 1; i < stride; ++i) mul *= (uint32_t)K;
+    for (int b = 0; b < 256; ++b) img[pos * 256 + b] = (uint8_t)(cls[b] * mul);
+  }
+  const size_t nent = (size_t)(A + 1) * P;
+  std::vector<uint16_t> tab(nent);
+  for (int s = 0; s <= A; ++s) {
+    for (uint32_t combo = 0; combo < P; ++combo) {
+      uint32_t t = (uint32_t)s;
+      uint32_t c = combo, div = P / (uint32_t)K;
+      for (int pos = 0; pos < stride; ++pos) {
+        int k = (int)(c / div);
+        c %= div;
+        if (div > 1) div /= (uint32_t)K;
+        if (t < (uint32_t)A) {
+          uint32_t nx = d.trans[(size_t)t * 256 + rep[k]];
+          t = nx < (uint32_t)A ? nx : (uint32_t)A;
+        }
+      }
+      tab[(size_t)s * P + combo] = (uint16_t)(t * P);
+    }
+  }
+  img.resize(1024 + nent * 2);
+  memcpy(img.data() + 1024, tab.data(), nent * 2);
+  img.resize((img.size() + 15) & ~(size_t)15, 0);
+  p->lds_s = std::move(img);
+  p->stride = (uint32_t)stride;
+  p->hot_s = (uint32_t)A;
+  p->P = P;
+  p->sent = (uint32_t)A * P;
+}
+
 bool pack_forward(const DenseDfa &d, PackedFwd *p, std::string *err) {
   if (d.nstates > 65535) {
     if (err) *err = "DFA has too many states for u16 tables";
     return false;
   }
-  uint32_t hot = (uint32_t)std::min(d.n_normal, 255);
+  // LDS fast table: the normal states reachable through ASCII bytes are
+  // numbered first; hold them plus further BFS-order states in the smallest
+  // of three table sizes (4 KiB / 16 KiB / 64 KiB) that fits the ASCII set,
+  // so that several workgroups stay resident per CU.
+  int need = std::min(d.n_ascii, d.n_normal);
+  int cap = need + 1 <= 16 ? 15 : need + 1 <= 64 ? 63 : 255;
+  uint32_t hot = (uint32_t)std::min(d.n_normal, cap);
   p->hot = hot;
   size_t lds_bytes = ((size_t)(hot + 1) * 256 + 15) & ~(size_t)15;
   p->lds.assign(lds_bytes, 0);
@@ -84,6 +155,7 @@ bool pack_forward(const DenseDfa &d, PackedFwd *p, std::string *err) {
       uint32_t t = (s < hot) ? d.trans[(size_t)s * 256 + b] : hot;
       p->lds[(size_t)s * 256 + b] = (uint8_t)(t < hot ? t : hot);
     }
+  build_stride_image(d, p);
   p->full.resize((size_t)d.nstates * 256);
   for (size_t i = 0; i < p->full.size(); ++i) p->full[i] = (uint16_t)d.trans[i];
   p->eof.assign(d.eof_match.begin(), d.eof_match.end());
@@ -254,6 +326,7 @@ DevTables *regex_device(rure *re, std::string *err) {
   for (int i = 0; i < 128; ++i) rstart[i] = (uint16_t)rv.start[i];
   Blob b;
   size_t o_lds = b.add(pf.lds.data(), pf.lds.size());
+  size_t o_lds_s = b.add(pf.lds_s.data(), pf.lds_s.size());
   size_t o_full = b.add(pf.full.data(), pf.full.size() * 2);
   size_t o_eof = b.add(pf.eof.data(), pf.eof.size());
   size_t o_start = b.add(pf.start.data(), 256);
@@ -271,6 +344,13 @@ DevTables *regex_device(rure *re, std::string *err) {
   t.f.lds_image = base + o_lds;
   t.f.lds_bytes = (uint32_t)pf.lds.size();
   t.f.hot = pf.hot;
+  t.f.lds_image_s = base + o_lds_s;
+  t.f.lds_bytes_s = (uint32_t)pf.lds_s.size();
+  t.f.stride = pf.stride;
+  t.f.hot_s = pf.hot_s;
+  t.f.P = pf.P;
+  t.f.sent = pf.sent;
+  t.f.cus = (uint32_t)device_cus(d);
   t.f.full = (const uint16_t *)(base + o_full);
   t.f.eof = base + o_eof;
   t.f.start = (const uint16_t *)(base + o_start);
@@ -412,7 +492,7 @@ int64_t export_prog(const Program &p, rure_amd_prog_info *info, rure_amd_inst *i
   return (int64_t)p.insts.size();
 }
 
-void fill_info(const DenseDfa &d, const Program &p, uint32_t hot, rure_amd_dfa_info *info) {
+void fill_info(const DenseDfa &d, const Program &p, uint32_t hot, rure_amd_dfa_info *info, const PackedFwd *pf = nullptr) {
   info->ok = 1;
   info->states = d.nstates;
   info->raw_states = d.raw_states;
@@ -423,6 +503,10 @@ void fill_info(const DenseDfa &d, const Program &p, uint32_t hot, rure_amd_dfa_i
   info->hot = (int32_t)hot;
   info->byte_classes = p.num_byte_classes();
   info->insts = (int32_t)p.insts.size();
+  info->fast_stride = pf ? (int32_t)pf->stride : 1;
+  uint32_t k = 1;
+  if (pf && pf->stride > 1) while (true) { uint32_t q = 1; for (uint32_t i = 0; i < pf->stride; ++i) q *= k; if (q >= pf->P) break; ++k; }
+  info->fast_classes = pf && pf->stride > 1 ? (int32_t)k : 0;
 }
 
 }  // namespace
@@ -676,7 +760,7 @@ int rure_amd_dfa_info_get(rure *re, int which, rure_amd_dfa_info *info) {
   if (!re || !info) return RURE_AMD_ERR_ARG;
   memset(info, 0, sizeof(*info));
   if (!build_regex_dfas(re)) { info->ok = 0; return RURE_AMD_ERR_DFA; }
-  if (which == 0) fill_info(re->dfwd, re->fwd, re->pf.hot, info);
+  if (which == 0) fill_info(re->dfwd, re->fwd, re->pf.hot, info, &re->pf);
   else fill_info(re->drev, re->rev, 0, info);
   return RURE_AMD_OK;
 }

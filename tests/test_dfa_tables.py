@@ -57,4 +57,4 @@ def test_matiter_tables(v):
 
 def test_date_dfa_shape():
     info = R.Regex(r"\d{4}-\d{2}-\d{2}").dfa_info(0)
-    assert info["ok"] == 1 and info["states"] <= 256 and info["hot"] == info["normal"]
+    assert info["ok"] == 1 and info["states"] <= 256 and 11 <= info["hot"] <= 63

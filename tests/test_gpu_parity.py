@@ -49,6 +49,32 @@ def test_find_batch_strided(cuda, pat):
         assert gs == es, (pat, i, gs, es)
 
 
+@pytest.mark.parametrize("pat", [r"\d{4}-\d{2}-\d{2}", r"[a-z]{3}\d", r"\w+@\w+\.\w+", r"(?m)^\d+$", "x*"])
+@pytest.mark.parametrize("n,L,stride", [(1000, 4096, 4096), (333, 1000, 1008), (64, 128, 128), (130, 300, 304)])
+def test_find_batch_tiles(cuda, pat, n, L, stride):
+    """Fixed-stride batches that take the coalesced-tile kernel (stride % 16 == 0)."""
+    import torch
+    buf2, _ = date_haystacks_host(n, stride, seed=7, frac=0.2)
+    # plant dates straddling 128-byte tile boundaries
+    for i in range(0, n, 5):
+        o = i * stride + min(L - 10, 123 + (i % 7))
+        buf2[o:o + 10] = np.frombuffer(b"1999-12-31", dtype=np.uint8)
+    re = R.Regex(pat)
+    o = OracleRegex(re)
+    dev = torch.from_numpy(buf2).to(cuda)
+    got = re.find_batch(dev, stride=stride, length=L, count=n).cpu().numpy()
+    ism = re.is_match_batch(dev, stride=stride, length=L, count=n).cpu().numpy()
+    sho = re.shortest_match_batch(dev, stride=stride, length=L, count=n).cpu().numpy()
+    for i in range(n):
+        t = bytes(buf2[i * stride:i * stride + L])
+        exp = o.find(t)
+        g = None if int(got[i, 0]) == -1 else (int(got[i, 0]), int(got[i, 1]))
+        assert g == exp, (pat, i, g, exp)
+        assert bool(ism[i]) == (exp is not None)
+        es = o.shortest_match(t)
+        assert (None if int(sho[i]) == -1 else int(sho[i])) == es
+
+
 def test_find_batch_ragged(cuda):
     import torch
     rng = np.random.default_rng(5)

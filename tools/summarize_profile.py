@@ -1,0 +1,47 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 run of bench.py (tools/gpu_profile.sh) into
+profiles/<tag>_summary.json: kernel-trace average duration of the scan kernel
+and FETCH_SIZE-derived HBM read bytes per launch (x1024 B per KB unit, x2
+gfx950 wide-read correction, MI355X_MICROARCH.md §HBM)."""
+import csv
+import json
+import os
+import sys
+
+
+def main(tag, kernel_substr="dfa_fwd_kernel"):
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = os.path.join(root, "gpurun_out", tag)
+    stats = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
+    ks = [r for r in stats if kernel_substr in r["Name"]]
+    pmc = list(csv.DictReader(open(os.path.join(src, "pmc", "pmc_counter_collection.csv"))))
+    fetch = [float(r["Counter_Value"]) for r in pmc
+             if kernel_substr in r["Kernel_Name"] and r["Counter_Name"] == "FETCH_SIZE"]
+    bench = json.loads(open(os.path.join(src, "bench_trace.json")).read().strip().splitlines()[-1])
+    out = {
+        "tag": tag,
+        "kernel": ks[0]["Name"] if ks else None,
+        "calls": int(ks[0]["Calls"]) if ks else 0,
+        "avg_ns": float(ks[0]["AverageNs"]) if ks else None,
+        "min_ns": float(ks[0]["MinNs"]) if ks else None,
+        "max_ns": float(ks[0]["MaxNs"]) if ks else None,
+        "fetch_size_kb_avg": sum(fetch) / len(fetch) if fetch else None,
+        "hbm_read_bytes_per_launch": (sum(fetch) / len(fetch)) * 1024 * 2 if fetch else None,
+        "bench_kernel_ms_events": bench["roofline"]["kernel_ms"],
+        "alg_bytes_per_launch": bench["roofline"]["alg_bytes_per_launch"],
+        "bench_value_GBps": bench["value"],
+        "note": "FETCH_SIZE (KB) x 1024 x 2: gfx950 reports half of wide streaming reads",
+    }
+    if out["hbm_read_bytes_per_launch"]:
+        out["traffic_over_alg"] = out["hbm_read_bytes_per_launch"] / out["alg_bytes_per_launch"]
+    os.makedirs(os.path.join(root, "profiles"), exist_ok=True)
+    with open(os.path.join(root, "profiles", tag + "_summary.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    # keep the raw kernel stats CSV next to it
+    with open(os.path.join(root, "profiles", tag + "_kernel_stats.csv"), "w") as f:
+        f.write(open(os.path.join(src, "trace", "run_kernel_stats.csv")).read())
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
