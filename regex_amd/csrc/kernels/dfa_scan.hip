@@ -64,6 +64,9 @@ struct LaneState {
 };
 
 static constexpr uint64_t NONE = ~0ull;
+// LDS fast-table row pitch: 256 bytes + one bank, so that lanes in different
+// states that read the same byte value land in different LDS banks.
+static constexpr uint32_t kRow = 260;
 static constexpr uint64_t QUITMARK = ~0ull - 1;
 
 // Full-table step for one byte at haystack position `pos` (careful path).
@@ -88,19 +91,20 @@ template <int MODE>
 __device__ __forceinline__ void step1(LaneState &L, const FwdDfaDev &f, const uint8_t *lds,
                                       uint32_t b, uint64_t pos) {
   if (L.s < f.hot) {
-    uint32_t t = lds[(L.s << 8) | b];
+    uint32_t t = lds[L.s * kRow + b];
     if (t != f.hot) { L.s = t; return; }
   }
   careful_step<MODE>(L, f, b, pos);
 }
 
-// 4 fast-path steps on the bytes of `w` (little endian).  v_perm_b32 builds
-// state<<8 | byte_k in one instruction.
+// 4 fast-path steps on the bytes of `w` (little endian): byte extraction is
+// off the dependency chain; the chain is one v_mad_u32_u24 + one ds_read_u8.
 __device__ __forceinline__ uint32_t fast4(uint32_t s, uint32_t w, const uint8_t *lds) {
-  s = lds[__builtin_amdgcn_perm(s, w, 0x0c0c0400u)];
-  s = lds[__builtin_amdgcn_perm(s, w, 0x0c0c0401u)];
-  s = lds[__builtin_amdgcn_perm(s, w, 0x0c0c0402u)];
-  s = lds[__builtin_amdgcn_perm(s, w, 0x0c0c0403u)];
+  const uint32_t b0 = w & 0xFF, b1 = (w >> 8) & 0xFF, b2 = (w >> 16) & 0xFF, b3 = w >> 24;
+  s = lds[s * kRow + b0];
+  s = lds[s * kRow + b1];
+  s = lds[s * kRow + b2];
+  s = lds[s * kRow + b3];
   return s;
 }
 
@@ -278,7 +282,8 @@ __global__ __launch_bounds__(256) void dfa_fwd_kernel(BatchDev bt, FwdDfaDev f, 
 // swizzled so the ds_read_b128 of 16 lanes hit 16 distinct bank groups), and
 // each lane then steps its own row through the DFA.  The next tile's loads
 // are in flight while the current one is scanned.
-static constexpr int kTileTab = 16384;   // largest LDS fast table of the tile path (hot + 1 <= 64 rows)
+static constexpr int kTileTab = 64 * 260 + 256;   // largest LDS fast table of the tile path (hot + 1 <= 64 rows)
+static constexpr int kTileTabSmall = 16 * 260 + 96; // hot + 1 <= 16 rows
 
 template <int MODE, int TAB, int STRIDE>
 __global__ __launch_bounds__(256) void dfa_fwd_tile_kernel(BatchDev bt, FwdDfaDev f, RevDfaDev r, void *out) {
@@ -384,7 +389,7 @@ __device__ __forceinline__ bool set_careful(uint32_t &s, const SetDfaDev &f, uin
 __device__ __forceinline__ bool set_step1(uint32_t &s, const SetDfaDev &f, const uint8_t *lds, uint32_t b,
                                           bool &quit) {
   if (s < f.hot) {
-    uint32_t t = lds[(s << 8) | b];
+    uint32_t t = lds[s * kRow + b];
     if (t != f.hot) { s = t; return false; }
   }
   return set_careful(s, f, b, quit);
@@ -449,8 +454,8 @@ template <int MODE, int STRIDE>
 static hipError_t launch_tile_s(const BatchDev &b, const FwdDfaDev &f, const RevDfaDev &r, void *out, hipStream_t st,
                                 int grid) {
   const uint32_t bytes = STRIDE == 1 ? f.lds_bytes : f.lds_bytes_s;
-  if (bytes <= 4096)
-    hipLaunchKernelGGL((dfa_fwd_tile_kernel<MODE, 4096, STRIDE>), dim3(grid), dim3(256), 0, st, b, f, r, out);
+  if (bytes <= (uint32_t)kTileTabSmall)
+    hipLaunchKernelGGL((dfa_fwd_tile_kernel<MODE, kTileTabSmall, STRIDE>), dim3(grid), dim3(256), 0, st, b, f, r, out);
   else
     hipLaunchKernelGGL((dfa_fwd_tile_kernel<MODE, kTileTab, STRIDE>), dim3(grid), dim3(256), 0, st, b, f, r, out);
   return hipGetLastError();

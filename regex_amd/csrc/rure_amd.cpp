@@ -148,12 +148,13 @@ bool pack_forward(const DenseDfa &d, PackedFwd *p, std::string *err) {
   int cap = need + 1 <= 16 ? 15 : need + 1 <= 64 ? 63 : 255;
   uint32_t hot = (uint32_t)std::min(d.n_normal, cap);
   p->hot = hot;
-  size_t lds_bytes = ((size_t)(hot + 1) * 256 + 15) & ~(size_t)15;
+  const size_t kRow = 260;  // row pitch of the LDS table (kernels: kRow)
+  size_t lds_bytes = ((size_t)(hot + 1) * kRow + 15) & ~(size_t)15;
   p->lds.assign(lds_bytes, 0);
   for (uint32_t s = 0; s <= hot; ++s)
     for (int b = 0; b < 256; ++b) {
       uint32_t t = (s < hot) ? d.trans[(size_t)s * 256 + b] : hot;
-      p->lds[(size_t)s * 256 + b] = (uint8_t)(t < hot ? t : hot);
+      p->lds[(size_t)s * kRow + b] = (uint8_t)(t < hot ? t : hot);
     }
   build_stride_image(d, p);
   p->full.resize((size_t)d.nstates * 256);
