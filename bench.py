@@ -162,12 +162,44 @@ def main():
                      "kernel_ms": round(kernel_ms, 4), "alg_bytes_per_launch": int(b_alg)},
     }
 
+    tr = profiled_traffic(line["config"], b_alg)
+    if tr is not None:
+        line["roofline"]["traffic"] = tr["bytes"]
+        line["roofline"]["traffic_source"] = tr["source"]
+
     if rank == 0 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(re, hay, res, n, L, args)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def profiled_traffic(config, b_alg):
+    """HBM bytes per launch of the scan kernel from the committed rocprofv3
+    PMC pass of this same command (profiles/<tag>_summary.json, written by
+    tools/gpu_profile.sh + tools/summarize_profile.py: FETCH_SIZE KB x 1024 x 2,
+    MI355X_MICROARCH.md HBM section).  PMC counters cannot be read from inside
+    the timed process, so the newest summary whose workload matches is used."""
+    import glob
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json"))):
+        try:
+            d = json.load(open(p))
+        except (OSError, ValueError):
+            continue
+        strip = lambda c: {k: v for k, v in (c or {}).items() if k != "parallelism"}
+        if strip(d.get("bench_config")) != strip(config) or not d.get("hbm_read_bytes_per_launch"):
+            continue
+        if best is None or os.path.getmtime(p) >= best[0]:
+            best = (os.path.getmtime(p), p, d)
+    if best is None:
+        return None
+    d = best[2]
+    return {"bytes": int(d["hbm_read_bytes_per_launch"]),
+            "source": "%s (rocprofv3 --pmc FETCH_SIZE, kernel %s, %.3fx algorithmic)" %
+                      (os.path.relpath(best[1], ROOT), d["kernel"].split("(")[0].replace("void ", ""),
+                       d["hbm_read_bytes_per_launch"] / b_alg)}
 
 
 def cpu_baseline(re, hay, res, n, L, args):

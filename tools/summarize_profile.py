@@ -9,14 +9,14 @@ import os
 import sys
 
 
-def main(tag, kernel_substr="dfa_fwd_kernel"):
+def main(tag, kernel_substr="rure_amd::dfa_"):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     src = os.path.join(root, "gpurun_out", tag)
     stats = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
-    ks = [r for r in stats if kernel_substr in r["Name"]]
+    ks = sorted([r for r in stats if kernel_substr in r["Name"]], key=lambda r: -float(r["TotalDurationNs"]))
     pmc = list(csv.DictReader(open(os.path.join(src, "pmc", "pmc_counter_collection.csv"))))
     fetch = [float(r["Counter_Value"]) for r in pmc
-             if kernel_substr in r["Kernel_Name"] and r["Counter_Name"] == "FETCH_SIZE"]
+             if ks and r["Kernel_Name"] == ks[0]["Name"] and r["Counter_Name"] == "FETCH_SIZE"]
     bench = json.loads(open(os.path.join(src, "bench_trace.json")).read().strip().splitlines()[-1])
     out = {
         "tag": tag,
@@ -30,6 +30,7 @@ def main(tag, kernel_substr="dfa_fwd_kernel"):
         "bench_kernel_ms_events": bench["roofline"]["kernel_ms"],
         "alg_bytes_per_launch": bench["roofline"]["alg_bytes_per_launch"],
         "bench_value_GBps": bench["value"],
+        "bench_config": bench["config"],
         "note": "FETCH_SIZE (KB) x 1024 x 2: gfx950 reports half of wide streaming reads",
     }
     if out["hbm_read_bytes_per_launch"]:
