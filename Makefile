@@ -3,9 +3,11 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 CXXFLAGS = -O3 -std=c++17 -fPIC -Wall -Wno-unused-function
 LIB = regex_amd/lib/librure_amd.so
-HOST_SRC = regex_amd/csrc/host/syntax.cpp regex_amd/csrc/host/compile.cpp regex_amd/csrc/host/dfa_build.cpp
+HOST_SRC = regex_amd/csrc/host/syntax.cpp regex_amd/csrc/host/compile.cpp regex_amd/csrc/host/dfa_build.cpp \
+           regex_amd/csrc/host/nfa_build.cpp
 RT_SRC = regex_amd/csrc/rure_amd.cpp
-KERNEL_SRC = regex_amd/csrc/kernels/dfa_scan.hip
+KERNEL_SRC = regex_amd/csrc/kernels/dfa_scan.hip regex_amd/csrc/kernels/nfa_scan.hip
+KERNEL_OBJ = $(patsubst regex_amd/csrc/kernels/%.hip,$(OBJDIR)/%.o,$(KERNEL_SRC))
 HDRS = $(wildcard regex_amd/csrc/host/*.hpp regex_amd/csrc/host/*.h regex_amd/csrc/kernels/*.hpp include/*.h)
 OBJDIR = regex_amd/build
 HOST_OBJ = $(patsubst regex_amd/csrc/host/%.cpp,$(OBJDIR)/%.o,$(HOST_SRC))
@@ -23,11 +25,11 @@ $(OBJDIR)/rure_amd.o: $(RT_SRC) $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(CXXFLAGS) -c $< -o $@
 
-$(OBJDIR)/dfa_scan.o: $(KERNEL_SRC) $(HDRS)
+$(OBJDIR)/%.o: regex_amd/csrc/kernels/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(CXXFLAGS) --offload-arch=$(ARCH) -c $< -o $@
 
-$(LIB): $(HOST_OBJ) $(OBJDIR)/rure_amd.o $(OBJDIR)/dfa_scan.o
+$(LIB): $(HOST_OBJ) $(OBJDIR)/rure_amd.o $(KERNEL_OBJ)
 	@mkdir -p regex_amd/lib
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^
 

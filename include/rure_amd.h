@@ -161,6 +161,23 @@ int64_t rure_amd_set_program_export(rure_set *re, int which, rure_amd_prog_info 
 int rure_amd_dfa_export(rure *re, int which, uint32_t *trans, uint8_t *eof_match,
                         uint32_t *start);
 
+/* Export of the Pike VM closure tables the NFA kernel runs (host only):
+ * leaves = 3 u32 per leaf (kind | lo << 8 | hi << 16, closure, slot),
+ * cl_off = closures + 1 u32, entries = 2 u32 per entry (leaf,
+ * cond | (1 + previous same-leaf entry) << 8).  Pass NULL arrays to query
+ * the sizes.  Returns RURE_AMD_OK or an error. */
+typedef struct rure_amd_nfa_info {
+  uint32_t leaves, closures, entries, root, nmatch, anchored, looks, unicode_wb;
+} rure_amd_nfa_info;
+int rure_amd_nfa_export(rure *re, rure_amd_nfa_info *info, uint32_t *leaves, uint32_t *cl_off,
+                        uint32_t *entries);
+int rure_amd_set_nfa_export(rure_set *re, rure_amd_nfa_info *info, uint32_t *leaves, uint32_t *cl_off,
+                            uint32_t *entries);
+/* 1 if batched searches of this regex run the DFA kernels, 0 if only the
+ * Pike VM kernel (automaton too large), negative on error. */
+int rure_amd_uses_dfa(rure *re);
+int rure_amd_set_uses_dfa(rure_set *re);
+
 #ifdef __cplusplus
 }
 #endif

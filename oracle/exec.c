@@ -131,6 +131,17 @@ int orc_find_at(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t le
   return orc_find_nfa(r, c, text, len, start, ms, me);
 }
 
+/* exec.rs:825-837 shortest_nfa: quit_after_match Pike VM, slots[1] */
+int orc_shortest_nfa(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t len, size_t start, size_t *end) {
+  uint8_t m[1] = {0};
+  size_t slots[2] = {SIZE_MAX, SIZE_MAX};
+  if (start > len) return 0;
+  if (!orc_pike_exec(r->nfa, c->pike, m, 1, slots, 2, 1, text, len, start)) return 0;
+  if (slots[1] == SIZE_MAX) return 0;
+  *end = slots[1];
+  return 1;
+}
+
 int orc_shortest_match_at(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t len, size_t start,
                           size_t *end) {
   if (start > len) return 0;
@@ -140,13 +151,7 @@ int orc_shortest_match_at(const orc_regex *r, orc_cache *c, const uint8_t *text,
   if (k == R_MATCH) { *end = e; return 1; }
   if (k == R_NOMATCH) return 0;
   c->st.quits++;
-  /* exec.rs:825-837 shortest_nfa: quit_after_match Pike VM, slots[1] */
-  uint8_t m[1] = {0};
-  size_t slots[2] = {SIZE_MAX, SIZE_MAX};
-  if (!orc_pike_exec(r->nfa, c->pike, m, 1, slots, 2, 1, text, len, start)) return 0;
-  if (slots[1] == SIZE_MAX) return 0;
-  *end = slots[1];
-  return 1;
+  return orc_shortest_nfa(r, c, text, len, start, end);
 }
 
 int orc_is_match_at(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t len, size_t start) {

@@ -57,6 +57,8 @@ int orc_is_match_at(const orc_regex *r, orc_cache *c, const uint8_t *text, size_
 /* Forced Pike VM (the reference's `nfa` test targets). */
 int orc_find_nfa(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t len, size_t start,
                  size_t *ms, size_t *me);
+int orc_shortest_nfa(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t len, size_t start,
+                     size_t *end);
 /* Pike VM captures: slots[2*ncaps] (SIZE_MAX = unset). */
 int orc_captures_nfa(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t len, size_t start,
                      size_t *slots, size_t nslots);

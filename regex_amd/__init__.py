@@ -189,6 +189,14 @@ class Regex(object):
         """Compiled byte program (0 fwd DFA, 1 reverse DFA, 2 NFA): (info, insts)."""
         return _export(N.rure_amd_program_export, self._re, which)
 
+    def uses_dfa(self):
+        """True if batched searches run the DFA kernels (else the Pike VM kernel)."""
+        return N.rure_amd_uses_dfa(self._re) == 1
+
+    def nfa_tables(self):
+        """Pike VM closure tables of the NFA kernel: (info, leaves, cl_off, entries)."""
+        return _nfa_export(N.rure_amd_nfa_export, self._re)
+
     def dfa_tables(self, which=0):
         import numpy as np
         info = self.dfa_info(which)
@@ -201,6 +209,18 @@ class Regex(object):
         _check(N.rure_amd_dfa_export(self._re, which, trans.ctypes.data, eof.ctypes.data, start.ctypes.data),
                "dfa_export")
         return info, trans.reshape(n, 256), eof, start
+
+
+def _nfa_export(fn, handle):
+    import numpy as np
+    info = N.NfaInfo()
+    _check(fn(handle, ctypes.byref(info), None, None, None), "nfa_export")
+    leaves = np.zeros(max(info.leaves, 1) * 3, dtype=np.uint32)
+    cl_off = np.zeros(info.closures + 1, dtype=np.uint32)
+    ent = np.zeros(max(info.entries, 1) * 2, dtype=np.uint32)
+    _check(fn(handle, ctypes.byref(info), leaves.ctypes.data, cl_off.ctypes.data, ent.ctypes.data), "nfa_export")
+    d = {k: getattr(info, k) for k, _ in N.NfaInfo._fields_}
+    return d, leaves[: info.leaves * 3].reshape(-1, 3), cl_off, ent[: info.entries * 2].reshape(-1, 2)
 
 
 def _export(fn, handle, which):
@@ -268,6 +288,12 @@ class RegexSet(object):
 
     def program(self, which):
         return _export(N.rure_amd_set_program_export, self._set, which)
+
+    def uses_dfa(self):
+        return N.rure_amd_set_uses_dfa(self._set) == 1
+
+    def nfa_tables(self):
+        return _nfa_export(N.rure_amd_set_nfa_export, self._set)
 
     def dfa_info(self):
         info = N.DfaInfo()

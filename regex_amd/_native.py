@@ -58,6 +58,11 @@ class Inst(ctypes.Structure):
                 ("hi", ctypes.c_uint8), ("x", ctypes.c_uint32), ("y", ctypes.c_uint32)]
 
 
+class NfaInfo(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint32) for n in (
+        "leaves", "closures", "entries", "root", "nmatch", "anchored", "looks", "unicode_wb")]
+
+
 def _sig(name, res, *args):
     f = getattr(lib, name)
     f.restype = res
@@ -104,6 +109,10 @@ rure_amd_program_export = _sig("rure_amd_program_export", ctypes.c_int64, VP, ct
 rure_amd_set_program_export = _sig("rure_amd_set_program_export", ctypes.c_int64, VP, ctypes.c_int,
                                    ctypes.POINTER(ProgInfo), VP, c_size)
 rure_amd_dfa_export = _sig("rure_amd_dfa_export", ctypes.c_int, VP, ctypes.c_int, VP, VP, VP)
+rure_amd_nfa_export = _sig("rure_amd_nfa_export", ctypes.c_int, VP, ctypes.POINTER(NfaInfo), VP, VP, VP)
+rure_amd_set_nfa_export = _sig("rure_amd_set_nfa_export", ctypes.c_int, VP, ctypes.POINTER(NfaInfo), VP, VP, VP)
+rure_amd_uses_dfa = _sig("rure_amd_uses_dfa", ctypes.c_int, VP)
+rure_amd_set_uses_dfa = _sig("rure_amd_set_uses_dfa", ctypes.c_int, VP)
 
 FLAG_CASEI = 1 << 0
 FLAG_MULTI = 1 << 1

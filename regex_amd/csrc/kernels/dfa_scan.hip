@@ -202,6 +202,7 @@ __device__ __forceinline__ void finish_lane(const LaneState &L, const RevDfaDev 
       }
       if (!dead && r.eof[s]) rs = lo;
       if (rq) { ms = me = QUITMARK; }
+      else if (rs == NONE) { ms = me = NONE; }  // exec.rs:656-660: reverse NoMatch -> no match
       else ms = rs;
     }
   }

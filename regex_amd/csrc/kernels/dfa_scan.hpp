@@ -53,6 +53,27 @@ struct SetDfaDev {
   uint32_t n_normal, n_match_end, dead, quit;
 };
 
+// Pike VM closure tables (host/nfa_build.hpp) on the device.
+struct NfaDev {
+  const uint32_t *leaves;     // 3 words per leaf: kind | lo << 8 | hi << 16, closure, slot
+  const uint32_t *cl_off;     // closure CSR offsets
+  const uint2 *entries;       // (leaf, cond | (1 + prev same-leaf entry) << 8)
+  const uint32_t *perlw;      // Unicode word-character ranges (pairs), regex-syntax PERLW
+  uint32_t perlw_n;
+  uint32_t nleaves, root, nmatch;
+  uint32_t anchored, single, looks, unicode_wb;
+};
+
+// Per-wave working set of the Pike VM: stamp + two thread lists.
+__host__ __device__ inline size_t nfa_wave_bytes(uint32_t nleaves) { return ((size_t)nleaves * 28 + 64 + 255) & ~(size_t)255; }
+constexpr size_t kNfaLdsMax = 160 * 1024;   // a gfx950 workgroup may take the whole LDS
+
+// mode: MODE_FIND / MODE_ISMATCH / MODE_SHORTEST, or MODE_SET.  fallback:
+// only haystacks whose DFA result is the quit marker are (re)computed.
+enum { MODE_SET = 3 };
+hipError_t launch_pike(int mode, bool fallback, const BatchDev &b, const NfaDev &n, void *out, void *scratch,
+                       hipStream_t st, int grid);
+
 hipError_t launch_dfa_fwd(int mode, const BatchDev &b, const FwdDfaDev &f, const RevDfaDev &r, void *out,
                           hipStream_t st, int grid);
 hipError_t launch_dfa_set(const BatchDev &b, const SetDfaDev &f, uint64_t *out, hipStream_t st, int grid);

@@ -20,8 +20,10 @@
 #include <vector>
 
 #include "host/dfa_build.hpp"
+#include "host/nfa_build.hpp"
 #include "host/program.hpp"
 #include "host/syntax.hpp"
+#include "host/unicode_tables.h"
 #include "kernels/dfa_scan.hpp"
 
 using namespace rure_amd;
@@ -55,6 +57,9 @@ struct DevTables {
   FwdDfaDev f{};
   RevDfaDev r{};
   SetDfaDev s{};
+  NfaDev n{};
+  bool has_dfa = false;     // the DFA materialised (else: Pike VM only)
+  bool quit_possible = false;  // the DFA can quit (Unicode \b): Pike VM fallback pass
   int cus = 256;
 };
 
@@ -238,6 +243,8 @@ struct rure {
   std::string dfa_err;
   DenseDfa dfwd, drev;
   PackedFwd pf;
+  NfaTables nt;
+  bool nfa_ok = false;
   std::map<int, DevTables> dev;
   Staging stage;
 };
@@ -254,6 +261,8 @@ struct rure_set {
   std::string dfa_err;
   DenseDfa dfa;
   PackedFwd pf;
+  NfaTables nt;
+  bool nfa_ok = false;
   std::map<int, DevTables> dev;
   Staging stage;
   rure *single = nullptr;   // one-pattern sets compile with compile_one
@@ -280,130 +289,255 @@ SyntaxFlags syntax_flags(uint32_t flags) {  // rure.rs:119-124
   return f;
 }
 
-bool build_regex_dfas(rure *re) {
+// Builds the automata of a regex once: the DFAs (when they materialise
+// within budget) and always the Pike VM closure tables.  Returns whether a
+// search engine is available.
+bool build_regex(rure *re) {
   std::lock_guard<std::mutex> g(re->mu);
-  if (re->built) return re->dfa_ok;
+  if (re->built) return re->dfa_ok || re->nfa_ok;
   re->built = true;
+  std::string nerr;
+  re->nfa_ok = build_nfa_tables(re->nfa, &re->nt, &nerr);
   DfaBuildLimits lim;
   std::string err;
   if (!build_dense_dfa(re->fwd, lim, &re->dfwd, &err) || !build_dense_dfa(re->rev, lim, &re->drev, &err) ||
       !pack_forward(re->dfwd, &re->pf, &err) || re->drev.nstates > 65535) {
     re->dfa_err = err.empty() ? "reverse DFA too large" : err;
     re->dfa_ok = false;
-    return false;
+    if (!re->nfa_ok) re->dfa_err += "; " + nerr;
+    return re->nfa_ok;
   }
   re->dfa_ok = true;
   return true;
 }
 
-bool build_set_dfa(rure_set *rs) {
+bool build_regex_dfas(rure *re) {
+  build_regex(re);
+  return re->dfa_ok;
+}
+
+bool build_set(rure_set *rs) {
   std::lock_guard<std::mutex> g(rs->mu);
-  if (rs->built) return rs->dfa_ok;
+  if (rs->built) return rs->dfa_ok || rs->nfa_ok;
   rs->built = true;
   if (rs->exprs.empty()) { rs->dfa_ok = true; return true; }
+  std::string nerr;
+  rs->nfa_ok = build_nfa_tables(rs->nfa, &rs->nt, &nerr);
   DfaBuildLimits lim;
   std::string err;
   if (!build_dense_dfa(rs->fwd, lim, &rs->dfa, &err) || !pack_forward(rs->dfa, &rs->pf, &err)) {
     rs->dfa_err = err;
     rs->dfa_ok = false;
-    return false;
+    if (!rs->nfa_ok) rs->dfa_err += "; " + nerr;
+    return rs->nfa_ok;
   }
   rs->dfa_ok = true;
   return true;
 }
 
+bool build_set_dfa(rure_set *rs) {
+  build_set(rs);
+  return rs->dfa_ok;
+}
+
+// Appends the Pike VM tables to an upload blob; fix_nfa() then points the
+// descriptor into the device copy.
+struct NfaOffsets { size_t leaves, cl_off, entries, perlw; };
+
+NfaOffsets add_nfa(Blob &b, const NfaTables &nt) {
+  NfaOffsets o;
+  std::vector<uint32_t> lv(nt.leaves.size() * 3);
+  for (size_t i = 0; i < nt.leaves.size(); ++i) {
+    const NfaLeaf &l = nt.leaves[i];
+    lv[3 * i] = (uint32_t)l.kind | ((uint32_t)l.lo << 8) | ((uint32_t)l.hi << 16);
+    lv[3 * i + 1] = l.closure;
+    lv[3 * i + 2] = l.slot;
+  }
+  o.leaves = b.add(lv.data(), lv.size() * 4);
+  o.cl_off = b.add(nt.cl_off.data(), nt.cl_off.size() * 4);
+  o.entries = b.add(nt.entries.data(), nt.entries.size() * 8);
+  namespace U = rure_amd_unicode;
+  o.perlw = b.add(U::kPairs + 2 * U::kPerlW.first, (size_t)U::kPerlW.count * 8);
+  return o;
+}
+
+void fix_nfa(NfaDev *n, uint8_t *base, const NfaOffsets &o, const NfaTables &nt, bool single) {
+  n->leaves = (const uint32_t *)(base + o.leaves);
+  n->cl_off = (const uint32_t *)(base + o.cl_off);
+  n->entries = (const uint2 *)(base + o.entries);
+  n->perlw = (const uint32_t *)(base + o.perlw);
+  n->perlw_n = rure_amd_unicode::kPerlW.count;
+  n->nleaves = (uint32_t)nt.leaves.size();
+  n->root = nt.root;
+  n->nmatch = nt.nmatch;
+  n->anchored = nt.anchored_start ? 1 : 0;
+  n->single = single ? 1 : 0;
+  n->looks = nt.looks_used;
+  n->unicode_wb = nt.unicode_wb ? 1 : 0;
+}
+
+bool upload_blob(const Blob &b, DevTables *t, std::string *err) {
+  if (!hip_ok(hipMalloc(&t->blob, b.bytes.size()), err)) return false;
+  if (!hip_ok(hipMemcpy(t->blob, b.bytes.data(), b.bytes.size(), hipMemcpyHostToDevice), err)) {
+    (void)hipFree(t->blob);
+    t->blob = nullptr;
+    return false;
+  }
+  return true;
+}
+
 // Upload (once per device) and return device descriptors.
 DevTables *regex_device(rure *re, std::string *err) {
-  if (!build_regex_dfas(re)) { if (err) *err = re->dfa_err; return nullptr; }
+  if (!build_regex(re)) { if (err) *err = re->dfa_err; return nullptr; }
   int d = 0;
   if (!hip_ok(hipGetDevice(&d), err)) return nullptr;
   std::lock_guard<std::mutex> g(re->mu);
   auto it = re->dev.find(d);
   if (it != re->dev.end()) return &it->second;
+  Blob b;
+  DevTables t;
+  t.cus = device_cus(d);
+  NfaOffsets no{};
+  if (re->nfa_ok) no = add_nfa(b, re->nt);
+  size_t o_lds = 0, o_lds_s = 0, o_full = 0, o_eof = 0, o_start = 0, o_rfull = 0, o_reof = 0, o_rstart = 0;
   const PackedFwd &pf = re->pf;
   const DenseDfa &rv = re->drev;
-  std::vector<uint16_t> rfull(rv.trans.size()), rstart(128);
-  for (size_t i = 0; i < rv.trans.size(); ++i) rfull[i] = (uint16_t)rv.trans[i];
-  for (int i = 0; i < 128; ++i) rstart[i] = (uint16_t)rv.start[i];
-  Blob b;
-  size_t o_lds = b.add(pf.lds.data(), pf.lds.size());
-  size_t o_lds_s = b.add(pf.lds_s.data(), pf.lds_s.size());
-  size_t o_full = b.add(pf.full.data(), pf.full.size() * 2);
-  size_t o_eof = b.add(pf.eof.data(), pf.eof.size());
-  size_t o_start = b.add(pf.start.data(), 256);
-  size_t o_rfull = b.add(rfull.data(), rfull.size() * 2);
-  size_t o_reof = b.add(rv.eof_match.data(), rv.eof_match.size());
-  size_t o_rstart = b.add(rstart.data(), 256);
-  DevTables t;
-  if (!hip_ok(hipMalloc(&t.blob, b.bytes.size()), err)) return nullptr;
-  if (!hip_ok(hipMemcpy(t.blob, b.bytes.data(), b.bytes.size(), hipMemcpyHostToDevice), err)) {
+  if (re->dfa_ok) {
+    std::vector<uint16_t> rfull(rv.trans.size()), rstart(128);
+    for (size_t i = 0; i < rv.trans.size(); ++i) rfull[i] = (uint16_t)rv.trans[i];
+    for (int i = 0; i < 128; ++i) rstart[i] = (uint16_t)rv.start[i];
+    o_lds = b.add(pf.lds.data(), pf.lds.size());
+    o_lds_s = b.add(pf.lds_s.data(), pf.lds_s.size());
+    o_full = b.add(pf.full.data(), pf.full.size() * 2);
+    o_eof = b.add(pf.eof.data(), pf.eof.size());
+    o_start = b.add(pf.start.data(), 256);
+    o_rfull = b.add(rfull.data(), rfull.size() * 2);
+    o_reof = b.add(rv.eof_match.data(), rv.eof_match.size());
+    o_rstart = b.add(rstart.data(), 256);
+  }
+  if (!upload_blob(b, &t, err)) return nullptr;
+  uint8_t *base = (uint8_t *)t.blob;
+  if (re->nfa_ok) fix_nfa(&t.n, base, no, re->nt, true);
+  if (re->dfa_ok) {
+    const DenseDfa &fw = re->dfwd;
+    t.has_dfa = true;
+    t.quit_possible = fw.quit >= 0 || rv.quit >= 0;
+    t.f.lds_image = base + o_lds;
+    t.f.lds_bytes = (uint32_t)pf.lds.size();
+    t.f.hot = pf.hot;
+    t.f.lds_image_s = base + o_lds_s;
+    t.f.lds_bytes_s = (uint32_t)pf.lds_s.size();
+    t.f.stride = pf.stride;
+    t.f.hot_s = pf.hot_s;
+    t.f.P = pf.P;
+    t.f.sent = pf.sent;
+    t.f.cus = (uint32_t)t.cus;
+    t.f.full = (const uint16_t *)(base + o_full);
+    t.f.eof = base + o_eof;
+    t.f.start = (const uint16_t *)(base + o_start);
+    t.f.n_normal = fw.n_normal;
+    t.f.n_match_end = fw.n_match_end;
+    t.f.dead = fw.dead;
+    t.f.quit = fw.quit < 0 ? 0xFFFFFFFFu : (uint32_t)fw.quit;
+    t.r.full = (const uint16_t *)(base + o_rfull);
+    t.r.eof = base + o_reof;
+    t.r.start = (const uint16_t *)(base + o_rstart);
+    t.r.n_normal = rv.n_normal;
+    t.r.n_match_end = rv.n_match_end;
+    t.r.dead = rv.dead;
+    t.r.quit = rv.quit < 0 ? 0xFFFFFFFFu : (uint32_t)rv.quit;
+  }
+  if (t.quit_possible && !re->nfa_ok) {
     (void)hipFree(t.blob);
+    if (err) *err = "the DFA can quit and the NFA tables could not be built";
     return nullptr;
   }
-  uint8_t *base = (uint8_t *)t.blob;
-  const DenseDfa &fw = re->dfwd;
-  t.f.lds_image = base + o_lds;
-  t.f.lds_bytes = (uint32_t)pf.lds.size();
-  t.f.hot = pf.hot;
-  t.f.lds_image_s = base + o_lds_s;
-  t.f.lds_bytes_s = (uint32_t)pf.lds_s.size();
-  t.f.stride = pf.stride;
-  t.f.hot_s = pf.hot_s;
-  t.f.P = pf.P;
-  t.f.sent = pf.sent;
-  t.f.cus = (uint32_t)device_cus(d);
-  t.f.full = (const uint16_t *)(base + o_full);
-  t.f.eof = base + o_eof;
-  t.f.start = (const uint16_t *)(base + o_start);
-  t.f.n_normal = fw.n_normal;
-  t.f.n_match_end = fw.n_match_end;
-  t.f.dead = fw.dead;
-  t.f.quit = fw.quit < 0 ? 0xFFFFFFFFu : (uint32_t)fw.quit;
-  t.r.full = (const uint16_t *)(base + o_rfull);
-  t.r.eof = base + o_reof;
-  t.r.start = (const uint16_t *)(base + o_rstart);
-  t.r.n_normal = rv.n_normal;
-  t.r.n_match_end = rv.n_match_end;
-  t.r.dead = rv.dead;
-  t.r.quit = rv.quit < 0 ? 0xFFFFFFFFu : (uint32_t)rv.quit;
-  t.cus = device_cus(d);
   return &(re->dev[d] = t);
 }
 
 DevTables *set_device(rure_set *rs, std::string *err) {
-  if (!build_set_dfa(rs)) { if (err) *err = rs->dfa_err; return nullptr; }
+  if (!build_set(rs)) { if (err) *err = rs->dfa_err; return nullptr; }
   int d = 0;
   if (!hip_ok(hipGetDevice(&d), err)) return nullptr;
   std::lock_guard<std::mutex> g(rs->mu);
   auto it = rs->dev.find(d);
   if (it != rs->dev.end()) return &it->second;
   const PackedFwd &pf = rs->pf;
-  const std::vector<uint64_t> &mask = pf.eof_mask;
   Blob b;
-  size_t o_lds = b.add(pf.lds.data(), pf.lds.size());
-  size_t o_full = b.add(pf.full.data(), pf.full.size() * 2);
-  size_t o_mask = b.add(mask.data(), mask.size() * 8);
-  size_t o_start = b.add(pf.start.data(), 256);
   DevTables t;
-  if (!hip_ok(hipMalloc(&t.blob, b.bytes.size()), err)) return nullptr;
-  if (!hip_ok(hipMemcpy(t.blob, b.bytes.data(), b.bytes.size(), hipMemcpyHostToDevice), err)) {
+  t.cus = device_cus(d);
+  NfaOffsets no{};
+  if (rs->nfa_ok) no = add_nfa(b, rs->nt);
+  size_t o_lds = 0, o_full = 0, o_mask = 0, o_start = 0;
+  if (rs->dfa_ok) {
+    o_lds = b.add(pf.lds.data(), pf.lds.size());
+    o_full = b.add(pf.full.data(), pf.full.size() * 2);
+    o_mask = b.add(pf.eof_mask.data(), pf.eof_mask.size() * 8);
+    o_start = b.add(pf.start.data(), 256);
+  }
+  if (!upload_blob(b, &t, err)) return nullptr;
+  uint8_t *base = (uint8_t *)t.blob;
+  // set programs: several Match instructions, no leftmost-first cut (pikevm.rs:196-212)
+  if (rs->nfa_ok) fix_nfa(&t.n, base, no, rs->nt, rs->nt.nmatch <= 1);
+  if (rs->dfa_ok) {
+    const DenseDfa &fw = rs->dfa;
+    t.has_dfa = true;
+    t.quit_possible = fw.quit >= 0;
+    t.s.lds_image = base + o_lds;
+    t.s.lds_bytes = (uint32_t)pf.lds.size();
+    t.s.hot = pf.hot;
+    t.s.full = (const uint16_t *)(base + o_full);
+    t.s.eof_mask = (const uint64_t *)(base + o_mask);
+    t.s.start = (const uint16_t *)(base + o_start);
+    t.s.n_normal = fw.n_normal;
+    t.s.n_match_end = fw.n_match_end;
+    t.s.dead = fw.dead;
+    t.s.quit = fw.quit < 0 ? 0xFFFFFFFFu : (uint32_t)fw.quit;
+  }
+  if (t.quit_possible && !rs->nfa_ok) {
     (void)hipFree(t.blob);
+    if (err) *err = "the DFA can quit and the NFA tables could not be built";
     return nullptr;
   }
-  uint8_t *base = (uint8_t *)t.blob;
-  const DenseDfa &fw = rs->dfa;
-  t.s.lds_image = base + o_lds;
-  t.s.lds_bytes = (uint32_t)pf.lds.size();
-  t.s.hot = pf.hot;
-  t.s.full = (const uint16_t *)(base + o_full);
-  t.s.eof_mask = (const uint64_t *)(base + o_mask);
-  t.s.start = (const uint16_t *)(base + o_start);
-  t.s.n_normal = fw.n_normal;
-  t.s.n_match_end = fw.n_match_end;
-  t.s.dead = fw.dead;
-  t.s.quit = fw.quit < 0 ? 0xFFFFFFFFu : (uint32_t)fw.quit;
-  t.cus = device_cus(d);
   return &(rs->dev[d] = t);
+}
+
+int pike_grid(size_t count, bool fallback, const NfaDev &n, int cus) {
+  size_t units = fallback ? (count + 63) / 64 : count;
+  size_t wb = nfa_wave_bytes(n.nleaves);
+  size_t per_cu = wb <= kNfaLdsMax ? std::max<size_t>(1, std::min<size_t>(32, (160u * 1024u) / wb)) : 4;
+  size_t g = std::min(units, (size_t)cus * per_cu);
+  return (int)std::max<size_t>(g, 1);
+}
+
+// Pike VM pass: all haystacks (no DFA) or only those the DFA quit on.
+hipError_t run_pike(int mode, bool fallback, const BatchDev &b, const DevTables &t, void *out, hipStream_t st) {
+  int grid = pike_grid(b.count, fallback, t.n, t.cus);
+  size_t wb = nfa_wave_bytes(t.n.nleaves);
+  if (wb <= kNfaLdsMax) return launch_pike(mode, fallback, b, t.n, out, nullptr, st, grid);
+  void *scratch = nullptr;
+  hipError_t e = hipMallocAsync(&scratch, wb * (size_t)grid, st);
+  if (e != hipSuccess) return e;
+  e = launch_pike(mode, fallback, b, t.n, out, scratch, st, grid);
+  hipError_t e2 = hipFreeAsync(scratch, st);
+  return e != hipSuccess ? e : e2;
+}
+
+// The engine dispatch of exec.rs:473-514 / 382-420 for a batch: DFA, and the
+// Pike VM where the DFA quits (or instead of it when it does not fit).
+hipError_t run_regex(int mode, const BatchDev &b, const DevTables &t, void *out, hipStream_t st, int dfa_grid) {
+  if (!t.has_dfa) return run_pike(mode, false, b, t, out, st);
+  hipError_t e = launch_dfa_fwd(mode, b, t.f, t.r, out, st, dfa_grid);
+  if (e != hipSuccess || !t.quit_possible) return e;
+  return run_pike(mode, true, b, t, out, st);
+}
+
+// exec.rs:998-1038 many_matches_at for a batch.
+hipError_t run_set(const BatchDev &b, const DevTables &t, uint64_t *out, hipStream_t st, int dfa_grid) {
+  if (!t.has_dfa) return run_pike(MODE_SET, false, b, t, out, st);
+  hipError_t e = launch_dfa_set(b, t.s, out, st, dfa_grid);
+  if (e != hipSuccess || !t.quit_possible) return e;
+  return run_pike(MODE_SET, true, b, t, out, st);
 }
 
 bool to_batch(const rure_amd_batch *b, BatchDev *o) {
@@ -432,18 +566,17 @@ bool single_call(rure *re, int mode, const uint8_t *hay, size_t len, size_t star
   hipStream_t st = re->stage.stream;
   if (len && !hip_ok(hipMemcpyAsync(re->stage.hay, hay, len, hipMemcpyHostToDevice, st), &err)) die(err);
   BatchDev b{re->stage.hay, nullptr, 0, len, 1, start};
-  if (!hip_ok(launch_dfa_fwd(mode, b, t->f, t->r, re->stage.res, st, 1), &err)) die(err);
+  if (!hip_ok(run_regex(mode, b, *t, re->stage.res, st, 1), &err)) die(err);
   uint64_t out[2] = {~0ull, ~0ull};
   size_t nbytes = mode == MODE_FIND ? 16 : mode == MODE_SHORTEST ? 8 : 1;
   if (!hip_ok(hipMemcpyAsync(out, re->stage.res, nbytes, hipMemcpyDeviceToHost, st), &err)) die(err);
   if (!hip_ok(hipStreamSynchronize(st), &err)) die(err);
   if (mode == MODE_ISMATCH) {
     uint8_t v = (uint8_t)(out[0] & 0xFF);
-    if (v == 2) die("Unicode word boundary on non-ASCII input needs the NFA kernel (not available)");
+    if (v > 1) die("internal error: unresolved DFA quit");
     return v == 1;
   }
-  if (out[0] == kQuit || (mode == MODE_FIND && out[1] == kQuit))
-    die("Unicode word boundary on non-ASCII input needs the NFA kernel (not available)");
+  if (out[0] == kQuit || (mode == MODE_FIND && out[1] == kQuit)) die("internal error: unresolved DFA quit");
   if (out[0] == ~0ull) return false;
   *r0 = out[0];
   if (r1) *r1 = out[1];
@@ -461,11 +594,11 @@ uint64_t set_single_call(rure_set *rs, const uint8_t *hay, size_t len, size_t st
   hipStream_t st = rs->stage.stream;
   if (len && !hip_ok(hipMemcpyAsync(rs->stage.hay, hay, len, hipMemcpyHostToDevice, st), &err)) die(err);
   BatchDev b{rs->stage.hay, nullptr, 0, len, 1, start};
-  if (!hip_ok(launch_dfa_set(b, t->s, rs->stage.res, st, 1), &err)) die(err);
+  if (!hip_ok(run_set(b, *t, rs->stage.res, st, 1), &err)) die(err);
   uint64_t out = 0;
   if (!hip_ok(hipMemcpyAsync(&out, rs->stage.res, 8, hipMemcpyDeviceToHost, st), &err)) die(err);
   if (!hip_ok(hipStreamSynchronize(st), &err)) die(err);
-  if (out == kQuit) die("Unicode word boundary on non-ASCII input needs the NFA kernel (not available)");
+  if (out == kQuit) die("internal error: unresolved DFA quit");
   return out;
 }
 
@@ -715,7 +848,7 @@ int rure_amd_find_batch(rure *re, const rure_amd_batch *batch, rure_match *out, 
   DevTables *t = regex_device(re, &err);
   if (!t) return err.rfind("HIP", 0) == 0 ? RURE_AMD_ERR_HIP : RURE_AMD_ERR_DFA;
   int grid = grid_for(b.count, t->f.lds_bytes, t->cus);
-  if (launch_dfa_fwd(MODE_FIND, b, t->f, t->r, out, (hipStream_t)stream, grid) != hipSuccess) return RURE_AMD_ERR_HIP;
+  if (run_regex(MODE_FIND, b, *t, out, (hipStream_t)stream, grid) != hipSuccess) return RURE_AMD_ERR_HIP;
   return RURE_AMD_OK;
 }
 
@@ -727,7 +860,7 @@ int rure_amd_is_match_batch(rure *re, const rure_amd_batch *batch, uint8_t *out,
   DevTables *t = regex_device(re, &err);
   if (!t) return err.rfind("HIP", 0) == 0 ? RURE_AMD_ERR_HIP : RURE_AMD_ERR_DFA;
   int grid = grid_for(b.count, t->f.lds_bytes, t->cus);
-  if (launch_dfa_fwd(MODE_ISMATCH, b, t->f, t->r, out, (hipStream_t)stream, grid) != hipSuccess) return RURE_AMD_ERR_HIP;
+  if (run_regex(MODE_ISMATCH, b, *t, out, (hipStream_t)stream, grid) != hipSuccess) return RURE_AMD_ERR_HIP;
   return RURE_AMD_OK;
 }
 
@@ -739,7 +872,7 @@ int rure_amd_shortest_match_batch(rure *re, const rure_amd_batch *batch, size_t 
   DevTables *t = regex_device(re, &err);
   if (!t) return err.rfind("HIP", 0) == 0 ? RURE_AMD_ERR_HIP : RURE_AMD_ERR_DFA;
   int grid = grid_for(b.count, t->f.lds_bytes, t->cus);
-  if (launch_dfa_fwd(MODE_SHORTEST, b, t->f, t->r, end, (hipStream_t)stream, grid) != hipSuccess) return RURE_AMD_ERR_HIP;
+  if (run_regex(MODE_SHORTEST, b, *t, end, (hipStream_t)stream, grid) != hipSuccess) return RURE_AMD_ERR_HIP;
   return RURE_AMD_OK;
 }
 
@@ -752,7 +885,7 @@ int rure_amd_set_matches_batch(rure_set *rs, const rure_amd_batch *batch, uint64
   DevTables *t = set_device(rs, &err);
   if (!t) return err.rfind("HIP", 0) == 0 ? RURE_AMD_ERR_HIP : RURE_AMD_ERR_DFA;
   int grid = grid_for(b.count, t->s.lds_bytes, t->cus);
-  if (launch_dfa_set(b, t->s, mask, (hipStream_t)stream, grid) != hipSuccess) return RURE_AMD_ERR_HIP;
+  if (run_set(b, *t, mask, (hipStream_t)stream, grid) != hipSuccess) return RURE_AMD_ERR_HIP;
   return RURE_AMD_OK;
 }
 
@@ -798,6 +931,60 @@ int rure_amd_dfa_export(rure *re, int which, uint32_t *trans, uint8_t *eof_match
   if (eof_match) memcpy(eof_match, d.eof_match.data(), d.eof_match.size());
   if (start) memcpy(start, d.start, sizeof(d.start));
   return RURE_AMD_OK;
+}
+
+static int export_nfa(const NfaTables &nt, rure_amd_nfa_info *info, uint32_t *leaves, uint32_t *cl_off,
+                      uint32_t *entries) {
+  if (info) {
+    info->leaves = (uint32_t)nt.leaves.size();
+    info->closures = (uint32_t)nt.cl_off.size() - 1;
+    info->entries = (uint32_t)nt.entries.size();
+    info->root = nt.root;
+    info->nmatch = nt.nmatch;
+    info->anchored = nt.anchored_start;
+    info->looks = nt.looks_used;
+    info->unicode_wb = nt.unicode_wb;
+  }
+  if (leaves)
+    for (size_t i = 0; i < nt.leaves.size(); ++i) {
+      const NfaLeaf &l = nt.leaves[i];
+      leaves[3 * i] = (uint32_t)l.kind | ((uint32_t)l.lo << 8) | ((uint32_t)l.hi << 16);
+      leaves[3 * i + 1] = l.closure;
+      leaves[3 * i + 2] = l.slot;
+    }
+  if (cl_off) memcpy(cl_off, nt.cl_off.data(), nt.cl_off.size() * 4);
+  if (entries) memcpy(entries, nt.entries.data(), nt.entries.size() * 8);
+  return RURE_AMD_OK;
+}
+
+int rure_amd_nfa_export(rure *re, rure_amd_nfa_info *info, uint32_t *leaves, uint32_t *cl_off, uint32_t *entries) {
+  if (!re) return RURE_AMD_ERR_ARG;
+  build_regex(re);
+  if (!re->nfa_ok) return RURE_AMD_ERR_DFA;
+  return export_nfa(re->nt, info, leaves, cl_off, entries);
+}
+
+int rure_amd_set_nfa_export(rure_set *rs, rure_amd_nfa_info *info, uint32_t *leaves, uint32_t *cl_off,
+                            uint32_t *entries) {
+  if (!rs) return RURE_AMD_ERR_ARG;
+  if (rs->single) return rure_amd_nfa_export(rs->single, info, leaves, cl_off, entries);
+  if (rs->exprs.empty()) return RURE_AMD_ERR_ARG;
+  build_set(rs);
+  if (!rs->nfa_ok) return RURE_AMD_ERR_DFA;
+  return export_nfa(rs->nt, info, leaves, cl_off, entries);
+}
+
+int rure_amd_uses_dfa(rure *re) {
+  if (!re) return RURE_AMD_ERR_ARG;
+  if (!build_regex(re)) return RURE_AMD_ERR_DFA;
+  return re->dfa_ok ? 1 : 0;
+}
+
+int rure_amd_set_uses_dfa(rure_set *rs) {
+  if (!rs) return RURE_AMD_ERR_ARG;
+  if (rs->single) return rure_amd_uses_dfa(rs->single);
+  if (!build_set(rs)) return RURE_AMD_ERR_DFA;
+  return rs->dfa_ok ? 1 : 0;
 }
 
 }  // extern "C"

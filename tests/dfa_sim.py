@@ -79,4 +79,6 @@ def find(fwd, rev, t, start=0, mode="find"):
                 raise QuitError()
     if not dead and reof[s]:
         rs = start
+    if rs is None:  # exec.rs:656-660: the reverse DFA over text[start..] found no start -> NoMatch
+        return None
     return (rs, last)

@@ -36,6 +36,7 @@ orc_cache_new = _sig("orc_cache_new", VP, VP)
 orc_cache_free = _sig("orc_cache_free", None, VP)
 orc_find_at = _sig("orc_find_at", ctypes.c_int, VP, VP, ctypes.c_char_p, SZ, SZ, ctypes.POINTER(SZ),
                    ctypes.POINTER(SZ))
+orc_shortest_nfa = _sig("orc_shortest_nfa", ctypes.c_int, VP, VP, ctypes.c_char_p, SZ, SZ, ctypes.POINTER(SZ))
 orc_find_nfa = _sig("orc_find_nfa", ctypes.c_int, VP, VP, ctypes.c_char_p, SZ, SZ, ctypes.POINTER(SZ),
                     ctypes.POINTER(SZ))
 orc_shortest_match_at = _sig("orc_shortest_match_at", ctypes.c_int, VP, VP, ctypes.c_char_p, SZ, SZ,
@@ -98,6 +99,12 @@ class OracleRegex(object):
         s, e = SZ(), SZ()
         if orc_find_nfa(self._r, self._c, text, len(text), start, ctypes.byref(s), ctypes.byref(e)):
             return (s.value, e.value)
+        return None
+
+    def shortest_nfa(self, text, start=0):
+        e = SZ()
+        if orc_shortest_nfa(self._r, self._c, text, len(text), start, ctypes.byref(e)):
+            return e.value
         return None
 
     def shortest_match(self, text, start=0):

@@ -10,17 +10,10 @@ pytestmark = pytest.mark.gpu
 V = vectors()
 
 
-def needs_nfa(re, text):
-    info = re.dfa_info(0)
-    return info["quit"] >= 0 and any(b >= 0x80 for b in text)
-
-
 @pytest.mark.parametrize("v", V["mat"], ids=[x["name"] for x in V["mat"]])
 def test_mat_gpu(cuda, v):
     re = R.Regex(v["re"])
     t = bytes.fromhex(v["text"])
-    if needs_nfa(re, t):
-        pytest.skip("Unicode word boundary on non-ASCII text: NFA path")
     exp = tuple(v["groups"][0]) if v["groups"][0] else None
     assert re.find(t) == exp
     assert re.is_match(t) == (exp is not None)
@@ -31,8 +24,6 @@ def test_mat_gpu(cuda, v):
 def test_matiter_gpu(cuda, v):
     re = R.Regex(v["re"])
     t = bytes.fromhex(v["text"])
-    if needs_nfa(re, t):
-        pytest.skip("Unicode word boundary on non-ASCII text: NFA path")
     assert re.find_iter(t) == [tuple(m) for m in v["matches"]]
 
 
@@ -40,8 +31,6 @@ def test_matiter_gpu(cuda, v):
 def test_matset_gpu(cuda, v):
     s = R.RegexSet(v["res"])
     t = bytes.fromhex(v["text"])
-    if len(v["res"]) > 1 and s.dfa_info()["quit"] >= 0 and any(b >= 0x80 for b in t):
-        pytest.skip("Unicode word boundary on non-ASCII text: NFA path")
     assert s.matches(t) == v["matches"]
     assert s.is_match(t) == bool(v["matches"])
 
