@@ -119,6 +119,16 @@ int rure_amd_shortest_match_batch(rure *re, const rure_amd_batch *batch, size_t 
 int rure_amd_set_matches_batch(rure_set *re, const rure_amd_batch *batch, uint64_t *mask,
                                void *stream);
 
+/* Batched find_iter (bytes::Regex::find_iter, re_trait.rs:197-221): every
+ * successive non-overlapping leftmost-first match of every haystack.
+ * counts[i] (device) = number of matches in haystack i; `matches` (device)
+ * receives them concatenated in haystack order, at most `capacity` records;
+ * *total (device) = the number of matches (rerun with a larger buffer if it
+ * exceeds `capacity`).  Long fixed-stride haystacks are scanned in parallel
+ * chunks with exact boundary repair. */
+int rure_amd_find_iter_batch(rure *re, const rure_amd_batch *batch, uint64_t *counts, rure_match *matches,
+                             size_t capacity, uint64_t *total, void *stream);
+
 /* Diagnostics (host only, no GPU needed). */
 typedef struct rure_amd_dfa_info {
   int32_t ok;            /* 1 if the automaton was materialized */
@@ -134,7 +144,7 @@ typedef struct rure_amd_dfa_info {
   int32_t fast_stride;   /* bytes per dependent LDS lookup in the tile kernel (1, 2, 4) */
   int32_t fast_classes;  /* local byte classes of the multi-byte table (K) */
 } rure_amd_dfa_info;
-/* which: 0 = forward DFA program, 1 = reverse DFA program. */
+/* which: 0 = forward DFA, 1 = reverse DFA, 2 = find_iter forward DFA. */
 int rure_amd_dfa_info_get(rure *re, int which, rure_amd_dfa_info *info);
 int rure_amd_set_dfa_info_get(rure_set *re, rure_amd_dfa_info *info);
 
@@ -157,9 +167,12 @@ int64_t rure_amd_program_export(rure *re, int which, rure_amd_prog_info *info,
 int64_t rure_amd_set_program_export(rure_set *re, int which, rure_amd_prog_info *info,
                                     rure_amd_inst *insts, size_t cap);
 /* Export of a materialized DFA: trans = states*256 u32, eof_match = states
- * bytes, start = 128 u32. */
+ * bytes, start = 128 u32.  which: 0 forward, 1 reverse, 2 the forward DFA
+ * of the chunked find_iter (with stripped states, see _strip_export). */
 int rure_amd_dfa_export(rure *re, int which, uint32_t *trans, uint8_t *eof_match,
                         uint32_t *start);
+/* strip[s] (states u32) of the find_iter forward DFA: s without the `.*?` prefix. */
+int rure_amd_dfa_strip_export(rure *re, uint32_t *strip);
 
 /* Export of the Pike VM closure tables the NFA kernel runs (host only):
  * leaves = 3 u32 per leaf (kind | lo << 8 | hi << 16, closure, slot),

@@ -115,7 +115,7 @@ class Regex(object):
 
     def __del__(self):
         re_ = getattr(self, "_re", None)
-        if re_:
+        if re_ and N is not None and getattr(N, "rure_free", None):
             N.rure_free(re_)
             self._re = None
 
@@ -179,6 +179,30 @@ class Regex(object):
                                                _stream_ptr(stream)), "shortest_match_batch")
         return out
 
+    def find_iter_batch(self, haystack, offsets=None, stride=None, length=None, count=None, start=0,
+                        capacity=None, stream=None):
+        """All successive non-overlapping matches of every haystack
+        (bytes::Regex::find_iter, re_trait.rs:197-221).  Returns (counts, matches):
+        counts = (n,) int64 per haystack, matches = (total, 2) int64 (start, end)
+        concatenated in haystack order."""
+        import torch
+        b = _batch(haystack, offsets, stride, length, count, start)
+        dev = haystack.device
+        counts = torch.empty((b.count,), dtype=torch.int64, device=dev)
+        total = torch.zeros((1,), dtype=torch.int64, device=dev)
+        cap = capacity if capacity is not None else max(1024, b.count * 4)
+        while True:
+            out = torch.empty((max(cap, 1), 2), dtype=torch.int64, device=dev)
+            _check(N.rure_amd_find_iter_batch(self._re, ctypes.byref(b), ctypes.c_void_p(counts.data_ptr()),
+                                              ctypes.c_void_p(out.data_ptr()), cap,
+                                              ctypes.c_void_p(total.data_ptr()), _stream_ptr(stream)),
+                   "find_iter_batch")
+            (stream or torch.cuda.current_stream()).synchronize()
+            t = int(total.item())
+            if t <= cap or capacity is not None:
+                return counts, out[: min(t, cap)]
+            cap = t
+
     # ----------------------------------------------------------- diagnostics
     def dfa_info(self, which=0):
         info = N.DfaInfo()
@@ -208,6 +232,10 @@ class Regex(object):
         start = np.zeros(128, dtype=np.uint32)
         _check(N.rure_amd_dfa_export(self._re, which, trans.ctypes.data, eof.ctypes.data, start.ctypes.data),
                "dfa_export")
+        if which == 2:
+            strip = np.zeros(n, dtype=np.uint32)
+            _check(N.rure_amd_dfa_strip_export(self._re, strip.ctypes.data), "dfa_strip_export")
+            info["strip"] = strip
         return info, trans.reshape(n, 256), eof, start
 
 
@@ -259,7 +287,7 @@ class RegexSet(object):
 
     def __del__(self):
         s = getattr(self, "_set", None)
-        if s:
+        if s and N is not None and getattr(N, "rure_set_free", None):
             N.rure_set_free(s)
             self._set = None
 

@@ -200,7 +200,7 @@ class Compiler {
     Patch dot{{}, 0};
     prog_.anchored_start = e.is_anchored_start();
     prog_.anchored_end = e.is_anchored_end();
-    if (needs_dotstar()) { dot = c_dotstar(); prog_.start = dot.entry; }
+    if (needs_dotstar()) { dot = c_dotstar(); prog_.start = dot.entry; prog_.dotstar_end = (uint32_t)len(); }
     prog_.capture_names = {""};
     prog_.capture_has_name = {false};
     Patch p = c_capture(0, e);
@@ -218,7 +218,7 @@ class Compiler {
     prog_.anchored_start = as;
     prog_.anchored_end = ae;
     Patch dot{{}, 0};
-    if (needs_dotstar()) { dot = c_dotstar(); prog_.start = dot.entry; }
+    if (needs_dotstar()) { dot = c_dotstar(); prog_.start = dot.entry; prog_.dotstar_end = (uint32_t)len(); }
     else prog_.start = 0;
     fill_to_next(dot.hole);
     Hole prev;

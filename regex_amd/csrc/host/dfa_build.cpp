@@ -31,6 +31,7 @@ class Builder {
   Builder(const Program &p, const DfaBuildLimits &lim)
       : p_(p), lim_(lim), qa_(p.insts.size() + 1), qb_(p.insts.size() + 1) {
     is_set_ = p.matches.size() > 1;
+    strip_ = lim.strip && p.dotstar_end > 0;
     cont_ = p.is_reverse || is_set_;  // dfa.rs:1557-1559
     word_matters_ = false;
     for (const Inst &i : p.insts)
@@ -62,6 +63,7 @@ class Builder {
         return false;
       }
       std::string key = keys_[s];  // copy: keys_ may grow
+      if (strip_) strip_raw_.push_back(strip_key(key));
       trans_cls_.resize((s + 1) * ncls);
       for (int c = 0; c < ncls; ++c) trans_cls_[s * ncls + c] = step(key, rep[c]);
       uint64_t mask = 0;
@@ -87,7 +89,8 @@ class Builder {
   DfaBuildLimits lim_;
   SparseSet qa_, qb_;
   std::vector<uint32_t> stack_;
-  bool is_set_, cont_, word_matters_, quit_;
+  bool is_set_, cont_, word_matters_, quit_, strip_ = false;
+  std::vector<uint32_t> strip_raw_;  // raw state (from 2) -> stripped raw state
   std::vector<std::string> keys_;
   std::unordered_map<std::string, uint32_t> ids_;
   std::vector<uint32_t> trans_cls_;
@@ -151,6 +154,25 @@ class Builder {
     keys_.push_back(std::move(key));
     return id;
   }
+
+  // The same ordered thread set without the `.*?` prefix instructions.
+  uint32_t strip_key(const std::string &key) {
+    std::string k(1, key[0]);
+    for (size_t i = 1; i + 4 <= key.size(); i += 4) {
+      uint32_t ip;
+      memcpy(&ip, key.data() + i, 4);
+      if (ip >= p_.dotstar_end) k.append(key, i, 4);
+    }
+    if (k.size() == 1 && !(k[0] & SF_MATCH)) return 0;
+    auto it = ids_.find(k);
+    if (it != ids_.end()) return it->second;
+    uint32_t id = (uint32_t)keys_.size();
+    ids_.emplace(k, id);
+    keys_.push_back(std::move(k));
+    return id;
+  }
+
+  uint32_t strip_of(int s) const { return s < 2 ? (uint32_t)s : strip_raw_[s - 2]; }
 
   void load(const std::string &key, SparseSet &q) {
     q.clear();
@@ -302,6 +324,7 @@ class Builder {
       for (int s = 0; s < n; ++s) {
         std::string sig((const char *)&block[s], 4);
         for (int b : colrep) sig.append((const char *)&block[t[(size_t)s * 256 + b]], 4);
+        if (strip_) sig.append((const char *)&block[strip_of(s)], 4);
         auto it = m.emplace(sig, (uint32_t)m.size()).first;
         nb[s] = it->second;
       }
@@ -387,6 +410,11 @@ class Builder {
       out->eof_mask[id] = eof_mask_[s];
     }
     for (int i = 0; i < 128; ++i) out->start[i] = (uint32_t)(start_used_[i] ? newid[block[start_raw_[i]]] : out->dead);
+    out->strip.clear();
+    if (strip_) {
+      out->strip.assign(next, 0);
+      for (uint32_t b = 0; b < nblocks; ++b) out->strip[newid[b]] = newid[block[strip_of(rep[b])]];
+    }
   }
 };
 

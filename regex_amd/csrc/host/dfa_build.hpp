@@ -36,10 +36,15 @@ struct DenseDfa {
   uint32_t start[128];             // start state per 7-bit start-flag index (dfa.rs:1381-1390)
   int raw_states = 0;              // states before minimisation (diagnostics)
   int n_ascii = 0;                 // normal states reachable through ASCII bytes (numbered first)
+  // With DfaBuildLimits::strip: strip[s] = the state holding the same threads
+  // as s minus the `.*?` prefix, i.e. no new match may start from here on
+  // (used to end a search once it crosses a chunk cut).
+  std::vector<uint32_t> strip;
 };
 
 struct DfaBuildLimits {
   int max_raw_states = 1 << 16;
+  bool strip = false;
 };
 
 // Builds the DFA for `prog` (a forward DFA program with `.*?` unless anchored,

@@ -33,6 +33,7 @@ struct Program {
   std::vector<Inst> insts;
   std::vector<uint32_t> matches;     // pcs of Match insts (prog.rs:24)
   uint32_t start = 0;
+  uint32_t dotstar_end = 0;          // insts [0, dotstar_end) are the `(?s-u:.)*?` prefix (DFA programs)
   uint8_t byte_classes[256] = {0};
   bool is_dfa = false, is_reverse = false;
   bool anchored_start = false, anchored_end = false;

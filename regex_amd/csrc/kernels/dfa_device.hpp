@@ -1,0 +1,276 @@
+// Device-side DFA stepping shared by the scan kernels (dfa_scan.hip) and the
+// find_iter kernels (iter_scan.hip).  See dfa_scan.hip for the layout.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dfa_scan.hpp"
+
+namespace rure_amd {
+
+__device__ __forceinline__ bool word_byte(uint32_t b) {
+  return b == '_' || (b - '0') < 10u || ((b | 0x20) - 'a') < 26u;
+}
+
+// dfa.rs:1415-1434
+__device__ __forceinline__ uint32_t fwd_flag_index(const uint8_t *base, uint64_t len, uint64_t at) {
+  bool start = at == 0, end = len == 0;
+  bool start_line = at == 0 || base[at - 1] == '\n';
+  bool wl = at > 0 && word_byte(base[at - 1]);
+  bool wn = at < len && word_byte(base[at]);
+  return (start ? 1u : 0u) | (end ? 2u : 0u) | (start_line ? 4u : 0u) | (end ? 8u : 0u) |
+         (wl != wn ? 16u : 32u) | (wl ? 64u : 0u);
+}
+
+// dfa.rs:1440-1464, on the slice text[lo..] with the search ending at `at`.
+__device__ __forceinline__ uint32_t rev_flag_index(const uint8_t *base, uint64_t lo, uint64_t len,
+                                                   uint64_t at) {
+  bool start = at == len, end = lo == len;
+  bool start_line = at == len || base[at] == '\n';
+  bool wl = at < len && word_byte(base[at]);
+  bool wn = at > lo && word_byte(base[at - 1]);
+  return (start ? 1u : 0u) | (end ? 2u : 0u) | (start_line ? 4u : 0u) | (end ? 8u : 0u) |
+         (wl != wn ? 16u : 32u) | (wl ? 64u : 0u);
+}
+
+struct LaneState {
+  uint32_t s;
+  uint64_t last;   // last match end (NONE if none)
+  bool done;
+  bool quit;
+  bool fast;       // multi-byte path: t holds s * P and s may be stale
+  uint32_t t;
+};
+
+static constexpr uint64_t NONE = ~0ull;
+// LDS fast-table row pitch: 256 bytes + one bank, so that lanes in different
+// states that read the same byte value land in different LDS banks.
+static constexpr uint32_t kRow = 260;
+static constexpr uint64_t QUITMARK = ~0ull - 1;
+
+// Full-table step for one byte at haystack position `pos` (careful path).
+template <int MODE>
+__device__ __forceinline__ void careful_step(LaneState &L, const FwdDfaDev &f, uint32_t b, uint64_t pos) {
+  uint32_t s = f.full[(size_t)L.s * 256 + b];
+  L.s = s;
+  if (s >= f.n_normal) {
+    if (s < f.n_match_end) {                 // dfa.rs:658-668: Match(at - 1)
+      L.last = pos;
+      if (MODE != MODE_FIND) L.done = true;  // quit_after_match
+    } else if (s == f.dead) {                // dfa.rs:728-731
+      L.done = true;
+    } else {                                 // STATE_QUIT (dfa.rs:713-715)
+      L.quit = true;
+      L.done = true;
+    }
+  }
+}
+
+template <int MODE>
+__device__ __forceinline__ void step1(LaneState &L, const FwdDfaDev &f, const uint8_t *lds,
+                                      uint32_t b, uint64_t pos) {
+  if (L.s < f.hot) {
+    uint32_t t = lds[L.s * kRow + b];
+    if (t != f.hot) { L.s = t; return; }
+  }
+  careful_step<MODE>(L, f, b, pos);
+}
+
+// 4 fast-path steps on the bytes of `w` (little endian): byte extraction is
+// off the dependency chain; the chain is one v_mad_u32_u24 + one ds_read_u8.
+__device__ __forceinline__ uint32_t fast4(uint32_t s, uint32_t w, const uint8_t *lds) {
+  const uint32_t b0 = w & 0xFF, b1 = (w >> 8) & 0xFF, b2 = (w >> 16) & 0xFF, b3 = w >> 24;
+  s = lds[s * kRow + b0];
+  s = lds[s * kRow + b1];
+  s = lds[s * kRow + b2];
+  s = lds[s * kRow + b3];
+  return s;
+}
+
+template <int MODE>
+__device__ __forceinline__ void chunk16(LaneState &L, const FwdDfaDev &f, const uint8_t *lds,
+                                        uint4 v, uint64_t pos) {
+  if (L.s < f.hot) {
+    uint32_t t = L.s;
+    t = fast4(t, v.x, lds);
+    t = fast4(t, v.y, lds);
+    t = fast4(t, v.z, lds);
+    t = fast4(t, v.w, lds);
+    if (t != f.hot) { L.s = t; return; }
+  }
+  // Re-run the chunk exactly, byte by byte.
+  uint32_t words[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll 1
+  for (int j = 0; j < 16; ++j) {
+    step1<MODE>(L, f, lds, (words[j >> 2] >> ((j & 3) * 8)) & 0xFF, pos + j);
+    if (L.done) return;
+  }
+}
+
+// Multi-byte fast path (STRIDE = 2 or 4 bytes per dependent LDS lookup).
+// The class lookups do not depend on the state, so only one LDS round trip
+// per STRIDE bytes sits on the critical path.
+template <int STRIDE>
+__device__ __forceinline__ uint32_t fastS(uint32_t t, uint32_t w, const uint8_t *cls, const uint16_t *tab) {
+  if (STRIDE == 4) {
+    uint32_t a = cls[w & 0xFF] + cls[256 + ((w >> 8) & 0xFF)] + cls[512 + ((w >> 16) & 0xFF)] + cls[768 + (w >> 24)];
+    return tab[t + a];
+  } else {
+    uint32_t a0 = cls[w & 0xFF] + cls[256 + ((w >> 8) & 0xFF)];
+    uint32_t a1 = cls[(w >> 16) & 0xFF] + cls[256 + (w >> 24)];
+    t = tab[t + a0];
+    return tab[t + a1];
+  }
+}
+
+template <int MODE, int STRIDE>
+__device__ __forceinline__ void chunk16s(LaneState &L, const FwdDfaDev &f, const uint8_t *cls, const uint16_t *tab,
+                                         uint4 v, uint64_t pos) {
+  if (L.fast) {
+    uint32_t t = L.t;
+    t = fastS<STRIDE>(t, v.x, cls, tab);
+    t = fastS<STRIDE>(t, v.y, cls, tab);
+    t = fastS<STRIDE>(t, v.z, cls, tab);
+    t = fastS<STRIDE>(t, v.w, cls, tab);
+    if (t != f.sent) { L.t = t; return; }
+    L.s = L.t / f.P;  // real state at the chunk start (rare path)
+    L.fast = false;
+  }
+  uint32_t words[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll 1
+  for (int j = 0; j < 16; ++j) {
+    careful_step<MODE>(L, f, (words[j >> 2] >> ((j & 3) * 8)) & 0xFF, pos + j);
+    if (L.done) return;
+  }
+  if (L.s < f.hot_s) { L.t = L.s * f.P; L.fast = true; }
+}
+
+// Reverse DFA over text[lo..me] (exec.rs:651-661, dfa.rs:768-866): longest
+// match, i.e. the smallest start.  Returns the start, NONE (reverse NoMatch)
+// or QUITMARK.
+__device__ __forceinline__ uint64_t rev_scan(const RevDfaDev &r, const uint8_t *base, uint64_t len, uint64_t lo,
+                                             uint64_t me) {
+  uint32_t s = r.start[rev_flag_index(base, lo, len, me)];
+  uint64_t rs = NONE;
+  bool dead = s == r.dead;
+  uint64_t a = me;
+  while (!dead && a > lo) {
+    --a;
+    s = r.full[(size_t)s * 256 + base[a]];
+    if (s >= r.n_normal) {
+      if (s < r.n_match_end) rs = a + 1;
+      else if (s == r.dead) dead = true;
+      else return QUITMARK;
+    }
+  }
+  if (!dead && r.eof[s]) rs = lo;
+  return rs;
+}
+
+// One lane's forward scan of text[at..end) (dfa.rs:576-764): 16-byte
+// chunks through the LDS fast table, 128-byte bursts per lane.  No EOF step.
+template <int MODE>
+__device__ __forceinline__ void fwd_range(LaneState &L, const FwdDfaDev &f, const uint8_t *lds, const uint8_t *base,
+                                          uint64_t at, uint64_t end) {
+  while (!L.done && at < end && (((uintptr_t)(base + at)) & 15)) {
+    step1<MODE>(L, f, lds, base[at], at);
+    ++at;
+  }
+  while (!L.done && at + 128 <= end) {
+    const uint4 *p = (const uint4 *)(base + at);
+    uint4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = p[k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (!L.done) chunk16<MODE>(L, f, lds, v[k], at + 16 * k);
+    at += 128;
+  }
+  while (!L.done && at + 16 <= end) {
+    uint4 v = *(const uint4 *)(base + at);
+    chunk16<MODE>(L, f, lds, v, at);
+    at += 16;
+  }
+  while (!L.done && at < end) {
+    step1<MODE>(L, f, lds, base[at], at);
+    ++at;
+  }
+}
+
+// Full forward scan of text[at..len] including the EOF step (dfa.rs:748-763).
+template <int MODE>
+__device__ __forceinline__ void fwd_run(LaneState &L, const FwdDfaDev &f, const uint8_t *lds, const uint8_t *base,
+                                        uint64_t len, uint64_t at) {
+  fwd_range<MODE>(L, f, lds, base, at, len);
+  if (!L.done && f.eof[L.s]) L.last = len;
+}
+
+__device__ __forceinline__ void lane_start(LaneState &L, const FwdDfaDev &f, const uint8_t *base, uint64_t len,
+                                           uint64_t at) {
+  L.last = NONE;
+  L.done = false;
+  L.quit = false;
+  L.fast = false;
+  L.t = 0;
+  if (at > len) {
+    L.done = true;
+    L.s = f.dead;
+  } else {
+    L.s = f.start[fwd_flag_index(base, len, at)];
+    if (L.s >= f.n_normal) L.done = true;  // dead start state (dfa.rs:484)
+  }
+}
+
+// ExecNoSync::find_dfa_forward (exec.rs:632-662) for one lane: 0 = no
+// match, 1 = match (ms, me), 2 = the DFA quit.
+__device__ __forceinline__ int dfa_find(const FwdDfaDev &f, const RevDfaDev &r, const uint8_t *lds,
+                                        const uint8_t *base, uint64_t len, uint64_t at, uint64_t *ms,
+                                        uint64_t *me) {
+  LaneState L;
+  lane_start(L, f, base, len, at);
+  fwd_run<MODE_FIND>(L, f, lds, base, len, at);
+  if (L.quit) return 2;
+  if (L.last == NONE) return 0;
+  *me = L.last;
+  if (L.last == at) { *ms = at; return 1; }  // exec.rs:647
+  const uint64_t rs = rev_scan(r, base, len, at, L.last);
+  if (rs == QUITMARK) return 2;
+  if (rs == NONE) return 0;  // exec.rs:656-660
+  *ms = rs;
+  return 1;
+}
+
+// dfa_find for a search that may not start a match at or after `cut`
+// (at < cut): the state at cut - 1 is replaced by its copy without the `.*?`
+// prefix (f.strip), so the scan stops once every match that started before
+// the cut has been decided.  Used by the chunked find_iter: its result equals
+// the unrestricted search whenever that search's match starts before the cut,
+// and is "no match" otherwise.
+__device__ __forceinline__ int dfa_find_cut(const FwdDfaDev &f, const RevDfaDev &r, const uint8_t *lds,
+                                            const uint8_t *base, uint64_t len, uint64_t at, uint64_t cut,
+                                            uint64_t *ms, uint64_t *me) {
+  LaneState L;
+  lane_start(L, f, base, len, at);
+  if (cut > at && cut - 1 <= len) {
+    fwd_range<MODE_FIND>(L, f, lds, base, at, cut - 1);
+    if (!L.done) {
+      L.s = f.strip[L.s];
+      if (L.s == f.dead) L.done = true;
+    }
+    fwd_range<MODE_FIND>(L, f, lds, base, cut - 1, len);
+  } else {
+    fwd_range<MODE_FIND>(L, f, lds, base, at, len);
+  }
+  if (!L.done && f.eof[L.s]) L.last = len;
+  if (L.quit) return 2;
+  if (L.last == NONE) return 0;
+  *me = L.last;
+  if (L.last == at) { *ms = at; return 1; }
+  const uint64_t rs = rev_scan(r, base, len, at, L.last);
+  if (rs == QUITMARK) return 2;
+  if (rs == NONE) return 0;
+  *ms = rs;
+  return 1;
+}
+
+}  // namespace rure_amd

@@ -32,6 +32,7 @@ struct FwdDfaDev {
   const uint16_t *full;       // nstates * 256
   const uint8_t *eof;         // nstates: EOF step yields a match flag
   const uint16_t *start;      // 128 start states by flag index
+  const uint16_t *strip;      // find_iter DFA only: state minus the `.*?` prefix (or null)
   uint32_t n_normal, n_match_end, dead, quit;
 };
 
@@ -73,6 +74,17 @@ constexpr size_t kNfaLdsMax = 160 * 1024;   // a gfx950 workgroup may take the w
 enum { MODE_SET = 3 };
 hipError_t launch_pike(int mode, bool fallback, const BatchDev &b, const NfaDev &n, void *out, void *scratch,
                        hipStream_t st, int grid);
+
+// Batched find_iter (iter_scan.hip).  counts: per haystack; matches:
+// (start, end) pairs, the first `cap` written; total: number of matches.
+struct IterOut {
+  uint64_t *counts;
+  uint64_t *matches;
+  uint64_t cap;
+  uint64_t *total;
+};
+hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaDev &r, const NfaDev *nf,
+                            bool chunked, uint64_t chunk, const IterOut &o, hipStream_t st, int cus);
 
 hipError_t launch_dfa_fwd(int mode, const BatchDev &b, const FwdDfaDev &f, const RevDfaDev &r, void *out,
                           hipStream_t st, int grid);

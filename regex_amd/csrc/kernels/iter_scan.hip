@@ -1,0 +1,509 @@
+// Batched find_iter (re_trait.rs:197-221 over ExecNoSync::find_at,
+// exec.rs:473-514) for gfx950.
+//
+// The iteration is sequential by nature: each search starts where the
+// previous match ended.  Long haystacks are cut into chunks ("units"); one
+// lane iterates each unit *speculatively* from a fresh start at the unit's
+// first byte, owning the matches that start inside it.  For patterns without
+// look-around assertions, a unit's speculative result is exact unless the
+// true sequence enters it in a different state: a match of the previous unit
+// that runs past the cut ("dirty" exit).  Those units are repaired by running
+// the true iteration and the speculative one in lockstep until they emit the
+// same match (from there on they coincide); a repair that does not converge
+// inside its unit changes that unit's exit and is propagated by a sequential
+// walker (rare).  Counts are prefix-summed on the device and a final pass
+// writes every unit's matches in order (copied from the unit's slot buffer
+// when the speculation held and the unit had few matches).
+//
+// Patterns whose DFA can quit (Unicode word boundary) or that have no DFA, and
+// patterns with assertions, are iterated one haystack per wavefront without
+// chunking (per search: DFA on one lane, the Pike VM on the wave when the DFA
+// quits or is absent) — the reference's per-search engine dispatch.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <rocprim/rocprim.hpp>
+#include <stdint.h>
+
+#include "dfa_device.hpp"
+#include "nfa_device.hpp"
+
+namespace rure_amd {
+
+namespace {
+
+constexpr uint32_t kSlots = 4;  // speculative matches kept per unit
+
+enum : uint32_t {
+  U_SPEC_CLEAN = 1,   // speculative exit is equivalent to a fresh start at the next unit
+  U_CLEAN = 2,        // final exit clean
+  U_FIXED = 4,        // final entry differs from the speculative one
+  U_QUIT = 8,         // a search quit (cannot happen on the chunked path)
+};
+
+struct IterSt {
+  uint64_t p, lm;  // next search start; end of the last match (NONE if none)
+};
+
+struct Unit {
+  IterSt entry, exit, spec_exit;
+  uint32_t spec_count, flags;
+};
+
+struct Geo {  // unit -> (haystack, chunk) for fixed-stride batches
+  uint64_t nk;      // units per haystack
+  uint64_t chunk;   // bytes per unit
+};
+
+__device__ __forceinline__ void unit_bounds(const BatchDev &b, const Geo &g, uint64_t u, uint64_t *h,
+                                            const uint8_t **base, uint64_t *len, uint64_t *c0, uint64_t *c1) {
+  *h = u / g.nk;
+  const uint64_t k = u % g.nk;
+  if (b.offs) {
+    const uint64_t o0 = b.offs[*h], o1 = b.offs[*h + 1];
+    *base = b.hay + o0;
+    *len = o1 - o0;
+  } else {
+    *base = b.hay + *h * b.stride;
+    *len = b.length;
+  }
+  *c0 = b.start + k * g.chunk;
+  *c1 = (k + 1 == g.nk) ? ~0ull : b.start + (k + 1) * g.chunk;
+}
+
+// One step of re_trait.rs:197-221 (empty-match rule: next search at e + 1,
+// an empty match at the previous match end is skipped).
+__device__ int iter_next(const FwdDfaDev &f, const RevDfaDev &r, const uint8_t *lds, const uint8_t *base,
+                         uint64_t len, uint64_t cut, IterSt &st, uint64_t *s, uint64_t *e) {
+  while (true) {
+    if (st.p > len) return 0;
+    const int k = dfa_find_cut(f, r, lds, base, len, st.p, cut, s, e);
+    if (k != 1) return k;
+    if (*s == *e) {
+      st.p = *e + 1;
+      if (st.lm == *e) continue;
+    } else {
+      st.p = *e;
+    }
+    st.lm = *e;
+    return 1;
+  }
+}
+
+// The matches a unit owns: those whose start is < c1, iterating from `st`.
+struct UnitIter {
+  IterSt st;
+  uint64_t c1;
+  bool ended, clean, quit;
+  IterSt exit;
+
+  __device__ void init(IterSt s0, uint64_t cut) {
+    st = s0;
+    c1 = cut;
+    ended = clean = quit = false;
+  }
+  // Returns true with the next owned match, false when the unit is finished.
+  __device__ bool next(const FwdDfaDev &f, const RevDfaDev &r, const uint8_t *lds, const uint8_t *base,
+                       uint64_t len, uint64_t *s, uint64_t *e) {
+    if (ended) return false;
+    if (st.p >= c1) {  // the previous match ran up to / past the cut
+      ended = true;
+      exit = st;
+      clean = st.p == c1 && st.lm != c1;
+      return false;
+    }
+    const IterSt snap = st;
+    const int k = iter_next(f, r, lds, base, len, c1, st, s, e);
+    if (k == 1 && *s < c1) return true;
+    // no match starts before the cut (the search is cut-bounded, see
+    // dfa_find_cut): a fresh search at the cut finds what the unrestricted
+    // one would (no assertions on this path)
+    ended = true;
+    exit = snap;
+    clean = k != 2;
+    quit = k == 2;
+    return false;
+  }
+};
+
+__device__ __forceinline__ bool exit_equiv(bool ca, const IterSt &a, bool cb, const IterSt &b) {
+  if (ca || cb) return ca && cb;
+  return a.p == b.p && a.lm == b.lm;
+}
+
+template <bool LDS_TABLE>
+__device__ __forceinline__ const uint8_t *stage_table(const FwdDfaDev &f, uint8_t *lds) {
+  for (uint32_t i = threadIdx.x * 16; i < f.lds_bytes; i += blockDim.x * 16)
+    *(uint4 *)(lds + i) = *(const uint4 *)(f.lds_image + i);
+  __syncthreads();
+  return lds;
+}
+
+// Pass 1: speculative iteration of every unit.
+__global__ __launch_bounds__(256) void iter_spec_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
+                                                        Unit *units, uint64_t *slots, uint32_t *counts) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  stage_table<true>(f, lds);
+  for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < nunits; u += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t h, len, c0, c1;
+    const uint8_t *base;
+    unit_bounds(b, g, u, &h, &base, &len, &c0, &c1);
+    UnitIter it;
+    it.init({c0, NONE}, c1);
+    uint32_t n = 0;
+    uint64_t s, e;
+    while (it.next(f, r, lds, base, len, &s, &e)) {
+      if (n < kSlots) {
+        slots[(u * kSlots + n) * 2] = s;
+        slots[(u * kSlots + n) * 2 + 1] = e;
+      }
+      ++n;
+    }
+    Unit U;
+    U.entry = {c0, NONE};
+    U.exit = it.exit;
+    U.spec_exit = it.exit;
+    U.spec_count = n;
+    U.flags = (it.clean ? (U_SPEC_CLEAN | U_CLEAN) : 0) | (it.quit ? U_QUIT : 0);
+    units[u] = U;
+    counts[u] = n;
+  }
+}
+
+// Repairs unit j given its true entry `E`: lockstep with its speculative
+// iteration until both emit the same match.  Updates the unit's record and
+// count; returns true if the unit's exit changed.
+__device__ bool repair_unit(const BatchDev &b, const Geo &g, const FwdDfaDev &f, const RevDfaDev &r,
+                            const uint8_t *lds, uint64_t j, IterSt E, Unit *units, uint32_t *counts) {
+  uint64_t h, len, c0, c1;
+  const uint8_t *base;
+  unit_bounds(b, g, j, &h, &base, &len, &c0, &c1);
+  Unit U = units[j];
+  UnitIter F, S;
+  F.init(E, c1);
+  S.init({c0, NONE}, c1);
+  uint64_t fs, fe, ss, se;
+  bool fm = F.next(f, r, lds, base, len, &fs, &fe);
+  bool sm = S.next(f, r, lds, base, len, &ss, &se);
+  uint32_t fcnt = 0, scnt = 0;
+  bool synced = false;
+  while (fm) {
+    if (sm && fs == ss && fe == se) { synced = true; break; }
+    if (!sm || fs < ss || (fs == ss && fe < se)) {
+      ++fcnt;
+      fm = F.next(f, r, lds, base, len, &fs, &fe);
+    } else {
+      ++scnt;
+      sm = S.next(f, r, lds, base, len, &ss, &se);
+    }
+  }
+  U.entry = E;
+  U.flags |= U_FIXED;
+  bool changed;
+  if (synced) {
+    counts[j] = fcnt + (U.spec_count - scnt);
+    U.exit = U.spec_exit;
+    U.flags = (U.flags & ~U_CLEAN) | ((U.flags & U_SPEC_CLEAN) ? U_CLEAN : 0);
+    changed = false;
+  } else {
+    counts[j] = fcnt;
+    changed = !exit_equiv(F.clean, F.exit, (U.flags & U_SPEC_CLEAN) != 0, U.spec_exit);
+    U.exit = F.exit;
+    U.flags = (U.flags & ~U_CLEAN) | (F.clean ? U_CLEAN : 0) | (F.quit ? U_QUIT : 0);
+  }
+  units[j] = U;
+  return changed;
+}
+
+// Pass 2: units entered through a dirty speculative exit are repaired in
+// parallel; repairs that change their own exit are queued for the walker.
+__global__ __launch_bounds__(256) void iter_fix_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
+                                                       Unit *units, uint32_t *counts, uint64_t *queue,
+                                                       unsigned long long *qlen) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  stage_table<true>(f, lds);
+  for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u + 1 < nunits;
+       u += (uint64_t)gridDim.x * blockDim.x) {
+    if ((u + 1) % g.nk == 0) continue;  // last unit of its haystack
+    const Unit U = units[u];
+    if (U.flags & U_SPEC_CLEAN) continue;
+    if (repair_unit(b, g, f, r, lds, u + 1, U.spec_exit, units, counts)) {
+      const unsigned long long q = atomicAdd(qlen, 1ull);
+      queue[q] = u + 1;
+    }
+  }
+}
+
+// Pass 3 (one thread): propagate exits that changed, in unit order.
+__global__ void iter_walk_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r, Unit *units,
+                                 uint32_t *counts, uint64_t *queue, unsigned long long *qlen) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const uint64_t n = *qlen;
+  if (n == 0) return;
+  for (uint64_t i = 1; i < n; ++i) {  // insertion sort (the queue is short)
+    uint64_t v = queue[i], k = i;
+    while (k > 0 && queue[k - 1] > v) { queue[k] = queue[k - 1]; --k; }
+    queue[k] = v;
+  }
+  uint64_t walked = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint64_t j = queue[i];
+    if (j + 1 <= walked) continue;
+    uint64_t u = j + 1;
+    Unit X = units[j];
+    while (u < nunits && u % g.nk != 0) {
+      const Unit V = units[u];
+      // entry the parallel passes assumed for unit u
+      const Unit P = units[u - 1];
+      const bool assumed_clean = (P.flags & U_SPEC_CLEAN) != 0;
+      if (exit_equiv((X.flags & U_CLEAN) != 0, X.exit, assumed_clean, P.spec_exit)) break;
+      Unit W = V;
+      if (X.flags & U_CLEAN) {  // back to the speculative entry
+        uint64_t h, len, c0, c1;
+        const uint8_t *base;
+        unit_bounds(b, g, u, &h, &base, &len, &c0, &c1);
+        W.entry = {c0, NONE};
+        W.exit = W.spec_exit;
+        W.flags = (W.flags & ~(U_FIXED | U_CLEAN)) | ((W.flags & U_SPEC_CLEAN) ? U_CLEAN : 0);
+        units[u] = W;
+        counts[u] = W.spec_count;
+      } else {
+        repair_unit(b, g, f, r, f.lds_image /* unused: hot = 0 */, u, X.exit, units, counts);
+      }
+      X = units[u];
+      ++u;
+    }
+    walked = u;
+  }
+}
+
+// Pass 4: write every unit's matches at its offset.
+__global__ __launch_bounds__(256) void iter_emit_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
+                                                        const Unit *units, const uint64_t *slots, const uint64_t *off,
+                                                        uint64_t *out, uint64_t cap) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  stage_table<true>(f, lds);
+  for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < nunits; u += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t o0 = off[u], cnt = off[u + 1] - o0;
+    if (cnt == 0 || o0 >= cap) continue;
+    const Unit U = units[u];
+    if (!(U.flags & U_FIXED) && cnt <= kSlots) {
+      for (uint64_t i = 0; i < cnt && o0 + i < cap; ++i) {
+        out[2 * (o0 + i)] = slots[(u * kSlots + i) * 2];
+        out[2 * (o0 + i) + 1] = slots[(u * kSlots + i) * 2 + 1];
+      }
+      continue;
+    }
+    uint64_t h, len, c0, c1;
+    const uint8_t *base;
+    unit_bounds(b, g, u, &h, &base, &len, &c0, &c1);
+    UnitIter it;
+    it.init(U.entry, c1);
+    uint64_t s, e, i = 0;
+    while (i < cnt && it.next(f, r, lds, base, len, &s, &e)) {
+      if (o0 + i < cap) {
+        out[2 * (o0 + i)] = s;
+        out[2 * (o0 + i) + 1] = e;
+      }
+      ++i;
+    }
+  }
+}
+
+// ---------------------------------------------------- one wave per haystack
+// exec.rs:473-514 per search: the DFA on lane 0; the Pike VM on the whole
+// wave when the DFA quits (or when there is no DFA).
+template <bool EMIT>
+__global__ __launch_bounds__(64) void iter_wave_kernel(BatchDev b, FwdDfaDev f, RevDfaDev r, NfaDev nf, int has_dfa,
+                                                       uint32_t *counts, const uint64_t *off, uint64_t *out,
+                                                       uint64_t cap, uint8_t *scratch) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds_mem[];
+  uint8_t *mem = scratch ? scratch + (size_t)blockIdx.x * nfa_wave_bytes(nf.nleaves) : lds_mem;
+  pike::Lists W;
+  const uint32_t N = nf.nleaves;
+  W.st[0] = (uint64_t *)mem;
+  W.st[1] = W.st[0] + N;
+  W.stamp = (uint32_t *)(W.st[1] + N);
+  W.leaf[0] = W.stamp + N;
+  W.leaf[1] = W.leaf[0] + N;
+  const uint32_t lane = pike::lane_id();
+  for (uint32_t i = lane; i < N; i += 64) W.stamp[i] = 0xFFFFFFFFu;
+  pike::wave_sync();
+  pike::TagGen tg;
+  FwdDfaDev fg = f;
+  fg.hot = 0;  // global-table stepping only (the LDS holds the Pike VM lists)
+  for (uint64_t h = blockIdx.x; h < b.count; h += gridDim.x) {
+    const uint8_t *base;
+    uint64_t len;
+    if (b.offs) {
+      const uint64_t o0 = b.offs[h], o1 = b.offs[h + 1];
+      base = b.hay + o0;
+      len = o1 - o0;
+    } else {
+      base = b.hay + h * b.stride;
+      len = b.length;
+    }
+    uint64_t p = b.start, lm = NONE, n = 0;
+    const uint64_t o0 = EMIT ? off[h] : 0, cnt = EMIT ? off[h + 1] - off[h] : 0;
+    while (p <= len && (!EMIT || n < cnt)) {
+      uint64_t s = NONE, e = NONE;
+      int k = 2;
+      if (has_dfa) {
+        uint64_t s0 = NONE, e0 = NONE;
+        int k0 = 0;
+        if (lane == 0) k0 = dfa_find(fg, r, nullptr, base, len, p, &s0, &e0);
+        k = __shfl(k0, 0);
+        s = __shfl(s0, 0);
+        e = __shfl(e0, 0);
+      }
+      if (k == 2) {
+        uint64_t r0, r1;
+        pike::pike_one<MODE_FIND>(nf, W, tg, base, len, p, &r0, &r1);
+        k = r1 == NONE ? 0 : 1;
+        s = r0;
+        e = r1;
+      }
+      if (k == 0) break;
+      if (s == e) {
+        p = e + 1;
+        if (lm == e) continue;
+      } else {
+        p = e;
+      }
+      lm = e;
+      if (EMIT && lane == 0 && o0 + n < cap) {
+        out[2 * (o0 + n)] = s;
+        out[2 * (o0 + n) + 1] = e;
+      }
+      ++n;
+    }
+    if (!EMIT && lane == 0) counts[h] = (uint32_t)n;
+  }
+}
+
+// counts[h] = matches of haystack h, total = all matches.
+__global__ void iter_counts_kernel(uint64_t nh, uint64_t nk, const uint64_t *off, uint64_t *hcounts,
+                                   uint64_t *total) {
+  for (uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; h < nh; h += (uint64_t)gridDim.x * blockDim.x)
+    hcounts[h] = off[(h + 1) * nk] - off[h * nk];
+  if (blockIdx.x == 0 && threadIdx.x == 0) *total = off[nh * nk];
+}
+
+hipError_t scan_counts(const uint32_t *counts, uint64_t *off, uint64_t n, hipStream_t st) {
+  // off[0..n] = exclusive prefix sums of counts[0..n) (off[n] = total)
+  size_t tmp = 0;
+  hipError_t e = rocprim::exclusive_scan(nullptr, tmp, counts, off, (uint64_t)0, (size_t)(n + 1),
+                                         rocprim::plus<uint64_t>(), st);
+  if (e != hipSuccess) return e;
+  void *buf = nullptr;
+  if ((e = hipMallocAsync(&buf, tmp, st)) != hipSuccess) return e;
+  e = rocprim::exclusive_scan(buf, tmp, counts, off, (uint64_t)0, (size_t)(n + 1), rocprim::plus<uint64_t>(), st);
+  hipError_t e2 = hipFreeAsync(buf, st);
+  return e != hipSuccess ? e : e2;
+}
+
+int grid_cap(uint64_t items, int threads, int cus, int per_cu) {
+  uint64_t g = (items + threads - 1) / threads;
+  uint64_t cap = (uint64_t)cus * per_cu;
+  if (g > cap) g = cap;
+  return (int)(g < 1 ? 1 : g);
+}
+
+}  // namespace
+
+hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaDev &r, const NfaDev *nf,
+                            bool chunked, uint64_t chunk, const IterOut &o, hipStream_t st, int cus) {
+  hipError_t e = hipSuccess;
+  if (b.count == 0) {
+    return hipMemsetAsync(o.total, 0, 8, st);
+  }
+  if (chunked) {
+    uint64_t span = (!b.offs && b.length > b.start) ? b.length - b.start : 0;
+    Geo g;
+    g.chunk = chunk;
+    g.nk = (b.offs || span <= chunk) ? 1 : (span + chunk - 1) / chunk;
+    if (b.offs) g.chunk = ~0ull >> 2;
+    const uint64_t nunits = b.count * g.nk;
+    // scratch: units, slots, counts (n + 1), offsets (n + 1), queue, qlen
+    const size_t sz_units = nunits * sizeof(Unit), sz_slots = nunits * kSlots * 16;
+    const size_t sz_counts = (nunits + 1) * 4, sz_off = (nunits + 1) * 8, sz_queue = nunits * 8;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t total = al(sz_units) + al(sz_slots) + al(sz_counts) + al(sz_off) + al(sz_queue) + 256;
+    uint8_t *buf = nullptr;
+    if ((e = hipMallocAsync((void **)&buf, total, st)) != hipSuccess) return e;
+    Unit *units = (Unit *)buf;
+    uint64_t *slots = (uint64_t *)(buf + al(sz_units));
+    uint32_t *counts = (uint32_t *)(buf + al(sz_units) + al(sz_slots));
+    uint64_t *off = (uint64_t *)(buf + al(sz_units) + al(sz_slots) + al(sz_counts));
+    uint64_t *queue = (uint64_t *)(buf + al(sz_units) + al(sz_slots) + al(sz_counts) + al(sz_off));
+    unsigned long long *qlen = (unsigned long long *)(buf + total - 256);
+    const int per_cu = std::max<int>(1, std::min<int>(8, (int)((160u * 1024u) / std::max<uint32_t>(f->lds_bytes, 1))));
+    const int grid = grid_cap(nunits, 256, cus, per_cu);
+    do {
+      if ((e = hipMemsetAsync(counts + nunits, 0, 4, st)) != hipSuccess) break;
+      if ((e = hipMemsetAsync(qlen, 0, 8, st)) != hipSuccess) break;
+      hipLaunchKernelGGL(iter_spec_kernel, dim3(grid), dim3(256), f->lds_bytes, st, b, g, nunits, *f, r, units, slots,
+                         counts);
+      if ((e = hipGetLastError()) != hipSuccess) break;
+      if (g.nk > 1) {
+        hipLaunchKernelGGL(iter_fix_kernel, dim3(grid), dim3(256), f->lds_bytes, st, b, g, nunits, *f, r, units,
+                           counts, queue, qlen);
+        if ((e = hipGetLastError()) != hipSuccess) break;
+        FwdDfaDev fw = *f;
+        fw.hot = 0;
+        hipLaunchKernelGGL(iter_walk_kernel, dim3(1), dim3(64), 0, st, b, g, nunits, fw, r, units, counts, queue, qlen);
+        if ((e = hipGetLastError()) != hipSuccess) break;
+      }
+      if ((e = scan_counts(counts, off, nunits, st)) != hipSuccess) break;
+      hipLaunchKernelGGL(iter_emit_kernel, dim3(grid), dim3(256), f->lds_bytes, st, b, g, nunits, *f, r, units, slots,
+                         off, o.matches, o.cap);
+      if ((e = hipGetLastError()) != hipSuccess) break;
+      hipLaunchKernelGGL(iter_counts_kernel, dim3(grid_cap(b.count, 256, cus, 4)), dim3(256), 0, st, b.count, g.nk,
+                         off, o.counts, o.total);
+      e = hipGetLastError();
+    } while (false);
+    hipError_t e2 = hipFreeAsync(buf, st);
+    return e != hipSuccess ? e : e2;
+  }
+  // one wavefront per haystack (assertions, DFA quit, or no DFA)
+  const size_t wb = nfa_wave_bytes(nf->nleaves);
+  const bool use_lds = wb <= kNfaLdsMax;
+  const int grid = grid_cap(b.count, 1, cus, use_lds ? std::max<int>(1, std::min<int>(32, (int)((160u * 1024u) / wb))) : 4);
+  uint8_t *buf = nullptr;
+  const size_t sz_counts = (b.count + 1) * 4, sz_off = (b.count + 1) * 8;
+  const size_t sz_scr = use_lds ? 0 : wb * (size_t)grid;
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  if ((e = hipMallocAsync((void **)&buf, al(sz_counts) + al(sz_off) + al(sz_scr), st)) != hipSuccess) return e;
+  uint32_t *counts = (uint32_t *)buf;
+  uint64_t *off = (uint64_t *)(buf + al(sz_counts));
+  uint8_t *scr = use_lds ? nullptr : buf + al(sz_counts) + al(sz_off);
+  const size_t lds = use_lds ? wb : 0;
+  FwdDfaDev fz{};
+  const FwdDfaDev &fa = f ? *f : fz;
+  do {
+    if (lds > 64 * 1024) {
+      if ((e = hipFuncSetAttribute((const void *)iter_wave_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)lds)) != hipSuccess)
+        break;
+      if ((e = hipFuncSetAttribute((const void *)iter_wave_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)lds)) != hipSuccess)
+        break;
+    }
+    if ((e = hipMemsetAsync(counts + b.count, 0, 4, st)) != hipSuccess) break;
+    hipLaunchKernelGGL(iter_wave_kernel<false>, dim3(grid), dim3(64), lds, st, b, fa, r, *nf, f ? 1 : 0, counts,
+                       (const uint64_t *)nullptr, (uint64_t *)nullptr, (uint64_t)0, scr);
+    if ((e = hipGetLastError()) != hipSuccess) break;
+    if ((e = scan_counts(counts, off, b.count, st)) != hipSuccess) break;
+    hipLaunchKernelGGL(iter_wave_kernel<true>, dim3(grid), dim3(64), lds, st, b, fa, r, *nf, f ? 1 : 0, counts,
+                       (const uint64_t *)off, o.matches, o.cap, scr);
+    if ((e = hipGetLastError()) != hipSuccess) break;
+    hipLaunchKernelGGL(iter_counts_kernel, dim3(grid_cap(b.count, 256, cus, 4)), dim3(256), 0, st, b.count,
+                       (uint64_t)1, off, o.counts, o.total);
+    e = hipGetLastError();
+  } while (false);
+  hipError_t e2 = hipFreeAsync(buf, st);
+  return e != hipSuccess ? e : e2;
+}
+
+}  // namespace rure_amd

@@ -247,6 +247,11 @@ struct rure {
   bool nfa_ok = false;
   std::map<int, DevTables> dev;
   Staging stage;
+  // find_iter: forward DFA with dotstar-stripped states (chunked iteration)
+  bool iter_built = false, iter_ok = false;
+  DenseDfa dfwd_iter;
+  PackedFwd pf_iter;
+  std::map<int, std::pair<void *, FwdDfaDev>> iter_dev;
 };
 
 struct rure_set {
@@ -523,6 +528,61 @@ hipError_t run_pike(int mode, bool fallback, const BatchDev &b, const DevTables 
   return e != hipSuccess ? e : e2;
 }
 
+bool build_iter_dfa(rure *re) {
+  if (!build_regex_dfas(re)) return false;
+  std::lock_guard<std::mutex> g(re->mu);
+  if (!re->iter_built) {
+    re->iter_built = true;
+    DfaBuildLimits lim;
+    lim.strip = true;
+    std::string e;
+    re->iter_ok = build_dense_dfa(re->fwd, lim, &re->dfwd_iter, &e) && pack_forward(re->dfwd_iter, &re->pf_iter, &e);
+  }
+  return re->iter_ok;
+}
+
+
+// Forward DFA with stripped states for the chunked find_iter (built and
+// uploaded on first use).  Returns null if it does not materialise.
+const FwdDfaDev *iter_device(rure *re, const DevTables &t, std::string *err) {
+  if (!build_iter_dfa(re)) return nullptr;
+  int d = 0;
+  if (!hip_ok(hipGetDevice(&d), err)) return nullptr;
+  std::lock_guard<std::mutex> g(re->mu);
+  auto it = re->iter_dev.find(d);
+  if (it != re->iter_dev.end()) return &it->second.second;
+  const PackedFwd &pf = re->pf_iter;
+  const DenseDfa &fw = re->dfwd_iter;
+  std::vector<uint16_t> strip(fw.strip.size());
+  for (size_t i = 0; i < strip.size(); ++i) strip[i] = (uint16_t)fw.strip[i];
+  Blob b;
+  size_t o_lds = b.add(pf.lds.data(), pf.lds.size());
+  size_t o_full = b.add(pf.full.data(), pf.full.size() * 2);
+  size_t o_eof = b.add(pf.eof.data(), pf.eof.size());
+  size_t o_start = b.add(pf.start.data(), 256);
+  size_t o_strip = b.add(strip.data(), strip.size() * 2);
+  DevTables tmp;
+  if (!upload_blob(b, &tmp, err)) return nullptr;
+  uint8_t *base = (uint8_t *)tmp.blob;
+  FwdDfaDev f{};
+  f.lds_image = base + o_lds;
+  f.lds_bytes = (uint32_t)pf.lds.size();
+  f.hot = pf.hot;
+  f.lds_image_s = nullptr;
+  f.stride = 1;
+  f.cus = (uint32_t)t.cus;
+  f.full = (const uint16_t *)(base + o_full);
+  f.eof = base + o_eof;
+  f.start = (const uint16_t *)(base + o_start);
+  f.strip = (const uint16_t *)(base + o_strip);
+  f.n_normal = fw.n_normal;
+  f.n_match_end = fw.n_match_end;
+  f.dead = fw.dead;
+  f.quit = fw.quit < 0 ? 0xFFFFFFFFu : (uint32_t)fw.quit;
+  re->iter_dev[d] = {tmp.blob, f};
+  return &re->iter_dev[d].second;
+}
+
 // The engine dispatch of exec.rs:473-514 / 382-420 for a batch: DFA, and the
 // Pike VM where the DFA quits (or instead of it when it does not fit).
 hipError_t run_regex(int mode, const BatchDev &b, const DevTables &t, void *out, hipStream_t st, int dfa_grid) {
@@ -707,6 +767,13 @@ rure *rure_compile_must(const char *pattern) {  // rure.rs:76-91
 
 void rure_free(rure *re) {
   if (!re) return;
+  for (auto &kv : re->iter_dev) {
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(kv.first);
+    (void)hipFree(kv.second.first);
+    (void)hipSetDevice(cur);
+  }
   for (auto &kv : re->dev) {
     int cur = 0;
     (void)hipGetDevice(&cur);
@@ -889,13 +956,48 @@ int rure_amd_set_matches_batch(rure_set *rs, const rure_amd_batch *batch, uint64
   return RURE_AMD_OK;
 }
 
+int rure_amd_find_iter_batch(rure *re, const rure_amd_batch *batch, uint64_t *counts, rure_match *matches,
+                             size_t capacity, uint64_t *total, void *stream) {
+  BatchDev b;
+  if (!re || !to_batch(batch, &b) || (!counts && b.count) || !total || (!matches && capacity))
+    return RURE_AMD_ERR_ARG;
+  std::string err;
+  DevTables *t = regex_device(re, &err);
+  if (!t) return err.rfind("HIP", 0) == 0 ? RURE_AMD_ERR_HIP : RURE_AMD_ERR_DFA;
+  // Chunked speculative iteration needs a DFA that cannot quit and a pattern
+  // without assertions (see iter_scan.hip); otherwise one wave per haystack.
+  const FwdDfaDev *fi = nullptr;
+  if (t->has_dfa && !t->quit_possible && re->nfa_ok && re->nt.looks_used == 0) fi = iter_device(re, *t, &err);
+  IterOut o{counts, (uint64_t *)matches, capacity, total};
+  hipError_t e;
+  if (fi) {
+    uint64_t chunk = ~0ull >> 2;
+    if (!b.offs && b.length > b.start && b.count) {
+      const uint64_t span = b.length - b.start;
+      const uint64_t target = (uint64_t)t->cus * 256;  // lanes to fill the chip
+      const uint64_t per_h = (target + b.count - 1) / b.count;
+      chunk = std::max<uint64_t>(4096, (span + per_h - 1) / per_h);
+      chunk = (chunk + 63) & ~(uint64_t)63;
+    }
+    e = launch_find_iter(b, fi, t->r, &t->n, true, chunk, o, (hipStream_t)stream, t->cus);
+  } else {
+    if (!re->nfa_ok) return RURE_AMD_ERR_DFA;
+    e = launch_find_iter(b, t->has_dfa ? &t->f : nullptr, t->r, &t->n, false, 0, o, (hipStream_t)stream, t->cus);
+  }
+  return e == hipSuccess ? RURE_AMD_OK : RURE_AMD_ERR_HIP;
+}
+
 // ------------------------------------------------------------- diagnostics
 int rure_amd_dfa_info_get(rure *re, int which, rure_amd_dfa_info *info) {
   if (!re || !info) return RURE_AMD_ERR_ARG;
   memset(info, 0, sizeof(*info));
   if (!build_regex_dfas(re)) { info->ok = 0; return RURE_AMD_ERR_DFA; }
   if (which == 0) fill_info(re->dfwd, re->fwd, re->pf.hot, info, &re->pf);
-  else fill_info(re->drev, re->rev, 0, info);
+  else if (which == 1) fill_info(re->drev, re->rev, 0, info);
+  else {
+    if (!build_iter_dfa(re)) { info->ok = 0; return RURE_AMD_ERR_DFA; }
+    fill_info(re->dfwd_iter, re->fwd, re->pf_iter.hot, info, &re->pf_iter);
+  }
   return RURE_AMD_OK;
 }
 
@@ -923,10 +1025,18 @@ int64_t rure_amd_set_program_export(rure_set *rs, int which, rure_amd_prog_info 
   return export_prog(which == 0 ? rs->fwd : rs->nfa, info, insts, cap);
 }
 
+int rure_amd_dfa_strip_export(rure *re, uint32_t *strip) {
+  if (!re) return RURE_AMD_ERR_ARG;
+  if (!build_iter_dfa(re)) return RURE_AMD_ERR_DFA;
+  if (strip) memcpy(strip, re->dfwd_iter.strip.data(), re->dfwd_iter.strip.size() * 4);
+  return RURE_AMD_OK;
+}
+
 int rure_amd_dfa_export(rure *re, int which, uint32_t *trans, uint8_t *eof_match, uint32_t *start) {
   if (!re) return RURE_AMD_ERR_ARG;
   if (!build_regex_dfas(re)) return RURE_AMD_ERR_DFA;
-  const DenseDfa &d = which == 0 ? re->dfwd : re->drev;
+  if (which == 2 && !build_iter_dfa(re)) return RURE_AMD_ERR_DFA;
+  const DenseDfa &d = which == 0 ? re->dfwd : which == 1 ? re->drev : re->dfwd_iter;
   if (trans) memcpy(trans, d.trans.data(), d.trans.size() * 4);
   if (eof_match) memcpy(eof_match, d.eof_match.data(), d.eof_match.size());
   if (start) memcpy(start, d.start, sizeof(d.start));

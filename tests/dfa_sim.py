@@ -29,7 +29,9 @@ class QuitError(Exception):
     pass
 
 
-def find(fwd, rev, t, start=0, mode="find"):
+def find(fwd, rev, t, start=0, mode="find", cut=None):
+    """cut: the search may not start a match at or after `cut` (the kernel's
+    dfa_find_cut: the state at cut - 1 is replaced by its stripped copy)."""
     info, tr, eof, st = fwd
     s = int(st[fwd_flag(t, start)])
     last = None
@@ -37,7 +39,13 @@ def find(fwd, rev, t, start=0, mode="find"):
         return None
     at = start
     done = False
+    strip_at = cut - 1 if (cut is not None and cut > start and cut - 1 <= len(t)) else None
     while at < len(t):
+        if at == strip_at:
+            s = int(info["strip"][s])
+            if s == info["dead"]:
+                done = True
+                break
         s = int(tr[s, t[at]])
         if s >= info["normal"]:
             if s < info["match_end"]:
@@ -51,6 +59,9 @@ def find(fwd, rev, t, start=0, mode="find"):
             else:
                 raise QuitError()
         at += 1
+    if not done and strip_at == len(t):
+        s = int(info["strip"][s])
+        done = s == info["dead"]
     if not done and eof[s]:
         last = len(t)
     if mode == "shortest":

@@ -1,0 +1,148 @@
+"""Host-side simulation of the chunked find_iter pipeline of
+regex_amd/csrc/kernels/iter_scan.hip (speculative units, lockstep repair,
+sequential walker, emit), over the exported find_iter DFA tables.
+TEST INFRASTRUCTURE: validates the boundary-repair algorithm on CPU."""
+from dfa_sim import find
+
+NONE = None
+
+
+class UnitIter(object):
+    def __init__(self, fwd, rev, t, st, c1):
+        self.fwd, self.rev, self.t = fwd, rev, t
+        self.p, self.lm = st
+        self.c1 = c1
+        self.ended = False
+        self.clean = False
+        self.exit = None
+
+    def _iter_next(self):
+        t = self.t
+        while True:
+            if self.p > len(t):
+                return None
+            m = find(self.fwd, self.rev, t, self.p, cut=self.c1)
+            if m is None:
+                return None
+            s, e = m
+            if s == e:
+                self.p = e + 1
+                if self.lm == e:
+                    continue
+            else:
+                self.p = e
+            self.lm = e
+            return m
+
+    def next(self):
+        if self.ended:
+            return None
+        if self.p >= self.c1:
+            self.ended = True
+            self.exit = (self.p, self.lm)
+            self.clean = self.p == self.c1 and self.lm != self.c1
+            return None
+        snap = (self.p, self.lm)
+        m = self._iter_next()
+        if m is not None and m[0] < self.c1:
+            return m
+        self.ended = True
+        self.exit = snap
+        self.clean = True
+        return None
+
+
+def equiv(ca, a, cb, b):
+    if ca or cb:
+        return ca and cb
+    return a == b
+
+
+def find_iter_chunked(fwd, rev, t, chunk, start=0):
+    INF = float("inf")
+    span = max(0, len(t) - start)
+    nk = 1 if span <= chunk else (span + chunk - 1) // chunk
+    bounds = [(start + k * chunk, INF if k + 1 == nk else start + (k + 1) * chunk) for k in range(nk)]
+    units = []
+    for k, (c0, c1) in enumerate(bounds):  # pass 1: speculation
+        it = UnitIter(fwd, rev, t, (c0, None), c1)
+        ms = []
+        while True:
+            m = it.next()
+            if m is None:
+                break
+            ms.append(m)
+        units.append({"entry": (c0, None), "spec": ms, "spec_exit": it.exit, "spec_clean": it.clean,
+                      "exit": it.exit, "clean": it.clean, "fixed": False, "count": len(ms)})
+
+    def repair(j, E):
+        c0, c1 = bounds[j]
+        U = units[j]
+        F = UnitIter(fwd, rev, t, E, c1)
+        S = UnitIter(fwd, rev, t, (c0, None), c1)
+        fm, sm = F.next(), S.next()
+        fcnt = scnt = 0
+        synced = False
+        while fm is not None:
+            if sm is not None and fm == sm:
+                synced = True
+                break
+            if sm is None or fm < sm:
+                fcnt += 1
+                fm = F.next()
+            else:
+                scnt += 1
+                sm = S.next()
+        U["entry"], U["fixed"] = E, True
+        if synced:
+            U["count"] = fcnt + U_len(U) - scnt
+            U["exit"], U["clean"] = U["spec_exit"], U["spec_clean"]
+            return False
+        U["count"] = fcnt
+        changed = not equiv(F.clean, F.exit, U["spec_clean"], U["spec_exit"])
+        U["exit"], U["clean"] = F.exit, F.clean
+        return changed
+
+    def U_len(U):
+        return len(U["spec"])
+
+    queue = []
+    for u in range(nk - 1):  # pass 2: parallel repair
+        if not units[u]["spec_clean"]:
+            if repair(u + 1, units[u]["spec_exit"]):
+                queue.append(u + 1)
+    walked = 0  # pass 3: sequential walker
+    for j in sorted(queue):
+        if j + 1 <= walked:
+            continue
+        u = j + 1
+        X = units[j]
+        while u < nk:
+            P = units[u - 1]
+            if equiv(X["clean"], X["exit"], P["spec_clean"], P["spec_exit"]):
+                break
+            if X["clean"]:
+                W = units[u]
+                W["entry"], W["exit"], W["clean"], W["fixed"], W["count"] = \
+                    (bounds[u][0], None), W["spec_exit"], W["spec_clean"], False, len(W["spec"])
+            else:
+                repair(u, X["exit"])
+            X = units[u]
+            u += 1
+        walked = u
+    out = []  # pass 4: emit
+    for u, U in enumerate(units):
+        if U["count"] == 0:
+            continue
+        if not U["fixed"]:
+            assert len(U["spec"]) == U["count"]
+            out.extend(U["spec"])
+            continue
+        it = UnitIter(fwd, rev, t, U["entry"], bounds[u][1])
+        got = []
+        while len(got) < U["count"]:
+            m = it.next()
+            assert m is not None
+            got.append(m)
+        out.extend(got)
+    return out

@@ -1,0 +1,43 @@
+"""CPU check of the chunked find_iter algorithm (iter_scan.hip, mirrored by
+tests/iter_sim.py) over the find_iter DFA with stripped states: with tiny
+chunks (many boundaries, matches straddling cuts) the result must equal the
+oracle's sequential find_iter (re_trait.rs:197-221) exactly."""
+import random
+import zlib
+
+import pytest
+
+import regex_amd as R
+from iter_sim import find_iter_chunked
+from oracle_py import OracleRegex
+
+PATTERNS = [r"a+", r"ab|a", r"[a-c]+d?", r"x*", r"(?s).", r"\w+@\w+\.\w+", r"\d{4}-\d{2}-\d{2}",
+            r"agggtaaa|tttaccct", r"[cgt]gggtaaa|tttaccc[acg]", r">[^\n]*\n|\n", r"a*?b", r"(a|ab)(c|bcd)(d*)",
+            r"[ab]{2,5}", r"", r"b*"]
+
+
+def text(seed, n):
+    rng = random.Random(seed)
+    alpha = b"aabbcd x@.\n>0123-gt"
+    return bytes(rng.choice(alpha) for _ in range(n))
+
+
+@pytest.mark.parametrize("pat", PATTERNS)
+@pytest.mark.parametrize("chunk", [7, 16, 61])
+def test_chunked_iter_matches_oracle(pat, chunk):
+    re = R.Regex(pat)
+    assert re.nfa_tables()[0]["looks"] == 0
+    fwd = re.dfa_tables(2)
+    rev = re.dfa_tables(1)
+    o = OracleRegex(re)
+    for i in range(6):
+        t = text(zlib.crc32(pat.encode()) + i, 150 + 37 * i)
+        exp = o.find_iter(t)
+        got = find_iter_chunked(fwd, rev, t, chunk)
+        assert got == exp, (pat, chunk, i)
+
+
+def test_strip_states_exist():
+    info = R.Regex(r"\w+@\w+\.\w+").dfa_info(2)
+    base = R.Regex(r"\w+@\w+\.\w+").dfa_info(0)
+    assert info["ok"] == 1 and info["states"] >= base["states"]
