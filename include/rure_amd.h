@@ -171,6 +171,11 @@ int64_t rure_amd_set_program_export(rure_set *re, int which, rure_amd_prog_info 
  * of the chunked find_iter (with stripped states, see _strip_export). */
 int rure_amd_dfa_export(rure *re, int which, uint32_t *trans, uint8_t *eof_match,
                         uint32_t *start);
+/* Export of a set's DFA (rure_amd_set_dfa_info_get gives the sizes): trans =
+ * states*256 u32, eof_mask / now_mask = states u64 (patterns matched at the
+ * end of the text / reported on entering the state), start = 128 u32. */
+int rure_amd_set_dfa_export(rure_set *re, uint32_t *trans, uint64_t *eof_mask, uint64_t *now_mask,
+                            uint32_t *start);
 /* strip[s] (states u32) of the find_iter forward DFA: s without the `.*?` prefix. */
 int rure_amd_dfa_strip_export(rure *re, uint32_t *strip);
 

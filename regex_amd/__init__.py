@@ -320,6 +320,21 @@ class RegexSet(object):
     def uses_dfa(self):
         return N.rure_amd_set_uses_dfa(self._set) == 1
 
+    def dfa_tables(self):
+        """Set DFA: (info, trans (states, 256), eof_mask, now_mask, start)."""
+        import numpy as np
+        info = self.dfa_info()
+        if info is None or not info.get("ok"):
+            return None
+        n = info["states"]
+        trans = np.zeros(n * 256, dtype=np.uint32)
+        eof = np.zeros(n, dtype=np.uint64)
+        now = np.zeros(n, dtype=np.uint64)
+        start = np.zeros(128, dtype=np.uint32)
+        _check(N.rure_amd_set_dfa_export(self._set, trans.ctypes.data, eof.ctypes.data, now.ctypes.data,
+                                         start.ctypes.data), "set_dfa_export")
+        return info, trans.reshape(n, 256), eof, now, start
+
     def nfa_tables(self):
         return _nfa_export(N.rure_amd_set_nfa_export, self._set)
 

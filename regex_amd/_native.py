@@ -111,6 +111,7 @@ rure_amd_set_program_export = _sig("rure_amd_set_program_export", ctypes.c_int64
 rure_amd_dfa_export = _sig("rure_amd_dfa_export", ctypes.c_int, VP, ctypes.c_int, VP, VP, VP)
 rure_amd_nfa_export = _sig("rure_amd_nfa_export", ctypes.c_int, VP, ctypes.POINTER(NfaInfo), VP, VP, VP)
 rure_amd_set_nfa_export = _sig("rure_amd_set_nfa_export", ctypes.c_int, VP, ctypes.POINTER(NfaInfo), VP, VP, VP)
+rure_amd_set_dfa_export = _sig("rure_amd_set_dfa_export", ctypes.c_int, VP, VP, VP, VP, VP)
 rure_amd_dfa_strip_export = _sig("rure_amd_dfa_strip_export", ctypes.c_int, VP, VP)
 rure_amd_find_iter_batch = _sig("rure_amd_find_iter_batch", ctypes.c_int, VP, ctypes.POINTER(RureBatch), VP, VP,
                                 c_size, VP, VP)

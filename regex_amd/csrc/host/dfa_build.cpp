@@ -65,6 +65,25 @@ class Builder {
       std::string key = keys_[s];  // copy: keys_ may grow
       if (strip_) strip_raw_.push_back(strip_key(key));
       trans_cls_.resize((s + 1) * ncls);
+      // Sets: states that differ only in the matches their entry reported
+      // step identically; compute each thread set's row once.
+      size_t cut = key.size();
+      if (is_set_) {
+        for (size_t k = 1; k + 4 <= key.size(); k += 4) {
+          uint32_t ip;
+          memcpy(&ip, key.data() + k, 4);
+          if (ip == 0xFFFFFFFFu) { cut = k; break; }
+        }
+        auto it = core_.find(key.substr(0, cut));
+        if (it != core_.end()) {
+          const size_t o = it->second;
+          for (int c = 0; c < ncls; ++c) trans_cls_[s * ncls + c] = trans_cls_[o * ncls + c];
+          eof_match_.push_back(eof_match_[o]);
+          eof_mask_.push_back(eof_mask_[o]);
+          continue;
+        }
+        core_.emplace(key.substr(0, cut), s);
+      }
       for (int c = 0; c < ncls; ++c) trans_cls_[s * ncls + c] = step(key, rep[c]);
       uint64_t mask = 0;
       bool m = step_eof(key, &mask);
@@ -93,6 +112,7 @@ class Builder {
   std::vector<uint32_t> strip_raw_;  // raw state (from 2) -> stripped raw state
   std::vector<std::string> keys_;
   std::unordered_map<std::string, uint32_t> ids_;
+  std::unordered_map<std::string, size_t> core_;  // sets: thread set -> first raw state with it
   std::vector<uint32_t> trans_cls_;
   std::vector<uint8_t> eof_match_;
   std::vector<uint64_t> eof_mask_;
@@ -129,8 +149,9 @@ class Builder {
     }
   }
 
-  // dfa.rs:1196-1244 plus interning; returns raw id (0 = DEAD).
-  uint32_t intern(const SparseSet &q, uint8_t sflags) {
+  // dfa.rs:1196-1244 plus interning; returns raw id (0 = DEAD).  `now`
+  // (sets only): Match slots reached by the step that produced this state.
+  uint32_t intern(const SparseSet &q, uint8_t sflags, uint64_t now = 0) {
     std::string key(1, '\0');
     for (size_t k = 0; k < q.n; ++k) {
       uint32_t ip = q.dense[k];
@@ -144,6 +165,11 @@ class Builder {
       }
       if (push) key.append((const char *)&ip, 4);
       if (stop) break;
+    }
+    if (now) {
+      const uint32_t sep = 0xFFFFFFFFu;
+      key.append((const char *)&sep, 4);
+      key.append((const char *)&now, 8);
     }
     if (key.size() == 1 && !(sflags & SF_MATCH)) return 0;
     key[0] = (char)sflags;
@@ -161,6 +187,7 @@ class Builder {
     for (size_t i = 1; i + 4 <= key.size(); i += 4) {
       uint32_t ip;
       memcpy(&ip, key.data() + i, 4);
+      if (ip == 0xFFFFFFFFu) { k.append(key, i, std::string::npos); break; }
       if (ip >= p_.dotstar_end) k.append(key, i, 4);
     }
     if (k.size() == 1 && !(k[0] & SF_MATCH)) return 0;
@@ -179,13 +206,27 @@ class Builder {
     for (size_t k = 1; k + 4 <= key.size(); k += 4) {
       uint32_t ip;
       memcpy(&ip, key.data() + k, 4);
+      if (ip == 0xFFFFFFFFu) break;  // sets: the `now` match mask follows
       q.insert(ip);
     }
   }
 
+  static uint64_t now_of(const std::string &key) {
+    for (size_t k = 1; k + 4 <= key.size(); k += 4) {
+      uint32_t ip;
+      memcpy(&ip, key.data() + k, 4);
+      if (ip == 0xFFFFFFFFu) {
+        uint64_t m;
+        memcpy(&m, key.data() + k + 4, 8);
+        return m;
+      }
+    }
+    return 0;
+  }
+
   // Shared body of exec_byte (dfa.rs:910-1048) for a real byte (b < 256) or
   // EOF (b == 256).  Leaves the resulting ordered set in *res and flags in *sf.
-  void exec(const std::string &key, int b, SparseSet **res, uint8_t *sf) {
+  void exec(const std::string &key, int b, SparseSet **res, uint8_t *sf, uint64_t *now = nullptr) {
     SparseSet *qcur = &qa_, *qnext = &qb_;
     load(key, *qcur);
     uint8_t flags = (uint8_t)key[0];
@@ -205,13 +246,19 @@ class Builder {
     uint8_t sflags = 0;
     if (is_word && word_matters_) sflags |= SF_WORD;
     qnext->clear();
+    uint64_t m_now = 0;
     for (size_t k = 0; k < qcur->n; ++k) {
       uint32_t ip = qcur->dense[k];
       const Inst &in = p_.insts[ip];
       if (in.op == OP_MATCH) {
         sflags |= SF_MATCH;
         if (!cont_) break;
-        if (is_set_ && !qnext->contains(ip)) qnext->insert(ip);
+        // Sets: the reference carries Match instructions forward in the
+        // state (dfa.rs:988-993) so the final state holds every pattern seen.
+        // Here they are reported by the step instead (the next state records
+        // the slots reached now), which gives the same union of matches with
+        // far fewer states (no subset-of-patterns-seen in the state).
+        if (is_set_ && in.x < 64) m_now |= 1ull << in.x;
       } else if (in.op == OP_BYTES) {
         if (b < 256 && in.lo <= b && b <= in.hi) follow(in.x, *qnext, ef2);
       }
@@ -219,12 +266,13 @@ class Builder {
     if (b == 256 && is_set_) std::swap(qcur, qnext);  // dfa.rs:1004-1015
     *res = qnext;
     *sf = sflags;
+    if (now) *now = m_now;
   }
 
   uint32_t step(const std::string &key, uint8_t b) {
-    SparseSet *q; uint8_t sf;
-    exec(key, b, &q, &sf);
-    return intern(*q, sf);
+    SparseSet *q; uint8_t sf; uint64_t now = 0;
+    exec(key, b, &q, &sf, &now);
+    return intern(*q, sf, is_set_ ? now : 0);
   }
 
   bool step_eof(const std::string &key, uint64_t *mask) {
@@ -300,7 +348,11 @@ class Builder {
       uint8_t tag = (s == 0 || (s == 1 && !quit_)) ? 1 : s == 1 ? 2 : 0;
       k.push_back((char)tag);
       if (s >= 2) {
-        if (is_set_) k.append((const char *)&eof_mask_[s], 8);
+        if (is_set_) {
+          k.append((const char *)&eof_mask_[s], 8);
+          uint64_t nm = now_of(keys_[s]);
+          k.append((const char *)&nm, 8);
+        }
         else {
           uint8_t m = (keys_[s][0] & SF_MATCH) ? 1 : 0;
           k.push_back((char)m);
@@ -342,10 +394,7 @@ class Builder {
     auto is_special = [&](uint32_t b) {
       int s = rep[b];
       if (b == dead_b || (quit_used && b == quit_b)) return false;
-      if (is_set_) {  // absorbing: result can no longer change
-        for (int c : colrep) if (block[t[(size_t)s * 256 + c]] != b) return false;
-        return true;
-      }
+      if (is_set_) return now_of(keys_[s]) != 0;  // entering it reports matches
       return (keys_[s][0] & SF_MATCH) != 0;
     };
     // order: normal states reachable from the start states through ASCII
@@ -403,11 +452,13 @@ class Builder {
     out->trans.assign((size_t)next * 256, 0);
     out->eof_match.assign(next, 0);
     out->eof_mask.assign(next, 0);
+    out->now_mask.assign(next, 0);
     for (uint32_t b = 0; b < nblocks; ++b) {
       int s = rep[b], id = newid[b];
       for (int c = 0; c < 256; ++c) out->trans[(size_t)id * 256 + c] = newid[block[t[(size_t)s * 256 + c]]];
       out->eof_match[id] = eof_match_[s];
       out->eof_mask[id] = eof_mask_[s];
+      if (is_set_) out->now_mask[id] = now_of(keys_[s]);
     }
     for (int i = 0; i < 128; ++i) out->start[i] = (uint32_t)(start_used_[i] ? newid[block[start_raw_[i]]] : out->dead);
     out->strip.clear();

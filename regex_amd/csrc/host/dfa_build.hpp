@@ -20,6 +20,7 @@ namespace rure_amd {
 // One materialized + minimised DFA.  State numbering (kernel contract):
 //   [0, n_normal)            ordinary states (no match flag)
 //   [n_normal, n_match_end)  states carrying the (one-byte delayed) match flag
+//                            (sets: states whose entry reports matches, now_mask)
 //   dead                     == n_match_end      (absorbing, never matches)
 //   quit                     == n_match_end + 1  (only if has_quit)
 struct DenseDfa {
@@ -32,7 +33,9 @@ struct DenseDfa {
   bool reverse = false;
   std::vector<uint32_t> trans;     // nstates * 256, next state per byte
   std::vector<uint8_t> eof_match;  // per state: EOF transition yields a match flag
-  std::vector<uint64_t> eof_mask;  // sets: Match slots visible after the EOF step
+  std::vector<uint64_t> eof_mask;  // sets: Match slots reached at the end of the text (EOF step)
+  std::vector<uint64_t> now_mask;  // sets: Match slots reached by the step into this state
+                                   // ([n_normal, n_match_end) are exactly the states with now_mask != 0)
   uint32_t start[128];             // start state per 7-bit start-flag index (dfa.rs:1381-1390)
   int raw_states = 0;              // states before minimisation (diagnostics)
   int n_ascii = 0;                 // normal states reachable through ASCII bytes (numbered first)

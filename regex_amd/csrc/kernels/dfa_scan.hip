@@ -184,26 +184,33 @@ __global__ __launch_bounds__(256) void dfa_fwd_tile_kernel(BatchDev bt, FwdDfaDe
 
 // ---------------------------------------------------------------- sets
 // RegexSet::matches (re_set.rs:184-213 -> exec.rs:998-1038 ->
-// dfa.rs:525-570 forward_many).  Match instructions are carried forward in
-// set states (dfa.rs:984-994), so the answer is the Match set visible after
-// the final EOF step (dfa.rs:1004-1015): eof_mask[final state].  Absorbing
-// states ([n_normal, n_match_end)) end the scan early (dfa.rs:675-682).
-__device__ __forceinline__ bool set_careful(uint32_t &s, const SetDfaDev &f, uint32_t b, bool &quit) {
+// dfa.rs:525-570 forward_many).  The reference carries Match instructions
+// forward in set states (dfa.rs:984-994) and reads the answer off the last
+// state (dfa.rs:1004-1015); our set DFA reports the patterns reached by each
+// step instead (now_mask of the state entered, host/dfa_build.cpp), so the
+// lane ORs them up: same union, far fewer states.  Only the few states that
+// report matches leave the LDS fast path.
+__device__ __forceinline__ bool set_careful(uint32_t &s, uint64_t &mask, const SetDfaDev &f, uint32_t b,
+                                            bool &quit) {
   s = f.full[(size_t)s * 256 + b];
   if (s >= f.n_normal) {
+    if (s < f.n_match_end) {
+      mask |= f.now_mask[s];
+      return mask == f.all;  // every pattern matched: nothing left to learn
+    }
     if (s == f.quit) quit = true;
-    return true;
+    return true;  // dead or quit
   }
   return false;
 }
 
-__device__ __forceinline__ bool set_step1(uint32_t &s, const SetDfaDev &f, const uint8_t *lds, uint32_t b,
-                                          bool &quit) {
+__device__ __forceinline__ bool set_step1(uint32_t &s, uint64_t &mask, const SetDfaDev &f, const uint8_t *lds,
+                                          uint32_t b, bool &quit) {
   if (s < f.hot) {
     uint32_t t = lds[s * kRow + b];
     if (t != f.hot) { s = t; return false; }
   }
-  return set_careful(s, f, b, quit);
+  return set_careful(s, mask, f, b, quit);
 }
 
 template <bool STRIDED>
@@ -218,13 +225,13 @@ __global__ __launch_bounds__(256) void dfa_set_kernel(BatchDev bt, SetDfaDev f, 
     uint64_t len;
     if (STRIDED) { base = bt.hay + h * bt.stride; len = bt.length; }
     else { uint64_t o0 = bt.offs[h], o1 = bt.offs[h + 1]; base = bt.hay + o0; len = o1 - o0; }
-    uint64_t at = bt.start;
+    uint64_t at = bt.start, mask = 0;
     bool quit = false, done = false;
     uint32_t s;
     if (at > len) { s = f.dead; done = true; }
-    else { s = f.start[fwd_flag_index(base, len, at)]; done = s >= f.n_normal; }
+    else { s = f.start[fwd_flag_index(base, len, at)]; done = s == f.dead; }
     while (!done && at < len && (((uintptr_t)(base + at)) & 15)) {
-      done = set_step1(s, f, lds, base[at], quit);
+      done = set_step1(s, mask, f, lds, base[at], quit);
       ++at;
     }
     while (!done && at + 16 <= len) {
@@ -238,17 +245,18 @@ __global__ __launch_bounds__(256) void dfa_set_kernel(BatchDev bt, SetDfaDev f, 
       s = s0;
       uint32_t words[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll 1
-      for (int j = 0; j < 16 && !done; ++j) done = set_step1(s, f, lds, (words[j >> 2] >> ((j & 3) * 8)) & 0xFF, quit);
+      for (int j = 0; j < 16 && !done; ++j)
+        done = set_step1(s, mask, f, lds, (words[j >> 2] >> ((j & 3) * 8)) & 0xFF, quit);
       at += 16;
     }
     while (!done && at < len) {
-      done = set_step1(s, f, lds, base[at], quit);
+      done = set_step1(s, mask, f, lds, base[at], quit);
       ++at;
     }
     uint64_t m;
     if (quit) m = QUITMARK;
-    else if (s == f.dead) m = 0;
-    else m = f.eof_mask[s];
+    else if (done) m = mask;  // dead, or every pattern already matched
+    else m = mask | f.eof_mask[s];
     out[h] = m;
   }
 }

@@ -43,13 +43,16 @@ struct RevDfaDev {
   uint32_t n_normal, n_match_end, dead, quit;
 };
 
-// Set DFA: final answer is eof_mask[state after the last byte].
+// Set DFA: the answer is the union of now_mask[s] over the states entered
+// ([n_normal, n_match_end) have now_mask != 0) and eof_mask[final state].
 struct SetDfaDev {
   const uint8_t *lds_image;
   uint32_t lds_bytes;
   uint32_t hot;
   const uint16_t *full;
   const uint64_t *eof_mask;
+  const uint64_t *now_mask;
+  uint64_t all;               // every pattern (early exit)
   const uint16_t *start;
   uint32_t n_normal, n_match_end, dead, quit;
 };

@@ -73,6 +73,7 @@ struct PackedFwd {
   std::vector<uint16_t> full;
   std::vector<uint8_t> eof;
   std::vector<uint64_t> eof_mask;
+  std::vector<uint64_t> now_mask;
   std::vector<uint16_t> start;
   uint32_t hot = 0;
 };
@@ -166,6 +167,7 @@ bool pack_forward(const DenseDfa &d, PackedFwd *p, std::string *err) {
   for (size_t i = 0; i < p->full.size(); ++i) p->full[i] = (uint16_t)d.trans[i];
   p->eof.assign(d.eof_match.begin(), d.eof_match.end());
   p->eof_mask.assign(d.eof_mask.begin(), d.eof_mask.end());
+  p->now_mask.assign(d.now_mask.begin(), d.now_mask.end());
   p->start.resize(128);
   for (int i = 0; i < 128; ++i) p->start[i] = (uint16_t)d.start[i];
   return true;
@@ -473,11 +475,12 @@ DevTables *set_device(rure_set *rs, std::string *err) {
   t.cus = device_cus(d);
   NfaOffsets no{};
   if (rs->nfa_ok) no = add_nfa(b, rs->nt);
-  size_t o_lds = 0, o_full = 0, o_mask = 0, o_start = 0;
+  size_t o_lds = 0, o_full = 0, o_mask = 0, o_now = 0, o_start = 0;
   if (rs->dfa_ok) {
     o_lds = b.add(pf.lds.data(), pf.lds.size());
     o_full = b.add(pf.full.data(), pf.full.size() * 2);
     o_mask = b.add(pf.eof_mask.data(), pf.eof_mask.size() * 8);
+    o_now = b.add(pf.now_mask.data(), pf.now_mask.size() * 8);
     o_start = b.add(pf.start.data(), 256);
   }
   if (!upload_blob(b, &t, err)) return nullptr;
@@ -493,6 +496,8 @@ DevTables *set_device(rure_set *rs, std::string *err) {
     t.s.hot = pf.hot;
     t.s.full = (const uint16_t *)(base + o_full);
     t.s.eof_mask = (const uint64_t *)(base + o_mask);
+    t.s.now_mask = (const uint64_t *)(base + o_now);
+    t.s.all = rs->exprs.size() >= 64 ? ~0ull : ((1ull << rs->exprs.size()) - 1);
     t.s.start = (const uint16_t *)(base + o_start);
     t.s.n_normal = fw.n_normal;
     t.s.n_match_end = fw.n_match_end;
@@ -1023,6 +1028,19 @@ int64_t rure_amd_set_program_export(rure_set *rs, int which, rure_amd_prog_info 
   if (rs->single) return rure_amd_program_export(rs->single, which, info, insts, cap);
   if (which == 1) return RURE_AMD_ERR_ARG;
   return export_prog(which == 0 ? rs->fwd : rs->nfa, info, insts, cap);
+}
+
+int rure_amd_set_dfa_export(rure_set *rs, uint32_t *trans, uint64_t *eof_mask, uint64_t *now_mask,
+                            uint32_t *start) {
+  if (!rs) return RURE_AMD_ERR_ARG;
+  if (rs->single || rs->exprs.size() < 2) return RURE_AMD_ERR_ARG;
+  if (!build_set_dfa(rs)) return RURE_AMD_ERR_DFA;
+  const DenseDfa &d = rs->dfa;
+  if (trans) memcpy(trans, d.trans.data(), d.trans.size() * 4);
+  if (eof_mask) memcpy(eof_mask, d.eof_mask.data(), d.eof_mask.size() * 8);
+  if (now_mask) memcpy(now_mask, d.now_mask.data(), d.now_mask.size() * 8);
+  if (start) memcpy(start, d.start, sizeof(d.start));
+  return RURE_AMD_OK;
 }
 
 int rure_amd_dfa_strip_export(rure *re, uint32_t *strip) {

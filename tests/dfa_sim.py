@@ -93,3 +93,28 @@ def find(fwd, rev, t, start=0, mode="find", cut=None):
     if rs is None:  # exec.rs:656-660: the reverse DFA over text[start..] found no start -> NoMatch
         return None
     return (rs, last)
+
+
+def set_matches(tables, t, start=0):
+    """The set kernel's walk (dfa_scan.hip dfa_set_kernel): OR of the now
+    masks of the states entered, plus the EOF mask of the last state."""
+    info, tr, eof, now, st = tables
+    if start > len(t):
+        return 0
+    s = int(st[fwd_flag(t, start)])
+    mask = 0
+    full = (1 << info["n"]) - 1
+    if s == info["dead"]:
+        return 0
+    for at in range(start, len(t)):
+        s = int(tr[s, t[at]])
+        if s >= info["normal"]:
+            if s < info["match_end"]:
+                mask |= int(now[s])
+                if mask == full:
+                    return mask
+            elif s == info["dead"]:
+                return mask
+            else:
+                raise QuitError()
+    return mask | int(eof[s])
