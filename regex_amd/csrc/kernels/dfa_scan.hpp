@@ -89,6 +89,11 @@ struct IterOut {
 hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaDev &r, const NfaDev *nf,
                             bool chunked, uint64_t chunk, const IterOut &o, hipStream_t st, int cus);
 
+// One search per haystack over few long fixed-stride haystacks, chunked
+// (iter_scan.hip); f must be the find_iter DFA (with strip).
+hipError_t launch_long_scan(int mode, const BatchDev &b, const FwdDfaDev &f, const RevDfaDev &r, uint64_t chunk,
+                            void *out, hipStream_t st, int cus);
+
 hipError_t launch_dfa_fwd(int mode, const BatchDev &b, const FwdDfaDev &f, const RevDfaDev &r, void *out,
                           hipStream_t st, int grid);
 hipError_t launch_dfa_set(const BatchDev &b, const SetDfaDev &f, uint64_t *out, hipStream_t st, int grid);

@@ -410,7 +410,111 @@ int grid_cap(uint64_t items, int threads, int cus, int per_cu) {
   return (int)(g < 1 ? 1 : g);
 }
 
+// ------------------------------------------ one search over long haystacks
+// find / is_match / shortest_match (exec.rs:473-514, 382-420) when a batch
+// holds few, long haystacks: every unit scans its chunk with the cut-bounded
+// search (threads started in [c0, c1) only).  The leftmost-first match lives
+// in the first unit whose threads reach a match state: its forward end equals
+// the unrestricted search's (the earlier-started threads never match and the
+// later-started ones are cut by the match or never outrank it), and the
+// reverse pass runs over text[start..end] as the reference's does.  The
+// earliest match end (shortest_match) is the minimum over units.
+template <int MODE>
+__global__ __launch_bounds__(256) void long_scan_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
+                                                        uint64_t *ures, unsigned long long *best) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  stage_table<true>(f, lds);
+  for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < nunits; u += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t h, len, c0, c1;
+    const uint8_t *base;
+    unit_bounds(b, g, u, &h, &base, &len, &c0, &c1);
+    LaneState L;
+    lane_start(L, f, base, len, c0);
+    if (c1 > c0 && c1 - 1 <= len) {
+      fwd_range<MODE>(L, f, lds, base, c0, c1 - 1);
+      if (!L.done) {
+        L.s = f.strip[L.s];
+        if (L.s == f.dead) L.done = true;
+      }
+      fwd_range<MODE>(L, f, lds, base, c1 - 1, len);
+    } else {
+      fwd_range<MODE>(L, f, lds, base, c0, len);
+    }
+    if (!L.done && f.eof[L.s]) L.last = len;
+    if (L.last == NONE) continue;
+    if (MODE == MODE_ISMATCH) {
+      best[h] = 1;
+    } else if (MODE == MODE_SHORTEST) {
+      atomicMin(&best[h], (unsigned long long)L.last);
+    } else {
+      uint64_t ms, me = L.last;
+      if (me == b.start) ms = me;  // exec.rs:647
+      else {
+        const uint64_t rs = rev_scan(r, base, len, b.start, me);
+        ms = rs;
+        if (rs == NONE) me = NONE;  // reverse NoMatch -> the search has no match
+      }
+      ures[2 * u] = ms;
+      ures[2 * u + 1] = me;
+      atomicMin(&best[h], (unsigned long long)u);
+    }
+  }
+}
+
+template <int MODE>
+__global__ void long_finish_kernel(uint64_t count, const uint64_t *ures, const unsigned long long *best, void *out) {
+  for (uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; h < count; h += (uint64_t)gridDim.x * blockDim.x) {
+    const unsigned long long v = best[h];
+    if (MODE == MODE_ISMATCH) {
+      ((uint8_t *)out)[h] = v == 1 ? 1 : 0;
+    } else if (MODE == MODE_SHORTEST) {
+      ((uint64_t *)out)[h] = v;
+    } else {
+      ((uint64_t *)out)[2 * h] = v == ~0ull ? NONE : ures[2 * v];
+      ((uint64_t *)out)[2 * h + 1] = v == ~0ull ? NONE : ures[2 * v + 1];
+    }
+  }
+}
+
+template <int MODE>
+hipError_t long_scan_m(const BatchDev &b, const FwdDfaDev &f, const RevDfaDev &r, uint64_t chunk, void *out,
+                       hipStream_t st, int cus) {
+  Geo g;
+  g.chunk = chunk;
+  const uint64_t span = b.length > b.start ? b.length - b.start : 0;
+  g.nk = span <= chunk ? 1 : (span + chunk - 1) / chunk;
+  const uint64_t nunits = b.count * g.nk;
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t sz_u = MODE == MODE_FIND ? nunits * 16 : 0, sz_b = b.count * 8;
+  uint8_t *buf = nullptr;
+  hipError_t e = hipMallocAsync((void **)&buf, al(sz_u) + al(sz_b), st);
+  if (e != hipSuccess) return e;
+  uint64_t *ures = (uint64_t *)buf;
+  unsigned long long *best = (unsigned long long *)(buf + al(sz_u));
+  do {
+    if ((e = hipMemsetAsync(best, MODE == MODE_ISMATCH ? 0 : 0xFF, sz_b, st)) != hipSuccess) break;
+    const int per_cu = std::max<int>(1, std::min<int>(8, (int)((160u * 1024u) / std::max<uint32_t>(f.lds_bytes, 1))));
+    hipLaunchKernelGGL(long_scan_kernel<MODE>, dim3(grid_cap(nunits, 256, cus, per_cu)), dim3(256), f.lds_bytes, st, b,
+                       g, nunits, f, r, ures, best);
+    if ((e = hipGetLastError()) != hipSuccess) break;
+    hipLaunchKernelGGL(long_finish_kernel<MODE>, dim3(grid_cap(b.count, 256, cus, 4)), dim3(256), 0, st, b.count,
+                       (const uint64_t *)ures, (const unsigned long long *)best, out);
+    e = hipGetLastError();
+  } while (false);
+  hipError_t e2 = hipFreeAsync(buf, st);
+  return e != hipSuccess ? e : e2;
+}
+
 }  // namespace
+
+hipError_t launch_long_scan(int mode, const BatchDev &b, const FwdDfaDev &f, const RevDfaDev &r, uint64_t chunk,
+                            void *out, hipStream_t st, int cus) {
+  switch (mode) {
+    case MODE_FIND: return long_scan_m<MODE_FIND>(b, f, r, chunk, out, st, cus);
+    case MODE_ISMATCH: return long_scan_m<MODE_ISMATCH>(b, f, r, chunk, out, st, cus);
+    default: return long_scan_m<MODE_SHORTEST>(b, f, r, chunk, out, st, cus);
+  }
+}
 
 hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaDev &r, const NfaDev *nf,
                             bool chunked, uint64_t chunk, const IterOut &o, hipStream_t st, int cus) {

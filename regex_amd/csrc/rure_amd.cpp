@@ -590,8 +590,25 @@ const FwdDfaDev *iter_device(rure *re, const DevTables &t, std::string *err) {
 
 // The engine dispatch of exec.rs:473-514 / 382-420 for a batch: DFA, and the
 // Pike VM where the DFA quits (or instead of it when it does not fit).
-hipError_t run_regex(int mode, const BatchDev &b, const DevTables &t, void *out, hipStream_t st, int dfa_grid) {
+// Few long haystacks: one lane per haystack would leave the chip idle, so the
+// search is split into chunks (launch_long_scan).  Needs a DFA that cannot
+// quit (the Pike VM fallback is per haystack).
+bool long_batch(const BatchDev &b, const DevTables &t, uint64_t *chunk) {
+  if (b.offs || !t.has_dfa || t.quit_possible || b.count == 0) return false;
+  const uint64_t span = b.length > b.start ? b.length - b.start : 0;
+  if (span < (256u << 10) || b.count >= (uint64_t)t.cus * 128) return false;
+  const uint64_t target = (uint64_t)t.cus * 256;
+  const uint64_t per_h = (target + b.count - 1) / b.count;
+  uint64_t c = std::max<uint64_t>(64u << 10, (span + per_h - 1) / per_h);
+  *chunk = (c + 127) & ~(uint64_t)127;
+  return true;
+}
+
+hipError_t run_regex(int mode, const BatchDev &b, const DevTables &t, void *out, hipStream_t st, int dfa_grid,
+                     const FwdDfaDev *iter = nullptr) {
   if (!t.has_dfa) return run_pike(mode, false, b, t, out, st);
+  uint64_t chunk = 0;
+  if (iter && long_batch(b, t, &chunk)) return launch_long_scan(mode, b, *iter, t.r, chunk, out, st, t.cus);
   hipError_t e = launch_dfa_fwd(mode, b, t.f, t.r, out, st, dfa_grid);
   if (e != hipSuccess || !t.quit_possible) return e;
   return run_pike(mode, true, b, t, out, st);
@@ -624,14 +641,17 @@ bool single_call(rure *re, int mode, const uint8_t *hay, size_t len, size_t star
   std::string err;
   DevTables *t = regex_device(re, &err);
   if (!t) die(err);
+  uint64_t chunk;
+  BatchDev probe{nullptr, nullptr, len, len, 1, start};
+  const FwdDfaDev *iter = long_batch(probe, *t, &chunk) ? iter_device(re, *t, &err) : nullptr;  // locks re->mu
   std::lock_guard<std::mutex> g(re->mu);
   int d = 0;
   if (!hip_ok(hipGetDevice(&d), &err)) die(err);
   if (!re->stage.ensure(d, len, &err)) die(err);
   hipStream_t st = re->stage.stream;
   if (len && !hip_ok(hipMemcpyAsync(re->stage.hay, hay, len, hipMemcpyHostToDevice, st), &err)) die(err);
-  BatchDev b{re->stage.hay, nullptr, 0, len, 1, start};
-  if (!hip_ok(run_regex(mode, b, *t, re->stage.res, st, 1), &err)) die(err);
+  BatchDev b{re->stage.hay, nullptr, len, len, 1, start};
+  if (!hip_ok(run_regex(mode, b, *t, re->stage.res, st, 1, iter), &err)) die(err);
   uint64_t out[2] = {~0ull, ~0ull};
   size_t nbytes = mode == MODE_FIND ? 16 : mode == MODE_SHORTEST ? 8 : 1;
   if (!hip_ok(hipMemcpyAsync(out, re->stage.res, nbytes, hipMemcpyDeviceToHost, st), &err)) die(err);
@@ -920,7 +940,9 @@ int rure_amd_find_batch(rure *re, const rure_amd_batch *batch, rure_match *out, 
   DevTables *t = regex_device(re, &err);
   if (!t) return err.rfind("HIP", 0) == 0 ? RURE_AMD_ERR_HIP : RURE_AMD_ERR_DFA;
   int grid = grid_for(b.count, t->f.lds_bytes, t->cus);
-  if (run_regex(MODE_FIND, b, *t, out, (hipStream_t)stream, grid) != hipSuccess) return RURE_AMD_ERR_HIP;
+  uint64_t chunk;
+  const FwdDfaDev *iter = long_batch(b, *t, &chunk) ? iter_device(re, *t, &err) : nullptr;
+  if (run_regex(MODE_FIND, b, *t, out, (hipStream_t)stream, grid, iter) != hipSuccess) return RURE_AMD_ERR_HIP;
   return RURE_AMD_OK;
 }
 
@@ -932,7 +954,9 @@ int rure_amd_is_match_batch(rure *re, const rure_amd_batch *batch, uint8_t *out,
   DevTables *t = regex_device(re, &err);
   if (!t) return err.rfind("HIP", 0) == 0 ? RURE_AMD_ERR_HIP : RURE_AMD_ERR_DFA;
   int grid = grid_for(b.count, t->f.lds_bytes, t->cus);
-  if (run_regex(MODE_ISMATCH, b, *t, out, (hipStream_t)stream, grid) != hipSuccess) return RURE_AMD_ERR_HIP;
+  uint64_t chunk;
+  const FwdDfaDev *iter = long_batch(b, *t, &chunk) ? iter_device(re, *t, &err) : nullptr;
+  if (run_regex(MODE_ISMATCH, b, *t, out, (hipStream_t)stream, grid, iter) != hipSuccess) return RURE_AMD_ERR_HIP;
   return RURE_AMD_OK;
 }
 
@@ -944,7 +968,9 @@ int rure_amd_shortest_match_batch(rure *re, const rure_amd_batch *batch, size_t 
   DevTables *t = regex_device(re, &err);
   if (!t) return err.rfind("HIP", 0) == 0 ? RURE_AMD_ERR_HIP : RURE_AMD_ERR_DFA;
   int grid = grid_for(b.count, t->f.lds_bytes, t->cus);
-  if (run_regex(MODE_SHORTEST, b, *t, end, (hipStream_t)stream, grid) != hipSuccess) return RURE_AMD_ERR_HIP;
+  uint64_t chunk;
+  const FwdDfaDev *iter = long_batch(b, *t, &chunk) ? iter_device(re, *t, &err) : nullptr;
+  if (run_regex(MODE_SHORTEST, b, *t, end, (hipStream_t)stream, grid, iter) != hipSuccess) return RURE_AMD_ERR_HIP;
   return RURE_AMD_OK;
 }
 
