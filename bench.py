@@ -1,20 +1,26 @@
 #!/usr/bin/env python3
 """Headline benchmark: batched `bytes::Regex::find` (BASELINE.json configs[1], C2).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
 
-A step = one pass of the hot path over one batch: the date regex
-`\\d{4}-\\d{2}-\\d{2}` `find` over 1,048,576 synthetic haystacks x 4 KiB
-(4 GiB, fixed stride, resident in HBM) on every rank (weak scaling: each
-rank owns its own shard of haystacks), followed, for N > 1, by an RCCL
-all-gather of the compacted match records (haystack id, start, end) — the
-only exchange step the path has.  One process per GPU (torch.distributed,
-backend "nccl" = RCCL).
+Default (the driver's line) = C2: a step is one pass of the hot path over one
+batch — the date regex `\\d{4}-\\d{2}-\\d{2}` `find` over 1,048,576 synthetic
+haystacks x 4 KiB (4 GiB, fixed stride, resident in HBM) on every rank (weak
+scaling: each rank owns its own shard), followed, for N > 1, by the only
+exchange the path has: an all-gather (RCCL) of the compacted match records.
+
+Other configs (for DESIGN.md's table; same timing protocol):
+  c3  regex-dna: `>[^\\n]*\\n|\\n` find_iter over the input replicated to
+      2 GiB, then the 9 variant patterns' find_iter over the stripped 2 GiB
+  c4  RegexSet of 64 patterns over 10M synthetic log lines (one mask per line)
+  c5  `\\w+@\\w+\\.\\w+` find over one 16 GiB haystack per GPU, one planted
+      match in its last MiB; records gathered across ranks
 
 Prints ONE JSON line (rank 0) with the roofline of the scan kernel (HIP
-events on the launch stream, algorithmic bytes per launch) and the CPU
-baseline (the oracle = restated reference lazy DFA, timed on a bounded
-sample of the same haystacks, multi-threaded).
+events on the launch stream, algorithmic bytes per launch; HBM traffic from
+the committed rocprofv3 PMC pass of the same command) and, for C2, the CPU
+baseline (the oracle = restated reference lazy DFA, timed on a bounded sample
+of the same haystacks, multi-threaded).
 """
 import argparse
 import json
@@ -29,6 +35,7 @@ sys.path.insert(0, ROOT)
 
 PATTERN = r"\d{4}-\d{2}-\d{2}"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+METRIC = "haystack GB/s scanned + matches/s, batched bytes::Regex::find, 1/2/4/8 MI355X"
 
 
 def parse():
@@ -36,6 +43,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"])
     ap.add_argument("--haystacks", type=int, default=1 << 20)
     ap.add_argument("--length", type=int, default=4096)
     ap.add_argument("--match-frac", type=float, default=0.01)
@@ -55,124 +63,76 @@ def cpu_threads(req):
     return max(1, min(16, n))
 
 
-def main():
-    args = parse()
-    import torch
-    import torch.distributed as dist
+class Ctx(object):
+    def __init__(self, args):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist, self.args = torch, dist, args
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        self.dev = torch.device("cuda", local)
+        if self.world > 1:
+            dist.init_process_group("nccl", device_id=self.dev)
+        self.stream = torch.cuda.current_stream(self.dev)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    def kernel_ms(self, fn):
+        """Mean duration of fn() over --steps launches, HIP events on the launch stream."""
+        torch = self.torch
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(self.args.steps)]
+        for a, b in ev:
+            a.record(self.stream)
+            fn()
+            b.record(self.stream)
+        torch.cuda.synchronize()
+        return float(np.mean([a.elapsed_time(b) for a, b in ev]))
 
-    import regex_amd as R
-    from regex_amd.workloads import date_haystacks_device
+    def timed(self, step):
+        """Warmup, then EXACTLY --steps steps between barrier + synchronize;
+        max over ranks (seconds per step)."""
+        torch, dist = self.torch, self.dist
+        for _ in range(self.args.warmup):
+            step()
+        torch.cuda.synchronize()
+        if self.world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(self.args.steps):
+            step()
+        torch.cuda.synchronize()
+        if self.world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        if self.world > 1:
+            from regex_amd.dist import max_over_ranks
+            dt = max_over_ranks(dt, self.dev)
+        return dt / self.args.steps
 
-    n, L = args.haystacks, args.length
-    seed = 0x5EED0002 ^ rank
-    hay, planted = date_haystacks_device(n, L, seed, dev, frac=args.match_frac)
-    re = R.Regex(PATTERN)
-    out = torch.empty((n, 2), dtype=torch.int64, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    def line(self, metric, value, unit, ms, dtype, data, config, **extra):
+        d = {"metric": metric, "value": round(value, 2), "unit": unit, "n_gpus": self.world,
+             "steps": self.args.steps, "warmup": self.args.warmup, "ms_per_step": round(ms, 4),
+             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": dtype,
+             "data": data, "config": config}
+        d.update(extra)
+        return d
 
-    def scan():
-        re.find_batch(hay, stride=L, length=L, count=n, out=out, stream=stream)
+    def close(self):
+        if self.world > 1:
+            self.dist.destroy_process_group()
 
-    max_rec = max(1024, int(n * args.match_frac * 2) + 1024)
 
-    def step():
-        scan()
-        if world > 1:
-            # compact (haystack id, start, end) records and gather them to all ranks
-            hit = (out[:, 0] >= 0).nonzero().squeeze(1)
-            k = min(hit.numel(), max_rec)
-            rec = torch.full((max_rec, 3), -1, dtype=torch.int64, device=dev)
-            rec[:k, 0] = hit[:k] + rank * n
-            rec[:k, 1:] = out[hit[:k]]
-            gathered = torch.empty((world * max_rec, 3), dtype=torch.int64, device=dev)
-            dist.all_gather_into_tensor(gathered, rec)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-
-    # kernel-only timing with HIP events on the launch stream
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    for a, b in ev:
-        a.record(stream)
-        scan()
-        b.record(stream)
-    torch.cuda.synchronize()
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-
-    # timed steps
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    ms_per_step = dt * 1000.0 / args.steps
-
-    res = out.cpu().numpy()
-    matched = int((res[:, 0] >= 0).sum())
-    # algorithmic bytes per launch (SURVEY §8d): forward bytes to the DFA's stop
-    # (whole haystack when there is no match; e+1 when the DFA dies after a
-    # match), reverse span, 16-byte result records.
-    m = res[:, 0] >= 0
-    fwd = np.where(m, np.minimum(res[:, 1] + 1, L), L).sum()
-    rev = (res[m, 1] - res[m, 0]).sum()
-    b_alg = float(fwd + rev + 16 * n)
-    achieved = b_alg / (kernel_ms * 1e-3) / 1e9
-
-    total_bytes = float(n) * L * world
-    value = total_bytes / (ms_per_step * 1e-3) / 1e9
-    matches_per_s = matched * world / (ms_per_step * 1e-3)
-
-    line = {
-        "metric": "haystack GB/s scanned + matches/s, batched bytes::Regex::find, 1/2/4/8 MI355X",
-        "value": round(value, 2),
-        "unit": "GB/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u8",
-        "data": "synthetic (seeded printable ASCII, 20% digits, 1% planted dates)",
-        "config": {"workload": "C2: find %s over %d x %d B haystacks per GPU" % (PATTERN, n, L),
-                   "haystacks_per_gpu": n, "haystack_bytes": L, "parallelism": "dp%d" % world},
-        "matches_per_s": round(matches_per_s, 1),
-        "matched_haystacks": matched,
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel_ms": round(kernel_ms, 4), "alg_bytes_per_launch": int(b_alg)},
-    }
-
-    tr = profiled_traffic(line["config"], b_alg)
+def roofline(achieved_gbs, kernel_ms, b_alg, config):
+    r = {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+         "kernel_ms": round(kernel_ms, 4), "alg_bytes_per_launch": int(b_alg)}
+    tr = profiled_traffic(config, b_alg)
     if tr is not None:
-        line["roofline"]["traffic"] = tr["bytes"]
-        line["roofline"]["traffic_source"] = tr["source"]
-
-    if rank == 0 and not args.no_cpu:
-        line["cpu_baseline"] = cpu_baseline(re, hay, res, n, L, args)
-    if rank == 0:
-        print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+        r["traffic"] = tr["bytes"]
+        r["traffic_source"] = tr["source"]
+    return r
 
 
 def profiled_traffic(config, b_alg):
@@ -202,6 +162,53 @@ def profiled_traffic(config, b_alg):
                        d["hbm_read_bytes_per_launch"] / b_alg)}
 
 
+# ------------------------------------------------------------------ C2
+def run_c2(ctx):
+    import regex_amd as R
+    from regex_amd.dist import compact_matches, gather_records
+    from regex_amd.workloads import date_haystacks_device
+    torch, args = ctx.torch, ctx.args
+    n, L = args.haystacks, args.length
+    hay, planted = date_haystacks_device(n, L, 0x5EED0002 ^ ctx.rank, ctx.dev, frac=args.match_frac)
+    re = R.Regex(PATTERN)
+    out = torch.empty((n, 2), dtype=torch.int64, device=ctx.dev)
+
+    def scan():
+        re.find_batch(hay, stride=L, length=L, count=n, out=out, stream=ctx.stream)
+
+    def step():
+        scan()
+        if ctx.world > 1:
+            gather_records(compact_matches(out, ctx.rank * n))
+
+    for _ in range(args.warmup):
+        scan()
+    torch.cuda.synchronize()
+    kernel_ms = ctx.kernel_ms(scan)
+    sec = ctx.timed(step)
+
+    res = out.cpu().numpy()
+    matched = int((res[:, 0] >= 0).sum())
+    # algorithmic bytes per launch (SURVEY §8d): forward bytes to the DFA's stop
+    # (whole haystack when there is no match; e+1 when the DFA dies after a
+    # match), reverse span, 16-byte result records.
+    m = res[:, 0] >= 0
+    fwd = np.where(m, np.minimum(res[:, 1] + 1, L), L).sum()
+    rev = (res[m, 1] - res[m, 0]).sum()
+    b_alg = float(fwd + rev + 16 * n)
+    achieved = b_alg / (kernel_ms * 1e-3) / 1e9
+    value = float(n) * L * ctx.world / sec / 1e9
+    config = {"workload": "C2: find %s over %d x %d B haystacks per GPU" % (PATTERN, n, L),
+              "haystacks_per_gpu": n, "haystack_bytes": L, "parallelism": "dp%d" % ctx.world}
+    line = ctx.line(METRIC, value, "GB/s", sec * 1e3, "u8",
+                    "synthetic (seeded printable ASCII, 20% digits, 1% planted dates)", config,
+                    matches_per_s=round(matched * ctx.world / sec, 1), matched_haystacks=matched,
+                    roofline=roofline(achieved, kernel_ms, b_alg, config))
+    if ctx.rank == 0 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline(re, hay, res, n, L, args)
+    return line
+
+
 def cpu_baseline(re, hay, res, n, L, args):
     """The oracle (restated reference lazy DFA, oracle/) on a bounded sample of
     the same haystacks, one private DFA cache per thread; also re-checks the
@@ -210,7 +217,6 @@ def cpu_baseline(re, hay, res, n, L, args):
     from oracle_py import OracleRegex
     threads = cpu_threads(args.cpu_threads)
     o = OracleRegex(re)
-    # sample: first S haystacks, sized so one pass is ~1 s of CPU time
     S = min(n, 65536)
     buf = hay[: S * L].cpu().numpy()
     t0 = time.perf_counter()
@@ -228,6 +234,176 @@ def cpu_baseline(re, hay, res, n, L, args):
             "sample": "%d passes over the first %d haystacks x %d B (%.0f MiB) of the same batch" %
                       (passes, S, L, S * L / 2**20),
             "parity_on_sample": parity, "fwd_bytes_per_pass": int(st["fwd_bytes"])}
+
+
+# ------------------------------------------------------------------ C3
+def run_c3(ctx):
+    import ctypes
+
+    import regex_amd as R
+    from regex_amd import _native as NN
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from golden_data import corpus, known_counts
+    from oracle_py import OracleRegex
+    torch = ctx.torch
+    kc = known_counts()["regexdna"]
+    raw = corpus("regexdna")
+    copies = (1 << 31) // len(raw)            # 21106 copies, 2,147,429,970 B
+    N = copies * len(raw)
+    one = torch.from_numpy(np.frombuffer(raw, dtype=np.uint8).copy()).to(ctx.dev)
+    big = torch.empty(N + 16, dtype=torch.uint8, device=ctx.dev)
+    big[:N].view(copies, len(raw)).copy_(one.expand(copies, len(raw)))
+    big[N:] = 0
+    strip = R.Regex(kc["strip"])
+    cap = 40_000_000
+    spans = torch.empty((cap, 2), dtype=torch.int64, device=ctx.dev)
+    cnt = torch.empty(1, dtype=torch.int64, device=ctx.dev)
+    tot = torch.empty(1, dtype=torch.int64, device=ctx.dev)
+
+    def find_iter_raw(re_, buf, n, out, counts, total):
+        b = R._batch(buf, None, n, n, 1, 0)
+        rc = NN.rure_amd_find_iter_batch(re_._re, ctypes.byref(b), ctypes.c_void_p(counts.data_ptr()),
+                                         ctypes.c_void_p(out.data_ptr()), out.shape[0],
+                                         ctypes.c_void_p(total.data_ptr()), R._stream_ptr(ctx.stream))
+        assert rc == 0
+
+    find_iter_raw(strip, big, N, spans, cnt, tot)
+    torch.cuda.synchronize()
+    nsp = int(tot.item())
+    assert nsp <= cap
+    # replace_all(strip, "") on the device: keep mask from the match spans
+    d = torch.zeros(N + 1, dtype=torch.int32, device=ctx.dev)
+    sp = spans[:nsp]
+    d.index_add_(0, sp[:, 0], torch.ones(nsp, dtype=torch.int32, device=ctx.dev))
+    d.index_add_(0, sp[:, 1], torch.full((nsp,), -1, dtype=torch.int32, device=ctx.dev))
+    keep = torch.cumsum(d[:N], 0) == 0
+    del d
+    seq = torch.cat([big[:N][keep], torch.zeros(16, dtype=torch.uint8, device=ctx.dev)])
+    del keep
+    M = seq.numel() - 16
+    assert M == kc["stripped_len"] * copies, (M, kc["stripped_len"] * copies)
+    variants = [R.Regex(v["re"]) for v in kc["variants"]]
+    vout = torch.empty((1 << 20, 2), dtype=torch.int64, device=ctx.dev)
+    vcnt = [torch.empty(1, dtype=torch.int64, device=ctx.dev) for _ in variants]
+    vtot = [torch.empty(1, dtype=torch.int64, device=ctx.dev) for _ in variants]
+
+    def strip_pass():
+        find_iter_raw(strip, big, N, spans, cnt, tot)
+
+    def variant_pass():
+        for v, c, t in zip(variants, vcnt, vtot):
+            find_iter_raw(v, seq, M, vout, c, t)
+
+    def step():
+        strip_pass()
+        variant_pass()
+
+    for _ in range(ctx.args.warmup):
+        step()
+    torch.cuda.synchronize()
+    # known answers: per-copy counts x copies + matches across copy seams
+    stripped_one = bytes(seq[: kc["stripped_len"]].cpu().numpy())
+    got = [int(t.item()) for t in vtot]
+    ok = True
+    for v, g in zip(kc["variants"], got):
+        o = OracleRegex(R.Regex(v["re"]))
+        seam = len(o.find_iter(stripped_one * 2)) - 2 * v["count"]
+        ok = ok and g == v["count"] * copies + seam * (copies - 1)
+    strip_ms = ctx.kernel_ms(strip_pass)
+    var_ms = ctx.kernel_ms(variant_pass)
+    sec = ctx.timed(step)
+    scanned = N + len(variants) * M
+    config = {"workload": "C3: regex-dna x%d (%d B raw, %d B stripped): strip find_iter + 9 variant find_iter"
+                          % (copies, N, M), "parallelism": "replicas%d" % ctx.world}
+    return ctx.line("haystack GB/s scanned, batched bytes::Regex::find_iter (regex-dna)",
+                    scanned * ctx.world / sec / 1e9, "GB/s", sec * 1e3, "u8",
+                    "examples/regexdna-input.txt replicated", config,
+                    strip_pass_ms=round(strip_ms, 3), strip_GBps=round(N / strip_ms / 1e6, 1),
+                    variant_passes_ms=round(var_ms, 3), variant_GBps=round(len(variants) * M / var_ms / 1e6, 1),
+                    strip_matches=nsp, variant_counts=got, known_answers_ok=ok)
+
+
+# ------------------------------------------------------------------ C4
+def run_c4(ctx):
+    import regex_amd as R
+    from regex_amd.workloads import C4_PATTERNS, log_lines_device
+    torch = ctx.torch
+    n = 10_000_000
+    buf, offs = log_lines_device(n, ctx.dev, seed=0x5EED0004 ^ ctx.rank)
+    rs = R.RegexSet(C4_PATTERNS)
+    out = torch.empty(n, dtype=torch.int64, device=ctx.dev)
+
+    def scan():
+        rs.matches_batch(buf, offsets=offs, out=out, stream=ctx.stream)
+
+    for _ in range(ctx.args.warmup):
+        scan()
+    torch.cuda.synchronize()
+    kms = ctx.kernel_ms(scan)
+    sec = ctx.timed(scan)
+    nb = int(offs[-1].item())
+    config = {"workload": "C4: RegexSet of %d patterns over %d log lines (%d B) per GPU" % (len(C4_PATTERNS), n, nb),
+              "parallelism": "dp%d" % ctx.world}
+    return ctx.line("haystack GB/s scanned, batched RegexSet::matches", nb * ctx.world / sec / 1e9, "GB/s",
+                    sec * 1e3, "u8", "synthetic log lines (seeded token stream)", config,
+                    lines_per_s=round(n * ctx.world / sec, 1), kernel_ms=round(kms, 4),
+                    roofline={"bound": "hbm", "achieved": round(nb / kms / 1e6, 1), "peak": HBM_PEAK_GBS,
+                              "unit": "GB/s", "frac": round(nb / kms / 1e6 / HBM_PEAK_GBS, 4), "traffic": None})
+
+
+# ------------------------------------------------------------------ C5
+def run_c5(ctx):
+    import regex_amd as R
+    from regex_amd.dist import gather_records
+    torch = ctx.torch
+    L = 16 << 30
+    g = torch.Generator(device=ctx.dev)
+    g.manual_seed(0x5EED0005 ^ ctx.rank)
+    hay = torch.empty(L + 16, dtype=torch.uint8, device=ctx.dev)
+    chunk = 1 << 30
+    for s in range(0, L, chunk):
+        v = torch.randint(0, 94, (min(chunk, L - s),), generator=g, device=ctx.dev, dtype=torch.int32)
+        v = v + 32
+        v = torch.where(v >= 64, v + 1, v)         # printable ASCII without '@'
+        hay[s:s + v.numel()] = v.to(torch.uint8)
+        del v
+    hay[L:] = 0
+    pos = L - (1 << 20) + 4096 * (ctx.rank + 1)
+    plant = b" user@example.org "
+    hay[pos:pos + len(plant)] = torch.frombuffer(bytearray(plant), dtype=torch.uint8).to(ctx.dev)
+    re = R.Regex(r"\w+@\w+\.\w+")
+    out = torch.empty((1, 2), dtype=torch.int64, device=ctx.dev)
+
+    def scan():
+        re.find_batch(hay, stride=L, length=L, count=1, out=out, stream=ctx.stream)
+
+    def step():
+        scan()
+        if ctx.world > 1:
+            rec = torch.cat([torch.tensor([[ctx.rank]], dtype=torch.int64, device=ctx.dev), out], dim=1)
+            gather_records(rec)
+
+    scan()
+    torch.cuda.synchronize()
+    got = [int(x) for x in out[0].cpu()]
+    kms = ctx.kernel_ms(scan)
+    sec = ctx.timed(step)
+    config = {"workload": "C5: find \\w+@\\w+\\.\\w+ over one 16 GiB haystack per GPU", "haystack_bytes": L,
+              "parallelism": "dp%d" % ctx.world}
+    return ctx.line("haystack GB/s scanned, bytes::Regex::find over 16 GiB shards", L * ctx.world / sec / 1e9,
+                    "GB/s", sec * 1e3, "u8", "synthetic (seeded printable ASCII without '@', one planted address)",
+                    config, match=got, expected=[pos + 1, pos + len(plant) - 1], kernel_ms=round(kms, 4),
+                    roofline={"bound": "hbm", "achieved": round(L / kms / 1e6, 1), "peak": HBM_PEAK_GBS,
+                              "unit": "GB/s", "frac": round(L / kms / 1e6 / HBM_PEAK_GBS, 4), "traffic": None})
+
+
+def main():
+    args = parse()
+    ctx = Ctx(args)
+    line = {"c2": run_c2, "c3": run_c3, "c4": run_c4, "c5": run_c5}[args.config](ctx)
+    if ctx.rank == 0:
+        print(json.dumps(line), flush=True)
+    ctx.close()
 
 
 if __name__ == "__main__":

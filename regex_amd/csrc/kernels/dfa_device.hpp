@@ -172,9 +172,16 @@ __device__ __forceinline__ uint64_t rev_scan(const RevDfaDev &r, const uint8_t *
 template <int MODE>
 __device__ __forceinline__ void fwd_range(LaneState &L, const FwdDfaDev &f, const uint8_t *lds, const uint8_t *base,
                                           uint64_t at, uint64_t end) {
-  while (!L.done && at < end && (((uintptr_t)(base + at)) & 15)) {
-    step1<MODE>(L, f, lds, base[at], at);
-    ++at;
+  // head: the bytes up to the next 16-byte boundary come from one aligned
+  // 16-byte load (the haystack buffer is readable up to its 16-byte-rounded
+  // end), not from a chain of byte loads
+  if (!L.done && at < end && (((uintptr_t)(base + at)) & 15)) {
+    const uintptr_t a = (uintptr_t)(base + at);
+    const uint4 v = *(const uint4 *)(a & ~(uintptr_t)15);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t j = (uint32_t)(a & 15);
+#pragma unroll 1
+    for (; j < 16 && at < end && !L.done; ++j, ++at) step1<MODE>(L, f, lds, (w[j >> 2] >> ((j & 3) * 8)) & 0xFF, at);
   }
   while (!L.done && at + 128 <= end) {
     const uint4 *p = (const uint4 *)(base + at);

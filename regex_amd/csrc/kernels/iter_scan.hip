@@ -33,7 +33,12 @@ namespace rure_amd {
 
 namespace {
 
-constexpr uint32_t kSlots = 4;  // speculative matches kept per unit
+// Speculative matches kept per unit: enough for one match per 32 bytes of
+// the unit (the emit pass copies them instead of re-running the unit).
+__host__ __device__ inline uint32_t unit_slots(uint64_t chunk) {
+  uint64_t s = chunk / 32;
+  return (uint32_t)(s < 4 ? 4 : s > 1024 ? 1024 : s);
+}
 
 enum : uint32_t {
   U_SPEC_CLEAN = 1,   // speculative exit is equivalent to a fresh start at the next unit
@@ -54,6 +59,7 @@ struct Unit {
 struct Geo {  // unit -> (haystack, chunk) for fixed-stride batches
   uint64_t nk;      // units per haystack
   uint64_t chunk;   // bytes per unit
+  uint32_t slots;   // speculative matches stored per unit
 };
 
 __device__ __forceinline__ void unit_bounds(const BatchDev &b, const Geo &g, uint64_t u, uint64_t *h,
@@ -154,9 +160,9 @@ __global__ __launch_bounds__(256) void iter_spec_kernel(BatchDev b, Geo g, uint6
     uint32_t n = 0;
     uint64_t s, e;
     while (it.next(f, r, lds, base, len, &s, &e)) {
-      if (n < kSlots) {
-        slots[(u * kSlots + n) * 2] = s;
-        slots[(u * kSlots + n) * 2 + 1] = e;
+      if (n < g.slots) {
+        slots[(u * g.slots + n) * 2] = s;
+        slots[(u * g.slots + n) * 2 + 1] = e;
       }
       ++n;
     }
@@ -288,10 +294,10 @@ __global__ __launch_bounds__(256) void iter_emit_kernel(BatchDev b, Geo g, uint6
     const uint64_t o0 = off[u], cnt = off[u + 1] - o0;
     if (cnt == 0 || o0 >= cap) continue;
     const Unit U = units[u];
-    if (!(U.flags & U_FIXED) && cnt <= kSlots) {
+    if (!(U.flags & U_FIXED) && cnt <= g.slots) {
       for (uint64_t i = 0; i < cnt && o0 + i < cap; ++i) {
-        out[2 * (o0 + i)] = slots[(u * kSlots + i) * 2];
-        out[2 * (o0 + i) + 1] = slots[(u * kSlots + i) * 2 + 1];
+        out[2 * (o0 + i)] = slots[(u * g.slots + i) * 2];
+        out[2 * (o0 + i) + 1] = slots[(u * g.slots + i) * 2 + 1];
       }
       continue;
     }
@@ -481,6 +487,7 @@ hipError_t long_scan_m(const BatchDev &b, const FwdDfaDev &f, const RevDfaDev &r
                        hipStream_t st, int cus) {
   Geo g;
   g.chunk = chunk;
+  g.slots = 0;
   const uint64_t span = b.length > b.start ? b.length - b.start : 0;
   g.nk = span <= chunk ? 1 : (span + chunk - 1) / chunk;
   const uint64_t nunits = b.count * g.nk;
@@ -530,7 +537,8 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
     if (b.offs) g.chunk = ~0ull >> 2;
     const uint64_t nunits = b.count * g.nk;
     // scratch: units, slots, counts (n + 1), offsets (n + 1), queue, qlen
-    const size_t sz_units = nunits * sizeof(Unit), sz_slots = nunits * kSlots * 16;
+    g.slots = b.offs ? 16 : unit_slots(std::min<uint64_t>(g.chunk, span ? span : 1));
+    const size_t sz_units = nunits * sizeof(Unit), sz_slots = nunits * (size_t)g.slots * 16;
     const size_t sz_counts = (nunits + 1) * 4, sz_off = (nunits + 1) * 8, sz_queue = nunits * 8;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t total = al(sz_units) + al(sz_slots) + al(sz_counts) + al(sz_off) + al(sz_queue) + 256;

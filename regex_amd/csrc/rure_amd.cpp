@@ -597,9 +597,9 @@ bool long_batch(const BatchDev &b, const DevTables &t, uint64_t *chunk) {
   if (b.offs || !t.has_dfa || t.quit_possible || b.count == 0) return false;
   const uint64_t span = b.length > b.start ? b.length - b.start : 0;
   if (span < (256u << 10) || b.count >= (uint64_t)t.cus * 128) return false;
-  const uint64_t target = (uint64_t)t.cus * 256;
+  const uint64_t target = (uint64_t)t.cus * 1024;  // 16 waves per CU: per-lane streams need latency hiding
   const uint64_t per_h = (target + b.count - 1) / b.count;
-  uint64_t c = std::max<uint64_t>(64u << 10, (span + per_h - 1) / per_h);
+  uint64_t c = std::max<uint64_t>(16u << 10, (span + per_h - 1) / per_h);
   *chunk = (c + 127) & ~(uint64_t)127;
   return true;
 }
@@ -1005,7 +1005,7 @@ int rure_amd_find_iter_batch(rure *re, const rure_amd_batch *batch, uint64_t *co
     uint64_t chunk = ~0ull >> 2;
     if (!b.offs && b.length > b.start && b.count) {
       const uint64_t span = b.length - b.start;
-      const uint64_t target = (uint64_t)t->cus * 256;  // lanes to fill the chip
+      const uint64_t target = (uint64_t)t->cus * 1024;  // 16 waves per CU
       const uint64_t per_h = (target + b.count - 1) / b.count;
       chunk = std::max<uint64_t>(4096, (span + per_h - 1) / per_h);
       chunk = (chunk + 63) & ~(uint64_t)63;
