@@ -147,23 +147,37 @@ __device__ __forceinline__ void chunk16s(LaneState &L, const FwdDfaDev &f, const
 
 // Reverse DFA over text[lo..me] (exec.rs:651-661, dfa.rs:768-866): longest
 // match, i.e. the smallest start.  Returns the start, NONE (reverse NoMatch)
-// or QUITMARK.
-__device__ __forceinline__ uint64_t rev_scan(const RevDfaDev &r, const uint8_t *base, uint64_t len, uint64_t lo,
-                                             uint64_t me) {
+// or QUITMARK.  Text bytes come from aligned 16-byte loads walked backwards;
+// with `rlds` (the reverse DFA's hot table staged in LDS, same layout as the
+// forward one) ordinary steps stay in LDS.
+__device__ __forceinline__ uint64_t rev_scan(const RevDfaDev &r, const uint8_t *rlds, const uint8_t *base,
+                                             uint64_t len, uint64_t lo, uint64_t me) {
   uint32_t s = r.start[rev_flag_index(base, lo, len, me)];
+  if (s == r.dead) return NONE;
+  const uint32_t hot = rlds ? r.hot : 0;
   uint64_t rs = NONE;
-  bool dead = s == r.dead;
   uint64_t a = me;
-  while (!dead && a > lo) {
-    --a;
-    s = r.full[(size_t)s * 256 + base[a]];
-    if (s >= r.n_normal) {
-      if (s < r.n_match_end) rs = a + 1;
-      else if (s == r.dead) dead = true;
-      else return QUITMARK;
+  while (a > lo) {
+    const uintptr_t p = (uintptr_t)(base + a - 1);
+    const uint4 v = *(const uint4 *)(p & ~(uintptr_t)15);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll 1
+    for (int j = (int)(p & 15); j >= 0 && a > lo; --j) {
+      const uint32_t b = (w[j >> 2] >> ((j & 3) * 8)) & 0xFF;
+      --a;
+      if (s < hot) {
+        const uint32_t t = rlds[s * kRow + b];
+        if (t != hot) { s = t; continue; }
+      }
+      s = r.full[(size_t)s * 256 + b];
+      if (s >= r.n_normal) {
+        if (s < r.n_match_end) rs = a + 1;
+        else if (s == r.dead) return rs;
+        else return QUITMARK;
+      }
     }
   }
-  if (!dead && r.eof[s]) rs = lo;
+  if (r.eof[s]) rs = lo;
   return rs;
 }
 
@@ -231,8 +245,8 @@ __device__ __forceinline__ void lane_start(LaneState &L, const FwdDfaDev &f, con
 // ExecNoSync::find_dfa_forward (exec.rs:632-662) for one lane: 0 = no
 // match, 1 = match (ms, me), 2 = the DFA quit.
 __device__ __forceinline__ int dfa_find(const FwdDfaDev &f, const RevDfaDev &r, const uint8_t *lds,
-                                        const uint8_t *base, uint64_t len, uint64_t at, uint64_t *ms,
-                                        uint64_t *me) {
+                                        const uint8_t *rlds, const uint8_t *base, uint64_t len, uint64_t at,
+                                        uint64_t *ms, uint64_t *me) {
   LaneState L;
   lane_start(L, f, base, len, at);
   fwd_run<MODE_FIND>(L, f, lds, base, len, at);
@@ -240,7 +254,7 @@ __device__ __forceinline__ int dfa_find(const FwdDfaDev &f, const RevDfaDev &r, 
   if (L.last == NONE) return 0;
   *me = L.last;
   if (L.last == at) { *ms = at; return 1; }  // exec.rs:647
-  const uint64_t rs = rev_scan(r, base, len, at, L.last);
+  const uint64_t rs = rev_scan(r, rlds, base, len, at, L.last);
   if (rs == QUITMARK) return 2;
   if (rs == NONE) return 0;  // exec.rs:656-660
   *ms = rs;
@@ -254,8 +268,8 @@ __device__ __forceinline__ int dfa_find(const FwdDfaDev &f, const RevDfaDev &r, 
 // the unrestricted search whenever that search's match starts before the cut,
 // and is "no match" otherwise.
 __device__ __forceinline__ int dfa_find_cut(const FwdDfaDev &f, const RevDfaDev &r, const uint8_t *lds,
-                                            const uint8_t *base, uint64_t len, uint64_t at, uint64_t cut,
-                                            uint64_t *ms, uint64_t *me) {
+                                            const uint8_t *rlds, const uint8_t *base, uint64_t len, uint64_t at,
+                                            uint64_t cut, uint64_t *ms, uint64_t *me) {
   LaneState L;
   lane_start(L, f, base, len, at);
   if (cut > at && cut - 1 <= len) {
@@ -273,7 +287,7 @@ __device__ __forceinline__ int dfa_find_cut(const FwdDfaDev &f, const RevDfaDev 
   if (L.last == NONE) return 0;
   *me = L.last;
   if (L.last == at) { *ms = at; return 1; }
-  const uint64_t rs = rev_scan(r, base, len, at, L.last);
+  const uint64_t rs = rev_scan(r, rlds, base, len, at, L.last);
   if (rs == QUITMARK) return 2;
   if (rs == NONE) return 0;
   *ms = rs;

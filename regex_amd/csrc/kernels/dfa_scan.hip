@@ -49,7 +49,7 @@ __device__ __forceinline__ void finish_lane(const LaneState &L, const RevDfaDev 
     if (me == lo) {
       ms = lo;                              // exec.rs:647
     } else {
-      const uint64_t rs = rev_scan(r, base, len, lo, me);
+      const uint64_t rs = rev_scan(r, nullptr, base, len, lo, me);
       if (rs == QUITMARK) ms = me = QUITMARK;
       else if (rs == NONE) ms = me = NONE;  // exec.rs:656-660: reverse NoMatch -> no match
       else ms = rs;

@@ -37,6 +37,9 @@ struct FwdDfaDev {
 };
 
 struct RevDfaDev {
+  const uint8_t *lds_image;   // hot table (same layout as FwdDfaDev::lds_image)
+  uint32_t lds_bytes;
+  uint32_t hot;
   const uint16_t *full;
   const uint8_t *eof;
   const uint16_t *start;

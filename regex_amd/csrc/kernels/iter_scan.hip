@@ -80,11 +80,11 @@ __device__ __forceinline__ void unit_bounds(const BatchDev &b, const Geo &g, uin
 
 // One step of re_trait.rs:197-221 (empty-match rule: next search at e + 1,
 // an empty match at the previous match end is skipped).
-__device__ int iter_next(const FwdDfaDev &f, const RevDfaDev &r, const uint8_t *lds, const uint8_t *base,
-                         uint64_t len, uint64_t cut, IterSt &st, uint64_t *s, uint64_t *e) {
+__device__ int iter_next(const FwdDfaDev &f, const RevDfaDev &r, const uint8_t *lds, const uint8_t *rlds,
+                         const uint8_t *base, uint64_t len, uint64_t cut, IterSt &st, uint64_t *s, uint64_t *e) {
   while (true) {
     if (st.p > len) return 0;
-    const int k = dfa_find_cut(f, r, lds, base, len, st.p, cut, s, e);
+    const int k = dfa_find_cut(f, r, lds, rlds, base, len, st.p, cut, s, e);
     if (k != 1) return k;
     if (*s == *e) {
       st.p = *e + 1;
@@ -110,8 +110,8 @@ struct UnitIter {
     ended = clean = quit = false;
   }
   // Returns true with the next owned match, false when the unit is finished.
-  __device__ bool next(const FwdDfaDev &f, const RevDfaDev &r, const uint8_t *lds, const uint8_t *base,
-                       uint64_t len, uint64_t *s, uint64_t *e) {
+  __device__ bool next(const FwdDfaDev &f, const RevDfaDev &r, const uint8_t *lds, const uint8_t *rlds,
+                       const uint8_t *base, uint64_t len, uint64_t *s, uint64_t *e) {
     if (ended) return false;
     if (st.p >= c1) {  // the previous match ran up to / past the cut
       ended = true;
@@ -120,7 +120,7 @@ struct UnitIter {
       return false;
     }
     const IterSt snap = st;
-    const int k = iter_next(f, r, lds, base, len, c1, st, s, e);
+    const int k = iter_next(f, r, lds, rlds, base, len, c1, st, s, e);
     if (k == 1 && *s < c1) return true;
     // no match starts before the cut (the search is cut-bounded, see
     // dfa_find_cut): a fresh search at the cut finds what the unrestricted
@@ -138,19 +138,26 @@ __device__ __forceinline__ bool exit_equiv(bool ca, const IterSt &a, bool cb, co
   return a.p == b.p && a.lm == b.lm;
 }
 
-template <bool LDS_TABLE>
-__device__ __forceinline__ const uint8_t *stage_table(const FwdDfaDev &f, uint8_t *lds) {
+// Dynamic LDS of the DFA kernels here: forward hot table, then the reverse
+// one (offset rev_lds_offset).
+__host__ __device__ inline uint32_t rev_lds_offset(uint32_t fwd_bytes) { return (fwd_bytes + 15) & ~15u; }
+inline size_t iter_lds_bytes(const FwdDfaDev &f, const RevDfaDev &r) { return rev_lds_offset(f.lds_bytes) + r.lds_bytes; }
+
+__device__ __forceinline__ const uint8_t *stage_tables(const FwdDfaDev &f, const RevDfaDev &r, uint8_t *lds) {
   for (uint32_t i = threadIdx.x * 16; i < f.lds_bytes; i += blockDim.x * 16)
     *(uint4 *)(lds + i) = *(const uint4 *)(f.lds_image + i);
+  uint8_t *rl = lds + rev_lds_offset(f.lds_bytes);
+  for (uint32_t i = threadIdx.x * 16; i < r.lds_bytes; i += blockDim.x * 16)
+    *(uint4 *)(rl + i) = *(const uint4 *)(r.lds_image + i);
   __syncthreads();
-  return lds;
+  return r.lds_bytes ? rl : nullptr;
 }
 
 // Pass 1: speculative iteration of every unit.
 __global__ __launch_bounds__(256) void iter_spec_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
                                                         Unit *units, uint64_t *slots, uint32_t *counts) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  stage_table<true>(f, lds);
+  const uint8_t *rlds = stage_tables(f, r, lds);
   for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < nunits; u += (uint64_t)gridDim.x * blockDim.x) {
     uint64_t h, len, c0, c1;
     const uint8_t *base;
@@ -159,7 +166,7 @@ __global__ __launch_bounds__(256) void iter_spec_kernel(BatchDev b, Geo g, uint6
     it.init({c0, NONE}, c1);
     uint32_t n = 0;
     uint64_t s, e;
-    while (it.next(f, r, lds, base, len, &s, &e)) {
+    while (it.next(f, r, lds, rlds, base, len, &s, &e)) {
       if (n < g.slots) {
         slots[(u * g.slots + n) * 2] = s;
         slots[(u * g.slots + n) * 2 + 1] = e;
@@ -181,7 +188,8 @@ __global__ __launch_bounds__(256) void iter_spec_kernel(BatchDev b, Geo g, uint6
 // iteration until both emit the same match.  Updates the unit's record and
 // count; returns true if the unit's exit changed.
 __device__ bool repair_unit(const BatchDev &b, const Geo &g, const FwdDfaDev &f, const RevDfaDev &r,
-                            const uint8_t *lds, uint64_t j, IterSt E, Unit *units, uint32_t *counts) {
+                            const uint8_t *lds, const uint8_t *rlds, uint64_t j, IterSt E, Unit *units,
+                            uint32_t *counts) {
   uint64_t h, len, c0, c1;
   const uint8_t *base;
   unit_bounds(b, g, j, &h, &base, &len, &c0, &c1);
@@ -190,18 +198,18 @@ __device__ bool repair_unit(const BatchDev &b, const Geo &g, const FwdDfaDev &f,
   F.init(E, c1);
   S.init({c0, NONE}, c1);
   uint64_t fs, fe, ss, se;
-  bool fm = F.next(f, r, lds, base, len, &fs, &fe);
-  bool sm = S.next(f, r, lds, base, len, &ss, &se);
+  bool fm = F.next(f, r, lds, rlds, base, len, &fs, &fe);
+  bool sm = S.next(f, r, lds, rlds, base, len, &ss, &se);
   uint32_t fcnt = 0, scnt = 0;
   bool synced = false;
   while (fm) {
     if (sm && fs == ss && fe == se) { synced = true; break; }
     if (!sm || fs < ss || (fs == ss && fe < se)) {
       ++fcnt;
-      fm = F.next(f, r, lds, base, len, &fs, &fe);
+      fm = F.next(f, r, lds, rlds, base, len, &fs, &fe);
     } else {
       ++scnt;
-      sm = S.next(f, r, lds, base, len, &ss, &se);
+      sm = S.next(f, r, lds, rlds, base, len, &ss, &se);
     }
   }
   U.entry = E;
@@ -228,13 +236,13 @@ __global__ __launch_bounds__(256) void iter_fix_kernel(BatchDev b, Geo g, uint64
                                                        Unit *units, uint32_t *counts, uint64_t *queue,
                                                        unsigned long long *qlen) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  stage_table<true>(f, lds);
+  const uint8_t *rlds = stage_tables(f, r, lds);
   for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u + 1 < nunits;
        u += (uint64_t)gridDim.x * blockDim.x) {
     if ((u + 1) % g.nk == 0) continue;  // last unit of its haystack
     const Unit U = units[u];
     if (U.flags & U_SPEC_CLEAN) continue;
-    if (repair_unit(b, g, f, r, lds, u + 1, U.spec_exit, units, counts)) {
+    if (repair_unit(b, g, f, r, lds, rlds, u + 1, U.spec_exit, units, counts)) {
       const unsigned long long q = atomicAdd(qlen, 1ull);
       queue[q] = u + 1;
     }
@@ -275,7 +283,7 @@ __global__ void iter_walk_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f
         units[u] = W;
         counts[u] = W.spec_count;
       } else {
-        repair_unit(b, g, f, r, f.lds_image /* unused: hot = 0 */, u, X.exit, units, counts);
+        repair_unit(b, g, f, r, f.lds_image /* unused: hot = 0 */, nullptr, u, X.exit, units, counts);
       }
       X = units[u];
       ++u;
@@ -289,7 +297,7 @@ __global__ __launch_bounds__(256) void iter_emit_kernel(BatchDev b, Geo g, uint6
                                                         const Unit *units, const uint64_t *slots, const uint64_t *off,
                                                         uint64_t *out, uint64_t cap) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  stage_table<true>(f, lds);
+  const uint8_t *rlds = stage_tables(f, r, lds);
   for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < nunits; u += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t o0 = off[u], cnt = off[u + 1] - o0;
     if (cnt == 0 || o0 >= cap) continue;
@@ -307,7 +315,7 @@ __global__ __launch_bounds__(256) void iter_emit_kernel(BatchDev b, Geo g, uint6
     UnitIter it;
     it.init(U.entry, c1);
     uint64_t s, e, i = 0;
-    while (i < cnt && it.next(f, r, lds, base, len, &s, &e)) {
+    while (i < cnt && it.next(f, r, lds, rlds, base, len, &s, &e)) {
       if (o0 + i < cap) {
         out[2 * (o0 + i)] = s;
         out[2 * (o0 + i) + 1] = e;
@@ -358,7 +366,7 @@ __global__ __launch_bounds__(64) void iter_wave_kernel(BatchDev b, FwdDfaDev f, 
       if (has_dfa) {
         uint64_t s0 = NONE, e0 = NONE;
         int k0 = 0;
-        if (lane == 0) k0 = dfa_find(fg, r, nullptr, base, len, p, &s0, &e0);
+        if (lane == 0) k0 = dfa_find(fg, r, nullptr, nullptr, base, len, p, &s0, &e0);
         k = __shfl(k0, 0);
         s = __shfl(s0, 0);
         e = __shfl(e0, 0);
@@ -409,6 +417,14 @@ hipError_t scan_counts(const uint32_t *counts, uint64_t *off, uint64_t n, hipStr
   return e != hipSuccess ? e : e2;
 }
 
+// Dynamic LDS beyond 64 KiB must be opted into per kernel (a gfx950
+// workgroup may use all 160 KiB).
+template <typename K>
+hipError_t allow_lds(K kernel, size_t bytes) {
+  if (bytes <= 64 * 1024) return hipSuccess;
+  return hipFuncSetAttribute((const void *)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
 int grid_cap(uint64_t items, int threads, int cus, int per_cu) {
   uint64_t g = (items + threads - 1) / threads;
   uint64_t cap = (uint64_t)cus * per_cu;
@@ -429,7 +445,7 @@ template <int MODE>
 __global__ __launch_bounds__(256) void long_scan_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
                                                         uint64_t *ures, unsigned long long *best) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  stage_table<true>(f, lds);
+  const uint8_t *rlds = stage_tables(f, r, lds);
   for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < nunits; u += (uint64_t)gridDim.x * blockDim.x) {
     uint64_t h, len, c0, c1;
     const uint8_t *base;
@@ -456,7 +472,7 @@ __global__ __launch_bounds__(256) void long_scan_kernel(BatchDev b, Geo g, uint6
       uint64_t ms, me = L.last;
       if (me == b.start) ms = me;  // exec.rs:647
       else {
-        const uint64_t rs = rev_scan(r, base, len, b.start, me);
+        const uint64_t rs = rev_scan(r, rlds, base, len, b.start, me);
         ms = rs;
         if (rs == NONE) me = NONE;  // reverse NoMatch -> the search has no match
       }
@@ -500,8 +516,9 @@ hipError_t long_scan_m(const BatchDev &b, const FwdDfaDev &f, const RevDfaDev &r
   unsigned long long *best = (unsigned long long *)(buf + al(sz_u));
   do {
     if ((e = hipMemsetAsync(best, MODE == MODE_ISMATCH ? 0 : 0xFF, sz_b, st)) != hipSuccess) break;
-    const int per_cu = std::max<int>(1, std::min<int>(8, (int)((160u * 1024u) / std::max<uint32_t>(f.lds_bytes, 1))));
-    hipLaunchKernelGGL(long_scan_kernel<MODE>, dim3(grid_cap(nunits, 256, cus, per_cu)), dim3(256), f.lds_bytes, st, b,
+    const int per_cu = std::max<int>(1, std::min<int>(8, (int)((160u * 1024u) / std::max<size_t>(iter_lds_bytes(f, r), 1))));
+    if ((e = allow_lds(long_scan_kernel<MODE>, iter_lds_bytes(f, r))) != hipSuccess) break;
+    hipLaunchKernelGGL(long_scan_kernel<MODE>, dim3(grid_cap(nunits, 256, cus, per_cu)), dim3(256), iter_lds_bytes(f, r), st, b,
                        g, nunits, f, r, ures, best);
     if ((e = hipGetLastError()) != hipSuccess) break;
     hipLaunchKernelGGL(long_finish_kernel<MODE>, dim3(grid_cap(b.count, 256, cus, 4)), dim3(256), 0, st, b.count,
@@ -550,25 +567,31 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
     uint64_t *off = (uint64_t *)(buf + al(sz_units) + al(sz_slots) + al(sz_counts));
     uint64_t *queue = (uint64_t *)(buf + al(sz_units) + al(sz_slots) + al(sz_counts) + al(sz_off));
     unsigned long long *qlen = (unsigned long long *)(buf + total - 256);
-    const int per_cu = std::max<int>(1, std::min<int>(8, (int)((160u * 1024u) / std::max<uint32_t>(f->lds_bytes, 1))));
+    const int per_cu = std::max<int>(1, std::min<int>(8, (int)((160u * 1024u) / std::max<size_t>(iter_lds_bytes(*f, r), 1))));
     const int grid = grid_cap(nunits, 256, cus, per_cu);
     do {
       if ((e = hipMemsetAsync(counts + nunits, 0, 4, st)) != hipSuccess) break;
       if ((e = hipMemsetAsync(qlen, 0, 8, st)) != hipSuccess) break;
-      hipLaunchKernelGGL(iter_spec_kernel, dim3(grid), dim3(256), f->lds_bytes, st, b, g, nunits, *f, r, units, slots,
+      const size_t lb = iter_lds_bytes(*f, r);
+      if ((e = allow_lds(iter_spec_kernel, lb)) != hipSuccess || (e = allow_lds(iter_fix_kernel, lb)) != hipSuccess ||
+          (e = allow_lds(iter_emit_kernel, lb)) != hipSuccess)
+        break;
+      hipLaunchKernelGGL(iter_spec_kernel, dim3(grid), dim3(256), iter_lds_bytes(*f, r), st, b, g, nunits, *f, r, units, slots,
                          counts);
       if ((e = hipGetLastError()) != hipSuccess) break;
       if (g.nk > 1) {
-        hipLaunchKernelGGL(iter_fix_kernel, dim3(grid), dim3(256), f->lds_bytes, st, b, g, nunits, *f, r, units,
+        hipLaunchKernelGGL(iter_fix_kernel, dim3(grid), dim3(256), iter_lds_bytes(*f, r), st, b, g, nunits, *f, r, units,
                            counts, queue, qlen);
         if ((e = hipGetLastError()) != hipSuccess) break;
         FwdDfaDev fw = *f;
         fw.hot = 0;
-        hipLaunchKernelGGL(iter_walk_kernel, dim3(1), dim3(64), 0, st, b, g, nunits, fw, r, units, counts, queue, qlen);
+        RevDfaDev rw = r;
+        rw.hot = 0;
+        hipLaunchKernelGGL(iter_walk_kernel, dim3(1), dim3(64), 0, st, b, g, nunits, fw, rw, units, counts, queue, qlen);
         if ((e = hipGetLastError()) != hipSuccess) break;
       }
       if ((e = scan_counts(counts, off, nunits, st)) != hipSuccess) break;
-      hipLaunchKernelGGL(iter_emit_kernel, dim3(grid), dim3(256), f->lds_bytes, st, b, g, nunits, *f, r, units, slots,
+      hipLaunchKernelGGL(iter_emit_kernel, dim3(grid), dim3(256), iter_lds_bytes(*f, r), st, b, g, nunits, *f, r, units, slots,
                          off, o.matches, o.cap);
       if ((e = hipGetLastError()) != hipSuccess) break;
       hipLaunchKernelGGL(iter_counts_kernel, dim3(grid_cap(b.count, 256, cus, 4)), dim3(256), 0, st, b.count, g.nk,

@@ -244,7 +244,7 @@ struct rure {
   bool built = false, dfa_ok = false;
   std::string dfa_err;
   DenseDfa dfwd, drev;
-  PackedFwd pf;
+  PackedFwd pf, pr;   // forward / reverse hot tables
   NfaTables nt;
   bool nfa_ok = false;
   std::map<int, DevTables> dev;
@@ -308,7 +308,7 @@ bool build_regex(rure *re) {
   DfaBuildLimits lim;
   std::string err;
   if (!build_dense_dfa(re->fwd, lim, &re->dfwd, &err) || !build_dense_dfa(re->rev, lim, &re->drev, &err) ||
-      !pack_forward(re->dfwd, &re->pf, &err) || re->drev.nstates > 65535) {
+      !pack_forward(re->dfwd, &re->pf, &err) || !pack_forward(re->drev, &re->pr, &err)) {
     re->dfa_err = err.empty() ? "reverse DFA too large" : err;
     re->dfa_ok = false;
     if (!re->nfa_ok) re->dfa_err += "; " + nerr;
@@ -406,7 +406,8 @@ DevTables *regex_device(rure *re, std::string *err) {
   t.cus = device_cus(d);
   NfaOffsets no{};
   if (re->nfa_ok) no = add_nfa(b, re->nt);
-  size_t o_lds = 0, o_lds_s = 0, o_full = 0, o_eof = 0, o_start = 0, o_rfull = 0, o_reof = 0, o_rstart = 0;
+  size_t o_lds = 0, o_lds_s = 0, o_full = 0, o_eof = 0, o_start = 0, o_rfull = 0, o_reof = 0, o_rstart = 0,
+         o_rlds = 0;
   const PackedFwd &pf = re->pf;
   const DenseDfa &rv = re->drev;
   if (re->dfa_ok) {
@@ -421,6 +422,7 @@ DevTables *regex_device(rure *re, std::string *err) {
     o_rfull = b.add(rfull.data(), rfull.size() * 2);
     o_reof = b.add(rv.eof_match.data(), rv.eof_match.size());
     o_rstart = b.add(rstart.data(), 256);
+    o_rlds = b.add(re->pr.lds.data(), re->pr.lds.size());
   }
   if (!upload_blob(b, &t, err)) return nullptr;
   uint8_t *base = (uint8_t *)t.blob;
@@ -446,6 +448,9 @@ DevTables *regex_device(rure *re, std::string *err) {
     t.f.n_match_end = fw.n_match_end;
     t.f.dead = fw.dead;
     t.f.quit = fw.quit < 0 ? 0xFFFFFFFFu : (uint32_t)fw.quit;
+    t.r.lds_image = base + o_rlds;
+    t.r.lds_bytes = (uint32_t)re->pr.lds.size();
+    t.r.hot = re->pr.hot;
     t.r.full = (const uint16_t *)(base + o_rfull);
     t.r.eof = base + o_reof;
     t.r.start = (const uint16_t *)(base + o_rstart);
