@@ -135,6 +135,11 @@ def roofline(achieved_gbs, kernel_ms, b_alg, config):
     return r
 
 
+def _short_kernel(name):
+    import re
+    return re.sub(r"\((rure_amd::BatchDev|unsigned|int|long|void\*).*$", "", name).replace("void ", "")
+
+
 def profiled_traffic(config, b_alg):
     """HBM bytes per launch of the scan kernel from the committed rocprofv3
     PMC pass of this same command (profiles/<tag>_summary.json, written by
@@ -158,7 +163,7 @@ def profiled_traffic(config, b_alg):
     d = best[2]
     return {"bytes": int(d["hbm_read_bytes_per_launch"]),
             "source": "%s (rocprofv3 --pmc FETCH_SIZE, kernel %s, %.3fx algorithmic)" %
-                      (os.path.relpath(best[1], ROOT), d["kernel"].split("(")[0].replace("void ", ""),
+                      (os.path.relpath(best[1], ROOT), _short_kernel(d["kernel"]),
                        d["hbm_read_bytes_per_launch"] / b_alg)}
 
 
@@ -346,9 +351,8 @@ def run_c4(ctx):
               "parallelism": "dp%d" % ctx.world}
     return ctx.line("haystack GB/s scanned, batched RegexSet::matches", nb * ctx.world / sec / 1e9, "GB/s",
                     sec * 1e3, "u8", "synthetic log lines (seeded token stream)", config,
-                    lines_per_s=round(n * ctx.world / sec, 1), kernel_ms=round(kms, 4),
-                    roofline={"bound": "hbm", "achieved": round(nb / kms / 1e6, 1), "peak": HBM_PEAK_GBS,
-                              "unit": "GB/s", "frac": round(nb / kms / 1e6 / HBM_PEAK_GBS, 4), "traffic": None})
+                    lines_per_s=round(n * ctx.world / sec, 1),
+                    roofline=roofline(nb / kms / 1e6, kms, nb, config))
 
 
 # ------------------------------------------------------------------ C5
@@ -392,9 +396,8 @@ def run_c5(ctx):
               "parallelism": "dp%d" % ctx.world}
     return ctx.line("haystack GB/s scanned, bytes::Regex::find over 16 GiB shards", L * ctx.world / sec / 1e9,
                     "GB/s", sec * 1e3, "u8", "synthetic (seeded printable ASCII without '@', one planted address)",
-                    config, match=got, expected=[pos + 1, pos + len(plant) - 1], kernel_ms=round(kms, 4),
-                    roofline={"bound": "hbm", "achieved": round(L / kms / 1e6, 1), "peak": HBM_PEAK_GBS,
-                              "unit": "GB/s", "frac": round(L / kms / 1e6 / HBM_PEAK_GBS, 4), "traffic": None})
+                    config, match=got, expected=[pos + 1, pos + len(plant) - 1],
+                    roofline=roofline(L / kms / 1e6, kms, L, config))
 
 
 def main():

@@ -1,15 +1,22 @@
 #!/usr/bin/env python3
 """Summarise a rocprofv3 run of bench.py (tools/gpu_profile.sh) into
-profiles/<tag>_summary.json: kernel-trace average duration of the scan kernel
-and FETCH_SIZE-derived HBM read bytes per launch (x1024 B per KB unit, x2
-gfx950 wide-read correction, MI355X_MICROARCH.md §HBM)."""
+profiles/<tag>_summary.json: kernel-trace durations of the library's
+kernels (the dominant one first) and the FETCH_SIZE-derived HBM read bytes
+per launch of the dominant kernel (x1024 B per KB unit, x2 gfx950
+wide-read correction, MI355X_MICROARCH.md §HBM)."""
 import csv
 import json
 import os
+import re
 import sys
 
 
-def main(tag, kernel_substr="rure_amd::dfa_"):
+def short(name):
+    """Kernel name without its parameter list."""
+    return re.sub(r"\((rure_amd::BatchDev|unsigned|int|long|void\*).*$", "", name)
+
+
+def main(tag, kernel_substr="rure_amd::"):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     src = os.path.join(root, "gpurun_out", tag)
     stats = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
@@ -18,6 +25,8 @@ def main(tag, kernel_substr="rure_amd::dfa_"):
     fetch = [float(r["Counter_Value"]) for r in pmc
              if ks and r["Kernel_Name"] == ks[0]["Name"] and r["Counter_Name"] == "FETCH_SIZE"]
     bench = json.loads(open(os.path.join(src, "bench_trace.json")).read().strip().splitlines()[-1])
+    roof = bench.get("roofline", {})
+    alg = roof.get("alg_bytes_per_launch")
     out = {
         "tag": tag,
         "kernel": ks[0]["Name"] if ks else None,
@@ -27,14 +36,17 @@ def main(tag, kernel_substr="rure_amd::dfa_"):
         "max_ns": float(ks[0]["MaxNs"]) if ks else None,
         "fetch_size_kb_avg": sum(fetch) / len(fetch) if fetch else None,
         "hbm_read_bytes_per_launch": (sum(fetch) / len(fetch)) * 1024 * 2 if fetch else None,
-        "bench_kernel_ms_events": bench["roofline"]["kernel_ms"],
-        "alg_bytes_per_launch": bench["roofline"]["alg_bytes_per_launch"],
+        "bench_kernel_ms_events": roof.get("kernel_ms", bench.get("kernel_ms")),
+        "alg_bytes_per_launch": alg,
         "bench_value_GBps": bench["value"],
         "bench_config": bench["config"],
         "note": "FETCH_SIZE (KB) x 1024 x 2: gfx950 reports half of wide streaming reads",
+        "library_kernels": [{"name": short(r["Name"]), "calls": int(r["Calls"]),
+                             "avg_ns": float(r["AverageNs"]), "total_ns": float(r["TotalDurationNs"])}
+                            for r in ks[:8]],
     }
-    if out["hbm_read_bytes_per_launch"]:
-        out["traffic_over_alg"] = out["hbm_read_bytes_per_launch"] / out["alg_bytes_per_launch"]
+    if out["hbm_read_bytes_per_launch"] and alg:
+        out["traffic_over_alg"] = out["hbm_read_bytes_per_launch"] / alg
     os.makedirs(os.path.join(root, "profiles"), exist_ok=True)
     with open(os.path.join(root, "profiles", tag + "_summary.json"), "w") as f:
         json.dump(out, f, indent=1)
