@@ -43,9 +43,6 @@ struct LaneState {
 };
 
 static constexpr uint64_t NONE = ~0ull;
-// LDS fast-table row pitch: 256 bytes + one bank, so that lanes in different
-// states that read the same byte value land in different LDS banks.
-static constexpr uint32_t kRow = 260;
 static constexpr uint64_t QUITMARK = ~0ull - 1;
 
 // Full-table step for one byte at haystack position `pos` (careful path).

@@ -94,11 +94,12 @@ __global__ __launch_bounds__(256) void dfa_fwd_kernel(BatchDev bt, FwdDfaDev f, 
 // swizzled so the ds_read_b128 of 16 lanes hit 16 distinct bank groups), and
 // each lane then steps its own row through the DFA.  The next tile's loads
 // are in flight while the current one is scanned.
-static constexpr int kTileTab = 64 * 260 + 256;   // largest LDS fast table of the tile path (hot + 1 <= 64 rows)
-static constexpr int kTileTabSmall = 16 * 260 + 96; // hot + 1 <= 16 rows
+static constexpr int kTileTab = 64 * kRow + 256;   // largest LDS fast table of the tile path (hot + 1 <= 64 rows)
+static constexpr int kTileTabSmall = 16 * kRow + 96; // hot + 1 <= 16 rows
 
 template <int MODE, int TAB, int STRIDE>
-__global__ __launch_bounds__(256) void dfa_fwd_tile_kernel(BatchDev bt, FwdDfaDev f, RevDfaDev r, void *out) {
+__global__ __launch_bounds__(256) void dfa_fwd_tile_kernel(BatchDev bt, FwdDfaDev f, RevDfaDev r, void *out,
+                                                           uint64_t gscatter) {
   __shared__ __attribute__((aligned(16))) uint8_t tab[TAB];
   const uint8_t *img = STRIDE == 1 ? f.lds_image : f.lds_image_s;
   const uint32_t img_bytes = STRIDE == 1 ? f.lds_bytes : f.lds_bytes_s;
@@ -113,7 +114,13 @@ __global__ __launch_bounds__(256) void dfa_fwd_tile_kernel(BatchDev bt, FwdDfaDe
   const uint64_t L128 = L & ~(uint64_t)127;
   const uint64_t nwaves = (uint64_t)gridDim.x * 4;
   const int src_h = lane >> 3, src_seg = lane & 7;
-  for (uint64_t g = (uint64_t)blockIdx.x * 4 + w; g * 64 < n; g += nwaves) {
+  const uint64_t ngroups = (n + 63) / 64;
+  for (uint64_t gi = (uint64_t)blockIdx.x * 4 + w; gi < ngroups; gi += nwaves) {
+    // Scattered group order: waves that run at the same time work on
+    // haystack groups far apart in memory.  With power-of-two strides,
+    // neighbouring groups progressing in lockstep concentrate the chip's
+    // requests on a few HBM channels (tools/tile_diag.hip: 4.75 -> 5.38 TB/s).
+    const uint64_t g = gscatter ? (gi * gscatter) % ngroups : gi;
     const uint64_t h = g * 64 + lane;
     const bool valid = h < n;
     const uint8_t *base = bt.hay + (valid ? h : 0) * S;
@@ -274,10 +281,17 @@ template <int MODE, int STRIDE>
 static hipError_t launch_tile_s(const BatchDev &b, const FwdDfaDev &f, const RevDfaDev &r, void *out, hipStream_t st,
                                 int grid) {
   const uint32_t bytes = STRIDE == 1 ? f.lds_bytes : f.lds_bytes_s;
+  // group scatter multiplier: a prime, coprime with the group count
+  const uint64_t ngroups = (b.count + 63) / 64;
+  uint64_t mul = 40503;
+  auto gcd = [](uint64_t a, uint64_t c) { while (c) { uint64_t t = a % c; a = c; c = t; } return a; };
+  while (ngroups > 1 && gcd(mul, ngroups) != 1) mul += 2;
+  if (ngroups <= 1) mul = 0;
   if (bytes <= (uint32_t)kTileTabSmall)
-    hipLaunchKernelGGL((dfa_fwd_tile_kernel<MODE, kTileTabSmall, STRIDE>), dim3(grid), dim3(256), 0, st, b, f, r, out);
+    hipLaunchKernelGGL((dfa_fwd_tile_kernel<MODE, kTileTabSmall, STRIDE>), dim3(grid), dim3(256), 0, st, b, f, r, out,
+                       mul);
   else
-    hipLaunchKernelGGL((dfa_fwd_tile_kernel<MODE, kTileTab, STRIDE>), dim3(grid), dim3(256), 0, st, b, f, r, out);
+    hipLaunchKernelGGL((dfa_fwd_tile_kernel<MODE, kTileTab, STRIDE>), dim3(grid), dim3(256), 0, st, b, f, r, out, mul);
   return hipGetLastError();
 }
 

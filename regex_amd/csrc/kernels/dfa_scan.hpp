@@ -5,6 +5,13 @@
 
 namespace rure_amd {
 
+// Row pitch of the LDS hot tables (bytes).  256 columns + 48 bytes: row s
+// starts 12 banks after row s-1, so lanes in the few dominant states reading
+// random printable bytes (24 dwords of a row) collide least; a bank-conflict
+// model over the C2 haystacks gives 4.15 LDS cycles per lookup
+// wave-instruction at 304 vs 4.67 at 260 and 4.86 at 256 (2 = conflict free).
+constexpr uint32_t kRow = 304;
+
 enum { MODE_FIND = 0, MODE_ISMATCH = 1, MODE_SHORTEST = 2 };
 
 struct BatchDev {

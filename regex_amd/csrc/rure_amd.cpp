@@ -154,7 +154,6 @@ bool pack_forward(const DenseDfa &d, PackedFwd *p, std::string *err) {
   int cap = need + 1 <= 16 ? 15 : need + 1 <= 64 ? 63 : 255;
   uint32_t hot = (uint32_t)std::min(d.n_normal, cap);
   p->hot = hot;
-  const size_t kRow = 260;  // row pitch of the LDS table (kernels: kRow)
   size_t lds_bytes = ((size_t)(hot + 1) * kRow + 15) & ~(size_t)15;
   p->lds.assign(lds_bytes, 0);
   for (uint32_t s = 0; s <= hot; ++s)
