@@ -594,6 +594,15 @@ const FwdDfaDev *iter_device(rure *re, const DevTables &t, std::string *err) {
 
 // The engine dispatch of exec.rs:473-514 / 382-420 for a batch: DFA, and the
 // Pike VM where the DFA quits (or instead of it when it does not fit).
+// Chunk sizes are an odd number of 128-byte lines: lanes that scan chunks in
+// lockstep then read addresses with different low bits, instead of hammering
+// the few HBM channels a power-of-two chunk would map them all to.
+uint64_t odd_lines(uint64_t bytes) {
+  uint64_t lines = (bytes + 127) / 128;
+  if ((lines & 1) == 0) ++lines;
+  return lines * 128;
+}
+
 // Few long haystacks: one lane per haystack would leave the chip idle, so the
 // search is split into chunks (launch_long_scan).  Needs a DFA that cannot
 // quit (the Pike VM fallback is per haystack).
@@ -604,7 +613,7 @@ bool long_batch(const BatchDev &b, const DevTables &t, uint64_t *chunk) {
   const uint64_t target = (uint64_t)t.cus * 1024;  // 16 waves per CU: per-lane streams need latency hiding
   const uint64_t per_h = (target + b.count - 1) / b.count;
   uint64_t c = std::max<uint64_t>(16u << 10, (span + per_h - 1) / per_h);
-  *chunk = (c + 127) & ~(uint64_t)127;
+  *chunk = odd_lines(c);
   return true;
 }
 
@@ -1011,8 +1020,7 @@ int rure_amd_find_iter_batch(rure *re, const rure_amd_batch *batch, uint64_t *co
       const uint64_t span = b.length - b.start;
       const uint64_t target = (uint64_t)t->cus * 1024;  // 16 waves per CU
       const uint64_t per_h = (target + b.count - 1) / b.count;
-      chunk = std::max<uint64_t>(4096, (span + per_h - 1) / per_h);
-      chunk = (chunk + 63) & ~(uint64_t)63;
+      chunk = odd_lines(std::max<uint64_t>(4096, (span + per_h - 1) / per_h));
     }
     e = launch_find_iter(b, fi, t->r, &t->n, true, chunk, o, (hipStream_t)stream, t->cus);
   } else {
