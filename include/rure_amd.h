@@ -176,6 +176,16 @@ int rure_amd_dfa_export(rure *re, int which, uint32_t *trans, uint8_t *eof_match
  * end of the text / reported on entering the state), start = 128 u32. */
 int rure_amd_set_dfa_export(rure_set *re, uint32_t *trans, uint64_t *eof_mask, uint64_t *now_mask,
                             uint32_t *start);
+/* Core form of a large set's DFA (used by the set kernel when the set DFA has
+ * more than 255 ordinary or match-reporting states): sizes in info; lds =
+ * 256-byte class map + (hot + 1) x K u16 entries (next core << 6 | output
+ * code), gcore / gout = ncores x K next core (u16) / reported patterns (u64),
+ * eof = ncores u64, start = 128 u16.  RURE_AMD_ERR_DFA if not in core form. */
+typedef struct rure_amd_core_info {
+  uint32_t K, ncores, hot, dead, quit, lds_bytes;
+} rure_amd_core_info;
+int rure_amd_set_core_export(rure_set *re, rure_amd_core_info *info, uint8_t *lds, uint16_t *gcore,
+                             uint64_t *gout, uint64_t *eof, uint16_t *start);
 /* strip[s] (states u32) of the find_iter forward DFA: s without the `.*?` prefix. */
 int rure_amd_dfa_strip_export(rure *re, uint32_t *strip);
 

@@ -320,6 +320,25 @@ class RegexSet(object):
     def uses_dfa(self):
         return N.rure_amd_set_uses_dfa(self._set) == 1
 
+    def core_tables(self):
+        """Core form of a large set's DFA (None if the set uses the byte-row
+        kernel): (info, class map, hot table, gcore, gout, eof, start)."""
+        import numpy as np
+        info = N.CoreInfo()
+        if N.rure_amd_set_core_export(self._set, ctypes.byref(info), None, None, None, None, None) != N.OK:
+            return None
+        d = {k: getattr(info, k) for k, _ in N.CoreInfo._fields_}
+        lds = np.zeros(info.lds_bytes, dtype=np.uint8)
+        gcore = np.zeros(info.ncores * info.K, dtype=np.uint16)
+        gout = np.zeros(info.ncores * info.K, dtype=np.uint64)
+        eof = np.zeros(info.ncores, dtype=np.uint64)
+        start = np.zeros(128, dtype=np.uint16)
+        _check(N.rure_amd_set_core_export(self._set, ctypes.byref(info), lds.ctypes.data, gcore.ctypes.data,
+                                          gout.ctypes.data, eof.ctypes.data, start.ctypes.data), "set_core_export")
+        K, hot = info.K, info.hot
+        hot_tab = lds[256:256 + (hot + 1) * K * 2].view(np.uint16).reshape(hot + 1, K)
+        return d, lds[:256].copy(), hot_tab, gcore.reshape(-1, K), gout.reshape(-1, K), eof, start
+
     def dfa_tables(self):
         """Set DFA: (info, trans (states, 256), eof_mask, now_mask, start)."""
         import numpy as np

@@ -63,6 +63,10 @@ class NfaInfo(ctypes.Structure):
         "leaves", "closures", "entries", "root", "nmatch", "anchored", "looks", "unicode_wb")]
 
 
+class CoreInfo(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint32) for n in ("K", "ncores", "hot", "dead", "quit", "lds_bytes")]
+
+
 def _sig(name, res, *args):
     f = getattr(lib, name)
     f.restype = res
@@ -112,6 +116,8 @@ rure_amd_dfa_export = _sig("rure_amd_dfa_export", ctypes.c_int, VP, ctypes.c_int
 rure_amd_nfa_export = _sig("rure_amd_nfa_export", ctypes.c_int, VP, ctypes.POINTER(NfaInfo), VP, VP, VP)
 rure_amd_set_nfa_export = _sig("rure_amd_set_nfa_export", ctypes.c_int, VP, ctypes.POINTER(NfaInfo), VP, VP, VP)
 rure_amd_set_dfa_export = _sig("rure_amd_set_dfa_export", ctypes.c_int, VP, VP, VP, VP, VP)
+rure_amd_set_core_export = _sig("rure_amd_set_core_export", ctypes.c_int, VP, ctypes.POINTER(CoreInfo), VP, VP,
+                                VP, VP, VP)
 rure_amd_dfa_strip_export = _sig("rure_amd_dfa_strip_export", ctypes.c_int, VP, VP)
 rure_amd_find_iter_batch = _sig("rure_amd_find_iter_batch", ctypes.c_int, VP, ctypes.POINTER(RureBatch), VP, VP,
                                 c_size, VP, VP)

@@ -269,6 +269,175 @@ __global__ __launch_bounds__(256) void dfa_set_kernel(BatchDev bt, SetDfaDev f, 
   }
 }
 
+// ------------------------------------------------------- sets, core form
+// Large sets (C4: 64 patterns, 6511 states): the states that differ only in
+// the matches their entry reports collapse into 1947 "cores", and byte
+// columns into K classes, so the table of the ~1000 most reachable cores fits
+// in one CU's LDS as u16 entries (next core + output code).  Each byte costs a
+// class lookup (independent of the state) and one dependent u16 lookup; the
+// output codes of a 16-byte chunk are collected in a 64-bit bag with one
+// shift + or per byte and merged after the chunk.  A chunk that leaves the
+// hot cores or meets a code that needs the global table is redone from its
+// first byte against the global tables (outputs are ORed, so redoing is
+// harmless).
+__device__ __forceinline__ bool core_careful(uint32_t &c, uint64_t &mask, const SetCoreDev &f, uint32_t k,
+                                             bool &quit) {
+  const size_t i = (size_t)c * f.K + k;
+  mask |= f.gout[i];
+  c = f.gcore[i];
+  if (c == f.dead) return true;
+  if (c == f.quit) { quit = true; return true; }
+  return (mask & f.all) == f.all;
+}
+
+__device__ __forceinline__ bool core_step1(uint32_t &c, uint64_t &mask, const SetCoreDev &f, const uint8_t *cls,
+                                           const uint16_t *T, uint32_t b, bool &quit) {
+  const uint32_t k = cls[b];
+  if (c < f.hot) {
+    const uint32_t e = T[c * f.K + k];
+    const uint32_t code = e & 63;
+    if ((e >> 6) != f.hot && code != 63) {
+      if (code) mask |= 1ull << (code - 1);
+      c = e >> 6;
+      if (c == f.dead) return true;
+      if (c == f.quit) { quit = true; return true; }
+      return (mask & f.all) == f.all;
+    }
+  }
+  return core_careful(c, mask, f, k, quit);
+}
+
+__device__ __forceinline__ bool core_chunk16(uint32_t &c, uint64_t &mask, uint64_t &pend, const SetCoreDev &f,
+                                             const uint8_t *cls, const uint16_t *T, uint4 v, bool &quit) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t k[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) k[j] = cls[(w[j >> 2] >> ((j & 3) * 8)) & 0xFF];
+  if (c < f.hot) {
+    uint32_t t = c;
+    uint64_t bag = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const uint32_t e = T[t * f.K + k[j]];
+      const uint32_t code = e & 63;
+      bag |= 1ull << code;
+      // code 63: the report is not a single pattern < 62; its mask comes from
+      // the global table, loaded now and merged at the end of the haystack
+      // (the load retires before the next data load is waited for)
+      if (code == 63) pend |= f.gout[(size_t)t * f.K + k[j]];
+      t = e >> 6;
+    }
+    if (t != f.hot) {
+      mask |= (bag >> 1) & 0x3FFFFFFFFFFFFFFFull;
+      c = t;
+      if (c == f.dead) return true;
+      if (c == f.quit) { quit = true; return true; }
+      return (mask & f.all) == f.all;
+    }
+  }
+#pragma unroll 1
+  for (int j = 0; j < 16; ++j)
+    if (core_careful(c, mask, f, k[j], quit)) return true;
+  return false;
+}
+
+template <bool STRIDED>
+__global__ __launch_bounds__(1024) void set_core_kernel(BatchDev bt, SetCoreDev f, uint64_t *out) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  for (uint32_t i = threadIdx.x * 16; i < f.lds_bytes; i += blockDim.x * 16)
+    *(uint4 *)(lds + i) = *(const uint4 *)(f.lds_image + i);
+  __syncthreads();
+  const uint8_t *cls = lds;
+  const uint16_t *T = (const uint16_t *)(lds + 256);
+  const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; h < bt.count; h += nthreads) {
+    const uint8_t *base;
+    uint64_t len;
+    if (STRIDED) { base = bt.hay + h * bt.stride; len = bt.length; }
+    else { const uint64_t o0 = bt.offs[h], o1 = bt.offs[h + 1]; base = bt.hay + o0; len = o1 - o0; }
+    uint64_t at = bt.start, mask = 0, pend = 0;
+    bool quit = false, done;
+    uint32_t c;
+    if (at > len) { c = f.dead; done = true; }
+    else { c = f.start[fwd_flag_index(base, len, at)]; done = c == f.dead; }
+    if (!done && at < len && (((uintptr_t)(base + at)) & 15)) {  // head from one aligned block
+      const uintptr_t a = (uintptr_t)(base + at);
+      const uint4 v = *(const uint4 *)(a & ~(uintptr_t)15);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll 1
+      for (uint32_t j = (uint32_t)(a & 15); j < 16 && at < len && !done; ++j, ++at)
+        done = core_step1(c, mask, f, cls, T, (w[j >> 2] >> ((j & 3) * 8)) & 0xFF, quit);
+    }
+    while (!done && at + 16 <= len) {
+      done = core_chunk16(c, mask, pend, f, cls, T, *(const uint4 *)(base + at), quit);
+      at += 16;
+    }
+    if (!done && at < len) {  // tail: at is 16-byte aligned here
+      const uint4 v = *(const uint4 *)(base + at);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll 1
+      for (uint32_t j = 0; at < len && !done; ++j, ++at)
+        done = core_step1(c, mask, f, cls, T, (w[j >> 2] >> ((j & 3) * 8)) & 0xFF, quit);
+    }
+    uint64_t m;
+    if (quit) m = QUITMARK;
+    else if (done) m = mask | pend;
+    else m = mask | pend | f.eof[c];
+    out[h] = m;
+  }
+}
+
+// Visit counts per core over a sample of the batch (global tables only): the
+// host then re-ranks the cores so the LDS table holds the ones this data
+// visits — the adaptive counterpart of the reference's lazily filled cache
+// (dfa.rs:1154-1244), with identical results whatever the ranking.
+__global__ __launch_bounds__(256) void core_profile_kernel(BatchDev bt, SetCoreDev f, uint64_t count,
+                                                           unsigned int *visits) {
+  const uint8_t *cls = f.lds_image;  // class map = first 256 bytes of the image
+  for (uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; h < count; h += (uint64_t)gridDim.x * blockDim.x) {
+    const uint8_t *base;
+    uint64_t len;
+    if (bt.offs) { const uint64_t o0 = bt.offs[h], o1 = bt.offs[h + 1]; base = bt.hay + o0; len = o1 - o0; }
+    else { base = bt.hay + h * bt.stride; len = bt.length; }
+    if (bt.start > len) continue;
+    uint32_t c = f.start[fwd_flag_index(base, len, bt.start)];
+    const uint64_t end = len < bt.start + 4096 ? len : bt.start + 4096;
+    for (uint64_t at = bt.start; at < end && c != f.dead && c != f.quit; ++at) {
+      c = f.gcore[(size_t)c * f.K + cls[base[at]]];
+      atomicAdd(&visits[c], 1u);
+    }
+  }
+}
+
+hipError_t launch_core_profile(const BatchDev &b, const SetCoreDev &f, uint64_t count, unsigned int *visits,
+                               hipStream_t st, int cus) {
+  const uint64_t blocks = (count + 255) / 256;
+  const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)cus * 4));
+  hipLaunchKernelGGL(core_profile_kernel, dim3(grid), dim3(256), 0, st, b, f, count, visits);
+  return hipGetLastError();
+}
+
+hipError_t launch_set_cores(const BatchDev &b, const SetCoreDev &f, uint64_t *out, hipStream_t st, int cus) {
+  const int per_cu = f.lds_bytes > 80 * 1024 ? 1 : 2;
+  const uint64_t blocks = (b.count + 1023) / 1024;
+  const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)cus * per_cu));
+  hipError_t e;
+  if (b.offs) {
+    if (f.lds_bytes > 64 * 1024 &&
+        (e = hipFuncSetAttribute((const void *)set_core_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)f.lds_bytes)) != hipSuccess)
+      return e;
+    hipLaunchKernelGGL((set_core_kernel<false>), dim3(grid), dim3(1024), f.lds_bytes, st, b, f, out);
+  } else {
+    if (f.lds_bytes > 64 * 1024 &&
+        (e = hipFuncSetAttribute((const void *)set_core_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)f.lds_bytes)) != hipSuccess)
+      return e;
+    hipLaunchKernelGGL((set_core_kernel<true>), dim3(grid), dim3(1024), f.lds_bytes, st, b, f, out);
+  }
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ launch
 template <int MODE, bool STRIDED>
 static hipError_t launch_fwd(const BatchDev &b, const FwdDfaDev &f, const RevDfaDev &r, void *out,

@@ -67,6 +67,27 @@ struct SetDfaDev {
   uint32_t n_normal, n_match_end, dead, quit;
 };
 
+// Set DFA in "core" form for large sets (host: build_set_cores): states that
+// differ only in the matches their entry reports share a core; a transition
+// (core, byte class) carries the next core and an output code.  Entries of
+// the LDS table (hot cores [0, hot), sentinel row `hot`): bits 15..6 = next
+// core (`hot` = leaves the LDS set), bits 5..0 = output code (0 none, 1..62 =
+// pattern code-1 matched, 63 = consult gout).  Global tables cover all cores.
+struct SetCoreDev {
+  const uint8_t *lds_image;   // 256-byte class map, then (hot + 1) x K u16 entries
+  uint32_t lds_bytes;
+  uint32_t hot, K;
+  const uint16_t *gcore;      // ncores x K next core
+  const uint64_t *gout;       // ncores x K matches reported by the transition
+  const uint64_t *eof;        // ncores: matches at the end of the text
+  const uint16_t *start;      // 128 start cores
+  uint64_t all;
+  uint32_t dead, quit;        // quit = 0xFFFFFFFF if none
+};
+hipError_t launch_set_cores(const BatchDev &b, const SetCoreDev &f, uint64_t *out, hipStream_t st, int cus);
+hipError_t launch_core_profile(const BatchDev &b, const SetCoreDev &f, uint64_t count, unsigned int *visits,
+                               hipStream_t st, int cus);
+
 // Pike VM closure tables (host/nfa_build.hpp) on the device.
 struct NfaDev {
   const uint32_t *leaves;     // 3 words per leaf: kind | lo << 8 | hi << 16, closure, slot

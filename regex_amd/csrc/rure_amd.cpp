@@ -13,6 +13,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <unordered_map>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -58,6 +60,10 @@ struct DevTables {
   RevDfaDev r{};
   SetDfaDev s{};
   NfaDev n{};
+  SetCoreDev c{};
+  bool use_cores = false;   // sets: core-form kernel
+  bool cores_adapted = false;
+  void *core_blob = nullptr;  // re-ranked core tables (adapt_cores)
   bool has_dfa = false;     // the DFA materialised (else: Pike VM only)
   bool quit_possible = false;  // the DFA can quit (Unicode \b): Pike VM fallback pass
   int cus = 256;
@@ -172,6 +178,115 @@ bool pack_forward(const DenseDfa &d, PackedFwd *p, std::string *err) {
   return true;
 }
 
+// Core form of a set DFA (kernel: set_core_kernel).  States whose rows and
+// EOF masks agree differ only in the matches their entry reports; they share
+// a core, and the report moves onto the transition (an output code).  Cores
+// are numbered in BFS order over ASCII bytes from the start states; the first
+// `hot` (as many as fit the LDS budget, at most 1023) are held in LDS.
+struct CoreSet {
+  bool ok = false;
+  uint32_t K = 0, ncores = 0, hot = 0, dead = 0, quit = 0xFFFFFFFFu;
+  std::vector<uint8_t> lds;       // class map (256 B), then (hot + 1) x K u16 entries
+  std::vector<uint16_t> gcore;    // ncores x K
+  std::vector<uint64_t> gout;     // ncores x K
+  std::vector<uint64_t> eof;      // ncores
+  uint16_t start[128];
+  std::vector<uint32_t> order;    // rank -> core (in first-appearance numbering)
+  bool profiled = false;
+};
+
+// weights (optional, by core in first-appearance numbering): rank the cores
+// by decreasing weight (measured visits), ties in BFS order.
+bool build_set_cores(const DenseDfa &d, size_t lds_budget, CoreSet *cs,
+                     const std::vector<uint64_t> *weights = nullptr) {
+  const int S = d.nstates;
+  std::unordered_map<std::string, uint32_t> key_core;
+  std::vector<uint32_t> core_of(S);
+  std::vector<int> rep;
+  for (int s = 0; s < S; ++s) {
+    std::string k((const char *)&d.trans[(size_t)s * 256], 256 * 4);
+    k.append((const char *)&d.eof_mask[s], 8);
+    auto it = key_core.emplace(k, (uint32_t)rep.size());
+    if (it.second) rep.push_back(s);
+    core_of[s] = it.first->second;
+  }
+  const uint32_t nc = (uint32_t)rep.size();
+  if (nc >= 65535) return false;
+  // BFS order over ASCII bytes from the start cores, then everything else
+  std::vector<int32_t> rank(nc, -1);
+  std::vector<uint32_t> order;
+  std::deque<uint32_t> dq;
+  auto push = [&](uint32_t c) { if (rank[c] < 0) { rank[c] = (int32_t)order.size(); order.push_back(c); dq.push_back(c); } };
+  for (int i = 0; i < 128; ++i) push(core_of[d.start[i]]);
+  while (!dq.empty()) {
+    uint32_t c = dq.front(); dq.pop_front();
+    for (int b = 0; b < 128; ++b) push(core_of[d.trans[(size_t)rep[c] * 256 + b]]);
+  }
+  for (uint32_t c = 0; c < nc; ++c) push(c);
+  if (weights) {
+    std::vector<uint32_t> bfs = order;
+    std::stable_sort(order.begin(), order.end(),
+                     [&](uint32_t a, uint32_t b2) { return (*weights)[a] > (*weights)[b2]; });
+    for (uint32_t r = 0; r < nc; ++r) rank[order[r]] = (int32_t)r;
+    (void)bfs;
+  }
+  // byte classes: identical (next core, output) columns over all cores
+  std::unordered_map<std::string, uint32_t> col_id;
+  uint8_t cls[256];
+  std::vector<int> col_rep;
+  for (int b = 0; b < 256; ++b) {
+    std::string k;
+    k.reserve(nc * 12);
+    for (uint32_t r = 0; r < nc; ++r) {
+      const uint32_t nxt = d.trans[(size_t)rep[order[r]] * 256 + b];
+      const uint32_t ncore = (uint32_t)rank[core_of[nxt]];
+      k.append((const char *)&ncore, 4);
+      k.append((const char *)&d.now_mask[nxt], 8);
+    }
+    auto it = col_id.emplace(k, (uint32_t)col_rep.size());
+    if (it.second) col_rep.push_back(b);
+    if (it.first->second > 255) return false;
+    cls[b] = (uint8_t)it.first->second;
+  }
+  const uint32_t K = (uint32_t)col_rep.size();
+  if (lds_budget < 256 + 4 * K) return false;
+  uint32_t hot = (uint32_t)std::min<size_t>({(size_t)nc, 1023, (lds_budget - 256) / (2 * K) - 1});
+  cs->K = K;
+  cs->ncores = nc;
+  cs->hot = hot;
+  cs->gcore.assign((size_t)nc * K, 0);
+  cs->gout.assign((size_t)nc * K, 0);
+  cs->eof.assign(nc, 0);
+  cs->lds.assign(256 + (size_t)(hot + 1) * K * 2, 0);
+  memcpy(cs->lds.data(), cls, 256);
+  uint16_t *T = (uint16_t *)(cs->lds.data() + 256);
+  for (uint32_t r = 0; r < nc; ++r) {
+    const int s = rep[order[r]];
+    cs->eof[r] = d.eof_mask[s];
+    for (uint32_t k = 0; k < K; ++k) {
+      const uint32_t nxt = d.trans[(size_t)s * 256 + col_rep[k]];
+      const uint32_t ncore = (uint32_t)rank[core_of[nxt]];
+      const uint64_t out = d.now_mask[nxt];
+      cs->gcore[(size_t)r * K + k] = (uint16_t)ncore;
+      cs->gout[(size_t)r * K + k] = out;
+      if (r < hot) {
+        uint32_t code = 0;
+        if (out) code = (__builtin_popcountll(out) == 1 && __builtin_ctzll(out) < 62) ? __builtin_ctzll(out) + 1 : 63;
+        const uint32_t tgt = ncore < hot ? ncore : hot;
+        T[(size_t)r * K + k] = (uint16_t)((tgt << 6) | (ncore < hot ? code : 0));
+      }
+    }
+  }
+  for (uint32_t k = 0; k < K; ++k) T[(size_t)hot * K + k] = (uint16_t)(hot << 6);  // sentinel row
+  for (int i = 0; i < 128; ++i) cs->start[i] = (uint16_t)rank[core_of[d.start[i]]];
+  cs->dead = (uint32_t)rank[core_of[d.dead]];
+  cs->quit = d.quit >= 0 ? (uint32_t)rank[core_of[d.quit]] : 0xFFFFFFFFu;
+  cs->lds.resize((cs->lds.size() + 15) & ~(size_t)15, 0);
+  cs->order = order;
+  cs->ok = true;
+  return true;
+}
+
 struct Blob {
   std::vector<uint8_t> bytes;
   size_t add(const void *src, size_t n) {
@@ -267,6 +382,7 @@ struct rure_set {
   std::string dfa_err;
   DenseDfa dfa;
   PackedFwd pf;
+  CoreSet cores;      // core form, used when the hot table cannot hold the set DFA
   NfaTables nt;
   bool nfa_ok = false;
   std::map<int, DevTables> dev;
@@ -337,6 +453,10 @@ bool build_set(rure_set *rs) {
     if (!rs->nfa_ok) rs->dfa_err += "; " + nerr;
     return rs->nfa_ok;
   }
+  // Large sets: the byte-row hot table holds at most 255 states; switch to
+  // the core form when more normal or match-reporting states than that exist.
+  if (rs->dfa.n_normal > 255 || rs->dfa.n_match_end - rs->dfa.n_normal > 255)
+    build_set_cores(rs->dfa, 150 * 1024, &rs->cores);
   rs->dfa_ok = true;
   return true;
 }
@@ -480,6 +600,15 @@ DevTables *set_device(rure_set *rs, std::string *err) {
   NfaOffsets no{};
   if (rs->nfa_ok) no = add_nfa(b, rs->nt);
   size_t o_lds = 0, o_full = 0, o_mask = 0, o_now = 0, o_start = 0;
+  size_t c_lds = 0, c_core = 0, c_out = 0, c_eof = 0, c_start = 0;
+  const CoreSet &cs = rs->cores;
+  if (rs->dfa_ok && cs.ok) {
+    c_lds = b.add(cs.lds.data(), cs.lds.size());
+    c_core = b.add(cs.gcore.data(), cs.gcore.size() * 2);
+    c_out = b.add(cs.gout.data(), cs.gout.size() * 8);
+    c_eof = b.add(cs.eof.data(), cs.eof.size() * 8);
+    c_start = b.add(cs.start, 256);
+  }
   if (rs->dfa_ok) {
     o_lds = b.add(pf.lds.data(), pf.lds.size());
     o_full = b.add(pf.full.data(), pf.full.size() * 2);
@@ -507,6 +636,20 @@ DevTables *set_device(rure_set *rs, std::string *err) {
     t.s.n_match_end = fw.n_match_end;
     t.s.dead = fw.dead;
     t.s.quit = fw.quit < 0 ? 0xFFFFFFFFu : (uint32_t)fw.quit;
+    if (cs.ok) {
+      t.use_cores = true;
+      t.c.lds_image = base + c_lds;
+      t.c.lds_bytes = (uint32_t)cs.lds.size();
+      t.c.hot = cs.hot;
+      t.c.K = cs.K;
+      t.c.gcore = (const uint16_t *)(base + c_core);
+      t.c.gout = (const uint64_t *)(base + c_out);
+      t.c.eof = (const uint64_t *)(base + c_eof);
+      t.c.start = (const uint16_t *)(base + c_start);
+      t.c.all = t.s.all;
+      t.c.dead = cs.dead;
+      t.c.quit = cs.quit;
+    }
   }
   if (t.quit_possible && !rs->nfa_ok) {
     (void)hipFree(t.blob);
@@ -627,10 +770,57 @@ hipError_t run_regex(int mode, const BatchDev &b, const DevTables &t, void *out,
   return run_pike(mode, true, b, t, out, st);
 }
 
+// First batched use of a core-form set on a device: count core visits over a
+// sample of the batch, re-rank the cores so the LDS table holds the visited
+// ones, and upload the re-ranked tables.  Costs one host sync, once.
+bool adapt_cores(rure_set *rs, DevTables *t, const BatchDev &b, hipStream_t st, std::string *err) {
+  std::lock_guard<std::mutex> g(rs->mu);
+  if (t->cores_adapted) return true;
+  t->cores_adapted = true;
+  const CoreSet &cs = rs->cores;
+  const uint64_t sample = std::min<uint64_t>(b.count, 16384);
+  unsigned int *visits = nullptr;
+  if (!hip_ok(hipMallocAsync((void **)&visits, (size_t)cs.ncores * 4, st), err)) return false;
+  std::vector<unsigned int> h(cs.ncores);
+  bool ok = hip_ok(hipMemsetAsync(visits, 0, (size_t)cs.ncores * 4, st), err) &&
+            hip_ok(launch_core_profile(b, t->c, sample, visits, st, t->cus), err) &&
+            hip_ok(hipMemcpyAsync(h.data(), visits, (size_t)cs.ncores * 4, hipMemcpyDeviceToHost, st), err) &&
+            hip_ok(hipFreeAsync(visits, st), err) && hip_ok(hipStreamSynchronize(st), err);
+  if (!ok) return false;
+  std::vector<uint64_t> w(cs.ncores, 0);
+  for (uint32_t r = 0; r < cs.ncores; ++r) w[cs.order[r]] = h[r];
+  CoreSet c2;
+  if (!build_set_cores(rs->dfa, 150 * 1024, &c2, &w)) return true;  // keep the BFS ranking
+  Blob bl;
+  size_t c_lds = bl.add(c2.lds.data(), c2.lds.size());
+  size_t c_core = bl.add(c2.gcore.data(), c2.gcore.size() * 2);
+  size_t c_out = bl.add(c2.gout.data(), c2.gout.size() * 8);
+  size_t c_eof = bl.add(c2.eof.data(), c2.eof.size() * 8);
+  size_t c_start = bl.add(c2.start, 256);
+  DevTables tmp;
+  if (!upload_blob(bl, &tmp, err)) return false;
+  uint8_t *base = (uint8_t *)tmp.blob;
+  SetCoreDev c = t->c;
+  c.lds_image = base + c_lds;
+  c.lds_bytes = (uint32_t)c2.lds.size();
+  c.hot = c2.hot;
+  c.K = c2.K;
+  c.gcore = (const uint16_t *)(base + c_core);
+  c.gout = (const uint64_t *)(base + c_out);
+  c.eof = (const uint64_t *)(base + c_eof);
+  c.start = (const uint16_t *)(base + c_start);
+  c.dead = c2.dead;
+  c.quit = c2.quit;
+  if (t->core_blob) (void)hipFree(t->core_blob);
+  t->core_blob = tmp.blob;
+  t->c = c;
+  return true;
+}
+
 // exec.rs:998-1038 many_matches_at for a batch.
 hipError_t run_set(const BatchDev &b, const DevTables &t, uint64_t *out, hipStream_t st, int dfa_grid) {
   if (!t.has_dfa) return run_pike(MODE_SET, false, b, t, out, st);
-  hipError_t e = launch_dfa_set(b, t.s, out, st, dfa_grid);
+  hipError_t e = t.use_cores ? launch_set_cores(b, t.c, out, st, t.cus) : launch_dfa_set(b, t.s, out, st, dfa_grid);
   if (e != hipSuccess || !t.quit_possible) return e;
   return run_pike(MODE_SET, true, b, t, out, st);
 }
@@ -918,6 +1108,7 @@ void rure_set_free(rure_set *rs) {
     (void)hipGetDevice(&cur);
     (void)hipSetDevice(kv.first);
     (void)hipFree(kv.second.blob);
+    if (kv.second.core_blob) (void)hipFree(kv.second.core_blob);
     (void)hipSetDevice(cur);
   }
   delete rs;
@@ -995,6 +1186,7 @@ int rure_amd_set_matches_batch(rure_set *rs, const rure_amd_batch *batch, uint64
   std::string err;
   DevTables *t = set_device(rs, &err);
   if (!t) return err.rfind("HIP", 0) == 0 ? RURE_AMD_ERR_HIP : RURE_AMD_ERR_DFA;
+  if (t->use_cores && !t->cores_adapted && !adapt_cores(rs, t, b, (hipStream_t)stream, &err)) return RURE_AMD_ERR_HIP;
   int grid = grid_for(b.count, t->s.lds_bytes, t->cus);
   if (run_set(b, *t, mask, (hipStream_t)stream, grid) != hipSuccess) return RURE_AMD_ERR_HIP;
   return RURE_AMD_OK;
@@ -1078,6 +1270,20 @@ int rure_amd_set_dfa_export(rure_set *rs, uint32_t *trans, uint64_t *eof_mask, u
   if (eof_mask) memcpy(eof_mask, d.eof_mask.data(), d.eof_mask.size() * 8);
   if (now_mask) memcpy(now_mask, d.now_mask.data(), d.now_mask.size() * 8);
   if (start) memcpy(start, d.start, sizeof(d.start));
+  return RURE_AMD_OK;
+}
+
+int rure_amd_set_core_export(rure_set *rs, rure_amd_core_info *info, uint8_t *lds, uint16_t *gcore,
+                             uint64_t *gout, uint64_t *eof, uint16_t *start) {
+  if (!rs || rs->single || rs->exprs.size() < 2) return RURE_AMD_ERR_ARG;
+  if (!build_set_dfa(rs) || !rs->cores.ok) return RURE_AMD_ERR_DFA;
+  const CoreSet &cs = rs->cores;
+  if (info) *info = rure_amd_core_info{cs.K, cs.ncores, cs.hot, cs.dead, cs.quit, (uint32_t)cs.lds.size()};
+  if (lds) memcpy(lds, cs.lds.data(), cs.lds.size());
+  if (gcore) memcpy(gcore, cs.gcore.data(), cs.gcore.size() * 2);
+  if (gout) memcpy(gout, cs.gout.data(), cs.gout.size() * 8);
+  if (eof) memcpy(eof, cs.eof.data(), cs.eof.size() * 8);
+  if (start) memcpy(start, cs.start, 256);
   return RURE_AMD_OK;
 }
 

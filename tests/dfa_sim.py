@@ -118,3 +118,77 @@ def set_matches(tables, t, start=0):
             else:
                 raise QuitError()
     return mask | int(eof[s])
+
+
+def core_set_matches(tables, t, start=0, n=64):
+    """The core-form set kernel's walk (dfa_scan.hip set_core_kernel): chunks
+    of 16 bytes through the hot table with an output bag, redone against the
+    global tables when they leave the hot cores or meet output code 63."""
+    info, cls, T, gcore, gout, eof, st = tables
+    hot, dead, quit = info["hot"], info["dead"], info["quit"]
+    full = (1 << n) - 1 if n < 64 else (1 << 64) - 1
+    if start > len(t):
+        return 0
+    c = int(st[fwd_flag(t, start)])
+    mask = 0
+    if c == dead:
+        return 0
+
+    def careful(c, mask, b):
+        k = int(cls[b])
+        mask |= int(gout[c, k])
+        c = int(gcore[c, k])
+        if c == quit:
+            raise QuitError()
+        return c, mask, c == dead or (mask & full) == full
+
+    def step1(c, mask, b):
+        k = int(cls[b])
+        if c < hot:
+            e = int(T[c, k])
+            code = e & 63
+            if (e >> 6) != hot and code != 63:
+                if code:
+                    mask |= 1 << (code - 1)
+                c = e >> 6
+                if c == quit:
+                    raise QuitError()
+                return c, mask, c == dead or (mask & full) == full
+        return careful(c, mask, b)
+
+    at = start
+    done = False
+    while not done and at < len(t) and (at % 16) != 0:  # haystack base is 16-aligned here
+        c, mask, done = step1(c, mask, t[at])
+        at += 1
+    while not done and at + 16 <= len(t):
+        chunk = t[at:at + 16]
+        ok = False
+        if c < hot:
+            x, bag, pend = c, 0, 0
+            for b in chunk:
+                e = int(T[x, int(cls[b])])
+                bag |= 1 << (e & 63)
+                if (e & 63) == 63:
+                    pend |= int(gout[x, int(cls[b])])
+                x = e >> 6
+            if x != hot:
+                mask |= (bag >> 1) & ((1 << 62) - 1)
+                mask |= pend
+                c = x
+                if c == quit:
+                    raise QuitError()
+                done = c == dead or (mask & full) == full
+                ok = True
+        if not ok:
+            for b in chunk:
+                c, mask, done = careful(c, mask, b)
+                if done:
+                    break
+        at += 16
+    while not done and at < len(t):
+        c, mask, done = step1(c, mask, t[at])
+        at += 1
+    if not done:
+        mask |= int(eof[c])
+    return mask

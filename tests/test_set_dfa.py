@@ -51,3 +51,38 @@ def test_set_dfa_vs_oracle(pats):
             m = set_matches(tb, t, start)
             exp = o.matches(t, start) if start <= len(t) else []
             assert [i for i in range(len(pats)) if m >> i & 1] == exp, (pats, t, start)
+
+
+def test_core_form_c4_lines():
+    """The 64-pattern C4 set in core form, walked as set_core_kernel walks it,
+    against the oracle on seeded log lines."""
+    import numpy as np
+    from dfa_sim import core_set_matches
+    from regex_amd.workloads import C4_PATTERNS, log_lines_host
+    rs = R.RegexSet(C4_PATTERNS)
+    ct = rs.core_tables()
+    assert ct is not None and ct[0]["hot"] > 500
+    buf, offs = log_lines_host(400, seed=77)
+    o = OracleRegex(rs)
+    for i in range(400):
+        t = bytes(buf[offs[i]:offs[i + 1]])
+        m = core_set_matches(ct, t, n=len(C4_PATTERNS))
+        assert [j for j in range(64) if m >> j & 1] == o.matches(t), i
+
+
+def test_core_form_fuzz():
+    """A set large enough for the core form, on texts with line anchors,
+    word boundaries (ASCII) and overlapping matches."""
+    from dfa_sim import core_set_matches
+    pats = [r"[a-c]+\d", r"\d{2,3}", r"(?m)^ab", r"(?m)c$", r"(?-u:\b)b", r"a.c", r"bb|cc", r"[0-9a-f]{4}",
+            r"x\d*y", r"(?i)ABC", r"c\nb", r"a+b+c+"]
+    rs = R.RegexSet(pats)
+    ct = rs.core_tables()
+    if ct is None:
+        pytest.skip("set small enough for the byte-row kernel")
+    o = OracleRegex(rs)
+    rng = random.Random(1234)
+    for _ in range(400):
+        t = bytes(rng.choice(b"abcdefxy0123\n ABC") for _ in range(rng.randint(0, 60)))
+        m = core_set_matches(ct, t, n=len(pats))
+        assert [j for j in range(len(pats)) if m >> j & 1] == o.matches(t), t
