@@ -1,0 +1,32 @@
+"""The C ABI as a C program uses it: tests/ctest/rure_ctest.c (the cases of
+the reference's regex-capi/ctest/test.c) compiled with gcc against
+include/rure_amd.h and linked to librure_amd.so.  Building runs on CPU; the
+run needs the GPU (every search launches kernels)."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "regex_amd", "lib")
+
+
+def build(tmp_path):
+    exe = str(tmp_path / "rure_ctest")
+    subprocess.check_call(["gcc", "-std=c11", "-Wall", "-Werror", "-o", exe,
+                           os.path.join(ROOT, "tests", "ctest", "rure_ctest.c"),
+                           "-I", os.path.join(ROOT, "include"), "-L", LIB, "-lrure_amd",
+                           "-Wl,-rpath," + LIB, "-Wl,--allow-shlib-undefined"])
+    return exe
+
+
+def test_ctest_builds(tmp_path):
+    assert os.path.exists(build(tmp_path))
+
+
+@pytest.mark.gpu
+def test_ctest_runs(tmp_path):
+    exe = build(tmp_path)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert "all checks passed" in r.stdout
