@@ -31,6 +31,8 @@ typedef struct rure_set rure_set;          /* rure.h:36 */
 typedef struct rure_options rure_options;  /* rure.h:47 */
 typedef struct rure_iter rure_iter;        /* rure.h:106 */
 typedef struct rure_error rure_error;      /* rure.h:127 */
+typedef struct rure_captures rure_captures;                      /* rure.h:95 */
+typedef struct rure_iter_capture_names rure_iter_capture_names;  /* rure.h:117 */
 
 /* rure.h:56-68 */
 #define RURE_FLAG_CASEI (1 << 0)
@@ -67,6 +69,24 @@ rure_iter *rure_iter_new(rure *re);
 void rure_iter_free(rure_iter *it);
 bool rure_iter_next(rure_iter *it, const uint8_t *haystack, size_t length,
                     rure_match *match);
+/* rure.h:248-249 — leftmost-first match with every capture group's location
+ * (exec.rs:524-596 dispatch: DFA bounds, then the Pike VM for the groups). */
+bool rure_find_captures(rure *re, const uint8_t *haystack, size_t length,
+                        size_t start, rure_captures *captures);
+/* rure.h:285 — index of the named group, -1 if none. */
+int32_t rure_capture_name_index(rure *re, const char *name);
+/* rure.h:292-307 — group names in index order ("" for unnamed groups). */
+rure_iter_capture_names *rure_iter_capture_names_new(rure *re);
+void rure_iter_capture_names_free(rure_iter_capture_names *it);
+bool rure_iter_capture_names_next(rure_iter_capture_names *it, char **name);
+/* rure.h:369-371 */
+bool rure_iter_next_captures(rure_iter *it, const uint8_t *haystack, size_t length,
+                             rure_captures *captures);
+/* rure.h:385-411 */
+rure_captures *rure_captures_new(rure *re);
+void rure_captures_free(rure_captures *captures);
+bool rure_captures_at(rure_captures *captures, size_t i, rure_match *match);
+size_t rure_captures_len(rure_captures *captures);
 /* rure.h:423-454 */
 rure_options *rure_options_new(void);
 void rure_options_free(rure_options *options);
@@ -128,6 +148,14 @@ int rure_amd_set_matches_batch(rure_set *re, const rure_amd_batch *batch, uint64
  * chunks with exact boundary repair. */
 int rure_amd_find_iter_batch(rure *re, const rure_amd_batch *batch, uint64_t *counts, rure_match *matches,
                              size_t capacity, uint64_t *total, void *stream);
+
+/* Batched rure_find_captures: slots[i * 2 * ngroups + 2 * g + {0, 1}]
+ * (device, size_t) = start / end of group g in haystack i, SIZE_MAX where the
+ * group did not participate or the haystack has no match.  ngroups =
+ * rure_amd_captures_len(re). */
+int rure_amd_captures_batch(rure *re, const rure_amd_batch *batch, size_t *slots, void *stream);
+/* Number of capture groups including group 0 (= rure_captures_len). */
+size_t rure_amd_captures_len(rure *re);
 
 /* Diagnostics (host only, no GPU needed). */
 typedef struct rure_amd_dfa_info {
@@ -201,6 +229,10 @@ int rure_amd_nfa_export(rure *re, rure_amd_nfa_info *info, uint32_t *leaves, uin
                         uint32_t *entries);
 int rure_amd_set_nfa_export(rure_set *re, rure_amd_nfa_info *info, uint32_t *leaves, uint32_t *cl_off,
                             uint32_t *entries);
+/* Capture slots each closure entry sets (the Saves on its path): save_off =
+ * entries + 1 u32 CSR offsets into save_slot (u16).  *n_slots receives the
+ * length of save_slot; NULL arrays query it. */
+int rure_amd_nfa_saves_export(rure *re, uint32_t *save_off, uint16_t *save_slot, size_t *n_slots);
 /* 1 if batched searches of this regex run the DFA kernels, 0 if only the
  * Pike VM kernel (automaton too large), negative on error. */
 int rure_amd_uses_dfa(rure *re);

@@ -131,6 +131,43 @@ int orc_find_at(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t le
   return orc_find_nfa(r, c, text, len, start, ms, me);
 }
 
+/* utf8.rs:24-39 */
+static size_t next_utf8(const uint8_t *text, size_t len, size_t i) {
+  if (i >= len) return i + 1;
+  uint8_t b = text[i];
+  return i + (b <= 0x7F ? 1 : b <= 0xDF ? 2 : b <= 0xEF ? 3 : 4);
+}
+
+/* exec.rs:524-596 read_captures_at, MatchType::Dfa arm (the literal and
+ * reverse match types produce the same bounds and also continue with
+ * captures_nfa_with_match, exec.rs:861-875). */
+int orc_captures_at(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t len, size_t start, size_t *slots,
+                    size_t nslots) {
+  for (size_t i = 0; i < nslots; ++i) slots[i] = SIZE_MAX;
+  if (start > len) return 0;
+  if (nslots <= 2) {
+    size_t ms, me;
+    if (!orc_find_at(r, c, text, len, start, &ms, &me)) return 0;
+    if (nslots == 2) { slots[0] = ms; slots[1] = me; }
+    return 1;
+  }
+  if (r->nfa->anchored_start) return orc_captures_nfa(r, c, text, len, start, slots, nslots) &&
+                                     slots[0] != SIZE_MAX && slots[1] != SIZE_MAX;
+  size_t ms, me;
+  int k = find_dfa_forward(r, c, text, len, start, &ms, &me);
+  if (k == R_NOMATCH) return 0;
+  size_t n = len;
+  if (k == R_MATCH) {
+    size_t e = next_utf8(text, len, next_utf8(text, len, me));
+    n = e < len ? e : len;
+    start = ms;
+  } else {
+    c->st.quits++;
+  }
+  if (!orc_captures_nfa(r, c, text, n, start, slots, nslots)) return 0;
+  return slots[0] != SIZE_MAX && slots[1] != SIZE_MAX;
+}
+
 /* exec.rs:825-837 shortest_nfa: quit_after_match Pike VM, slots[1] */
 int orc_shortest_nfa(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t len, size_t start, size_t *end) {
   uint8_t m[1] = {0};

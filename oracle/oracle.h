@@ -62,6 +62,10 @@ int orc_shortest_nfa(const orc_regex *r, orc_cache *c, const uint8_t *text, size
 /* Pike VM captures: slots[2*ncaps] (SIZE_MAX = unset). */
 int orc_captures_nfa(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t len, size_t start,
                      size_t *slots, size_t nslots);
+/* exec.rs:524-596 read_captures_at (DFA bounds, then the Pike VM on
+ * text[..min(next_utf8(next_utf8(end)), len)] from the match start). */
+int orc_captures_at(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t len, size_t start,
+                    size_t *slots, size_t nslots);
 /* re_trait.rs:197-221 find_iter.  Writes up to cap (s,e) pairs; returns the total count. */
 int64_t orc_find_iter(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t len, size_t *pairs,
                       size_t cap);

@@ -146,7 +146,63 @@ class Regex(object):
             N.rure_iter_free(it)
         return out
 
+    def captures(self, text, start=0):
+        """Leftmost-first match with its groups (bytes::Regex::captures,
+        re_bytes.rs:227-240): a list of (start, end) | None per group (group 0
+        = the whole match), or None without a match."""
+        caps = N.rure_captures_new(self._re)
+        try:
+            if not N.rure_find_captures(self._re, text, len(text), start, caps):
+                return None
+            return _read_caps(caps)
+        finally:
+            N.rure_captures_free(caps)
+
+    def captures_iter(self, text):
+        """Successive captures, iterated as rure_iter_next_captures does."""
+        it = N.rure_iter_new(self._re)
+        caps = N.rure_captures_new(self._re)
+        out = []
+        try:
+            while N.rure_iter_next_captures(it, text, len(text), caps):
+                out.append(_read_caps(caps))
+        finally:
+            N.rure_captures_free(caps)
+            N.rure_iter_free(it)
+        return out
+
+    def captures_len(self):
+        return int(N.rure_amd_captures_len(self._re))
+
+    def capture_names(self):
+        """Group names in index order, None for unnamed groups (re_bytes.rs:580-590)."""
+        it = N.rure_iter_capture_names_new(self._re)
+        out = []
+        try:
+            p = ctypes.c_char_p()
+            while N.rure_iter_capture_names_next(it, ctypes.byref(p)):
+                out.append(p.value.decode("utf-8") or None)
+        finally:
+            N.rure_iter_capture_names_free(it)
+        return out
+
+    def capture_name_index(self, name):
+        i = N.rure_capture_name_index(self._re, name.encode("utf-8"))
+        return None if i < 0 else i
+
     # -------------------------------------------- batches (device tensors)
+    def captures_batch(self, haystack, offsets=None, stride=None, length=None, count=None,
+                       start=0, out=None, stream=None):
+        """Captures per haystack: an (n, groups, 2) int64 tensor of
+        (start, end), -1 where a group did not participate or there is no match."""
+        import torch
+        b = _batch(haystack, offsets, stride, length, count, start)
+        if out is None:
+            out = torch.empty((b.count, self.captures_len(), 2), dtype=torch.int64, device=haystack.device)
+        _check(N.rure_amd_captures_batch(self._re, ctypes.byref(b), ctypes.c_void_p(out.data_ptr()),
+                                         _stream_ptr(stream)), "captures_batch")
+        return out
+
     def find_batch(self, haystack, offsets=None, stride=None, length=None, count=None,
                    start=0, out=None, stream=None):
         """Leftmost-first match per haystack.  Returns an (n, 2) int64 tensor of
@@ -221,6 +277,18 @@ class Regex(object):
         """Pike VM closure tables of the NFA kernel: (info, leaves, cl_off, entries)."""
         return _nfa_export(N.rure_amd_nfa_export, self._re)
 
+    def nfa_saves(self):
+        """Capture slots set by each closure entry: (save_off, save_slot)."""
+        import numpy as np
+        n = N.c_size()
+        _check(N.rure_amd_nfa_saves_export(self._re, None, None, ctypes.byref(n)), "nfa_saves_export")
+        ents = self.nfa_tables()[0]["entries"]
+        off = np.zeros(ents + 1, dtype=np.uint32)
+        slot = np.zeros(max(n.value, 1), dtype=np.uint16)
+        _check(N.rure_amd_nfa_saves_export(self._re, off.ctypes.data, slot.ctypes.data, ctypes.byref(n)),
+               "nfa_saves_export")
+        return off, slot[: n.value]
+
     def dfa_tables(self, which=0):
         import numpy as np
         info = self.dfa_info(which)
@@ -237,6 +305,14 @@ class Regex(object):
             _check(N.rure_amd_dfa_strip_export(self._re, strip.ctypes.data), "dfa_strip_export")
             info["strip"] = strip
         return info, trans.reshape(n, 256), eof, start
+
+
+def _read_caps(caps):
+    out = []
+    m = N.RureMatch()
+    for i in range(N.rure_captures_len(caps)):
+        out.append((m.start, m.end) if N.rure_captures_at(caps, i, ctypes.byref(m)) else None)
+    return out
 
 
 def _nfa_export(fn, handle):

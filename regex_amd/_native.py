@@ -93,6 +93,17 @@ rure_iter_new = _sig("rure_iter_new", VP, VP)
 rure_iter_free = _sig("rure_iter_free", None, VP)
 rure_iter_next = _sig("rure_iter_next", ctypes.c_bool, VP, ctypes.c_char_p, c_size,
                       ctypes.POINTER(RureMatch))
+rure_captures_new = _sig("rure_captures_new", VP, VP)
+rure_captures_free = _sig("rure_captures_free", None, VP)
+rure_captures_len = _sig("rure_captures_len", c_size, VP)
+rure_captures_at = _sig("rure_captures_at", ctypes.c_bool, VP, c_size, ctypes.POINTER(RureMatch))
+rure_find_captures = _sig("rure_find_captures", ctypes.c_bool, VP, ctypes.c_char_p, c_size, c_size, VP)
+rure_iter_next_captures = _sig("rure_iter_next_captures", ctypes.c_bool, VP, ctypes.c_char_p, c_size, VP)
+rure_capture_name_index = _sig("rure_capture_name_index", ctypes.c_int32, VP, ctypes.c_char_p)
+rure_iter_capture_names_new = _sig("rure_iter_capture_names_new", VP, VP)
+rure_iter_capture_names_free = _sig("rure_iter_capture_names_free", None, VP)
+rure_iter_capture_names_next = _sig("rure_iter_capture_names_next", ctypes.c_bool, VP,
+                                    ctypes.POINTER(ctypes.c_char_p))
 rure_compile_set = _sig("rure_compile_set", VP, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(c_size),
                         c_size, ctypes.c_uint32, VP, VP)
 rure_set_free = _sig("rure_set_free", None, VP)
@@ -106,6 +117,9 @@ rure_amd_shortest_match_batch = _sig("rure_amd_shortest_match_batch", ctypes.c_i
                                      ctypes.POINTER(RureBatch), VP, VP)
 rure_amd_set_matches_batch = _sig("rure_amd_set_matches_batch", ctypes.c_int, VP, ctypes.POINTER(RureBatch),
                                   VP, VP)
+rure_amd_captures_batch = _sig("rure_amd_captures_batch", ctypes.c_int, VP, ctypes.POINTER(RureBatch), VP, VP)
+rure_amd_captures_len = _sig("rure_amd_captures_len", c_size, VP)
+rure_amd_nfa_saves_export = _sig("rure_amd_nfa_saves_export", ctypes.c_int, VP, VP, VP, ctypes.POINTER(c_size))
 rure_amd_dfa_info_get = _sig("rure_amd_dfa_info_get", ctypes.c_int, VP, ctypes.c_int, ctypes.POINTER(DfaInfo))
 rure_amd_set_dfa_info_get = _sig("rure_amd_set_dfa_info_get", ctypes.c_int, VP, ctypes.POINTER(DfaInfo))
 rure_amd_program_export = _sig("rure_amd_program_export", ctypes.c_int64, VP, ctypes.c_int,

@@ -45,35 +45,45 @@ struct Builder {
   }
 
   // Depth-first walk in the reference's order (pikevm.rs:319-352): Split
-  // follows goto1 first; Save is transparent; EmptyLook adds its assertion.
-  // An instruction already walked with a subset of the current assertions is
-  // not walked again (everything it reaches was already listed); entries dominated by an earlier
-  // entry of the same leaf with a subset of its assertions are dropped.
-  std::vector<std::pair<uint32_t, uint32_t>> walk(uint32_t ip0) {
-    std::vector<std::pair<uint32_t, uint32_t>> out;  // (inst, cond)
+  // follows goto1 first; Save is transparent but recorded; EmptyLook adds its
+  // assertion.  An instruction already walked with a subset of the current
+  // assertions is not walked again (everything it reaches was already
+  // listed, by a path that is taken whenever this one would be); entries
+  // dominated by an earlier entry of the same leaf with a subset of its
+  // assertions are dropped.
+  struct Raw {
+    uint32_t ip, cond;
+    int32_t saves;  // node in `snodes` (the Saves on the path), -1 if none
+  };
+  std::vector<std::pair<uint16_t, int32_t>> snodes;  // (slot, parent node)
+
+  std::vector<Raw> walk(uint32_t ip0) {
+    std::vector<Raw> out;
     std::map<uint32_t, std::vector<uint32_t>> seen;  // inst -> assertion sets walked
-    std::vector<std::pair<uint32_t, uint32_t>> stack{{ip0, 0}};
+    std::vector<Raw> stack{{ip0, 0, -1}};
     while (!stack.empty()) {
-      auto [ip, cond] = stack.back();
+      Raw f = stack.back();
       stack.pop_back();
       while (true) {
-        auto &sv = seen[ip];
+        auto &sv = seen[f.ip];
         bool covered = false;
         for (uint32_t c : sv)
-          if ((c & ~cond) == 0) { covered = true; break; }  // walked with fewer assertions
+          if ((c & ~f.cond) == 0) { covered = true; break; }  // walked with fewer assertions
         if (covered) break;
-        sv.push_back(cond);
-        const Inst &in = p.insts[ip];
+        sv.push_back(f.cond);
+        const Inst &in = p.insts[f.ip];
         if (in.op == OP_SPLIT) {
-          stack.push_back({in.y, cond});
-          ip = in.x;
+          stack.push_back({in.y, f.cond, f.saves});
+          f.ip = in.x;
         } else if (in.op == OP_SAVE) {
-          ip = in.x;
+          snodes.push_back({(uint16_t)in.y, f.saves});
+          f.saves = (int32_t)snodes.size() - 1;
+          f.ip = in.x;
         } else if (in.op == OP_EMPTY) {
-          cond |= 1u << in.look;
-          ip = in.x;
+          f.cond |= 1u << in.look;
+          f.ip = in.x;
         } else {
-          out.push_back({ip, cond});
+          out.push_back(f);
           break;
         }
       }
@@ -82,12 +92,13 @@ struct Builder {
   }
 
   void build_closure(uint32_t ip0) {
+    snodes.clear();
     auto raw = walk(ip0);
     std::vector<NfaEntry> ents;
     std::map<uint32_t, std::vector<std::pair<uint32_t, uint32_t>>> by_leaf;  // leaf -> (cond, index)
     for (auto &pc : raw) {
-      uint32_t leaf = leaf_id(pc.first);
-      uint32_t cond = pc.second;
+      uint32_t leaf = leaf_id(pc.ip);
+      uint32_t cond = pc.cond;
       auto &prev = by_leaf[leaf];
       bool dominated = false;
       for (auto &q : prev)
@@ -97,6 +108,8 @@ struct Builder {
       prev.push_back({cond, (uint32_t)ents.size()});
       ents.push_back({leaf, (cond & 0xFF) | (prev_idx << 8)});
       t.looks_used |= cond;
+      for (int32_t n = pc.saves; n >= 0; n = snodes[n].second) t.save_slot.push_back(snodes[n].first);
+      t.save_off.push_back((uint32_t)t.save_slot.size());
     }
     t.entries.insert(t.entries.end(), ents.begin(), ents.end());
     if (ents.size() > t.max_closure) t.max_closure = ents.size();
@@ -110,6 +123,7 @@ bool build_nfa_tables(const Program &prog, NfaTables *out, std::string *err) {
   Builder b(prog, t);
   t.root = b.closure_id(prog.start);
   t.cl_off.push_back(0);
+  t.save_off.push_back(0);
   // Closures are built in id order; building one may create new ids.
   for (size_t k = 0; k < b.pending.size(); ++k) {
     b.build_closure(b.pending[k]);

@@ -43,6 +43,10 @@ struct NfaTables {
   bool unicode_wb = false;          // needs Unicode word-character tests
   uint32_t looks_used = 0;          // union of all assertion bits
   size_t max_closure = 0;
+  // Capture slots set on the path to each entry (pikevm.rs:319-352: every
+  // Save on the walk sets its slot to the current position): CSR by entry.
+  std::vector<uint32_t> save_off;   // entries.size() + 1
+  std::vector<uint16_t> save_slot;
 };
 
 bool build_nfa_tables(const Program &prog, NfaTables *out, std::string *err);

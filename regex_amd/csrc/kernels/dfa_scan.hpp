@@ -97,6 +97,8 @@ struct NfaDev {
   uint32_t perlw_n;
   uint32_t nleaves, root, nmatch;
   uint32_t anchored, single, looks, unicode_wb;
+  const uint32_t *save_off;   // per entry: CSR offsets into save_slot (Saves on its path)
+  const uint16_t *save_slot;
 };
 
 // Per-wave working set of the Pike VM: stamp + two thread lists.
@@ -108,6 +110,17 @@ constexpr size_t kNfaLdsMax = 160 * 1024;   // a gfx950 workgroup may take the w
 enum { MODE_SET = 3 };
 hipError_t launch_pike(int mode, bool fallback, const BatchDev &b, const NfaDev &n, void *out, void *scratch,
                        hipStream_t st, int grid);
+
+// Captures (exec.rs:524-596 read_captures_at; Pike VM with capture slots,
+// pikevm.rs:237-352).  found: per haystack the forward/reverse DFA's
+// (start, end), NONE or the quit marker; null when every haystack is searched
+// whole from `start` (anchored-start programs).  slots: count x nslots u64,
+// NONE = unset.  Per-wave working set: caps_wave_bytes (LDS when it fits).
+__host__ __device__ inline size_t caps_wave_bytes(uint32_t nleaves, uint32_t nslots) {
+  return ((size_t)nleaves * (16 * (size_t)nslots + 12) + 64 + 255) & ~(size_t)255;
+}
+hipError_t launch_captures(const BatchDev &b, const NfaDev &n, const uint64_t *found, uint64_t *slots,
+                           uint32_t nslots, void *scratch, hipStream_t st, int grid);
 
 // Batched find_iter (iter_scan.hip).  counts: per haystack; matches:
 // (start, end) pairs, the first `cap` written; total: number of matches.

@@ -390,6 +390,16 @@ struct rure_set {
   rure *single = nullptr;   // one-pattern sets compile with compile_one
 };
 
+struct rure_captures {           // rure.rs Captures(Locations): 2 slots per group
+  std::vector<uint64_t> slots;
+};
+
+struct rure_iter_capture_names {
+  std::vector<std::string> names;
+  size_t next = 0;
+  std::vector<char *> owned;     // handed-out C strings, freed with the iterator
+};
+
 struct rure_iter {
   rure *re;
   size_t last_end = 0;
@@ -468,7 +478,7 @@ bool build_set_dfa(rure_set *rs) {
 
 // Appends the Pike VM tables to an upload blob; fix_nfa() then points the
 // descriptor into the device copy.
-struct NfaOffsets { size_t leaves, cl_off, entries, perlw; };
+struct NfaOffsets { size_t leaves, cl_off, entries, perlw, save_off, save_slot; };
 
 NfaOffsets add_nfa(Blob &b, const NfaTables &nt) {
   NfaOffsets o;
@@ -484,6 +494,8 @@ NfaOffsets add_nfa(Blob &b, const NfaTables &nt) {
   o.entries = b.add(nt.entries.data(), nt.entries.size() * 8);
   namespace U = rure_amd_unicode;
   o.perlw = b.add(U::kPairs + 2 * U::kPerlW.first, (size_t)U::kPerlW.count * 8);
+  o.save_off = b.add(nt.save_off.data(), nt.save_off.size() * 4);
+  o.save_slot = b.add(nt.save_slot.data(), nt.save_slot.size() * 2);
   return o;
 }
 
@@ -493,6 +505,8 @@ void fix_nfa(NfaDev *n, uint8_t *base, const NfaOffsets &o, const NfaTables &nt,
   n->entries = (const uint2 *)(base + o.entries);
   n->perlw = (const uint32_t *)(base + o.perlw);
   n->perlw_n = rure_amd_unicode::kPerlW.count;
+  n->save_off = (const uint32_t *)(base + o.save_off);
+  n->save_slot = (const uint16_t *)(base + o.save_slot);
   n->nleaves = (uint32_t)nt.leaves.size();
   n->root = nt.root;
   n->nmatch = nt.nmatch;
@@ -825,6 +839,37 @@ hipError_t run_set(const BatchDev &b, const DevTables &t, uint64_t *out, hipStre
   return run_pike(MODE_SET, true, b, t, out, st);
 }
 
+// exec.rs:524-596 read_captures_at for a batch.  One group (two slots): the
+// plain find.  Otherwise the DFA's (start, end) per haystack (the quit marker
+// kept, not resolved), then the Pike VM with slots: from the match start over
+// the text up to two characters past the match end, or over the whole
+// haystack where the DFA quit and for anchored-start programs.  A regex whose
+// DFA does not materialise takes its bounds from the Pike VM (the reference's
+// lazy DFA would have produced them).
+hipError_t run_captures(const BatchDev &b, const DevTables &t, uint64_t *slots, uint32_t ns, hipStream_t st,
+                        int dfa_grid) {
+  if (ns <= 2) return run_regex(MODE_FIND, b, t, slots, st, dfa_grid);
+  hipError_t e = hipSuccess;
+  uint64_t *found = nullptr;
+  if (!t.n.anchored) {
+    if ((e = hipMallocAsync((void **)&found, b.count * 16, st)) != hipSuccess) return e;
+    e = t.has_dfa ? launch_dfa_fwd(MODE_FIND, b, t.f, t.r, found, st, dfa_grid)
+                  : run_pike(MODE_FIND, false, b, t, found, st);
+  }
+  const size_t wb = caps_wave_bytes(t.n.nleaves, ns);
+  const bool in_lds = wb <= kNfaLdsMax;
+  const size_t per_cu = in_lds ? std::max<size_t>(1, std::min<size_t>(32, (160u * 1024u) / wb)) : 4;
+  size_t g = std::min<size_t>(b.count, (size_t)t.cus * per_cu);
+  if (!in_lds) g = std::min<size_t>(g, (256u << 20) / wb);  // bound the scratch (wide programs: MiBs per wave)
+  const int grid = (int)std::max<size_t>(1, g);
+  void *scratch = nullptr;
+  if (e == hipSuccess && !in_lds) e = hipMallocAsync(&scratch, wb * (size_t)grid, st);
+  if (e == hipSuccess) e = launch_captures(b, t.n, found, slots, ns, scratch, st, grid);
+  if (scratch) { hipError_t e2 = hipFreeAsync(scratch, st); if (e == hipSuccess) e = e2; }
+  if (found) { hipError_t e2 = hipFreeAsync(found, st); if (e == hipSuccess) e = e2; }
+  return e;
+}
+
 bool to_batch(const rure_amd_batch *b, BatchDev *o) {
   if (!b || (!b->haystack && b->count > 0)) return false;
   o->hay = b->haystack;
@@ -1057,6 +1102,106 @@ bool rure_iter_next(rure_iter *it, const uint8_t *hay, size_t len, rure_match *m
   }
 }
 
+// ----------------------------------------------------------------- captures
+namespace {
+
+uint32_t capture_slots(rure *re) {
+  if (!build_regex(re)) die(re->dfa_err);
+  return (uint32_t)(2 * re->nfa.capture_names.size());
+}
+
+// One haystack through run_captures (staged like single_call).  slots: ns.
+bool captures_call(rure *re, const uint8_t *hay, size_t len, size_t start, uint64_t *slots, uint32_t ns) {
+  std::string err;
+  DevTables *t = regex_device(re, &err);
+  if (!t) die(err);
+  if (ns > 2 && !re->nfa_ok) die("captures need the NFA tables, which could not be built");
+  std::lock_guard<std::mutex> g(re->mu);
+  int d = 0;
+  if (!hip_ok(hipGetDevice(&d), &err)) die(err);
+  if (!re->stage.ensure(d, len, &err)) die(err);
+  hipStream_t st = re->stage.stream;
+  if (len && !hip_ok(hipMemcpyAsync(re->stage.hay, hay, len, hipMemcpyHostToDevice, st), &err)) die(err);
+  BatchDev b{re->stage.hay, nullptr, len, len, 1, start};
+  uint64_t *dev = re->stage.res;
+  if (ns > 64 && !hip_ok(hipMallocAsync((void **)&dev, (size_t)ns * 8, st), &err)) die(err);
+  if (!hip_ok(run_captures(b, *t, dev, ns, st, 1), &err)) die(err);
+  if (!hip_ok(hipMemcpyAsync(slots, dev, (size_t)ns * 8, hipMemcpyDeviceToHost, st), &err)) die(err);
+  if (dev != re->stage.res && !hip_ok(hipFreeAsync(dev, st), &err)) die(err);
+  if (!hip_ok(hipStreamSynchronize(st), &err)) die(err);
+  if (slots[0] == kQuit || slots[1] == kQuit) die("internal error: unresolved DFA quit");
+  return slots[0] != ~0ull && slots[1] != ~0ull;
+}
+
+}  // namespace
+
+rure_captures *rure_captures_new(rure *re) {
+  rure_captures *c = new rure_captures();
+  c->slots.assign(capture_slots(re), ~0ull);
+  return c;
+}
+void rure_captures_free(rure_captures *c) { delete c; }
+size_t rure_captures_len(rure_captures *c) { return c->slots.size() / 2; }
+
+bool rure_captures_at(rure_captures *c, size_t i, rure_match *m) {  // rure.rs:413-433 (Locations::pos)
+  if (2 * i + 1 >= c->slots.size()) return false;
+  const uint64_t s = c->slots[2 * i], e = c->slots[2 * i + 1];
+  if (s == ~0ull || e == ~0ull) return false;
+  if (m) { m->start = (size_t)s; m->end = (size_t)e; }
+  return true;
+}
+
+bool rure_find_captures(rure *re, const uint8_t *hay, size_t len, size_t start, rure_captures *c) {
+  std::fill(c->slots.begin(), c->slots.end(), ~0ull);
+  return captures_call(re, hay, len, start, c->slots.data(), (uint32_t)c->slots.size());
+}
+
+bool rure_iter_next_captures(rure_iter *it, const uint8_t *hay, size_t len, rure_captures *c) {  // rure.rs:363-397
+  while (true) {
+    if (it->last_end > len) return false;
+    if (!rure_find_captures(it->re, hay, len, it->last_end, c)) return false;
+    const size_t s = (size_t)c->slots[0], e = (size_t)c->slots[1];
+    if (s == e) {
+      it->last_end += 1;
+      if (it->has_last_match && it->last_match == e) continue;
+    } else {
+      it->last_end = e;
+    }
+    it->has_last_match = true;
+    it->last_match = e;
+    return true;
+  }
+}
+
+int32_t rure_capture_name_index(rure *re, const char *name) {  // rure.rs:233-240
+  if (!build_regex(re)) die(re->dfa_err);
+  const auto &names = re->nfa.capture_names;
+  for (size_t i = 0; i < names.size(); ++i)
+    if (re->nfa.capture_has_name[i] && names[i] == name) return (int32_t)i;
+  return -1;
+}
+
+rure_iter_capture_names *rure_iter_capture_names_new(rure *re) {
+  if (!build_regex(re)) die(re->dfa_err);
+  rure_iter_capture_names *it = new rure_iter_capture_names();
+  it->names = re->nfa.capture_names;
+  return it;
+}
+
+void rure_iter_capture_names_free(rure_iter_capture_names *it) {
+  for (char *p : it->owned) free(p);
+  delete it;
+}
+
+bool rure_iter_capture_names_next(rure_iter_capture_names *it, char **name) {  // rure.rs:267-301
+  if (!name || it->next >= it->names.size()) return false;
+  char *p = strdup(it->names[it->next++].c_str());
+  if (!p) return false;
+  it->owned.push_back(p);
+  *name = p;
+  return true;
+}
+
 // --------------------------------------------------------------------- sets
 rure_set *rure_compile_set(const uint8_t **patterns, const size_t *lens, size_t count, uint32_t flags,
                            rure_options *options, rure_error *error) {
@@ -1147,6 +1292,23 @@ int rure_amd_find_batch(rure *re, const rure_amd_batch *batch, rure_match *out, 
   uint64_t chunk;
   const FwdDfaDev *iter = long_batch(b, *t, &chunk) ? iter_device(re, *t, &err) : nullptr;
   if (run_regex(MODE_FIND, b, *t, out, (hipStream_t)stream, grid, iter) != hipSuccess) return RURE_AMD_ERR_HIP;
+  return RURE_AMD_OK;
+}
+
+size_t rure_amd_captures_len(rure *re) { return re ? capture_slots(re) / 2 : 0; }
+
+int rure_amd_captures_batch(rure *re, const rure_amd_batch *batch, size_t *slots, void *stream) {
+  static_assert(sizeof(size_t) == 8, "64-bit slots");
+  BatchDev b;
+  if (!re || !to_batch(batch, &b) || (!slots && b.count)) return RURE_AMD_ERR_ARG;
+  if (b.count == 0) return RURE_AMD_OK;
+  std::string err;
+  DevTables *t = regex_device(re, &err);
+  if (!t) return err.rfind("HIP", 0) == 0 ? RURE_AMD_ERR_HIP : RURE_AMD_ERR_DFA;
+  const uint32_t ns = capture_slots(re);
+  if (ns > 2 && !re->nfa_ok) return RURE_AMD_ERR_DFA;
+  int grid = grid_for(b.count, t->f.lds_bytes, t->cus);
+  if (run_captures(b, *t, (uint64_t *)slots, ns, (hipStream_t)stream, grid) != hipSuccess) return RURE_AMD_ERR_HIP;
   return RURE_AMD_OK;
 }
 
@@ -1344,6 +1506,16 @@ int rure_amd_set_nfa_export(rure_set *rs, rure_amd_nfa_info *info, uint32_t *lea
   build_set(rs);
   if (!rs->nfa_ok) return RURE_AMD_ERR_DFA;
   return export_nfa(rs->nt, info, leaves, cl_off, entries);
+}
+
+int rure_amd_nfa_saves_export(rure *re, uint32_t *save_off, uint16_t *save_slot, size_t *n_slots) {
+  if (!re) return RURE_AMD_ERR_ARG;
+  build_regex(re);
+  if (!re->nfa_ok) return RURE_AMD_ERR_DFA;
+  if (n_slots) *n_slots = re->nt.save_slot.size();
+  if (save_off) memcpy(save_off, re->nt.save_off.data(), re->nt.save_off.size() * 4);
+  if (save_slot) memcpy(save_slot, re->nt.save_slot.data(), re->nt.save_slot.size() * 2);
+  return RURE_AMD_OK;
 }
 
 int rure_amd_uses_dfa(rure *re) {

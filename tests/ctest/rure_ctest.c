@@ -2,7 +2,8 @@
  * C-ABI drop-in check: the calls a C program written against the
  * reference's regex-capi/include/rure.h makes (the same cases its
  * regex-capi/ctest/test.c covers: is_match, shortest_match, find, iter,
- * flags, compile errors, size limit, sets, set start offsets), made against
+ * flags, compile errors, size limit, sets, set start offsets, captures,
+ * iteration with captures, capture names), made against
  * include/rure_amd.h and librure_amd.so.  Exit status 0 = all passed.
  */
 #include <stdio.h>
@@ -54,6 +55,46 @@ static void iter(void) {
   while (rure_iter_next(it, (const uint8_t *)"ab", 2, &m)) ++n;
   CHECK(n == 3, "empty-pattern iter yields 3 empty matches");
   rure_iter_free(it);
+  rure_free(re);
+}
+
+static void captures(void) {
+  const char *hay = "snowman: \xE2\x98\x83";
+  rure *re = rure_compile_must(".(.*(?P<snowman>\\p{So}))$");
+  rure_captures *caps = rure_captures_new(re);
+  CHECK(rure_find_captures(re, (const uint8_t *)hay, strlen(hay), 0, caps), "find_captures matches");
+  CHECK(rure_captures_len(caps) == 3, "captures_len 3");
+  CHECK(rure_capture_name_index(re, "snowman") == 2, "capture_name_index snowman = 2");
+  CHECK(rure_capture_name_index(re, "nope") == -1, "capture_name_index unknown = -1");
+  rure_match m = {0, 0};
+  CHECK(rure_captures_at(caps, 2, &m) && m.start == 9 && m.end == 12, "capture 2 at (9, 12)");
+  CHECK(rure_captures_at(caps, 0, &m) && m.start == 0 && m.end == 12, "capture 0 at (0, 12)");
+  CHECK(!rure_captures_at(caps, 3, &m), "capture 3 out of range");
+  CHECK(!rure_find_captures(re, (const uint8_t *)"x", 1, 0, caps), "find_captures no match");
+  CHECK(!rure_captures_at(caps, 0, &m), "no groups after a failed search");
+  rure_captures_free(caps);
+  rure_free(re);
+
+  re = rure_compile_must("\\w+(\\w)");
+  caps = rure_captures_new(re);
+  rure_iter *it = rure_iter_new(re);
+  const uint8_t *h2 = (const uint8_t *)"abc xyz";
+  CHECK(rure_iter_next(it, h2, 7, &m) && m.start == 0 && m.end == 3, "iter first (0, 3)");
+  CHECK(rure_iter_next_captures(it, h2, 7, caps), "iter_next_captures second match");
+  CHECK(rure_captures_at(caps, 1, &m) && m.start == 6 && m.end == 7, "second match group 1 at (6, 7)");
+  CHECK(!rure_iter_next_captures(it, h2, 7, caps), "iter_next_captures exhausted");
+  rure_iter_free(it);
+  rure_captures_free(caps);
+  rure_free(re);
+
+  re = rure_compile_must("(?P<year>\\d{4})-(?P<month>\\d{2})-(?P<day>\\d{2})");
+  rure_iter_capture_names *names = rure_iter_capture_names_new(re);
+  char *name = NULL;
+  const char *expect[] = {"", "year", "month", "day"};
+  for (int i = 0; i < 4; ++i)
+    CHECK(rure_iter_capture_names_next(names, &name) && strcmp(name, expect[i]) == 0, "capture name in order");
+  CHECK(!rure_iter_capture_names_next(names, &name), "capture names exhausted");
+  rure_iter_capture_names_free(names);
   rure_free(re);
 }
 
@@ -113,6 +154,7 @@ int main(void) {
   is_match_and_find();
   shortest();
   iter();
+  captures();
   flags();
   compile_errors();
   sets();

@@ -190,3 +190,84 @@ class NfaSim(object):
         if mode == "shortest":
             return me
         return (ms, me) if me is not None else None
+
+
+def next_utf8(t, i):
+    """utf8.rs:24-39"""
+    if i >= len(t):
+        return i + 1
+    b = t[i]
+    return i + (1 if b <= 0x7F else 2 if b <= 0xDF else 3 if b <= 0xEF else 4)
+
+
+class CapsSim(NfaSim):
+    """The captures kernel (nfa_scan.hip caps_kernel / pike_caps): thread
+    lists carry slot rows; an entry's Saves set its slots to the add position."""
+
+    def __init__(self, tables, saves, nslots):
+        NfaSim.__init__(self, tables, True)
+        self.save_off = [int(x) for x in saves[0]]
+        self.save_slot = [int(x) for x in saves[1]]
+        self.ns = nslots
+
+    def append_caps(self, cid, holds, prow, at, lst, members):
+        o0, o1 = self.cl_off[cid], self.cl_off[cid + 1]
+        for k in range(o0, o1):
+            leaf, cp = self.ent[k]
+            ok = (cp & 0xFF) & ~holds == 0
+            pv = cp >> 8
+            while ok and pv:
+                q = self.ent[o0 + pv - 1][1]
+                if (q & 0xFF) & ~holds == 0:
+                    ok = False
+                pv = q >> 8
+            if ok and leaf not in members:
+                members.add(leaf)
+                row = list(prow) if prow is not None else [None] * self.ns
+                for q in range(self.save_off[k], self.save_off[k + 1]):
+                    if self.save_slot[q] < self.ns:
+                        row[self.save_slot[q]] = at
+                lst.append((leaf, row))
+
+    def pike(self, t, start):
+        """Slots of the leftmost-first match in t from start, or None."""
+        info = self.info
+        if start > len(t):
+            return None
+        out = None
+        clist, cmem = [], set()
+        at = start
+        while True:
+            if not clist and (out is not None or (at != 0 and info["anchored"])):
+                break
+            if not clist or (not info["anchored"] and out is None):
+                self.append_caps(info["root"], look_holds(t, at, info), None, at, clist, cmem)
+            b = t[at] if at < len(t) else 0x100
+            hnx = look_holds(t, at + 1, info) if at < len(t) else 0
+            nlist, nmem = [], set()
+            for leaf, row in clist:
+                w0, cid, _ = self.leaves[leaf]
+                kind, lo, hi = w0 & 0xFF, (w0 >> 8) & 0xFF, (w0 >> 16) & 0xFF
+                if kind == 1:
+                    out = list(row)
+                    break
+                if lo <= b <= hi:
+                    self.append_caps(cid, hnx, row, at + 1, nlist, nmem)
+            if at >= len(t):
+                break
+            at += 1
+            clist, cmem = nlist, nmem
+        if out is None or out[0] is None or out[1] is None:
+            return None
+        return out
+
+    def captures(self, t, start, bounds):
+        """caps_kernel's dispatch given the DFA's bounds: (s, e) -> Pike VM
+        from s over t[..min(next_utf8(next_utf8(e)), len)]; None -> no match;
+        "quit" (or an anchored program) -> the whole text from start."""
+        if not self.info["anchored"] and bounds != "quit":
+            if bounds is None:
+                return None
+            s, e = bounds
+            return self.pike(t[:min(next_utf8(t, next_utf8(t, e)), len(t))], s)
+        return self.pike(t, start)

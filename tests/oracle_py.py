@@ -43,6 +43,7 @@ orc_shortest_match_at = _sig("orc_shortest_match_at", ctypes.c_int, VP, VP, ctyp
                              ctypes.POINTER(SZ))
 orc_is_match_at = _sig("orc_is_match_at", ctypes.c_int, VP, VP, ctypes.c_char_p, SZ, SZ)
 orc_captures_nfa = _sig("orc_captures_nfa", ctypes.c_int, VP, VP, ctypes.c_char_p, SZ, SZ, VP, SZ)
+orc_captures_at = _sig("orc_captures_at", ctypes.c_int, VP, VP, ctypes.c_char_p, SZ, SZ, VP, SZ)
 orc_find_iter = _sig("orc_find_iter", ctypes.c_int64, VP, VP, ctypes.c_char_p, SZ, VP, SZ)
 orc_many_matches_at = _sig("orc_many_matches_at", ctypes.c_int, VP, VP, ctypes.c_char_p, SZ, SZ, VP)
 orc_many_matches_nfa = _sig("orc_many_matches_nfa", ctypes.c_int, VP, VP, ctypes.c_char_p, SZ, SZ, VP)
@@ -117,9 +118,17 @@ class OracleRegex(object):
         return bool(orc_is_match_at(self._r, self._c, text, len(text), start))
 
     def captures(self, text, start=0):
+        """exec.rs:524-596 read_captures_at (the reference's dispatch)."""
+        return self._caps(orc_captures_at, text, start)
+
+    def captures_nfa(self, text, start=0):
+        """Forced Pike VM over the whole text."""
+        return self._caps(orc_captures_nfa, text, start)
+
+    def _caps(self, fn, text, start):
         n = 2 * self.ncaps
         slots = np.zeros(max(n, 1), dtype=np.uint64)
-        if not orc_captures_nfa(self._r, self._c, text, len(text), start, slots.ctypes.data, n):
+        if not fn(self._r, self._c, text, len(text), start, slots.ctypes.data, n):
             return None
         out = []
         for i in range(self.ncaps):

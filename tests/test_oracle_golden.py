@@ -26,11 +26,11 @@ def test_mat(v):
     assert o.find_nfa(text) == exp[0]
     assert o.is_match(text) == (exp[0] is not None)
     assert (o.shortest_match(text) is not None) == (exp[0] is not None)
-    caps = o.captures(text)
-    if caps is None:
-        assert exp == [None]
-    else:
-        assert caps[:len(exp)] == exp, (v["src"], caps, exp)
+    for caps in (o.captures(text), o.captures_nfa(text)):
+        if caps is None:
+            assert exp == [None]
+        else:
+            assert caps[:len(exp)] == exp, (v["src"], caps, exp)
 
 
 @pytest.mark.parametrize("v", V["matiter"], ids=_ids(V["matiter"]))
