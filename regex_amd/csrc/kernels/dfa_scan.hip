@@ -160,14 +160,50 @@ __global__ __launch_bounds__(256) void dfa_fwd_tile_kernel(BatchDev bt, FwdDfaDe
       const uint64_t an = (at + 128 < L128) ? at + 128 : at;
       RURE_LOAD_TILE(an)
       uint4 cur = buf[lane * 8 + sw];
-#pragma unroll 1
-      for (int m = 0; m < 8; ++m) {
-        uint4 nx = buf[lane * 8 + ((m + 1 < 8 ? m + 1 : 7) ^ sw)];
-        if (!L_.done) {
-          if (STRIDE == 1) chunk16<MODE>(L_, f, tab, cur, at + 16 * m);
-          else chunk16s<MODE, STRIDE>(L_, f, tab, tab16, cur, at + 16 * m);
+      if (STRIDE == 1) {
+        // Branch-free pass over the tile's 128 bytes through the LDS table:
+        // the sentinel row (`hot`) is absorbing, so a lane that leaves the
+        // hot states (or is done, or starts outside them) just rides the
+        // sentinel; the first chunk it entered the sentinel in and the state
+        // at that chunk's start are kept with selects.  Per byte the wave
+        // issues one v_mad + one ds_read_u8 and no scalar work.
+        const uint32_t hot = f.hot;
+        uint32_t t = (L_.done || L_.s >= hot) ? hot : L_.s;
+        uint32_t bad = (L_.done || L_.s < hot) ? 8u : 0u;  // first chunk to redo exactly
+        uint32_t sbad = L_.s;
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+          const uint4 nx = buf[lane * 8 + ((m + 1 < 8 ? m + 1 : 7) ^ sw)];
+          const uint32_t t0 = t;
+          t = fast4(t, cur.x, tab);
+          t = fast4(t, cur.y, tab);
+          t = fast4(t, cur.z, tab);
+          t = fast4(t, cur.w, tab);
+          const bool hit = (t == hot) & (t0 != hot);
+          bad = hit ? (uint32_t)m : bad;
+          sbad = hit ? t0 : sbad;
+          cur = nx;
         }
-        cur = nx;
+        if (bad < 8) {  // rare: redo exactly from the chunk that left the hot states
+          L_.s = sbad;
+#pragma unroll 1
+          for (uint32_t m = bad; m < 8 && !L_.done; ++m) {
+            const uint4 v = buf[lane * 8 + (m ^ sw)];
+            const uint32_t words[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll 1
+            for (int j = 0; j < 16 && !L_.done; ++j)
+              step1<MODE>(L_, f, tab, (words[j >> 2] >> ((j & 3) * 8)) & 0xFF, at + 16 * m + j);
+          }
+        } else if (!L_.done) {
+          L_.s = t;
+        }
+      } else {
+#pragma unroll 1
+        for (int m = 0; m < 8; ++m) {
+          uint4 nx = buf[lane * 8 + ((m + 1 < 8 ? m + 1 : 7) ^ sw)];
+          if (!L_.done) chunk16s<MODE, STRIDE>(L_, f, tab, tab16, cur, at + 16 * m);
+          cur = nx;
+        }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
