@@ -149,6 +149,26 @@ int rure_amd_set_matches_batch(rure_set *re, const rure_amd_batch *batch, uint64
 int rure_amd_find_iter_batch(rure *re, const rure_amd_batch *batch, uint64_t *counts, rure_match *matches,
                              size_t capacity, uint64_t *total, void *stream);
 
+/* Batched replacen with a literal replacement (bytes::Regex::replacen's
+ * no-expansion path, re_bytes.rs:489-512): in every haystack the first
+ * `limit` matches (0 = all) of the batched find_iter are replaced by
+ * rep[0..rep_len) (host memory; `$` is not expanded, as with NoExpand).
+ * out_offsets (device, n + 1) = the output layout (exclusive sums of the
+ * output lengths); out (device) receives the concatenated outputs, at most
+ * out_capacity bytes; *total (device) = the bytes needed (call again with a
+ * larger buffer if it exceeds out_capacity).  Synchronises the stream once
+ * (to size the match buffer). */
+int rure_amd_replace_batch(rure *re, const rure_amd_batch *batch, const uint8_t *rep, size_t rep_len,
+                           size_t limit, uint8_t *out, uint64_t *out_offsets, size_t out_capacity,
+                           uint64_t *total, void *stream);
+/* Batched split / splitn (re_bytes.rs:699-749): the fields between matches
+ * as (start, end) records relative to each haystack, concatenated;
+ * counts[i] (device) = fields of haystack i; at most `limit` fields per
+ * haystack with SplitN's rule (the last is the rest of the haystack);
+ * limit = SIZE_MAX for split.  *total (device) = number of fields. */
+int rure_amd_split_batch(rure *re, const rure_amd_batch *batch, size_t limit, uint64_t *counts,
+                         rure_match *pieces, size_t capacity, uint64_t *total, void *stream);
+
 /* Batched rure_find_captures: slots[i * 2 * ngroups + 2 * g + {0, 1}]
  * (device, size_t) = start / end of group g in haystack i, SIZE_MAX where the
  * group did not participate or the haystack has no match.  ngroups =

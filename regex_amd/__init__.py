@@ -15,7 +15,7 @@ import ctypes
 
 from . import _native as N
 
-__all__ = ["Regex", "RegexSet", "Error", "NONE"]
+__all__ = ["Regex", "RegexSet", "Error", "NoExpand", "NONE"]
 
 NONE = N.NONE
 
@@ -91,6 +91,90 @@ def _stream_ptr(stream):
     return ctypes.c_void_p(s.cuda_stream)
 
 
+class NoExpand(object):
+    """A replacement used literally, `$` included (re_bytes.rs:1014-1032)."""
+
+    def __init__(self, rep):
+        self.rep = bytes(rep)
+
+
+def _cap_letter(b):
+    return 48 <= b <= 57 or 97 <= b <= 122 or 65 <= b <= 90 or b == 95
+
+
+def _find_cap_ref(rep):
+    """expand.rs:127-166: (name or number, end) of the reference at rep[0]."""
+    if len(rep) <= 1 or rep[0] != 0x24:
+        return None
+    i, brace = 1, False
+    if rep[i] == 0x7B:
+        brace, i = True, 2
+    end = i
+    while end < len(rep) and _cap_letter(rep[end]):
+        end += 1
+    if end == i:
+        return None
+    cap = rep[i:end].decode("ascii")
+    if brace:
+        if end >= len(rep) or rep[end] != 0x7D:
+            return None
+        end += 1
+    try:
+        ref = int(cap)
+        if ref >= 1 << 32:
+            ref = cap
+    except ValueError:
+        ref = cap
+    return ref, end
+
+
+def expand(groups, names, rep, text):
+    """expand.rs:50-91 (expand_bytes): `$N`, `$name`, `${...}` and `$$`."""
+    out = bytearray()
+    index = {n: i for i, n in enumerate(names) if n}
+    while rep:
+        i = rep.find(b"$")
+        if i < 0:
+            break
+        out += rep[:i]
+        rep = rep[i:]
+        if len(rep) > 1 and rep[1] == 0x24:
+            out += b"$"
+            rep = rep[2:]
+            continue
+        ref = _find_cap_ref(rep)
+        if ref is None:
+            out += b"$"
+            rep = rep[1:]
+            continue
+        cap, end = ref
+        rep = rep[end:]
+        g = cap if isinstance(cap, int) else index.get(cap)
+        if g is not None and g < len(groups) and groups[g] is not None:
+            out += text[groups[g][0]:groups[g][1]]
+    out += rep
+    return bytes(out)
+
+
+class _Split(object):
+    """re_bytes.rs:699-721 over the match list of a find_iter."""
+
+    def __init__(self, text, matches):
+        self.text, self.ms, self.last = text, iter(matches), 0
+
+    def next(self):
+        m = next(self.ms, None)
+        if m is None:
+            if self.last >= len(self.text):
+                return None
+            s = self.text[self.last:]
+            self.last = len(self.text)
+            return s
+        s = self.text[self.last:m[0]]
+        self.last = m[1]
+        return s
+
+
 class Regex(object):
     """`regex::bytes::Regex` (re_bytes.rs:78-605): Unicode on by default."""
 
@@ -136,6 +220,19 @@ class Regex(object):
         return None
 
     def find_iter(self, text):
+        """bytes::Regex::find_iter (re_trait.rs:197-221): one batched launch
+        over the staged haystack."""
+        import torch
+        text = bytes(text)
+        dev = torch.device("cuda", torch.cuda.current_device())
+        buf = torch.frombuffer(bytearray(text) + bytearray(16), dtype=torch.uint8).to(dev)
+        _, m = self.find_iter_batch(buf, stride=len(text), length=len(text), count=1)
+        return [(int(a), int(b)) for a, b in m.cpu().tolist()]
+
+    def iter_rure(self, text):
+        """The C API's iteration (rure_iter_next, regex-capi/src/rure.rs:322-360:
+        after an empty match the next search starts one past the previous
+        search start, which can revisit positions find_iter skips)."""
         it = N.rure_iter_new(self._re)
         out = []
         try:
@@ -159,7 +256,25 @@ class Regex(object):
             N.rure_captures_free(caps)
 
     def captures_iter(self, text):
-        """Successive captures, iterated as rure_iter_next_captures does."""
+        """bytes::Regex::captures_iter (CaptureMatches, re_trait.rs:243-273)."""
+        out, last_end, last_match = [], 0, None
+        while last_end <= len(text):
+            g = self.captures(text, last_end)
+            if g is None:
+                break
+            s, e = g[0]
+            if s == e:
+                last_end = e + 1
+                if last_match == e:
+                    continue
+            else:
+                last_end = e
+            last_match = e
+            out.append(g)
+        return out
+
+    def captures_iter_rure(self, text):
+        """Successive captures as rure_iter_next_captures iterates them."""
         it = N.rure_iter_new(self._re)
         caps = N.rure_captures_new(self._re)
         out = []
@@ -190,7 +305,116 @@ class Regex(object):
         i = N.rure_capture_name_index(self._re, name.encode("utf-8"))
         return None if i < 0 else i
 
+    # ------------------------------------ replace / split (re_bytes.rs:316-535)
+    def replacen(self, text, limit, rep):
+        """Replaces the first `limit` matches (0 = all).  `rep` is bytes with
+        `$` expansion, a NoExpand, or a function f(groups, text) -> bytes (the
+        reference's FnMut(&Captures) replacer)."""
+        text = bytes(text)
+        if isinstance(rep, NoExpand) or (isinstance(rep, (bytes, bytearray)) and b"$" not in rep):
+            lit = rep.rep if isinstance(rep, NoExpand) else bytes(rep)
+            ms = self.find_iter(text)
+            if limit:
+                ms = ms[:limit]
+            out, last = bytearray(), 0
+            for s, e in ms:
+                out += text[last:s]
+                out += lit
+                last = e
+            return bytes(out + text[last:])
+        caps = self.captures_iter(text)
+        if limit:
+            caps = caps[:limit]
+        names = self.capture_names() if not callable(rep) else None
+        out, last = bytearray(), 0
+        for g in caps:
+            s, e = g[0]
+            out += text[last:s]
+            out += rep(g, text) if callable(rep) else expand(g, names, bytes(rep), text)
+            last = e
+        return bytes(out + text[last:])
+
+    def replace(self, text, rep):
+        return self.replacen(text, 1, rep)
+
+    def replace_all(self, text, rep):
+        return self.replacen(text, 0, rep)
+
+    def split(self, text):
+        """Fields between matches (re_bytes.rs:699-721)."""
+        text = bytes(text)
+        sp = _Split(text, self.find_iter(text))
+        out = []
+        while True:
+            x = sp.next()
+            if x is None:
+                return out
+            out.append(x)
+
+    def splitn(self, text, limit):
+        """At most `limit` fields, the last being the rest (re_bytes.rs:729-749)."""
+        text = bytes(text)
+        sp = _Split(text, self.find_iter(text))
+        out, n = [], limit
+        while n:
+            n -= 1
+            if n == 0:
+                out.append(text[sp.last:])
+                break
+            x = sp.next()
+            if x is None:
+                break
+            out.append(x)
+        return out
+
     # -------------------------------------------- batches (device tensors)
+    def replace_batch(self, haystack, rep, limit=0, offsets=None, stride=None, length=None, count=None,
+                      stream=None):
+        """replacen over every haystack with a literal replacement (`$` is
+        not expanded; NoExpand semantics).  Returns (out, out_offsets): the
+        concatenated outputs (uint8) and n+1 int64 offsets into them."""
+        import torch
+        if isinstance(rep, NoExpand):
+            rep = rep.rep
+        rep = bytes(rep)
+        b = _batch(haystack, offsets, stride, length, count, 0)
+        dev = haystack.device
+        ooff = torch.empty((b.count + 1,), dtype=torch.int64, device=dev)
+        total = torch.zeros((1,), dtype=torch.int64, device=dev)
+        cap = haystack.numel() + 1024
+        while True:
+            out = torch.empty((max(cap, 16) + 16,), dtype=torch.uint8, device=dev)
+            _check(N.rure_amd_replace_batch(self._re, ctypes.byref(b), rep, len(rep), limit,
+                                            ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(ooff.data_ptr()), cap,
+                                            ctypes.c_void_p(total.data_ptr()), _stream_ptr(stream)), "replace_batch")
+            (stream or torch.cuda.current_stream()).synchronize()
+            t = int(total.item())
+            if t <= cap:
+                return out[:t], ooff
+            cap = t
+
+    def split_batch(self, haystack, limit=None, offsets=None, stride=None, length=None, count=None,
+                    capacity=None, stream=None):
+        """split (limit None) / splitn over every haystack.  Returns (counts,
+        pieces): fields per haystack and (total, 2) int64 (start, end)."""
+        import torch
+        b = _batch(haystack, offsets, stride, length, count, 0)
+        dev = haystack.device
+        lim = (1 << 64) - 1 if limit is None else limit
+        counts = torch.empty((b.count,), dtype=torch.int64, device=dev)
+        total = torch.zeros((1,), dtype=torch.int64, device=dev)
+        cap = capacity if capacity is not None else max(1024, 4 * b.count)
+        while True:
+            out = torch.empty((max(cap, 1), 2), dtype=torch.int64, device=dev)
+            _check(N.rure_amd_split_batch(self._re, ctypes.byref(b), lim, ctypes.c_void_p(counts.data_ptr()),
+                                          ctypes.c_void_p(out.data_ptr()), cap, ctypes.c_void_p(total.data_ptr()),
+                                          _stream_ptr(stream)), "split_batch")
+            (stream or torch.cuda.current_stream()).synchronize()
+            t = int(total.item())
+            if t <= cap or capacity is not None:
+                return counts, out[:min(t, cap)]
+            cap = t
+
     def captures_batch(self, haystack, offsets=None, stride=None, length=None, count=None,
                        start=0, out=None, stream=None):
         """Captures per haystack: an (n, groups, 2) int64 tensor of

@@ -117,6 +117,10 @@ rure_amd_shortest_match_batch = _sig("rure_amd_shortest_match_batch", ctypes.c_i
                                      ctypes.POINTER(RureBatch), VP, VP)
 rure_amd_set_matches_batch = _sig("rure_amd_set_matches_batch", ctypes.c_int, VP, ctypes.POINTER(RureBatch),
                                   VP, VP)
+rure_amd_replace_batch = _sig("rure_amd_replace_batch", ctypes.c_int, VP, ctypes.POINTER(RureBatch), ctypes.c_char_p,
+                              c_size, c_size, VP, VP, c_size, VP, VP)
+rure_amd_split_batch = _sig("rure_amd_split_batch", ctypes.c_int, VP, ctypes.POINTER(RureBatch), c_size, VP, VP,
+                            c_size, VP, VP)
 rure_amd_captures_batch = _sig("rure_amd_captures_batch", ctypes.c_int, VP, ctypes.POINTER(RureBatch), VP, VP)
 rure_amd_captures_len = _sig("rure_amd_captures_len", c_size, VP)
 rure_amd_nfa_saves_export = _sig("rure_amd_nfa_saves_export", ctypes.c_int, VP, VP, VP, ctypes.POINTER(c_size))

@@ -122,6 +122,20 @@ __host__ __device__ inline size_t caps_wave_bytes(uint32_t nleaves, uint32_t nsl
 hipError_t launch_captures(const BatchDev &b, const NfaDev &n, const uint64_t *found, uint64_t *slots,
                            uint32_t nslots, void *scratch, hipStream_t st, int grid);
 
+// replacen / split over find_iter output (replace_scan.hip).  counts / moff:
+// matches per haystack and their exclusive sums; m: the records.
+hipError_t exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, hipStream_t st);
+hipError_t launch_replace_plan(const BatchDev &b, const uint64_t *counts, const uint64_t *moff, const uint64_t *m,
+                               uint64_t limit, uint64_t rep_len, int64_t *shift, uint64_t *out_len, hipStream_t st,
+                               int cus);
+hipError_t launch_replace_copy(const BatchDev &b, const uint64_t *ooff, const uint64_t *counts, const uint64_t *moff,
+                               const uint64_t *m, const int64_t *shift, uint64_t limit, const uint8_t *rep,
+                               uint64_t rep_len, uint8_t *out, uint64_t cap, uint64_t total_hint, hipStream_t st,
+                               int cus);
+hipError_t launch_split(const BatchDev &b, const uint64_t *counts, const uint64_t *moff, const uint64_t *m,
+                        uint64_t lim, uint64_t *fields, uint64_t *foff, uint64_t *pieces, uint64_t cap,
+                        uint64_t nmatches, hipStream_t st, int cus);
+
 // Batched find_iter (iter_scan.hip).  counts: per haystack; matches:
 // (start, end) pairs, the first `cap` written; total: number of matches.
 struct IterOut {

@@ -1354,20 +1354,15 @@ int rure_amd_set_matches_batch(rure_set *rs, const rure_amd_batch *batch, uint64
   return RURE_AMD_OK;
 }
 
-int rure_amd_find_iter_batch(rure *re, const rure_amd_batch *batch, uint64_t *counts, rure_match *matches,
-                             size_t capacity, uint64_t *total, void *stream) {
-  BatchDev b;
-  if (!re || !to_batch(batch, &b) || (!counts && b.count) || !total || (!matches && capacity))
-    return RURE_AMD_ERR_ARG;
-  std::string err;
-  DevTables *t = regex_device(re, &err);
-  if (!t) return err.rfind("HIP", 0) == 0 ? RURE_AMD_ERR_HIP : RURE_AMD_ERR_DFA;
+namespace {
+
+// The batched find_iter (re_trait.rs:197-221) on one stream.
+hipError_t run_find_iter(rure *re, DevTables *t, const BatchDev &b, const IterOut &o, hipStream_t st,
+                         std::string *err) {
   // Chunked speculative iteration needs a DFA that cannot quit and a pattern
   // without assertions (see iter_scan.hip); otherwise one wave per haystack.
   const FwdDfaDev *fi = nullptr;
-  if (t->has_dfa && !t->quit_possible && re->nfa_ok && re->nt.looks_used == 0) fi = iter_device(re, *t, &err);
-  IterOut o{counts, (uint64_t *)matches, capacity, total};
-  hipError_t e;
+  if (t->has_dfa && !t->quit_possible && re->nfa_ok && re->nt.looks_used == 0) fi = iter_device(re, *t, err);
   if (fi) {
     uint64_t chunk = ~0ull >> 2;
     if (!b.offs && b.length > b.start && b.count) {
@@ -1376,11 +1371,130 @@ int rure_amd_find_iter_batch(rure *re, const rure_amd_batch *batch, uint64_t *co
       const uint64_t per_h = (target + b.count - 1) / b.count;
       chunk = odd_lines(std::max<uint64_t>(4096, (span + per_h - 1) / per_h));
     }
-    e = launch_find_iter(b, fi, t->r, &t->n, true, chunk, o, (hipStream_t)stream, t->cus);
-  } else {
-    if (!re->nfa_ok) return RURE_AMD_ERR_DFA;
-    e = launch_find_iter(b, t->has_dfa ? &t->f : nullptr, t->r, &t->n, false, 0, o, (hipStream_t)stream, t->cus);
+    return launch_find_iter(b, fi, t->r, &t->n, true, chunk, o, st, t->cus);
   }
+  if (!re->nfa_ok) return hipErrorInvalidValue;
+  return launch_find_iter(b, t->has_dfa ? &t->f : nullptr, t->r, &t->n, false, 0, o, st, t->cus);
+}
+
+// find_iter into internal device buffers: counts (n + 1, last 0), their
+// exclusive sums moff (n + 1) and the match records; reads the total on the
+// host (one sync) and reruns once with an exact buffer if the guess was short.
+struct IterBufs {
+  uint64_t *counts = nullptr, *moff = nullptr, *m = nullptr, *total = nullptr;
+  uint64_t nm = 0;
+  hipStream_t st = nullptr;
+  ~IterBufs() {
+    if (counts) (void)hipFreeAsync(counts, st);
+    if (moff) (void)hipFreeAsync(moff, st);
+    if (m) (void)hipFreeAsync(m, st);
+    if (total) (void)hipFreeAsync(total, st);
+  }
+};
+
+hipError_t iter_to_device(rure *re, DevTables *t, const BatchDev &b, hipStream_t st, IterBufs *ib, std::string *err) {
+  ib->st = st;
+  hipError_t e;
+  const size_t n = b.count;
+  if ((e = hipMallocAsync((void **)&ib->counts, (n + 1) * 8, st)) != hipSuccess) return e;
+  if ((e = hipMallocAsync((void **)&ib->moff, (n + 1) * 8, st)) != hipSuccess) return e;
+  if ((e = hipMallocAsync((void **)&ib->total, 8, st)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(ib->counts, 0, (n + 1) * 8, st)) != hipSuccess) return e;
+  const uint64_t bytes = b.offs ? 0 : (uint64_t)b.count * b.length;
+  uint64_t cap = std::max<uint64_t>(1024, bytes / 64 + 2 * n);
+  for (int pass = 0; pass < 2; ++pass) {
+    if ((e = hipMallocAsync((void **)&ib->m, cap * 16, st)) != hipSuccess) return e;
+    IterOut o{ib->counts, ib->m, cap, ib->total};
+    if ((e = run_find_iter(re, t, b, o, st, err)) != hipSuccess) return e;
+    uint64_t tot = 0;
+    if ((e = hipMemcpyAsync(&tot, ib->total, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+    ib->nm = tot;
+    if (tot <= cap) break;
+    (void)hipFreeAsync(ib->m, st);
+    ib->m = nullptr;
+    cap = tot;
+  }
+  return exclusive_scan_u64(ib->counts, ib->moff, n + 1, st);
+}
+
+}  // namespace
+
+int rure_amd_find_iter_batch(rure *re, const rure_amd_batch *batch, uint64_t *counts, rure_match *matches,
+                             size_t capacity, uint64_t *total, void *stream) {
+  BatchDev b;
+  if (!re || !to_batch(batch, &b) || (!counts && b.count) || !total || (!matches && capacity))
+    return RURE_AMD_ERR_ARG;
+  std::string err;
+  DevTables *t = regex_device(re, &err);
+  if (!t) return err.rfind("HIP", 0) == 0 ? RURE_AMD_ERR_HIP : RURE_AMD_ERR_DFA;
+  if (!t->has_dfa && !re->nfa_ok) return RURE_AMD_ERR_DFA;
+  IterOut o{counts, (uint64_t *)matches, capacity, total};
+  return run_find_iter(re, t, b, o, (hipStream_t)stream, &err) == hipSuccess ? RURE_AMD_OK : RURE_AMD_ERR_HIP;
+}
+
+int rure_amd_replace_batch(rure *re, const rure_amd_batch *batch, const uint8_t *rep, size_t rep_len, size_t limit,
+                           uint8_t *out, uint64_t *out_offsets, size_t out_capacity, uint64_t *total, void *stream) {
+  BatchDev b;
+  if (!re || !to_batch(batch, &b) || !out_offsets || !total || (!out && out_capacity) || (!rep && rep_len))
+    return RURE_AMD_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  if (b.count == 0) return hipMemsetAsync(out_offsets, 0, 8, st) == hipSuccess &&
+                           hipMemsetAsync(total, 0, 8, st) == hipSuccess ? RURE_AMD_OK : RURE_AMD_ERR_HIP;
+  std::string err;
+  DevTables *t = regex_device(re, &err);
+  if (!t) return err.rfind("HIP", 0) == 0 ? RURE_AMD_ERR_HIP : RURE_AMD_ERR_DFA;
+  if (!t->has_dfa && !re->nfa_ok) return RURE_AMD_ERR_DFA;
+  IterBufs ib;
+  int64_t *shift = nullptr;
+  uint64_t *olen = nullptr;
+  uint8_t *drep = nullptr;
+  const uint64_t lim = limit == 0 ? ~0ull : (uint64_t)limit;  // replacen: 0 = all
+  hipError_t e = iter_to_device(re, t, b, st, &ib, &err);
+  if (e == hipSuccess) e = hipMallocAsync((void **)&shift, std::max<uint64_t>(ib.nm, 1) * 8, st);
+  if (e == hipSuccess) e = hipMallocAsync((void **)&olen, (b.count + 1) * 8, st);
+  if (e == hipSuccess) e = hipMallocAsync((void **)&drep, std::max<size_t>(rep_len, 1), st);
+  if (e == hipSuccess && rep_len) e = hipMemcpyAsync(drep, rep, rep_len, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemsetAsync(olen + b.count, 0, 8, st);
+  if (e == hipSuccess)
+    e = launch_replace_plan(b, ib.counts, ib.moff, ib.m, lim, rep_len, shift, olen, st, t->cus);
+  if (e == hipSuccess) e = exclusive_scan_u64(olen, out_offsets, b.count + 1, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(total, out_offsets + b.count, 8, hipMemcpyDeviceToDevice, st);
+  if (e == hipSuccess && out_capacity) {
+    const uint64_t hint = b.offs ? out_capacity : std::min<uint64_t>(out_capacity, b.count * b.length + ib.nm * rep_len);
+    e = launch_replace_copy(b, out_offsets, ib.counts, ib.moff, ib.m, shift, lim, drep, rep_len, out, out_capacity,
+                            hint, st, t->cus);
+  }
+  if (shift) (void)hipFreeAsync(shift, st);
+  if (olen) (void)hipFreeAsync(olen, st);
+  if (drep) (void)hipFreeAsync(drep, st);
+  return e == hipSuccess ? RURE_AMD_OK : RURE_AMD_ERR_HIP;
+}
+
+int rure_amd_split_batch(rure *re, const rure_amd_batch *batch, size_t limit, uint64_t *counts, rure_match *pieces,
+                         size_t capacity, uint64_t *total, void *stream) {
+  BatchDev b;
+  if (!re || !to_batch(batch, &b) || (!counts && b.count) || !total || (!pieces && capacity))
+    return RURE_AMD_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  if (b.count == 0) return hipMemsetAsync(total, 0, 8, st) == hipSuccess ? RURE_AMD_OK : RURE_AMD_ERR_HIP;
+  std::string err;
+  DevTables *t = regex_device(re, &err);
+  if (!t) return err.rfind("HIP", 0) == 0 ? RURE_AMD_ERR_HIP : RURE_AMD_ERR_DFA;
+  if (!t->has_dfa && !re->nfa_ok) return RURE_AMD_ERR_DFA;
+  IterBufs ib;
+  uint64_t *fields = nullptr, *foff = nullptr;
+  hipError_t e = iter_to_device(re, t, b, st, &ib, &err);
+  if (e == hipSuccess) e = hipMallocAsync((void **)&fields, (b.count + 1) * 8, st);
+  if (e == hipSuccess) e = hipMallocAsync((void **)&foff, (b.count + 1) * 8, st);
+  if (e == hipSuccess) e = hipMemsetAsync(fields + b.count, 0, 8, st);
+  if (e == hipSuccess)
+    e = launch_split(b, ib.counts, ib.moff, ib.m, (uint64_t)limit, fields, foff, (uint64_t *)pieces, capacity, ib.nm,
+                     st, t->cus);
+  if (e == hipSuccess) e = hipMemcpyAsync(counts, fields, b.count * 8, hipMemcpyDeviceToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(total, foff + b.count, 8, hipMemcpyDeviceToDevice, st);
+  if (fields) (void)hipFreeAsync(fields, st);
+  if (foff) (void)hipFreeAsync(foff, st);
   return e == hipSuccess ? RURE_AMD_OK : RURE_AMD_ERR_HIP;
 }
 

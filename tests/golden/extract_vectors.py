@@ -9,7 +9,8 @@ unicode, word_boundary, word_boundary_ascii, plus its own inline mat!s) and the
 bench known answers (bench/src/sherlock.rs, bench/src/regexdna.rs,
 examples/regexdna-output.txt), and writes:
 
-  tests/golden/reference_vectors.json   mat!/matiter!/matset!/nomatset!/ismatch!/noparse!
+  tests/golden/reference_vectors.json   mat!/matiter!/matset!/nomatset!/ismatch!/noparse!,
+                                        replace!/expand!/split!
   tests/golden/known_counts.json        find_iter counts on the bench corpora
   tests/golden/sherlock.txt.gz          corpus data (bench/src/data/sherlock.txt)
   tests/golden/regexdna-input.txt.gz    corpus data (examples/regexdna-input.txt)
@@ -28,7 +29,7 @@ OUT = os.path.dirname(os.path.abspath(__file__))
 MODULES = ["api", "bytes", "crazy", "flags", "fowler", "multiline", "noparse", "regression",
            "replace", "set", "shortest_match", "suffix_reverse", "unicode", "word_boundary",
            "word_boundary_ascii"]
-MACROS = ("mat", "matiter", "matset", "nomatset", "ismatch", "noparse")
+MACROS = ("mat", "matiter", "matset", "nomatset", "ismatch", "noparse", "replace", "expand", "split")
 
 
 class Lit(object):
@@ -129,6 +130,10 @@ def split_args(s, i):
 
 def parse_value(a):
     a = a.strip()
+    m = re.match(r"^(t|no_expand)!\((.*)\)$", a, re.S)
+    if m:  # tests/macros_bytes.rs:3,8-13: text as bytes; NoExpand(text)
+        lit = parse_value(m.group(2))
+        return ("literal" if m.group(1) == "no_expand" else "expand", lit)
     if a.startswith("R(") and a.endswith(")"):
         return parse_value(a[2:-1])
     if re.match(r'^(b?r#*"|b?")', a):
@@ -165,7 +170,7 @@ def scan_file(path, vectors, skipped):
         try:
             raw, _ = split_args(s, m.end())
             name = raw[0]
-            vals = [parse_value(x) for x in raw[1:]]
+            vals = [parse_value(x) for x in raw[(2 if kind == "replace" else 1):]]
         except Exception as e:  # noqa
             skipped.append("%s:%d %s (%s)" % (base, line, kind, e))
             continue
@@ -187,6 +192,17 @@ def scan_file(path, vectors, skipped):
                                        "text": vals[1].as_bytes().hex(), "expect": vals[2]})
         elif kind == "noparse":
             vectors["noparse"].append({"name": name, "src": src, "re": vals[0].val})
+        elif kind == "replace":  # tests/replace.rs:1-10
+            which, (re_, text, rep, result) = raw[1].strip(), vals
+            vectors["replace"].append({"name": name, "src": src, "which": which, "re": re_.val,
+                                       "text": text.as_bytes().hex(), "mode": rep[0],
+                                       "rep": rep[1].as_bytes().hex(), "result": result.as_bytes().hex()})
+        elif kind == "expand":  # tests/macros_bytes.rs:26-38
+            vectors["expand"].append({"name": name, "src": src, "re": vals[0].val, "text": vals[1].as_bytes().hex(),
+                                      "template": vals[2].as_bytes().hex(), "result": vals[3].as_bytes().hex()})
+        elif kind == "split":  # tests/macros.rs:140-149
+            vectors["split"].append({"name": name, "src": src, "re": vals[0].val, "text": vals[1].as_bytes().hex(),
+                                     "fields": [f[1].as_bytes().hex() for f in vals[2]]})
 
 
 def bench_counts(path, macro, corpus):
@@ -204,7 +220,8 @@ def bench_counts(path, macro, corpus):
 
 
 def main():
-    vectors = {k: [] for k in ("mat", "matiter", "matset", "nomatset", "ismatch", "noparse")}
+    vectors = {k: [] for k in ("mat", "matiter", "matset", "nomatset", "ismatch", "noparse", "replace", "expand",
+                               "split")}
     skipped = []
     for mod in MODULES:
         scan_file(os.path.join(REF, "tests", mod + ".rs"), vectors, skipped)

@@ -125,15 +125,21 @@ def test_captures_scratch_path(cuda):
 
 
 def test_captures_iter_vs_oracle(cuda):
-    re = R.Regex(r"(\w)(\d)?")
-    o = OracleRegex(re)
-    t = b"a1 b c22 d" * 3 + "é3".encode()
-    exp, last_end, last_match = [], 0, None   # rure.rs:363-397 over the oracle
+    import replace_ref as RR
+    for pat, t in ((r"(\w)(\d)?", b"a1 b c22 d" * 3 + "\u00e93".encode()),
+                   (r"\b", b"\nb1ybby2\n y\nb" + "\u00e9\u00e9".encode() + b"y")):
+        re = R.Regex(pat)
+        assert re.captures_iter(t) == RR.captures_iter(OracleRegex(re), t), pat
+
+
+def rure_iter_oracle(o, t, caps=False):
+    """regex-capi/src/rure.rs:322-397 over the oracle."""
+    out, last_end, last_match = [], 0, None
     while last_end <= len(t):
-        c = o.captures(t, last_end)
-        if c is None:
+        g = o.captures(t, last_end) if caps else o.find(t, last_end)
+        if g is None:
             break
-        s, e = c[0]
+        s, e = g[0] if caps else g
         if s == e:
             last_end += 1
             if last_match == e:
@@ -141,8 +147,23 @@ def test_captures_iter_vs_oracle(cuda):
         else:
             last_end = e
         last_match = e
-        exp.append(c)
-    assert re.captures_iter(t) == exp
+        out.append(g)
+    return out
+
+
+def test_c_api_iteration_differs_from_find_iter(cuda):
+    """After an empty match rure_iter_next restarts one past the previous
+    search start, not past the match: with a Unicode word boundary next to
+    non-ASCII bytes (the DFA reads only the byte before the start) it revisits
+    an earlier position, which find_iter never does.  Both reproduced."""
+    t = b"\nb1ybby2\n y\nb" + "\u00e9\u00e9".encode() + b"y"
+    re = R.Regex(r"\b")
+    o = OracleRegex(re)
+    assert re.find_iter(t) == o.find_iter(t)
+    assert re.iter_rure(t) == rure_iter_oracle(o, t)
+    assert re.captures_iter_rure(t) == rure_iter_oracle(o, t, caps=True)
+    assert re.iter_rure(t)[-3:] == [(18, 18), (17, 17), (18, 18)]
+    assert re.find_iter(t)[-1] == (18, 18) and (17, 17) not in re.find_iter(t)
 
 
 def test_reference_quirk_on_gpu(cuda):
