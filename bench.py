@@ -11,7 +11,9 @@ exchange the path has: an all-gather (RCCL) of the compacted match records.
 
 Other configs (for DESIGN.md's table; same timing protocol):
   c3  regex-dna: `>[^\\n]*\\n|\\n` find_iter over the input replicated to
-      2 GiB, then the 9 variant patterns' find_iter over the stripped 2 GiB
+      2 GiB, then the 9 variant patterns' find_iter over the stripped 2 GiB;
+      for N > 1 each logical stream is cut into N contiguous spans (strong
+      scaling) with one exit exchange (all-gather) per step
   c4  RegexSet of 64 patterns over 10M synthetic log lines (one mask per line)
   c5  `\\w+@\\w+\\.\\w+` find over one 16 GiB haystack per GPU, one planted
       match in its last MiB; records gathered across ranks
@@ -301,27 +303,74 @@ def run_c3(ctx):
     assert M == kc["stripped_len"] * copies, (M, kc["stripped_len"] * copies)
     variants = [R.Regex(v["re"]) for v in kc["variants"]]
     vout = torch.empty((1 << 20, 2), dtype=torch.int64, device=ctx.dev)
-    vcnt = [torch.empty(1, dtype=torch.int64, device=ctx.dev) for _ in variants]
-    vtot = [torch.empty(1, dtype=torch.int64, device=ctx.dev) for _ in variants]
+    # one pass = one find_iter over the rank's span of one logical haystack
+    # (the whole haystack at N = 1); SURVEY §8e: contiguous spans, one exit
+    # exchange per step, recomputation only where a match crosses a cut
+    from regex_amd.dist import _entry_key, iterate_spans, span_bounds
+    passes = [(strip, big, N, spans)] + [(v, seq, M, vout) for v in variants]
+    P, W, rk = len(passes), ctx.world, ctx.rank
+    pcount = torch.zeros((P,), dtype=torch.int64, device=ctx.dev)
+    pexit = torch.zeros((P, 3), dtype=torch.int64, device=ctx.dev)
+    sp = R._stream_ptr(ctx.stream)
+    stats = {"recomputed": 0}
+
+    def span_raw(j, i, entry):
+        re_, buf, L, out = passes[j]
+        lo, hi = span_bounds(L, W, i)
+        ent = ctypes.c_void_p(entry.data_ptr()) if entry is not None else None
+        rc = NN.rure_amd_find_iter_span(re_._re, ctypes.c_void_p(buf.data_ptr()), L, lo, hi, ent,
+                                        ctypes.c_void_p(pcount[j:].data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                        out.shape[0], ctypes.c_void_p(pexit[j].data_ptr()), sp)
+        assert rc == 0
+
+    def repair(j):
+        # rare: a match crosses a cut of pass j; the generic exchange loop
+        stats["recomputed"] += 1
+
+        def run(i, entry):
+            e = None if entry is None else torch.tensor(entry, dtype=torch.int64, device=ctx.dev)
+            span_raw(j, i, e)
+            return pcount[j:j + 1], None, pexit[j]
+
+        def gather(mine):
+            parts = [torch.empty(3, dtype=torch.int64, device=ctx.dev) for _ in range(W)]
+            ctx.dist.all_gather(parts, mine[rk].clone())
+            return [q.tolist() for q in parts]
+
+        iterate_spans(run, W, [rk], gather)
+
+    def exchange():
+        parts = [torch.empty_like(pexit) for _ in range(W)]
+        ctx.dist.all_gather(parts, pexit)
+        ex = torch.stack(parts).cpu().tolist()     # (W, P, 3): one sync per step
+        for j in range(P):
+            if any(_entry_key(ex[i - 1][j]) != ("fresh",) for i in range(1, W)):
+                repair(j)
 
     def strip_pass():
-        find_iter_raw(strip, big, N, spans, cnt, tot)
+        span_raw(0, rk, None)
 
     def variant_pass():
-        for v, c, t in zip(variants, vcnt, vtot):
-            find_iter_raw(v, seq, M, vout, c, t)
+        for j in range(1, P):
+            span_raw(j, rk, None)
 
     def step():
         strip_pass()
         variant_pass()
+        if W > 1:
+            exchange()
 
     for _ in range(ctx.args.warmup):
         step()
     torch.cuda.synchronize()
+    tot = pcount.clone()
+    if W > 1:
+        ctx.dist.all_reduce(tot)
+    got_all = [int(x) for x in tot.tolist()]
+    nsp_sharded, got = got_all[0], got_all[1:]
     # known answers: per-copy counts x copies + matches across copy seams
     stripped_one = bytes(seq[: kc["stripped_len"]].cpu().numpy())
-    got = [int(t.item()) for t in vtot]
-    ok = True
+    ok = nsp_sharded == nsp
     for v, g in zip(kc["variants"], got):
         o = OracleRegex(R.Regex(v["re"]))
         seam = len(o.find_iter(stripped_one * 2)) - 2 * v["count"]
@@ -331,14 +380,19 @@ def run_c3(ctx):
     strip_ms = ctx.kernel_ms(strip_pass)
     var_ms = ctx.kernel_ms(variant_pass)
     scanned = N + len(variants) * M
+    my_bytes = sum(span_bounds(L, W, rk)[1] - span_bounds(L, W, rk)[0] for _, _, L, _ in passes)
     config = {"workload": "C3: regex-dna x%d (%d B raw, %d B stripped): strip find_iter + 9 variant find_iter"
-                          % (copies, N, M), "parallelism": "replicas%d" % ctx.world}
+                          % (copies, N, M),
+              "parallelism": "span%d (one logical stream cut into %d contiguous spans, exit exchange per step)"
+                             % (W, W)}
     return ctx.line("haystack GB/s scanned, batched bytes::Regex::find_iter (regex-dna)",
-                    scanned * ctx.world / sec / 1e9, "GB/s", sec * 1e3, "u8",
-                    "examples/regexdna-input.txt replicated", config,
-                    strip_pass_ms=round(strip_ms, 3), strip_GBps=round(N / strip_ms / 1e6, 1),
-                    variant_passes_ms=round(var_ms, 3), variant_GBps=round(len(variants) * M / var_ms / 1e6, 1),
-                    strip_matches=nsp, variant_counts=got, known_answers_ok=ok)
+                    scanned / sec / 1e9, "GB/s", sec * 1e3, "u8",
+                    "examples/regexdna-input.txt replicated", config, scaling="strong",
+                    strip_pass_ms=round(strip_ms, 3), strip_GBps=round(N / W / strip_ms / 1e6, 1),
+                    variant_passes_ms=round(var_ms, 3),
+                    variant_GBps=round((my_bytes - (N + W - 1) // W) / var_ms / 1e6, 1),
+                    strip_matches=nsp_sharded, variant_counts=got, known_answers_ok=ok,
+                    cut_recomputations=stats["recomputed"])
 
 
 # ------------------------------------------------------------------ C4

@@ -149,6 +149,28 @@ int rure_amd_set_matches_batch(rure_set *re, const rure_amd_batch *batch, uint64
 int rure_amd_find_iter_batch(rure *re, const rure_amd_batch *batch, uint64_t *counts, rure_match *matches,
                              size_t capacity, uint64_t *total, void *stream);
 
+/* find_iter over one span [lo, hi) of a long haystack (sharded or streamed
+ * iteration): the iteration of re_trait.rs:197-221 restricted to
+ * the matches that START in [lo, hi) (a match may end past hi; the haystack
+ * bytes after hi and before lo are read as context).  entry (device, may be
+ * NULL) = the state the previous span's call left in its `exit`; NULL or
+ * entry->fresh != 0 starts afresh at lo (no previous match).  *count
+ * (device) = matches owned, the first `capacity` written to `matches`
+ * (device).  *exit (device) = the state at hi: fresh != 0 when it is
+ * equivalent to a fresh start at hi (the next span's speculative result
+ * stands), else the next span must be recomputed with it as entry.  A span
+ * with hi == length also owns an empty match at the very end.  Concatenating
+ * the spans' matches in order equals rure_amd_find_iter_batch over the whole
+ * haystack from lo of the first span. */
+typedef struct rure_amd_iter_state {
+  uint64_t next;        /* where the next search starts */
+  uint64_t last_match;  /* end of the previous match, SIZE_MAX if none */
+  uint64_t fresh;       /* 1: same as a fresh iteration from the span end */
+} rure_amd_iter_state;
+int rure_amd_find_iter_span(rure *re, const uint8_t *haystack, size_t length, size_t lo, size_t hi,
+                            const rure_amd_iter_state *entry, uint64_t *count, rure_match *matches,
+                            size_t capacity, rure_amd_iter_state *exit, void *stream);
+
 /* Batched replacen with a literal replacement (bytes::Regex::replacen's
  * no-expansion path, re_bytes.rs:489-512): in every haystack the first
  * `limit` matches (0 = all) of the batched find_iter are replaced by

@@ -483,6 +483,32 @@ class Regex(object):
                 return counts, out[: min(t, cap)]
             cap = t
 
+    def find_iter_span(self, haystack, lo, hi, length=None, entry=None, capacity=None, stream=None):
+        """find_iter restricted to the matches starting in [lo, hi) of one long
+        haystack (rure_amd_find_iter_span; sharded / streamed iteration).
+        entry: None (fresh start at lo) or the (3,) int64 device tensor a
+        previous span returned as its exit.  Returns (count, matches, exit):
+        count = (1,) int64, matches = (k, 2) int64, exit = (3,) int64
+        (next, last match or -1, fresh)."""
+        import torch
+        dev = haystack.device
+        n = haystack.numel() if length is None else length
+        count = torch.zeros((1,), dtype=torch.int64, device=dev)
+        exit_ = torch.empty((3,), dtype=torch.int64, device=dev)
+        cap = capacity if capacity is not None else max(1024, (hi - lo) // 64)
+        ent = ctypes.c_void_p(entry.data_ptr()) if entry is not None else None
+        while True:
+            out = torch.empty((max(cap, 1), 2), dtype=torch.int64, device=dev)
+            _check(N.rure_amd_find_iter_span(self._re, ctypes.c_void_p(haystack.data_ptr()), n, lo, hi, ent,
+                                             ctypes.c_void_p(count.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                             cap, ctypes.c_void_p(exit_.data_ptr()), _stream_ptr(stream)),
+                   "find_iter_span")
+            (stream or torch.cuda.current_stream()).synchronize()
+            t = int(count.item())
+            if t <= cap or capacity is not None:
+                return count, out[: min(t, cap)], exit_
+            cap = t
+
     # ----------------------------------------------------------- diagnostics
     def dfa_info(self, which=0):
         info = N.DfaInfo()

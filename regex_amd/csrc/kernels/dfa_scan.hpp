@@ -144,8 +144,19 @@ struct IterOut {
   uint64_t cap;
   uint64_t *total;
 };
+// A span of one haystack (sharded / streamed find_iter): the iteration owns
+// the matches starting before `hi`; entry (device, 3 u64: next, last match,
+// fresh) = the state the previous span left (fresh: start at b.start); exit
+// (device, 3 u64) receives the state at hi (fresh = equivalent to a fresh
+// iteration starting at hi).
+struct IterSpan {
+  uint64_t hi;
+  const uint64_t *entry;
+  uint64_t *exit;
+};
 hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaDev &r, const NfaDev *nf,
-                            bool chunked, uint64_t chunk, const IterOut &o, hipStream_t st, int cus);
+                            bool chunked, uint64_t chunk, const IterOut &o, hipStream_t st, int cus,
+                            const IterSpan *span = nullptr);
 
 // One search per haystack over few long fixed-stride haystacks, chunked
 // (iter_scan.hip); f must be the find_iter DFA (with strip).

@@ -59,6 +59,7 @@ struct Unit {
 struct Geo {  // unit -> (haystack, chunk) for fixed-stride batches
   uint64_t nk;      // units per haystack
   uint64_t chunk;   // bytes per unit
+  uint64_t end;     // cut of the last unit (~0: the haystack end; a span's hi)
   uint32_t slots;   // speculative matches stored per unit
 };
 
@@ -75,7 +76,7 @@ __device__ __forceinline__ void unit_bounds(const BatchDev &b, const Geo &g, uin
     *len = b.length;
   }
   *c0 = b.start + k * g.chunk;
-  *c1 = (k + 1 == g.nk) ? ~0ull : b.start + (k + 1) * g.chunk;
+  *c1 = (k + 1 == g.nk) ? g.end : b.start + (k + 1) * g.chunk;
 }
 
 // One step of re_trait.rs:197-221 (empty-match rule: next search at e + 1,
@@ -292,6 +293,31 @@ __global__ void iter_walk_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f
   }
 }
 
+// Span entry (sharded / streamed find_iter): the first unit is entered with
+// the iteration state the previous span left.  Runs after the speculative
+// pass and before the parallel repairs, which read only the speculative
+// fields of unit 0; a changed exit is queued for the walker.
+__global__ void iter_entry_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r, Unit *units,
+                                  uint32_t *counts, const uint64_t *entry, uint64_t *queue,
+                                  unsigned long long *qlen) {
+  if (threadIdx.x != 0 || blockIdx.x != 0 || entry[2]) return;
+  if (repair_unit(b, g, f, r, f.lds_image /* unused: hot = 0 */, nullptr, 0, IterSt{entry[0], entry[1]}, units,
+                  counts) &&
+      g.nk > 1) {
+    const unsigned long long q = atomicAdd(qlen, 1ull);
+    queue[q] = 0;
+  }
+}
+
+// The state the iteration leaves at the span end: (next, last_match, fresh).
+__global__ void iter_exit_kernel(const Unit *units, uint64_t nunits, uint64_t *exit) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const Unit U = units[nunits - 1];
+  exit[0] = U.exit.p;
+  exit[1] = U.exit.lm;
+  exit[2] = (U.flags & U_CLEAN) ? 1 : 0;
+}
+
 // Pass 4: write every unit's matches at its offset.
 __global__ __launch_bounds__(256) void iter_emit_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
                                                         const Unit *units, const uint64_t *slots, const uint64_t *off,
@@ -331,7 +357,8 @@ __global__ __launch_bounds__(256) void iter_emit_kernel(BatchDev b, Geo g, uint6
 template <bool EMIT>
 __global__ __launch_bounds__(64) void iter_wave_kernel(BatchDev b, FwdDfaDev f, RevDfaDev r, NfaDev nf, int has_dfa,
                                                        uint32_t *counts, const uint64_t *off, uint64_t *out,
-                                                       uint64_t cap, uint8_t *scratch) {
+                                                       uint64_t cap, uint8_t *scratch, const uint64_t *entry,
+                                                       uint64_t hi, uint64_t *exit) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_mem[];
   uint8_t *mem = scratch ? scratch + (size_t)blockIdx.x * nfa_wave_bytes(nf.nleaves) : lds_mem;
   pike::Lists W;
@@ -359,6 +386,10 @@ __global__ __launch_bounds__(64) void iter_wave_kernel(BatchDev b, FwdDfaDev f, 
       len = b.length;
     }
     uint64_t p = b.start, lm = NONE, n = 0;
+    if (entry && !entry[2]) {  // span entered with the previous span's state
+      p = entry[0];
+      lm = entry[1];
+    }
     const uint64_t o0 = EMIT ? off[h] : 0, cnt = EMIT ? off[h + 1] - off[h] : 0;
     while (p <= len && (!EMIT || n < cnt)) {
       uint64_t s = NONE, e = NONE;
@@ -379,6 +410,7 @@ __global__ __launch_bounds__(64) void iter_wave_kernel(BatchDev b, FwdDfaDev f, 
         e = r1;
       }
       if (k == 0) break;
+      if (s >= hi) break;  // owned by the next span
       if (s == e) {
         p = e + 1;
         if (lm == e) continue;
@@ -392,7 +424,14 @@ __global__ __launch_bounds__(64) void iter_wave_kernel(BatchDev b, FwdDfaDev f, 
       }
       ++n;
     }
-    if (!EMIT && lane == 0) counts[h] = (uint32_t)n;
+    if (!EMIT && lane == 0) {
+      counts[h] = (uint32_t)n;
+      if (exit) {
+        exit[0] = p;
+        exit[1] = lm;
+        exit[2] = (p == hi && lm != hi) ? 1 : 0;
+      }
+    }
   }
 }
 
@@ -503,6 +542,7 @@ hipError_t long_scan_m(const BatchDev &b, const FwdDfaDev &f, const RevDfaDev &r
                        hipStream_t st, int cus) {
   Geo g;
   g.chunk = chunk;
+  g.end = ~0ull;
   g.slots = 0;
   const uint64_t span = b.length > b.start ? b.length - b.start : 0;
   g.nk = span <= chunk ? 1 : (span + chunk - 1) / chunk;
@@ -541,15 +581,19 @@ hipError_t launch_long_scan(int mode, const BatchDev &b, const FwdDfaDev &f, con
 }
 
 hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaDev &r, const NfaDev *nf,
-                            bool chunked, uint64_t chunk, const IterOut &o, hipStream_t st, int cus) {
+                            bool chunked, uint64_t chunk, const IterOut &o, hipStream_t st, int cus,
+                            const IterSpan *spn) {
+  const uint64_t hi = spn ? spn->hi : ~0ull;
   hipError_t e = hipSuccess;
   if (b.count == 0) {
     return hipMemsetAsync(o.total, 0, 8, st);
   }
   if (chunked) {
-    uint64_t span = (!b.offs && b.length > b.start) ? b.length - b.start : 0;
+    const uint64_t lim = std::min<uint64_t>(b.length, hi);
+    uint64_t span = (!b.offs && lim > b.start) ? lim - b.start : 0;
     Geo g;
     g.chunk = chunk;
+    g.end = hi;
     g.nk = (b.offs || span <= chunk) ? 1 : (span + chunk - 1) / chunk;
     if (b.offs) g.chunk = ~0ull >> 2;
     const uint64_t nunits = b.count * g.nk;
@@ -579,6 +623,15 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
       hipLaunchKernelGGL(iter_spec_kernel, dim3(grid), dim3(256), iter_lds_bytes(*f, r), st, b, g, nunits, *f, r, units, slots,
                          counts);
       if ((e = hipGetLastError()) != hipSuccess) break;
+      if (spn && spn->entry) {
+        FwdDfaDev fw = *f;
+        fw.hot = 0;
+        RevDfaDev rw = r;
+        rw.hot = 0;
+        hipLaunchKernelGGL(iter_entry_kernel, dim3(1), dim3(64), 0, st, b, g, nunits, fw, rw, units, counts,
+                           spn->entry, queue, qlen);
+        if ((e = hipGetLastError()) != hipSuccess) break;
+      }
       if (g.nk > 1) {
         hipLaunchKernelGGL(iter_fix_kernel, dim3(grid), dim3(256), iter_lds_bytes(*f, r), st, b, g, nunits, *f, r, units,
                            counts, queue, qlen);
@@ -596,7 +649,11 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
       if ((e = hipGetLastError()) != hipSuccess) break;
       hipLaunchKernelGGL(iter_counts_kernel, dim3(grid_cap(b.count, 256, cus, 4)), dim3(256), 0, st, b.count, g.nk,
                          off, o.counts, o.total);
-      e = hipGetLastError();
+      if ((e = hipGetLastError()) != hipSuccess) break;
+      if (spn && spn->exit) {
+        hipLaunchKernelGGL(iter_exit_kernel, dim3(1), dim3(64), 0, st, (const Unit *)units, nunits, spn->exit);
+        e = hipGetLastError();
+      }
     } while (false);
     hipError_t e2 = hipFreeAsync(buf, st);
     return e != hipSuccess ? e : e2;
@@ -627,11 +684,13 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
     }
     if ((e = hipMemsetAsync(counts + b.count, 0, 4, st)) != hipSuccess) break;
     hipLaunchKernelGGL(iter_wave_kernel<false>, dim3(grid), dim3(64), lds, st, b, fa, r, *nf, f ? 1 : 0, counts,
-                       (const uint64_t *)nullptr, (uint64_t *)nullptr, (uint64_t)0, scr);
+                       (const uint64_t *)nullptr, (uint64_t *)nullptr, (uint64_t)0, scr,
+                       spn ? spn->entry : (const uint64_t *)nullptr, hi, spn ? spn->exit : (uint64_t *)nullptr);
     if ((e = hipGetLastError()) != hipSuccess) break;
     if ((e = scan_counts(counts, off, b.count, st)) != hipSuccess) break;
     hipLaunchKernelGGL(iter_wave_kernel<true>, dim3(grid), dim3(64), lds, st, b, fa, r, *nf, f ? 1 : 0, counts,
-                       (const uint64_t *)off, o.matches, o.cap, scr);
+                       (const uint64_t *)off, o.matches, o.cap, scr,
+                       spn ? spn->entry : (const uint64_t *)nullptr, hi, (uint64_t *)nullptr);
     if ((e = hipGetLastError()) != hipSuccess) break;
     hipLaunchKernelGGL(iter_counts_kernel, dim3(grid_cap(b.count, 256, cus, 4)), dim3(256), 0, st, b.count,
                        (uint64_t)1, off, o.counts, o.total);

@@ -1358,23 +1358,24 @@ namespace {
 
 // The batched find_iter (re_trait.rs:197-221) on one stream.
 hipError_t run_find_iter(rure *re, DevTables *t, const BatchDev &b, const IterOut &o, hipStream_t st,
-                         std::string *err) {
+                         std::string *err, const IterSpan *sp = nullptr) {
   // Chunked speculative iteration needs a DFA that cannot quit and a pattern
   // without assertions (see iter_scan.hip); otherwise one wave per haystack.
   const FwdDfaDev *fi = nullptr;
   if (t->has_dfa && !t->quit_possible && re->nfa_ok && re->nt.looks_used == 0) fi = iter_device(re, *t, err);
   if (fi) {
     uint64_t chunk = ~0ull >> 2;
-    if (!b.offs && b.length > b.start && b.count) {
-      const uint64_t span = b.length - b.start;
+    const uint64_t lim = sp ? std::min<uint64_t>(b.length, sp->hi) : b.length;
+    if (!b.offs && lim > b.start && b.count) {
+      const uint64_t span = lim - b.start;
       const uint64_t target = (uint64_t)t->cus * 1024;  // 16 waves per CU
       const uint64_t per_h = (target + b.count - 1) / b.count;
       chunk = odd_lines(std::max<uint64_t>(4096, (span + per_h - 1) / per_h));
     }
-    return launch_find_iter(b, fi, t->r, &t->n, true, chunk, o, st, t->cus);
+    return launch_find_iter(b, fi, t->r, &t->n, true, chunk, o, st, t->cus, sp);
   }
   if (!re->nfa_ok) return hipErrorInvalidValue;
-  return launch_find_iter(b, t->has_dfa ? &t->f : nullptr, t->r, &t->n, false, 0, o, st, t->cus);
+  return launch_find_iter(b, t->has_dfa ? &t->f : nullptr, t->r, &t->n, false, 0, o, st, t->cus, sp);
 }
 
 // find_iter into internal device buffers: counts (n + 1, last 0), their
@@ -1431,6 +1432,30 @@ int rure_amd_find_iter_batch(rure *re, const rure_amd_batch *batch, uint64_t *co
   if (!t->has_dfa && !re->nfa_ok) return RURE_AMD_ERR_DFA;
   IterOut o{counts, (uint64_t *)matches, capacity, total};
   return run_find_iter(re, t, b, o, (hipStream_t)stream, &err) == hipSuccess ? RURE_AMD_OK : RURE_AMD_ERR_HIP;
+}
+
+int rure_amd_find_iter_span(rure *re, const uint8_t *haystack, size_t length, size_t lo, size_t hi,
+                            const rure_amd_iter_state *entry, uint64_t *count, rure_match *matches,
+                            size_t capacity, rure_amd_iter_state *exit, void *stream) {
+  if (!re || (!haystack && length) || lo > hi || hi > length || !count || !exit || (!matches && capacity))
+    return RURE_AMD_ERR_ARG;
+  std::string err;
+  DevTables *t = regex_device(re, &err);
+  if (!t) return err.rfind("HIP", 0) == 0 ? RURE_AMD_ERR_HIP : RURE_AMD_ERR_DFA;
+  if (!t->has_dfa && !re->nfa_ok) return RURE_AMD_ERR_DFA;
+  BatchDev b;
+  b.hay = haystack;
+  b.offs = nullptr;
+  b.stride = length;
+  b.length = length;
+  b.count = 1;
+  b.start = lo;
+  // hi == length: the span runs to the end of the text, so the iteration
+  // may also own the empty match at the very end (re_trait.rs:205-214)
+  IterSpan sp{hi == length ? ~0ull : (uint64_t)hi, (const uint64_t *)entry, (uint64_t *)exit};
+  IterOut o{count, (uint64_t *)matches, capacity, count};
+  hipStream_t st = (hipStream_t)stream;
+  return run_find_iter(re, t, b, o, st, &err, &sp) == hipSuccess ? RURE_AMD_OK : RURE_AMD_ERR_HIP;
 }
 
 int rure_amd_replace_batch(rure *re, const rure_amd_batch *batch, const uint8_t *rep, size_t rep_len, size_t limit,

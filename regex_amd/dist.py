@@ -49,3 +49,89 @@ def max_over_ranks(seconds, device, group=None):
     t = torch.tensor([seconds], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return float(t.item())
+
+
+# ----------------------------------------------------- sharded find_iter (C3)
+# One logical haystack (regex-dna's 2 GiB stream) cut into contiguous spans,
+# one per rank.  Every rank iterates its span speculatively from a fresh start
+# (rure_amd_find_iter_span); the exits are exchanged (an all-gather of 3 x
+# int64 per rank) and a rank whose predecessor's exit is not equivalent to a
+# fresh start recomputes its span entered with that exit.  Rank r's exit is
+# final once ranks < r are, so this takes at most world - 1 rounds; with no
+# match crossing a cut it takes none.
+
+
+def _entry_key(ex):
+    ex = [int(x) for x in ex]
+    return ("fresh",) if ex[2] else (ex[0], ex[1])
+
+
+def iterate_spans(run_span, nspans, mine, gather_exits):
+    """Exact chained iteration over `nspans` spans.
+
+    run_span(i, entry) -> (count, matches, exit) runs span i entered with
+    `entry` (None = fresh, else (next, last_match, 0)); exit is a 3-int
+    sequence or tensor (next, last_match, fresh).  `mine` = the span ids this
+    process runs; gather_exits({i: exit}) -> list of every span's exit.
+    Returns ({i: result}, rounds of recomputation)."""
+    res = {i: run_span(i, None) for i in mine}
+    used = [("fresh",)] * nspans
+    rounds = 0
+    while True:
+        exits = gather_exits({i: res[i][2] for i in mine})
+        redo = [i for i in range(1, nspans) if _entry_key(exits[i - 1]) != used[i]]
+        if not redo:
+            return res, rounds
+        rounds += 1
+        for i in redo:
+            used[i] = _entry_key(exits[i - 1])
+            if i in res:
+                k = used[i]
+                res[i] = run_span(i, None if k == ("fresh",) else (k[0], k[1], 0))
+
+
+def span_bounds(length, nspans, i):
+    """[lo, hi) of span i; the last span ends at `length` (and owns an empty
+    match at the very end)."""
+    return shard_range(length, nspans, i)
+
+
+def find_iter_sharded(re, hay, length, group=None, stream=None):
+    """bytes::Regex::find_iter over one haystack sharded across the ranks of
+    `group` (every rank holds the haystack; each scans its own span).
+    Returns (matches owned by this rank, global index of its first match,
+    total matches, recomputation rounds)."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+
+    def run(i, entry):
+        lo, hi = span_bounds(length, world, i)
+        ent = None if entry is None else torch.tensor(entry, dtype=torch.int64, device=hay.device)
+        return re.find_iter_span(hay, lo, hi, length=length, entry=ent, stream=stream)
+
+    def gather(mine):
+        ex = mine[rank]
+        parts = [torch.empty_like(ex) for _ in range(world)]
+        dist.all_gather(parts, ex, group=group)
+        return [p.tolist() for p in parts]
+
+    res, rounds = iterate_spans(run, world, [rank], gather)
+    count, matches, _ = res[rank]
+    counts = [torch.empty_like(count) for _ in range(world)]
+    dist.all_gather(counts, count, group=group)
+    counts = [int(c.item()) for c in counts]
+    return matches, sum(counts[:rank]), sum(counts), rounds
+
+
+def find_iter_spans_local(re, hay, length, nspans, stream=None):
+    """The same chained span iteration with every span on this device (tests
+    and single-GPU rehearsal of the sharded protocol).  Returns (matches in
+    order, rounds)."""
+    def run(i, entry):
+        lo, hi = span_bounds(length, nspans, i)
+        ent = None if entry is None else torch.tensor(entry, dtype=torch.int64, device=hay.device)
+        return re.find_iter_span(hay, lo, hi, length=length, entry=ent, stream=stream)
+
+    res, rounds = iterate_spans(run, nspans, list(range(nspans)),
+                                lambda mine: [mine[i].tolist() for i in range(nspans)])
+    return torch.cat([res[i][1] for i in range(nspans)], dim=0), rounds
