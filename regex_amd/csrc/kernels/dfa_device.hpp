@@ -45,10 +45,9 @@ struct LaneState {
 static constexpr uint64_t NONE = ~0ull;
 static constexpr uint64_t QUITMARK = ~0ull - 1;
 
-// Full-table step for one byte at haystack position `pos` (careful path).
+// The bookkeeping of entering state s at haystack position `pos`.
 template <int MODE>
-__device__ __forceinline__ void careful_step(LaneState &L, const FwdDfaDev &f, uint32_t b, uint64_t pos) {
-  uint32_t s = f.full[(size_t)L.s * 256 + b];
+__device__ __forceinline__ void enter_state(LaneState &L, const FwdDfaDev &f, uint32_t s, uint64_t pos) {
   L.s = s;
   if (s >= f.n_normal) {
     if (s < f.n_match_end) {                 // dfa.rs:658-668: Match(at - 1)
@@ -63,9 +62,19 @@ __device__ __forceinline__ void careful_step(LaneState &L, const FwdDfaDev &f, u
   }
 }
 
+// Full-table step for one byte at haystack position `pos` (careful path).
+template <int MODE>
+__device__ __forceinline__ void careful_step(LaneState &L, const FwdDfaDev &f, uint32_t b, uint64_t pos) {
+  enter_state<MODE>(L, f, f.full[(size_t)L.s * 256 + b], pos);
+}
+
 template <int MODE>
 __device__ __forceinline__ void step1(LaneState &L, const FwdDfaDev &f, const uint8_t *lds,
                                       uint32_t b, uint64_t pos) {
+  if (f.all) {  // exact LDS table for every state
+    enter_state<MODE>(L, f, lds[L.s * kRow + b], pos);
+    return;
+  }
   if (L.s < f.hot) {
     uint32_t t = lds[L.s * kRow + b];
     if (t != f.hot) { L.s = t; return; }
@@ -84,10 +93,31 @@ __device__ __forceinline__ uint32_t fast4(uint32_t s, uint32_t w, const uint8_t 
   return s;
 }
 
+// 4 exact steps (every state in LDS); mx collects the largest state entered
+// (off the dependency chain): mx < n_normal means no match / dead / quit.
+__device__ __forceinline__ uint32_t exact4(uint32_t s, uint32_t w, const uint8_t *lds, uint32_t &mx) {
+  s = lds[s * kRow + (w & 0xFF)];
+  mx = max(mx, s);
+  s = lds[s * kRow + ((w >> 8) & 0xFF)];
+  mx = max(mx, s);
+  s = lds[s * kRow + ((w >> 16) & 0xFF)];
+  mx = max(mx, s);
+  s = lds[s * kRow + (w >> 24)];
+  mx = max(mx, s);
+  return s;
+}
+
 template <int MODE>
 __device__ __forceinline__ void chunk16(LaneState &L, const FwdDfaDev &f, const uint8_t *lds,
                                         uint4 v, uint64_t pos) {
-  if (L.s < f.hot) {
+  if (f.all) {
+    uint32_t t = L.s, mx = 0;
+    t = exact4(t, v.x, lds, mx);
+    t = exact4(t, v.y, lds, mx);
+    t = exact4(t, v.z, lds, mx);
+    t = exact4(t, v.w, lds, mx);
+    if (mx < f.n_normal) { L.s = t; return; }
+  } else if (L.s < f.hot) {
     uint32_t t = L.s;
     t = fast4(t, v.x, lds);
     t = fast4(t, v.y, lds);
@@ -149,9 +179,10 @@ __device__ __forceinline__ void chunk16s(LaneState &L, const FwdDfaDev &f, const
 // forward one) ordinary steps stay in LDS.
 __device__ __forceinline__ uint64_t rev_scan(const RevDfaDev &r, const uint8_t *rlds, const uint8_t *base,
                                              uint64_t len, uint64_t lo, uint64_t me) {
-  uint32_t s = r.start[rev_flag_index(base, lo, len, me)];
+  uint32_t s = r.ustart1 ? r.ustart1 - 1 : r.start[rev_flag_index(base, lo, len, me)];
   if (s == r.dead) return NONE;
   const uint32_t hot = rlds ? r.hot : 0;
+  const bool all = rlds && r.all;
   uint64_t rs = NONE;
   uint64_t a = me;
   while (a > lo) {
@@ -162,11 +193,15 @@ __device__ __forceinline__ uint64_t rev_scan(const RevDfaDev &r, const uint8_t *
     for (int j = (int)(p & 15); j >= 0 && a > lo; --j) {
       const uint32_t b = (w[j >> 2] >> ((j & 3) * 8)) & 0xFF;
       --a;
-      if (s < hot) {
-        const uint32_t t = rlds[s * kRow + b];
-        if (t != hot) { s = t; continue; }
+      if (all) {
+        s = rlds[s * kRow + b];
+      } else {
+        if (s < hot) {
+          const uint32_t t = rlds[s * kRow + b];
+          if (t != hot) { s = t; continue; }
+        }
+        s = r.full[(size_t)s * 256 + b];
       }
-      s = r.full[(size_t)s * 256 + b];
       if (s >= r.n_normal) {
         if (s < r.n_match_end) rs = a + 1;
         else if (s == r.dead) return rs;
@@ -234,7 +269,7 @@ __device__ __forceinline__ void lane_start(LaneState &L, const FwdDfaDev &f, con
     L.done = true;
     L.s = f.dead;
   } else {
-    L.s = f.start[fwd_flag_index(base, len, at)];
+    L.s = f.ustart1 ? f.ustart1 - 1 : f.start[fwd_flag_index(base, len, at)];
     if (L.s >= f.n_normal) L.done = true;  // dead start state (dfa.rs:484)
   }
 }

@@ -41,6 +41,8 @@ struct FwdDfaDev {
   const uint16_t *start;      // 128 start states by flag index
   const uint16_t *strip;      // find_iter DFA only: state minus the `.*?` prefix (or null)
   uint32_t n_normal, n_match_end, dead, quit;
+  uint32_t all;               // lds_image rows are exact for every state (hot = nstates <= 255)
+  uint32_t ustart1;           // 1 + the start state when it does not depend on the flags, else 0
 };
 
 struct RevDfaDev {
@@ -51,6 +53,8 @@ struct RevDfaDev {
   const uint8_t *eof;
   const uint16_t *start;
   uint32_t n_normal, n_match_end, dead, quit;
+  uint32_t all;               // as FwdDfaDev::all
+  uint32_t ustart1;           // as FwdDfaDev::ustart1
 };
 
 // Set DFA: the answer is the union of now_mask[s] over the states entered

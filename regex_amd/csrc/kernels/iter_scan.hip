@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <rocprim/rocprim.hpp>
 #include <stdint.h>
@@ -45,6 +46,7 @@ enum : uint32_t {
   U_CLEAN = 2,        // final exit clean
   U_FIXED = 4,        // final entry differs from the speculative one
   U_QUIT = 8,         // a search quit (cannot happen on the chunked path)
+  U_COPY = 16,        // fixed, and its matches are slots[skip, skip + count)
 };
 
 struct IterSt {
@@ -54,6 +56,7 @@ struct IterSt {
 struct Unit {
   IterSt entry, exit, spec_exit;
   uint32_t spec_count, flags;
+  uint32_t skip, pad;  // U_COPY: speculative matches dropped at the front
 };
 
 struct Geo {  // unit -> (haystack, chunk) for fixed-stride batches
@@ -155,7 +158,7 @@ __device__ __forceinline__ const uint8_t *stage_tables(const FwdDfaDev &f, const
 }
 
 // Pass 1: speculative iteration of every unit.
-__global__ __launch_bounds__(256) void iter_spec_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
+__global__ __launch_bounds__(1024) void iter_spec_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
                                                         Unit *units, uint64_t *slots, uint32_t *counts) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const uint8_t *rlds = stage_tables(f, r, lds);
@@ -168,10 +171,7 @@ __global__ __launch_bounds__(256) void iter_spec_kernel(BatchDev b, Geo g, uint6
     uint32_t n = 0;
     uint64_t s, e;
     while (it.next(f, r, lds, rlds, base, len, &s, &e)) {
-      if (n < g.slots) {
-        slots[(u * g.slots + n) * 2] = s;
-        slots[(u * g.slots + n) * 2 + 1] = e;
-      }
+      if (n < g.slots) *(ulonglong2 *)&slots[(u * g.slots + n) * 2] = make_ulonglong2(s, e);
       ++n;
     }
     Unit U;
@@ -180,21 +180,96 @@ __global__ __launch_bounds__(256) void iter_spec_kernel(BatchDev b, Geo g, uint6
     U.spec_exit = it.exit;
     U.spec_count = n;
     U.flags = (it.clean ? (U_SPEC_CLEAN | U_CLEAN) : 0) | (it.quit ? U_QUIT : 0);
+    U.skip = U.pad = 0;
     units[u] = U;
     counts[u] = n;
   }
 }
 
-// Repairs unit j given its true entry `E`: lockstep with its speculative
-// iteration until both emit the same match.  Updates the unit's record and
-// count; returns true if the unit's exit changed.
+// Where the true iteration of unit j, entered with E, joins the speculative
+// one S (started fresh at c0), read off S's recorded matches: S's state
+// before it yielded match i is (p_i, lm_i) (p_0 = c0, lm_0 = none; then the
+// end of match i-1, plus one after an empty match).  For the last i with
+// p_i <= E.p: if E.p > p_i (or the states are equal), no match starts in
+// [E.p, s_i) except what S saw, so the search from E.p yields S's match i
+// unless it is an empty match at E's last match end (skipped); with E.p ==
+// p_i the two searches are the same one.  Returns i
+// (i == spec_count: no owned match at all), or -1 = undecided.
+__device__ int64_t join_speculation(const Unit &U, uint64_t c0, IterSt E, const uint64_t *slots, const Geo &g,
+                                    uint64_t j) {
+  const uint32_t n = U.spec_count;
+  if (n > g.slots || E.p < c0) return -1;
+  const uint64_t *sl = slots + j * g.slots * 2;
+  uint32_t lo = 0, hi = n;  // last i in [0, n] with p_i <= E.p (p_i strictly increasing)
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1) >> 1;
+    const uint64_t s = sl[2 * (mid - 1)], e = sl[2 * (mid - 1) + 1];
+    if ((s == e ? e + 1 : e) <= E.p) lo = mid;
+    else hi = mid - 1;
+  }
+  const uint32_t i = lo;
+  uint64_t pi = c0, lmi = NONE;
+  if (i > 0) {
+    const uint64_t s = sl[2 * (i - 1)], e = sl[2 * (i - 1) + 1];
+    pi = s == e ? e + 1 : e;
+    lmi = e;
+  }
+  if (E.p == pi && E.lm != lmi) {
+    // same search start, different last match: S's search from p_i yielded
+    // its match i directly (no empty match skipped) when S had no last match
+    // (i == 0) or match i starts at p_i
+    if (!(i == 0 || (i < n && sl[2 * i] == pi))) return -1;
+  }
+  if (i < n) {
+    const uint64_t s = sl[2 * i], e = sl[2 * i + 1];
+    if (s < E.p || (s == e && e == E.lm)) return -1;
+    return i;
+  }
+  return (U.flags & U_SPEC_CLEAN) ? (int64_t)i : -1;
+}
+
+// Repairs unit j given its true entry `E`.  Usually decided from the
+// speculative slots (join_speculation); otherwise the true and the
+// speculative iterations run in lockstep until both emit the same match.
+// Updates the unit's record and count; returns true if its exit changed.
 __device__ bool repair_unit(const BatchDev &b, const Geo &g, const FwdDfaDev &f, const RevDfaDev &r,
                             const uint8_t *lds, const uint8_t *rlds, uint64_t j, IterSt E, Unit *units,
-                            uint32_t *counts) {
+                            uint32_t *counts, const uint64_t *slots) {
   uint64_t h, len, c0, c1;
   const uint8_t *base;
   unit_bounds(b, g, j, &h, &base, &len, &c0, &c1);
   Unit U = units[j];
+  const bool spec_clean = (U.flags & U_SPEC_CLEAN) != 0;
+  U.entry = E;
+  U.flags = (U.flags & ~(U_COPY | U_CLEAN | U_QUIT)) | U_FIXED;
+  U.skip = 0;
+  bool changed;
+  if (E.p >= c1) {  // the true iteration passes over the whole unit
+    const bool cl = E.p == c1 && E.lm != c1;
+    counts[j] = 0;
+    changed = !exit_equiv(cl, E, spec_clean, U.spec_exit);
+    U.exit = E;
+    U.flags |= cl ? U_CLEAN : 0;
+    units[j] = U;
+    return changed;
+  }
+  const int64_t i = join_speculation(U, c0, E, slots, g, j);
+  if (i >= 0) {
+    if (i < (int64_t)U.spec_count) {
+      counts[j] = U.spec_count - (uint32_t)i;
+      U.skip = (uint32_t)i;
+      U.flags |= U_COPY | (spec_clean ? U_CLEAN : 0);
+      U.exit = U.spec_exit;
+      changed = false;
+    } else {
+      counts[j] = 0;
+      U.exit = E;
+      U.flags |= U_CLEAN;
+      changed = !spec_clean;
+    }
+    units[j] = U;
+    return changed;
+  }
   UnitIter F, S;
   F.init(E, c1);
   S.init({c0, NONE}, c1);
@@ -213,19 +288,20 @@ __device__ bool repair_unit(const BatchDev &b, const Geo &g, const FwdDfaDev &f,
       sm = S.next(f, r, lds, rlds, base, len, &ss, &se);
     }
   }
-  U.entry = E;
-  U.flags |= U_FIXED;
-  bool changed;
   if (synced) {
     counts[j] = fcnt + (U.spec_count - scnt);
     U.exit = U.spec_exit;
-    U.flags = (U.flags & ~U_CLEAN) | ((U.flags & U_SPEC_CLEAN) ? U_CLEAN : 0);
+    U.flags |= spec_clean ? U_CLEAN : 0;
+    if (fcnt == 0 && U.spec_count <= g.slots) {
+      U.skip = scnt;
+      U.flags |= U_COPY;
+    }
     changed = false;
   } else {
     counts[j] = fcnt;
-    changed = !exit_equiv(F.clean, F.exit, (U.flags & U_SPEC_CLEAN) != 0, U.spec_exit);
+    changed = !exit_equiv(F.clean, F.exit, spec_clean, U.spec_exit);
     U.exit = F.exit;
-    U.flags = (U.flags & ~U_CLEAN) | (F.clean ? U_CLEAN : 0) | (F.quit ? U_QUIT : 0);
+    U.flags |= (F.clean ? U_CLEAN : 0) | (F.quit ? U_QUIT : 0);
   }
   units[j] = U;
   return changed;
@@ -233,17 +309,23 @@ __device__ bool repair_unit(const BatchDev &b, const Geo &g, const FwdDfaDev &f,
 
 // Pass 2: units entered through a dirty speculative exit are repaired in
 // parallel; repairs that change their own exit are queued for the walker.
-__global__ __launch_bounds__(256) void iter_fix_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
-                                                       Unit *units, uint32_t *counts, uint64_t *queue,
-                                                       unsigned long long *qlen) {
+// Dirty exits are rare, so a block stages the hot tables into LDS only when
+// one of its units needs a repair.
+__global__ __launch_bounds__(1024) void iter_fix_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
+                                                       Unit *units, uint32_t *counts, const uint64_t *slots,
+                                                       uint64_t *queue, unsigned long long *qlen) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const uint8_t *rlds = stage_tables(f, r, lds);
-  for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u + 1 < nunits;
-       u += (uint64_t)gridDim.x * blockDim.x) {
-    if ((u + 1) % g.nk == 0) continue;  // last unit of its haystack
-    const Unit U = units[u];
-    if (U.flags & U_SPEC_CLEAN) continue;
-    if (repair_unit(b, g, f, r, lds, rlds, u + 1, U.spec_exit, units, counts)) {
+  const uint8_t *rlds = nullptr;
+  bool staged = false;
+  for (uint64_t u0 = (uint64_t)blockIdx.x * blockDim.x; u0 + 1 < nunits; u0 += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t u = u0 + threadIdx.x;
+    const bool need = u + 1 < nunits && (u + 1) % g.nk != 0 && !(units[u].flags & U_SPEC_CLEAN);
+    if (!__syncthreads_or(need)) continue;
+    if (!staged) {
+      rlds = stage_tables(f, r, lds);
+      staged = true;
+    }
+    if (need && repair_unit(b, g, f, r, lds, rlds, u + 1, units[u].spec_exit, units, counts, slots)) {
       const unsigned long long q = atomicAdd(qlen, 1ull);
       queue[q] = u + 1;
     }
@@ -252,7 +334,7 @@ __global__ __launch_bounds__(256) void iter_fix_kernel(BatchDev b, Geo g, uint64
 
 // Pass 3 (one thread): propagate exits that changed, in unit order.
 __global__ void iter_walk_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r, Unit *units,
-                                 uint32_t *counts, uint64_t *queue, unsigned long long *qlen) {
+                                 uint32_t *counts, const uint64_t *slots, uint64_t *queue, unsigned long long *qlen) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const uint64_t n = *qlen;
   if (n == 0) return;
@@ -280,11 +362,12 @@ __global__ void iter_walk_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f
         unit_bounds(b, g, u, &h, &base, &len, &c0, &c1);
         W.entry = {c0, NONE};
         W.exit = W.spec_exit;
-        W.flags = (W.flags & ~(U_FIXED | U_CLEAN)) | ((W.flags & U_SPEC_CLEAN) ? U_CLEAN : 0);
+        W.flags = (W.flags & ~(U_FIXED | U_CLEAN | U_COPY | U_QUIT)) | ((W.flags & U_SPEC_CLEAN) ? U_CLEAN : 0);
+        W.skip = 0;
         units[u] = W;
         counts[u] = W.spec_count;
       } else {
-        repair_unit(b, g, f, r, f.lds_image /* unused: hot = 0 */, nullptr, u, X.exit, units, counts);
+        repair_unit(b, g, f, r, f.lds_image /* unused: hot = 0 */, nullptr, u, X.exit, units, counts, slots);
       }
       X = units[u];
       ++u;
@@ -298,11 +381,11 @@ __global__ void iter_walk_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f
 // pass and before the parallel repairs, which read only the speculative
 // fields of unit 0; a changed exit is queued for the walker.
 __global__ void iter_entry_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r, Unit *units,
-                                  uint32_t *counts, const uint64_t *entry, uint64_t *queue,
+                                  uint32_t *counts, const uint64_t *slots, const uint64_t *entry, uint64_t *queue,
                                   unsigned long long *qlen) {
   if (threadIdx.x != 0 || blockIdx.x != 0 || entry[2]) return;
   if (repair_unit(b, g, f, r, f.lds_image /* unused: hot = 0 */, nullptr, 0, IterSt{entry[0], entry[1]}, units,
-                  counts) &&
+                  counts, slots) &&
       g.nk > 1) {
     const unsigned long long q = atomicAdd(qlen, 1ull);
     queue[q] = 0;
@@ -318,23 +401,50 @@ __global__ void iter_exit_kernel(const Unit *units, uint64_t nunits, uint64_t *e
   exit[2] = (U.flags & U_CLEAN) ? 1 : 0;
 }
 
-// Pass 4: write every unit's matches at its offset.
-__global__ __launch_bounds__(256) void iter_emit_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
+// Pass 4: write every unit's matches at its offset.  Units whose speculation
+// held copy their slot buffer; the 64 lanes of a wave copy one unit at a time
+// (coalesced 16-byte records).  Units that were repaired, or had more matches
+// than slots, re-run their iteration (the block stages the hot tables only
+// then).
+__global__ __launch_bounds__(1024) void iter_emit_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
                                                         const Unit *units, const uint64_t *slots, const uint64_t *off,
                                                         uint64_t *out, uint64_t cap) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const uint8_t *rlds = stage_tables(f, r, lds);
-  for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < nunits; u += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t o0 = off[u], cnt = off[u + 1] - o0;
-    if (cnt == 0 || o0 >= cap) continue;
-    const Unit U = units[u];
-    if (!(U.flags & U_FIXED) && cnt <= g.slots) {
-      for (uint64_t i = 0; i < cnt && o0 + i < cap; ++i) {
-        out[2 * (o0 + i)] = slots[(u * g.slots + i) * 2];
-        out[2 * (o0 + i) + 1] = slots[(u * g.slots + i) * 2 + 1];
+  const uint8_t *rlds = nullptr;
+  bool staged = false;
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint64_t u0 = (uint64_t)blockIdx.x * blockDim.x; u0 < nunits; u0 += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t u = u0 + threadIdx.x;
+    uint64_t o0 = 0, cnt = 0;
+    bool rerun = false, copy = false;
+    if (u < nunits) {
+      o0 = off[u];
+      cnt = off[u + 1] - o0;
+      if (cnt && o0 < cap) {
+        const uint32_t fl = units[u].flags;
+        rerun = ((fl & U_FIXED) && !(fl & U_COPY)) || cnt > g.slots;
+        copy = !rerun;
       }
-      continue;
     }
+    uint64_t m = __ballot(copy);
+    while (m) {
+      const int l = __builtin_ctzll(m);
+      m &= m - 1;
+      const uint64_t uu = __shfl(u, l), oo = __shfl(o0, l);
+      const uint64_t cc = min(__shfl(cnt, l), cap - oo);
+      const uint32_t sk = (units[uu].flags & U_COPY) ? units[uu].skip : 0;
+      // `out` (rure_match records) is only guaranteed 8-byte aligned
+      const uint64_t *src = slots + (uu * g.slots + sk) * 2;
+      uint64_t *dst = out + 2 * oo;
+      for (uint64_t i = lane; i < 2 * cc; i += 64) dst[i] = src[i];
+    }
+    if (!__syncthreads_or(rerun)) continue;
+    if (!staged) {
+      rlds = stage_tables(f, r, lds);
+      staged = true;
+    }
+    if (!rerun) continue;
+    const Unit U = units[u];
     uint64_t h, len, c0, c1;
     const uint8_t *base;
     unit_bounds(b, g, u, &h, &base, &len, &c0, &c1);
@@ -374,6 +484,7 @@ __global__ __launch_bounds__(64) void iter_wave_kernel(BatchDev b, FwdDfaDev f, 
   pike::TagGen tg;
   FwdDfaDev fg = f;
   fg.hot = 0;  // global-table stepping only (the LDS holds the Pike VM lists)
+  fg.all = 0;
   for (uint64_t h = blockIdx.x; h < b.count; h += gridDim.x) {
     const uint8_t *base;
     uint64_t len;
@@ -611,8 +722,13 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
     uint64_t *off = (uint64_t *)(buf + al(sz_units) + al(sz_slots) + al(sz_counts));
     uint64_t *queue = (uint64_t *)(buf + al(sz_units) + al(sz_slots) + al(sz_counts) + al(sz_off));
     unsigned long long *qlen = (unsigned long long *)(buf + total - 256);
-    const int per_cu = std::max<int>(1, std::min<int>(8, (int)((160u * 1024u) / std::max<size_t>(iter_lds_bytes(*f, r), 1))));
-    const int grid = grid_cap(nunits, 256, cus, per_cu);
+    // threads per block: the hot tables are staged once per block, so larger
+    // blocks let more waves share one LDS copy (occupancy of these latency-
+    // bound per-lane scans); RURE_AMD_ITER_BS overrides (tuning)
+    int bs = 1024;
+    if (const char *v = getenv("RURE_AMD_ITER_BS")) bs = std::max(64, std::min(1024, atoi(v)));
+    const int per_cu = std::max<int>(1, std::min<int>(2048 / bs, (int)((160u * 1024u) / std::max<size_t>(iter_lds_bytes(*f, r), 1))));
+    const int grid = grid_cap(nunits, bs, cus, per_cu);
     do {
       if ((e = hipMemsetAsync(counts + nunits, 0, 4, st)) != hipSuccess) break;
       if ((e = hipMemsetAsync(qlen, 0, 8, st)) != hipSuccess) break;
@@ -620,8 +736,8 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
       if ((e = allow_lds(iter_spec_kernel, lb)) != hipSuccess || (e = allow_lds(iter_fix_kernel, lb)) != hipSuccess ||
           (e = allow_lds(iter_emit_kernel, lb)) != hipSuccess)
         break;
-      hipLaunchKernelGGL(iter_spec_kernel, dim3(grid), dim3(256), iter_lds_bytes(*f, r), st, b, g, nunits, *f, r, units, slots,
-                         counts);
+      hipLaunchKernelGGL(iter_spec_kernel, dim3(grid), dim3(bs), iter_lds_bytes(*f, r), st, b, g, nunits, *f, r, units,
+                         slots, counts);
       if ((e = hipGetLastError()) != hipSuccess) break;
       if (spn && spn->entry) {
         FwdDfaDev fw = *f;
@@ -629,22 +745,23 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
         RevDfaDev rw = r;
         rw.hot = 0;
         hipLaunchKernelGGL(iter_entry_kernel, dim3(1), dim3(64), 0, st, b, g, nunits, fw, rw, units, counts,
-                           spn->entry, queue, qlen);
+                           (const uint64_t *)slots, spn->entry, queue, qlen);
         if ((e = hipGetLastError()) != hipSuccess) break;
       }
       if (g.nk > 1) {
-        hipLaunchKernelGGL(iter_fix_kernel, dim3(grid), dim3(256), iter_lds_bytes(*f, r), st, b, g, nunits, *f, r, units,
-                           counts, queue, qlen);
+        hipLaunchKernelGGL(iter_fix_kernel, dim3(grid), dim3(bs), iter_lds_bytes(*f, r), st, b, g, nunits, *f, r, units,
+                           counts, (const uint64_t *)slots, queue, qlen);
         if ((e = hipGetLastError()) != hipSuccess) break;
         FwdDfaDev fw = *f;
         fw.hot = 0;
         RevDfaDev rw = r;
         rw.hot = 0;
-        hipLaunchKernelGGL(iter_walk_kernel, dim3(1), dim3(64), 0, st, b, g, nunits, fw, rw, units, counts, queue, qlen);
+        hipLaunchKernelGGL(iter_walk_kernel, dim3(1), dim3(64), 0, st, b, g, nunits, fw, rw, units, counts,
+                           (const uint64_t *)slots, queue, qlen);
         if ((e = hipGetLastError()) != hipSuccess) break;
       }
       if ((e = scan_counts(counts, off, nunits, st)) != hipSuccess) break;
-      hipLaunchKernelGGL(iter_emit_kernel, dim3(grid), dim3(256), iter_lds_bytes(*f, r), st, b, g, nunits, *f, r, units, slots,
+      hipLaunchKernelGGL(iter_emit_kernel, dim3(grid), dim3(bs), iter_lds_bytes(*f, r), st, b, g, nunits, *f, r, units, slots,
                          off, o.matches, o.cap);
       if ((e = hipGetLastError()) != hipSuccess) break;
       hipLaunchKernelGGL(iter_counts_kernel, dim3(grid_cap(b.count, 256, cus, 4)), dim3(256), 0, st, b.count, g.nk,

@@ -82,7 +82,32 @@ struct PackedFwd {
   std::vector<uint64_t> now_mask;
   std::vector<uint16_t> start;
   uint32_t hot = 0;
+  uint32_t all = 0;       // the LDS rows are exact for every state (hot = nstates)
+  uint32_t ustart1 = 0;   // 1 + the start state if every reachable flag set gives the same one
 };
+
+// 1 + the start state when all start flags a search can present (dfa.rs:
+// 1415-1464: text start / empty text / line start / word before / word
+// after, in the index layout of fwd_flag_index) map to one state — always
+// so without look-around assertions; 0 otherwise.
+uint32_t uniform_start(const DenseDfa &d) {
+  int found = -1;
+  for (int st = 0; st < 2; ++st)
+    for (int en = 0; en < 2; ++en)
+      for (int nl = 0; nl < 2; ++nl)
+        for (int wl = 0; wl < 2; ++wl)
+          for (int wn = 0; wn < 2; ++wn) {
+            if (st && (wl || !nl)) continue;  // no byte before the text start
+            if (nl && wl) continue;           // '\n' is not a word byte
+            if (en && (wn || !st)) continue;  // empty text: no byte after, start == end
+            const int idx = (st ? 1 : 0) | (en ? 2 : 0) | (nl ? 4 : 0) | (en ? 8 : 0) | (wl != wn ? 16 : 32) |
+                            (wl ? 64 : 0);
+            const int v = (int)d.start[idx];
+            if (found < 0) found = v;
+            else if (found != v) return 0;
+          }
+  return found < 0 ? 0 : (uint32_t)found + 1;
+}
 
 // Multi-byte fast table over the ASCII-hot sub-DFA (states [0, A)): bytes
 // are grouped into K local classes (identical columns over the hot states,
@@ -147,10 +172,26 @@ void build_stride_image(const DenseDfa &d, PackedFwd *p) {
   p->sent = (uint32_t)A * P;
 }
 
-bool pack_forward(const DenseDfa &d, PackedFwd *p, std::string *err) {
+bool pack_forward(const DenseDfa &d, PackedFwd *p, std::string *err, bool all = false) {
   if (d.nstates > 65535) {
     if (err) *err = "DFA has too many states for u16 tables";
     return false;
+  }
+  p->ustart1 = uniform_start(d);
+  if (all && d.nstates <= 255) {
+    // small automata (find_iter / reverse scans): every state's exact row in
+    // LDS, so match, dead and restart steps never touch the global table
+    p->all = 1;
+    p->hot = (uint32_t)d.nstates;
+    p->lds.assign(((size_t)d.nstates * kRow + 15) & ~(size_t)15, 0);
+    for (int st = 0; st < d.nstates; ++st)
+      for (int b = 0; b < 256; ++b) p->lds[(size_t)st * kRow + b] = (uint8_t)d.trans[(size_t)st * 256 + b];
+    p->full.resize((size_t)d.nstates * 256);
+    for (size_t i = 0; i < p->full.size(); ++i) p->full[i] = (uint16_t)d.trans[i];
+    p->eof.assign(d.eof_match.begin(), d.eof_match.end());
+    p->start.resize(128);
+    for (int i = 0; i < 128; ++i) p->start[i] = (uint16_t)d.start[i];
+    return true;
   }
   // LDS fast table: the normal states reachable through ASCII bytes are
   // numbered first; hold them plus further BFS-order states in the smallest
@@ -433,7 +474,7 @@ bool build_regex(rure *re) {
   DfaBuildLimits lim;
   std::string err;
   if (!build_dense_dfa(re->fwd, lim, &re->dfwd, &err) || !build_dense_dfa(re->rev, lim, &re->drev, &err) ||
-      !pack_forward(re->dfwd, &re->pf, &err) || !pack_forward(re->drev, &re->pr, &err)) {
+      !pack_forward(re->dfwd, &re->pf, &err) || !pack_forward(re->drev, &re->pr, &err, true)) {
     re->dfa_err = err.empty() ? "reverse DFA too large" : err;
     re->dfa_ok = false;
     if (!re->nfa_ok) re->dfa_err += "; " + nerr;
@@ -591,6 +632,9 @@ DevTables *regex_device(rure *re, std::string *err) {
     t.r.n_match_end = rv.n_match_end;
     t.r.dead = rv.dead;
     t.r.quit = rv.quit < 0 ? 0xFFFFFFFFu : (uint32_t)rv.quit;
+    t.r.all = re->pr.all;
+    t.r.ustart1 = re->pr.ustart1;
+    t.f.ustart1 = pf.ustart1;
   }
   if (t.quit_possible && !re->nfa_ok) {
     (void)hipFree(t.blob);
@@ -702,7 +746,7 @@ bool build_iter_dfa(rure *re) {
     DfaBuildLimits lim;
     lim.strip = true;
     std::string e;
-    re->iter_ok = build_dense_dfa(re->fwd, lim, &re->dfwd_iter, &e) && pack_forward(re->dfwd_iter, &re->pf_iter, &e);
+    re->iter_ok = build_dense_dfa(re->fwd, lim, &re->dfwd_iter, &e) && pack_forward(re->dfwd_iter, &re->pf_iter, &e, true);
   }
   return re->iter_ok;
 }
@@ -745,6 +789,8 @@ const FwdDfaDev *iter_device(rure *re, const DevTables &t, std::string *err) {
   f.n_match_end = fw.n_match_end;
   f.dead = fw.dead;
   f.quit = fw.quit < 0 ? 0xFFFFFFFFu : (uint32_t)fw.quit;
+  f.all = pf.all;
+  f.ustart1 = pf.ustart1;
   re->iter_dev[d] = {tmp.blob, f};
   return &re->iter_dev[d].second;
 }
@@ -1368,7 +1414,11 @@ hipError_t run_find_iter(rure *re, DevTables *t, const BatchDev &b, const IterOu
     const uint64_t lim = sp ? std::min<uint64_t>(b.length, sp->hi) : b.length;
     if (!b.offs && lim > b.start && b.count) {
       const uint64_t span = lim - b.start;
-      const uint64_t target = (uint64_t)t->cus * 1024;  // 16 waves per CU
+      // lanes in flight: 32 waves per CU (per-lane scans are latency-bound);
+      // RURE_AMD_ITER_LANES (per CU) overrides (tuning)
+      uint64_t per_cu = 2048;
+      if (const char *v = getenv("RURE_AMD_ITER_LANES")) per_cu = std::max(64, atoi(v));
+      const uint64_t target = (uint64_t)t->cus * per_cu;
       const uint64_t per_h = (target + b.count - 1) / b.count;
       chunk = odd_lines(std::max<uint64_t>(4096, (span + per_h - 1) / per_h));
     }
@@ -1529,7 +1579,7 @@ int rure_amd_dfa_info_get(rure *re, int which, rure_amd_dfa_info *info) {
   memset(info, 0, sizeof(*info));
   if (!build_regex_dfas(re)) { info->ok = 0; return RURE_AMD_ERR_DFA; }
   if (which == 0) fill_info(re->dfwd, re->fwd, re->pf.hot, info, &re->pf);
-  else if (which == 1) fill_info(re->drev, re->rev, 0, info);
+  else if (which == 1) fill_info(re->drev, re->rev, re->pr.hot, info);
   else {
     if (!build_iter_dfa(re)) { info->ok = 0; return RURE_AMD_ERR_DFA; }
     fill_info(re->dfwd_iter, re->fwd, re->pf_iter.hot, info, &re->pf_iter);

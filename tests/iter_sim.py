@@ -58,7 +58,7 @@ def equiv(ca, a, cb, b):
     return a == b
 
 
-def find_iter_chunked(fwd, rev, t, chunk, start=0):
+def find_iter_chunked(fwd, rev, t, chunk, start=0, slots=1 << 30):
     INF = float("inf")
     span = max(0, len(t) - start)
     nk = 1 if span <= chunk else (span + chunk - 1) // chunk
@@ -75,9 +75,49 @@ def find_iter_chunked(fwd, rev, t, chunk, start=0):
         units.append({"entry": (c0, None), "spec": ms, "spec_exit": it.exit, "spec_clean": it.clean,
                       "exit": it.exit, "clean": it.clean, "fixed": False, "count": len(ms)})
 
+    def sync_from_slots(j, E):
+        """repair_unit's fast path: S's recorded matches tell where the true
+        iteration entered with E joins the speculative one."""
+        c0, c1 = bounds[j]
+        U = units[j]
+        spec = U["spec"]
+        if len(spec) > slots or E[0] < c0:
+            return None
+        # p_i, lm_i: S's iteration state before it yielded match i
+        ps, lms = [c0], [None]
+        for (s_, e_) in spec:
+            ps.append(e_ + 1 if s_ == e_ else e_)
+            lms.append(e_)
+        i = max(k for k in range(len(ps)) if ps[k] <= E[0])
+        if E[0] == ps[i] and E[1] != lms[i]:
+            # same search start, different last match: S's search from p_i
+            # yielded its match i directly (no empty match skipped) when it
+            # had no last match (i == 0) or match i starts at p_i
+            if not (i == 0 or (i < len(spec) and spec[i][0] == ps[i])):
+                return None
+        if i < len(spec):
+            s_, e_ = spec[i]
+            if s_ < E[0] or (s_ == e_ and e_ == E[1]):
+                return None
+            return i
+        return i if U["spec_clean"] else None
+
     def repair(j, E):
         c0, c1 = bounds[j]
         U = units[j]
+        U["entry"], U["fixed"], U["skip"] = E, True, None
+        if E[0] >= c1:  # the true iteration skips the whole unit
+            U["count"], U["exit"] = 0, E
+            U["clean"] = E[0] == c1 and E[1] != c1
+            return not equiv(U["clean"], U["exit"], U["spec_clean"], U["spec_exit"])
+        i = sync_from_slots(j, E)
+        if i is not None:
+            if i < len(U["spec"]):
+                U["count"], U["skip"] = len(U["spec"]) - i, i
+                U["exit"], U["clean"] = U["spec_exit"], U["spec_clean"]
+                return False
+            U["count"], U["exit"], U["clean"] = 0, E, True
+            return not equiv(True, E, U["spec_clean"], U["spec_exit"])
         F = UnitIter(fwd, rev, t, E, c1)
         S = UnitIter(fwd, rev, t, (c0, None), c1)
         fm, sm = F.next(), S.next()
@@ -93,9 +133,10 @@ def find_iter_chunked(fwd, rev, t, chunk, start=0):
             else:
                 scnt += 1
                 sm = S.next()
-        U["entry"], U["fixed"] = E, True
         if synced:
             U["count"] = fcnt + U_len(U) - scnt
+            if fcnt == 0 and len(U["spec"]) <= slots:
+                U["skip"] = scnt
             U["exit"], U["clean"] = U["spec_exit"], U["spec_clean"]
             return False
         U["count"] = fcnt
@@ -123,8 +164,8 @@ def find_iter_chunked(fwd, rev, t, chunk, start=0):
                 break
             if X["clean"]:
                 W = units[u]
-                W["entry"], W["exit"], W["clean"], W["fixed"], W["count"] = \
-                    (bounds[u][0], None), W["spec_exit"], W["spec_clean"], False, len(W["spec"])
+                W["entry"], W["exit"], W["clean"], W["fixed"], W["count"], W["skip"] = \
+                    (bounds[u][0], None), W["spec_exit"], W["spec_clean"], False, len(W["spec"]), None
             else:
                 repair(u, X["exit"])
             X = units[u]
@@ -137,6 +178,9 @@ def find_iter_chunked(fwd, rev, t, chunk, start=0):
         if not U["fixed"]:
             assert len(U["spec"]) == U["count"]
             out.extend(U["spec"])
+            continue
+        if U.get("skip") is not None:  # repaired by joining the speculation: copy
+            out.extend(U["spec"][U["skip"]:U["skip"] + U["count"]])
             continue
         it = UnitIter(fwd, rev, t, U["entry"], bounds[u][1])
         got = []

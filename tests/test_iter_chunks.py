@@ -24,7 +24,8 @@ def text(seed, n):
 
 @pytest.mark.parametrize("pat", PATTERNS)
 @pytest.mark.parametrize("chunk", [7, 16, 61])
-def test_chunked_iter_matches_oracle(pat, chunk):
+@pytest.mark.parametrize("slots", [2, 1 << 30])
+def test_chunked_iter_matches_oracle(pat, chunk, slots):
     re = R.Regex(pat)
     assert re.nfa_tables()[0]["looks"] == 0
     fwd = re.dfa_tables(2)
@@ -33,7 +34,7 @@ def test_chunked_iter_matches_oracle(pat, chunk):
     for i in range(6):
         t = text(zlib.crc32(pat.encode()) + i, 150 + 37 * i)
         exp = o.find_iter(t)
-        got = find_iter_chunked(fwd, rev, t, chunk)
+        got = find_iter_chunked(fwd, rev, t, chunk, slots=slots)
         assert got == exp, (pat, chunk, i)
 
 
