@@ -275,6 +275,13 @@ int rure_amd_set_nfa_export(rure_set *re, rure_amd_nfa_info *info, uint32_t *lea
  * entries + 1 u32 CSR offsets into save_slot (u16).  *n_slots receives the
  * length of save_slot; NULL arrays query it. */
 int rure_amd_nfa_saves_export(rure *re, uint32_t *save_off, uint16_t *save_slot, size_t *n_slots);
+/* The regex as a finite string set, as the literal find_iter engine uses it
+ * (the GPU counterpart of the reference's complete-prefix Literal engine,
+ * exec.rs:1148-1166): returns the number of literals (0 = not a string set:
+ * the DFA kernels iterate), in leftmost-first priority order; lens[i] and
+ * bytes[32 * i ...] receive the first `cap` of them (NULL arrays: count only).
+ * Host only. */
+int64_t rure_amd_literals_export(rure *re, uint32_t *lens, uint8_t *bytes, size_t cap);
 /* 1 if batched searches of this regex run the DFA kernels, 0 if only the
  * Pike VM kernel (automaton too large), negative on error. */
 int rure_amd_uses_dfa(rure *re);

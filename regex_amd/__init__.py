@@ -523,6 +523,18 @@ class Regex(object):
         """True if batched searches run the DFA kernels (else the Pike VM kernel)."""
         return N.rure_amd_uses_dfa(self._re) == 1
 
+    def literals(self):
+        """The regex as a finite string set in leftmost-first priority order, as
+        the literal find_iter engine uses it, or None if it is not one."""
+        import numpy as np
+        n = N.rure_amd_literals_export(self._re, None, None, 0)
+        if n <= 0:
+            return None
+        lens = np.zeros(n, dtype=np.uint32)
+        buf = np.zeros(32 * n, dtype=np.uint8)
+        N.rure_amd_literals_export(self._re, lens.ctypes.data, buf.ctypes.data, n)
+        return [bytes(buf[32 * i:32 * i + int(lens[i])]) for i in range(n)]
+
     def nfa_tables(self):
         """Pike VM closure tables of the NFA kernel: (info, leaves, cl_off, entries)."""
         return _nfa_export(N.rure_amd_nfa_export, self._re)

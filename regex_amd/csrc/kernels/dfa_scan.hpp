@@ -43,7 +43,19 @@ struct FwdDfaDev {
   uint32_t n_normal, n_match_end, dead, quit;
   uint32_t all;               // lds_image rows are exact for every state (hot = nstates <= 255)
   uint32_t ustart1;           // 1 + the start state when it does not depend on the flags, else 0
+  // find_iter DFA only: the regex as a finite string set (host/literals.hpp),
+  // lit_n = 0 if it is not one.  Image (kLit* offsets): 64 Kibit bitmap over
+  // a hash of the first lit_k bytes, then keys (u32, first lit_k bytes), lens
+  // (u8) and bytes (32 per literal), in leftmost-first priority order.
+  const uint8_t *lit_image;
+  uint32_t lit_bytes, lit_n, lit_k, lit_minlen, lit_maxlen;
 };
+
+// Literal engine image layout (at most kLitMax literals of kLitLen bytes).
+constexpr uint32_t kLitMax = 64, kLitLen = 32;
+constexpr uint32_t kLitKeys = 8192, kLitLens = kLitKeys + 4 * kLitMax, kLitBytes = kLitLens + kLitMax;
+constexpr uint32_t kLitImage = kLitBytes + kLitMax * kLitLen;
+__host__ __device__ inline uint32_t lit_hash(uint32_t key) { return (key * 0x9E3779B1u) >> 16; }
 
 struct RevDfaDev {
   const uint8_t *lds_image;   // hot table (same layout as FwdDfaDev::lds_image)

@@ -186,6 +186,296 @@ __global__ __launch_bounds__(1024) void iter_spec_kernel(BatchDev b, Geo g, uint
   }
 }
 
+// Branch-free exact steps for small automata (FwdDfaDev::all /
+// RevDfaDev::all: every state's row in LDS; dead and quit absorb).  Bytes
+// k in [k0, kend) of the 16 in `w` are stepped from `s`; lastk = the last k
+// whose step entered a match-flag state [nn, nme).  No per-byte branches:
+// a match, the dead state or a quit mid-chunk costs the same instructions as
+// any other byte, so the rare-event path of find_iter is not a serial
+// byte loop run by one lane while the rest of its wave waits.
+__device__ __forceinline__ uint32_t steps16(uint32_t s, const uint32_t w[4], uint32_t k0, uint32_t kend,
+                                            const uint8_t *tab, uint32_t nn, uint32_t nme, int &lastk) {
+#pragma unroll
+  for (uint32_t k = 0; k < 16; ++k) {
+    const uint32_t t = tab[s * kRow + ((w[k >> 2] >> ((k & 3) * 8)) & 0xFF)];
+    const bool act = k >= k0 && k < kend;
+    s = act ? t : s;
+    lastk = (act && t - nn < nme - nn) ? (int)k : lastk;
+  }
+  return s;
+}
+
+// Forward scan of text[at..end) (end - at <= 128 + 15, all-mode tables,
+// MODE_FIND: dfa.rs:576-764 up to the dead state): the window's blocks are
+// loaded first, then each goes through the exact4 fast chain and, if that
+// entered a match / dead / quit state, the branch-free steps16.
+__device__ __forceinline__ void fwd_window_all(LaneState &L, const FwdDfaDev &f, const uint8_t *lds,
+                                               const uint8_t *base, uint64_t at, uint64_t end) {
+  const uintptr_t a0 = (uintptr_t)(base + at) & ~(uintptr_t)15;
+  const uintptr_t ae = (uintptr_t)(base + end);
+  uint4 v[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+    if (a0 + 16 * k < ae) v[k] = *(const uint4 *)(a0 + 16 * k);
+  // position of the window's first byte (negative when the haystack starts
+  // mid-block)
+  const int64_t p0 = (int64_t)at - (int64_t)((uintptr_t)(base + at) & 15);
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const int64_t bp = p0 + 16 * k;
+    if (L.done || bp >= (int64_t)end) break;
+    const uint32_t k0 = bp < (int64_t)at ? (uint32_t)((int64_t)at - bp) : 0;
+    const uint32_t kend = (int64_t)end - bp < 16 ? (uint32_t)((int64_t)end - bp) : 16;
+    const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+    if (k0 == 0 && kend == 16) {
+      uint32_t t = L.s, mx = 0;
+      t = exact4(t, w[0], lds, mx);
+      t = exact4(t, w[1], lds, mx);
+      t = exact4(t, w[2], lds, mx);
+      t = exact4(t, w[3], lds, mx);
+      if (mx < f.n_normal) { L.s = t; continue; }
+    }
+    int lastk = -1;
+    L.s = steps16(L.s, w, k0, kend, lds, f.n_normal, f.n_match_end, lastk);
+    if (lastk >= 0) L.last = (uint64_t)(bp + lastk);  // Match(at - 1): the byte's position
+    if (L.s >= f.n_match_end) {
+      L.done = true;
+      L.quit = L.s != f.dead;
+    }
+  }
+}
+
+// rev_scan (exec.rs:651-661, dfa.rs:768-866) for all-mode reverse tables:
+// blocks walked backwards, bytes reversed in registers, branch-free steps.
+__device__ __forceinline__ uint64_t rev_scan_all(const RevDfaDev &r, const uint8_t *rlds, const uint8_t *base,
+                                                 uint64_t len, uint64_t lo, uint64_t me) {
+  uint32_t s = r.ustart1 ? r.ustart1 - 1 : r.start[rev_flag_index(base, lo, len, me)];
+  if (s == r.dead) return NONE;
+  uint64_t rs = NONE, a = me;
+  while (a > lo) {
+    const uintptr_t p = (uintptr_t)(base + a - 1);
+    const uint4 v = *(const uint4 *)(p & ~(uintptr_t)15);
+    const uint32_t w[4] = {__builtin_bswap32(v.w), __builtin_bswap32(v.z), __builtin_bswap32(v.y),
+                           __builtin_bswap32(v.x)};
+    const uint32_t k0 = 15 - (uint32_t)(p & 15);  // reversed index of the byte at a - 1
+    const uint32_t kend = a - lo < 16 - k0 ? k0 + (uint32_t)(a - lo) : 16;
+    int lastk = -1;
+    s = steps16(s, w, k0, kend, rlds, r.n_normal, r.n_match_end, lastk);
+    if (lastk >= 0) rs = a - (uint32_t)(lastk - k0);  // the reverse match flag: start = byte position + 1
+    a -= kend - k0;
+    if (s >= r.n_match_end) return s == r.dead ? rs : QUITMARK;
+  }
+  if (r.eof[s]) rs = lo;
+  return rs;
+}
+
+// Pass 1, burst-interleaved.  In iter_spec_kernel every search is a nest of
+// loops (forward scan to the dead state, reverse scan, restart), so a lane
+// whose search ends early waits, masked off, until every other lane of its
+// wave has finished its own forward loop — usually its whole unit — and then
+// scans the rest of its unit alone.  Here the wave loop is over bursts: in
+// each iteration every searching lane advances its current forward scan by
+// at most one aligned 128-byte burst (the same LDS fast path, fwd_range); a
+// lane whose scan ended does its reverse scan, applies the iteration rule
+// (re_trait.rs:197-221) and sets up its next search (exec.rs:632-662) in
+// the same iteration.  Same unit records as iter_spec_kernel.
+__global__ __launch_bounds__(1024) void iter_spec_burst_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f,
+                                                              RevDfaDev r, Unit *units, uint64_t *slots,
+                                                              uint32_t *counts) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const uint8_t *rlds = stage_tables(f, r, lds);
+  for (uint64_t u0 = (uint64_t)blockIdx.x * blockDim.x; u0 < nunits; u0 += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t u = u0 + threadIdx.x;
+    uint64_t h = 0, len = 0, c0 = 0, c1 = 0;
+    const uint8_t *base = b.hay;
+    uint64_t p = 0, lm = NONE, sp = 0, slm = NONE;  // iteration state and UnitIter's snapshot
+    uint64_t at = 0, at0 = 0, cutpos = NONE;        // the current forward scan
+    uint64_t ex_p = 0, ex_lm = NONE;
+    bool clean = true, quit = false, searching = false;
+    uint32_t n = 0;
+    LaneState L;
+    L.done = true;
+
+    auto finish = [&](uint64_t ep, uint64_t elm, bool cl) {
+      searching = false;
+      ex_p = ep;
+      ex_lm = elm;
+      clean = cl;
+    };
+    auto begin_search = [&]() {  // iter_next's loop top
+      if (p > len) { finish(sp, slm, true); return; }
+      lane_start(L, f, base, len, p);
+      at0 = at = p;
+      cutpos = (c1 > p && c1 - 1 <= len) ? c1 - 1 : NONE;
+      searching = true;
+    };
+    auto unit_next = [&]() {  // UnitIter::next's entry
+      if (p >= c1) { finish(p, lm, p == c1 && lm != c1); return; }
+      sp = p;
+      slm = lm;
+      begin_search();
+    };
+    if (u < nunits) {
+      unit_bounds(b, g, u, &h, &base, &len, &c0, &c1);
+      p = c0;
+      unit_next();
+    }
+    while (__ballot(searching)) {
+      if (!searching) continue;
+      if (at == cutpos) {  // dfa_find_cut: no new match may start at or after the cut
+        L.s = f.strip[L.s];
+        if (L.s == f.dead) L.done = true;
+        cutpos = NONE;
+      }
+      if (!L.done && at < len) {
+        uint64_t lim = (((uintptr_t)(base + at) & ~(uintptr_t)15) + 128) - (uintptr_t)base;
+        lim = min(lim, len);
+        if (cutpos != NONE) lim = min(lim, cutpos);
+        if (f.all) fwd_window_all(L, f, lds, base, at, lim);
+        else fwd_range<MODE_FIND>(L, f, lds, base, at, lim);
+        at = lim;
+      }
+      if (!L.done && (at < len || cutpos == len)) continue;  // the scan goes on next burst
+      // the forward scan ended: EOF step, reverse scan, iteration rule
+      if (!L.done && f.eof[L.s]) L.last = len;
+      if (L.quit) { quit = true; finish(sp, slm, false); continue; }
+      if (L.last == NONE) { finish(sp, slm, true); continue; }
+      const uint64_t me = L.last;
+      uint64_t ms = at0;
+      if (me != at0) {  // exec.rs:647
+        const uint64_t rs = r.all ? rev_scan_all(r, rlds, base, len, at0, me) : rev_scan(r, rlds, base, len, at0, me);
+        if (rs == QUITMARK) { quit = true; finish(sp, slm, false); continue; }
+        if (rs == NONE) { finish(sp, slm, true); continue; }
+        ms = rs;
+      }
+      if (ms == me) {
+        p = me + 1;
+        if (lm == me) { begin_search(); continue; }  // empty match at the previous match end: skipped
+      } else {
+        p = me;
+      }
+      lm = me;
+      if (ms >= c1) { finish(sp, slm, true); continue; }  // owned by the next unit
+      if (n < g.slots) *(ulonglong2 *)&slots[(u * g.slots + n) * 2] = make_ulonglong2(ms, me);
+      ++n;
+      unit_next();
+    }
+    if (u < nunits) {
+      Unit U;
+      U.entry = {c0, NONE};
+      U.exit = {ex_p, ex_lm};
+      U.spec_exit = U.exit;
+      U.spec_count = n;
+      U.flags = (clean ? (U_SPEC_CLEAN | U_CLEAN) : 0) | (quit ? U_QUIT : 0);
+      U.skip = U.pad = 0;
+      units[u] = U;
+      counts[u] = n;
+    }
+  }
+}
+
+// Pass 1 with the literal engine, for regexes that are a finite set of
+// strings (host/literals.hpp; the reference runs its complete-prefix Literal
+// engine for them, exec.rs:1148-1166, literals.rs:28-250).  A unit's
+// speculative iteration needs no automaton: every start position is tested
+// on its own — a hash of its first lit_k bytes against a 64 Kibit LDS bitmap
+// of the literals' prefixes, the counterpart of Teddy's fingerprint filter
+// (simd_accel/teddy128.rs) — so the 64 positions of a step are independent
+// (no dependent chain per byte).  Hits are verified in priority order (the
+// first literal that matches is the leftmost-first match) and the greedy
+// iteration of re_trait.rs:197-221 keeps those starting at or after the
+// previous match end (literals are non-empty).  The unit records are the
+// same as iter_spec_kernel's; repairs and the walker use the DFA.
+__device__ __forceinline__ int lit_verify(const FwdDfaDev &f, const uint8_t *lds, const uint8_t *base, uint64_t len,
+                                          uint64_t i) {
+  uint32_t key = 0;
+  for (uint32_t j = 0; j < f.lit_k; ++j) key |= (uint32_t)base[i + j] << (8 * j);
+  const uint32_t *keys = (const uint32_t *)(lds + kLitKeys);
+  for (uint32_t x = 0; x < f.lit_n; ++x) {
+    if (keys[x] != key) continue;
+    const uint32_t ln = lds[kLitLens + x];
+    if (i + ln > len) continue;
+    const uint8_t *lb = lds + kLitBytes + x * kLitLen;
+    uint32_t j = f.lit_k;
+    while (j < ln && base[i + j] == lb[j]) ++j;
+    if (j == ln) return (int)x;
+  }
+  return -1;
+}
+
+template <bool K4>
+__global__ __launch_bounds__(1024) void iter_spec_lit_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f,
+                                                            Unit *units, uint64_t *slots, uint32_t *counts) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  for (uint32_t i = threadIdx.x * 16; i < f.lit_bytes; i += blockDim.x * 16)
+    *(uint4 *)(lds + i) = *(const uint4 *)(f.lit_image + i);
+  __syncthreads();
+  const uint32_t *bitmap = (const uint32_t *)lds;
+  const uint32_t kmask = K4 ? 0xFFFFFFFFu : ((1u << (8 * f.lit_k)) - 1);
+  for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < nunits; u += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t h, len, c0, c1;
+    const uint8_t *base;
+    unit_bounds(b, g, u, &h, &base, &len, &c0, &c1);
+    uint64_t p = c0, lm = NONE;
+    uint32_t n = 0;
+    // candidate starts: [c0, iend) — before the cut, room for the shortest literal
+    const uint64_t iend = min(c1, len + 1 >= f.lit_minlen ? len + 1 - f.lit_minlen : 0);
+    if (iend > c0) {
+      const uintptr_t hi_blk = (uintptr_t)(base + len);
+      const uintptr_t aend = (uintptr_t)(base + iend);
+      for (uintptr_t a = (uintptr_t)(base + c0) & ~(uintptr_t)15; a < aend; a += 64) {
+        // 64 positions per step: 4 blocks and the first word after them
+        uint32_t d[17];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          uint4 v = make_uint4(0, 0, 0, 0);
+          if (a + 16 * k < hi_blk) v = *(const uint4 *)(a + 16 * k);
+          d[4 * k] = v.x;
+          d[4 * k + 1] = v.y;
+          d[4 * k + 2] = v.z;
+          d[4 * k + 3] = v.w;
+        }
+        d[16] = (a + 64 < hi_blk) ? *(const uint32_t *)(a + 64) : 0u;
+        uint32_t clo = 0, chi = 0;
+#pragma unroll
+        for (int j = 0; j < 64; ++j) {
+          const uint32_t w = (j & 3) ? __builtin_amdgcn_alignbyte(d[(j >> 2) + 1], d[j >> 2], j & 3) : d[j >> 2];
+          const uint32_t hh = lit_hash(K4 ? w : (w & kmask));
+          const uint32_t bit = (bitmap[hh >> 5] >> (hh & 31)) & 1u;
+          if (j < 32) clo |= bit << j;
+          else chi |= bit << (j - 32);
+        }
+        uint64_t cand = ((uint64_t)chi << 32) | clo;
+        const int64_t p0 = (int64_t)(a - (uintptr_t)base);
+        while (cand) {
+          const int j = __builtin_ctzll(cand);
+          cand &= cand - 1;
+          const int64_t i = p0 + j;
+          if (i < (int64_t)c0 || i < (int64_t)p || (uint64_t)i >= iend) continue;
+          const int x = lit_verify(f, lds, base, len, (uint64_t)i);
+          if (x < 0) continue;
+          const uint64_t e = (uint64_t)i + lds[kLitLens + x];
+          if (n < g.slots) *(ulonglong2 *)&slots[(u * g.slots + n) * 2] = make_ulonglong2((uint64_t)i, e);
+          ++n;
+          p = lm = e;
+        }
+      }
+    }
+    // UnitIter's exit: the state before the search that finds no owned match
+    // (clean), or the end of a match running up to / past the cut
+    Unit U;
+    U.entry = {c0, NONE};
+    U.exit = {p, lm};
+    U.spec_exit = U.exit;
+    U.spec_count = n;
+    const bool clean = p < c1 || (p == c1 && lm != c1);
+    U.flags = clean ? (U_SPEC_CLEAN | U_CLEAN) : 0;
+    U.skip = U.pad = 0;
+    units[u] = U;
+    counts[u] = n;
+  }
+}
+
 // Where the true iteration of unit j, entered with E, joins the speculative
 // one S (started fresh at c0), read off S's recorded matches: S's state
 // before it yielded match i is (p_i, lm_i) (p_0 = c0, lm_0 = none; then the
@@ -725,7 +1015,7 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
     // threads per block: the hot tables are staged once per block, so larger
     // blocks let more waves share one LDS copy (occupancy of these latency-
     // bound per-lane scans); RURE_AMD_ITER_BS overrides (tuning)
-    int bs = 1024;
+    int bs = 256;
     if (const char *v = getenv("RURE_AMD_ITER_BS")) bs = std::max(64, std::min(1024, atoi(v)));
     const int per_cu = std::max<int>(1, std::min<int>(2048 / bs, (int)((160u * 1024u) / std::max<size_t>(iter_lds_bytes(*f, r), 1))));
     const int grid = grid_cap(nunits, bs, cus, per_cu);
@@ -733,11 +1023,23 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
       if ((e = hipMemsetAsync(counts + nunits, 0, 4, st)) != hipSuccess) break;
       if ((e = hipMemsetAsync(qlen, 0, 8, st)) != hipSuccess) break;
       const size_t lb = iter_lds_bytes(*f, r);
-      if ((e = allow_lds(iter_spec_kernel, lb)) != hipSuccess || (e = allow_lds(iter_fix_kernel, lb)) != hipSuccess ||
+      if ((e = allow_lds(iter_spec_kernel, lb)) != hipSuccess || (e = allow_lds(iter_spec_burst_kernel, lb)) != hipSuccess || (e = allow_lds(iter_fix_kernel, lb)) != hipSuccess ||
           (e = allow_lds(iter_emit_kernel, lb)) != hipSuccess)
         break;
-      hipLaunchKernelGGL(iter_spec_kernel, dim3(grid), dim3(bs), iter_lds_bytes(*f, r), st, b, g, nunits, *f, r, units,
-                         slots, counts);
+      if (f->lit_n && getenv("RURE_AMD_LIT")) {  // opt-in: measured slower than the DFA
+        if (f->lit_k == 4)
+          hipLaunchKernelGGL(iter_spec_lit_kernel<true>, dim3(grid_cap(nunits, bs, cus, 2048 / bs)), dim3(bs),
+                             kLitImage, st, b, g, nunits, *f, units, slots, counts);
+        else
+          hipLaunchKernelGGL(iter_spec_lit_kernel<false>, dim3(grid_cap(nunits, bs, cus, 2048 / bs)), dim3(bs),
+                             kLitImage, st, b, g, nunits, *f, units, slots, counts);
+      } else if (!getenv("RURE_AMD_ITER_NESTED")) {
+        hipLaunchKernelGGL(iter_spec_burst_kernel, dim3(grid), dim3(bs), iter_lds_bytes(*f, r), st, b, g, nunits, *f,
+                           r, units, slots, counts);
+      } else {
+        hipLaunchKernelGGL(iter_spec_kernel, dim3(grid), dim3(bs), iter_lds_bytes(*f, r), st, b, g, nunits, *f, r,
+                           units, slots, counts);
+      }
       if ((e = hipGetLastError()) != hipSuccess) break;
       if (spn && spn->entry) {
         FwdDfaDev fw = *f;

@@ -23,6 +23,7 @@
 
 #include "host/dfa_build.hpp"
 #include "host/nfa_build.hpp"
+#include "host/literals.hpp"
 #include "host/program.hpp"
 #include "host/syntax.hpp"
 #include "host/unicode_tables.h"
@@ -408,6 +409,8 @@ struct rure {
   bool iter_built = false, iter_ok = false;
   DenseDfa dfwd_iter;
   PackedFwd pf_iter;
+  bool lit_ok = false;      // the regex is a finite string set (literal find_iter engine)
+  LiteralSet lits;
   std::map<int, std::pair<void *, FwdDfaDev>> iter_dev;
 };
 
@@ -747,6 +750,7 @@ bool build_iter_dfa(rure *re) {
     lim.strip = true;
     std::string e;
     re->iter_ok = build_dense_dfa(re->fwd, lim, &re->dfwd_iter, &e) && pack_forward(re->dfwd_iter, &re->pf_iter, &e, true);
+    re->lit_ok = extract_literals(re->nfa, kLitMax, kLitLen, &re->lits);
   }
   return re->iter_ok;
 }
@@ -771,6 +775,26 @@ const FwdDfaDev *iter_device(rure *re, const DevTables &t, std::string *err) {
   size_t o_eof = b.add(pf.eof.data(), pf.eof.size());
   size_t o_start = b.add(pf.start.data(), 256);
   size_t o_strip = b.add(strip.data(), strip.size() * 2);
+  std::vector<uint8_t> lit_img;
+  uint32_t lit_k = 0;
+  if (re->lit_ok) {
+    // literal engine image (dfa_scan.hpp kLit*): prefix-hash bitmap, keys,
+    // lengths, bytes
+    lit_k = (uint32_t)std::min<size_t>(re->lits.minlen, 4);
+    lit_img.assign(kLitImage, 0);
+    uint32_t *bitmap = (uint32_t *)lit_img.data();
+    for (size_t x = 0; x < re->lits.lits.size(); ++x) {
+      const std::string &l = re->lits.lits[x];
+      uint32_t key = 0;
+      for (uint32_t j = 0; j < lit_k; ++j) key |= (uint32_t)(uint8_t)l[j] << (8 * j);
+      const uint32_t h = lit_hash(key);
+      bitmap[h >> 5] |= 1u << (h & 31);
+      std::memcpy(lit_img.data() + kLitKeys + 4 * x, &key, 4);
+      lit_img[kLitLens + x] = (uint8_t)l.size();
+      std::memcpy(lit_img.data() + kLitBytes + kLitLen * x, l.data(), l.size());
+    }
+  }
+  size_t o_lit = lit_img.empty() ? 0 : b.add(lit_img.data(), lit_img.size());
   DevTables tmp;
   if (!upload_blob(b, &tmp, err)) return nullptr;
   uint8_t *base = (uint8_t *)tmp.blob;
@@ -791,6 +815,14 @@ const FwdDfaDev *iter_device(rure *re, const DevTables &t, std::string *err) {
   f.quit = fw.quit < 0 ? 0xFFFFFFFFu : (uint32_t)fw.quit;
   f.all = pf.all;
   f.ustart1 = pf.ustart1;
+  if (!lit_img.empty()) {
+    f.lit_image = base + o_lit;
+    f.lit_bytes = kLitImage;
+    f.lit_n = (uint32_t)re->lits.lits.size();
+    f.lit_k = lit_k;
+    f.lit_minlen = (uint32_t)re->lits.minlen;
+    f.lit_maxlen = (uint32_t)re->lits.maxlen;
+  }
   re->iter_dev[d] = {tmp.blob, f};
   return &re->iter_dev[d].second;
 }
@@ -1414,9 +1446,9 @@ hipError_t run_find_iter(rure *re, DevTables *t, const BatchDev &b, const IterOu
     const uint64_t lim = sp ? std::min<uint64_t>(b.length, sp->hi) : b.length;
     if (!b.offs && lim > b.start && b.count) {
       const uint64_t span = lim - b.start;
-      // lanes in flight: 32 waves per CU (per-lane scans are latency-bound);
+      // lanes in flight: 16 waves per CU (tools/iter_sweep.py);
       // RURE_AMD_ITER_LANES (per CU) overrides (tuning)
-      uint64_t per_cu = 2048;
+      uint64_t per_cu = 1024;
       if (const char *v = getenv("RURE_AMD_ITER_LANES")) per_cu = std::max(64, atoi(v));
       const uint64_t target = (uint64_t)t->cus * per_cu;
       const uint64_t per_h = (target + b.count - 1) / b.count;
@@ -1482,6 +1514,19 @@ int rure_amd_find_iter_batch(rure *re, const rure_amd_batch *batch, uint64_t *co
   if (!t->has_dfa && !re->nfa_ok) return RURE_AMD_ERR_DFA;
   IterOut o{counts, (uint64_t *)matches, capacity, total};
   return run_find_iter(re, t, b, o, (hipStream_t)stream, &err) == hipSuccess ? RURE_AMD_OK : RURE_AMD_ERR_HIP;
+}
+
+int64_t rure_amd_literals_export(rure *re, uint32_t *lens, uint8_t *bytes, size_t cap) {
+  if (!re) return RURE_AMD_ERR_ARG;
+  build_iter_dfa(re);
+  std::lock_guard<std::mutex> g(re->mu);
+  if (!re->lit_ok) return 0;
+  const auto &L = re->lits.lits;
+  for (size_t x = 0; x < L.size() && x < cap; ++x) {
+    if (lens) lens[x] = (uint32_t)L[x].size();
+    if (bytes) std::memcpy(bytes + kLitLen * x, L[x].data(), L[x].size());
+  }
+  return (int64_t)L.size();
 }
 
 int rure_amd_find_iter_span(rure *re, const uint8_t *haystack, size_t length, size_t lo, size_t hi,

@@ -1,0 +1,96 @@
+"""GPU parity of the literal find_iter engine (iter_spec_lit_kernel, used
+when the regex is a finite string set): chunked find_iter over long
+haystacks and over sharded spans must equal the oracle's find_iter
+(re_trait.rs:197-221) bit for bit, including overlapping candidates
+(`aa` in runs of `a`), priority between a literal and its prefix
+(`a|ab`, `ab|a`) and matches across unit cuts."""
+import random
+import zlib
+
+import numpy as np
+import pytest
+
+import regex_amd as R
+from golden_data import corpus, known_counts
+from oracle_py import OracleRegex
+from regex_amd.dist import find_iter_spans_local
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def literal_engine(monkeypatch):
+    # the literal engine is opt-in (slower than the DFA on the C3 variants)
+    monkeypatch.setenv("RURE_AMD_LIT", "1")
+
+PATTERNS = [r"agggtaaa|tttaccct", r"[cgt]gggtaaa|tttaccc[acg]", r"a|ab", r"ab|a", r"aa", r"e", r"(?i)holm",
+            r"Sherlock|Holmes|Watson", r"foo(bar)?", r"x(a|ab)(c|bcd)", r"[0-3]{2}", r"abc|abd|ab", r"é"]
+
+
+def dev(buf, cuda):
+    import torch
+    t = torch.zeros(len(buf) + 16, dtype=torch.uint8)
+    t[: len(buf)] = torch.from_numpy(np.frombuffer(buf, dtype=np.uint8).copy())
+    return t.to(cuda)
+
+
+def pairs(m):
+    return [(int(a), int(b)) for a, b in m.cpu().numpy()]
+
+
+def texts(pat):
+    rng = random.Random(zlib.crc32(pat.encode()))
+    alpha = [b"a", b"b", b"c", b"d", b"x", b"g", b"t", b"foo", b"bar", b"0", b"1", b"2", b"3", "é".encode(),
+             b"Holm", b"holm", b" ", b"aaaaaaaa"]
+    yield corpus("sherlock")[:300000]
+    yield corpus("regexdna")
+    yield b"a" * 100001
+    yield b"".join(rng.choice(alpha) for _ in range(60000))
+
+
+@pytest.mark.parametrize("pat", PATTERNS)
+def test_literal_find_iter(cuda, pat):
+    re = R.Regex(pat)
+    assert re.literals(), pat
+    o = OracleRegex(re)
+    for t in texts(pat):
+        exp = o.find_iter(t)
+        c, m = re.find_iter_batch(dev(t, cuda), stride=len(t), length=len(t), count=1)
+        assert int(c[0]) == len(exp) and pairs(m) == exp, (pat, len(t))
+
+
+@pytest.mark.parametrize("pat", [r"aa", r"a|ab", r"agggtaaa|tttaccct", r"Sherlock|Holmes|Watson"])
+def test_literal_spans(cuda, pat):
+    re = R.Regex(pat)
+    o = OracleRegex(re)
+    for t in texts(pat):
+        exp = o.find_iter(t)
+        for k in (2, 7):
+            got, _ = find_iter_spans_local(re, dev(t, cuda), len(t), k)
+            assert pairs(got) == exp, (pat, k)
+
+
+def test_literal_batch_of_haystacks(cuda):
+    re = R.Regex(r"Holmes|Watson")
+    o = OracleRegex(re)
+    text = corpus("sherlock")
+    L = 20000
+    n = len(text) // L
+    buf = text[: n * L]
+    c, m = re.find_iter_batch(dev(buf, cuda), stride=L, length=L, count=n)
+    got, k = pairs(m), 0
+    for i in range(n):
+        exp = o.find_iter(buf[i * L:(i + 1) * L])
+        assert int(c[i]) == len(exp) and got[k:k + len(exp)] == exp, i
+        k += len(exp)
+
+
+def test_regexdna_variants_literal_engine(cuda):
+    kc = known_counts()["regexdna"]
+    seq = R.Regex(kc["strip"]).replace_all(corpus("regexdna"), b"")
+    big = seq * 50
+    d = dev(big, cuda)
+    for v in kc["variants"]:
+        re = R.Regex(v["re"])
+        c, m = re.find_iter_batch(d, stride=len(big), length=len(big), count=1)
+        assert pairs(m) == OracleRegex(re).find_iter(big), v["re"]
