@@ -326,23 +326,6 @@ __device__ __forceinline__ bool core_careful(uint32_t &c, uint64_t &mask, const 
   return (mask & f.all) == f.all;
 }
 
-__device__ __forceinline__ bool core_step1(uint32_t &c, uint64_t &mask, const SetCoreDev &f, const uint8_t *cls,
-                                           const uint16_t *T, uint32_t b, bool &quit) {
-  const uint32_t k = cls[b];
-  if (c < f.hot) {
-    const uint32_t e = T[c * f.K + k];
-    const uint32_t code = e & 63;
-    if ((e >> 6) != f.hot && code != 63) {
-      if (code) mask |= 1ull << (code - 1);
-      c = e >> 6;
-      if (c == f.dead) return true;
-      if (c == f.quit) { quit = true; return true; }
-      return (mask & f.all) == f.all;
-    }
-  }
-  return core_careful(c, mask, f, k, quit);
-}
-
 __device__ __forceinline__ bool core_chunk16(uint32_t &c, uint64_t &mask, uint64_t &pend, const SetCoreDev &f,
                                              const uint8_t *cls, const uint16_t *T, uint4 v, bool &quit) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -377,6 +360,43 @@ __device__ __forceinline__ bool core_chunk16(uint32_t &c, uint64_t &mask, uint64
   return false;
 }
 
+// core_chunk16 over the bytes k in [k0, kend) of an aligned block only: the
+// head and the tail of a line (lines start anywhere) cost one pass of the
+// same branch-free lookup chain instead of up to 15 single steps each; the
+// inactive bytes leave the core and the bag unchanged.
+__device__ __forceinline__ bool core_chunk_masked(uint32_t &c, uint64_t &mask, uint64_t &pend, const SetCoreDev &f,
+                                                  const uint8_t *cls, const uint16_t *T, uint4 v, uint32_t k0,
+                                                  uint32_t kend, bool &quit) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t k[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) k[j] = cls[(w[j >> 2] >> ((j & 3) * 8)) & 0xFF];
+  if (c < f.hot) {
+    uint32_t t = c;
+    uint64_t bag = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) {
+      const uint32_t e = T[t * f.K + k[j]];
+      const bool act = j >= k0 && j < kend;
+      const uint32_t code = act ? (e & 63) : 0;
+      bag |= 1ull << code;
+      if (code == 63) pend |= f.gout[(size_t)t * f.K + k[j]];
+      t = act ? e >> 6 : t;
+    }
+    if (t != f.hot) {
+      mask |= (bag >> 1) & 0x3FFFFFFFFFFFFFFFull;
+      c = t;
+      if (c == f.dead) return true;
+      if (c == f.quit) { quit = true; return true; }
+      return (mask & f.all) == f.all;
+    }
+  }
+#pragma unroll 1
+  for (uint32_t j = k0; j < kend; ++j)
+    if (core_careful(c, mask, f, k[j], quit)) return true;
+  return false;
+}
+
 template <bool STRIDED>
 __global__ __launch_bounds__(1024) void set_core_kernel(BatchDev bt, SetCoreDev f, uint64_t *out) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -396,25 +416,19 @@ __global__ __launch_bounds__(1024) void set_core_kernel(BatchDev bt, SetCoreDev 
     uint32_t c;
     if (at > len) { c = f.dead; done = true; }
     else { c = f.start[fwd_flag_index(base, len, at)]; done = c == f.dead; }
-    if (!done && at < len && (((uintptr_t)(base + at)) & 15)) {  // head from one aligned block
+    if (!done && at < len && (((uintptr_t)(base + at)) & 15)) {  // head: the rest of one aligned block
       const uintptr_t a = (uintptr_t)(base + at);
-      const uint4 v = *(const uint4 *)(a & ~(uintptr_t)15);
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll 1
-      for (uint32_t j = (uint32_t)(a & 15); j < 16 && at < len && !done; ++j, ++at)
-        done = core_step1(c, mask, f, cls, T, (w[j >> 2] >> ((j & 3) * 8)) & 0xFF, quit);
+      const uint32_t k0 = (uint32_t)(a & 15);
+      const uint32_t kend = len - at < 16 - k0 ? k0 + (uint32_t)(len - at) : 16;
+      done = core_chunk_masked(c, mask, pend, f, cls, T, *(const uint4 *)(a & ~(uintptr_t)15), k0, kend, quit);
+      at += kend - k0;
     }
     while (!done && at + 16 <= len) {
       done = core_chunk16(c, mask, pend, f, cls, T, *(const uint4 *)(base + at), quit);
       at += 16;
     }
-    if (!done && at < len) {  // tail: at is 16-byte aligned here
-      const uint4 v = *(const uint4 *)(base + at);
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll 1
-      for (uint32_t j = 0; at < len && !done; ++j, ++at)
-        done = core_step1(c, mask, f, cls, T, (w[j >> 2] >> ((j & 3) * 8)) & 0xFF, quit);
-    }
+    if (!done && at < len)  // tail: at is 16-byte aligned here
+      done = core_chunk_masked(c, mask, pend, f, cls, T, *(const uint4 *)(base + at), 0, (uint32_t)(len - at), quit);
     uint64_t m;
     if (quit) m = QUITMARK;
     else if (done) m = mask | pend;
