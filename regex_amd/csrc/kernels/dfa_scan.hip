@@ -468,8 +468,12 @@ hipError_t launch_core_profile(const BatchDev &b, const SetCoreDev &f, uint64_t 
 }
 
 hipError_t launch_set_cores(const BatchDev &b, const SetCoreDev &f, uint64_t *out, hipStream_t st, int cus) {
-  const int per_cu = f.lds_bytes > 80 * 1024 ? 1 : 2;
-  const uint64_t blocks = (b.count + 1023) / 1024;
+  // threads per block (RURE_AMD_CORE_BS overrides, tuning); blocks per CU
+  // as the LDS table allows
+  int bs = 1024;
+  if (const char *v = getenv("RURE_AMD_CORE_BS")) bs = std::max(64, std::min(1024, atoi(v)));
+  const int per_cu = std::max<int>(1, std::min<int>(2048 / bs, (int)((160u * 1024u) / std::max<uint32_t>(f.lds_bytes, 1))));
+  const uint64_t blocks = (b.count + bs - 1) / bs;
   const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)cus * per_cu));
   hipError_t e;
   if (b.offs) {
@@ -477,13 +481,13 @@ hipError_t launch_set_cores(const BatchDev &b, const SetCoreDev &f, uint64_t *ou
         (e = hipFuncSetAttribute((const void *)set_core_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                  (int)f.lds_bytes)) != hipSuccess)
       return e;
-    hipLaunchKernelGGL((set_core_kernel<false>), dim3(grid), dim3(1024), f.lds_bytes, st, b, f, out);
+    hipLaunchKernelGGL((set_core_kernel<false>), dim3(grid), dim3(bs), f.lds_bytes, st, b, f, out);
   } else {
     if (f.lds_bytes > 64 * 1024 &&
         (e = hipFuncSetAttribute((const void *)set_core_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                  (int)f.lds_bytes)) != hipSuccess)
       return e;
-    hipLaunchKernelGGL((set_core_kernel<true>), dim3(grid), dim3(1024), f.lds_bytes, st, b, f, out);
+    hipLaunchKernelGGL((set_core_kernel<true>), dim3(grid), dim3(bs), f.lds_bytes, st, b, f, out);
   }
   return hipGetLastError();
 }

@@ -237,6 +237,13 @@ struct CoreSet {
   bool profiled = false;
 };
 
+// LDS budget of the core table (RURE_AMD_CORE_LDS overrides, tuning).
+size_t core_lds_budget() {
+  size_t b = 150 * 1024;
+  if (const char *v = getenv("RURE_AMD_CORE_LDS")) b = std::max<size_t>(4096, std::min<size_t>(150 * 1024, atol(v)));
+  return b;
+}
+
 // weights (optional, by core in first-appearance numbering): rank the cores
 // by decreasing weight (measured visits), ties in BFS order.
 bool build_set_cores(const DenseDfa &d, size_t lds_budget, CoreSet *cs,
@@ -510,7 +517,7 @@ bool build_set(rure_set *rs) {
   // Large sets: the byte-row hot table holds at most 255 states; switch to
   // the core form when more normal or match-reporting states than that exist.
   if (rs->dfa.n_normal > 255 || rs->dfa.n_match_end - rs->dfa.n_normal > 255)
-    build_set_cores(rs->dfa, 150 * 1024, &rs->cores);
+    build_set_cores(rs->dfa, core_lds_budget(), &rs->cores);
   rs->dfa_ok = true;
   return true;
 }
@@ -882,7 +889,7 @@ bool adapt_cores(rure_set *rs, DevTables *t, const BatchDev &b, hipStream_t st, 
   std::vector<uint64_t> w(cs.ncores, 0);
   for (uint32_t r = 0; r < cs.ncores; ++r) w[cs.order[r]] = h[r];
   CoreSet c2;
-  if (!build_set_cores(rs->dfa, 150 * 1024, &c2, &w)) return true;  // keep the BFS ranking
+  if (!build_set_cores(rs->dfa, core_lds_budget(), &c2, &w)) return true;  // keep the BFS ranking
   Blob bl;
   size_t c_lds = bl.add(c2.lds.data(), c2.lds.size());
   size_t c_core = bl.add(c2.gcore.data(), c2.gcore.size() * 2);
