@@ -73,10 +73,19 @@ class Ctx(object):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         local = int(os.environ.get("LOCAL_RANK", "0"))
+        # REGEX_AMD_BENCH_BACKEND=gloo rehearses the N > 1 paths with several
+        # ranks sharing one GPU (RCCL refuses duplicate devices); the driver's
+        # multi-GPU runs use the default, nccl (= RCCL over xGMI)
+        backend = os.environ.get("REGEX_AMD_BENCH_BACKEND", "nccl")
+        if backend != "nccl":
+            local %= max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
         self.dev = torch.device("cuda", local)
         if self.world > 1:
-            dist.init_process_group("nccl", device_id=self.dev)
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=self.dev)
+            else:
+                dist.init_process_group(backend)
         self.stream = torch.cuda.current_stream(self.dev)
 
     def kernel_ms(self, fn):

@@ -76,4 +76,24 @@ bool extract_literals(const Program &prog, size_t max_lits, size_t max_len, Lite
   return true;
 }
 
+bool can_match_empty(const Program &prog) {
+  std::vector<uint8_t> seen(prog.insts.size(), 0);
+  std::vector<uint32_t> stack{prog.start};
+  while (!stack.empty()) {
+    const uint32_t pc = stack.back();
+    stack.pop_back();
+    if (pc >= prog.insts.size() || seen[pc]) continue;
+    seen[pc] = 1;
+    const Inst &in = prog.insts[pc];
+    switch (in.op) {
+      case OP_MATCH: return true;
+      case OP_SAVE:
+      case OP_EMPTY: stack.push_back(in.x); break;
+      case OP_SPLIT: stack.push_back(in.x); stack.push_back(in.y); break;
+      default: break;  // OP_BYTES consumes a byte
+    }
+  }
+  return false;
+}
+
 }  // namespace rure_amd

@@ -28,4 +28,9 @@ struct LiteralSet {
 
 bool extract_literals(const Program &prog, size_t max_lits, size_t max_len, LiteralSet *out);
 
+// True if a Match instruction is reachable from the start without consuming
+// a byte (look-around assertions taken as passable): the regex may match the
+// empty string, so re_trait.rs:205-214's empty-match rule can apply.
+bool can_match_empty(const Program &prog);
+
 }  // namespace rure_amd

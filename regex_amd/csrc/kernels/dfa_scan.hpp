@@ -43,6 +43,8 @@ struct FwdDfaDev {
   uint32_t n_normal, n_match_end, dead, quit;
   uint32_t all;               // lds_image rows are exact for every state (hot = nstates <= 255)
   uint32_t ustart1;           // 1 + the start state when it does not depend on the flags, else 0
+  uint32_t nonempty;          // the regex never matches the empty string (the iteration's
+                              // last-match state then never matters)
   // find_iter DFA only: the regex as a finite string set (host/literals.hpp),
   // lit_n = 0 if it is not one.  Image (kLit* offsets): 64 Kibit bitmap over
   // a hash of the first lit_k bytes, then keys (u32, first lit_k bytes), lens

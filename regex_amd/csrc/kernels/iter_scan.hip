@@ -120,7 +120,7 @@ struct UnitIter {
     if (st.p >= c1) {  // the previous match ran up to / past the cut
       ended = true;
       exit = st;
-      clean = st.p == c1 && st.lm != c1;
+      clean = st.p == c1 && (st.lm != c1 || f.nonempty);
       return false;
     }
     const IterSt snap = st;
@@ -310,7 +310,7 @@ __global__ __launch_bounds__(1024) void iter_spec_burst_kernel(BatchDev b, Geo g
       searching = true;
     };
     auto unit_next = [&]() {  // UnitIter::next's entry
-      if (p >= c1) { finish(p, lm, p == c1 && lm != c1); return; }
+      if (p >= c1) { finish(p, lm, p == c1 && (lm != c1 || f.nonempty)); return; }
       sp = p;
       slm = lm;
       begin_search();
@@ -468,7 +468,7 @@ __global__ __launch_bounds__(1024) void iter_spec_lit_kernel(BatchDev b, Geo g, 
     U.exit = {p, lm};
     U.spec_exit = U.exit;
     U.spec_count = n;
-    const bool clean = p < c1 || (p == c1 && lm != c1);
+    const bool clean = p < c1 || (p == c1 && (lm != c1 || f.nonempty));
     U.flags = clean ? (U_SPEC_CLEAN | U_CLEAN) : 0;
     U.skip = U.pad = 0;
     units[u] = U;
@@ -535,7 +535,7 @@ __device__ bool repair_unit(const BatchDev &b, const Geo &g, const FwdDfaDev &f,
   U.skip = 0;
   bool changed;
   if (E.p >= c1) {  // the true iteration passes over the whole unit
-    const bool cl = E.p == c1 && E.lm != c1;
+    const bool cl = E.p == c1 && (E.lm != c1 || f.nonempty);
     counts[j] = 0;
     changed = !exit_equiv(cl, E, spec_clean, U.spec_exit);
     U.exit = E;
@@ -830,7 +830,7 @@ __global__ __launch_bounds__(64) void iter_wave_kernel(BatchDev b, FwdDfaDev f, 
       if (exit) {
         exit[0] = p;
         exit[1] = lm;
-        exit[2] = (p == hi && lm != hi) ? 1 : 0;
+        exit[2] = (p == hi && (lm != hi || f.nonempty)) ? 1 : 0;
       }
     }
   }

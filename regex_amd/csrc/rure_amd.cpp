@@ -645,6 +645,7 @@ DevTables *regex_device(rure *re, std::string *err) {
     t.r.all = re->pr.all;
     t.r.ustart1 = re->pr.ustart1;
     t.f.ustart1 = pf.ustart1;
+    t.f.nonempty = can_match_empty(re->nfa) ? 0 : 1;
   }
   if (t.quit_possible && !re->nfa_ok) {
     (void)hipFree(t.blob);
@@ -822,6 +823,7 @@ const FwdDfaDev *iter_device(rure *re, const DevTables &t, std::string *err) {
   f.quit = fw.quit < 0 ? 0xFFFFFFFFu : (uint32_t)fw.quit;
   f.all = pf.all;
   f.ustart1 = pf.ustart1;
+  f.nonempty = can_match_empty(re->nfa) ? 0 : 1;
   if (!lit_img.empty()) {
     f.lit_image = base + o_lit;
     f.lit_bytes = kLitImage;
