@@ -51,12 +51,14 @@ struct FwdDfaDev {
   // (u8) and bytes (32 per literal), in leftmost-first priority order.
   const uint8_t *lit_image;
   uint32_t lit_bytes, lit_n, lit_k, lit_minlen, lit_maxlen;
+  uint32_t lit_k8;            // every literal has >= 8 bytes: a second bitmap filters on bytes 4..7
 };
 
 // Literal engine image layout (at most kLitMax literals of kLitLen bytes).
 constexpr uint32_t kLitMax = 64, kLitLen = 32;
 constexpr uint32_t kLitKeys = 8192, kLitLens = kLitKeys + 4 * kLitMax, kLitBytes = kLitLens + kLitMax;
-constexpr uint32_t kLitImage = kLitBytes + kLitMax * kLitLen;
+constexpr uint32_t kLitBitmap2 = kLitBytes + kLitMax * kLitLen;  // second bitmap: bytes 4..7 (lit_k8)
+constexpr uint32_t kLitImage = kLitBitmap2 + 8192;
 __host__ __device__ inline uint32_t lit_hash(uint32_t key) { return (key * 0x9E3779B1u) >> 16; }
 
 struct RevDfaDev {

@@ -403,7 +403,7 @@ __device__ __forceinline__ int lit_verify(const FwdDfaDev &f, const uint8_t *lds
   return -1;
 }
 
-template <bool K4>
+template <bool K4, bool K8>
 __global__ __launch_bounds__(1024) void iter_spec_lit_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f,
                                                             Unit *units, uint64_t *slots, uint32_t *counts) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -411,6 +411,7 @@ __global__ __launch_bounds__(1024) void iter_spec_lit_kernel(BatchDev b, Geo g, 
     *(uint4 *)(lds + i) = *(const uint4 *)(f.lit_image + i);
   __syncthreads();
   const uint32_t *bitmap = (const uint32_t *)lds;
+  const uint32_t *bitmap2 = (const uint32_t *)(lds + kLitBitmap2);
   const uint32_t kmask = K4 ? 0xFFFFFFFFu : ((1u << (8 * f.lit_k)) - 1);
   for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < nunits; u += (uint64_t)gridDim.x * blockDim.x) {
     uint64_t h, len, c0, c1;
@@ -425,7 +426,7 @@ __global__ __launch_bounds__(1024) void iter_spec_lit_kernel(BatchDev b, Geo g, 
       const uintptr_t aend = (uintptr_t)(base + iend);
       for (uintptr_t a = (uintptr_t)(base + c0) & ~(uintptr_t)15; a < aend; a += 64) {
         // 64 positions per step: 4 blocks and the first word after them
-        uint32_t d[17];
+        uint32_t d[18];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           uint4 v = make_uint4(0, 0, 0, 0);
@@ -435,13 +436,25 @@ __global__ __launch_bounds__(1024) void iter_spec_lit_kernel(BatchDev b, Geo g, 
           d[4 * k + 2] = v.z;
           d[4 * k + 3] = v.w;
         }
-        d[16] = (a + 64 < hi_blk) ? *(const uint32_t *)(a + 64) : 0u;
+        if (a + 64 < hi_blk) {
+          const uint2 t2 = *(const uint2 *)(a + 64);
+          d[16] = t2.x;
+          d[17] = t2.y;
+        } else {
+          d[16] = d[17] = 0u;
+        }
         uint32_t clo = 0, chi = 0;
 #pragma unroll
         for (int j = 0; j < 64; ++j) {
           const uint32_t w = (j & 3) ? __builtin_amdgcn_alignbyte(d[(j >> 2) + 1], d[j >> 2], j & 3) : d[j >> 2];
           const uint32_t hh = lit_hash(K4 ? w : (w & kmask));
-          const uint32_t bit = (bitmap[hh >> 5] >> (hh & 31)) & 1u;
+          uint32_t bit = (bitmap[hh >> 5] >> (hh & 31)) & 1u;
+          if (K8) {  // bytes 4..7 too: candidates of a small alphabet (DNA) stay rare
+            const uint32_t w2 =
+                (j & 3) ? __builtin_amdgcn_alignbyte(d[(j >> 2) + 2], d[(j >> 2) + 1], j & 3) : d[(j >> 2) + 1];
+            const uint32_t h2 = lit_hash(w2);
+            bit &= (bitmap2[h2 >> 5] >> (h2 & 31)) & 1u;
+          }
           if (j < 32) clo |= bit << j;
           else chi |= bit << (j - 32);
         }
@@ -1026,13 +1039,24 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
       if ((e = allow_lds(iter_spec_kernel, lb)) != hipSuccess || (e = allow_lds(iter_spec_burst_kernel, lb)) != hipSuccess || (e = allow_lds(iter_fix_kernel, lb)) != hipSuccess ||
           (e = allow_lds(iter_emit_kernel, lb)) != hipSuccess)
         break;
-      if (f->lit_n && getenv("RURE_AMD_LIT")) {  // opt-in: measured slower than the DFA
-        if (f->lit_k == 4)
-          hipLaunchKernelGGL(iter_spec_lit_kernel<true>, dim3(grid_cap(nunits, bs, cus, 2048 / bs)), dim3(bs),
-                             kLitImage, st, b, g, nunits, *f, units, slots, counts);
+      // Literal engine: where the DFA does not fit LDS exactly (> 255 states,
+      // e.g. alternations of many words) it wins clearly (tools/lit_vs_dfa.py:
+      // 16 words 2.29 -> 0.72 ms, 64 words 5.43 -> 2.29 ms per GiB); with a
+      // small DFA it depends on the text (English -25 %, DNA +25 %), so the
+      // DFA stays.  RURE_AMD_LIT=1 / 0 forces it on / off.
+      const char *lit_env = getenv("RURE_AMD_LIT");
+      const bool use_lit = f->lit_n && (lit_env ? lit_env[0] == '1' : !f->all);
+      if (use_lit) {
+        const dim3 lg(grid_cap(nunits, bs, cus, 2048 / bs));
+        if (f->lit_k8)
+          hipLaunchKernelGGL((iter_spec_lit_kernel<true, true>), lg, dim3(bs), kLitImage, st, b, g, nunits, *f, units,
+                             slots, counts);
+        else if (f->lit_k == 4)
+          hipLaunchKernelGGL((iter_spec_lit_kernel<true, false>), lg, dim3(bs), kLitImage, st, b, g, nunits, *f, units,
+                             slots, counts);
         else
-          hipLaunchKernelGGL(iter_spec_lit_kernel<false>, dim3(grid_cap(nunits, bs, cus, 2048 / bs)), dim3(bs),
-                             kLitImage, st, b, g, nunits, *f, units, slots, counts);
+          hipLaunchKernelGGL((iter_spec_lit_kernel<false, false>), lg, dim3(bs), kLitImage, st, b, g, nunits, *f,
+                             units, slots, counts);
       } else if (!getenv("RURE_AMD_ITER_NESTED")) {
         hipLaunchKernelGGL(iter_spec_burst_kernel, dim3(grid), dim3(bs), iter_lds_bytes(*f, r), st, b, g, nunits, *f,
                            r, units, slots, counts);

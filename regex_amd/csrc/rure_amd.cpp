@@ -800,6 +800,12 @@ const FwdDfaDev *iter_device(rure *re, const DevTables &t, std::string *err) {
       std::memcpy(lit_img.data() + kLitKeys + 4 * x, &key, 4);
       lit_img[kLitLens + x] = (uint8_t)l.size();
       std::memcpy(lit_img.data() + kLitBytes + kLitLen * x, l.data(), l.size());
+      if (re->lits.minlen >= 8) {
+        uint32_t key2 = 0;
+        std::memcpy(&key2, l.data() + 4, 4);
+        const uint32_t h2 = lit_hash(key2);
+        ((uint32_t *)(lit_img.data() + kLitBitmap2))[h2 >> 5] |= 1u << (h2 & 31);
+      }
     }
   }
   size_t o_lit = lit_img.empty() ? 0 : b.add(lit_img.data(), lit_img.size());
@@ -831,6 +837,7 @@ const FwdDfaDev *iter_device(rure *re, const DevTables &t, std::string *err) {
     f.lit_k = lit_k;
     f.lit_minlen = (uint32_t)re->lits.minlen;
     f.lit_maxlen = (uint32_t)re->lits.maxlen;
+    f.lit_k8 = re->lits.minlen >= 8 ? 1 : 0;
   }
   re->iter_dev[d] = {tmp.blob, f};
   return &re->iter_dev[d].second;

@@ -20,7 +20,8 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(autouse=True)
 def literal_engine(monkeypatch):
-    # the literal engine is opt-in (slower than the DFA on the C3 variants)
+    # force the literal engine (by default it runs only where the DFA does not
+    # fit LDS exactly)
     monkeypatch.setenv("RURE_AMD_LIT", "1")
 
 PATTERNS = [r"agggtaaa|tttaccct", r"[cgt]gggtaaa|tttaccc[acg]", r"a|ab", r"ab|a", r"aa", r"e", r"(?i)holm",
@@ -94,3 +95,19 @@ def test_regexdna_variants_literal_engine(cuda):
         re = R.Regex(v["re"])
         c, m = re.find_iter_batch(d, stride=len(big), length=len(big), count=1)
         assert pairs(m) == OracleRegex(re).find_iter(big), v["re"]
+
+
+def test_default_dispatch_large_word_set(cuda, monkeypatch):
+    """A 40-word alternation (DFA > 255 states): the literal engine is the
+    default engine here; same matches as the oracle and as the DFA."""
+    monkeypatch.delenv("RURE_AMD_LIT", raising=False)
+    text = corpus("sherlock")
+    words = sorted(set(w for w in text.decode("latin-1").split() if w.isalpha() and 6 <= len(w) <= 10))[:40]
+    re = R.Regex("|".join(words))
+    assert re.literals() and re.dfa_info(2)["states"] > 255
+    exp = OracleRegex(re).find_iter(text)
+    c, m = re.find_iter_batch(dev(text, cuda), stride=len(text), length=len(text), count=1)
+    assert pairs(m) == exp
+    monkeypatch.setenv("RURE_AMD_LIT", "0")
+    c, m = re.find_iter_batch(dev(text, cuda), stride=len(text), length=len(text), count=1)
+    assert pairs(m) == exp

@@ -74,3 +74,9 @@ def test_regexdna_variants_are_string_sets():
     for v in known_counts()["regexdna"]["variants"]:
         lits = R.Regex(v["re"]).literals()
         assert lits and all(len(x) == 8 for x in lits), v["re"]
+
+
+def test_long_literals_second_filter():
+    """Literals of >= 8 bytes get the bytes-4..7 bitmap (C3 variants)."""
+    lits = R.Regex(r"agggtaa[cgt]|[acg]ttaccct").literals()
+    assert min(len(x) for x in lits) >= 8
