@@ -52,6 +52,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive measurement (C2)")
     return ap.parse_args()
 
 
@@ -234,7 +235,31 @@ def run_c2(ctx):
                     roofline=roofline(achieved, kernel_ms, b_alg, config))
     if ctx.rank == 0 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(re, hay, res, n, L, args)
+    if ctx.rank == 0 and not args.no_pcie:
+        line["pcie_inclusive"] = pcie_inclusive(ctx, hay, scan)
     return line
+
+
+def pcie_inclusive(ctx, hay, scan):
+    """End-to-end rate when the batch starts in (pinned) host memory: one
+    host->HBM copy of the whole batch plus the find launch, on the launch
+    stream (never the headline `value`)."""
+    torch = ctx.torch
+    host = hay.cpu().pin_memory()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    for rep in range(2):  # the second repetition is reported
+        ev[0].record(ctx.stream)
+        with torch.cuda.stream(ctx.stream):
+            hay.copy_(host, non_blocking=True)
+        ev[1].record(ctx.stream)
+        scan()
+        ev[2].record(ctx.stream)
+        torch.cuda.synchronize()
+    h2d = ev[0].elapsed_time(ev[1])
+    tot = ev[0].elapsed_time(ev[2])
+    nbytes = hay.numel()
+    return {"GBps": round(nbytes / (tot * 1e-3) / 1e9, 2), "h2d_ms": round(h2d, 3), "find_ms": round(tot - h2d, 3),
+            "h2d_GBps": round(nbytes / (h2d * 1e-3) / 1e9, 2), "note": "pinned host -> HBM copy + find, per batch"}
 
 
 def cpu_baseline(re, hay, res, n, L, args):
