@@ -253,17 +253,28 @@ __device__ __forceinline__ uint64_t rev_scan_all(const RevDfaDev &r, const uint8
   if (s == r.dead) return NONE;
   uint64_t rs = NONE, a = me;
   while (a > lo) {
-    const uintptr_t p = (uintptr_t)(base + a - 1);
-    const uint4 v = *(const uint4 *)(p & ~(uintptr_t)15);
-    const uint32_t w[4] = {__builtin_bswap32(v.w), __builtin_bswap32(v.z), __builtin_bswap32(v.y),
-                           __builtin_bswap32(v.x)};
-    const uint32_t k0 = 15 - (uint32_t)(p & 15);  // reversed index of the byte at a - 1
-    const uint32_t kend = a - lo < 16 - k0 ? k0 + (uint32_t)(a - lo) : 16;
-    int lastk = -1;
-    s = steps16(s, w, k0, kend, rlds, r.n_normal, r.n_match_end, lastk);
-    if (lastk >= 0) rs = a - (uint32_t)(lastk - k0);  // the reverse match flag: start = byte position + 1
-    a -= kend - k0;
-    if (s >= r.n_match_end) return s == r.dead ? rs : QUITMARK;
+    // up to 8 blocks below `a` loaded at once (their latencies overlap)
+    const uintptr_t top = (uintptr_t)(base + a - 1) & ~(uintptr_t)15;
+    const uintptr_t bot = (uintptr_t)(base + lo);
+    uint4 vb[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (top - 16 * k + 15 >= bot) vb[k] = *(const uint4 *)(top - 16 * k);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (a <= lo) break;
+      const uintptr_t p = (uintptr_t)(base + a - 1);
+      const uint4 v = vb[k];
+      const uint32_t w[4] = {__builtin_bswap32(v.w), __builtin_bswap32(v.z), __builtin_bswap32(v.y),
+                             __builtin_bswap32(v.x)};
+      const uint32_t k0 = 15 - (uint32_t)(p & 15);  // reversed index of the byte at a - 1
+      const uint32_t kend = a - lo < 16 - k0 ? k0 + (uint32_t)(a - lo) : 16;
+      int lastk = -1;
+      s = steps16(s, w, k0, kend, rlds, r.n_normal, r.n_match_end, lastk);
+      if (lastk >= 0) rs = a - (uint32_t)(lastk - k0);  // the reverse match flag: start = byte position + 1
+      a -= kend - k0;
+      if (s >= r.n_match_end) return s == r.dead ? rs : QUITMARK;
+    }
   }
   if (r.eof[s]) rs = lo;
   return rs;
