@@ -173,6 +173,7 @@ struct IterSpan {
   uint64_t hi;
   const uint64_t *entry;
   uint64_t *exit;
+  uint64_t tail;  // the text length when the span runs to the end (hi = ~0), else ~0
 };
 hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaDev &r, const NfaDev *nf,
                             bool chunked, uint64_t chunk, const IterOut &o, hipStream_t st, int cus,

@@ -707,12 +707,18 @@ __global__ void iter_entry_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev 
 }
 
 // The state the iteration leaves at the span end: (next, last_match, fresh).
-__global__ void iter_exit_kernel(const Unit *units, uint64_t nunits, uint64_t *exit) {
+// A span that runs to the end of the text (`tail` = its length) iterated
+// without a cut; "fresh" then means equivalent to a fresh start at the text
+// end, where only an empty match at the end could differ.
+__global__ void iter_exit_kernel(const Unit *units, uint64_t nunits, uint64_t *exit, uint64_t tail,
+                                 uint32_t nonempty) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const Unit U = units[nunits - 1];
+  bool fresh = (U.flags & U_CLEAN) != 0;
+  if (tail != ~0ull && U.exit.p >= tail) fresh = U.exit.p == tail && (U.exit.lm != tail || nonempty);
   exit[0] = U.exit.p;
   exit[1] = U.exit.lm;
-  exit[2] = (U.flags & U_CLEAN) ? 1 : 0;
+  exit[2] = fresh ? 1 : 0;
 }
 
 // Pass 4: write every unit's matches at its offset.  Units whose speculation
@@ -1105,7 +1111,8 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
                          off, o.counts, o.total);
       if ((e = hipGetLastError()) != hipSuccess) break;
       if (spn && spn->exit) {
-        hipLaunchKernelGGL(iter_exit_kernel, dim3(1), dim3(64), 0, st, (const Unit *)units, nunits, spn->exit);
+        hipLaunchKernelGGL(iter_exit_kernel, dim3(1), dim3(64), 0, st, (const Unit *)units, nunits, spn->exit,
+                           spn->tail, f->nonempty);
         e = hipGetLastError();
       }
     } while (false);

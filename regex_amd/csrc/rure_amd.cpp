@@ -1563,7 +1563,8 @@ int rure_amd_find_iter_span(rure *re, const uint8_t *haystack, size_t length, si
   b.start = lo;
   // hi == length: the span runs to the end of the text, so the iteration
   // may also own the empty match at the very end (re_trait.rs:205-214)
-  IterSpan sp{hi == length ? ~0ull : (uint64_t)hi, (const uint64_t *)entry, (uint64_t *)exit};
+  IterSpan sp{hi == length ? ~0ull : (uint64_t)hi, (const uint64_t *)entry, (uint64_t *)exit,
+              hi == length ? (uint64_t)length : ~0ull};
   IterOut o{count, (uint64_t *)matches, capacity, count};
   hipStream_t st = (hipStream_t)stream;
   return run_find_iter(re, t, b, o, st, &err, &sp) == hipSuccess ? RURE_AMD_OK : RURE_AMD_ERR_HIP;

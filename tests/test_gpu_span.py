@@ -79,3 +79,44 @@ def test_spans_regexdna_known_answers(cuda):
         re = R.Regex(v["re"])
         got, _ = find_iter_spans_local(re, dev(seq, cuda), len(seq), 5)
         assert len(pairs(got)) == v["count"], v["re"]
+
+
+def _chain(re, h, n, bounds):
+    """iterate_spans over arbitrary span bounds [b0, b1), [b1, b2), ..."""
+    import torch
+    from regex_amd.dist import iterate_spans
+    k = len(bounds) - 1
+
+    def run(i, entry):
+        ent = None if entry is None else torch.tensor(entry, dtype=torch.int64, device=h.device)
+        return re.find_iter_span(h, bounds[i], bounds[i + 1], length=n, entry=ent)
+
+    res, rounds = iterate_spans(run, k, list(range(k)), lambda mine: [mine[i].tolist() for i in range(k)])
+    return [m for i in range(k) for m in pairs(res[i][1])], rounds
+
+
+@pytest.mark.parametrize("pat", [r"a+", r"a*", r"\ba+\b", r"(?m)^a+$", r"x|a{3}"])
+def test_spans_custom_bounds(cuda, pat):
+    # empty spans, spans inside one long match, a span starting mid-match,
+    # spans of one byte, and the empty-match rule at every cut
+    text = b"x" + b"a" * 300 + b"y\naaa\n" + b"ab" * 40 + b"a" * 5
+    n = len(text)
+    re = R.Regex(pat)
+    exp = OracleRegex(re).find_iter(text)
+    h = dev(text, cuda)
+    for bounds in ([0, 5, 5, 100, 200, 302, n], [0, 1, 2, 3, 301, 302, 303, n], [0, 0, n], [0, n, n],
+                   list(range(0, n, 7)) + [n]):
+        got, _ = _chain(re, h, n, bounds)
+        assert got == exp, (pat, bounds)
+
+
+def test_span_entry_past_the_span(cuda):
+    # a match that covers a whole span: that span owns nothing and passes the
+    # entry on unchanged (not fresh)
+    text = b"x" + b"a" * 300 + b"y"
+    re = R.Regex(r"a+")
+    h = dev(text, cuda)
+    c0, m0, e0 = re.find_iter_span(h, 0, 10, length=len(text))
+    assert pairs(m0) == [(1, 301)]
+    c1, m1, e1 = re.find_iter_span(h, 10, 20, length=len(text), entry=e0)
+    assert pairs(m1) == [] and e1.tolist() == e0.tolist()
