@@ -111,3 +111,49 @@ def test_default_dispatch_large_word_set(cuda, monkeypatch):
     monkeypatch.setenv("RURE_AMD_LIT", "0")
     c, m = re.find_iter_batch(dev(text, cuda), stride=len(text), length=len(text), count=1)
     assert pairs(m) == exp
+
+
+def test_literal_ragged_and_start(cuda):
+    """Ragged batches (one unit per haystack) and a search start > 0 (look-
+    behind context kept, rure.h:186-192) through the literal engine."""
+    import torch
+    text = corpus("sherlock")
+    rng = random.Random(11)
+    hs = []
+    for _ in range(300):
+        a = rng.randint(0, len(text) - 2000)
+        hs.append(text[a:a + rng.randint(0, 2000)])
+    offs = np.zeros(len(hs) + 1, dtype=np.int64)
+    offs[1:] = np.cumsum([len(h) for h in hs])
+    buf = dev(b"".join(hs), cuda)
+    for pat in (r"Holmes|Watson|the", r"aa", r"a|ab"):
+        re = R.Regex(pat)
+        o = OracleRegex(re)
+        c, m = re.find_iter_batch(buf, offsets=torch.from_numpy(offs).to(cuda))
+        got, k = pairs(m), 0
+        for i, h in enumerate(hs):
+            exp = o.find_iter(h)
+            assert int(c[i]) == len(exp) and got[k:k + len(exp)] == exp, (pat, i)
+            k += len(exp)
+    t = text[:200000]
+    for pat in (r"Holmes|Watson|the", r"aa"):
+        re = R.Regex(pat)
+        o = OracleRegex(re)
+        for start in (1, 5, 777):
+            exp = []
+            p, lm = start, None
+            while p <= len(t):  # the iteration of re_trait.rs:197-221 from `start`
+                mm = o.find(t, p)
+                if mm is None:
+                    break
+                s, e = mm
+                if s == e:
+                    p = e + 1
+                    if lm == e:
+                        continue
+                else:
+                    p = e
+                lm = e
+                exp.append((s, e))
+            c, m = re.find_iter_batch(dev(t, cuda), stride=len(t), length=len(t), count=1, start=start)
+            assert pairs(m) == exp, (pat, start)
