@@ -30,3 +30,27 @@ def test_ctest_runs(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     assert "all checks passed" in r.stdout
+
+
+def build_batch(tmp_path):
+    """tests/ctest/batch_ctest.c: the batched device entry points from C, with
+    device buffers from the HIP runtime (C API, hip_runtime_api.h)."""
+    exe = str(tmp_path / "batch_ctest")
+    subprocess.check_call(["gcc", "-std=c11", "-Wall", "-Werror", "-D__HIP_PLATFORM_AMD__", "-o", exe,
+                           os.path.join(ROOT, "tests", "ctest", "batch_ctest.c"),
+                           "-I", os.path.join(ROOT, "include"), "-I", "/opt/rocm/include",
+                           "-L", LIB, "-lrure_amd", "-L", "/opt/rocm/lib", "-lamdhip64",
+                           "-Wl,-rpath," + LIB, "-Wl,-rpath,/opt/rocm/lib", "-Wl,--allow-shlib-undefined"])
+    return exe
+
+
+def test_batch_ctest_builds(tmp_path):
+    assert os.path.exists(build_batch(tmp_path))
+
+
+@pytest.mark.gpu
+def test_batch_ctest_runs(tmp_path):
+    exe = build_batch(tmp_path)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert "all checks passed" in r.stdout
