@@ -861,7 +861,11 @@ bool long_batch(const BatchDev &b, const DevTables &t, uint64_t *chunk) {
   if (b.offs || !t.has_dfa || t.quit_possible || b.count == 0) return false;
   const uint64_t span = b.length > b.start ? b.length - b.start : 0;
   if (span < (256u << 10) || b.count >= (uint64_t)t.cus * 128) return false;
-  const uint64_t target = (uint64_t)t.cus * 1024;  // 16 waves per CU: per-lane streams need latency hiding
+  // 16 waves per CU: per-lane streams need latency hiding (RURE_AMD_LONG_LANES
+  // per CU overrides, tuning)
+  uint64_t per_cu = 1024;
+  if (const char *v = getenv("RURE_AMD_LONG_LANES")) per_cu = std::max(64, atoi(v));
+  const uint64_t target = (uint64_t)t.cus * per_cu;
   const uint64_t per_h = (target + b.count - 1) / b.count;
   uint64_t c = std::max<uint64_t>(16u << 10, (span + per_h - 1) / per_h);
   *chunk = odd_lines(c);
