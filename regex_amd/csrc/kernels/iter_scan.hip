@@ -159,7 +159,7 @@ __device__ __forceinline__ const uint8_t *stage_tables(const FwdDfaDev &f, const
 
 // Pass 1: speculative iteration of every unit.
 __global__ __launch_bounds__(1024) void iter_spec_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
-                                                        Unit *units, uint64_t *slots, uint32_t *counts) {
+                                                        Unit *units, uint64_t *slots, uint32_t *counts, uint32_t *dirty) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const uint8_t *rlds = stage_tables(f, r, lds);
   for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < nunits; u += (uint64_t)gridDim.x * blockDim.x) {
@@ -183,6 +183,7 @@ __global__ __launch_bounds__(1024) void iter_spec_kernel(BatchDev b, Geo g, uint
     U.skip = U.pad = 0;
     units[u] = U;
     counts[u] = n;
+    if (!(U.flags & U_SPEC_CLEAN)) atomicOr(dirty, 1u);  // the fix pass has work
   }
 }
 
@@ -292,7 +293,7 @@ __device__ __forceinline__ uint64_t rev_scan_all(const RevDfaDev &r, const uint8
 // the same iteration.  Same unit records as iter_spec_kernel.
 __global__ __launch_bounds__(1024) void iter_spec_burst_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f,
                                                               RevDfaDev r, Unit *units, uint64_t *slots,
-                                                              uint32_t *counts) {
+                                                              uint32_t *counts, uint32_t *dirty) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const uint8_t *rlds = stage_tables(f, r, lds);
   for (uint64_t u0 = (uint64_t)blockIdx.x * blockDim.x; u0 < nunits; u0 += (uint64_t)gridDim.x * blockDim.x) {
@@ -381,6 +382,7 @@ __global__ __launch_bounds__(1024) void iter_spec_burst_kernel(BatchDev b, Geo g
       U.skip = U.pad = 0;
       units[u] = U;
       counts[u] = n;
+      if (!(U.flags & U_SPEC_CLEAN)) atomicOr(dirty, 1u);  // the fix pass has work
     }
   }
 }
@@ -416,7 +418,7 @@ __device__ __forceinline__ int lit_verify(const FwdDfaDev &f, const uint8_t *lds
 
 template <bool K4, bool K8>
 __global__ __launch_bounds__(1024) void iter_spec_lit_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f,
-                                                            Unit *units, uint64_t *slots, uint32_t *counts) {
+                                                            Unit *units, uint64_t *slots, uint32_t *counts, uint32_t *dirty) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   for (uint32_t i = threadIdx.x * 16; i < f.lit_bytes; i += blockDim.x * 16)
     *(uint4 *)(lds + i) = *(const uint4 *)(f.lit_image + i);
@@ -497,6 +499,7 @@ __global__ __launch_bounds__(1024) void iter_spec_lit_kernel(BatchDev b, Geo g, 
     U.skip = U.pad = 0;
     units[u] = U;
     counts[u] = n;
+    if (!(U.flags & U_SPEC_CLEAN)) atomicOr(dirty, 1u);  // the fix pass has work
   }
 }
 
@@ -627,7 +630,9 @@ __device__ bool repair_unit(const BatchDev &b, const Geo &g, const FwdDfaDev &f,
 // one of its units needs a repair.
 __global__ __launch_bounds__(1024) void iter_fix_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
                                                        Unit *units, uint32_t *counts, const uint64_t *slots,
-                                                       uint64_t *queue, unsigned long long *qlen) {
+                                                       uint64_t *queue, unsigned long long *qlen,
+                                                       const uint32_t *dirty) {
+  if (*dirty == 0) return;  // every speculative exit was clean
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const uint8_t *rlds = nullptr;
   bool staged = false;
@@ -1042,6 +1047,7 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
     uint64_t *off = (uint64_t *)(buf + al(sz_units) + al(sz_slots) + al(sz_counts));
     uint64_t *queue = (uint64_t *)(buf + al(sz_units) + al(sz_slots) + al(sz_counts) + al(sz_off));
     unsigned long long *qlen = (unsigned long long *)(buf + total - 256);
+    uint32_t *dirty = (uint32_t *)(buf + total - 256 + 8);
     // threads per block: the hot tables are staged once per block, so larger
     // blocks let more waves share one LDS copy (occupancy of these latency-
     // bound per-lane scans); RURE_AMD_ITER_BS overrides (tuning)
@@ -1051,7 +1057,7 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
     const int grid = grid_cap(nunits, bs, cus, per_cu);
     do {
       if ((e = hipMemsetAsync(counts + nunits, 0, 4, st)) != hipSuccess) break;
-      if ((e = hipMemsetAsync(qlen, 0, 8, st)) != hipSuccess) break;
+      if ((e = hipMemsetAsync(qlen, 0, 16, st)) != hipSuccess) break;  // qlen, dirty
       const size_t lb = iter_lds_bytes(*f, r);
       if ((e = allow_lds(iter_spec_kernel, lb)) != hipSuccess || (e = allow_lds(iter_spec_burst_kernel, lb)) != hipSuccess || (e = allow_lds(iter_fix_kernel, lb)) != hipSuccess ||
           (e = allow_lds(iter_emit_kernel, lb)) != hipSuccess)
@@ -1067,19 +1073,19 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
         const dim3 lg(grid_cap(nunits, bs, cus, 2048 / bs));
         if (f->lit_k8)
           hipLaunchKernelGGL((iter_spec_lit_kernel<true, true>), lg, dim3(bs), kLitImage, st, b, g, nunits, *f, units,
-                             slots, counts);
+                             slots, counts, dirty);
         else if (f->lit_k == 4)
           hipLaunchKernelGGL((iter_spec_lit_kernel<true, false>), lg, dim3(bs), kLitImage, st, b, g, nunits, *f, units,
-                             slots, counts);
+                             slots, counts, dirty);
         else
           hipLaunchKernelGGL((iter_spec_lit_kernel<false, false>), lg, dim3(bs), kLitImage, st, b, g, nunits, *f,
-                             units, slots, counts);
+                             units, slots, counts, dirty);
       } else if (!getenv("RURE_AMD_ITER_NESTED")) {
         hipLaunchKernelGGL(iter_spec_burst_kernel, dim3(grid), dim3(bs), iter_lds_bytes(*f, r), st, b, g, nunits, *f,
-                           r, units, slots, counts);
+                           r, units, slots, counts, dirty);
       } else {
         hipLaunchKernelGGL(iter_spec_kernel, dim3(grid), dim3(bs), iter_lds_bytes(*f, r), st, b, g, nunits, *f, r,
-                           units, slots, counts);
+                           units, slots, counts, dirty);
       }
       if ((e = hipGetLastError()) != hipSuccess) break;
       if (spn && spn->entry) {
@@ -1093,7 +1099,7 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
       }
       if (g.nk > 1) {
         hipLaunchKernelGGL(iter_fix_kernel, dim3(grid), dim3(bs), iter_lds_bytes(*f, r), st, b, g, nunits, *f, r, units,
-                           counts, (const uint64_t *)slots, queue, qlen);
+                           counts, (const uint64_t *)slots, queue, qlen, (const uint32_t *)dirty);
         if ((e = hipGetLastError()) != hipSuccess) break;
         FwdDfaDev fw = *f;
         fw.hot = 0;
