@@ -414,6 +414,9 @@ def run_c3(ctx):
     strip_ms = ctx.kernel_ms(strip_pass)
     var_ms = ctx.kernel_ms(variant_pass)
     scanned = N + len(variants) * M
+    extra = {}
+    if ctx.rank == 0 and not ctx.args.no_cpu:
+        extra["cpu_baseline"] = cpu_baseline_c3(variants, seq, M, got, ctx.args)
     my_bytes = sum(span_bounds(L, W, rk)[1] - span_bounds(L, W, rk)[0] for _, _, L, _ in passes)
     config = {"workload": "C3: regex-dna x%d (%d B raw, %d B stripped): strip find_iter + 9 variant find_iter"
                           % (copies, N, M),
@@ -426,7 +429,50 @@ def run_c3(ctx):
                     variant_passes_ms=round(var_ms, 3),
                     variant_GBps=round((my_bytes - (N + W - 1) // W) / var_ms / 1e6, 1),
                     strip_matches=nsp_sharded, variant_counts=got, known_answers_ok=ok,
-                    cut_recomputations=stats["recomputed"])
+                    cut_recomputations=stats["recomputed"], roofline=roofline_c3(my_bytes - (N + W - 1) // W,
+                                                                                 var_ms, len(variants)),
+                    **extra)
+
+
+def roofline_c3(var_bytes, var_ms, nvar):
+    """Pass-level roofline of one variant find_iter pass (the spec burst
+    kernel plus its fix/emit/count kernels, HIP events on the launch stream):
+    algorithmic bytes = the stripped span one pass reads.  traffic stays null:
+    the committed PMC pass (profiles/r01_c3_summary.json) averages the strip
+    and variant launches of the burst kernel together."""
+    per = var_bytes / nvar
+    ms = var_ms / nvar
+    a = per / ms / 1e6
+    return {"bound": "hbm", "achieved": round(a, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(a / HBM_PEAK_GBS, 4), "traffic": None, "kernel_ms": round(ms, 4),
+            "alg_bytes_per_launch": int(per), "kernel": "variant find_iter pass (iter_spec_burst_kernel + fix/emit)"}
+
+
+def cpu_baseline_c3(variants, seq, M, gpu_counts, args):
+    """Oracle find_iter (restated lazy DFA + re_trait.rs:197-221 iteration),
+    single-threaded like the reference's find_iter, over the first 16 MiB of
+    the stripped stream for each of the 9 variants; counts re-checked against
+    the GPU's find_iter of the same slice."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_py import OracleRegex
+    import regex_amd as R
+    S = min(M, 16 << 20)
+    piece = bytes(seq[:S].cpu().numpy())
+    os_ = [OracleRegex(v) for v in variants]
+    t0 = time.perf_counter()
+    exp = [len(o.find_iter(piece)) for o in os_]
+    passes, elapsed = 1, time.perf_counter() - t0
+    while elapsed < args.cpu_seconds and passes < 64:
+        t0 = time.perf_counter()
+        for o in os_:
+            o.find_iter(piece)
+        elapsed += time.perf_counter() - t0
+        passes += 1
+    got = [int(v.find_iter_batch(seq[:S + 16], stride=S, length=S, count=1)[0][0]) for v in variants]
+    return {"value": round(S * len(variants) * passes / elapsed / 1e9, 3), "unit": "GB/s", "cores": 1,
+            "kind": "port", "sample": "%d passes of the 9 variant find_iter over the first %d MiB of the stripped "
+                                      "stream" % (passes, S >> 20),
+            "parity_on_sample": exp == got}
 
 
 # ------------------------------------------------------------------ C4
@@ -448,10 +494,38 @@ def run_c4(ctx):
     nb = int(offs[-1].item())
     config = {"workload": "C4: RegexSet of %d patterns over %d log lines (%d B) per GPU" % (len(C4_PATTERNS), n, nb),
               "parallelism": "dp%d" % ctx.world}
+    extra = {}
+    if ctx.rank == 0 and not ctx.args.no_cpu:
+        extra["cpu_baseline"] = cpu_baseline_c4(rs, buf, offs, out, ctx.args)
     return ctx.line("haystack GB/s scanned, batched RegexSet::matches", nb * ctx.world / sec / 1e9, "GB/s",
                     sec * 1e3, "u8", "synthetic log lines (seeded token stream)", config,
                     lines_per_s=round(n * ctx.world / sec, 1),
-                    roofline=roofline(nb / kms / 1e6, kms, nb, config))
+                    roofline=roofline(nb / kms / 1e6, kms, nb, config), **extra)
+
+
+def cpu_baseline_c4(rs, buf, offs, out, args):
+    """Oracle set matcher (restated DfaMany lazy DFA, dfa.rs:525-570) on the
+    first lines of the same batch; re-checks the GPU masks of the sample."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_py import OracleRegex
+    threads = cpu_threads(args.cpu_threads)
+    o = OracleRegex(rs)
+    S = 500_000
+    so = offs[: S + 1].cpu().numpy().astype(np.uint64)
+    hb = buf[: int(so[-1])].cpu().numpy()
+    t0 = time.perf_counter()
+    exp = o.set_batch(hb, 0, 0, S, nthreads=threads, offsets=so)
+    passes, elapsed = 1, time.perf_counter() - t0
+    while elapsed < args.cpu_seconds and passes < 64:
+        t0 = time.perf_counter()
+        o.set_batch(hb, 0, 0, S, nthreads=threads, offsets=so)
+        elapsed += time.perf_counter() - t0
+        passes += 1
+    got = out[:S].cpu().numpy().view(np.uint64)
+    return {"value": round(int(so[-1]) * passes / elapsed / 1e9, 3), "unit": "GB/s", "cores": threads,
+            "kind": "port", "lines_per_s": round(S * passes / elapsed, 1),
+            "sample": "%d passes over the first %d lines (%.0f MiB) of the same batch" % (passes, S, so[-1] / 2**20),
+            "parity_on_sample": bool(np.array_equal(exp, got))}
 
 
 # ------------------------------------------------------------------ C5
@@ -494,10 +568,44 @@ def run_c5(ctx):
     kms = ctx.kernel_ms(scan)
     config = {"workload": "C5: find \\w+@\\w+\\.\\w+ over one 16 GiB haystack per GPU", "haystack_bytes": L,
               "parallelism": "dp%d" % ctx.world}
+    extra = {}
+    if ctx.rank == 0 and not ctx.args.no_cpu:
+        extra["cpu_baseline"] = cpu_baseline_c5(re, hay, pos, plant, ctx)
     return ctx.line("haystack GB/s scanned, bytes::Regex::find over 16 GiB shards", L * ctx.world / sec / 1e9,
                     "GB/s", sec * 1e3, "u8", "synthetic (seeded printable ASCII without '@', one planted address)",
                     config, match=got, expected=[pos + 1, pos + len(plant) - 1],
-                    roofline=roofline(L / kms / 1e6, kms, L, config))
+                    roofline=roofline(L / kms / 1e6, kms, L, config), **extra)
+
+
+def cpu_baseline_c5(re, hay, pos, plant, ctx):
+    """One `find` over one haystack is one sequential lazy-DFA scan in the
+    reference (exec.rs:473-514), so the oracle runs single-threaded on the
+    shard's last 256 MiB (which holds the planted address); the GPU's answer
+    on the same slice is re-checked."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_py import OracleRegex
+    torch = ctx.torch
+    S = 256 << 20
+    L = hay.numel() - 16
+    lo = L - S
+    piece = hay[lo:L].cpu().numpy()
+    o = OracleRegex(re)
+    t0 = time.perf_counter()
+    exp, _ = o.find_batch(piece, S, S, 1, nthreads=1)
+    passes, elapsed = 1, time.perf_counter() - t0
+    while elapsed < ctx.args.cpu_seconds and passes < 16:
+        t0 = time.perf_counter()
+        o.find_batch(piece, S, S, 1, nthreads=1)
+        elapsed += time.perf_counter() - t0
+        passes += 1
+    sub = torch.empty((1, 2), dtype=torch.int64, device=ctx.dev)
+    re.find_batch(hay[lo:], stride=S, length=S, count=1, out=sub, stream=ctx.stream)
+    torch.cuda.synchronize()
+    return {"value": round(S * passes / elapsed / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": "%d passes of find over the shard's last %d MiB (one sequential scan, as the reference's "
+                      "single-haystack find)" % (passes, S >> 20),
+            "parity_on_sample": [int(x) for x in exp[0]] == [int(x) for x in sub[0].cpu()] ==
+                                [pos - lo + 1, pos - lo + len(plant) - 1]}
 
 
 def main():
