@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
+#include <cstdlib>
 
 __global__ __launch_bounds__(256) void lane_per_hay(const uint8_t *hay, uint64_t n, uint64_t L, uint32_t *out) {
   uint32_t acc = 0;
@@ -62,8 +63,9 @@ __global__ __launch_bounds__(256) void tile_lds(const uint8_t *hay, uint64_t n, 
   if (acc == 0x12345678) out[0] = acc;
 }
 
-int main() {
-  const uint64_t n = 1 << 20, L = 4096, bytes = n * L;
+int main(int argc, char **argv) {
+  const uint64_t L = argc > 1 ? strtoull(argv[1], nullptr, 10) : 4096, n = (4ull << 30) / L, bytes = n * L;
+  printf("L=%llu n=%llu\n", (unsigned long long)L, (unsigned long long)n);
   uint8_t *hay; uint32_t *out;
   hipMalloc(&hay, bytes); hipMalloc(&out, 4);
   hipMemset(hay, 1, bytes);
