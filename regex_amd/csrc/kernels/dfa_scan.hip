@@ -326,34 +326,46 @@ __device__ __forceinline__ bool core_careful(uint32_t &c, uint64_t &mask, const 
   return (mask & f.all) == f.all;
 }
 
+// One lookup of the hot core table: entry (core t, class k) at byte
+// 2 * (t * K + k) past the class map — one 24-bit multiply-add (full rate)
+// and a u16 LDS read on the dependent chain.
+__device__ __forceinline__ uint32_t core_entry(const uint16_t *T, uint32_t t, uint32_t K2, uint32_t k2) {
+  return *(const uint16_t *)((const uint8_t *)T + __umul24(t, K2) + k2);
+}
+
+// Code 63 (a report that is not one pattern < 62) takes its mask from the
+// global table; the loads of a chunk go to separate registers and are ORed
+// after the chunk, so no byte waits on a global load.
+#define RURE_CORE_CHUNK(ACTIVE)                                                         \
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};                                           \
+  uint32_t k[16];                                                                       \
+  _Pragma("unroll") for (int j = 0; j < 16; ++j) k[j] = cls[(w[j >> 2] >> ((j & 3) * 8)) & 0xFF]; \
+  if (c < f.hot) {                                                                      \
+    const uint32_t K2 = 2 * f.K;                                                        \
+    uint32_t t = c;                                                                     \
+    uint64_t bag = 0, g63[16];                                                          \
+    _Pragma("unroll") for (int j = 0; j < 16; ++j) {                                    \
+      const uint32_t e = core_entry(T, t, K2, 2 * k[j]);                                \
+      const bool act = ACTIVE;                                                          \
+      const uint32_t code = act ? (e & 63) : 0;                                         \
+      bag |= 1ull << code;                                                              \
+      g63[j] = 0;                                                                       \
+      if (code == 63) g63[j] = f.gout[(size_t)t * f.K + k[j]];                          \
+      t = act ? e >> 6 : t;                                                             \
+    }                                                                                   \
+    _Pragma("unroll") for (int j = 0; j < 16; ++j) pend |= g63[j];                      \
+    if (t != f.hot) {                                                                   \
+      mask |= (bag >> 1) & 0x3FFFFFFFFFFFFFFFull;                                       \
+      c = t;                                                                            \
+      if (c == f.dead) return true;                                                     \
+      if (c == f.quit) { quit = true; return true; }                                    \
+      return (mask & f.all) == f.all;                                                   \
+    }                                                                                   \
+  }
+
 __device__ __forceinline__ bool core_chunk16(uint32_t &c, uint64_t &mask, uint64_t &pend, const SetCoreDev &f,
                                              const uint8_t *cls, const uint16_t *T, uint4 v, bool &quit) {
-  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-  uint32_t k[16];
-#pragma unroll
-  for (int j = 0; j < 16; ++j) k[j] = cls[(w[j >> 2] >> ((j & 3) * 8)) & 0xFF];
-  if (c < f.hot) {
-    uint32_t t = c;
-    uint64_t bag = 0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const uint32_t e = T[t * f.K + k[j]];
-      const uint32_t code = e & 63;
-      bag |= 1ull << code;
-      // code 63: the report is not a single pattern < 62; its mask comes from
-      // the global table, loaded now and merged at the end of the haystack
-      // (the load retires before the next data load is waited for)
-      if (code == 63) pend |= f.gout[(size_t)t * f.K + k[j]];
-      t = e >> 6;
-    }
-    if (t != f.hot) {
-      mask |= (bag >> 1) & 0x3FFFFFFFFFFFFFFFull;
-      c = t;
-      if (c == f.dead) return true;
-      if (c == f.quit) { quit = true; return true; }
-      return (mask & f.all) == f.all;
-    }
-  }
+  RURE_CORE_CHUNK(true)
 #pragma unroll 1
   for (int j = 0; j < 16; ++j)
     if (core_careful(c, mask, f, k[j], quit)) return true;
@@ -367,35 +379,13 @@ __device__ __forceinline__ bool core_chunk16(uint32_t &c, uint64_t &mask, uint64
 __device__ __forceinline__ bool core_chunk_masked(uint32_t &c, uint64_t &mask, uint64_t &pend, const SetCoreDev &f,
                                                   const uint8_t *cls, const uint16_t *T, uint4 v, uint32_t k0,
                                                   uint32_t kend, bool &quit) {
-  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-  uint32_t k[16];
-#pragma unroll
-  for (int j = 0; j < 16; ++j) k[j] = cls[(w[j >> 2] >> ((j & 3) * 8)) & 0xFF];
-  if (c < f.hot) {
-    uint32_t t = c;
-    uint64_t bag = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < 16; ++j) {
-      const uint32_t e = T[t * f.K + k[j]];
-      const bool act = j >= k0 && j < kend;
-      const uint32_t code = act ? (e & 63) : 0;
-      bag |= 1ull << code;
-      if (code == 63) pend |= f.gout[(size_t)t * f.K + k[j]];
-      t = act ? e >> 6 : t;
-    }
-    if (t != f.hot) {
-      mask |= (bag >> 1) & 0x3FFFFFFFFFFFFFFFull;
-      c = t;
-      if (c == f.dead) return true;
-      if (c == f.quit) { quit = true; return true; }
-      return (mask & f.all) == f.all;
-    }
-  }
+  RURE_CORE_CHUNK((uint32_t)j >= k0 && (uint32_t)j < kend)
 #pragma unroll 1
   for (uint32_t j = k0; j < kend; ++j)
     if (core_careful(c, mask, f, k[j], quit)) return true;
   return false;
 }
+#undef RURE_CORE_CHUNK
 
 template <bool STRIDED>
 __global__ __launch_bounds__(1024) void set_core_kernel(BatchDev bt, SetCoreDev f, uint64_t *out) {
