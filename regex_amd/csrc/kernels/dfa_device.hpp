@@ -72,11 +72,11 @@ template <int MODE>
 __device__ __forceinline__ void step1(LaneState &L, const FwdDfaDev &f, const uint8_t *lds,
                                       uint32_t b, uint64_t pos) {
   if (f.all) {  // exact LDS table for every state
-    enter_state<MODE>(L, f, lds[L.s * kRow + b], pos);
+    enter_state<MODE>(L, f, lds[__umul24(L.s, kRow) + b], pos);
     return;
   }
   if (L.s < f.hot) {
-    uint32_t t = lds[L.s * kRow + b];
+    uint32_t t = lds[__umul24(L.s, kRow) + b];
     if (t != f.hot) { L.s = t; return; }
   }
   careful_step<MODE>(L, f, b, pos);
@@ -86,23 +86,23 @@ __device__ __forceinline__ void step1(LaneState &L, const FwdDfaDev &f, const ui
 // off the dependency chain; the chain is one v_mad_u32_u24 + one ds_read_u8.
 __device__ __forceinline__ uint32_t fast4(uint32_t s, uint32_t w, const uint8_t *lds) {
   const uint32_t b0 = w & 0xFF, b1 = (w >> 8) & 0xFF, b2 = (w >> 16) & 0xFF, b3 = w >> 24;
-  s = lds[s * kRow + b0];
-  s = lds[s * kRow + b1];
-  s = lds[s * kRow + b2];
-  s = lds[s * kRow + b3];
+  s = lds[__umul24(s, kRow) + b0];
+  s = lds[__umul24(s, kRow) + b1];
+  s = lds[__umul24(s, kRow) + b2];
+  s = lds[__umul24(s, kRow) + b3];
   return s;
 }
 
 // 4 exact steps (every state in LDS); mx collects the largest state entered
 // (off the dependency chain): mx < n_normal means no match / dead / quit.
 __device__ __forceinline__ uint32_t exact4(uint32_t s, uint32_t w, const uint8_t *lds, uint32_t &mx) {
-  s = lds[s * kRow + (w & 0xFF)];
+  s = lds[__umul24(s, kRow) + (w & 0xFF)];
   mx = max(mx, s);
-  s = lds[s * kRow + ((w >> 8) & 0xFF)];
+  s = lds[__umul24(s, kRow) + ((w >> 8) & 0xFF)];
   mx = max(mx, s);
-  s = lds[s * kRow + ((w >> 16) & 0xFF)];
+  s = lds[__umul24(s, kRow) + ((w >> 16) & 0xFF)];
   mx = max(mx, s);
-  s = lds[s * kRow + (w >> 24)];
+  s = lds[__umul24(s, kRow) + (w >> 24)];
   mx = max(mx, s);
   return s;
 }
@@ -194,10 +194,10 @@ __device__ __forceinline__ uint64_t rev_scan(const RevDfaDev &r, const uint8_t *
       const uint32_t b = (w[j >> 2] >> ((j & 3) * 8)) & 0xFF;
       --a;
       if (all) {
-        s = rlds[s * kRow + b];
+        s = rlds[__umul24(s, kRow) + b];
       } else {
         if (s < hot) {
-          const uint32_t t = rlds[s * kRow + b];
+          const uint32_t t = rlds[__umul24(s, kRow) + b];
           if (t != hot) { s = t; continue; }
         }
         s = r.full[(size_t)s * 256 + b];

@@ -251,7 +251,7 @@ __device__ __forceinline__ bool set_careful(uint32_t &s, uint64_t &mask, const S
 __device__ __forceinline__ bool set_step1(uint32_t &s, uint64_t &mask, const SetDfaDev &f, const uint8_t *lds,
                                           uint32_t b, bool &quit) {
   if (s < f.hot) {
-    uint32_t t = lds[s * kRow + b];
+    uint32_t t = lds[__umul24(s, kRow) + b];
     if (t != f.hot) { s = t; return false; }
   }
   return set_careful(s, mask, f, b, quit);

@@ -198,7 +198,7 @@ __device__ __forceinline__ uint32_t steps16(uint32_t s, const uint32_t w[4], uin
                                             const uint8_t *tab, uint32_t nn, uint32_t nme, int &lastk) {
 #pragma unroll
   for (uint32_t k = 0; k < 16; ++k) {
-    const uint32_t t = tab[s * kRow + ((w[k >> 2] >> ((k & 3) * 8)) & 0xFF)];
+    const uint32_t t = tab[__umul24(s, kRow) + ((w[k >> 2] >> ((k & 3) * 8)) & 0xFF)];
     const bool act = k >= k0 && k < kend;
     s = act ? t : s;
     lastk = (act && t - nn < nme - nn) ? (int)k : lastk;
