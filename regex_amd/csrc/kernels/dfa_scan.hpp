@@ -52,6 +52,14 @@ struct FwdDfaDev {
   const uint8_t *lit_image;
   uint32_t lit_bytes, lit_n, lit_k, lit_minlen, lit_maxlen;
   uint32_t lit_k8;            // every literal has >= 8 bytes: a second bitmap filters on bytes 4..7
+  // find_iter DFA only: the string set as a bit-parallel Shift-And automaton
+  // (sa_len = 0: none).  Every string has sa_len bytes; the set is a union of
+  // class sequences (strings that differ in one position merged), sequence x
+  // owning bits [x * sa_len, (x + 1) * sa_len).  sa_image: 256 u64 masks,
+  // bit i of mask[b] = byte b is in the class of bit position i.
+  const uint64_t *sa_image;
+  uint64_t sa_init, sa_final;   // first / last bit of every sequence
+  uint32_t sa_len, sa_bits;
 };
 
 // Literal engine image layout (at most kLitMax literals of kLitLen bytes).

@@ -503,6 +503,287 @@ __global__ __launch_bounds__(1024) void iter_spec_lit_kernel(BatchDev b, Geo g, 
   }
 }
 
+// Pass 1 with the Shift-And engine, for string sets whose strings all have
+// the same length L (host: sa_* fields; the regex-dna variants).  The set is
+// a bit-parallel NFA (class sequences, one bit per position): per byte
+// D = ((D << 1) | init) & mask[b] — the mask read does not depend on D, so a
+// lane's dependent chain is two VALU operations per byte instead of an LDS
+// round trip.  A sequence's last bit set after byte q is a string ending at
+// q, i.e. the match [q - L + 1, q + 1); equal lengths make the leftmost-first
+// match at a start unique and the iteration greedy on ends (re_trait.rs:
+// 197-221).  A unit scans from c0 with D = 0 (starts < c0 are not its own)
+// to c1 + L - 1, so it sees every string starting before its cut; blocks whose
+// OR of final bits is zero (almost all) take no per-byte branch.  Same unit
+// records as iter_spec_lit_kernel.
+template <typename W>
+__global__ __launch_bounds__(256) void iter_spec_sa_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f,
+                                                           Unit *units, uint64_t *slots, uint32_t *counts,
+                                                           uint32_t *dirty) {
+  __shared__ W B[256];
+  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) B[i] = (W)f.sa_image[i];
+  __syncthreads();
+  const W I = (W)f.sa_init, F = (W)f.sa_final;
+  const uint64_t L = f.sa_len;
+  for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < nunits; u += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t h, len, c0, c1;
+    const uint8_t *base;
+    unit_bounds(b, g, u, &h, &base, &len, &c0, &c1);
+    uint64_t p = c0, lm = NONE;
+    uint32_t n = 0;
+    const uint64_t qend = c1 >= len ? len : min(len, c1 + L - 1);  // last bytes q < qend
+    W D = 0;
+    if (qend > c0) {
+      // 128-byte windows of 8 aligned blocks; the next window's loads are in
+      // flight while this one is stepped
+      const uintptr_t ae = (uintptr_t)(base + qend);
+      uintptr_t a = (uintptr_t)(base + c0) & ~(uintptr_t)15;
+      uint4 cur[8], nxt[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (a + 16 * k < ae) cur[k] = *(const uint4 *)(a + 16 * k);
+      while (a < ae) {
+        const uintptr_t an = a + 128;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (an + 16 * k < ae) nxt[k] = *(const uint4 *)(an + 16 * k);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uintptr_t ab = a + 16 * k;
+          if (ab >= ae) break;
+          const uint4 v = cur[k];
+          const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+          const int64_t bp = (int64_t)(ab - (uintptr_t)base);
+          const uint32_t k0 = bp < (int64_t)c0 ? (uint32_t)((int64_t)c0 - bp) : 0;
+          const uint32_t kend = (int64_t)qend - bp < 16 ? (uint32_t)((int64_t)qend - bp) : 16;
+          const W D0 = D;
+          W acc = 0;
+          if (k0 == 0 && kend == 16) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+              D = ((D << 1) | I) & B[(w[j >> 2] >> (8 * (j & 3))) & 0xFF];
+              acc |= D & F;
+            }
+          } else {
+#pragma unroll
+            for (uint32_t j = 0; j < 16; ++j) {
+              const W Dn = ((D << 1) | I) & B[(w[j >> 2] >> (8 * (j & 3))) & 0xFF];
+              const bool act = j >= k0 && j < kend;
+              D = act ? Dn : D;
+              acc |= act ? (Dn & F) : (W)0;
+            }
+          }
+          if (acc) {  // rare: the block holds string ends; walk it byte by byte
+            W E = D0;
+#pragma unroll 1
+            for (uint32_t j = k0; j < kend; ++j) {
+              E = ((E << 1) | I) & B[(w[j >> 2] >> (8 * (j & 3))) & 0xFF];
+              if (E & F) {
+                const uint64_t e = (uint64_t)bp + j + 1, st = e - L;
+                if (st >= p && st < c1) {
+                  if (n < g.slots) *(ulonglong2 *)&slots[(u * g.slots + n) * 2] = make_ulonglong2(st, e);
+                  ++n;
+                  p = lm = e;
+                }
+              }
+            }
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) cur[k] = nxt[k];
+        a = an;
+      }
+    }
+    Unit U;
+    U.entry = {c0, NONE};
+    U.exit = {p, lm};
+    U.spec_exit = U.exit;
+    U.spec_count = n;
+    const bool clean = p < c1 || (p == c1 && (lm != c1 || f.nonempty));
+    U.flags = clean ? (U_SPEC_CLEAN | U_CLEAN) : 0;
+    U.skip = U.pad = 0;
+    units[u] = U;
+    counts[u] = n;
+    if (!(U.flags & U_SPEC_CLEAN)) atomicOr(dirty, 1u);  // the fix pass has work
+  }
+}
+
+// iter_spec_sa_kernel with coalesced loads, for fixed-stride batches whose
+// units are whole 128-byte lines at 16-byte aligned starts: one wave owns 64
+// consecutive units and each load covers 8 units x one 128-byte line,
+// transposed through a per-wave XOR-swizzled LDS stage (dfa_scan.hip's tile
+// layout), so the scan reads HBM at the tile kernel's rate instead of the
+// lane-per-unit rate.  The L - 1 bytes past a unit's cut (strings starting
+// before it) come from the next unit's first 16 bytes, held by the next lane,
+// or from memory for the wave's last lane.  The last unit of each haystack
+// (ragged) runs the per-lane loop of iter_spec_sa_kernel.
+template <typename W>
+__device__ __forceinline__ void sa_block(W &D, const W *B, W I, W F, const uint32_t w[4], uint32_t k0, uint32_t kend,
+                                         int64_t bp, uint64_t L, uint64_t c1, uint64_t &p, uint64_t &lm,
+                                         uint32_t &n, uint64_t *myslots, uint32_t nslots) {
+  const W D0 = D;
+  W acc = 0;
+  if (k0 == 0 && kend == 16) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      D = ((D << 1) | I) & B[(w[j >> 2] >> (8 * (j & 3))) & 0xFF];
+      acc |= D & F;
+    }
+  } else {
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) {
+      const W Dn = ((D << 1) | I) & B[(w[j >> 2] >> (8 * (j & 3))) & 0xFF];
+      const bool act = j >= k0 && j < kend;
+      D = act ? Dn : D;
+      acc |= act ? (Dn & F) : (W)0;
+    }
+  }
+  if (acc) {  // rare: the block holds string ends; walk it byte by byte
+    W E = D0;
+#pragma unroll 1
+    for (uint32_t j = k0; j < kend; ++j) {
+      E = ((E << 1) | I) & B[(w[j >> 2] >> (8 * (j & 3))) & 0xFF];
+      if (E & F) {
+        const uint64_t e = (uint64_t)bp + j + 1, st = e - L;
+        if (st >= p && st < c1) {
+          if (n < nslots) *(ulonglong2 *)&myslots[2 * n] = make_ulonglong2(st, e);
+          ++n;
+          p = lm = e;
+        }
+      }
+    }
+  }
+}
+
+template <typename W>
+__device__ __forceinline__ void sa_unit_record(const FwdDfaDev &f, uint64_t u, uint64_t c0, uint64_t c1, uint64_t p,
+                                               uint64_t lm, uint32_t n, Unit *units, uint32_t *counts,
+                                               uint32_t *dirty) {
+  Unit U;
+  U.entry = {c0, NONE};
+  U.exit = {p, lm};
+  U.spec_exit = U.exit;
+  U.spec_count = n;
+  const bool clean = p < c1 || (p == c1 && (lm != c1 || f.nonempty));
+  U.flags = clean ? (U_SPEC_CLEAN | U_CLEAN) : 0;
+  U.skip = U.pad = 0;
+  units[u] = U;
+  counts[u] = n;
+  if (!clean) atomicOr(dirty, 1u);  // the fix pass has work
+}
+
+template <typename W>
+__global__ __launch_bounds__(256) void iter_spec_sa_tile_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f,
+                                                                Unit *units, uint64_t *slots, uint32_t *counts,
+                                                                uint32_t *dirty) {
+  __shared__ W B[256];
+  __shared__ __attribute__((aligned(16))) uint4 stage[4][64 * 8];
+  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) B[i] = (W)f.sa_image[i];
+  __syncthreads();
+  const W I = (W)f.sa_init, F = (W)f.sa_final;
+  const uint64_t L = f.sa_len, C = g.chunk, nk = g.nk;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint4 *buf = stage[w];
+  const int src_h = lane >> 3, src_seg = lane & 7, sw = (lane >> 1) & 7;
+  const uint64_t ngroups = (nunits + 63) / 64, nwaves = (uint64_t)gridDim.x * 4;
+  const bool single = b.count == 1;
+  auto hk = [&](uint64_t uu, uint64_t &h, uint64_t &k) {
+    if (single) { h = 0; k = uu; } else { h = uu / nk; k = uu - h * nk; }
+  };
+  for (uint64_t gi = (uint64_t)blockIdx.x * 4 + w; gi < ngroups; gi += nwaves) {
+    const uint64_t u = gi * 64 + lane;
+    uint64_t h, k;
+    hk(u, h, k);
+    const bool valid = u < nunits;
+    const bool full = valid && k + 1 < nk;
+    const uint8_t *src[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      uint64_t us = gi * 64 + 8 * j + src_h, hs, ks;
+      hk(us, hs, ks);
+      if (us >= nunits || ks + 1 >= nk) hs = ks = 0;  // absent / ragged units re-read unit 0 (full)
+      src[j] = b.hay + hs * b.stride + b.start + ks * C + 16 * src_seg;
+    }
+    const uint8_t *base = b.hay + h * b.stride;
+    const uint64_t len = b.length, c0 = b.start + k * C;
+    const uint64_t c1 = k + 1 == nk ? g.end : c0 + C;
+    uint64_t *myslots = slots + u * g.slots * 2;
+    uint64_t p = c0, lm = NONE;
+    uint32_t n = 0;
+    W D = 0;
+    uint4 first = make_uint4(0, 0, 0, 0);
+    uint4 n0, n1, n2, n3, n4, n5, n6, n7;
+#define RURE_LOAD_TILE(a)                                                                                     \
+  n0 = *(const uint4 *)(src[0] + (a)); n1 = *(const uint4 *)(src[1] + (a));                                  \
+  n2 = *(const uint4 *)(src[2] + (a)); n3 = *(const uint4 *)(src[3] + (a));                                  \
+  n4 = *(const uint4 *)(src[4] + (a)); n5 = *(const uint4 *)(src[5] + (a));                                  \
+  n6 = *(const uint4 *)(src[6] + (a)); n7 = *(const uint4 *)(src[7] + (a));
+#define RURE_STAGE(kk, v) buf[(8 * (kk) + src_h) * 8 + (src_seg ^ (((8 * (kk) + src_h) >> 1) & 7))] = (v);
+    RURE_LOAD_TILE(0)
+    for (uint64_t at = 0; at < C; at += 128) {
+      RURE_STAGE(0, n0) RURE_STAGE(1, n1) RURE_STAGE(2, n2) RURE_STAGE(3, n3)
+      RURE_STAGE(4, n4) RURE_STAGE(5, n5) RURE_STAGE(6, n6) RURE_STAGE(7, n7)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const uint64_t an = at + 128 < C ? at + 128 : at;
+      RURE_LOAD_TILE(an)
+      if (full) {
+        uint4 cur = buf[lane * 8 + sw];
+        if (at == 0) first = cur;
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+          const uint4 nx = buf[lane * 8 + ((m + 1 < 8 ? m + 1 : 7) ^ sw)];
+          const uint32_t wd[4] = {cur.x, cur.y, cur.z, cur.w};
+          sa_block<W>(D, B, I, F, wd, 0, 16, (int64_t)(c0 + at + 16 * m), L, c1, p, lm, n, myslots, g.slots);
+          cur = nx;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+#undef RURE_LOAD_TILE
+#undef RURE_STAGE
+    // the next unit's first 16 bytes from the next lane (its unit follows
+    // this one in memory when this one is full)
+    uint4 nxt;
+    nxt.x = __shfl_down(first.x, 1);
+    nxt.y = __shfl_down(first.y, 1);
+    nxt.z = __shfl_down(first.z, 1);
+    nxt.w = __shfl_down(first.w, 1);
+    if (!valid) continue;
+    if (full) {
+      // strings starting before the cut end in [c1, c1 + L - 1)
+      const uint64_t qend = min(len, c1 + L - 1);
+      uint64_t q = c1;
+      if (q < qend && lane < 63 && k + 2 < nk) {  // the next unit is full: lane + 1 holds its first block
+        const uint32_t wd[4] = {nxt.x, nxt.y, nxt.z, nxt.w};
+        const uint32_t kend = qend - q < 16 ? (uint32_t)(qend - q) : 16;
+        sa_block<W>(D, B, I, F, wd, 0, kend, (int64_t)q, L, c1, p, lm, n, myslots, g.slots);
+        q += 16;
+      }
+      for (; q < qend; q += 16) {  // from memory (aligned: c1 is)
+        const uint4 v = *(const uint4 *)(base + q);
+        const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+        const uint32_t kend = qend - q < 16 ? (uint32_t)(qend - q) : 16;
+        sa_block<W>(D, B, I, F, wd, 0, kend, (int64_t)q, L, c1, p, lm, n, myslots, g.slots);
+      }
+    } else {
+      // ragged last unit of its haystack: the per-lane loop
+      const uint64_t qend = c1 >= len ? len : min(len, c1 + L - 1);
+      for (uintptr_t a = (uintptr_t)(base + c0) & ~(uintptr_t)15; c0 < qend && a < (uintptr_t)(base + qend); a += 16) {
+        const uint4 v = *(const uint4 *)a;
+        const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+        const int64_t bp = (int64_t)(a - (uintptr_t)base);
+        const uint32_t k0 = bp < (int64_t)c0 ? (uint32_t)((int64_t)c0 - bp) : 0;
+        const uint32_t kend = (int64_t)qend - bp < 16 ? (uint32_t)((int64_t)qend - bp) : 16;
+        sa_block<W>(D, B, I, F, wd, k0, kend, bp, L, c1, p, lm, n, myslots, g.slots);
+      }
+    }
+    sa_unit_record<W>(f, u, c0, c1, p, lm, n, units, counts, dirty);
+  }
+}
+
 // Where the true iteration of unit j, entered with E, joins the speculative
 // one S (started fresh at c0), read off S's recorded matches: S's state
 // before it yielded match i is (p_i, lm_i) (p_0 = c0, lm_0 = none; then the
@@ -1069,7 +1350,28 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
       // DFA stays.  RURE_AMD_LIT=1 / 0 forces it on / off.
       const char *lit_env = getenv("RURE_AMD_LIT");
       const bool use_lit = f->lit_n && (lit_env ? lit_env[0] == '1' : !f->all);
-      if (use_lit) {
+      // Shift-And engine for equal-length string sets; RURE_AMD_SA=0 disables
+      const char *sa_env = getenv("RURE_AMD_SA");
+      const bool use_sa = f->sa_len && !(sa_env && sa_env[0] == '0') && !(lit_env && lit_env[0] == '1');
+      const bool sa_tile = !b.offs && g.nk >= 2 && (g.chunk % 128) == 0 && (b.count == 1 || (b.stride % 16) == 0) &&
+                           (((uintptr_t)(b.hay + b.start)) & 15) == 0 && !(sa_env && sa_env[0] == '2');
+      if (use_sa && sa_tile) {
+        const dim3 sg(grid_cap((nunits + 63) / 64, 4, cus, 4));
+        if (f->sa_bits <= 32)
+          hipLaunchKernelGGL((iter_spec_sa_tile_kernel<uint32_t>), sg, dim3(256), 0, st, b, g, nunits, *f, units,
+                             slots, counts, dirty);
+        else
+          hipLaunchKernelGGL((iter_spec_sa_tile_kernel<uint64_t>), sg, dim3(256), 0, st, b, g, nunits, *f, units,
+                             slots, counts, dirty);
+      } else if (use_sa) {
+        const dim3 sg(grid_cap(nunits, 256, cus, 8));
+        if (f->sa_bits <= 32)
+          hipLaunchKernelGGL((iter_spec_sa_kernel<uint32_t>), sg, dim3(256), 0, st, b, g, nunits, *f, units, slots,
+                             counts, dirty);
+        else
+          hipLaunchKernelGGL((iter_spec_sa_kernel<uint64_t>), sg, dim3(256), 0, st, b, g, nunits, *f, units, slots,
+                             counts, dirty);
+      } else if (use_lit) {
         const dim3 lg(grid_cap(nunits, bs, cus, 2048 / bs));
         if (f->lit_k8)
           hipLaunchKernelGGL((iter_spec_lit_kernel<true, true>), lg, dim3(bs), kLitImage, st, b, g, nunits, *f, units,

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -809,6 +810,49 @@ const FwdDfaDev *iter_device(rure *re, const DevTables &t, std::string *err) {
     }
   }
   size_t o_lit = lit_img.empty() ? 0 : b.add(lit_img.data(), lit_img.size());
+  // Shift-And image: equal-length strings merged into class sequences
+  // (two sequences equal but in one position become one, with the union of
+  // that position's classes: the same language), <= 64 bits in all
+  std::vector<uint64_t> sa_img;
+  uint64_t sa_init = 0, sa_final = 0;
+  uint32_t sa_len = 0, sa_bits = 0;
+  if (re->lit_ok && re->lits.minlen == re->lits.maxlen && re->lits.minlen >= 1) {
+    const size_t L = re->lits.minlen;
+    using Cls = std::array<uint64_t, 4>;
+    std::vector<std::vector<Cls>> seqs;
+    for (const std::string &l : re->lits.lits) {
+      std::vector<Cls> q(L, Cls{0, 0, 0, 0});
+      for (size_t i = 0; i < L; ++i) q[i][(uint8_t)l[i] >> 6] |= 1ull << ((uint8_t)l[i] & 63);
+      seqs.push_back(q);
+    }
+    for (bool merged = true; merged;) {
+      merged = false;
+      for (size_t x = 0; x < seqs.size() && !merged; ++x)
+        for (size_t y = x + 1; y < seqs.size() && !merged; ++y) {
+          int diff = -1, nd = 0;
+          for (size_t i = 0; i < L && nd < 2; ++i)
+            if (seqs[x][i] != seqs[y][i]) { diff = (int)i; ++nd; }
+          if (nd == 1) {
+            for (int w = 0; w < 4; ++w) seqs[x][diff][w] |= seqs[y][diff][w];
+            seqs.erase(seqs.begin() + y);
+            merged = true;
+          }
+        }
+    }
+    if (seqs.size() * L <= 64) {
+      sa_len = (uint32_t)L;
+      sa_bits = (uint32_t)(seqs.size() * L);
+      sa_img.assign(256, 0);
+      for (size_t x = 0; x < seqs.size(); ++x) {
+        sa_init |= 1ull << (x * L);
+        sa_final |= 1ull << (x * L + L - 1);
+        for (size_t i = 0; i < L; ++i)
+          for (int c = 0; c < 256; ++c)
+            if ((seqs[x][i][c >> 6] >> (c & 63)) & 1) sa_img[c] |= 1ull << (x * L + i);
+      }
+    }
+  }
+  size_t o_sa = sa_img.empty() ? 0 : b.add(sa_img.data(), sa_img.size() * 8);
   DevTables tmp;
   if (!upload_blob(b, &tmp, err)) return nullptr;
   uint8_t *base = (uint8_t *)tmp.blob;
@@ -838,6 +882,13 @@ const FwdDfaDev *iter_device(rure *re, const DevTables &t, std::string *err) {
     f.lit_minlen = (uint32_t)re->lits.minlen;
     f.lit_maxlen = (uint32_t)re->lits.maxlen;
     f.lit_k8 = re->lits.minlen >= 8 ? 1 : 0;
+  }
+  if (!sa_img.empty()) {
+    f.sa_image = (const uint64_t *)(base + o_sa);
+    f.sa_init = sa_init;
+    f.sa_final = sa_final;
+    f.sa_len = sa_len;
+    f.sa_bits = sa_bits;
   }
   re->iter_dev[d] = {tmp.blob, f};
   return &re->iter_dev[d].second;
