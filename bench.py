@@ -430,22 +430,28 @@ def run_c3(ctx):
                     variant_GBps=round((my_bytes - (N + W - 1) // W) / var_ms / 1e6, 1),
                     strip_matches=nsp_sharded, variant_counts=got, known_answers_ok=ok,
                     cut_recomputations=stats["recomputed"], roofline=roofline_c3(my_bytes - (N + W - 1) // W,
-                                                                                 var_ms, len(variants)),
+                                                                                 var_ms, len(variants), config),
                     **extra)
 
 
-def roofline_c3(var_bytes, var_ms, nvar):
-    """Pass-level roofline of one variant find_iter pass (the spec burst
-    kernel plus its fix/emit/count kernels, HIP events on the launch stream):
-    algorithmic bytes = the stripped span one pass reads.  traffic stays null:
-    the committed PMC pass (profiles/r01_c3_summary.json) averages the strip
-    and variant launches of the burst kernel together."""
+def roofline_c3(var_bytes, var_ms, nvar, config):
+    """Pass-level roofline of one variant find_iter pass (the Shift-And
+    spec kernel plus its fix/emit/count kernels, HIP events on the launch
+    stream): algorithmic bytes = the stripped span one pass reads.  traffic =
+    HBM bytes per launch of the spec kernel (only the variant passes run it)
+    from the committed PMC pass of this command."""
     per = var_bytes / nvar
     ms = var_ms / nvar
     a = per / ms / 1e6
-    return {"bound": "hbm", "achieved": round(a, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(a / HBM_PEAK_GBS, 4), "traffic": None, "kernel_ms": round(ms, 4),
-            "alg_bytes_per_launch": int(per), "kernel": "variant find_iter pass (iter_spec_burst_kernel + fix/emit)"}
+    r = {"bound": "hbm", "achieved": round(a, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": round(a / HBM_PEAK_GBS, 4), "traffic": None, "kernel_ms": round(ms, 4),
+         "alg_bytes_per_launch": int(per),
+         "kernel": "variant find_iter pass (iter_spec_sa_tile_kernel + fix/emit/count kernels)"}
+    tr = profiled_traffic(config, per)
+    if tr is not None:
+        r["traffic"] = tr["bytes"]
+        r["traffic_source"] = tr["source"]
+    return r
 
 
 def cpu_baseline_c3(variants, seq, M, gpu_counts, args):
