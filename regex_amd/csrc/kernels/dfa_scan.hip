@@ -334,8 +334,8 @@ __device__ __forceinline__ uint32_t core_entry(const uint16_t *T, uint32_t t, ui
 }
 
 // Code 63 (a report that is not one pattern < 62) takes its mask from the
-// global table; the loads of a chunk go to separate registers and are ORed
-// after the chunk, so no byte waits on a global load.
+// global table: the chain only sets bit 63 of the bag, and a chunk that has it
+// walks its bytes again for those loads (no byte waits on a global load).
 #define RURE_CORE_CHUNK(ACTIVE)                                                         \
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};                                           \
   uint32_t k[16];                                                                       \
@@ -343,17 +343,23 @@ __device__ __forceinline__ uint32_t core_entry(const uint16_t *T, uint32_t t, ui
   if (c < f.hot) {                                                                      \
     const uint32_t K2 = 2 * f.K;                                                        \
     uint32_t t = c;                                                                     \
-    uint64_t bag = 0, g63[16];                                                          \
+    uint64_t bag = 0;                                                                   \
     _Pragma("unroll") for (int j = 0; j < 16; ++j) {                                    \
       const uint32_t e = core_entry(T, t, K2, 2 * k[j]);                                \
       const bool act = ACTIVE;                                                          \
       const uint32_t code = act ? (e & 63) : 0;                                         \
       bag |= 1ull << code;                                                              \
-      g63[j] = 0;                                                                       \
-      if (code == 63) g63[j] = f.gout[(size_t)t * f.K + k[j]];                          \
       t = act ? e >> 6 : t;                                                             \
     }                                                                                   \
-    _Pragma("unroll") for (int j = 0; j < 16; ++j) pend |= g63[j];                      \
+    if ((bag >> 63) && t != f.hot) {                                                    \
+      uint32_t x = c;                                                                   \
+      for (int j = 0; j < 16; ++j) {                                                    \
+        const uint32_t e = core_entry(T, x, K2, 2 * k[j]);                              \
+        const bool act = ACTIVE;                                                        \
+        if (act && (e & 63) == 63) pend |= f.gout[(size_t)x * f.K + k[j]];             \
+        x = act ? e >> 6 : x;                                                           \
+      }                                                                                 \
+    }                                                                                   \
     if (t != f.hot) {                                                                   \
       mask |= (bag >> 1) & 0x3FFFFFFFFFFFFFFFull;                                       \
       c = t;                                                                            \
