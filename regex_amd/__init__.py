@@ -674,7 +674,9 @@ class RegexSet(object):
         _check(N.rure_amd_set_core_export(self._set, ctypes.byref(info), lds.ctypes.data, gcore.ctypes.data,
                                           gout.ctypes.data, eof.ctypes.data, start.ctypes.data), "set_core_export")
         K, hot = info.K, info.hot
-        hot_tab = lds[256:256 + (hot + 1) * K * 2].view(np.uint16).reshape(hot + 1, K)
+        # rows of K + 1 entries: column K is the identity (the class of the
+        # bytes outside a masked head / tail chunk)
+        hot_tab = lds[256:256 + (hot + 1) * (K + 1) * 2].view(np.uint16).reshape(hot + 1, K + 1)
         return d, lds[:256].copy(), hot_tab, gcore.reshape(-1, K), gout.reshape(-1, K), eof, start
 
     def dfa_tables(self):

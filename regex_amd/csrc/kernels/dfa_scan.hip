@@ -341,23 +341,25 @@ __device__ __forceinline__ uint32_t core_entry(const uint16_t *T, uint32_t t, ui
   uint32_t k[16];                                                                       \
   _Pragma("unroll") for (int j = 0; j < 16; ++j) k[j] = cls[(w[j >> 2] >> ((j & 3) * 8)) & 0xFF]; \
   if (c < f.hot) {                                                                      \
-    const uint32_t K2 = 2 * f.K;                                                        \
+    const uint32_t K2 = 2 * (f.K + 1); /* LDS rows: K classes + the identity column */ \
     uint32_t t = c;                                                                     \
     uint64_t bag = 0;                                                                   \
+    uint32_t kc[16];                                                                    \
     _Pragma("unroll") for (int j = 0; j < 16; ++j) {                                    \
-      const uint32_t e = core_entry(T, t, K2, 2 * k[j]);                                \
       const bool act = ACTIVE;                                                          \
-      const uint32_t code = act ? (e & 63) : 0;                                         \
-      bag |= 1ull << code;                                                              \
-      t = act ? e >> 6 : t;                                                             \
+      kc[j] = act ? 2 * k[j] : 2 * f.K;                                                 \
+    }                                                                                   \
+    _Pragma("unroll") for (int j = 0; j < 16; ++j) {                                    \
+      const uint32_t e = core_entry(T, t, K2, kc[j]);                                   \
+      bag |= 1ull << (e & 63);                                                          \
+      t = e >> 6;                                                                       \
     }                                                                                   \
     if ((bag >> 63) && t != f.hot) {                                                    \
       uint32_t x = c;                                                                   \
       for (int j = 0; j < 16; ++j) {                                                    \
-        const uint32_t e = core_entry(T, x, K2, 2 * k[j]);                              \
-        const bool act = ACTIVE;                                                        \
-        if (act && (e & 63) == 63) pend |= f.gout[(size_t)x * f.K + k[j]];             \
-        x = act ? e >> 6 : x;                                                           \
+        const uint32_t e = core_entry(T, x, K2, kc[j]);                                 \
+        if ((e & 63) == 63) pend |= f.gout[(size_t)x * f.K + k[j]];                     \
+        x = e >> 6;                                                                     \
       }                                                                                 \
     }                                                                                   \
     if (t != f.hot) {                                                                   \

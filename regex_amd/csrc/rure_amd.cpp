@@ -300,14 +300,17 @@ bool build_set_cores(const DenseDfa &d, size_t lds_budget, CoreSet *cs,
   }
   const uint32_t K = (uint32_t)col_rep.size();
   if (lds_budget < 256 + 4 * K) return false;
-  uint32_t hot = (uint32_t)std::min<size_t>({(size_t)nc, 1023, (lds_budget - 256) / (2 * K) - 1});
+  // LDS rows have K + 1 entries: column K is the identity (same core, no
+  // output), the class of the bytes outside a masked head / tail chunk
+  const uint32_t KL = K + 1;
+  uint32_t hot = (uint32_t)std::min<size_t>({(size_t)nc, 1023, (lds_budget - 256) / (2 * KL) - 1});
   cs->K = K;
   cs->ncores = nc;
   cs->hot = hot;
   cs->gcore.assign((size_t)nc * K, 0);
   cs->gout.assign((size_t)nc * K, 0);
   cs->eof.assign(nc, 0);
-  cs->lds.assign(256 + (size_t)(hot + 1) * K * 2, 0);
+  cs->lds.assign(256 + (size_t)(hot + 1) * KL * 2, 0);
   memcpy(cs->lds.data(), cls, 256);
   uint16_t *T = (uint16_t *)(cs->lds.data() + 256);
   for (uint32_t r = 0; r < nc; ++r) {
@@ -323,11 +326,12 @@ bool build_set_cores(const DenseDfa &d, size_t lds_budget, CoreSet *cs,
         uint32_t code = 0;
         if (out) code = (__builtin_popcountll(out) == 1 && __builtin_ctzll(out) < 62) ? __builtin_ctzll(out) + 1 : 63;
         const uint32_t tgt = ncore < hot ? ncore : hot;
-        T[(size_t)r * K + k] = (uint16_t)((tgt << 6) | (ncore < hot ? code : 0));
+        T[(size_t)r * KL + k] = (uint16_t)((tgt << 6) | (ncore < hot ? code : 0));
       }
     }
+    if (r < hot) T[(size_t)r * KL + K] = (uint16_t)(r << 6);  // identity column
   }
-  for (uint32_t k = 0; k < K; ++k) T[(size_t)hot * K + k] = (uint16_t)(hot << 6);  // sentinel row
+  for (uint32_t k = 0; k < KL; ++k) T[(size_t)hot * KL + k] = (uint16_t)(hot << 6);  // sentinel row
   for (int i = 0; i < 128; ++i) cs->start[i] = (uint16_t)rank[core_of[d.start[i]]];
   cs->dead = (uint32_t)rank[core_of[d.dead]];
   cs->quit = d.quit >= 0 ? (uint32_t)rank[core_of[d.quit]] : 0xFFFFFFFFu;

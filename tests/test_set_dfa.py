@@ -61,6 +61,8 @@ def test_core_form_c4_lines():
     from regex_amd.workloads import C4_PATTERNS, log_lines_host
     rs = R.RegexSet(C4_PATTERNS)
     ct = rs.core_tables()
+    T, hot = ct[2], ct[0]["hot"]
+    assert all(int(T[r, -1]) == r << 6 for r in range(hot))  # identity column
     assert ct is not None and ct[0]["hot"] > 500
     buf, offs = log_lines_host(400, seed=77)
     o = OracleRegex(rs)
