@@ -282,6 +282,11 @@ int rure_amd_nfa_saves_export(rure *re, uint32_t *save_off, uint16_t *save_slot,
  * bytes[32 * i ...] receive the first `cap` of them (NULL arrays: count only).
  * Host only. */
 int64_t rure_amd_literals_export(rure *re, uint32_t *lens, uint8_t *bytes, size_t cap);
+/* Diagnostics (host only): the Shift-And image of the find_iter string set
+ * (iter_spec_sa_kernel) — 256 u64 byte masks, the first / last bit of every
+ * class sequence and the string length.  Returns the state width in bits, 0
+ * when the regex is not a set of equal-length strings that fits 64 bits. */
+int64_t rure_amd_shiftand_export(rure *re, uint64_t *mask, uint64_t *init, uint64_t *fin, uint32_t *len);
 /* 1 if batched searches of this regex run the DFA kernels, 0 if only the
  * Pike VM kernel (automaton too large), negative on error. */
 int rure_amd_uses_dfa(rure *re);

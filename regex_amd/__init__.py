@@ -523,6 +523,19 @@ class Regex(object):
         """True if batched searches run the DFA kernels (else the Pike VM kernel)."""
         return N.rure_amd_uses_dfa(self._re) == 1
 
+    def shiftand(self):
+        """The Shift-And image the find_iter string-set engine runs
+        (iter_spec_sa_kernel), or None: (bits, masks (256 u64), init, final,
+        string length)."""
+        import numpy as np
+        mask = np.zeros(256, dtype=np.uint64)
+        init, fin, ln = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_uint32(0)
+        bits = N.rure_amd_shiftand_export(self._re, mask.ctypes.data, ctypes.byref(init), ctypes.byref(fin),
+                                          ctypes.byref(ln))
+        if bits <= 0:
+            return None
+        return int(bits), [int(x) for x in mask], init.value, fin.value, ln.value
+
     def literals(self):
         """The regex as a finite string set in leftmost-first priority order, as
         the literal find_iter engine uses it, or None if it is not one."""

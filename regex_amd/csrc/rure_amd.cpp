@@ -771,6 +771,54 @@ bool build_iter_dfa(rure *re) {
 
 // Forward DFA with stripped states for the chunked find_iter (built and
 // uploaded on first use).  Returns null if it does not materialise.
+// The Shift-And image of a string set whose strings all have one length L
+// (iter_spec_sa_kernel): strings equal but in one position are merged into
+// class sequences (the union of that position's classes; the same language),
+// until no pair merges; sequence x owns bits [x L, (x + 1) L) of the state.
+// mask[b] bit i = byte b is in the class of bit position i.  Returns false
+// (and leaves the outputs empty) unless the sequences fit 64 bits.
+static bool build_shiftand(const LiteralSet &ls, std::vector<uint64_t> *mask, uint64_t *init, uint64_t *fin,
+                           uint32_t *len, uint32_t *bits) {
+  mask->clear();
+  *init = *fin = 0;
+  *len = *bits = 0;
+  if (ls.lits.empty() || ls.minlen != ls.maxlen || ls.minlen < 1) return false;
+  const size_t L = ls.minlen;
+  using Cls = std::array<uint64_t, 4>;
+  std::vector<std::vector<Cls>> seqs;
+  for (const std::string &l : ls.lits) {
+    std::vector<Cls> q(L, Cls{0, 0, 0, 0});
+    for (size_t i = 0; i < L; ++i) q[i][(uint8_t)l[i] >> 6] |= 1ull << ((uint8_t)l[i] & 63);
+    seqs.push_back(q);
+  }
+  for (bool merged = true; merged;) {
+    merged = false;
+    for (size_t x = 0; x < seqs.size() && !merged; ++x)
+      for (size_t y = x + 1; y < seqs.size() && !merged; ++y) {
+        int diff = -1, nd = 0;
+        for (size_t i = 0; i < L && nd < 2; ++i)
+          if (seqs[x][i] != seqs[y][i]) { diff = (int)i; ++nd; }
+        if (nd == 1) {
+          for (int w = 0; w < 4; ++w) seqs[x][diff][w] |= seqs[y][diff][w];
+          seqs.erase(seqs.begin() + y);
+          merged = true;
+        }
+      }
+  }
+  if (seqs.size() * L > 64) return false;
+  *len = (uint32_t)L;
+  *bits = (uint32_t)(seqs.size() * L);
+  mask->assign(256, 0);
+  for (size_t x = 0; x < seqs.size(); ++x) {
+    *init |= 1ull << (x * L);
+    *fin |= 1ull << (x * L + L - 1);
+    for (size_t i = 0; i < L; ++i)
+      for (int c = 0; c < 256; ++c)
+        if ((seqs[x][i][c >> 6] >> (c & 63)) & 1) (*mask)[c] |= 1ull << (x * L + i);
+  }
+  return true;
+}
+
 const FwdDfaDev *iter_device(rure *re, const DevTables &t, std::string *err) {
   if (!build_iter_dfa(re)) return nullptr;
   int d = 0;
@@ -814,48 +862,11 @@ const FwdDfaDev *iter_device(rure *re, const DevTables &t, std::string *err) {
     }
   }
   size_t o_lit = lit_img.empty() ? 0 : b.add(lit_img.data(), lit_img.size());
-  // Shift-And image: equal-length strings merged into class sequences
-  // (two sequences equal but in one position become one, with the union of
-  // that position's classes: the same language), <= 64 bits in all
+  // Shift-And image (build_shiftand)
   std::vector<uint64_t> sa_img;
   uint64_t sa_init = 0, sa_final = 0;
   uint32_t sa_len = 0, sa_bits = 0;
-  if (re->lit_ok && re->lits.minlen == re->lits.maxlen && re->lits.minlen >= 1) {
-    const size_t L = re->lits.minlen;
-    using Cls = std::array<uint64_t, 4>;
-    std::vector<std::vector<Cls>> seqs;
-    for (const std::string &l : re->lits.lits) {
-      std::vector<Cls> q(L, Cls{0, 0, 0, 0});
-      for (size_t i = 0; i < L; ++i) q[i][(uint8_t)l[i] >> 6] |= 1ull << ((uint8_t)l[i] & 63);
-      seqs.push_back(q);
-    }
-    for (bool merged = true; merged;) {
-      merged = false;
-      for (size_t x = 0; x < seqs.size() && !merged; ++x)
-        for (size_t y = x + 1; y < seqs.size() && !merged; ++y) {
-          int diff = -1, nd = 0;
-          for (size_t i = 0; i < L && nd < 2; ++i)
-            if (seqs[x][i] != seqs[y][i]) { diff = (int)i; ++nd; }
-          if (nd == 1) {
-            for (int w = 0; w < 4; ++w) seqs[x][diff][w] |= seqs[y][diff][w];
-            seqs.erase(seqs.begin() + y);
-            merged = true;
-          }
-        }
-    }
-    if (seqs.size() * L <= 64) {
-      sa_len = (uint32_t)L;
-      sa_bits = (uint32_t)(seqs.size() * L);
-      sa_img.assign(256, 0);
-      for (size_t x = 0; x < seqs.size(); ++x) {
-        sa_init |= 1ull << (x * L);
-        sa_final |= 1ull << (x * L + L - 1);
-        for (size_t i = 0; i < L; ++i)
-          for (int c = 0; c < 256; ++c)
-            if ((seqs[x][i][c >> 6] >> (c & 63)) & 1) sa_img[c] |= 1ull << (x * L + i);
-      }
-    }
-  }
+  if (re->lit_ok) build_shiftand(re->lits, &sa_img, &sa_init, &sa_final, &sa_len, &sa_bits);
   size_t o_sa = sa_img.empty() ? 0 : b.add(sa_img.data(), sa_img.size() * 8);
   DevTables tmp;
   if (!upload_blob(b, &tmp, err)) return nullptr;
@@ -1602,6 +1613,21 @@ int64_t rure_amd_literals_export(rure *re, uint32_t *lens, uint8_t *bytes, size_
     if (bytes) std::memcpy(bytes + kLitLen * x, L[x].data(), L[x].size());
   }
   return (int64_t)L.size();
+}
+
+int64_t rure_amd_shiftand_export(rure *re, uint64_t *mask, uint64_t *init, uint64_t *fin, uint32_t *len) {
+  if (!re) return RURE_AMD_ERR_ARG;
+  build_iter_dfa(re);
+  std::lock_guard<std::mutex> g(re->mu);
+  std::vector<uint64_t> m;
+  uint64_t i0 = 0, f0 = 0;
+  uint32_t l0 = 0, b0 = 0;
+  if (!re->lit_ok || !build_shiftand(re->lits, &m, &i0, &f0, &l0, &b0)) return 0;
+  if (mask) std::memcpy(mask, m.data(), 256 * 8);
+  if (init) *init = i0;
+  if (fin) *fin = f0;
+  if (len) *len = l0;
+  return (int64_t)b0;
 }
 
 int rure_amd_find_iter_span(rure *re, const uint8_t *haystack, size_t length, size_t lo, size_t hi,
