@@ -541,7 +541,10 @@ hipError_t launch_dfa_fwd(int mode, const BatchDev &b, const FwdDfaDev &f, const
   const bool strided = b.offs == nullptr;
   if (tile_path_ok(b, f)) {
     int waves = (int)((b.count + 63) / 64);
-    int tgrid = std::min(grid, (waves + 3) / 4);
+    // one haystack group per wave (C2: 0.810 ms vs 0.818 with two groups per
+    // wave, 0.84 with a persistent 4-blocks-per-CU grid)
+    (void)grid;
+    int tgrid = (int)std::min<uint64_t>((uint64_t)(waves + 3) / 4, (uint64_t)f.cus * 64);
     if (tgrid < 1) tgrid = 1;
     switch (mode) {
       case MODE_FIND: return launch_tile<MODE_FIND>(b, f, r, out, st, tgrid);
