@@ -1022,6 +1022,7 @@ __global__ __launch_bounds__(1024) void iter_emit_kernel(BatchDev b, Geo g, uint
   for (uint64_t u0 = (uint64_t)blockIdx.x * blockDim.x; u0 < nunits; u0 += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t u = u0 + threadIdx.x;
     uint64_t o0 = 0, cnt = 0;
+    uint32_t skip = 0;
     bool rerun = false, copy = false;
     if (u < nunits) {
       o0 = off[u];
@@ -1030,6 +1031,7 @@ __global__ __launch_bounds__(1024) void iter_emit_kernel(BatchDev b, Geo g, uint
         const uint32_t fl = units[u].flags;
         rerun = ((fl & U_FIXED) && !(fl & U_COPY)) || cnt > g.slots;
         copy = !rerun;
+        skip = (fl & U_COPY) ? units[u].skip : 0;  // loaded by every lane at once, not per copied unit
       }
     }
     uint64_t m = __ballot(copy);
@@ -1038,11 +1040,20 @@ __global__ __launch_bounds__(1024) void iter_emit_kernel(BatchDev b, Geo g, uint
       m &= m - 1;
       const uint64_t uu = __shfl(u, l), oo = __shfl(o0, l);
       const uint64_t cc = min(__shfl(cnt, l), cap - oo);
-      const uint32_t sk = (units[uu].flags & U_COPY) ? units[uu].skip : 0;
+      const uint32_t sk = __shfl(skip, l);
       // `out` (rure_match records) is only guaranteed 8-byte aligned
       const uint64_t *src = slots + (uu * g.slots + sk) * 2;
       uint64_t *dst = out + 2 * oo;
-      for (uint64_t i = lane; i < 2 * cc; i += 64) dst[i] = src[i];
+      // four loads in flight per lane before the stores
+      uint64_t i = lane;
+      for (; i + 192 < 2 * cc; i += 256) {
+        const uint64_t a0 = src[i], a1 = src[i + 64], a2 = src[i + 128], a3 = src[i + 192];
+        dst[i] = a0;
+        dst[i + 64] = a1;
+        dst[i + 128] = a2;
+        dst[i + 192] = a3;
+      }
+      for (; i < 2 * cc; i += 64) dst[i] = src[i];
     }
     if (!__syncthreads_or(rerun)) continue;
     if (!staged) {
