@@ -1,7 +1,12 @@
 #!/usr/bin/env python3
 """Headline benchmark: batched `bytes::Regex::find` (BASELINE.json configs[1], C2).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c3|c4|c5]
+
+With --gpus N > 1 and no torch.distributed environment (WORLD_SIZE unset),
+this process starts N rank processes itself (RANK / LOCAL_RANK / WORLD_SIZE /
+MASTER_ADDR=127.0.0.1 / MASTER_PORT set, one per GPU), before anything touches
+the GPU, and prints rank 0's line; under torchrun it is one of the ranks.
 
 Default (the driver's line) = C2: a step is one pass of the hot path over one
 batch — the date regex `\\d{4}-\\d{2}-\\d{2}` `find` over 1,048,576 synthetic
@@ -10,6 +15,9 @@ scaling: each rank owns its own shard), followed, for N > 1, by the only
 exchange the path has: an all-gather (RCCL) of the compacted match records.
 
 Other configs (for DESIGN.md's table; same timing protocol):
+  c1  the date regex `is_match` over 1K x 1 KiB ASCII buffers (BASELINE
+      configs[0], the reference's CPU-runnable case): the batched GPU call
+      and the oracle on the host, whole-batch parity
   c3  regex-dna: `>[^\\n]*\\n|\\n` find_iter over the input replicated to
       2 GiB, then the 9 variant patterns' find_iter over the stripped 2 GiB;
       for N > 1 each logical stream is cut into N contiguous spans (strong
@@ -45,7 +53,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"])
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "rehearsal"])
     ap.add_argument("--haystacks", type=int, default=1 << 20)
     ap.add_argument("--length", type=int, default=4096)
     ap.add_argument("--match-frac", type=float, default=0.01)
@@ -53,17 +61,49 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive measurement (C2)")
+    ap.add_argument("--no-parity", action="store_true", help="skip the whole-batch oracle check (C2)")
     return ap.parse_args()
 
 
-def cpu_threads(req):
-    if req > 0:
-        return req
+def host_cpus():
+    """(CPUs this process may run on, the cgroup CPU quota in CPUs or None)."""
     try:
         n = len(os.sched_getaffinity(0))
     except AttributeError:
         n = os.cpu_count() or 1
-    return max(1, min(16, n))
+    quota = None
+    for path, split in (("/sys/fs/cgroup/cpu.max", lambda t: t.split()),
+                        ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", lambda t: [t.strip(), open(
+                            "/sys/fs/cgroup/cpu/cpu.cfs_period_us").read().strip()])):
+        try:
+            q, per = split(open(path).read())
+            if q not in ("max", "-1"):
+                quota = int(q) / int(per)
+            break
+        except (OSError, ValueError):
+            continue
+    return n, quota
+
+
+def cpu_threads(req):
+    """Threads for the CPU baseline: every CPU the process may use, bounded
+    by the cgroup quota and by OMP_NUM_THREADS (the GPU box grants 16 CPUs
+    per GPU and says so there) — the host's full count is reported beside."""
+    if req > 0:
+        return req
+    n, quota = host_cpus()
+    if quota:
+        n = min(n, max(1, int(quota)))
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def cpu_info(threads):
+    n, quota = host_cpus()
+    return {"cores": threads, "host_cpus": os.cpu_count(), "affinity_cpus": n,
+            "cgroup_cpu_quota": quota, "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
 class Ctx(object):
@@ -74,10 +114,17 @@ class Ctx(object):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         local = int(os.environ.get("LOCAL_RANK", "0"))
+        if self.world != args.gpus:
+            raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, self.world))
         # REGEX_AMD_BENCH_BACKEND=gloo rehearses the N > 1 paths with several
         # ranks sharing one GPU (RCCL refuses duplicate devices); the driver's
         # multi-GPU runs use the default, nccl (= RCCL over xGMI)
         backend = os.environ.get("REGEX_AMD_BENCH_BACKEND", "nccl")
+        if args.config == "rehearsal":   # CPU-only protocol check (tests/test_bench_launch.py)
+            self.dev, self.stream = torch.device("cpu"), None
+            if self.world > 1:
+                dist.init_process_group("gloo")
+            return
         if backend != "nccl":
             local %= max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
@@ -112,20 +159,24 @@ class Ctx(object):
             torch.cuda.synchronize()
         self.ramp_s = round(time.perf_counter() - t0, 3)
 
+    def sync(self):
+        if self.dev.type == "cuda":
+            self.torch.cuda.synchronize()
+
     def timed(self, step):
         """Warmup, then EXACTLY --steps steps between barrier + synchronize;
         max over ranks (seconds per step)."""
-        torch, dist = self.torch, self.dist
+        dist = self.dist
         for _ in range(self.args.warmup):
             step()
-        torch.cuda.synchronize()
+        self.sync()
         if self.world > 1:
             dist.barrier()
-        torch.cuda.synchronize()
+        self.sync()
         t0 = time.perf_counter()
         for _ in range(self.args.steps):
             step()
-        torch.cuda.synchronize()
+        self.sync()
         if self.world > 1:
             dist.barrier()
         dt = time.perf_counter() - t0
@@ -194,7 +245,7 @@ def profiled_traffic(config, b_alg):
 # ------------------------------------------------------------------ C2
 def run_c2(ctx):
     import regex_amd as R
-    from regex_amd.dist import compact_matches, gather_records
+    from regex_amd.dist import RecordGather
     from regex_amd.workloads import date_haystacks_device
     torch, args = ctx.torch, ctx.args
     n, L = args.haystacks, args.length
@@ -205,10 +256,20 @@ def run_c2(ctx):
     def scan():
         re.find_batch(hay, stride=L, length=L, count=n, out=out, stream=ctx.stream)
 
+    gather = None
+    if ctx.world > 1:
+        # fixed-capacity record exchange sized from an untimed first scan
+        scan()
+        torch.cuda.synchronize()
+        hits = int((out[:, 0] >= 0).sum().item())
+        cap = torch.tensor([hits], dtype=torch.int64, device=ctx.dev)
+        ctx.dist.all_reduce(cap, op=ctx.dist.ReduceOp.MAX)
+        gather = RecordGather(int(cap.item()) + 1024, ctx.dev)
+
     def step():
         scan()
-        if ctx.world > 1:
-            gather_records(compact_matches(out, ctx.rank * n))
+        if gather is not None:
+            gather.step(out, ctx.rank * n, ctx.stream)
 
     ctx.ramp(scan)
     sec = ctx.timed(step)
@@ -218,6 +279,16 @@ def run_c2(ctx):
 
     res = out.cpu().numpy()
     matched = int((res[:, 0] >= 0).sum())
+    extra = {}
+    if gather is not None:
+        recs, counts = gather.result()
+        mine = recs[sum(counts[:ctx.rank]):sum(counts[:ctx.rank + 1])].cpu().numpy()
+        hit = np.nonzero(res[:, 0] >= 0)[0]
+        extra["gathered_records"] = int(recs.shape[0])
+        extra["gather_ok"] = bool(counts[ctx.rank] == matched and np.array_equal(mine[:, 0], hit + ctx.rank * n)
+                                  and np.array_equal(mine[:, 1:], res[hit]))
+    if not args.no_parity:
+        extra["parity"] = full_parity(re, hay, res, n, L, args)
     # algorithmic bytes per launch: forward bytes to the DFA's stop
     # (whole haystack when there is no match; e+1 when the DFA dies after a
     # match), reverse span, 16-byte result records.
@@ -232,7 +303,7 @@ def run_c2(ctx):
     line = ctx.line(METRIC, value, "GB/s", sec * 1e3, "u8",
                     "synthetic (seeded printable ASCII, 20% digits, 1% planted dates)", config,
                     matches_per_s=round(matched * ctx.world / sec, 1), matched_haystacks=matched,
-                    roofline=roofline(achieved, kernel_ms, b_alg, config))
+                    roofline=roofline(achieved, kernel_ms, b_alg, config), **extra)
     if ctx.rank == 0 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(re, hay, res, n, L, args)
     if ctx.rank == 0 and not args.no_pcie:
@@ -262,6 +333,26 @@ def pcie_inclusive(ctx, hay, scan):
             "h2d_GBps": round(nbytes / (h2d * 1e-3) / 1e9, 2), "note": "pinned host -> HBM copy + find, per batch"}
 
 
+def full_parity(re, hay, res, n, L, args):
+    """Whole-batch bit-exact check of this rank's GPU find results against the
+    oracle (the restated reference lazy DFA, dfa.rs:576-764 + exec.rs:632-662),
+    multi-threaded on the host.  A mismatch ends the run with a non-zero exit
+    status before any metric line is printed."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_py import OracleRegex
+    t0 = time.perf_counter()
+    buf = hay[: n * L].cpu().numpy()
+    exp, _ = OracleRegex(re).find_batch(buf, L, L, n, nthreads=cpu_threads(args.cpu_threads))
+    bad = np.nonzero((exp.astype(np.int64) != res).any(axis=1))[0]
+    if bad.size:
+        i = int(bad[0])
+        sys.stderr.write("PARITY FAILURE: %d of %d haystacks differ from the oracle; first %d: gpu %s oracle %s\n"
+                         % (bad.size, n, i, res[i].tolist(), exp[i].astype(np.int64).tolist()))
+        sys.exit(3)
+    return {"haystacks_checked": n, "mismatches": 0, "check_s": round(time.perf_counter() - t0, 2),
+            "against": "oracle (restated reference lazy DFA), whole batch"}
+
+
 def cpu_baseline(re, hay, res, n, L, args):
     """The oracle (restated reference lazy DFA, oracle/) on a bounded sample of
     the same haystacks, one private DFA cache per thread; also re-checks the
@@ -283,10 +374,13 @@ def cpu_baseline(re, hay, res, n, L, args):
         passes += 1
     gbps = S * L * passes / elapsed / 1e9
     parity = bool(np.array_equal(exp.astype(np.int64), res[:S]))
-    return {"value": round(gbps, 3), "unit": "GB/s", "cores": threads, "kind": "port",
-            "sample": "%d passes over the first %d haystacks x %d B (%.0f MiB) of the same batch" %
-                      (passes, S, L, S * L / 2**20),
-            "parity_on_sample": parity, "fwd_bytes_per_pass": int(st["fwd_bytes"])}
+    d = {"value": round(gbps, 3), "unit": "GB/s", "kind": "port",
+         "sample": "%d passes over the first %d haystacks x %d B (%.0f MiB) of the same batch" %
+                   (passes, S, L, S * L / 2**20),
+         "per_core_GBps": round(gbps / threads, 3),
+         "parity_on_sample": parity, "fwd_bytes_per_pass": int(st["fwd_bytes"])}
+    d.update(cpu_info(threads))
+    return d
 
 
 # ------------------------------------------------------------------ C3
@@ -528,16 +622,18 @@ def cpu_baseline_c4(rs, buf, offs, out, args):
         elapsed += time.perf_counter() - t0
         passes += 1
     got = out[:S].cpu().numpy().view(np.uint64)
-    return {"value": round(int(so[-1]) * passes / elapsed / 1e9, 3), "unit": "GB/s", "cores": threads,
-            "kind": "port", "lines_per_s": round(S * passes / elapsed, 1),
-            "sample": "%d passes over the first %d lines (%.0f MiB) of the same batch" % (passes, S, so[-1] / 2**20),
-            "parity_on_sample": bool(np.array_equal(exp, got))}
+    d = {"value": round(int(so[-1]) * passes / elapsed / 1e9, 3), "unit": "GB/s",
+         "kind": "port", "lines_per_s": round(S * passes / elapsed, 1),
+         "sample": "%d passes over the first %d lines (%.0f MiB) of the same batch" % (passes, S, so[-1] / 2**20),
+         "parity_on_sample": bool(np.array_equal(exp, got))}
+    d.update(cpu_info(threads))
+    return d
 
 
 # ------------------------------------------------------------------ C5
 def run_c5(ctx):
     import regex_amd as R
-    from regex_amd.dist import gather_records
+    from regex_amd.dist import RecordGather
     torch = ctx.torch
     L = 16 << 30
     g = torch.Generator(device=ctx.dev)
@@ -556,15 +652,15 @@ def run_c5(ctx):
     hay[pos:pos + len(plant)] = torch.frombuffer(bytearray(plant), dtype=torch.uint8).to(ctx.dev)
     re = R.Regex(r"\w+@\w+\.\w+")
     out = torch.empty((1, 2), dtype=torch.int64, device=ctx.dev)
+    gather = RecordGather(1, ctx.dev) if ctx.world > 1 else None
 
     def scan():
         re.find_batch(hay, stride=L, length=L, count=1, out=out, stream=ctx.stream)
 
     def step():
         scan()
-        if ctx.world > 1:
-            rec = torch.cat([torch.tensor([[ctx.rank]], dtype=torch.int64, device=ctx.dev), out], dim=1)
-            gather_records(rec)
+        if gather is not None:
+            gather.step(out, ctx.rank, ctx.stream)
 
     scan()
     torch.cuda.synchronize()
@@ -575,6 +671,9 @@ def run_c5(ctx):
     config = {"workload": "C5: find \\w+@\\w+\\.\\w+ over one 16 GiB haystack per GPU", "haystack_bytes": L,
               "parallelism": "dp%d" % ctx.world}
     extra = {}
+    if gather is not None:
+        recs, _ = gather.result()
+        extra["gathered_records"] = recs.cpu().tolist()
     if ctx.rank == 0 and not ctx.args.no_cpu:
         extra["cpu_baseline"] = cpu_baseline_c5(re, hay, pos, plant, ctx)
     return ctx.line("haystack GB/s scanned, bytes::Regex::find over 16 GiB shards", L * ctx.world / sec / 1e9,
@@ -614,10 +713,128 @@ def cpu_baseline_c5(re, hay, pos, plant, ctx):
                                 [pos - lo + 1, pos - lo + len(plant) - 1]}
 
 
+def launch_ranks(n):
+    """Start n rank processes of this same command (one per GPU) and relay rank
+    0's JSON line.  The parent never touches the GPU (no torch import) and does
+    not exec: the ranks are children.  If a rank fails, the others are stopped
+    and the exit status is non-zero."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else None))
+    out0 = procs[0].stdout
+    lines = []
+    rc = 0
+    while any(p.poll() is None for p in procs):
+        failed = [p for p in procs if p.poll() not in (None, 0)]
+        if failed:
+            rc = failed[0].returncode
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            break
+        time.sleep(0.2)
+    for p in procs:
+        try:
+            p.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+    lines = out0.read().decode().splitlines()
+    rc = rc or max(abs(p.returncode) for p in procs)
+    for ln in lines:
+        print(ln, flush=True)
+    return rc
+
+
+def run_rehearsal(ctx):
+    """CPU-only rehearsal of the N-rank protocol (launcher, barrier + max over
+    ranks timing, fixed-capacity record gather) with synthetic find results;
+    no kernel runs.  tests/test_bench_launch.py drives it with gloo."""
+    import torch
+    from regex_amd.dist import RecordGather
+    n = 4096
+    g = torch.Generator().manual_seed(1234 + ctx.rank)
+    found = torch.full((n, 2), -1, dtype=torch.int64)
+    hit = torch.randperm(n, generator=g)[: 100 + ctx.rank]
+    found[hit, 0] = hit
+    found[hit, 1] = hit + 10
+    gather = RecordGather(512, ctx.dev)
+    sec = ctx.timed(lambda: gather.step(found, ctx.rank * n))
+    recs, counts = gather.result()
+    exp = []
+    for r in range(ctx.world):
+        m = torch.full((n, 2), -1, dtype=torch.int64)
+        h = torch.randperm(n, generator=torch.Generator().manual_seed(1234 + r))[: 100 + r]
+        m[h, 0], m[h, 1] = h, h + 10
+        idx = (m[:, 0] >= 0).nonzero().squeeze(1)
+        exp.append(torch.stack([idx + r * n, m[idx, 0], m[idx, 1]], 1))
+    ok = bool(torch.equal(recs, torch.cat(exp)))
+    return ctx.line("rehearsal", n * ctx.world / sec, "haystacks/s", sec * 1e3, "int64", "synthetic find results",
+                    {"workload": "rehearsal", "parallelism": "dp%d" % ctx.world}, gathered_records=int(recs.shape[0]),
+                    gather_ok=ok, counts=counts)
+
+
+def run_c1(ctx):
+    """BASELINE configs[0]: the date regex `is_match` over 1K x 1 KiB ASCII
+    buffers.  The batched GPU call (latency-bound at this size: one launch
+    over 1 MiB) next to the oracle (restated reference lazy DFA) on the
+    host, whole-batch parity."""
+    import regex_amd as R
+    from regex_amd.workloads import date_haystacks_host
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_py import OracleRegex
+    torch, args = ctx.torch, ctx.args
+    n, L = 1024, 1024
+    buf, planted = date_haystacks_host(n, L, seed=0x5EED0001 ^ ctx.rank, frac=0.5)
+    hay = torch.from_numpy(buf).to(ctx.dev)
+    re = R.Regex(PATTERN)
+    out = torch.empty((n,), dtype=torch.uint8, device=ctx.dev)
+
+    def scan():
+        re.is_match_batch(hay, stride=L, length=L, count=n, out=out, stream=ctx.stream)
+
+    ctx.ramp(scan)
+    sec = ctx.timed(scan)
+    kms = ctx.kernel_ms(scan)
+    got = out.cpu().numpy().astype(bool)
+    o = OracleRegex(re)
+    exp = o.is_match_batch(buf, L, L, n, nthreads=1).astype(bool)
+    if not np.array_equal(got, exp):
+        sys.stderr.write("PARITY FAILURE (c1): %d haystacks differ\n" % int((got != exp).sum()))
+        sys.exit(3)
+    extra = {}
+    if ctx.rank == 0 and not args.no_cpu:
+        reps, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < min(args.cpu_seconds, 5.0):
+            o.is_match_batch(buf, L, L, n, nthreads=1)
+            reps += 1
+        el = time.perf_counter() - t0
+        extra["cpu_baseline"] = {"value": round(n * L * reps / el / 1e9, 3), "unit": "GB/s", "cores": 1,
+                                 "kind": "port", "sample": "%d passes of the whole 1K x 1 KiB batch, one thread (the "
+                                                           "reference's is_match is one call per buffer)" % reps}
+    config = {"workload": "C1: is_match %s over %d x %d B ASCII buffers" % (PATTERN, n, L),
+              "haystacks_per_gpu": n, "haystack_bytes": L, "parallelism": "dp%d" % ctx.world}
+    return ctx.line("haystack GB/s scanned, batched bytes::Regex::is_match", n * L * ctx.world / sec / 1e9, "GB/s",
+                    sec * 1e3, "u8", "synthetic (seeded printable ASCII, 20% digits, 50% planted dates)", config,
+                    matched_haystacks=int(got.sum()), parity={"haystacks_checked": n, "mismatches": 0},
+                    kernel_ms=round(kms, 4), note="latency-bound: one launch over 1 MiB", **extra)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     ctx = Ctx(args)
-    line = {"c2": run_c2, "c3": run_c3, "c4": run_c4, "c5": run_c5}[args.config](ctx)
+    line = {"c1": run_c1, "c2": run_c2, "c3": run_c3, "c4": run_c4, "c5": run_c5,
+            "rehearsal": run_rehearsal}[args.config](ctx)
     if ctx.rank == 0:
         print(json.dumps(line), flush=True)
     ctx.close()

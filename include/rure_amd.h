@@ -51,20 +51,20 @@ typedef struct rure_match {
 
 /* rure.h:147 — aborts (after printing the error) if the pattern is invalid. */
 rure *rure_compile_must(const char *pattern);
-/* rure.h:168-170 — NULL on error (error filled if non-NULL). */
+/* rure.h:168-169 — NULL on error (error filled if non-NULL). */
 rure *rure_compile(const uint8_t *pattern, size_t length, uint32_t flags,
                    rure_options *options, rure_error *error);
-/* rure.h:175 */
+/* rure.h:177 */
 void rure_free(rure *re);
 /* rure.h:197-198 */
 bool rure_is_match(rure *re, const uint8_t *haystack, size_t length, size_t start);
-/* rure.h:217-218 — `match` may be NULL. */
+/* rure.h:220-221 — `match` may be NULL. */
 bool rure_find(rure *re, const uint8_t *haystack, size_t length, size_t start,
                rure_match *match);
-/* rure.h:264-265 */
+/* rure.h:273-274 */
 bool rure_shortest_match(rure *re, const uint8_t *haystack, size_t length,
                          size_t start, size_t *end);
-/* rure.h:317-330 — iterator over successive non-overlapping matches. */
+/* rure.h:317-345 — iterator over successive non-overlapping matches. */
 rure_iter *rure_iter_new(rure *re);
 void rure_iter_free(rure_iter *it);
 bool rure_iter_next(rure_iter *it, const uint8_t *haystack, size_t length,
@@ -191,6 +191,15 @@ int rure_amd_replace_batch(rure *re, const rure_amd_batch *batch, const uint8_t 
 int rure_amd_split_batch(rure *re, const rure_amd_batch *batch, size_t limit, uint64_t *counts,
                          rure_match *pieces, size_t capacity, uint64_t *total, void *stream);
 
+/* Match records of a batched find for the multi-GPU gather (the
+ * path's only exchange): records[3*j .. 3*j+2] (device) = (base + i, start,
+ * end) of the j-th haystack i, in haystack order, whose found[i] (device,
+ * the output of rure_amd_find_batch over n haystacks) holds a match; at most
+ * `capacity` records are written; *count (device) = the number of matches
+ * (may exceed capacity).  No host synchronisation. */
+int rure_amd_compact_matches(const rure_match *found, size_t n, uint64_t base, uint64_t *records,
+                             size_t capacity, uint64_t *count, void *stream);
+
 /* Batched rure_find_captures: slots[i * 2 * ngroups + 2 * g + {0, 1}]
  * (device, size_t) = start / end of group g in haystack i, SIZE_MAX where the
  * group did not participate or the haystack has no match.  ngroups =
@@ -291,6 +300,11 @@ int64_t rure_amd_shiftand_export(rure *re, uint64_t *mask, uint64_t *init, uint6
  * Pike VM kernel (automaton too large), negative on error. */
 int rure_amd_uses_dfa(rure *re);
 int rure_amd_set_uses_dfa(rure_set *re);
+/* Diagnostics (host only): the forward-scan kernel the last batched
+ * find / is_match / shortest_match launch of this process used — 0 = the
+ * per-lane streaming kernel, 1 / 2 / 4 = the coalesced-tile kernel with that
+ * many bytes per dependent table lookup; -1 before the first launch. */
+int rure_amd_last_fwd_path(void);
 
 #ifdef __cplusplus
 }

@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
 #include <algorithm>
 #include <cstdlib>
 
@@ -498,10 +499,14 @@ static hipError_t launch_fwd(const BatchDev &b, const FwdDfaDev &f, const RevDfa
   return hipGetLastError();
 }
 
+static std::atomic<int> g_last_fwd_path{-1};
+int last_fwd_path() { return g_last_fwd_path.load(); }
+
 template <int MODE, int STRIDE>
 static hipError_t launch_tile_s(const BatchDev &b, const FwdDfaDev &f, const RevDfaDev &r, void *out, hipStream_t st,
                                 int grid) {
   const uint32_t bytes = STRIDE == 1 ? f.lds_bytes : f.lds_bytes_s;
+  g_last_fwd_path.store(STRIDE);
   // group scatter multiplier: a prime, coprime with the group count
   const uint64_t ngroups = (b.count + 63) / 64;
   uint64_t mul = 40503;
@@ -552,6 +557,7 @@ hipError_t launch_dfa_fwd(int mode, const BatchDev &b, const FwdDfaDev &f, const
       default: return launch_tile<MODE_SHORTEST>(b, f, r, out, st, tgrid);
     }
   }
+  g_last_fwd_path.store(0);
   switch (mode) {
     case MODE_FIND: return strided ? launch_fwd<MODE_FIND, true>(b, f, r, out, st, grid)
                                    : launch_fwd<MODE_FIND, false>(b, f, r, out, st, grid);

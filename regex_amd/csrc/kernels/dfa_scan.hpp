@@ -194,6 +194,15 @@ hipError_t launch_long_scan(int mode, const BatchDev &b, const FwdDfaDev &f, con
 
 hipError_t launch_dfa_fwd(int mode, const BatchDev &b, const FwdDfaDev &f, const RevDfaDev &r, void *out,
                           hipStream_t st, int grid);
+// Which forward-scan kernel the last launch_dfa_fwd call launched (tests
+// assert the instantiation the bench times): 0 = dfa_fwd_kernel (per-lane
+// streaming), 1 / 2 / 4 = dfa_fwd_tile_kernel with that many bytes per
+// dependent LDS lookup.
+int last_fwd_path();
+// Multi-GPU gather (gather_scan.hip): records (3 u64: base + haystack, start,
+// end) of the haystacks whose find result holds a match, first `cap`; *count.
+hipError_t launch_compact_matches(const uint64_t *found, uint64_t n, uint64_t base, uint64_t *rec, uint64_t cap,
+                                  uint64_t *count, hipStream_t st);
 hipError_t launch_dfa_set(const BatchDev &b, const SetDfaDev &f, uint64_t *out, hipStream_t st, int grid);
 
 }  // namespace rure_amd

@@ -1,0 +1,114 @@
+// Match-record compaction for the multi-GPU gather.
+//
+// A rank's batched find leaves one (start, end) pair per haystack, SIZE_MAX
+// where there is no match.  The only data-path exchange of the sharded scan is
+// an all-gather of the matches, so they are compacted on the device first —
+// (base + haystack, start, end) records in haystack order plus their count —
+// without a host round trip (a `nonzero` would synchronise every step).
+//
+// Two launches, no scan library: count_kernel writes the number of matching
+// haystacks of every 1024-haystack block; write_kernel sums the counts of the
+// blocks before its own (at most a few thousand u32, read by 256 threads),
+// scans its block in registers / LDS and writes its records.  The last block
+// also writes the total.  Deterministic order; O(n) bytes read twice.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dfa_scan.hpp"
+
+namespace rure_amd {
+
+namespace {
+
+constexpr uint32_t kCompactPer = 4;                    // haystacks per thread
+constexpr uint32_t kCompactBlock = 256 * kCompactPer;  // haystacks per block
+
+__device__ __forceinline__ uint32_t hits4(const uint64_t *found, uint64_t n, uint64_t h0, uint32_t *mask) {
+  uint32_t m = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kCompactPer; ++k) {
+    const uint64_t h = h0 + k;
+    if (h < n && found[2 * h] != ~(uint64_t)0) m |= 1u << k;
+  }
+  *mask = m;
+  return __popc(m);
+}
+
+// Exclusive prefix of v over the 256 threads of the block; *total = the sum.
+__device__ __forceinline__ uint32_t block_excl(uint32_t v, uint32_t *total) {
+  __shared__ uint32_t wsum[4];
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t incl = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t x = __shfl_up(incl, o, 64);
+    if (lane >= (uint32_t)o) incl += x;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  uint32_t before = 0, all = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < 4; ++j) {
+    before += j < w ? wsum[j] : 0;
+    all += wsum[j];
+  }
+  *total = all;
+  return before + incl - v;
+}
+
+__global__ __launch_bounds__(256) void compact_count_kernel(const uint64_t *found, uint64_t n, uint32_t *blk) {
+  const uint64_t h0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * kCompactPer;
+  uint32_t m, total;
+  block_excl(hits4(found, n, h0, &m), &total);
+  if (threadIdx.x == 0) blk[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(256) void compact_write_kernel(const uint64_t *found, uint64_t n, uint64_t base,
+                                                            const uint32_t *blk, uint64_t *rec, uint64_t cap,
+                                                            uint64_t *count) {
+  // records before this block
+  __shared__ uint64_t red[4];
+  uint64_t s = 0;
+  for (uint32_t j = threadIdx.x; j < blockIdx.x; j += 256) s += blk[j];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  const uint64_t off = red[0] + red[1] + red[2] + red[3];
+  const uint64_t h0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * kCompactPer;
+  uint32_t m, total;
+  uint64_t o = off + block_excl(hits4(found, n, h0, &m), &total);
+  while (m) {
+    const uint32_t k = __ffs(m) - 1;
+    m &= m - 1;
+    if (o < cap) {
+      const uint64_t h = h0 + k;
+      rec[3 * o] = base + h;
+      rec[3 * o + 1] = found[2 * h];
+      rec[3 * o + 2] = found[2 * h + 1];
+    }
+    ++o;
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *count = off + total;
+}
+
+}  // namespace
+
+hipError_t launch_compact_matches(const uint64_t *found, uint64_t n, uint64_t base, uint64_t *rec, uint64_t cap,
+                                  uint64_t *count, hipStream_t st) {
+  const uint64_t nb = n ? (n + kCompactBlock - 1) / kCompactBlock : 1;
+  if (nb > 0x7fffffffull) return hipErrorInvalidValue;
+  uint32_t *blk = nullptr;
+  hipError_t e = hipMallocAsync((void **)&blk, nb * 4, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(compact_count_kernel, dim3((uint32_t)nb), dim3(256), 0, st, found, n, blk);
+  if ((e = hipGetLastError()) == hipSuccess) {
+    hipLaunchKernelGGL(compact_write_kernel, dim3((uint32_t)nb), dim3(256), 0, st, found, n, base, blk, rec, cap,
+                       count);
+    e = hipGetLastError();
+  }
+  hipError_t e2 = hipFreeAsync(blk, st);
+  return e != hipSuccess ? e : e2;
+}
+
+}  // namespace rure_amd

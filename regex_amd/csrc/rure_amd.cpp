@@ -1459,6 +1459,15 @@ int rure_amd_find_batch(rure *re, const rure_amd_batch *batch, rure_match *out, 
   return RURE_AMD_OK;
 }
 
+int rure_amd_compact_matches(const rure_match *found, size_t n, uint64_t base, uint64_t *records, size_t capacity,
+                             uint64_t *count, void *stream) {
+  if ((!found && n) || (!records && capacity) || !count) return RURE_AMD_ERR_ARG;
+  return launch_compact_matches((const uint64_t *)found, n, base, records, capacity, count, (hipStream_t)stream) ==
+                 hipSuccess
+             ? RURE_AMD_OK
+             : RURE_AMD_ERR_HIP;
+}
+
 size_t rure_amd_captures_len(rure *re) { return re ? capture_slots(re) / 2 : 0; }
 
 int rure_amd_captures_batch(rure *re, const rure_amd_batch *batch, size_t *slots, void *stream) {
@@ -1859,6 +1868,8 @@ int rure_amd_uses_dfa(rure *re) {
   if (!build_regex(re)) return RURE_AMD_ERR_DFA;
   return re->dfa_ok ? 1 : 0;
 }
+
+int rure_amd_last_fwd_path(void) { return rure_amd::last_fwd_path(); }
 
 int rure_amd_set_uses_dfa(rure_set *rs) {
   if (!rs) return RURE_AMD_ERR_ARG;

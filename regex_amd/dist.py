@@ -44,6 +44,60 @@ def gather_records(rec, group=None):
     return torch.cat([p[: int(c.item())] for p, c in zip(parts, ks)], dim=0)
 
 
+def _all_gather_flat(out, inp, group=None):
+    """all_gather into one (world * rows, ...) tensor (no per-part copies);
+    backends without the flat collective get the list form."""
+    try:
+        dist.all_gather_into_tensor(out, inp, group=group)
+    except (RuntimeError, NotImplementedError, AttributeError):
+        dist.all_gather(list(out.chunk(dist.get_world_size(group))), inp, group=group)
+
+
+class RecordGather(object):
+    """Sync-free gathering of a rank's find results (the path's
+    only exchange).  Every step: the device compacts the (n, 2) find output
+    into (base + haystack, start, end) records with their count
+    (rure_amd_compact_matches, one HIP kernel pair, no host round trip), then
+    one all-gather of a fixed-capacity (capacity + 1, 3) block per rank — row
+    0 holds the count.  Nothing is read back until result(), after the timed
+    region, which also detects a capacity overflow."""
+
+    def __init__(self, capacity, device, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.cap = int(capacity)
+        self.send = torch.zeros((self.cap + 1, 3), dtype=torch.int64, device=device)
+        self.recv = torch.empty((self.world * (self.cap + 1), 3), dtype=torch.int64, device=device)
+
+    def compact(self, found, base, stream=None):
+        import ctypes
+        from . import _native as N, _stream_ptr
+        rc = N.rure_amd_compact_matches(ctypes.c_void_p(found.data_ptr()), found.shape[0], int(base),
+                                        ctypes.c_void_p(self.send[1:].data_ptr()), self.cap,
+                                        ctypes.c_void_p(self.send.data_ptr()), _stream_ptr(stream))
+        if rc != N.OK:
+            raise RuntimeError("rure_amd_compact_matches failed (%d)" % rc)
+
+    def step(self, found, base, stream=None):
+        if found.is_cuda:
+            self.compact(found, base, stream)
+        else:  # CPU rehearsal (gloo tests): the same layout from torch ops
+            rec = compact_matches(found, base)
+            k = rec.shape[0]
+            self.send[0, 0] = k
+            self.send[1:1 + min(k, self.cap)] = rec[: self.cap]
+        _all_gather_flat(self.recv, self.send, self.group)
+
+    def result(self):
+        """(records of every rank in rank order, per-rank counts); raises
+        OverflowError if a rank found more matches than the capacity."""
+        blocks = self.recv.view(self.world, self.cap + 1, 3)
+        counts = blocks[:, 0, 0].tolist()
+        if max(counts) > self.cap:
+            raise OverflowError("match records exceed the gather capacity (%d > %d)" % (max(counts), self.cap))
+        return torch.cat([blocks[r, 1:1 + c] for r, c in enumerate(counts)], dim=0), counts
+
+
 def max_over_ranks(seconds, device, group=None):
     """The slowest rank's time (the bench contract: max over ranks)."""
     t = torch.tensor([seconds], dtype=torch.float64, device=device)
