@@ -135,9 +135,15 @@ int rure_amd_find_batch(rure *re, const rure_amd_batch *batch, rure_match *out, 
 int rure_amd_is_match_batch(rure *re, const rure_amd_batch *batch, uint8_t *out, void *stream);
 /* Batched rure_shortest_match: end[i] or SIZE_MAX. */
 int rure_amd_shortest_match_batch(rure *re, const rure_amd_batch *batch, size_t *end, void *stream);
-/* Batched rure_set_matches: bit j of mask[i] set iff pattern j matches (<= 64 patterns). */
+/* Batched rure_set_matches (rure.h:532-533): bit j of mask[i] set iff
+ * pattern j matches; sets of at most 64 patterns (RURE_AMD_ERR_ARG above). */
 int rure_amd_set_matches_batch(rure_set *re, const rure_amd_batch *batch, uint64_t *mask,
                                void *stream);
+/* The same for any number of patterns: `words` >= ceil(rure_set_len / 64)
+ * u64 per haystack; bit (j % 64) of mask[i * words + j / 64] set iff pattern j
+ * matches haystack i (unused bits and words are zero). */
+int rure_amd_set_matches_batch_words(rure_set *re, const rure_amd_batch *batch, uint64_t *mask,
+                                     size_t words, void *stream);
 
 /* Batched find_iter (bytes::Regex::find_iter, re_trait.rs:197-221): every
  * successive non-overlapping leftmost-first match of every haystack.

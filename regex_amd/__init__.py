@@ -654,15 +654,24 @@ class RegexSet(object):
         N.rure_set_matches(self._set, text, len(text), start, buf)
         return [i for i in range(n) if buf[i]]
 
+    @property
+    def words(self):
+        """u64 mask words per haystack in matches_batch's output."""
+        return max(1, (len(self) + 63) // 64)
+
     def matches_batch(self, haystack, offsets=None, stride=None, length=None, count=None,
                       start=0, out=None, stream=None):
-        """One int64 bit mask per haystack (bit j <=> pattern j matched)."""
+        """Bit masks of the patterns matching each haystack: an (n,) int64
+        tensor (bit j <=> pattern j matched) for sets of up to 64 patterns,
+        else (n, words) with pattern j at bit j % 64 of word j // 64."""
         import torch
         b = _batch(haystack, offsets, stride, length, count, start)
+        w = self.words
         if out is None:
-            out = torch.empty((b.count,), dtype=torch.int64, device=haystack.device)
-        _check(N.rure_amd_set_matches_batch(self._set, ctypes.byref(b), ctypes.c_void_p(out.data_ptr()),
-                                            _stream_ptr(stream)), "matches_batch")
+            shape = (b.count,) if len(self) <= 64 else (b.count, w)
+            out = torch.empty(shape, dtype=torch.int64, device=haystack.device)
+        _check(N.rure_amd_set_matches_batch_words(self._set, ctypes.byref(b), ctypes.c_void_p(out.data_ptr()), w,
+                                                  _stream_ptr(stream)), "matches_batch")
         return out
 
     def program(self, which):

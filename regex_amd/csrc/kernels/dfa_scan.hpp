@@ -203,6 +203,9 @@ int last_fwd_path();
 // end) of the haystacks whose find result holds a match, first `cap`; *count.
 hipError_t launch_compact_matches(const uint64_t *found, uint64_t n, uint64_t base, uint64_t *rec, uint64_t cap,
                                   uint64_t *count, hipStream_t st);
+// dst[i * words + w] = src (u8 0/1 or u64 mask) of haystack i (gather_scan.hip).
+hipError_t launch_mask_column(const uint8_t *s8, const uint64_t *s64, uint64_t n, uint64_t *dst, uint64_t words,
+                              uint64_t w, hipStream_t st);
 hipError_t launch_dfa_set(const BatchDev &b, const SetDfaDev &f, uint64_t *out, hipStream_t st, int grid);
 
 }  // namespace rure_amd

@@ -6,13 +6,16 @@
 // (base + haystack, start, end) records in haystack order plus their count —
 // without a host round trip (a `nonzero` would synchronise every step).
 //
-// Two launches, no scan library: count_kernel writes the number of matching
-// haystacks of every 1024-haystack block; write_kernel sums the counts of the
-// blocks before its own (at most a few thousand u32, read by 256 threads),
-// scans its block in registers / LDS and writes its records.  The last block
-// also writes the total.  Deterministic order; O(n) bytes read twice.
+// count_kernel writes the number of matching haystacks of every 1024-haystack
+// block; write_kernel sums the counts of the blocks before its own (up to
+// 4096 blocks: a few thousand u64 read by 256 threads; beyond, a rocPRIM
+// exclusive scan of the counts runs in between), scans its block in
+// registers / LDS and writes its records.  The last block also writes the
+// total.  Deterministic order; the find output is read twice.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <algorithm>
 
 #include "dfa_scan.hpp"
 
@@ -56,7 +59,7 @@ __device__ __forceinline__ uint32_t block_excl(uint32_t v, uint32_t *total) {
   return before + incl - v;
 }
 
-__global__ __launch_bounds__(256) void compact_count_kernel(const uint64_t *found, uint64_t n, uint32_t *blk) {
+__global__ __launch_bounds__(256) void compact_count_kernel(const uint64_t *found, uint64_t n, uint64_t *blk) {
   const uint64_t h0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * kCompactPer;
   uint32_t m, total;
   block_excl(hits4(found, n, h0, &m), &total);
@@ -64,12 +67,14 @@ __global__ __launch_bounds__(256) void compact_count_kernel(const uint64_t *foun
 }
 
 __global__ __launch_bounds__(256) void compact_write_kernel(const uint64_t *found, uint64_t n, uint64_t base,
-                                                            const uint32_t *blk, uint64_t *rec, uint64_t cap,
-                                                            uint64_t *count) {
+                                                            const uint64_t *blk, const uint64_t *excl, uint64_t *rec,
+                                                            uint64_t cap, uint64_t *count) {
   // records before this block
   __shared__ uint64_t red[4];
   uint64_t s = 0;
-  for (uint32_t j = threadIdx.x; j < blockIdx.x; j += 256) s += blk[j];
+  if (excl) s = threadIdx.x == 0 ? excl[blockIdx.x] : 0;
+  else
+    for (uint32_t j = threadIdx.x; j < blockIdx.x; j += 256) s += blk[j];
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
@@ -92,19 +97,35 @@ __global__ __launch_bounds__(256) void compact_write_kernel(const uint64_t *foun
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *count = off + total;
 }
 
+__global__ __launch_bounds__(256) void mask_column_kernel(const uint8_t *s8, const uint64_t *s64, uint64_t n,
+                                                          uint64_t *dst, uint64_t words, uint64_t w) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
+    dst[i * words + w] = s8 ? (uint64_t)(s8[i] != 0) : s64[i];
+}
+
 }  // namespace
+
+hipError_t launch_mask_column(const uint8_t *s8, const uint64_t *s64, uint64_t n, uint64_t *dst, uint64_t words,
+                              uint64_t w, hipStream_t st) {
+  const uint64_t g = std::min<uint64_t>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(mask_column_kernel, dim3((uint32_t)(g ? g : 1)), dim3(256), 0, st, s8, s64, n, dst, words, w);
+  return hipGetLastError();
+}
 
 hipError_t launch_compact_matches(const uint64_t *found, uint64_t n, uint64_t base, uint64_t *rec, uint64_t cap,
                                   uint64_t *count, hipStream_t st) {
   const uint64_t nb = n ? (n + kCompactBlock - 1) / kCompactBlock : 1;
   if (nb > 0x7fffffffull) return hipErrorInvalidValue;
-  uint32_t *blk = nullptr;
-  hipError_t e = hipMallocAsync((void **)&blk, nb * 4, st);
+  const bool scan = nb > 4096;
+  uint64_t *blk = nullptr;
+  hipError_t e = hipMallocAsync((void **)&blk, nb * 8 * (scan ? 2 : 1), st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(compact_count_kernel, dim3((uint32_t)nb), dim3(256), 0, st, found, n, blk);
-  if ((e = hipGetLastError()) == hipSuccess) {
-    hipLaunchKernelGGL(compact_write_kernel, dim3((uint32_t)nb), dim3(256), 0, st, found, n, base, blk, rec, cap,
-                       count);
+  e = hipGetLastError();
+  if (e == hipSuccess && scan) e = exclusive_scan_u64(blk, blk + nb, nb, st);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(compact_write_kernel, dim3((uint32_t)nb), dim3(256), 0, st, found, n, base, blk,
+                       scan ? blk + nb : nullptr, rec, cap, count);
     e = hipGetLastError();
   }
   hipError_t e2 = hipFreeAsync(blk, st);

@@ -444,6 +444,13 @@ struct rure_set {
   std::map<int, DevTables> dev;
   Staging stage;
   rure *single = nullptr;   // one-pattern sets compile with compile_one
+  // Sets of more than 64 patterns: the device work runs in groups of 64
+  // consecutive patterns (group g owns mask word g).  Which patterns match a
+  // haystack does not depend on the other patterns of the set (every pattern
+  // is searched to completion, dfa.rs:525-570, pikevm.rs:150-180), so the
+  // groups' answers concatenated are the set's.  The combined programs are
+  // still compiled (size limit, program export).
+  std::vector<rure_set *> groups;
 };
 
 struct rure_captures {           // rure.rs Captures(Locations): 2 slots per group
@@ -511,6 +518,10 @@ bool build_set(rure_set *rs) {
   if (rs->exprs.empty()) { rs->dfa_ok = true; return true; }
   std::string nerr;
   rs->nfa_ok = build_nfa_tables(rs->nfa, &rs->nt, &nerr);
+  if (!rs->groups.empty()) {  // searched group by group; no combined DFA
+    rs->dfa_err = "set of more than 64 patterns: automata are built per 64-pattern group";
+    return rs->nfa_ok;
+  }
   DfaBuildLimits lim;
   std::string err;
   if (!build_dense_dfa(rs->fwd, lim, &rs->dfa, &err) || !pack_forward(rs->dfa, &rs->pf, &err)) {
@@ -1389,10 +1400,6 @@ rure_set *rure_compile_set(const uint8_t **patterns, const size_t *lens, size_t 
     rs->patterns.push_back(pat);
     rs->exprs.push_back(std::move(e));
   }
-  if (rs->exprs.size() > 64) {
-    if (error) error->msg = "rure_amd: sets of more than 64 patterns are not supported yet";
-    return nullptr;
-  }
   if (rs->exprs.size() == 1) {
     rs->single = rure_compile((const uint8_t *)rs->patterns[0].data(), rs->patterns[0].size(), flags,
                               options, error);
@@ -1406,12 +1413,22 @@ rure_set *rure_compile_set(const uint8_t **patterns, const size_t *lens, size_t 
     o.dfa = false;
     if (!compile_program(rs->exprs, o, &rs->nfa, &err)) { if (error) error->msg = err; return nullptr; }
   }
+  for (size_t lo = 0; count > 64 && lo < count; lo += 64) {
+    rure_set *g = rure_compile_set(patterns + lo, lens + lo, std::min<size_t>(64, count - lo), flags, options, error);
+    if (!g) {
+      for (rure_set *x : rs->groups) rure_set_free(x);
+      rs->groups.clear();
+      return nullptr;
+    }
+    rs->groups.push_back(g);
+  }
   return rs.release();
 }
 
 void rure_set_free(rure_set *rs) {
   if (!rs) return;
   if (rs->single) rure_free(rs->single);
+  for (rure_set *g : rs->groups) rure_set_free(g);
   for (auto &kv : rs->dev) {
     int cur = 0;
     (void)hipGetDevice(&cur);
@@ -1432,12 +1449,20 @@ static uint64_t set_mask_single(rure_set *rs, const uint8_t *hay, size_t len, si
 }
 
 bool rure_set_is_match(rure_set *rs, const uint8_t *hay, size_t len, size_t start) {
+  for (rure_set *g : rs->groups)
+    if (rure_set_is_match(g, hay, len, start)) return true;
+  if (!rs->groups.empty()) return false;
   return set_mask_single(rs, hay, len, start) != 0;
 }
 
 bool rure_set_matches(rure_set *rs, const uint8_t *hay, size_t len, size_t start, bool *matches) {
   size_t n = rs->exprs.size();
   for (size_t i = 0; i < n; ++i) matches[i] = false;  // rure.rs:557-562
+  if (!rs->groups.empty()) {
+    bool any = false;
+    for (size_t g = 0; g < rs->groups.size(); ++g) any |= rure_set_matches(rs->groups[g], hay, len, start, matches + 64 * g);
+    return any;
+  }
   uint64_t m = set_mask_single(rs, hay, len, start);
   for (size_t i = 0; i < n; ++i) matches[i] = (m >> i) & 1;
   return m != 0;
@@ -1513,18 +1538,59 @@ int rure_amd_shortest_match_batch(rure *re, const rure_amd_batch *batch, size_t 
   return RURE_AMD_OK;
 }
 
-int rure_amd_set_matches_batch(rure_set *rs, const rure_amd_batch *batch, uint64_t *mask, void *stream) {
-  BatchDev b;
-  if (!rs || !to_batch(batch, &b) || (!mask && b.count)) return RURE_AMD_ERR_ARG;
-  if (b.count == 0) return RURE_AMD_OK;
-  if (rs->exprs.size() < 2) return RURE_AMD_ERR_ARG;  // see rure_set_matches
+namespace {
+
+// One set of at most 64 patterns (>= 2) into one mask word per haystack.
+int set_batch_word(rure_set *rs, const BatchDev &b, uint64_t *mask, hipStream_t stream) {
   std::string err;
   DevTables *t = set_device(rs, &err);
   if (!t) return err.rfind("HIP", 0) == 0 ? RURE_AMD_ERR_HIP : RURE_AMD_ERR_DFA;
-  if (t->use_cores && !t->cores_adapted && !adapt_cores(rs, t, b, (hipStream_t)stream, &err)) return RURE_AMD_ERR_HIP;
+  if (t->use_cores && !t->cores_adapted && !adapt_cores(rs, t, b, stream, &err)) return RURE_AMD_ERR_HIP;
   int grid = grid_for(b.count, t->s.lds_bytes, t->cus);
-  if (run_set(b, *t, mask, (hipStream_t)stream, grid) != hipSuccess) return RURE_AMD_ERR_HIP;
+  if (run_set(b, *t, mask, stream, grid) != hipSuccess) return RURE_AMD_ERR_HIP;
   return RURE_AMD_OK;
+}
+
+// Group g (patterns [64 g, 64 g + len)) into word g of mask (words per haystack).
+int set_batch_group(rure_set *g, const rure_amd_batch *batch, const BatchDev &b, uint64_t *mask, size_t words,
+                    size_t w, hipStream_t st) {
+  void *tmp = nullptr;
+  const bool single = g->single != nullptr;
+  if (hipMallocAsync(&tmp, b.count * (single ? 1 : 8), st) != hipSuccess) return RURE_AMD_ERR_HIP;
+  int rc = single ? rure_amd_is_match_batch(g->single, batch, (uint8_t *)tmp, st)
+                  : set_batch_word(g, b, (uint64_t *)tmp, st);
+  if (rc == RURE_AMD_OK &&
+      launch_mask_column(single ? (const uint8_t *)tmp : nullptr, single ? nullptr : (const uint64_t *)tmp, b.count,
+                         mask, words, w, st) != hipSuccess)
+    rc = RURE_AMD_ERR_HIP;
+  if (hipFreeAsync(tmp, st) != hipSuccess && rc == RURE_AMD_OK) rc = RURE_AMD_ERR_HIP;
+  return rc;
+}
+
+}  // namespace
+
+int rure_amd_set_matches_batch_words(rure_set *rs, const rure_amd_batch *batch, uint64_t *mask, size_t words,
+                                     void *stream) {
+  BatchDev b;
+  if (!rs || !to_batch(batch, &b) || (!mask && b.count)) return RURE_AMD_ERR_ARG;
+  const size_t n = rs->exprs.size();
+  if (words < std::max<size_t>(1, (n + 63) / 64)) return RURE_AMD_ERR_ARG;
+  if (b.count == 0) return RURE_AMD_OK;
+  hipStream_t st = (hipStream_t)stream;
+  if (words == 1 && n >= 2) return set_batch_word(rs, b, mask, st);
+  if (hipMemsetAsync(mask, 0, b.count * words * 8, st) != hipSuccess) return RURE_AMD_ERR_HIP;
+  if (n == 0) return RURE_AMD_OK;  // MatchType::Nothing (exec.rs:276-286)
+  if (rs->groups.empty()) return set_batch_group(rs, batch, b, mask, words, 0, st);
+  for (size_t g = 0; g < rs->groups.size(); ++g) {
+    int rc = set_batch_group(rs->groups[g], batch, b, mask, words, g, st);
+    if (rc != RURE_AMD_OK) return rc;
+  }
+  return RURE_AMD_OK;
+}
+
+int rure_amd_set_matches_batch(rure_set *rs, const rure_amd_batch *batch, uint64_t *mask, void *stream) {
+  if (rs && rs->exprs.size() > 64) return RURE_AMD_ERR_ARG;  // use rure_amd_set_matches_batch_words
+  return rure_amd_set_matches_batch_words(rs, batch, mask, 1, stream);
 }
 
 namespace {
@@ -1874,6 +1940,15 @@ int rure_amd_last_fwd_path(void) { return rure_amd::last_fwd_path(); }
 int rure_amd_set_uses_dfa(rure_set *rs) {
   if (!rs) return RURE_AMD_ERR_ARG;
   if (rs->single) return rure_amd_uses_dfa(rs->single);
+  if (!rs->groups.empty()) {
+    int all = 1;
+    for (rure_set *g : rs->groups) {
+      int u = rure_amd_set_uses_dfa(g);
+      if (u < 0) return u;
+      all &= u;
+    }
+    return all;
+  }
   if (!build_set(rs)) return RURE_AMD_ERR_DFA;
   return rs->dfa_ok ? 1 : 0;
 }
