@@ -273,6 +273,12 @@ int rure_amd_set_core_export(rure_set *re, rure_amd_core_info *info, uint8_t *ld
                              uint64_t *gout, uint64_t *eof, uint16_t *start);
 /* strip[s] (states u32) of the find_iter forward DFA: s without the `.*?` prefix. */
 int rure_amd_dfa_strip_export(rure *re, uint32_t *strip);
+/* The first-byte start rule of the find_iter DFA (host only): returns |F|
+ * (1..4, bytes[0..|F|) = F) when every match starts with a byte of F and an
+ * anchored run from such a byte cannot die before matching — the chunked
+ * find_iter then takes a match's start from the first F byte of its search
+ * instead of a reverse scan — else 0; negative on error. */
+int rure_amd_first_byte_export(rure *re, uint8_t *bytes);
 
 /* Export of the Pike VM closure tables the NFA kernel runs (host only):
  * leaves = 3 u32 per leaf (kind | lo << 8 | hi << 16, closure, slot),

@@ -515,6 +515,13 @@ class Regex(object):
         rc = N.rure_amd_dfa_info_get(self._re, which, ctypes.byref(info))
         return {k: getattr(info, k) for k, _ in N.DfaInfo._fields_} if rc == N.OK else None
 
+    def first_bytes(self):
+        """The first-byte start rule of the chunked find_iter (bytes of F, or
+        None when the rule does not hold)."""
+        buf = (ctypes.c_uint8 * 4)()
+        n = N.rure_amd_first_byte_export(self._re, buf)
+        return bytes(buf[:n]) if n > 0 else None
+
     def program(self, which):
         """Compiled byte program (0 fwd DFA, 1 reverse DFA, 2 NFA): (info, insts)."""
         return _export(N.rure_amd_program_export, self._re, which)

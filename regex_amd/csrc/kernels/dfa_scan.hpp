@@ -60,6 +60,14 @@ struct FwdDfaDev {
   const uint64_t *sa_image;
   uint64_t sa_init, sa_final;   // first / last bit of every sequence
   uint32_t sa_len, sa_bits;
+  // find_iter DFA only: the first-byte start rule (fb_n = 0: off).  Every
+  // match starts with one of fb_n <= 4 bytes (fb_rep[i] = byte * 0x01010101),
+  // and an anchored run from such a byte never dies before it has matched
+  // (host: first_byte_rule).  Then the leftmost match of a search from p
+  // that ends in the dead state before the end of the text starts at the
+  // first of those bytes at or after p, so the start needs no reverse scan.
+  uint32_t fb_n;
+  uint32_t fb_rep[4];
 };
 
 // Literal engine image layout (at most kLitMax literals of kLitLen bytes).

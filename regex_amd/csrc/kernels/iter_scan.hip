@@ -210,14 +210,18 @@ __device__ __forceinline__ uint32_t steps16(uint32_t s, const uint32_t w[4], uin
 // MODE_FIND: dfa.rs:576-764 up to the dead state): the window's blocks are
 // loaded first, then each goes through the exact4 fast chain and, if that
 // entered a match / dead / quit state, the branch-free steps16.
+// hib: OR of every word loaded (the first-byte rule needs ASCII-only scans).
 __device__ __forceinline__ void fwd_window_all(LaneState &L, const FwdDfaDev &f, const uint8_t *lds,
-                                               const uint8_t *base, uint64_t at, uint64_t end) {
+                                               const uint8_t *base, uint64_t at, uint64_t end, uint32_t &hib) {
   const uintptr_t a0 = (uintptr_t)(base + at) & ~(uintptr_t)15;
   const uintptr_t ae = (uintptr_t)(base + end);
   uint4 v[9];
 #pragma unroll
   for (int k = 0; k < 9; ++k)
-    if (a0 + 16 * k < ae) v[k] = *(const uint4 *)(a0 + 16 * k);
+    if (a0 + 16 * k < ae) {
+      v[k] = *(const uint4 *)(a0 + 16 * k);
+      hib |= v[k].x | v[k].y | v[k].z | v[k].w;
+    }
   // position of the window's first byte (negative when the haystack starts
   // mid-block)
   const int64_t p0 = (int64_t)at - (int64_t)((uintptr_t)(base + at) & 15);
@@ -281,6 +285,32 @@ __device__ __forceinline__ uint64_t rev_scan_all(const RevDfaDev &r, const uint8
   return rs;
 }
 
+// First-byte start rule (FwdDfaDev::fb_n): the first position in [lo, hi)
+// holding a byte of F (ASCII; SWAR zero-byte tests without cross-byte carries),
+// or NONE.
+__device__ __forceinline__ uint32_t fb_zero_bytes(uint32_t x) {  // 0x80 in each zero byte of x
+  return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+}
+__device__ __forceinline__ uint64_t fb_first(const FwdDfaDev &f, const uint8_t *base, uint64_t lo, uint64_t hi) {
+  for (uintptr_t a = (uintptr_t)(base + lo) & ~(uintptr_t)15; a < (uintptr_t)(base + hi); a += 16) {
+    const uint4 v = *(const uint4 *)a;
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    const int64_t bp = (int64_t)(a - (uintptr_t)base);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint32_t z = fb_zero_bytes(w[j] ^ f.fb_rep[0]) | fb_zero_bytes(w[j] ^ f.fb_rep[1]) |
+                   fb_zero_bytes(w[j] ^ f.fb_rep[2]) | fb_zero_bytes(w[j] ^ f.fb_rep[3]);
+      const int64_t wp = bp + 4 * j;
+      if (wp < (int64_t)lo) z = (int64_t)lo - wp >= 4 ? 0u : z & (0xFFFFFFFFu << (8 * ((int64_t)lo - wp)));
+      if (z) {
+        const uint64_t q = (uint64_t)wp + (__builtin_ctz(z) >> 3);
+        return q < hi ? q : NONE;
+      }
+    }
+  }
+  return NONE;
+}
+
 // Pass 1, burst-interleaved.  In iter_spec_kernel every search is a nest of
 // loops (forward scan to the dead state, reverse scan, restart), so a lane
 // whose search ends early waits, masked off, until every other lane of its
@@ -304,7 +334,7 @@ __global__ __launch_bounds__(1024) void iter_spec_burst_kernel(BatchDev b, Geo g
     uint64_t at = 0, at0 = 0, cutpos = NONE;        // the current forward scan
     uint64_t ex_p = 0, ex_lm = NONE;
     bool clean = true, quit = false, searching = false;
-    uint32_t n = 0;
+    uint32_t n = 0, hib = 0;
     LaneState L;
     L.done = true;
 
@@ -318,6 +348,7 @@ __global__ __launch_bounds__(1024) void iter_spec_burst_kernel(BatchDev b, Geo g
       if (p > len) { finish(sp, slm, true); return; }
       lane_start(L, f, base, len, p);
       at0 = at = p;
+      hib = 0;
       cutpos = (c1 > p && c1 - 1 <= len) ? c1 - 1 : NONE;
       searching = true;
     };
@@ -343,7 +374,7 @@ __global__ __launch_bounds__(1024) void iter_spec_burst_kernel(BatchDev b, Geo g
         uint64_t lim = (((uintptr_t)(base + at) & ~(uintptr_t)15) + 128) - (uintptr_t)base;
         lim = min(lim, len);
         if (cutpos != NONE) lim = min(lim, cutpos);
-        if (f.all) fwd_window_all(L, f, lds, base, at, lim);
+        if (f.all) fwd_window_all(L, f, lds, base, at, lim, hib);
         else fwd_range<MODE_FIND>(L, f, lds, base, at, lim);
         at = lim;
       }
@@ -355,7 +386,11 @@ __global__ __launch_bounds__(1024) void iter_spec_burst_kernel(BatchDev b, Geo g
       const uint64_t me = L.last;
       uint64_t ms = at0;
       if (me != at0) {  // exec.rs:647
-        const uint64_t rs = r.all ? rev_scan_all(r, rlds, base, len, at0, me) : rev_scan(r, rlds, base, len, at0, me);
+        // the scan died before the end over ASCII bytes: the match starts at
+        // the first F byte (first_byte_rule), else the reverse scan finds it
+        uint64_t rs = f.fb_n && f.all && L.done && !(hib & 0x80808080u) ? fb_first(f, base, at0, me) : NONE;
+        if (rs == NONE)
+          rs = r.all ? rev_scan_all(r, rlds, base, len, at0, me) : rev_scan(r, rlds, base, len, at0, me);
         if (rs == QUITMARK) { quit = true; finish(sp, slm, false); continue; }
         if (rs == NONE) { finish(sp, slm, true); continue; }
         ms = rs;

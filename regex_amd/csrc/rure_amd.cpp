@@ -422,6 +422,8 @@ struct rure {
   DenseDfa dfwd_iter;
   PackedFwd pf_iter;
   bool lit_ok = false;      // the regex is a finite string set (literal find_iter engine)
+  uint32_t fb_n = 0;        // first-byte start rule (first_byte_rule): |F| or 0
+  uint8_t fb_bytes[4] = {0, 0, 0, 0};
   LiteralSet lits;
   std::map<int, std::pair<void *, FwdDfaDev>> iter_dev;
 };
@@ -765,6 +767,46 @@ hipError_t run_pike(int mode, bool fallback, const BatchDev &b, const DevTables 
   return e != hipSuccess ? e : e2;
 }
 
+// The first-byte start rule of FwdDfaDev::fb_n, decided on the find_iter DFA
+// (with strip states, no look-around, flag-independent start).  F = the
+// ASCII bytes on which the anchored start state strip[start] does not die
+// (every match starts with a byte on which it does not die).  Every state
+// reachable from it through F and then ASCII bytes, before a match-flag state
+// is entered, must have no ASCII transition to `dead` or `quit`: an anchored
+// run from an F byte over ASCII text then cannot fail except by reaching the
+// end of the text.  So in a forward search (`.*?` prefix, leftmost-first)
+// from p over ASCII text, the thread started at the first c >= p with text[c]
+// in F stays alive until it has matched, the DFA reaches `dead` before the
+// end only after that, and the match it reports starts at c (threads from
+// earlier starts have priority, dfa.rs:910-1048).  The kernel applies the
+// rule to a search only when every byte it loaded was ASCII (Unicode classes
+// such as `[^\n]` die on invalid UTF-8).  Returns |F| (1..4) or 0.
+static uint32_t first_byte_rule(const DenseDfa &d, uint32_t ustart1, bool nonempty, uint8_t bytes[4]) {
+  if (!ustart1 || !nonempty || d.strip.empty() || d.quit >= 0) return 0;
+  const uint32_t a0 = d.strip[ustart1 - 1];
+  if ((int)a0 >= d.n_normal) return 0;
+  uint32_t nf = 0;
+  std::vector<uint32_t> todo;
+  std::vector<uint8_t> seen(d.nstates, 0);
+  for (int c = 0; c < 128; ++c) {
+    const uint32_t t = d.trans[(size_t)a0 * 256 + c];
+    if ((int)t == d.dead) continue;
+    if (nf == 4) return 0;
+    bytes[nf++] = (uint8_t)c;
+    if ((int)t < d.n_normal && !seen[t]) { seen[t] = 1; todo.push_back(t); }
+  }
+  while (!todo.empty()) {  // pre-match states: normal states reached before a match flag
+    const uint32_t x = todo.back();
+    todo.pop_back();
+    for (int c = 0; c < 128; ++c) {
+      const uint32_t t = d.trans[(size_t)x * 256 + c];
+      if ((int)t == d.dead) return 0;
+      if ((int)t < d.n_normal && !seen[t]) { seen[t] = 1; todo.push_back(t); }
+    }
+  }
+  return nf;
+}
+
 bool build_iter_dfa(rure *re) {
   if (!build_regex_dfas(re)) return false;
   std::lock_guard<std::mutex> g(re->mu);
@@ -775,6 +817,8 @@ bool build_iter_dfa(rure *re) {
     std::string e;
     re->iter_ok = build_dense_dfa(re->fwd, lim, &re->dfwd_iter, &e) && pack_forward(re->dfwd_iter, &re->pf_iter, &e, true);
     re->lit_ok = extract_literals(re->nfa, kLitMax, kLitLen, &re->lits);
+    if (re->iter_ok)
+      re->fb_n = first_byte_rule(re->dfwd_iter, re->pf_iter.ustart1, !can_match_empty(re->nfa), re->fb_bytes);
   }
   return re->iter_ok;
 }
@@ -900,6 +944,9 @@ const FwdDfaDev *iter_device(rure *re, const DevTables &t, std::string *err) {
   f.all = pf.all;
   f.ustart1 = pf.ustart1;
   f.nonempty = can_match_empty(re->nfa) ? 0 : 1;
+  // RURE_AMD_FB=0 turns the first-byte start rule off (reverse scans)
+  f.fb_n = getenv("RURE_AMD_FB") && getenv("RURE_AMD_FB")[0] == '0' ? 0 : re->fb_n;
+  for (uint32_t i = 0; i < 4; ++i) f.fb_rep[i] = (i < re->fb_n ? re->fb_bytes[i] : re->fb_bytes[0]) * 0x01010101u;
   if (!lit_img.empty()) {
     f.lit_image = base + o_lit;
     f.lit_bytes = kLitImage;
@@ -1858,6 +1905,13 @@ int rure_amd_set_core_export(rure_set *rs, rure_amd_core_info *info, uint8_t *ld
   if (eof) memcpy(eof, cs.eof.data(), cs.eof.size() * 8);
   if (start) memcpy(start, cs.start, 256);
   return RURE_AMD_OK;
+}
+
+int rure_amd_first_byte_export(rure *re, uint8_t *bytes) {
+  if (!re) return RURE_AMD_ERR_ARG;
+  if (!build_iter_dfa(re)) return RURE_AMD_ERR_DFA;
+  if (bytes) memcpy(bytes, re->fb_bytes, 4);
+  return (int)re->fb_n;
 }
 
 int rure_amd_dfa_strip_export(rure *re, uint32_t *strip) {

@@ -29,9 +29,12 @@ class QuitError(Exception):
     pass
 
 
-def find(fwd, rev, t, start=0, mode="find", cut=None):
+def find(fwd, rev, t, start=0, mode="find", cut=None, fb=None):
     """cut: the search may not start a match at or after `cut` (the kernel's
-    dfa_find_cut: the state at cut - 1 is replaced by its stripped copy)."""
+    dfa_find_cut: the state at cut - 1 is replaced by its stripped copy).
+    fb: the first-byte start rule's bytes (iter_scan.hip, host
+    first_byte_rule): when the scan ended in the dead state and every byte it
+    read was ASCII, the start is the first fb byte at or after `start`."""
     info, tr, eof, st = fwd
     s = int(st[fwd_flag(t, start)])
     last = None
@@ -72,6 +75,8 @@ def find(fwd, rev, t, start=0, mode="find", cut=None):
         return None
     if last == start:
         return (start, start)
+    if fb and done and all(b < 0x80 for b in t[start:at + 1]):
+        return (next(i for i in range(start, last) if t[i] in fb), last)
     rinfo, rtr, reof, rst = rev
     s = int(rst[rev_flag(t, start, last)])
     rs = None

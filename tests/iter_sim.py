@@ -8,8 +8,8 @@ NONE = None
 
 
 class UnitIter(object):
-    def __init__(self, fwd, rev, t, st, c1):
-        self.fwd, self.rev, self.t = fwd, rev, t
+    def __init__(self, fwd, rev, t, st, c1, fb=None):
+        self.fwd, self.rev, self.t, self.fb = fwd, rev, t, fb
         self.p, self.lm = st
         self.c1 = c1
         self.ended = False
@@ -21,7 +21,7 @@ class UnitIter(object):
         while True:
             if self.p > len(t):
                 return None
-            m = find(self.fwd, self.rev, t, self.p, cut=self.c1)
+            m = find(self.fwd, self.rev, t, self.p, cut=self.c1, fb=self.fb)
             if m is None:
                 return None
             s, e = m
@@ -58,14 +58,14 @@ def equiv(ca, a, cb, b):
     return a == b
 
 
-def find_iter_chunked(fwd, rev, t, chunk, start=0, slots=1 << 30):
+def find_iter_chunked(fwd, rev, t, chunk, start=0, slots=1 << 30, fb=None):
     INF = float("inf")
     span = max(0, len(t) - start)
     nk = 1 if span <= chunk else (span + chunk - 1) // chunk
     bounds = [(start + k * chunk, INF if k + 1 == nk else start + (k + 1) * chunk) for k in range(nk)]
     units = []
     for k, (c0, c1) in enumerate(bounds):  # pass 1: speculation
-        it = UnitIter(fwd, rev, t, (c0, None), c1)
+        it = UnitIter(fwd, rev, t, (c0, None), c1, fb)
         ms = []
         while True:
             m = it.next()

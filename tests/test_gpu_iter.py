@@ -106,3 +106,29 @@ def test_regexdna_replicated_counts(cuda):
     o = OracleRegex(strip)
     c, m = strip.find_iter_batch(to_dev(big + b"\0" * 16, cuda), stride=len(big), length=len(big), count=1)
     assert as_pairs(m) == o.find_iter(big)
+
+
+FB_PATTERNS = [r">[^\n]*\n|\n", r"a+", r"a[^b]*b", r"[ab]c*", r"\n", r">[^\n]*", r"(?-u)>[^\n]*\n|\n",
+               r"a(b|cd)*e?", r"(?s)a.*b|c"]
+
+
+def _fb_text(seed, n, nonascii):
+    rng = random.Random(seed)
+    alpha = [b"a", b"b", b"c", b"d", b"e", b"\n", b">", b"g", b"t"] + ([b"\xc3\xa9", b"\xff", b"\x80"] if nonascii else [])
+    w = [8, 3, 5, 3, 2, 2, 1, 20, 20] + ([1, 1, 1] if nonascii else [])
+    return b"".join(rng.choices(alpha, weights=w, k=n))
+
+
+@pytest.mark.parametrize("pat", FB_PATTERNS)
+@pytest.mark.parametrize("nonascii", [False, True])
+def test_find_iter_first_byte_rule(cuda, pat, nonascii):
+    """The first-byte start rule of the speculative pass (no reverse scan where
+    the host proved the match start is the first F byte) against the oracle,
+    on one long chunked haystack with ASCII-only and mixed bytes."""
+    re = R.Regex(pat)
+    assert re.first_bytes()
+    text = _fb_text(zlib.crc32(pat.encode()), 300000, nonascii)
+    exp = OracleRegex(re).find_iter(text)
+    counts, m = re.find_iter_batch(to_dev(text + b"\0" * 16, cuda), stride=len(text), length=len(text), count=1)
+    assert int(counts[0]) == len(exp)
+    assert as_pairs(m) == exp

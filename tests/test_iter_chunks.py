@@ -42,3 +42,45 @@ def test_strip_states_exist():
     info = R.Regex(r"\w+@\w+\.\w+").dfa_info(2)
     base = R.Regex(r"\w+@\w+\.\w+").dfa_info(0)
     assert info["ok"] == 1 and info["states"] >= base["states"]
+
+
+FB_PATTERNS = [r">[^\n]*\n|\n", r"a+", r"a[^b]*b", r"[ab]c*", r"\n", r">[^\n]*", r"(?-u)>[^\n]*\n|\n",
+               r"a(b|cd)*e?", r"ab*|ac*", r"(?s)a.*b|c"]
+
+
+def mixed_text(seed, n):
+    rng = random.Random(seed)
+    alpha = [b"a", b"b", b"c", b"d", b"e", b"\n", b">", b"x", "é".encode(), b"\xff", b"\x80"]
+    w = [8, 6, 5, 3, 2, 4, 3, 6, 1, 1, 1]
+    return b"".join(rng.choices(alpha, weights=w, k=n))
+
+
+@pytest.mark.parametrize("pat", FB_PATTERNS)
+def test_first_byte_rule(pat):
+    """The first-byte start rule (iter_scan.hip / host first_byte_rule): where
+    the host says it holds, every cut-bounded search from every start that
+    ends in the dead state over ASCII bytes starts at the first F byte — the
+    same match the reverse scan finds."""
+    re = R.Regex(pat)
+    fb = re.first_bytes()
+    assert fb, pat
+    fwd = re.dfa_tables(2)
+    rev = re.dfa_tables(1)
+    o = OracleRegex(re)
+    from dfa_sim import find
+    used = 0
+    for i in range(5):
+        t = mixed_text(zlib.crc32(pat.encode()) + i, 120) if i % 2 else text(i, 120)
+        for st in range(len(t) + 1):
+            for cut in (None, st + 1, st + 5, st + 40):
+                a = find(fwd, rev, t, st, cut=cut)
+                b = find(fwd, rev, t, st, cut=cut, fb=fb)
+                assert a == b, (pat, i, st, cut, a, b)
+                used += a is not None
+        assert find_iter_chunked(fwd, rev, t, 13, fb=fb) == o.find_iter(t)
+    assert used > 50
+
+
+def test_first_byte_rule_rejects():
+    for pat in [r"abc|ab", r"\w+", r"\d{4}-\d{2}-\d{2}", r"x*", r"agggtaaa|tttaccct", r"a\b"]:
+        assert R.Regex(pat).first_bytes() is None, pat
