@@ -210,28 +210,14 @@ __device__ __forceinline__ uint32_t steps16(uint32_t s, const uint32_t w[4], uin
 // MODE_FIND: dfa.rs:576-764 up to the dead state): the window's blocks are
 // loaded first, then each goes through the exact4 fast chain and, if that
 // entered a match / dead / quit state, the branch-free steps16.
-// First-byte start rule (FwdDfaDev::fb_n): SWAR zero-byte test without
-// cross-byte carries (exact per byte).
-__device__ __forceinline__ uint32_t fb_zero_bytes(uint32_t x) {  // 0x80 in each zero byte of x
-  return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
-}
-// FB (first-byte start rule): hib = OR of every word loaded (the rule needs
-// ASCII-only scans) and fc = the first F byte at or after at0 (NONE until
-// seen), tracked on the blocks already in registers, independent of the
-// dependent LDS chain.
-template <bool FB>
 __device__ __forceinline__ void fwd_window_all(LaneState &L, const FwdDfaDev &f, const uint8_t *lds,
-                                               const uint8_t *base, uint64_t at, uint64_t end, uint32_t &hib,
-                                               uint64_t &fc, uint64_t at0) {
+                                               const uint8_t *base, uint64_t at, uint64_t end) {
   const uintptr_t a0 = (uintptr_t)(base + at) & ~(uintptr_t)15;
   const uintptr_t ae = (uintptr_t)(base + end);
   uint4 v[9];
 #pragma unroll
   for (int k = 0; k < 9; ++k)
-    if (a0 + 16 * k < ae) {
-      v[k] = *(const uint4 *)(a0 + 16 * k);
-      if (FB) hib |= v[k].x | v[k].y | v[k].z | v[k].w;
-    }
+    if (a0 + 16 * k < ae) v[k] = *(const uint4 *)(a0 + 16 * k);
   // position of the window's first byte (negative when the haystack starts
   // mid-block)
   const int64_t p0 = (int64_t)at - (int64_t)((uintptr_t)(base + at) & 15);
@@ -242,16 +228,6 @@ __device__ __forceinline__ void fwd_window_all(LaneState &L, const FwdDfaDev &f,
     const uint32_t k0 = bp < (int64_t)at ? (uint32_t)((int64_t)at - bp) : 0;
     const uint32_t kend = (int64_t)end - bp < 16 ? (uint32_t)((int64_t)end - bp) : 16;
     const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
-    if (FB && fc == NONE) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        uint32_t z = fb_zero_bytes(w[j] ^ f.fb_rep[0]);
-        for (uint32_t q = 1; q < f.fb_n; ++q) z |= fb_zero_bytes(w[j] ^ f.fb_rep[q]);
-        const int64_t wp = bp + 4 * j;
-        if (wp < (int64_t)at0) z = (int64_t)at0 - wp >= 4 ? 0u : z & (0xFFFFFFFFu << (8 * ((int64_t)at0 - wp)));
-        if (z && fc == NONE) fc = (uint64_t)wp + (__builtin_ctz(z) >> 3);
-      }
-    }
     if (k0 == 0 && kend == 16) {
       uint32_t t = L.s, mx = 0;
       t = exact4(t, w[0], lds, mx);
@@ -315,9 +291,7 @@ __device__ __forceinline__ uint64_t rev_scan_all(const RevDfaDev &r, const uint8
 // lane whose scan ended does its reverse scan, applies the iteration rule
 // (re_trait.rs:197-221) and sets up its next search (exec.rs:632-662) in
 // the same iteration.  Same unit records as iter_spec_kernel.
-// (FB: 256-thread blocks so the extra tracking fits registers without spills)
-template <bool FB>
-__global__ __launch_bounds__(FB ? 256 : 1024) void iter_spec_burst_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f,
+__global__ __launch_bounds__(1024) void iter_spec_burst_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f,
                                                               RevDfaDev r, Unit *units, uint64_t *slots,
                                                               uint32_t *counts, uint32_t *dirty) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -330,8 +304,7 @@ __global__ __launch_bounds__(FB ? 256 : 1024) void iter_spec_burst_kernel(BatchD
     uint64_t at = 0, at0 = 0, cutpos = NONE;        // the current forward scan
     uint64_t ex_p = 0, ex_lm = NONE;
     bool clean = true, quit = false, searching = false;
-    uint32_t n = 0, hib = 0;
-    uint64_t fc = NONE;  // first-byte rule: the first F byte of the current search
+    uint32_t n = 0;
     LaneState L;
     L.done = true;
 
@@ -345,8 +318,6 @@ __global__ __launch_bounds__(FB ? 256 : 1024) void iter_spec_burst_kernel(BatchD
       if (p > len) { finish(sp, slm, true); return; }
       lane_start(L, f, base, len, p);
       at0 = at = p;
-      hib = 0;
-      fc = NONE;
       cutpos = (c1 > p && c1 - 1 <= len) ? c1 - 1 : NONE;
       searching = true;
     };
@@ -372,7 +343,7 @@ __global__ __launch_bounds__(FB ? 256 : 1024) void iter_spec_burst_kernel(BatchD
         uint64_t lim = (((uintptr_t)(base + at) & ~(uintptr_t)15) + 128) - (uintptr_t)base;
         lim = min(lim, len);
         if (cutpos != NONE) lim = min(lim, cutpos);
-        if (f.all) fwd_window_all<FB>(L, f, lds, base, at, lim, hib, fc, at0);
+        if (f.all) fwd_window_all(L, f, lds, base, at, lim);
         else fwd_range<MODE_FIND>(L, f, lds, base, at, lim);
         at = lim;
       }
@@ -384,11 +355,7 @@ __global__ __launch_bounds__(FB ? 256 : 1024) void iter_spec_burst_kernel(BatchD
       const uint64_t me = L.last;
       uint64_t ms = at0;
       if (me != at0) {  // exec.rs:647
-        // the scan died before the end over ASCII bytes: the match starts at
-        // the first F byte (first_byte_rule), else the reverse scan finds it
-        uint64_t rs = FB && L.done && !(hib & 0x80808080u) && fc < me ? fc : NONE;
-        if (rs == NONE)
-          rs = r.all ? rev_scan_all(r, rlds, base, len, at0, me) : rev_scan(r, rlds, base, len, at0, me);
+        const uint64_t rs = r.all ? rev_scan_all(r, rlds, base, len, at0, me) : rev_scan(r, rlds, base, len, at0, me);
         if (rs == QUITMARK) { quit = true; finish(sp, slm, false); continue; }
         if (rs == NONE) { finish(sp, slm, true); continue; }
         ms = rs;
@@ -1384,8 +1351,7 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
       if ((e = hipMemsetAsync(counts + nunits, 0, 4, st)) != hipSuccess) break;
       if ((e = hipMemsetAsync(qlen, 0, 16, st)) != hipSuccess) break;  // qlen, dirty
       const size_t lb = iter_lds_bytes(*f, r);
-      if ((e = allow_lds(iter_spec_kernel, lb)) != hipSuccess || (e = allow_lds(iter_spec_burst_kernel<false>, lb)) != hipSuccess ||
-          (e = allow_lds(iter_spec_burst_kernel<true>, lb)) != hipSuccess || (e = allow_lds(iter_fix_kernel, lb)) != hipSuccess ||
+      if ((e = allow_lds(iter_spec_kernel, lb)) != hipSuccess || (e = allow_lds(iter_spec_burst_kernel, lb)) != hipSuccess || (e = allow_lds(iter_fix_kernel, lb)) != hipSuccess ||
           (e = allow_lds(iter_emit_kernel, lb)) != hipSuccess)
         break;
       // Literal engine: where the DFA does not fit LDS exactly (> 255 states,
@@ -1428,13 +1394,8 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
           hipLaunchKernelGGL((iter_spec_lit_kernel<false, false>), lg, dim3(bs), kLitImage, st, b, g, nunits, *f,
                              units, slots, counts, dirty);
       } else if (!getenv("RURE_AMD_ITER_NESTED")) {
-        // first-byte start rule (host first_byte_rule) on the all-in-LDS tables
-        if (f->fb_n && f->all && bs <= 256)
-          hipLaunchKernelGGL(iter_spec_burst_kernel<true>, dim3(grid), dim3(bs), iter_lds_bytes(*f, r), st, b, g, nunits,
-                             *f, r, units, slots, counts, dirty);
-        else
-          hipLaunchKernelGGL(iter_spec_burst_kernel<false>, dim3(grid), dim3(bs), iter_lds_bytes(*f, r), st, b, g, nunits,
-                             *f, r, units, slots, counts, dirty);
+        hipLaunchKernelGGL(iter_spec_burst_kernel, dim3(grid), dim3(bs), iter_lds_bytes(*f, r), st, b, g, nunits, *f,
+                           r, units, slots, counts, dirty);
       } else {
         hipLaunchKernelGGL(iter_spec_kernel, dim3(grid), dim3(bs), iter_lds_bytes(*f, r), st, b, g, nunits, *f, r,
                            units, slots, counts, dirty);
