@@ -522,6 +522,16 @@ class Regex(object):
         n = N.rure_amd_first_byte_export(self._re, buf)
         return bytes(buf[:n]) if n > 0 else None
 
+    def lex_table(self):
+        """The find_iter lexer table ((rows, 264) uint16, see rure_amd.h), or None."""
+        import numpy as np
+        n = N.rure_amd_lex_export(self._re, None, 0)
+        if n <= 0:
+            return None
+        t = np.zeros(n, dtype=np.uint16)
+        N.rure_amd_lex_export(self._re, t.ctypes.data, n)
+        return t.reshape(-1, 264)
+
     def program(self, which):
         """Compiled byte program (0 fwd DFA, 1 reverse DFA, 2 NFA): (info, insts)."""
         return _export(N.rure_amd_program_export, self._re, which)

@@ -68,7 +68,19 @@ struct FwdDfaDev {
   // first of those bytes at or after p, so the start needs no reverse scan.
   uint32_t fb_n;
   uint32_t fb_rep[4];
+  // find_iter DFA only: the lexer table (lex_bytes = 0: none; host build_lex).
+  // When the first-byte start rule holds and every match-flag state is
+  // terminal (all transitions dead), the iteration itself is a DFA: entering
+  // a match state at byte x ends the search there and the next one starts at
+  // x, so that transition is replaced by the start state's on the same byte.
+  // u16 entries, rows of kLexPitch entries: entry = row offset of the next
+  // state (in entries, a multiple of 8) | kLexEmit (a match ended at this
+  // byte) | kLexZ (the next state is the start state: the next byte may begin
+  // the search's first match).  lex_s0 = the start state's row offset.
+  const uint16_t *lex_image;
+  uint32_t lex_bytes, lex_s0;
 };
+constexpr uint32_t kLexPitch = 264, kLexEmit = 1, kLexZ = 2;
 
 // Literal engine image layout (at most kLitMax literals of kLitLen bytes).
 constexpr uint32_t kLitMax = 64, kLitLen = 32;

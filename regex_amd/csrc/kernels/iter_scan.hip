@@ -47,6 +47,8 @@ enum : uint32_t {
   U_FIXED = 4,        // final entry differs from the speculative one
   U_QUIT = 8,         // a search quit (cannot happen on the chunked path)
   U_COPY = 16,        // fixed, and its matches are slots[skip, skip + count)
+  U_LEX_TAIL = 32,    // iter_spec_lex_tile_kernel: exit = the lexer's state at c1 - 1, the tail pass finishes
+  U_LEX_REDO = 64,    // iter_spec_lex_tile_kernel: the tail pass iterates the whole unit
 };
 
 struct IterSt {
@@ -784,6 +786,183 @@ __global__ __launch_bounds__(256) void iter_spec_sa_tile_kernel(BatchDev b, Geo 
   }
 }
 
+// Pass 1 with the lexer table (FwdDfaDev::lex_image, host build_lex), for
+// patterns whose matches all end in terminal states and start at the first
+// byte of F (the regex-dna strip pattern `>[^\n]*\n|\n`): the iteration is a
+// DFA walk with no reverse scans and no restarts — a byte whose transition
+// would enter a match state instead enters the start state's successor on
+// that byte, flagged kLexEmit.  Per byte the chain is a mask, an add and one
+// LDS u16 read; the entry's two flag bits go into a 32-bit word per 16-byte
+// block (EMIT = a match [start, x) ended at byte x; Z = the next state is the
+// start state).  A match's start is the last position before it where the
+// state before the byte was the start state or a match had just ended
+// (first-byte rule), read off those words.  Coalesced tiles as in
+// iter_spec_sa_tile_kernel.  The lexer covers [c0, c1 - 1); from there
+// iter_lex_tail_kernel's generic cut-bounded iteration (UnitIter) finishes
+// the search in progress at the cut, and iterates whole units that hold a
+// byte >= 0x80 (the first-byte rule is proven for ASCII) and ragged last
+// units (a separate pass keeps this kernel's registers to its byte loop).
+// Together: the unit records of iter_spec_burst_kernel.
+template <bool LAST>
+__device__ __forceinline__ uint32_t lex16(uint32_t &s, const uint32_t w[4], const uint16_t *tab) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int k = 0; k < (LAST ? 15 : 16); ++k) {
+    const uint32_t e = tab[(s & ~7u) + ((w[k >> 2] >> (8 * (k & 3))) & 0xFF)];
+    m |= (e & 3u) << (2 * k);
+    s = e;
+  }
+  return m;
+}
+
+template <bool LAST>
+__device__ __forceinline__ void lex_events(uint32_t m, uint64_t bp, uint32_t &cz, uint64_t &fc, uint64_t &p,
+                                           uint64_t &lm, uint32_t &n, uint64_t *myslots, uint32_t nslots) {
+  uint32_t E = m & 0x55555555u;
+  // A: positions where the search's first match may begin (the state before
+  // the byte was the start state, or a match ended there); Z of byte k marks
+  // position k + 1
+  const uint32_t A = E | ((m & (LAST ? 0x0AAAAAAAu : 0xAAAAAAAAu)) << 1) | cz;
+  while (E) {
+    const uint32_t j = __builtin_ctz(E);
+    E &= E - 1;
+    const uint32_t below = A & ((1u << j) - 1u);
+    const uint64_t st = below ? bp + ((31 - __builtin_clz(below)) >> 1) : fc;
+    const uint64_t x = bp + (j >> 1);
+    if (n < nslots) *(ulonglong2 *)&myslots[2 * n] = make_ulonglong2(st, x);
+    ++n;
+    p = lm = x;
+  }
+  if (A) fc = bp + ((31 - __builtin_clz(A)) >> 1);
+  cz = (m >> (LAST ? 29 : 31)) & 1u;
+}
+
+__global__ __launch_bounds__(256) void iter_spec_lex_tile_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f,
+                                                                 RevDfaDev r, Unit *units, uint64_t *slots,
+                                                                 uint32_t *counts, uint32_t *dirty) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lex_lds[];
+  __shared__ __attribute__((aligned(16))) uint4 stage[4][64 * 8];
+  for (uint32_t i = threadIdx.x * 16; i < f.lex_bytes; i += blockDim.x * 16)
+    *(uint4 *)(lex_lds + i) = *(const uint4 *)((const uint8_t *)f.lex_image + i);
+  __syncthreads();
+  const uint16_t *tab = (const uint16_t *)lex_lds;
+  const uint64_t C = g.chunk, nk = g.nk;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint4 *buf = stage[w];
+  const int src_h = lane >> 3, src_seg = lane & 7, sw = (lane >> 1) & 7;
+  const uint64_t ngroups = (nunits + 63) / 64, nwaves = (uint64_t)gridDim.x * 4;
+  const bool single = b.count == 1;
+  auto hk = [&](uint64_t uu, uint64_t &h, uint64_t &k) {
+    if (single) { h = 0; k = uu; } else { h = uu / nk; k = uu - h * nk; }
+  };
+  for (uint64_t gi = (uint64_t)blockIdx.x * 4 + w; gi < ngroups; gi += nwaves) {
+    const uint64_t u = gi * 64 + lane;
+    uint64_t h, k;
+    hk(u, h, k);
+    const bool valid = u < nunits;
+    const bool full = valid && k + 1 < nk;
+    const uint8_t *src[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      uint64_t us = gi * 64 + 8 * j + src_h, hs, ks;
+      hk(us, hs, ks);
+      if (us >= nunits || ks + 1 >= nk) hs = ks = 0;  // absent / ragged units re-read unit 0 (full)
+      src[j] = b.hay + hs * b.stride + b.start + ks * C + 16 * src_seg;
+    }
+    const uint8_t *base = b.hay + h * b.stride;
+    const uint64_t len = b.length, c0 = b.start + k * C;
+    const uint64_t c1 = k + 1 == nk ? g.end : c0 + C;
+    uint64_t *myslots = slots + u * g.slots * 2;
+    uint64_t p = c0, lm = NONE, fc = c0;
+    uint32_t n = 0, s = f.lex_s0, cz = 1, hib = 0;
+    uint4 n0, n1, n2, n3, n4, n5, n6, n7;
+#define RURE_LOAD_TILE(a)                                                                                     \
+  n0 = *(const uint4 *)(src[0] + (a)); n1 = *(const uint4 *)(src[1] + (a));                                  \
+  n2 = *(const uint4 *)(src[2] + (a)); n3 = *(const uint4 *)(src[3] + (a));                                  \
+  n4 = *(const uint4 *)(src[4] + (a)); n5 = *(const uint4 *)(src[5] + (a));                                  \
+  n6 = *(const uint4 *)(src[6] + (a)); n7 = *(const uint4 *)(src[7] + (a));
+#define RURE_STAGE(kk, v) buf[(8 * (kk) + src_h) * 8 + (src_seg ^ (((8 * (kk) + src_h) >> 1) & 7))] = (v);
+    RURE_LOAD_TILE(0)
+    for (uint64_t at = 0; at < C; at += 128) {
+      RURE_STAGE(0, n0) RURE_STAGE(1, n1) RURE_STAGE(2, n2) RURE_STAGE(3, n3)
+      RURE_STAGE(4, n4) RURE_STAGE(5, n5) RURE_STAGE(6, n6) RURE_STAGE(7, n7)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const bool last_tile = at + 128 >= C;
+      const uint64_t an = last_tile ? at : at + 128;
+      RURE_LOAD_TILE(an)
+      if (full) {
+        uint4 cur = buf[lane * 8 + sw];
+#pragma unroll 1
+        for (int m = 0; m < 8; ++m) {
+          const uint4 nx = buf[lane * 8 + ((m + 1 < 8 ? m + 1 : 7) ^ sw)];
+          const uint32_t wd[4] = {cur.x, cur.y, cur.z, cur.w};
+          hib |= cur.x | cur.y | cur.z | cur.w;
+          const uint64_t bp = c0 + at + 16 * m;
+          if (m == 7 && last_tile) {  // the unit's last byte (c1 - 1) is left to the generic path
+            const uint32_t mw = lex16<true>(s, wd, tab);
+            lex_events<true>(mw, bp, cz, fc, p, lm, n, myslots, g.slots);
+          } else {
+            const uint32_t mw = lex16<false>(s, wd, tab);
+            lex_events<false>(mw, bp, cz, fc, p, lm, n, myslots, g.slots);
+          }
+          cur = nx;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+#undef RURE_LOAD_TILE
+#undef RURE_STAGE
+    if (!valid) continue;
+    (void)base;
+    (void)len;
+    (void)c1;
+    Unit U;
+    U.entry = {c0, NONE};
+    U.exit = {p, lm};
+    U.spec_exit = U.exit;
+    U.spec_count = n;
+    U.flags = (!full || (hib & 0x80808080u)) ? U_LEX_REDO : U_LEX_TAIL;
+    U.skip = U.pad = 0;
+    units[u] = U;
+  }
+}
+
+// The lexer pass's tail: per unit, the generic cut-bounded iteration from the
+// state the lexer left at c1 - 1 (or from c0 for U_LEX_REDO units), appending
+// to the unit's slots; writes the final speculative record.
+__global__ __launch_bounds__(256) void iter_lex_tail_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f,
+                                                            RevDfaDev r, Unit *units, uint64_t *slots,
+                                                            uint32_t *counts, uint32_t *dirty) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const uint8_t *rlds = stage_tables(f, r, lds);
+  for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < nunits; u += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t h, len, c0, c1;
+    const uint8_t *base;
+    unit_bounds(b, g, u, &h, &base, &len, &c0, &c1);
+    Unit U = units[u];
+    const bool redo = (U.flags & U_LEX_REDO) != 0;
+    uint32_t n = redo ? 0 : U.spec_count;
+    UnitIter it;
+    it.init(redo ? IterSt{c0, NONE} : U.exit, c1);
+    uint64_t ms, me;
+    while (it.next(f, r, lds, rlds, base, len, &ms, &me)) {
+      if (n < g.slots) *(ulonglong2 *)&slots[(u * g.slots + n) * 2] = make_ulonglong2(ms, me);
+      ++n;
+    }
+    U.exit = it.exit;
+    U.spec_exit = it.exit;
+    U.spec_count = n;
+    U.flags = (it.clean ? (U_SPEC_CLEAN | U_CLEAN) : 0) | (it.quit ? U_QUIT : 0);
+    units[u] = U;
+    counts[u] = n;
+    if (!(U.flags & U_SPEC_CLEAN)) atomicOr(dirty, 1u);  // the fix pass has work
+  }
+}
+
 // Where the true iteration of unit j, entered with E, joins the speculative
 // one S (started fresh at c0), read off S's recorded matches: S's state
 // before it yielded match i is (p_i, lm_i) (p_0 = c0, lm_0 = none; then the
@@ -1366,7 +1545,20 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
       const bool use_sa = f->sa_len && !(sa_env && sa_env[0] == '0') && !(lit_env && lit_env[0] == '1');
       const bool sa_tile = !b.offs && g.nk >= 2 && (g.chunk % 128) == 0 && (b.count == 1 || (b.stride % 16) == 0) &&
                            (((uintptr_t)(b.hay + b.start)) & 15) == 0 && !(sa_env && sa_env[0] == '2');
-      if (use_sa && sa_tile) {
+      // Lexer engine (terminal matches + first-byte rule); RURE_AMD_LEX=0 disables
+      const char *lex_env = getenv("RURE_AMD_LEX");
+      const bool use_lex = f->lex_bytes && !(lex_env && lex_env[0] == '0') && !b.offs && g.nk >= 2 &&
+                           (g.chunk % 128) == 0 && (b.count == 1 || (b.stride % 16) == 0) &&
+                           (((uintptr_t)(b.hay + b.start)) & 15) == 0;
+      if (use_lex) {
+        if ((e = allow_lds(iter_spec_lex_tile_kernel, f->lex_bytes)) != hipSuccess) break;
+        hipLaunchKernelGGL(iter_spec_lex_tile_kernel, dim3(grid_cap((nunits + 63) / 64, 4, cus, 4)), dim3(256),
+                           f->lex_bytes, st, b, g, nunits, *f, r, units, slots, counts, dirty);
+        if ((e = hipGetLastError()) != hipSuccess) break;
+        if ((e = allow_lds(iter_lex_tail_kernel, lb)) != hipSuccess) break;
+        hipLaunchKernelGGL(iter_lex_tail_kernel, dim3(grid_cap(nunits, 256, cus, 8)), dim3(256), lb, st, b, g, nunits,
+                           *f, r, units, slots, counts, dirty);
+      } else if (use_sa && sa_tile) {
         const dim3 sg(grid_cap((nunits + 63) / 64, 4, cus, 4));
         if (f->sa_bits <= 32)
           hipLaunchKernelGGL((iter_spec_sa_tile_kernel<uint32_t>), sg, dim3(256), 0, st, b, g, nunits, *f, units,

@@ -424,6 +424,8 @@ struct rure {
   bool lit_ok = false;      // the regex is a finite string set (literal find_iter engine)
   uint32_t fb_n = 0;        // first-byte start rule (first_byte_rule): |F| or 0
   uint8_t fb_bytes[4] = {0, 0, 0, 0};
+  std::vector<uint16_t> lex;  // lexer table (build_lex), empty if none
+  uint32_t lex_s0 = 0;
   LiteralSet lits;
   std::map<int, std::pair<void *, FwdDfaDev>> iter_dev;
 };
@@ -807,6 +809,70 @@ static uint32_t first_byte_rule(const DenseDfa &d, uint32_t ustart1, bool nonemp
   return nf;
 }
 
+// The lexer table of FwdDfaDev::lex_image (iter_spec_lex_tile_kernel).
+// Needs the first-byte start rule (a match's start is the first F byte of its
+// search on ASCII text) and terminal match states: every state carrying the
+// (one-byte delayed) match flag has only dead transitions, so entering one at
+// byte x ends the search with the match [start, x), and the iteration's next
+// search begins at x with the start state S0 (re_trait.rs:197-221; the regex
+// is nonempty).  The table composes the two: the transition into a match
+// state on byte b becomes S0's transition on b, marked kLexEmit; rows exist
+// for the states reachable from S0 that way plus a twin per restart target
+// (same row; entering a twin = a match ended).  Entries are row offsets so the
+// kernel's chain is one mask, one add and one LDS read per byte.
+static bool build_lex(const DenseDfa &d, uint32_t ustart1, uint32_t fb_n, std::vector<uint16_t> *img,
+                      uint32_t *s0_off) {
+  img->clear();
+  if (!fb_n || !ustart1 || d.quit >= 0) return false;
+  const uint32_t s0 = ustart1 - 1;
+  for (int m = d.n_normal; m < d.n_match_end; ++m)
+    for (int c = 0; c < 256; ++c)
+      if ((int)d.trans[(size_t)m * 256 + c] != d.dead) return false;
+  auto is_match = [&](uint32_t t) { return (int)t >= d.n_normal && (int)t < d.n_match_end; };
+  // plain rows: states reachable from S0 (match transitions replaced by restarts)
+  std::vector<int> plain(d.nstates, -1), twin(d.nstates, -1);
+  std::vector<uint32_t> order, todo{s0};
+  plain[s0] = 0;
+  order.push_back(s0);
+  while (!todo.empty()) {
+    const uint32_t q = todo.back();
+    todo.pop_back();
+    for (int c = 0; c < 256; ++c) {
+      uint32_t t = d.trans[(size_t)q * 256 + c];
+      if (is_match(t)) t = d.trans[(size_t)s0 * 256 + c];
+      if (is_match(t)) return false;  // S0 itself matching on one byte: an empty match
+      if (plain[t] < 0) { plain[t] = (int)order.size(); order.push_back(t); todo.push_back(t); }
+    }
+  }
+  const uint32_t nplain = (uint32_t)order.size();
+  std::vector<uint32_t> twins;
+  for (int c = 0; c < 256; ++c) {
+    const uint32_t t = d.trans[(size_t)s0 * 256 + c];
+    if (twin[t] < 0) { twin[t] = (int)(nplain + twins.size()); twins.push_back(t); }
+  }
+  const uint32_t rows = nplain + (uint32_t)twins.size();
+  if ((uint64_t)rows * kLexPitch >= 65536) return false;
+  img->assign((size_t)rows * kLexPitch, 0);
+  auto row_entries = [&](uint32_t q, uint16_t *out) {
+    for (int c = 0; c < 256; ++c) {
+      uint32_t t = d.trans[(size_t)q * 256 + c];
+      uint32_t e;
+      if (is_match(t)) {
+        t = d.trans[(size_t)s0 * 256 + c];
+        e = (uint32_t)twin[t] * kLexPitch | kLexEmit;
+      } else {
+        e = (uint32_t)plain[t] * kLexPitch;
+      }
+      if (t == s0) e |= kLexZ;
+      out[c] = (uint16_t)e;
+    }
+  };
+  for (uint32_t i = 0; i < nplain; ++i) row_entries(order[i], img->data() + (size_t)i * kLexPitch);
+  for (uint32_t i = 0; i < twins.size(); ++i) row_entries(twins[i], img->data() + (size_t)(nplain + i) * kLexPitch);
+  *s0_off = 0;  // plain[s0] == 0
+  return true;
+}
+
 bool build_iter_dfa(rure *re) {
   if (!build_regex_dfas(re)) return false;
   std::lock_guard<std::mutex> g(re->mu);
@@ -819,6 +885,7 @@ bool build_iter_dfa(rure *re) {
     re->lit_ok = extract_literals(re->nfa, kLitMax, kLitLen, &re->lits);
     if (re->iter_ok)
       re->fb_n = first_byte_rule(re->dfwd_iter, re->pf_iter.ustart1, !can_match_empty(re->nfa), re->fb_bytes);
+    if (re->iter_ok) build_lex(re->dfwd_iter, re->pf_iter.ustart1, re->fb_n, &re->lex, &re->lex_s0);
   }
   return re->iter_ok;
 }
@@ -923,6 +990,7 @@ const FwdDfaDev *iter_device(rure *re, const DevTables &t, std::string *err) {
   uint32_t sa_len = 0, sa_bits = 0;
   if (re->lit_ok) build_shiftand(re->lits, &sa_img, &sa_init, &sa_final, &sa_len, &sa_bits);
   size_t o_sa = sa_img.empty() ? 0 : b.add(sa_img.data(), sa_img.size() * 8);
+  size_t o_lex = re->lex.empty() ? 0 : b.add(re->lex.data(), re->lex.size() * 2);
   DevTables tmp;
   if (!upload_blob(b, &tmp, err)) return nullptr;
   uint8_t *base = (uint8_t *)tmp.blob;
@@ -955,6 +1023,11 @@ const FwdDfaDev *iter_device(rure *re, const DevTables &t, std::string *err) {
     f.lit_minlen = (uint32_t)re->lits.minlen;
     f.lit_maxlen = (uint32_t)re->lits.maxlen;
     f.lit_k8 = re->lits.minlen >= 8 ? 1 : 0;
+  }
+  if (!re->lex.empty()) {
+    f.lex_image = (const uint16_t *)(base + o_lex);
+    f.lex_bytes = (uint32_t)(re->lex.size() * 2);
+    f.lex_s0 = re->lex_s0;
   }
   if (!sa_img.empty()) {
     f.sa_image = (const uint64_t *)(base + o_sa);
@@ -1905,6 +1978,13 @@ int rure_amd_set_core_export(rure_set *rs, rure_amd_core_info *info, uint8_t *ld
   if (eof) memcpy(eof, cs.eof.data(), cs.eof.size() * 8);
   if (start) memcpy(start, cs.start, 256);
   return RURE_AMD_OK;
+}
+
+int64_t rure_amd_lex_export(rure *re, uint16_t *table, size_t cap) {
+  if (!re) return RURE_AMD_ERR_ARG;
+  if (!build_iter_dfa(re)) return RURE_AMD_ERR_DFA;
+  if (table) memcpy(table, re->lex.data(), std::min(cap, re->lex.size()) * 2);
+  return (int64_t)re->lex.size();
 }
 
 int rure_amd_first_byte_export(rure *re, uint8_t *bytes) {

@@ -132,3 +132,44 @@ def test_find_iter_first_byte_rule(cuda, pat, nonascii):
     counts, m = re.find_iter_batch(to_dev(text + b"\0" * 16, cuda), stride=len(text), length=len(text), count=1)
     assert int(counts[0]) == len(exp)
     assert as_pairs(m) == exp
+
+
+LEX_PATTERNS = [r">[^\n]*\n|\n", r"\n", r"a[^b]*b", r"(?-u)>[^\n]*\n|\n", r'"[^"]*"', r"<[^>]*>"]
+
+
+def _lex_text(seed, n, nonascii):
+    rng = random.Random(seed)
+    alpha = [b"a", b"b", b"c", b"g", b"t", b"\n", b">", b'"', b"<", b" "] + ([b"\xc3\xa9", b"\xff"] if nonascii else [])
+    w = [6, 2, 3, 20, 20, 2, 1, 1, 1, 3] + ([0.02, 0.02] if nonascii else [])
+    return b"".join(rng.choices(alpha, weights=w, k=n))
+
+
+@pytest.mark.parametrize("pat", LEX_PATTERNS)
+@pytest.mark.parametrize("nonascii", [False, True])
+def test_find_iter_lexer(cuda, pat, nonascii):
+    """The lexer engine (iter_spec_lex_tile_kernel + tail pass) against the
+    oracle and against the burst kernel (RURE_AMD_LEX=0): one long haystack
+    (many units) and a fixed-stride batch of several haystacks."""
+    import os
+    re = R.Regex(pat)
+    assert re.lex_table() is not None
+    o = OracleRegex(re)
+    text = _lex_text(zlib.crc32(pat.encode()), 400000, nonascii)
+    d = to_dev(text + b"\0" * 16, cuda)
+    exp = o.find_iter(text)
+    counts, m = re.find_iter_batch(d, stride=len(text), length=len(text), count=1)
+    assert as_pairs(m) == exp
+    os.environ["RURE_AMD_LEX"] = "0"
+    try:
+        _, m0 = re.find_iter_batch(d, stride=len(text), length=len(text), count=1)
+    finally:
+        del os.environ["RURE_AMD_LEX"]
+    assert as_pairs(m0) == exp
+    n, L = 6, 60000
+    counts, m = re.find_iter_batch(d, stride=L, length=L - 5, count=n)
+    got, k = as_pairs(m), 0
+    for i in range(n):
+        e = o.find_iter(text[i * L:i * L + L - 5])
+        assert got[k:k + len(e)] == e, (pat, i)
+        k += len(e)
+    assert k == len(got)

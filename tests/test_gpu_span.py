@@ -14,7 +14,7 @@ from regex_amd.dist import find_iter_spans_local, span_bounds
 
 pytestmark = pytest.mark.gpu
 
-CHUNK = [r"\w+", r"a+", r"x*", r"(?s).", r">[^\n]*\n|\n", r"[a-q][^u-z]{13}x", r"agggtaaa|tttaccct", r""]
+CHUNK = [r"\w+", r"a+", r"x*", r"(?s).", r">[^\n]*\n|\n", r"\n", r'"[^"]*"', r"[a-q][^u-z]{13}x", r"agggtaaa|tttaccct", r""]
 WAVE = [r"\b\w+\b", r"(?m)^\w+$", r"\bthe\b", r"\B"]
 
 
