@@ -47,8 +47,7 @@ enum : uint32_t {
   U_FIXED = 4,        // final entry differs from the speculative one
   U_QUIT = 8,         // a search quit (cannot happen on the chunked path)
   U_COPY = 16,        // fixed, and its matches are slots[skip, skip + count)
-  U_LEX_TAIL = 32,    // iter_spec_lex_tile_kernel: exit = the lexer's state at c1 - 1, the tail pass finishes
-  U_LEX_REDO = 64,    // iter_spec_lex_tile_kernel: the tail pass iterates the whole unit
+  U_LEX_TAIL = 32,    // iter_spec_lex_tile_kernel: exit = the lexer's iteration state, the tail pass finishes
 };
 
 struct IterSt {
@@ -799,30 +798,39 @@ __global__ __launch_bounds__(256) void iter_spec_sa_tile_kernel(BatchDev b, Geo 
 // (first-byte rule), read off those words.  Coalesced tiles as in
 // iter_spec_sa_tile_kernel.  The lexer covers [c0, c1 - 1); from there
 // iter_lex_tail_kernel's generic cut-bounded iteration (UnitIter) finishes
-// the search in progress at the cut, and iterates whole units that hold a
-// byte >= 0x80 (the first-byte rule is proven for ASCII) and ragged last
-// units (a separate pass keeps this kernel's registers to its byte loop).
-// Together: the unit records of iter_spec_burst_kernel.
-template <bool LAST>
-__device__ __forceinline__ uint32_t lex16(uint32_t &s, const uint32_t w[4], const uint16_t *tab) {
+// the search in progress at the cut or at the end of the text, and a unit's
+// rest from its last match before a block holding a byte >= 0x80 (the
+// first-byte rule is proven for ASCII); a separate pass keeps this kernel's
+// registers to its byte loop.  Ragged last units run in the tile loop with
+// their loads clamped to the batch.  Together: the unit records of
+// iter_spec_burst_kernel.
+// 16 lexer steps; FULL = false: only bytes [0, kend) (kend < 16), the rest
+// leave s unchanged and add no flags.
+template <bool FULL>
+__device__ __forceinline__ uint32_t lex16(uint32_t &s, const uint32_t w[4], const uint16_t *tab, uint32_t kend) {
   uint32_t m = 0;
 #pragma unroll
-  for (int k = 0; k < (LAST ? 15 : 16); ++k) {
+  for (uint32_t k = 0; k < 16; ++k) {
     const uint32_t e = tab[(s & ~7u) + ((w[k >> 2] >> (8 * (k & 3))) & 0xFF)];
-    m |= (e & 3u) << (2 * k);
-    s = e;
+    if (FULL || k < kend) {
+      m |= (e & 3u) << (2 * k);
+      s = e;
+    }
   }
   return m;
 }
 
-template <bool LAST>
-__device__ __forceinline__ void lex_events(uint32_t m, uint64_t bp, uint32_t &cz, uint64_t &fc, uint64_t &p,
-                                           uint64_t &lm, uint32_t &n, uint64_t *myslots, uint32_t nslots) {
+// The block's matches: EMIT at byte j = a match ended at bp + j; its start is
+// the last earlier position where the search may have begun its match.
+__device__ __forceinline__ void lex_events(uint32_t m, uint32_t kend, uint64_t bp, uint32_t &cz, uint64_t &fc,
+                                           uint64_t &p, uint64_t &lm, uint32_t &n, uint64_t *myslots,
+                                           uint32_t nslots) {
   uint32_t E = m & 0x55555555u;
   // A: positions where the search's first match may begin (the state before
   // the byte was the start state, or a match ended there); Z of byte k marks
-  // position k + 1
-  const uint32_t A = E | ((m & (LAST ? 0x0AAAAAAAu : 0xAAAAAAAAu)) << 1) | cz;
+  // position k + 1 (bytes 0 .. kend - 2)
+  const uint32_t zmask = kend == 16 ? 0xAAAAAAAAu : (0xAAAAAAAAu & ((1u << (2 * kend - 1)) - 1u));
+  const uint32_t A = E | ((m & zmask) << 1) | cz;
   while (E) {
     const uint32_t j = __builtin_ctz(E);
     E &= E - 1;
@@ -834,12 +842,11 @@ __device__ __forceinline__ void lex_events(uint32_t m, uint64_t bp, uint32_t &cz
     p = lm = x;
   }
   if (A) fc = bp + ((31 - __builtin_clz(A)) >> 1);
-  cz = (m >> (LAST ? 29 : 31)) & 1u;
+  cz = (m >> (2 * kend - 1)) & 1u;
 }
 
 __global__ __launch_bounds__(256) void iter_spec_lex_tile_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f,
-                                                                 RevDfaDev r, Unit *units, uint64_t *slots,
-                                                                 uint32_t *counts, uint32_t *dirty) {
+                                                                 Unit *units, uint64_t *slots, uint32_t *counts) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lex_lds[];
   __shared__ __attribute__((aligned(16))) uint4 stage[4][64 * 8];
   for (uint32_t i = threadIdx.x * 16; i < f.lex_bytes; i += blockDim.x * 16)
@@ -852,6 +859,9 @@ __global__ __launch_bounds__(256) void iter_spec_lex_tile_kernel(BatchDev b, Geo
   const int src_h = lane >> 3, src_seg = lane & 7, sw = (lane >> 1) & 7;
   const uint64_t ngroups = (nunits + 63) / 64, nwaves = (uint64_t)gridDim.x * 4;
   const bool single = b.count == 1;
+  // the last readable 16-byte block of the batch (ragged last units' tiles
+  // are clamped to it; their bytes past the haystack are ignored)
+  const uint8_t *last_blk = b.hay + (b.count - 1) * b.stride + ((b.length + 15) & ~(uint64_t)15) - 16;
   auto hk = [&](uint64_t uu, uint64_t &h, uint64_t &k) {
     if (single) { h = 0; k = uu; } else { h = uu / nk; k = uu - h * nk; }
   };
@@ -860,27 +870,28 @@ __global__ __launch_bounds__(256) void iter_spec_lex_tile_kernel(BatchDev b, Geo
     uint64_t h, k;
     hk(u, h, k);
     const bool valid = u < nunits;
-    const bool full = valid && k + 1 < nk;
     const uint8_t *src[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       uint64_t us = gi * 64 + 8 * j + src_h, hs, ks;
       hk(us, hs, ks);
-      if (us >= nunits || ks + 1 >= nk) hs = ks = 0;  // absent / ragged units re-read unit 0 (full)
+      if (us >= nunits) hs = ks = 0;  // absent units re-read unit 0
       src[j] = b.hay + hs * b.stride + b.start + ks * C + 16 * src_seg;
     }
-    const uint8_t *base = b.hay + h * b.stride;
     const uint64_t len = b.length, c0 = b.start + k * C;
     const uint64_t c1 = k + 1 == nk ? g.end : c0 + C;
+    // the lexer covers [c0, lim): the byte at c1 - 1 (where the search is cut)
+    // and the end of the text are left to the tail pass
+    const uint64_t lim = valid ? min(c1 - 1, len) : c0;
     uint64_t *myslots = slots + u * g.slots * 2;
     uint64_t p = c0, lm = NONE, fc = c0;
-    uint32_t n = 0, s = f.lex_s0, cz = 1, hib = 0;
+    uint32_t n = 0, s = f.lex_s0, cz = 1;
+    bool frozen = false;  // a byte >= 0x80 was seen: the rest is the tail pass's
     uint4 n0, n1, n2, n3, n4, n5, n6, n7;
+#define RURE_LD(j, a) (*(const uint4 *)min(src[j] + (a), last_blk))
 #define RURE_LOAD_TILE(a)                                                                                     \
-  n0 = *(const uint4 *)(src[0] + (a)); n1 = *(const uint4 *)(src[1] + (a));                                  \
-  n2 = *(const uint4 *)(src[2] + (a)); n3 = *(const uint4 *)(src[3] + (a));                                  \
-  n4 = *(const uint4 *)(src[4] + (a)); n5 = *(const uint4 *)(src[5] + (a));                                  \
-  n6 = *(const uint4 *)(src[6] + (a)); n7 = *(const uint4 *)(src[7] + (a));
+  n0 = RURE_LD(0, a); n1 = RURE_LD(1, a); n2 = RURE_LD(2, a); n3 = RURE_LD(3, a);                            \
+  n4 = RURE_LD(4, a); n5 = RURE_LD(5, a); n6 = RURE_LD(6, a); n7 = RURE_LD(7, a);
 #define RURE_STAGE(kk, v) buf[(8 * (kk) + src_h) * 8 + (src_seg ^ (((8 * (kk) + src_h) >> 1) & 7))] = (v);
     RURE_LOAD_TILE(0)
     for (uint64_t at = 0; at < C; at += 128) {
@@ -889,45 +900,56 @@ __global__ __launch_bounds__(256) void iter_spec_lex_tile_kernel(BatchDev b, Geo
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const bool last_tile = at + 128 >= C;
-      const uint64_t an = last_tile ? at : at + 128;
+      const uint64_t an = at + 128 < C ? at + 128 : at;
       RURE_LOAD_TILE(an)
-      if (full) {
-        uint4 cur = buf[lane * 8 + sw];
+      uint4 cur = buf[lane * 8 + sw];
 #pragma unroll 1
-        for (int m = 0; m < 8; ++m) {
-          const uint4 nx = buf[lane * 8 + ((m + 1 < 8 ? m + 1 : 7) ^ sw)];
-          const uint32_t wd[4] = {cur.x, cur.y, cur.z, cur.w};
-          hib |= cur.x | cur.y | cur.z | cur.w;
-          const uint64_t bp = c0 + at + 16 * m;
-          if (m == 7 && last_tile) {  // the unit's last byte (c1 - 1) is left to the generic path
-            const uint32_t mw = lex16<true>(s, wd, tab);
-            lex_events<true>(mw, bp, cz, fc, p, lm, n, myslots, g.slots);
+      for (int m = 0; m < 8; ++m) {
+        const uint4 nx = buf[lane * 8 + ((m + 1 < 8 ? m + 1 : 7) ^ sw)];
+        const uint32_t wd[4] = {cur.x, cur.y, cur.z, cur.w};
+        const uint64_t bp = c0 + at + 16 * m;
+        if (!frozen && bp + 16 <= lim) {
+          if ((cur.x | cur.y | cur.z | cur.w) & 0x80808080u) {
+            frozen = true;
           } else {
-            const uint32_t mw = lex16<false>(s, wd, tab);
-            lex_events<false>(mw, bp, cz, fc, p, lm, n, myslots, g.slots);
+            const uint32_t mw = lex16<true>(s, wd, tab, 16);
+            lex_events(mw, 16, bp, cz, fc, p, lm, n, myslots, g.slots);
           }
-          cur = nx;
+        } else if (!frozen && bp < lim) {  // the unit's last lexer block
+          const uint32_t kend = (uint32_t)(lim - bp);
+          const uint32_t keep = kend >= 4 ? 0xFFFFFFFFu : (1u << (8 * kend)) - 1u;
+          const uint32_t hi8 = (cur.x & (kend >= 4 ? 0xFFFFFFFFu : keep)) |
+                               (kend > 4 ? cur.y & (kend >= 8 ? 0xFFFFFFFFu : (1u << (8 * (kend - 4))) - 1u) : 0u) |
+                               (kend > 8 ? cur.z & (kend >= 12 ? 0xFFFFFFFFu : (1u << (8 * (kend - 8))) - 1u) : 0u) |
+                               (kend > 12 ? cur.w & ((1u << (8 * (kend - 12))) - 1u) : 0u);
+          if (hi8 & 0x80808080u) {
+            frozen = true;
+          } else {
+            const uint32_t mw = lex16<false>(s, wd, tab, kend);
+            lex_events(mw, kend, bp, cz, fc, p, lm, n, myslots, g.slots);
+          }
         }
+        cur = nx;
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+#undef RURE_LD
 #undef RURE_LOAD_TILE
 #undef RURE_STAGE
     if (!valid) continue;
-    (void)base;
-    (void)len;
-    (void)c1;
+    // (clean flags and counts only matter when the tail pass is skipped,
+    // RURE_AMD_LEX_TAIL=0: a diagnostic that leaves the lexer's matches alone)
     Unit U;
     U.entry = {c0, NONE};
     U.exit = {p, lm};
     U.spec_exit = U.exit;
     U.spec_count = n;
-    U.flags = (!full || (hib & 0x80808080u)) ? U_LEX_REDO : U_LEX_TAIL;
+    U.flags = U_LEX_TAIL | U_SPEC_CLEAN | U_CLEAN;
     U.skip = U.pad = 0;
     units[u] = U;
+    counts[u] = n;
   }
 }
 
@@ -944,10 +966,9 @@ __global__ __launch_bounds__(256) void iter_lex_tail_kernel(BatchDev b, Geo g, u
     const uint8_t *base;
     unit_bounds(b, g, u, &h, &base, &len, &c0, &c1);
     Unit U = units[u];
-    const bool redo = (U.flags & U_LEX_REDO) != 0;
-    uint32_t n = redo ? 0 : U.spec_count;
+    uint32_t n = U.spec_count;
     UnitIter it;
-    it.init(redo ? IterSt{c0, NONE} : U.exit, c1);
+    it.init(U.exit, c1);
     uint64_t ms, me;
     while (it.next(f, r, lds, rlds, base, len, &ms, &me)) {
       if (n < g.slots) *(ulonglong2 *)&slots[(u * g.slots + n) * 2] = make_ulonglong2(ms, me);
@@ -1553,10 +1574,11 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
       if (use_lex) {
         if ((e = allow_lds(iter_spec_lex_tile_kernel, f->lex_bytes)) != hipSuccess) break;
         hipLaunchKernelGGL(iter_spec_lex_tile_kernel, dim3(grid_cap((nunits + 63) / 64, 4, cus, 4)), dim3(256),
-                           f->lex_bytes, st, b, g, nunits, *f, r, units, slots, counts, dirty);
+                           f->lex_bytes, st, b, g, nunits, *f, units, slots, counts);
         if ((e = hipGetLastError()) != hipSuccess) break;
         if ((e = allow_lds(iter_lex_tail_kernel, lb)) != hipSuccess) break;
-        hipLaunchKernelGGL(iter_lex_tail_kernel, dim3(grid_cap(nunits, 256, cus, 8)), dim3(256), lb, st, b, g, nunits,
+        if (!(getenv("RURE_AMD_LEX_TAIL") && getenv("RURE_AMD_LEX_TAIL")[0] == '0'))
+          hipLaunchKernelGGL(iter_lex_tail_kernel, dim3(grid_cap(nunits, 256, cus, 8)), dim3(256), lb, st, b, g, nunits,
                            *f, r, units, slots, counts, dirty);
       } else if (use_sa && sa_tile) {
         const dim3 sg(grid_cap((nunits + 63) / 64, 4, cus, 4));

@@ -9,20 +9,21 @@ NONE = None
 
 def lex_walk(tab, t, c0, end):
     """Walk text[c0, end) from the start state as the kernel does, block by
-    block (16-byte blocks aligned to c0 here).  Returns (matches, p, lm,
-    nonascii): the matches whose search ended inside, the iteration state
-    after them, and whether any byte was >= 0x80 (the kernel then redoes the
-    unit with the generic path)."""
+    block (16-byte blocks aligned to c0 here).  A block holding a byte >= 0x80
+    freezes the walk (the kernel leaves the rest to the tail pass).  Returns
+    (matches, p, lm, frozen): the matches whose search ended inside, the
+    iteration state after them, and whether the walk froze."""
     flat = tab.reshape(-1)
     s = 0                  # row offset of S0
     carry_z = 1            # the state before c0 is the start state
     fc = None
     p, lm = c0, NONE
     out = []
-    nonascii = any(b >= 0x80 for b in t[c0:end])
     for bp in range(c0, end, 16):
-        m = 0
         kend = min(16, end - bp)
+        if any(b >= 0x80 for b in t[bp:bp + kend]):
+            return out, p, lm, True
+        m = 0
         for k in range(kend):
             e = int(flat[(s & ~7) + t[bp + k]])
             m |= (e & 3) << (2 * k)
@@ -41,24 +42,17 @@ def lex_walk(tab, t, c0, end):
         if A:
             fc = bp + (A.bit_length() - 1) // 2
         carry_z = (m >> (2 * kend - 1)) & 1
-    return out, p, lm, nonascii
+    return out, p, lm, False
 
 
-def lex_unit(tab, fwd, rev, t, c0, c1, last_unit):
+def lex_unit(tab, fwd, rev, t, c0, c1):
     """One unit's speculative iteration as the kernel computes it: the lexer
-    over [c0, c1 - 1) (full units, ASCII), then the generic cut-bounded
-    iteration from the state it left (the search in progress at the cut);
-    ragged last units and units with non-ASCII bytes run the generic
-    iteration from c0.  Returns (matches, exit, clean)."""
+    over [c0, min(c1 - 1, len)) up to a block holding a byte >= 0x80, then the
+    tail pass's generic cut-bounded iteration from the state it left.
+    Returns (matches, exit, clean)."""
     from iter_sim import UnitIter
-    if last_unit or c1 - 1 <= c0:
-        ms, st = [], (c0, NONE)
-    else:
-        ms, p, lm, nonascii = lex_walk(tab, t, c0, c1 - 1)
-        st = (c0, NONE) if nonascii else (p, lm)
-        if nonascii:
-            ms = []
-    it = UnitIter(fwd, rev, t, st, c1)
+    ms, p, lm, _ = lex_walk(tab, t, c0, max(c0, min(c1 - 1, len(t))))
+    it = UnitIter(fwd, rev, t, (p, lm), c1)
     while True:
         m = it.next()
         if m is None:

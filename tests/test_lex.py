@@ -39,8 +39,8 @@ def test_lex_walk_whole_text(pat):
     o = OracleRegex(re)
     for i in range(4):
         t = ascii_text(zlib.crc32(pat.encode()) + i, 700)
-        ms, p, lm, na = lex_walk(tab, t, 0, len(t))
-        assert not na
+        ms, p, lm, frozen = lex_walk(tab, t, 0, len(t))
+        assert not frozen
         exp = o.find_iter(t)
         # matches ending before the end of the text (the kernel leaves the
         # search in progress at the end to the generic path)
@@ -56,12 +56,12 @@ def test_lex_units_equal_generic(pat, chunk):
     fwd, rev = re.dfa_tables(2), re.dfa_tables(1)
     for i in range(3):
         t = ascii_text(zlib.crc32(pat.encode()) * 7 + i, 900)
-        if i == 2:  # a non-ASCII byte in one unit: that unit runs the generic path
-            t = t[:300] + "é".encode() + t[302:]
+        if i == 2:  # non-ASCII bytes: those units finish with the generic path
+            t = t[:300] + "é".encode() + t[302:500] + b"\xff" + t[501:]
         nk = (len(t) + chunk - 1) // chunk
         for k in range(nk):
-            c0, c1 = k * chunk, (float("inf") if k + 1 == nk else (k + 1) * chunk)
-            got = lex_unit(tab, fwd, rev, t, c0, c1, k + 1 == nk)
+            c0, c1 = k * chunk, (1 << 62 if k + 1 == nk else (k + 1) * chunk)
+            got = lex_unit(tab, fwd, rev, t, c0, c1)
             it = UnitIter(fwd, rev, t, (c0, None), c1)
             ms = []
             while True:
