@@ -279,12 +279,12 @@ int rure_amd_dfa_strip_export(rure *re, uint32_t *strip);
  * find_iter then takes a match's start from the first F byte of its search
  * instead of a reverse scan — else 0; negative on error. */
 int rure_amd_first_byte_export(rure *re, uint8_t *bytes);
-/* The find_iter lexer table (host only; iter_spec_lex_tile_kernel): u16
- * entries, rows of 264 — entry = next row offset | 1 (a match ended at this
- * byte) | 2 (the next state is the search start state); row 0 = the start
- * state.  Returns the number of entries (0: no lexer table), copies at most
- * `cap`. */
-int64_t rure_amd_lex_export(rure *re, uint16_t *table, size_t cap);
+/* The find_iter lexer table (host only; iter_spec_lex_tile_kernel): u8
+ * next-state rows of 304 bytes (256 used); *s0 = the start state's row; rows
+ * above it: its twin, then the other restart twins (entering a twin = a match
+ * ended at that byte).  Returns the table's size in bytes (0: no lexer
+ * table), copies at most `cap`. */
+int64_t rure_amd_lex_export(rure *re, uint8_t *table, size_t cap, uint32_t *s0);
 
 /* Export of the Pike VM closure tables the NFA kernel runs (host only):
  * leaves = 3 u32 per leaf (kind | lo << 8 | hi << 16, closure, slot),

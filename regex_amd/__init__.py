@@ -523,14 +523,16 @@ class Regex(object):
         return bytes(buf[:n]) if n > 0 else None
 
     def lex_table(self):
-        """The find_iter lexer table ((rows, 264) uint16, see rure_amd.h), or None."""
+        """The find_iter lexer table: ((rows, 304) uint8 next states, start
+        row), or None (see rure_amd.h rure_amd_lex_export)."""
         import numpy as np
-        n = N.rure_amd_lex_export(self._re, None, 0)
+        n = N.rure_amd_lex_export(self._re, None, 0, None)
         if n <= 0:
             return None
-        t = np.zeros(n, dtype=np.uint16)
-        N.rure_amd_lex_export(self._re, t.ctypes.data, n)
-        return t.reshape(-1, 264)
+        t = np.zeros(n, dtype=np.uint8)
+        s0 = ctypes.c_uint32()
+        N.rure_amd_lex_export(self._re, t.ctypes.data, n, ctypes.byref(s0))
+        return t.reshape(-1, 304), s0.value
 
     def program(self, which):
         """Compiled byte program (0 fwd DFA, 1 reverse DFA, 2 NFA): (info, insts)."""

@@ -72,15 +72,15 @@ struct FwdDfaDev {
   // When the first-byte start rule holds and every match-flag state is
   // terminal (all transitions dead), the iteration itself is a DFA: entering
   // a match state at byte x ends the search there and the next one starts at
-  // x, so that transition is replaced by the start state's on the same byte.
-  // u16 entries, rows of kLexPitch entries: entry = row offset of the next
-  // state (in entries, a multiple of 8) | kLexEmit (a match ended at this
-  // byte) | kLexZ (the next state is the start state: the next byte may begin
-  // the search's first match).  lex_s0 = the start state's row offset.
-  const uint16_t *lex_image;
+  // x, so that transition goes to a twin of the start state's successor on
+  // the same byte.  u8 rows of kRow bytes; states numbered [others, S0 =
+  // lex_s0, twin(S0), other twins]: clamp(s - (lex_s0 - 1), 0, 3) = the
+  // byte's flags: 1 = the state after it is the start state (Z), 2 = Z and a
+  // match ended at it (EMIT), 3 = EMIT only.
+  const uint8_t *lex_image;
   uint32_t lex_bytes, lex_s0;
 };
-constexpr uint32_t kLexPitch = 264, kLexEmit = 1, kLexZ = 2;
+constexpr uint32_t kLexMaxRows = 24;  // lexer table rows (iter_spec_lex_tile_kernel's static LDS)
 
 // Literal engine image layout (at most kLitMax literals of kLitLen bytes).
 constexpr uint32_t kLitMax = 64, kLitLen = 32;

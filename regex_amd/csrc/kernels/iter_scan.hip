@@ -805,32 +805,37 @@ __global__ __launch_bounds__(256) void iter_spec_sa_tile_kernel(BatchDev b, Geo 
 // their loads clamped to the batch.  Together: the unit records of
 // iter_spec_burst_kernel.
 // 16 lexer steps; FULL = false: only bytes [0, kend) (kend < 16), the rest
-// leave s unchanged and add no flags.
+// leave s unchanged and add no flags.  The chain per byte is one 24-bit
+// multiply-add and one LDS u8 read (as the tile kernel's); the flags come off
+// it: code = clamp(s - zb, 0, 3) (FwdDfaDev::lex_image numbering), two bits
+// per byte of the returned word.
 template <bool FULL>
-__device__ __forceinline__ uint32_t lex16(uint32_t &s, const uint32_t w[4], const uint16_t *tab, uint32_t kend) {
+__device__ __forceinline__ uint32_t lex16(uint32_t &s, const uint32_t w[4], const uint8_t *tab, int32_t zb,
+                                          uint32_t kend) {
   uint32_t m = 0;
 #pragma unroll
   for (uint32_t k = 0; k < 16; ++k) {
-    const uint32_t e = tab[(s & ~7u) + ((w[k >> 2] >> (8 * (k & 3))) & 0xFF)];
+    const uint32_t t = tab[__umul24(s, kRow) + ((w[k >> 2] >> (8 * (k & 3))) & 0xFF)];
     if (FULL || k < kend) {
-      m |= (e & 3u) << (2 * k);
-      s = e;
+      m |= (uint32_t)min(max((int32_t)t - zb, 0), 3) << (2 * k);
+      s = t;
     }
   }
   return m;
 }
 
-// The block's matches: EMIT at byte j = a match ended at bp + j; its start is
-// the last earlier position where the search may have begun its match.
+// The block's matches from its flag word (kend bytes): EMIT at byte j = a
+// match ended at bp + j; its start is the last earlier position where the
+// search may have begun its match (the state before the byte was the start
+// state — Z of the byte before — or a match ended there).
 __device__ __forceinline__ void lex_events(uint32_t m, uint32_t kend, uint64_t bp, uint32_t &cz, uint64_t &fc,
                                            uint64_t &p, uint64_t &lm, uint32_t &n, uint64_t *myslots,
                                            uint32_t nslots) {
-  uint32_t E = m & 0x55555555u;
-  // A: positions where the search's first match may begin (the state before
-  // the byte was the start state, or a match ended there); Z of byte k marks
-  // position k + 1 (bytes 0 .. kend - 2)
-  const uint32_t zmask = kend == 16 ? 0xAAAAAAAAu : (0xAAAAAAAAu & ((1u << (2 * kend - 1)) - 1u));
-  const uint32_t A = E | ((m & zmask) << 1) | cz;
+  uint32_t E = (m >> 1) & 0x55555555u;
+  const uint32_t Z = (m ^ (m >> 1)) & 0x55555555u;
+  const uint32_t zlast = (Z >> (2 * kend - 2)) & 1u;
+  const uint32_t zmask = kend == 16 ? 0xFFFFFFFFu : (1u << (2 * kend - 2)) - 1u;  // Z of bytes 0 .. kend - 2
+  const uint32_t A = E | ((Z & zmask) << 2) | cz;
   while (E) {
     const uint32_t j = __builtin_ctz(E);
     E &= E - 1;
@@ -842,17 +847,19 @@ __device__ __forceinline__ void lex_events(uint32_t m, uint32_t kend, uint64_t b
     p = lm = x;
   }
   if (A) fc = bp + ((31 - __builtin_clz(A)) >> 1);
-  cz = (m >> (2 * kend - 1)) & 1u;
+  cz = zlast;
 }
 
 __global__ __launch_bounds__(256) void iter_spec_lex_tile_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f,
                                                                  Unit *units, uint64_t *slots, uint32_t *counts) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lex_lds[];
+  // the table first in LDS (address 0): the chain's address is one 24-bit
+  // multiply-add; 24 rows + the tile stage = 39 KB, 4 blocks (16 waves) per CU
+  __shared__ __attribute__((aligned(16))) uint8_t tab[kLexMaxRows * kRow];
   __shared__ __attribute__((aligned(16))) uint4 stage[4][64 * 8];
   for (uint32_t i = threadIdx.x * 16; i < f.lex_bytes; i += blockDim.x * 16)
-    *(uint4 *)(lex_lds + i) = *(const uint4 *)((const uint8_t *)f.lex_image + i);
+    *(uint4 *)(tab + i) = *(const uint4 *)(f.lex_image + i);
   __syncthreads();
-  const uint16_t *tab = (const uint16_t *)lex_lds;
+  const int32_t zb = (int32_t)f.lex_s0 - 1;
   const uint64_t C = g.chunk, nk = g.nk;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   uint4 *buf = stage[w];
@@ -902,34 +909,48 @@ __global__ __launch_bounds__(256) void iter_spec_lex_tile_kernel(BatchDev b, Geo
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       const uint64_t an = at + 128 < C ? at + 128 : at;
       RURE_LOAD_TILE(an)
-      uint4 cur = buf[lane * 8 + sw];
-#pragma unroll 1
-      for (int m = 0; m < 8; ++m) {
-        const uint4 nx = buf[lane * 8 + ((m + 1 < 8 ? m + 1 : 7) ^ sw)];
-        const uint32_t wd[4] = {cur.x, cur.y, cur.z, cur.w};
-        const uint64_t bp = c0 + at + 16 * m;
-        if (!frozen && bp + 16 <= lim) {
-          if ((cur.x | cur.y | cur.z | cur.w) & 0x80808080u) {
-            frozen = true;
-          } else {
-            const uint32_t mw = lex16<true>(s, wd, tab, 16);
-            lex_events(mw, 16, bp, cz, fc, p, lm, n, myslots, g.slots);
-          }
-        } else if (!frozen && bp < lim) {  // the unit's last lexer block
-          const uint32_t kend = (uint32_t)(lim - bp);
-          const uint32_t keep = kend >= 4 ? 0xFFFFFFFFu : (1u << (8 * kend)) - 1u;
-          const uint32_t hi8 = (cur.x & (kend >= 4 ? 0xFFFFFFFFu : keep)) |
-                               (kend > 4 ? cur.y & (kend >= 8 ? 0xFFFFFFFFu : (1u << (8 * (kend - 4))) - 1u) : 0u) |
-                               (kend > 8 ? cur.z & (kend >= 12 ? 0xFFFFFFFFu : (1u << (8 * (kend - 8))) - 1u) : 0u) |
-                               (kend > 12 ? cur.w & ((1u << (8 * (kend - 12))) - 1u) : 0u);
-          if (hi8 & 0x80808080u) {
-            frozen = true;
-          } else {
-            const uint32_t mw = lex16<false>(s, wd, tab, kend);
-            lex_events(mw, kend, bp, cz, fc, p, lm, n, myslots, g.slots);
+      // the tile's 8 blocks through the chain first (flag words kept), then
+      // their matches: the event bookkeeping stays off the dependent chain.
+      // Active bytes: [c0 + at, lim) up to the first block with a byte >= 0x80.
+      const uint64_t t0 = c0 + at;
+      const uint32_t span = frozen || lim <= t0 ? 0u : (uint32_t)min<uint64_t>(lim - t0, 128);
+      uint32_t mw[8];
+      uint32_t act = 0;  // bytes of the tile the lexer took
+      if (__builtin_expect(__all(span == 128), 1)) {
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+          const uint4 cur = buf[lane * 8 + (m ^ sw)];
+          const uint32_t wd[4] = {cur.x, cur.y, cur.z, cur.w};
+          const bool hi8 = ((cur.x | cur.y | cur.z | cur.w) & 0x80808080u) != 0;
+          frozen = frozen || hi8;
+          mw[m] = 0;
+          if (!frozen) {
+            mw[m] = lex16<true>(s, wd, tab, zb, 16);
+            act += 16;
           }
         }
-        cur = nx;
+      } else {
+#pragma unroll 1
+        for (int m = 0; m < 8; ++m) {
+          const uint4 cur = buf[lane * 8 + (m ^ sw)];
+          const uint32_t wd[4] = {cur.x, cur.y, cur.z, cur.w};
+          const uint32_t kend = span > 16u * m ? min(span - 16u * m, 16u) : 0u;
+          uint32_t hi8 = 0;
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            hi8 |= wd[q] & (kend >= 4u * q + 4 ? 0xFFFFFFFFu : kend <= 4u * q ? 0u : (1u << (8 * (kend - 4 * q))) - 1u);
+          frozen = frozen || (hi8 & 0x80808080u);
+          mw[m] = 0;
+          if (!frozen && kend) {
+            mw[m] = kend == 16 ? lex16<true>(s, wd, tab, zb, 16) : lex16<false>(s, wd, tab, zb, kend);
+            act += kend;
+          }
+        }
+      }
+#pragma unroll 1
+      for (int m = 0; m < 8 && 16u * m < act; ++m) {
+        const uint32_t kend = min(act - 16u * m, 16u);
+        lex_events(mw[m], kend, t0 + 16 * m, cz, fc, p, lm, n, myslots, g.slots);
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -1572,9 +1593,8 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
                            (g.chunk % 128) == 0 && (b.count == 1 || (b.stride % 16) == 0) &&
                            (((uintptr_t)(b.hay + b.start)) & 15) == 0;
       if (use_lex) {
-        if ((e = allow_lds(iter_spec_lex_tile_kernel, f->lex_bytes)) != hipSuccess) break;
-        hipLaunchKernelGGL(iter_spec_lex_tile_kernel, dim3(grid_cap((nunits + 63) / 64, 4, cus, 4)), dim3(256),
-                           f->lex_bytes, st, b, g, nunits, *f, units, slots, counts);
+        hipLaunchKernelGGL(iter_spec_lex_tile_kernel, dim3(grid_cap((nunits + 63) / 64, 4, cus, 4)), dim3(256), 0,
+                           st, b, g, nunits, *f, units, slots, counts);
         if ((e = hipGetLastError()) != hipSuccess) break;
         if ((e = allow_lds(iter_lex_tail_kernel, lb)) != hipSuccess) break;
         if (!(getenv("RURE_AMD_LEX_TAIL") && getenv("RURE_AMD_LEX_TAIL")[0] == '0'))

@@ -424,7 +424,7 @@ struct rure {
   bool lit_ok = false;      // the regex is a finite string set (literal find_iter engine)
   uint32_t fb_n = 0;        // first-byte start rule (first_byte_rule): |F| or 0
   uint8_t fb_bytes[4] = {0, 0, 0, 0};
-  std::vector<uint16_t> lex;  // lexer table (build_lex), empty if none
+  std::vector<uint8_t> lex;   // lexer table (build_lex), empty if none
   uint32_t lex_s0 = 0;
   LiteralSet lits;
   std::map<int, std::pair<void *, FwdDfaDev>> iter_dev;
@@ -816,12 +816,14 @@ static uint32_t first_byte_rule(const DenseDfa &d, uint32_t ustart1, bool nonemp
 // byte x ends the search with the match [start, x), and the iteration's next
 // search begins at x with the start state S0 (re_trait.rs:197-221; the regex
 // is nonempty).  The table composes the two: the transition into a match
-// state on byte b becomes S0's transition on b, marked kLexEmit; rows exist
-// for the states reachable from S0 that way plus a twin per restart target
-// (same row; entering a twin = a match ended).  Entries are row offsets so the
-// kernel's chain is one mask, one add and one LDS read per byte.
-static bool build_lex(const DenseDfa &d, uint32_t ustart1, uint32_t fb_n, std::vector<uint16_t> *img,
-                      uint32_t *s0_off) {
+// state on byte b becomes S0's transition on b into a *twin* of its target
+// (same row; entering a twin = a match ended here).  u8 state numbers, rows
+// of kRow bytes (the forward kernels' LDS layout), numbered [other states,
+// S0, twin(S0), other twins] so that one clamp of the state number gives the
+// byte's flags (FwdDfaDev::lex_z).  Returns false if the rule does not hold
+// or the states do not fit u8.
+static bool build_lex(const DenseDfa &d, uint32_t ustart1, uint32_t fb_n, std::vector<uint8_t> *img,
+                      uint32_t *s0_idx) {
   img->clear();
   if (!fb_n || !ustart1 || d.quit >= 0) return false;
   const uint32_t s0 = ustart1 - 1;
@@ -829,11 +831,10 @@ static bool build_lex(const DenseDfa &d, uint32_t ustart1, uint32_t fb_n, std::v
     for (int c = 0; c < 256; ++c)
       if ((int)d.trans[(size_t)m * 256 + c] != d.dead) return false;
   auto is_match = [&](uint32_t t) { return (int)t >= d.n_normal && (int)t < d.n_match_end; };
-  // plain rows: states reachable from S0 (match transitions replaced by restarts)
-  std::vector<int> plain(d.nstates, -1), twin(d.nstates, -1);
-  std::vector<uint32_t> order, todo{s0};
-  plain[s0] = 0;
-  order.push_back(s0);
+  // states reachable from S0 (match transitions replaced by restarts)
+  std::vector<uint8_t> reach(d.nstates, 0);
+  std::vector<uint32_t> todo{s0};
+  reach[s0] = 1;
   while (!todo.empty()) {
     const uint32_t q = todo.back();
     todo.pop_back();
@@ -841,35 +842,29 @@ static bool build_lex(const DenseDfa &d, uint32_t ustart1, uint32_t fb_n, std::v
       uint32_t t = d.trans[(size_t)q * 256 + c];
       if (is_match(t)) t = d.trans[(size_t)s0 * 256 + c];
       if (is_match(t)) return false;  // S0 itself matching on one byte: an empty match
-      if (plain[t] < 0) { plain[t] = (int)order.size(); order.push_back(t); todo.push_back(t); }
+      if (!reach[t]) { reach[t] = 1; todo.push_back(t); }
     }
   }
-  const uint32_t nplain = (uint32_t)order.size();
-  std::vector<uint32_t> twins;
+  std::vector<int> plain(d.nstates, -1), twin(d.nstates, -1);
+  std::vector<uint32_t> rows;  // DFA state of each lexer row
+  for (int q = 0; q < d.nstates; ++q)
+    if (reach[q] && (uint32_t)q != s0) { plain[q] = (int)rows.size(); rows.push_back(q); }
+  plain[s0] = (int)rows.size();
+  rows.push_back(s0);
+  twin[s0] = (int)rows.size();
+  rows.push_back(s0);
   for (int c = 0; c < 256; ++c) {
     const uint32_t t = d.trans[(size_t)s0 * 256 + c];
-    if (twin[t] < 0) { twin[t] = (int)(nplain + twins.size()); twins.push_back(t); }
+    if (twin[t] < 0) { twin[t] = (int)rows.size(); rows.push_back(t); }
   }
-  const uint32_t rows = nplain + (uint32_t)twins.size();
-  if ((uint64_t)rows * kLexPitch >= 65536) return false;
-  img->assign((size_t)rows * kLexPitch, 0);
-  auto row_entries = [&](uint32_t q, uint16_t *out) {
+  if (rows.size() > kLexMaxRows || plain[s0] < 1) return false;
+  img->assign(rows.size() * kRow, 0);
+  for (size_t i = 0; i < rows.size(); ++i)
     for (int c = 0; c < 256; ++c) {
-      uint32_t t = d.trans[(size_t)q * 256 + c];
-      uint32_t e;
-      if (is_match(t)) {
-        t = d.trans[(size_t)s0 * 256 + c];
-        e = (uint32_t)twin[t] * kLexPitch | kLexEmit;
-      } else {
-        e = (uint32_t)plain[t] * kLexPitch;
-      }
-      if (t == s0) e |= kLexZ;
-      out[c] = (uint16_t)e;
+      const uint32_t t = d.trans[(size_t)rows[i] * 256 + c];
+      (*img)[i * kRow + c] = (uint8_t)(is_match(t) ? twin[d.trans[(size_t)s0 * 256 + c]] : plain[t]);
     }
-  };
-  for (uint32_t i = 0; i < nplain; ++i) row_entries(order[i], img->data() + (size_t)i * kLexPitch);
-  for (uint32_t i = 0; i < twins.size(); ++i) row_entries(twins[i], img->data() + (size_t)(nplain + i) * kLexPitch);
-  *s0_off = 0;  // plain[s0] == 0
+  *s0_idx = (uint32_t)plain[s0];
   return true;
 }
 
@@ -990,7 +985,7 @@ const FwdDfaDev *iter_device(rure *re, const DevTables &t, std::string *err) {
   uint32_t sa_len = 0, sa_bits = 0;
   if (re->lit_ok) build_shiftand(re->lits, &sa_img, &sa_init, &sa_final, &sa_len, &sa_bits);
   size_t o_sa = sa_img.empty() ? 0 : b.add(sa_img.data(), sa_img.size() * 8);
-  size_t o_lex = re->lex.empty() ? 0 : b.add(re->lex.data(), re->lex.size() * 2);
+  size_t o_lex = re->lex.empty() ? 0 : b.add(re->lex.data(), re->lex.size());
   DevTables tmp;
   if (!upload_blob(b, &tmp, err)) return nullptr;
   uint8_t *base = (uint8_t *)tmp.blob;
@@ -1025,8 +1020,8 @@ const FwdDfaDev *iter_device(rure *re, const DevTables &t, std::string *err) {
     f.lit_k8 = re->lits.minlen >= 8 ? 1 : 0;
   }
   if (!re->lex.empty()) {
-    f.lex_image = (const uint16_t *)(base + o_lex);
-    f.lex_bytes = (uint32_t)(re->lex.size() * 2);
+    f.lex_image = base + o_lex;
+    f.lex_bytes = (uint32_t)re->lex.size();
     f.lex_s0 = re->lex_s0;
   }
   if (!sa_img.empty()) {
@@ -1980,10 +1975,11 @@ int rure_amd_set_core_export(rure_set *rs, rure_amd_core_info *info, uint8_t *ld
   return RURE_AMD_OK;
 }
 
-int64_t rure_amd_lex_export(rure *re, uint16_t *table, size_t cap) {
+int64_t rure_amd_lex_export(rure *re, uint8_t *table, size_t cap, uint32_t *s0) {
   if (!re) return RURE_AMD_ERR_ARG;
   if (!build_iter_dfa(re)) return RURE_AMD_ERR_DFA;
-  if (table) memcpy(table, re->lex.data(), std::min(cap, re->lex.size()) * 2);
+  if (table) memcpy(table, re->lex.data(), std::min(cap, re->lex.size()));
+  if (s0) *s0 = re->lex_s0;
   return (int64_t)re->lex.size();
 }
 

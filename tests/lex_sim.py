@@ -3,19 +3,18 @@ lexer table walk with the per-block flag words, the first-byte start
 positions recovered from them, and the hand-over to the generic cut-bounded
 iteration for a unit's last byte.
 TEST INFRASTRUCTURE: validates the lexer algorithm on CPU."""
-PITCH, EMIT, Z = 264, 1, 2
 NONE = None
 
 
-def lex_walk(tab, t, c0, end):
+def lex_walk(lex, t, c0, end):
     """Walk text[c0, end) from the start state as the kernel does, block by
     block (16-byte blocks aligned to c0 here).  A block holding a byte >= 0x80
     freezes the walk (the kernel leaves the rest to the tail pass).  Returns
     (matches, p, lm, frozen): the matches whose search ended inside, the
     iteration state after them, and whether the walk froze."""
-    flat = tab.reshape(-1)
-    s = 0                  # row offset of S0
-    carry_z = 1            # the state before c0 is the start state
+    tab, s0 = lex
+    s = s0
+    cz = 1                 # the state before c0 is the start state
     fc = None
     p, lm = c0, NONE
     out = []
@@ -25,12 +24,12 @@ def lex_walk(tab, t, c0, end):
             return out, p, lm, True
         m = 0
         for k in range(kend):
-            e = int(flat[(s & ~7) + t[bp + k]])
-            m |= (e & 3) << (2 * k)
-            s = e
-        E = m & 0x55555555
-        zb = m & 0xAAAAAAAA & ((1 << (2 * kend - 1)) - 1)   # Z of bytes 0..kend-2
-        A = E | (zb << 1) | carry_z
+            s = int(tab[s, t[bp + k]])
+            m |= min(max(s - (s0 - 1), 0), 3) << (2 * k)
+        E = (m >> 1) & 0x55555555
+        Z = (m ^ (m >> 1)) & 0x55555555
+        zlast = (Z >> (2 * kend - 2)) & 1
+        A = E | ((Z & ((1 << (2 * kend - 2)) - 1)) << 2) | cz
         while E:
             j = (E & -E).bit_length() - 1
             E &= E - 1
@@ -41,7 +40,7 @@ def lex_walk(tab, t, c0, end):
             p = lm = x
         if A:
             fc = bp + (A.bit_length() - 1) // 2
-        carry_z = (m >> (2 * kend - 1)) & 1
+        cz = zlast
     return out, p, lm, False
 
 
