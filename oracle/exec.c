@@ -5,10 +5,17 @@
  *   is_match_at        427-468   (Dfa arm; Quit -> match_nfa)
  *   find_at            473-514   (Dfa arm; Quit -> find_nfa)
  *   find_dfa_forward   632-662
+ *   find_dfa_anchored_reverse 671-688 and the DfaAnchoredReverse arms of
+ *                      the above (chosen at exec.rs:1175-1177 for regexes
+ *                      anchored at the end but not at the start)
  *   many_matches_at    998-1038  (DfaMany arm; Quit -> exec_nfa)
  * and the iteration rule of src/re_trait.rs:197-221 (Matches::next).
- * Engine choice (literal / DFA / NFA) is result-neutral in the reference
- * (HACKING.md:60-61), so the DFA arms stand for every match type.
+ * Engine choice is result-neutral in the reference (HACKING.md:60-61) except
+ * for DfaAnchoredReverse, which runs the reverse DFA over text[start..] from
+ * the end: the byte before `start` is not visible to it (a match at `start`
+ * of e.g. `\bx$` or `(?m)^x$` is found where the forward DFA's look-behind
+ * rejects it), so that arm is restated as well; the literal arms answer as
+ * the DFA arms.
  */
 #include <pthread.h>
 #include <stdlib.h>
@@ -104,6 +111,27 @@ int orc_captures_nfa(const orc_regex *r, orc_cache *c, const uint8_t *text, size
   return orc_pike_exec(r->nfa, c->pike, m, 1, slots, nslots, 0, text, len, start);
 }
 
+/* exec.rs:1175-1177: a single regex anchored at the end and not at the start
+ * runs the reverse DFA from the end of the text (MatchType::DfaAnchoredReverse;
+ * Literal(AnchoredEnd), chosen before it for complete suffixes, answers the
+ * same: such regexes have no assertions). */
+static int anchored_rev(const orc_regex *r) {
+  return r->rev && r->nfa && r->nfa->nmatches == 1 && !r->nfa->anchored_start && r->nfa->anchored_end;
+}
+
+/* exec.rs:671-688 find_dfa_anchored_reverse (quit_after_match: the
+ * is_match / shortest_match arms, exec.rs:395-406, 442-453) */
+static int find_dfa_anchored_reverse(const orc_regex *r, orc_cache *c, int quit_after_match, const uint8_t *text,
+                                     size_t len, size_t start, size_t *ms, size_t *me) {
+  size_t s, consumed;
+  int k = orc_dfa_reverse(r->rev, c->rev, quit_after_match, text + start, len - start, len - start, &s, &consumed);
+  c->st.rev_bytes += consumed;
+  if (k != R_MATCH) return k;
+  *ms = start + s;
+  *me = len;
+  return R_MATCH;
+}
+
 /* exec.rs:632-662 find_dfa_forward */
 static int find_dfa_forward(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t len, size_t start,
                             size_t *ms, size_t *me) {
@@ -124,7 +152,8 @@ static int find_dfa_forward(const orc_regex *r, orc_cache *c, const uint8_t *tex
 int orc_find_at(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t len, size_t start, size_t *ms,
                 size_t *me) {
   if (start > len) return 0;
-  int k = find_dfa_forward(r, c, text, len, start, ms, me);
+  int k = anchored_rev(r) ? find_dfa_anchored_reverse(r, c, 0, text, len, start, ms, me)
+                          : find_dfa_forward(r, c, text, len, start, ms, me);
   if (k == R_MATCH) return 1;
   if (k == R_NOMATCH) return 0;
   c->st.quits++;
@@ -154,7 +183,8 @@ int orc_captures_at(const orc_regex *r, orc_cache *c, const uint8_t *text, size_
   if (r->nfa->anchored_start) return orc_captures_nfa(r, c, text, len, start, slots, nslots) &&
                                      slots[0] != SIZE_MAX && slots[1] != SIZE_MAX;
   size_t ms, me;
-  int k = find_dfa_forward(r, c, text, len, start, &ms, &me);
+  int k = anchored_rev(r) ? find_dfa_anchored_reverse(r, c, 0, text, len, start, &ms, &me)
+                          : find_dfa_forward(r, c, text, len, start, &ms, &me);
   if (k == R_NOMATCH) return 0;
   size_t n = len;
   if (k == R_MATCH) {
@@ -183,8 +213,14 @@ int orc_shortest_match_at(const orc_regex *r, orc_cache *c, const uint8_t *text,
                           size_t *end) {
   if (start > len) return 0;
   size_t e, stop;
-  int k = orc_dfa_forward(r->fwd, c->fwd, 1, text, len, start, &e, &stop);
-  c->st.fwd_bytes += stop - start;
+  int k;
+  if (anchored_rev(r)) {
+    size_t s;
+    k = find_dfa_anchored_reverse(r, c, 1, text, len, start, &s, &e);
+  } else {
+    k = orc_dfa_forward(r->fwd, c->fwd, 1, text, len, start, &e, &stop);
+    c->st.fwd_bytes += stop - start;
+  }
   if (k == R_MATCH) { *end = e; return 1; }
   if (k == R_NOMATCH) return 0;
   c->st.quits++;
@@ -194,8 +230,14 @@ int orc_shortest_match_at(const orc_regex *r, orc_cache *c, const uint8_t *text,
 int orc_is_match_at(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t len, size_t start) {
   if (start > len) return 0;
   size_t e, stop;
-  int k = orc_dfa_forward(r->fwd, c->fwd, 1, text, len, start, &e, &stop);
-  c->st.fwd_bytes += stop - start;
+  int k;
+  if (anchored_rev(r)) {
+    size_t s;
+    k = find_dfa_anchored_reverse(r, c, 1, text, len, start, &s, &e);
+  } else {
+    k = orc_dfa_forward(r->fwd, c->fwd, 1, text, len, start, &e, &stop);
+    c->st.fwd_bytes += stop - start;
+  }
   if (k == R_MATCH) return 1;
   if (k == R_NOMATCH) return 0;
   c->st.quits++;

@@ -177,6 +177,9 @@ __device__ __forceinline__ void chunk16s(LaneState &L, const FwdDfaDev &f, const
 // or QUITMARK.  Text bytes come from aligned 16-byte loads walked backwards;
 // with `rlds` (the reverse DFA's hot table staged in LDS, same layout as the
 // forward one) ordinary steps stay in LDS.
+// QAM (quit_after_match, dfa.rs:805-812): return at the first match flag
+// (is_match / shortest_match of DfaAnchoredReverse; any match position).
+template <bool QAM = false>
 __device__ __forceinline__ uint64_t rev_scan(const RevDfaDev &r, const uint8_t *rlds, const uint8_t *base,
                                              uint64_t len, uint64_t lo, uint64_t me) {
   uint32_t s = r.ustart1 ? r.ustart1 - 1 : r.start[rev_flag_index(base, lo, len, me)];
@@ -203,9 +206,14 @@ __device__ __forceinline__ uint64_t rev_scan(const RevDfaDev &r, const uint8_t *
         s = r.full[(size_t)s * 256 + b];
       }
       if (s >= r.n_normal) {
-        if (s < r.n_match_end) rs = a + 1;
-        else if (s == r.dead) return rs;
-        else return QUITMARK;
+        if (s < r.n_match_end) {
+          rs = a + 1;
+          if (QAM) return rs;
+        } else if (s == r.dead) {
+          return rs;
+        } else {
+          return QUITMARK;
+        }
       }
     }
   }

@@ -491,6 +491,67 @@ hipError_t launch_set_cores(const BatchDev &b, const SetCoreDev &f, uint64_t *ou
   return hipGetLastError();
 }
 
+static std::atomic<int> g_last_fwd_path{-1};
+int last_fwd_path() { return g_last_fwd_path.load(); }
+
+// ------------------------------------------------------- anchored reverse
+// MatchType::DfaAnchoredReverse (exec.rs:1175-1177): a regex anchored at the
+// end and not at the start matches only at the end of the text, so the
+// reverse DFA runs from there over text[start..] (find_dfa_anchored_reverse,
+// exec.rs:671-688; quit_after_match for is_match / shortest_match, exec.rs:
+// 395-406, 442-453) and reads O(match) bytes instead of the haystack.  The
+// slice hides the byte before `start` from the reverse DFA's look-behind, as
+// in the reference.  One lane per haystack.
+template <int MODE, bool STRIDED>
+__global__ __launch_bounds__(256) void dfa_anchored_rev_kernel(BatchDev bt, RevDfaDev r, void *out) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  for (uint32_t i = threadIdx.x * 16; i < r.lds_bytes; i += blockDim.x * 16)
+    *(uint4 *)(lds + i) = *(const uint4 *)(r.lds_image + i);
+  __syncthreads();
+  const uint8_t *rlds = r.lds_bytes ? lds : nullptr;
+  const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; h < bt.count; h += nthreads) {
+    const uint8_t *base;
+    uint64_t len;
+    if (STRIDED) {
+      base = bt.hay + h * bt.stride;
+      len = bt.length;
+    } else {
+      const uint64_t o0 = bt.offs[h], o1 = bt.offs[h + 1];
+      base = bt.hay + o0;
+      len = o1 - o0;
+    }
+    const uint64_t rs = bt.start > len ? NONE : rev_scan<MODE != MODE_FIND>(r, rlds, base, len, bt.start, len);
+    if (MODE == MODE_ISMATCH) {
+      ((uint8_t *)out)[h] = rs == QUITMARK ? 2 : (rs != NONE ? 1 : 0);
+    } else if (MODE == MODE_SHORTEST) {
+      ((uint64_t *)out)[h] = rs == QUITMARK ? QUITMARK : (rs != NONE ? len : NONE);
+    } else {
+      ((uint64_t *)out)[2 * h] = rs;
+      ((uint64_t *)out)[2 * h + 1] = rs == QUITMARK ? QUITMARK : (rs != NONE ? len : NONE);
+    }
+  }
+}
+
+template <int MODE>
+static hipError_t launch_anchored_rev_m(const BatchDev &b, const RevDfaDev &r, void *out, hipStream_t st, int grid) {
+  if (b.offs)
+    hipLaunchKernelGGL((dfa_anchored_rev_kernel<MODE, false>), dim3(grid), dim3(256), r.lds_bytes, st, b, r, out);
+  else
+    hipLaunchKernelGGL((dfa_anchored_rev_kernel<MODE, true>), dim3(grid), dim3(256), r.lds_bytes, st, b, r, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_dfa_anchored_rev(int mode, const BatchDev &b, const RevDfaDev &r, void *out, hipStream_t st,
+                                   int grid) {
+  g_last_fwd_path.store(-2);
+  switch (mode) {
+    case MODE_FIND: return launch_anchored_rev_m<MODE_FIND>(b, r, out, st, grid);
+    case MODE_ISMATCH: return launch_anchored_rev_m<MODE_ISMATCH>(b, r, out, st, grid);
+    default: return launch_anchored_rev_m<MODE_SHORTEST>(b, r, out, st, grid);
+  }
+}
+
 // ------------------------------------------------------------------ launch
 template <int MODE, bool STRIDED>
 static hipError_t launch_fwd(const BatchDev &b, const FwdDfaDev &f, const RevDfaDev &r, void *out,
@@ -499,8 +560,6 @@ static hipError_t launch_fwd(const BatchDev &b, const FwdDfaDev &f, const RevDfa
   return hipGetLastError();
 }
 
-static std::atomic<int> g_last_fwd_path{-1};
-int last_fwd_path() { return g_last_fwd_path.load(); }
 
 template <int MODE, int STRIDE>
 static hipError_t launch_tile_s(const BatchDev &b, const FwdDfaDev &f, const RevDfaDev &r, void *out, hipStream_t st,

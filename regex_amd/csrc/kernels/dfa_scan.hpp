@@ -223,9 +223,18 @@ int last_fwd_path();
 // end) of the haystacks whose find result holds a match, first `cap`; *count.
 hipError_t launch_compact_matches(const uint64_t *found, uint64_t n, uint64_t base, uint64_t *rec, uint64_t cap,
                                   uint64_t *count, hipStream_t st);
+// find_iter from the batched find result when a haystack holds at most that
+// match (gather_scan.hip): counts, records, total as launch_find_iter.
+hipError_t launch_find_to_iter(const uint64_t *found, uint64_t n, uint64_t *counts, uint64_t *matches, uint64_t cap,
+                               uint64_t *total, hipStream_t st);
 // dst[i * words + w] = src (u8 0/1 or u64 mask) of haystack i (gather_scan.hip).
 hipError_t launch_mask_column(const uint8_t *s8, const uint64_t *s64, uint64_t n, uint64_t *dst, uint64_t words,
                               uint64_t w, hipStream_t st);
+// MatchType::DfaAnchoredReverse (exec.rs:671-688, 395-406, 442-453): the
+// reverse DFA over text[start..] from its end; same output layout and quit
+// markers as launch_dfa_fwd.
+hipError_t launch_dfa_anchored_rev(int mode, const BatchDev &b, const RevDfaDev &r, void *out, hipStream_t st,
+                                   int grid);
 hipError_t launch_dfa_set(const BatchDev &b, const SetDfaDev &f, uint64_t *out, hipStream_t st, int grid);
 
 }  // namespace rure_amd

@@ -103,7 +103,49 @@ __global__ __launch_bounds__(256) void mask_column_kernel(const uint8_t *s8, con
     dst[i * words + w] = s8 ? (uint64_t)(s8[i] != 0) : s64[i];
 }
 
+// find_iter of a regex whose every match ends at the end of the text
+// (DfaAnchoredReverse): at most the find result (rure_amd.cpp run_find_iter).
+__global__ __launch_bounds__(256) void one_match_counts_kernel(const uint64_t *found, uint64_t n, uint64_t *cnt) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
+    cnt[i] = found[2 * i] != ~(uint64_t)0 ? 1 : 0;
+}
+
+__global__ __launch_bounds__(256) void one_match_write_kernel(const uint64_t *found, uint64_t n, const uint64_t *off,
+                                                              uint64_t *counts, uint64_t *m, uint64_t cap,
+                                                              uint64_t *total) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    const uint64_t c = off[i + 1] - off[i];
+    counts[i] = c;
+    if (c && off[i] < cap) {
+      m[2 * off[i]] = found[2 * i];
+      m[2 * off[i] + 1] = found[2 * i + 1];
+    }
+    if (i + 1 == n) *total = off[n];
+  }
+}
+
 }  // namespace
+
+hipError_t launch_find_to_iter(const uint64_t *found, uint64_t n, uint64_t *counts, uint64_t *matches, uint64_t cap,
+                               uint64_t *total, hipStream_t st) {
+  uint64_t *buf = nullptr;
+  hipError_t e = hipMallocAsync((void **)&buf, (n + 1) * 16, st);
+  if (e != hipSuccess) return e;
+  const uint32_t g = (uint32_t)std::min<uint64_t>((n + 255) / 256 ? (n + 255) / 256 : 1, 8192);
+  e = hipMemsetAsync(buf + n, 0, 8, st);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(one_match_counts_kernel, dim3(g), dim3(256), 0, st, found, n, buf);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = exclusive_scan_u64(buf, buf + n + 1, n + 1, st);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(one_match_write_kernel, dim3(g), dim3(256), 0, st, found, n, buf + n + 1, counts, matches, cap,
+                       total);
+    e = hipGetLastError();
+  }
+  hipError_t e2 = hipFreeAsync(buf, st);
+  return e != hipSuccess ? e : e2;
+}
 
 hipError_t launch_mask_column(const uint8_t *s8, const uint64_t *s64, uint64_t n, uint64_t *dst, uint64_t words,
                               uint64_t w, hipStream_t st) {

@@ -68,6 +68,7 @@ struct DevTables {
   void *core_blob = nullptr;  // re-ranked core tables (adapt_cores)
   bool has_dfa = false;     // the DFA materialised (else: Pike VM only)
   bool quit_possible = false;  // the DFA can quit (Unicode \b): Pike VM fallback pass
+  bool anchored_rev = false;   // MatchType::DfaAnchoredReverse (exec.rs:1175-1177)
   int cus = 256;
 };
 
@@ -666,6 +667,9 @@ DevTables *regex_device(rure *re, std::string *err) {
     t.r.ustart1 = re->pr.ustart1;
     t.f.ustart1 = pf.ustart1;
     t.f.nonempty = can_match_empty(re->nfa) ? 0 : 1;
+    // a regex anchored at the end and not at the start runs the reverse DFA
+    // from the end of the text (exec.rs:1175-1177, 671-688)
+    t.anchored_rev = !re->nfa.anchored_start && re->nfa.anchored_end;
   }
   if (t.quit_possible && !re->nfa_ok) {
     (void)hipFree(t.blob);
@@ -1064,12 +1068,27 @@ bool long_batch(const BatchDev &b, const DevTables &t, uint64_t *chunk) {
   return true;
 }
 
+// The DFA step of find / is_match / shortest_match (the quit marker where the
+// DFA quit): the forward DFA (+ reverse for find), or for DfaAnchoredReverse
+// regexes the reverse DFA from the end of each haystack.  Long haystacks
+// searched from their start take the chunked forward scan for either (the
+// two answer alike at start 0: only the look-behind at `start` differs).
+hipError_t run_dfa_step(int mode, const BatchDev &b, const DevTables &t, void *out, hipStream_t st, int dfa_grid,
+                        const FwdDfaDev *iter) {
+  uint64_t chunk = 0;
+  const bool long_fwd = iter && long_batch(b, t, &chunk);
+  if (t.anchored_rev && !(long_fwd && b.start == 0)) return launch_dfa_anchored_rev(mode, b, t.r, out, st, dfa_grid);
+  if (long_fwd) return launch_long_scan(mode, b, *iter, t.r, chunk, out, st, t.cus);
+  return launch_dfa_fwd(mode, b, t.f, t.r, out, st, dfa_grid);
+}
+
 hipError_t run_regex(int mode, const BatchDev &b, const DevTables &t, void *out, hipStream_t st, int dfa_grid,
                      const FwdDfaDev *iter = nullptr) {
   if (!t.has_dfa) return run_pike(mode, false, b, t, out, st);
   uint64_t chunk = 0;
-  if (iter && long_batch(b, t, &chunk)) return launch_long_scan(mode, b, *iter, t.r, chunk, out, st, t.cus);
-  hipError_t e = launch_dfa_fwd(mode, b, t.f, t.r, out, st, dfa_grid);
+  if (iter && long_batch(b, t, &chunk) && !(t.anchored_rev && b.start != 0))
+    return launch_long_scan(mode, b, *iter, t.r, chunk, out, st, t.cus);
+  hipError_t e = run_dfa_step(mode, b, t, out, st, dfa_grid, nullptr);
   if (e != hipSuccess || !t.quit_possible) return e;
   return run_pike(mode, true, b, t, out, st);
 }
@@ -1143,7 +1162,7 @@ hipError_t run_captures(const BatchDev &b, const DevTables &t, uint64_t *slots, 
   uint64_t *found = nullptr;
   if (!t.n.anchored) {
     if ((e = hipMallocAsync((void **)&found, b.count * 16, st)) != hipSuccess) return e;
-    e = t.has_dfa ? launch_dfa_fwd(MODE_FIND, b, t.f, t.r, found, st, dfa_grid)
+    e = t.has_dfa ? run_dfa_step(MODE_FIND, b, t, found, st, dfa_grid, nullptr)
                   : run_pike(MODE_FIND, false, b, t, found, st);
   }
   const size_t wb = caps_wave_bytes(t.n.nleaves, ns);
@@ -1713,6 +1732,21 @@ namespace {
 // The batched find_iter (re_trait.rs:197-221) on one stream.
 hipError_t run_find_iter(rure *re, DevTables *t, const BatchDev &b, const IterOut &o, hipStream_t st,
                          std::string *err, const IterSpan *sp = nullptr) {
+  // DfaAnchoredReverse regexes match only at the end of the text, so the
+  // iteration (re_trait.rs:197-221) yields at most the first search's match
+  // (the next search starts at the end, where an empty match is the one just
+  // reported or skipped).  Searched from `start` > 0, that first search is
+  // the reverse DFA over text[start..] (its look-behind differs from the
+  // forward scan's); from 0 the chunked path below answers the same.
+  if (!sp && t->anchored_rev && b.start > 0 && b.count) {
+    uint64_t *found = nullptr;
+    hipError_t e = hipMallocAsync((void **)&found, b.count * 16, st);
+    if (e != hipSuccess) return e;
+    e = run_regex(MODE_FIND, b, *t, found, st, grid_for(b.count, t->r.lds_bytes, t->cus));
+    if (e == hipSuccess) e = launch_find_to_iter(found, b.count, o.counts, o.matches, o.cap, o.total, st);
+    hipError_t e2 = hipFreeAsync(found, st);
+    return e != hipSuccess ? e : e2;
+  }
   // Chunked speculative iteration needs a DFA that cannot quit and a pattern
   // without assertions (see iter_scan.hip); otherwise one wave per haystack.
   const FwdDfaDev *fi = nullptr;
