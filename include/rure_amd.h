@@ -119,7 +119,11 @@ const char *rure_error_message(rure_error *err);
  *   bytes [i*stride, i*stride + length)         (fixed stride).
  * The search in every haystack starts at `start` (with look-behind context,
  * like rure_find's `start`, rure.h:186-192).  Offsets in results are relative
- * to the haystack's first byte. */
+ * to the haystack's first byte.
+ * The kernels load whole aligned 16-byte blocks: the buffer must be readable
+ * up to the 16-byte-rounded end of its last haystack (device allocations of
+ * the HIP runtime and torch are); bytes outside a haystack never influence
+ * its results. */
 typedef struct rure_amd_batch {
   const uint8_t *haystack;
   const uint64_t *offsets;

@@ -262,9 +262,9 @@ int orc_many_matches_at(const orc_regex *r, orc_cache *c, const uint8_t *text, s
   return orc_many_matches_nfa(r, c, text, len, start, matches);
 }
 
-int64_t orc_find_iter(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t len, size_t *pairs,
-                      size_t cap) {  /* re_trait.rs:197-221 */
-  size_t last_end = 0;
+int64_t orc_find_iter_at(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t len, size_t start,
+                         size_t *pairs, size_t cap) {  /* re_trait.rs:197-221, the first search at `start` */
+  size_t last_end = start;
   int has_last = 0;
   size_t last_match = 0;
   int64_t count = 0;
@@ -284,6 +284,11 @@ int64_t orc_find_iter(const orc_regex *r, orc_cache *c, const uint8_t *text, siz
     count++;
   }
   return count;
+}
+
+int64_t orc_find_iter(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t len, size_t *pairs,
+                      size_t cap) {
+  return orc_find_iter_at(r, c, text, len, 0, pairs, cap);
 }
 
 /* ---------------------------------------------------------- batch baseline */

@@ -69,6 +69,8 @@ int orc_captures_at(const orc_regex *r, orc_cache *c, const uint8_t *text, size_
 /* re_trait.rs:197-221 find_iter.  Writes up to cap (s,e) pairs; returns the total count. */
 int64_t orc_find_iter(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t len, size_t *pairs,
                       size_t cap);
+int64_t orc_find_iter_at(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t len, size_t start,
+                         size_t *pairs, size_t cap);
 /* exec.rs:998-1038 many_matches_at; matches[nmatches]. */
 int orc_many_matches_at(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t len, size_t start,
                         uint8_t *matches);

@@ -45,6 +45,7 @@ orc_is_match_at = _sig("orc_is_match_at", ctypes.c_int, VP, VP, ctypes.c_char_p,
 orc_captures_nfa = _sig("orc_captures_nfa", ctypes.c_int, VP, VP, ctypes.c_char_p, SZ, SZ, VP, SZ)
 orc_captures_at = _sig("orc_captures_at", ctypes.c_int, VP, VP, ctypes.c_char_p, SZ, SZ, VP, SZ)
 orc_find_iter = _sig("orc_find_iter", ctypes.c_int64, VP, VP, ctypes.c_char_p, SZ, VP, SZ)
+orc_find_iter_at = _sig("orc_find_iter_at", ctypes.c_int64, VP, VP, ctypes.c_char_p, SZ, SZ, VP, SZ)
 orc_many_matches_at = _sig("orc_many_matches_at", ctypes.c_int, VP, VP, ctypes.c_char_p, SZ, SZ, VP)
 orc_many_matches_nfa = _sig("orc_many_matches_nfa", ctypes.c_int, VP, VP, ctypes.c_char_p, SZ, SZ, VP)
 orc_cache_stats = _sig("orc_cache_stats", None, VP, ctypes.POINTER(Stats))
@@ -136,11 +137,12 @@ class OracleRegex(object):
             out.append(None if a == NONE or b == NONE else (a, b))
         return out
 
-    def find_iter(self, text):
+    def find_iter(self, text, start=0):
+        """re_trait.rs:197-221, the first search at `start` (find_at semantics)."""
         cap = 16
         while True:
             buf = np.zeros(2 * cap, dtype=np.uint64)
-            n = orc_find_iter(self._r, self._c, text, len(text), buf.ctypes.data, cap)
+            n = orc_find_iter_at(self._r, self._c, text, len(text), start, buf.ctypes.data, cap)
             if n <= cap:
                 return [(int(buf[2 * i]), int(buf[2 * i + 1])) for i in range(n)]
             cap = n

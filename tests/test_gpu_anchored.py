@@ -62,25 +62,6 @@ def test_anchored_reverse_batch(cuda, pat, start):
         assert (None if int(sho[i]) == -1 else int(sho[i])) == es, (pat, start, t)
 
 
-def _iter_from(o, t, start):
-    """re_trait.rs:197-221 from `start`, over the oracle's find_at."""
-    out, last_end, last_match = [], start, None
-    while last_end <= len(t):
-        m = o.find(t, last_end)
-        if m is None:
-            break
-        s, e = m
-        if s == e:
-            last_end = e + 1
-            if last_match == e:
-                continue
-        else:
-            last_end = e
-        last_match = e
-        out.append(m)
-    return out
-
-
 @pytest.mark.parametrize("pat", [r"\d$", r"(?-u)\bx$", r"x*$", r"$", r"(a|ab)$"])
 @pytest.mark.parametrize("start", [0, 2])
 def test_anchored_reverse_find_iter(cuda, pat, start):
@@ -92,7 +73,7 @@ def test_anchored_reverse_find_iter(cuda, pat, start):
     got = [(int(a), int(b)) for a, b in m.cpu().numpy()]
     k = 0
     for i, t in enumerate(texts):
-        exp = _iter_from(o, t, start)
+        exp = o.find_iter(t, start)
         assert int(counts[i]) == len(exp), (pat, i, t)
         assert got[k:k + len(exp)] == exp, (pat, i, t)
         k += len(exp)

@@ -119,15 +119,11 @@ def test_shiftand_batches_and_start(cuda):
     for pat in (r"Holmes|Watson", r"aa"):
         re = R.Regex(pat)
         o = OracleRegex(re)
-        for start in (1, 777, 100003):
+        # every start, including inside a match of the whole-text iteration
+        straddling = [s + 1 for s, e in o.find_iter(t)[:3] if e - s > 1]
+        for start in [1, 777, 100003] + straddling:
             c, m = re.find_iter_batch(dev(t, cuda), stride=len(t), length=len(t), count=1, start=start)
-            exp = [(s, e) for s, e in o.find_iter(t) if s >= start]
-            # literal patterns have no look-around: iteration from `start` is
-            # the whole-text iteration's matches starting at or after it,
-            # unless a match straddles `start`
-            straddle = [(s, e) for s, e in o.find_iter(t) if s < start < e]
-            if not straddle:
-                assert pairs(m) == exp, (pat, start)
+            assert pairs(m) == o.find_iter(t, start), (pat, start)
 
 
 def test_regexdna_variants_shiftand(cuda):
@@ -141,3 +137,28 @@ def test_regexdna_variants_shiftand(cuda):
         got = pairs(m)
         assert got == OracleRegex(re).find_iter(big), v["re"]
         assert len(got) == 50 * v["count"] + 49 * (len(OracleRegex(re).find_iter(seq * 2)) - 2 * v["count"])
+
+
+@pytest.mark.parametrize("L", [70001, 70003, 4099])
+def test_shiftand_haystack_end(cuda, L, monkeypatch):
+    """Odd-length haystacks followed, inside their stride, by bytes that would
+    complete a match straddling the end: the kernels read whole aligned
+    16-byte blocks (include/rure_amd.h: the buffer must be readable to its
+    16-byte-rounded end) but take no byte past the haystack's end."""
+    import torch
+    n, S = 8, (L + 16 + 15) & ~15
+    rng = random.Random(L)
+    buf = bytearray()
+    for i in range(n):
+        body = bytes(rng.choice(b"acgt") for _ in range(L - 5)) + b"agggt"   # a match cut at the end
+        buf += body + b"aaa" + b"agggtaaa"[: S - L - 3].ljust(S - L - 3, b"a")
+    d = torch.from_numpy(np.frombuffer(bytes(buf), dtype=np.uint8).copy()).to(cuda)
+    re = R.Regex(r"agggtaaa|tttaccct")
+    o = OracleRegex(re)
+    for _ in both_engines(monkeypatch):
+        c, m = re.find_iter_batch(d, stride=S, length=L, count=n)
+        got, k = pairs(m), 0
+        for i in range(n):
+            exp = o.find_iter(bytes(buf[i * S:i * S + L]))
+            assert int(c[i]) == len(exp) and got[k:k + len(exp)] == exp, (L, i)
+            k += len(exp)
