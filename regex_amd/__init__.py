@@ -701,7 +701,8 @@ class RegexSet(object):
 
     def core_tables(self):
         """Core form of a large set's DFA (None if the set uses the byte-row
-        kernel): (info, class map, hot table, gcore, gout, eof, start)."""
+        kernel): (info, class map, hot table, gcore, gout, eof, start,
+        code masks)."""
         import numpy as np
         info = N.CoreInfo()
         if N.rure_amd_set_core_export(self._set, ctypes.byref(info), None, None, None, None, None) != N.OK:
@@ -716,9 +717,12 @@ class RegexSet(object):
                                           gout.ctypes.data, eof.ctypes.data, start.ctypes.data), "set_core_export")
         K, hot = info.K, info.hot
         # rows of K + 1 entries: column K is the identity (the class of the
-        # bytes outside a masked head / tail chunk)
-        hot_tab = lds[256:256 + (hot + 1) * (K + 1) * 2].view(np.uint16).reshape(hot + 1, K + 1)
-        return d, lds[:256].copy(), hot_tab, gcore.reshape(-1, K), gout.reshape(-1, K), eof, start
+        # bytes outside a masked head / tail chunk); then the 64 code masks
+        t_end = 256 + (hot + 1) * (K + 1) * 2
+        hot_tab = lds[256:t_end].view(np.uint16).reshape(hot + 1, K + 1)
+        mt = (t_end + 7) & ~7
+        masktab = lds[mt:mt + 512].view(np.uint64).copy()
+        return d, lds[:256].copy(), hot_tab, gcore.reshape(-1, K), gout.reshape(-1, K), eof, start, masktab
 
     def dfa_tables(self):
         """Set DFA: (info, trans (states, 256), eof_mask, now_mask, start)."""

@@ -364,7 +364,11 @@ __device__ __forceinline__ uint32_t core_entry(const uint16_t *T, uint32_t t, ui
       }                                                                                 \
     }                                                                                   \
     if (t != f.hot) {                                                                   \
-      mask |= (bag >> 1) & 0x3FFFFFFFFFFFFFFFull;                                       \
+      uint64_t bb = bag & 0x7FFFFFFFFFFFFFFEull; /* codes 1..62: the LDS code table */  \
+      while (bb) {                                                                      \
+        mask |= MT[__builtin_ctzll(bb)];                                                \
+        bb &= bb - 1;                                                                   \
+      }                                                                                 \
       c = t;                                                                            \
       if (c == f.dead) return true;                                                     \
       if (c == f.quit) { quit = true; return true; }                                    \
@@ -373,7 +377,8 @@ __device__ __forceinline__ uint32_t core_entry(const uint16_t *T, uint32_t t, ui
   }
 
 __device__ __forceinline__ bool core_chunk16(uint32_t &c, uint64_t &mask, uint64_t &pend, const SetCoreDev &f,
-                                             const uint8_t *cls, const uint16_t *T, uint4 v, bool &quit) {
+                                             const uint8_t *cls, const uint16_t *T, const uint64_t *MT, uint4 v,
+                                             bool &quit) {
   RURE_CORE_CHUNK(true)
 #pragma unroll 1
   for (int j = 0; j < 16; ++j)
@@ -386,8 +391,8 @@ __device__ __forceinline__ bool core_chunk16(uint32_t &c, uint64_t &mask, uint64
 // same branch-free lookup chain instead of up to 15 single steps each; the
 // inactive bytes leave the core and the bag unchanged.
 __device__ __forceinline__ bool core_chunk_masked(uint32_t &c, uint64_t &mask, uint64_t &pend, const SetCoreDev &f,
-                                                  const uint8_t *cls, const uint16_t *T, uint4 v, uint32_t k0,
-                                                  uint32_t kend, bool &quit) {
+                                                  const uint8_t *cls, const uint16_t *T, const uint64_t *MT, uint4 v,
+                                                  uint32_t k0, uint32_t kend, bool &quit) {
   RURE_CORE_CHUNK((uint32_t)j >= k0 && (uint32_t)j < kend)
 #pragma unroll 1
   for (uint32_t j = k0; j < kend; ++j)
@@ -404,6 +409,7 @@ __global__ __launch_bounds__(1024) void set_core_kernel(BatchDev bt, SetCoreDev 
   __syncthreads();
   const uint8_t *cls = lds;
   const uint16_t *T = (const uint16_t *)(lds + 256);
+  const uint64_t *MT = (const uint64_t *)(lds + f.mt_off);
   const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; h < bt.count; h += nthreads) {
     const uint8_t *base;
@@ -419,15 +425,15 @@ __global__ __launch_bounds__(1024) void set_core_kernel(BatchDev bt, SetCoreDev 
       const uintptr_t a = (uintptr_t)(base + at);
       const uint32_t k0 = (uint32_t)(a & 15);
       const uint32_t kend = len - at < 16 - k0 ? k0 + (uint32_t)(len - at) : 16;
-      done = core_chunk_masked(c, mask, pend, f, cls, T, *(const uint4 *)(a & ~(uintptr_t)15), k0, kend, quit);
+      done = core_chunk_masked(c, mask, pend, f, cls, T, MT, *(const uint4 *)(a & ~(uintptr_t)15), k0, kend, quit);
       at += kend - k0;
     }
     while (!done && at + 16 <= len) {
-      done = core_chunk16(c, mask, pend, f, cls, T, *(const uint4 *)(base + at), quit);
+      done = core_chunk16(c, mask, pend, f, cls, T, MT, *(const uint4 *)(base + at), quit);
       at += 16;
     }
     if (!done && at < len)  // tail: at is 16-byte aligned here
-      done = core_chunk_masked(c, mask, pend, f, cls, T, *(const uint4 *)(base + at), 0, (uint32_t)(len - at), quit);
+      done = core_chunk_masked(c, mask, pend, f, cls, T, MT, *(const uint4 *)(base + at), 0, (uint32_t)(len - at), quit);
     uint64_t m;
     if (quit) m = QUITMARK;
     else if (done) m = mask | pend;
@@ -441,7 +447,7 @@ __global__ __launch_bounds__(1024) void set_core_kernel(BatchDev bt, SetCoreDev 
 // visits — the adaptive counterpart of the reference's lazily filled cache
 // (dfa.rs:1154-1244), with identical results whatever the ranking.
 __global__ __launch_bounds__(256) void core_profile_kernel(BatchDev bt, SetCoreDev f, uint64_t count,
-                                                           unsigned int *visits) {
+                                                           unsigned int *visits, unsigned int *mask_counts) {
   const uint8_t *cls = f.lds_image;  // class map = first 256 bytes of the image
   for (uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; h < count; h += (uint64_t)gridDim.x * blockDim.x) {
     const uint8_t *base;
@@ -452,17 +458,20 @@ __global__ __launch_bounds__(256) void core_profile_kernel(BatchDev bt, SetCoreD
     uint32_t c = f.start[fwd_flag_index(base, len, bt.start)];
     const uint64_t end = len < bt.start + 4096 ? len : bt.start + 4096;
     for (uint64_t at = bt.start; at < end && c != f.dead && c != f.quit; ++at) {
-      c = f.gcore[(size_t)c * f.K + cls[base[at]]];
+      const size_t i = (size_t)c * f.K + cls[base[at]];
+      const uint32_t m = f.mid[i];
+      if (m) atomicAdd(&mask_counts[m], 1u);
+      c = f.gcore[i];
       atomicAdd(&visits[c], 1u);
     }
   }
 }
 
 hipError_t launch_core_profile(const BatchDev &b, const SetCoreDev &f, uint64_t count, unsigned int *visits,
-                               hipStream_t st, int cus) {
+                               unsigned int *mask_counts, hipStream_t st, int cus) {
   const uint64_t blocks = (count + 255) / 256;
   const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)cus * 4));
-  hipLaunchKernelGGL(core_profile_kernel, dim3(grid), dim3(256), 0, st, b, f, count, visits);
+  hipLaunchKernelGGL(core_profile_kernel, dim3(grid), dim3(256), 0, st, b, f, count, visits, mask_counts);
   return hipGetLastError();
 }
 

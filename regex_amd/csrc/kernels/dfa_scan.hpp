@@ -131,10 +131,12 @@ struct SetCoreDev {
   const uint16_t *start;      // 128 start cores
   uint64_t all;
   uint32_t dead, quit;        // quit = 0xFFFFFFFF if none
+  uint32_t mt_off;            // byte offset in the LDS image of the 64 u64 code masks
+  const uint16_t *mid;        // profile only: ncores x K mask id + 1 of gout (0: none)
 };
 hipError_t launch_set_cores(const BatchDev &b, const SetCoreDev &f, uint64_t *out, hipStream_t st, int cus);
 hipError_t launch_core_profile(const BatchDev &b, const SetCoreDev &f, uint64_t count, unsigned int *visits,
-                               hipStream_t st, int cus);
+                               unsigned int *mask_counts, hipStream_t st, int cus);
 
 // Pike VM closure tables (host/nfa_build.hpp) on the device.
 struct NfaDev {

@@ -237,6 +237,13 @@ struct CoreSet {
   uint16_t start[128];
   std::vector<uint32_t> order;    // rank -> core (in first-appearance numbering)
   bool profiled = false;
+  // output codes: code c in 1..62 reports codemask[c] (the table is in the
+  // LDS image at mt_off); 63 = look the mask up in gout.  mid (ncores x K)
+  // = 1 + the index of gout's mask in `masks` (0: none), for the profile.
+  uint64_t codemask[64] = {0};
+  uint32_t mt_off = 0;
+  std::vector<uint64_t> masks;
+  std::vector<uint16_t> mid;
 };
 
 // LDS budget of the core table (RURE_AMD_CORE_LDS overrides, tuning).
@@ -248,8 +255,12 @@ size_t core_lds_budget() {
 
 // weights (optional, by core in first-appearance numbering): rank the cores
 // by decreasing weight (measured visits), ties in BFS order.
+// mask_weights: how often each reported mask occurred on a sample (the
+// profile of adapt_cores); the 62 most frequent masks get the LDS codes.
+// Without it, masks rank by the number of hot transitions reporting them.
 bool build_set_cores(const DenseDfa &d, size_t lds_budget, CoreSet *cs,
-                     const std::vector<uint64_t> *weights = nullptr) {
+                     const std::vector<uint64_t> *weights = nullptr,
+                     const std::unordered_map<uint64_t, uint64_t> *mask_weights = nullptr) {
   const int S = d.nstates;
   std::unordered_map<std::string, uint32_t> key_core;
   std::vector<uint32_t> core_of(S);
@@ -300,37 +311,74 @@ bool build_set_cores(const DenseDfa &d, size_t lds_budget, CoreSet *cs,
     cls[b] = (uint8_t)it.first->second;
   }
   const uint32_t K = (uint32_t)col_rep.size();
-  if (lds_budget < 256 + 4 * K) return false;
+  if (lds_budget < 256 + 64 * 8 + 16 + 4 * (K + 1)) return false;
   // LDS rows have K + 1 entries: column K is the identity (same core, no
   // output), the class of the bytes outside a masked head / tail chunk
   const uint32_t KL = K + 1;
-  uint32_t hot = (uint32_t)std::min<size_t>({(size_t)nc, 1023, (lds_budget - 256) / (2 * KL) - 1});
+  // (the image: class map, (hot + 1) rows, the 64 code masks)
+  uint32_t hot = (uint32_t)std::min<size_t>({(size_t)nc, 1023, (lds_budget - 256 - 64 * 8 - 16) / (2 * KL) - 1});
   cs->K = K;
   cs->ncores = nc;
   cs->hot = hot;
   cs->gcore.assign((size_t)nc * K, 0);
   cs->gout.assign((size_t)nc * K, 0);
   cs->eof.assign(nc, 0);
-  cs->lds.assign(256 + (size_t)(hot + 1) * KL * 2, 0);
-  memcpy(cs->lds.data(), cls, 256);
-  uint16_t *T = (uint16_t *)(cs->lds.data() + 256);
+  cs->mid.assign((size_t)nc * K, 0);
+  cs->masks.clear();
+  std::unordered_map<uint64_t, uint32_t> mask_idx;
+  std::unordered_map<uint64_t, uint64_t> hot_uses;
   for (uint32_t r = 0; r < nc; ++r) {
     const int s = rep[order[r]];
     cs->eof[r] = d.eof_mask[s];
     for (uint32_t k = 0; k < K; ++k) {
       const uint32_t nxt = d.trans[(size_t)s * 256 + col_rep[k]];
-      const uint32_t ncore = (uint32_t)rank[core_of[nxt]];
       const uint64_t out = d.now_mask[nxt];
-      cs->gcore[(size_t)r * K + k] = (uint16_t)ncore;
+      cs->gcore[(size_t)r * K + k] = (uint16_t)rank[core_of[nxt]];
       cs->gout[(size_t)r * K + k] = out;
-      if (r < hot) {
-        uint32_t code = 0;
-        if (out) code = (__builtin_popcountll(out) == 1 && __builtin_ctzll(out) < 62) ? __builtin_ctzll(out) + 1 : 63;
-        const uint32_t tgt = ncore < hot ? ncore : hot;
-        T[(size_t)r * KL + k] = (uint16_t)((tgt << 6) | (ncore < hot ? code : 0));
-      }
+      if (!out) continue;
+      auto it = mask_idx.emplace(out, (uint32_t)cs->masks.size());
+      if (it.second) cs->masks.push_back(out);
+      if (cs->masks.size() >= 65535) return false;
+      cs->mid[(size_t)r * K + k] = (uint16_t)(it.first->second + 1);
+      if (r < hot) ++hot_uses[out];
     }
-    if (r < hot) T[(size_t)r * KL + K] = (uint16_t)(r << 6);  // identity column
+  }
+  // output codes 1..62 for the most frequent masks (measured when profiled)
+  std::vector<uint64_t> ranked = cs->masks;
+  auto weight = [&](uint64_t m) -> uint64_t {
+    if (mask_weights) {
+      auto it = mask_weights->find(m);
+      return it == mask_weights->end() ? 0 : it->second;
+    }
+    auto it = hot_uses.find(m);
+    return it == hot_uses.end() ? 0 : it->second;
+  };
+  std::stable_sort(ranked.begin(), ranked.end(), [&](uint64_t a, uint64_t b2) { return weight(a) > weight(b2); });
+  std::unordered_map<uint64_t, uint32_t> code_of;
+  memset(cs->codemask, 0, sizeof(cs->codemask));
+  for (uint32_t i = 0; i < ranked.size() && i < 62; ++i) {
+    code_of[ranked[i]] = i + 1;
+    cs->codemask[i + 1] = ranked[i];
+  }
+  const size_t t_end = 256 + (size_t)(hot + 1) * KL * 2;
+  cs->mt_off = (uint32_t)((t_end + 7) & ~(size_t)7);
+  cs->lds.assign(cs->mt_off + 64 * 8, 0);
+  memcpy(cs->lds.data(), cls, 256);
+  memcpy(cs->lds.data() + cs->mt_off, cs->codemask, 64 * 8);
+  uint16_t *T = (uint16_t *)(cs->lds.data() + 256);
+  for (uint32_t r = 0; r < hot; ++r) {
+    for (uint32_t k = 0; k < K; ++k) {
+      const uint32_t ncore = cs->gcore[(size_t)r * K + k];
+      const uint64_t out = cs->gout[(size_t)r * K + k];
+      uint32_t code = 0;
+      if (out) {
+        auto it = code_of.find(out);
+        code = it == code_of.end() ? 63 : it->second;
+      }
+      const uint32_t tgt = ncore < hot ? ncore : hot;
+      T[(size_t)r * KL + k] = (uint16_t)((tgt << 6) | (ncore < hot ? code : 0));
+    }
+    T[(size_t)r * KL + K] = (uint16_t)(r << 6);  // identity column
   }
   for (uint32_t k = 0; k < KL; ++k) T[(size_t)hot * KL + k] = (uint16_t)(hot << 6);  // sentinel row
   for (int i = 0; i < 128; ++i) cs->start[i] = (uint16_t)rank[core_of[d.start[i]]];
@@ -742,6 +790,7 @@ DevTables *set_device(rure_set *rs, std::string *err) {
       t.c.all = t.s.all;
       t.c.dead = cs.dead;
       t.c.quit = cs.quit;
+      t.c.mt_off = cs.mt_off;
     }
   }
   if (t.quit_possible && !rs->nfa_ok) {
@@ -1102,18 +1151,28 @@ bool adapt_cores(rure_set *rs, DevTables *t, const BatchDev &b, hipStream_t st, 
   t->cores_adapted = true;
   const CoreSet &cs = rs->cores;
   const uint64_t sample = std::min<uint64_t>(b.count, 16384);
+  // visits per core and reports per mask (mask ids: cs.mid) over a sample
   unsigned int *visits = nullptr;
-  if (!hip_ok(hipMallocAsync((void **)&visits, (size_t)cs.ncores * 4, st), err)) return false;
-  std::vector<unsigned int> h(cs.ncores);
-  bool ok = hip_ok(hipMemsetAsync(visits, 0, (size_t)cs.ncores * 4, st), err) &&
-            hip_ok(launch_core_profile(b, t->c, sample, visits, st, t->cus), err) &&
-            hip_ok(hipMemcpyAsync(h.data(), visits, (size_t)cs.ncores * 4, hipMemcpyDeviceToHost, st), err) &&
-            hip_ok(hipFreeAsync(visits, st), err) && hip_ok(hipStreamSynchronize(st), err);
+  uint16_t *mid = nullptr;
+  const size_t nm = cs.masks.size() + 1;
+  if (!hip_ok(hipMallocAsync((void **)&visits, (cs.ncores + nm) * 4, st), err)) return false;
+  if (!hip_ok(hipMallocAsync((void **)&mid, cs.mid.size() * 2, st), err)) return false;
+  std::vector<unsigned int> h(cs.ncores + nm);
+  SetCoreDev pc = t->c;
+  pc.mid = mid;
+  bool ok = hip_ok(hipMemsetAsync(visits, 0, (cs.ncores + nm) * 4, st), err) &&
+            hip_ok(hipMemcpyAsync(mid, cs.mid.data(), cs.mid.size() * 2, hipMemcpyHostToDevice, st), err) &&
+            hip_ok(launch_core_profile(b, pc, sample, visits, visits + cs.ncores, st, t->cus), err) &&
+            hip_ok(hipMemcpyAsync(h.data(), visits, h.size() * 4, hipMemcpyDeviceToHost, st), err) &&
+            hip_ok(hipFreeAsync(visits, st), err) && hip_ok(hipFreeAsync(mid, st), err) &&
+            hip_ok(hipStreamSynchronize(st), err);
   if (!ok) return false;
   std::vector<uint64_t> w(cs.ncores, 0);
   for (uint32_t r = 0; r < cs.ncores; ++r) w[cs.order[r]] = h[r];
+  std::unordered_map<uint64_t, uint64_t> mw;
+  for (size_t i = 1; i < nm; ++i) mw[cs.masks[i - 1]] = h[cs.ncores + i];
   CoreSet c2;
-  if (!build_set_cores(rs->dfa, core_lds_budget(), &c2, &w)) return true;  // keep the BFS ranking
+  if (!build_set_cores(rs->dfa, core_lds_budget(), &c2, &w, &mw)) return true;  // keep the BFS ranking
   Blob bl;
   size_t c_lds = bl.add(c2.lds.data(), c2.lds.size());
   size_t c_core = bl.add(c2.gcore.data(), c2.gcore.size() * 2);
@@ -1134,6 +1193,7 @@ bool adapt_cores(rure_set *rs, DevTables *t, const BatchDev &b, hipStream_t st, 
   c.start = (const uint16_t *)(base + c_start);
   c.dead = c2.dead;
   c.quit = c2.quit;
+  c.mt_off = c2.mt_off;
   if (t->core_blob) (void)hipFree(t->core_blob);
   t->core_blob = tmp.blob;
   t->c = c;

@@ -129,7 +129,7 @@ def core_set_matches(tables, t, start=0, n=64):
     """The core-form set kernel's walk (dfa_scan.hip set_core_kernel): chunks
     of 16 bytes through the hot table with an output bag, redone against the
     global tables when they leave the hot cores or meet output code 63."""
-    info, cls, T, gcore, gout, eof, st = tables
+    info, cls, T, gcore, gout, eof, st, masktab = tables
     hot, dead, quit = info["hot"], info["dead"], info["quit"]
     full = (1 << n) - 1 if n < 64 else (1 << 64) - 1
     if start > len(t):
@@ -154,7 +154,7 @@ def core_set_matches(tables, t, start=0, n=64):
             code = e & 63
             if (e >> 6) != hot and code != 63:
                 if code:
-                    mask |= 1 << (code - 1)
+                    mask |= int(masktab[code])
                 c = e >> 6
                 if c == quit:
                     raise QuitError()
@@ -178,7 +178,9 @@ def core_set_matches(tables, t, start=0, n=64):
                     pend |= int(gout[x, int(cls[b])])
                 x = e >> 6
             if x != hot:
-                mask |= (bag >> 1) & ((1 << 62) - 1)
+                for code in range(1, 63):  # codes 1..62: the code mask table
+                    if (bag >> code) & 1:
+                        mask |= int(masktab[code])
                 mask |= pend
                 c = x
                 if c == quit:
