@@ -20,3 +20,9 @@ def corpus(name):
     fn = {"sherlock": "sherlock.txt.gz", "regexdna": "regexdna-input.txt.gz"}[name]
     with gzip.open(os.path.join(G, fn), "rb") as f:
         return f.read()
+
+
+def stdlib_fixtures():
+    """Python-`re` answers for the BASELINE patterns (gen_stdlib_fixtures.py)."""
+    with gzip.open(os.path.join(G, "stdlib_re_fixtures.json.gz"), "rt", encoding="ascii") as f:
+        return json.load(f)
