@@ -31,9 +31,14 @@
 
 namespace rure_amd {
 
+__device__ __forceinline__ void note_quit(uint32_t *flag) {
+  if (flag) atomicOr(flag, 1u);
+}
+
 template <int MODE>
 __device__ __forceinline__ void finish_lane(const LaneState &L, const RevDfaDev &r, const uint8_t *base,
-                                            uint64_t len, uint64_t lo, uint64_t h, void *out) {
+                                            uint64_t len, uint64_t lo, uint64_t h, void *out, uint32_t *qf) {
+  if (L.quit) note_quit(qf);
   if (MODE == MODE_ISMATCH) {
     ((uint8_t *)out)[h] = L.quit ? 2 : (L.last != NONE ? 1 : 0);
     return;
@@ -51,6 +56,7 @@ __device__ __forceinline__ void finish_lane(const LaneState &L, const RevDfaDev 
       ms = lo;                              // exec.rs:647
     } else {
       const uint64_t rs = rev_scan(r, nullptr, base, len, lo, me);
+      if (rs == QUITMARK) note_quit(qf);
       if (rs == QUITMARK) ms = me = QUITMARK;
       else if (rs == NONE) ms = me = NONE;  // exec.rs:656-660: reverse NoMatch -> no match
       else ms = rs;
@@ -82,7 +88,7 @@ __global__ __launch_bounds__(256) void dfa_fwd_kernel(BatchDev bt, FwdDfaDev f, 
     LaneState L;
     lane_start(L, f, base, len, bt.start);
     fwd_run<MODE>(L, f, lds, base, len, bt.start);
-    finish_lane<MODE>(L, r, base, len, bt.start, h, out);
+    finish_lane<MODE>(L, r, base, len, bt.start, h, out, bt.quit_flag);
   }
 }
 
@@ -222,7 +228,7 @@ __global__ __launch_bounds__(256) void dfa_fwd_tile_kernel(BatchDev bt, FwdDfaDe
         ++at;
       }
       if (!L_.done && f.eof[L_.s]) L_.last = L;
-      finish_lane<MODE>(L_, r, base, L, 0, h, out);
+      finish_lane<MODE>(L_, r, base, L, 0, h, out, bt.quit_flag);
     }
   }
 }
@@ -299,6 +305,7 @@ __global__ __launch_bounds__(256) void dfa_set_kernel(BatchDev bt, SetDfaDev f, 
       ++at;
     }
     uint64_t m;
+    if (quit) note_quit(bt.quit_flag);
     if (quit) m = QUITMARK;
     else if (done) m = mask;  // dead, or every pattern already matched
     else m = mask | f.eof_mask[s];
@@ -435,6 +442,7 @@ __global__ __launch_bounds__(1024) void set_core_kernel(BatchDev bt, SetCoreDev 
     if (!done && at < len)  // tail: at is 16-byte aligned here
       done = core_chunk_masked(c, mask, pend, f, cls, T, MT, *(const uint4 *)(base + at), 0, (uint32_t)(len - at), quit);
     uint64_t m;
+    if (quit) note_quit(bt.quit_flag);
     if (quit) m = QUITMARK;
     else if (done) m = mask | pend;
     else m = mask | pend | f.eof[c];
@@ -531,6 +539,7 @@ __global__ __launch_bounds__(256) void dfa_anchored_rev_kernel(BatchDev bt, RevD
       len = o1 - o0;
     }
     const uint64_t rs = bt.start > len ? NONE : rev_scan<MODE != MODE_FIND>(r, rlds, base, len, bt.start, len);
+    if (rs == QUITMARK) note_quit(bt.quit_flag);
     if (MODE == MODE_ISMATCH) {
       ((uint8_t *)out)[h] = rs == QUITMARK ? 2 : (rs != NONE ? 1 : 0);
     } else if (MODE == MODE_SHORTEST) {

@@ -18,6 +18,9 @@ struct BatchDev {
   const uint8_t *hay;
   const uint64_t *offs;   // n+1 offsets or nullptr (fixed stride)
   uint64_t stride, length, count, start;
+  // set (atomic OR) by the DFA kernels when a haystack's DFA quit; the Pike VM
+  // fallback pass then runs, else it returns at once (nullptr: always runs)
+  uint32_t *quit_flag = nullptr;
 };
 
 // Forward DFA on the device.  State ids: [0, hot) are in the LDS fast table

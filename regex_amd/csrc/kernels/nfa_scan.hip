@@ -29,6 +29,8 @@ using namespace pike;
 
 template <int MODE, bool FALLBACK, bool STRIDED>
 __global__ __launch_bounds__(64) void pike_kernel(BatchDev bt, NfaDev nf, void *out, uint8_t *scratch) {
+  // the DFA pass flagged no quit: nothing to redo
+  if (FALLBACK && bt.quit_flag && __atomic_load_n(bt.quit_flag, __ATOMIC_RELAXED) == 0) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   uint8_t *mem = scratch ? scratch + (size_t)blockIdx.x * nfa_wave_bytes(nf.nleaves) : lds;
   Lists W;

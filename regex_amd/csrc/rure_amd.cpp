@@ -1137,9 +1137,18 @@ hipError_t run_regex(int mode, const BatchDev &b, const DevTables &t, void *out,
   uint64_t chunk = 0;
   if (iter && long_batch(b, t, &chunk) && !(t.anchored_rev && b.start != 0))
     return launch_long_scan(mode, b, *iter, t.r, chunk, out, st, t.cus);
-  hipError_t e = run_dfa_step(mode, b, t, out, st, dfa_grid, nullptr);
-  if (e != hipSuccess || !t.quit_possible) return e;
-  return run_pike(mode, true, b, t, out, st);
+  if (!t.quit_possible) return run_dfa_step(mode, b, t, out, st, dfa_grid, nullptr);
+  // the DFA kernels flag a quit; the Pike VM fallback returns at once without
+  BatchDev bq = b;
+  hipError_t e = hipMallocAsync((void **)&bq.quit_flag, 4, st);
+  if (e == hipSuccess) e = hipMemsetAsync(bq.quit_flag, 0, 4, st);
+  if (e == hipSuccess) e = run_dfa_step(mode, bq, t, out, st, dfa_grid, nullptr);
+  if (e == hipSuccess) e = run_pike(mode, true, bq, t, out, st);
+  if (bq.quit_flag) {
+    hipError_t e2 = hipFreeAsync(bq.quit_flag, st);
+    if (e == hipSuccess) e = e2;
+  }
+  return e;
 }
 
 // First batched use of a core-form set on a device: count core visits over a
@@ -1203,9 +1212,19 @@ bool adapt_cores(rure_set *rs, DevTables *t, const BatchDev &b, hipStream_t st, 
 // exec.rs:998-1038 many_matches_at for a batch.
 hipError_t run_set(const BatchDev &b, const DevTables &t, uint64_t *out, hipStream_t st, int dfa_grid) {
   if (!t.has_dfa) return run_pike(MODE_SET, false, b, t, out, st);
-  hipError_t e = t.use_cores ? launch_set_cores(b, t.c, out, st, t.cus) : launch_dfa_set(b, t.s, out, st, dfa_grid);
-  if (e != hipSuccess || !t.quit_possible) return e;
-  return run_pike(MODE_SET, true, b, t, out, st);
+  if (!t.quit_possible)
+    return t.use_cores ? launch_set_cores(b, t.c, out, st, t.cus) : launch_dfa_set(b, t.s, out, st, dfa_grid);
+  BatchDev bq = b;  // quit flag: see run_regex
+  hipError_t e = hipMallocAsync((void **)&bq.quit_flag, 4, st);
+  if (e == hipSuccess) e = hipMemsetAsync(bq.quit_flag, 0, 4, st);
+  if (e == hipSuccess)
+    e = t.use_cores ? launch_set_cores(bq, t.c, out, st, t.cus) : launch_dfa_set(bq, t.s, out, st, dfa_grid);
+  if (e == hipSuccess) e = run_pike(MODE_SET, true, bq, t, out, st);
+  if (bq.quit_flag) {
+    hipError_t e2 = hipFreeAsync(bq.quit_flag, st);
+    if (e == hipSuccess) e = e2;
+  }
+  return e;
 }
 
 // exec.rs:524-596 read_captures_at for a batch.  One group (two slots): the
@@ -1247,6 +1266,7 @@ bool to_batch(const rure_amd_batch *b, BatchDev *o) {
   o->length = b->length;
   o->count = b->count;
   o->start = b->start;
+  o->quit_flag = nullptr;
   return true;
 }
 
