@@ -334,11 +334,16 @@ __device__ __forceinline__ bool core_careful(uint32_t &c, uint64_t &mask, const 
   return (mask & f.all) == f.all;
 }
 
-// One lookup of the hot core table: entry (core t, class k) at byte
-// 2 * (t * K + k) past the class map — one 24-bit multiply-add (full rate)
-// and a u16 LDS read on the dependent chain.
-__device__ __forceinline__ uint32_t core_entry(const uint16_t *T, uint32_t t, uint32_t K2, uint32_t k2) {
-  return *(const uint16_t *)((const uint8_t *)T + __umul24(t, K2) + k2);
+// One lookup of the hot core table: entry (core t, class k) at LDS byte
+// 256 + t * K2 + 2k — one 24-bit multiply-add (v_mad_u32_u24, full rate) and
+// a u16 LDS read on the dependent chain.  The address is formed as an LDS
+// (address space 3) integer: set_core_kernel has no static LDS, so its dynamic
+// window starts at byte 0, and a generic pointer would cost an extra add of
+// the window's base per byte.  k2 = 2k comes from the LDS class map, which
+// the kernel stores doubled.
+typedef __attribute__((address_space(3))) const uint16_t lds_u16_t;
+__device__ __forceinline__ uint32_t core_entry(uint32_t t, uint32_t K2, uint32_t k2) {
+  return *(lds_u16_t *)(uintptr_t)(256u + __umul24(t, K2) + k2);
 }
 
 // Code 63 (a report that is not one pattern < 62) takes its mask from the
@@ -346,27 +351,26 @@ __device__ __forceinline__ uint32_t core_entry(const uint16_t *T, uint32_t t, ui
 // walks its bytes again for those loads (no byte waits on a global load).
 #define RURE_CORE_CHUNK(ACTIVE)                                                         \
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};                                           \
-  uint32_t k[16];                                                                       \
-  _Pragma("unroll") for (int j = 0; j < 16; ++j) k[j] = cls[(w[j >> 2] >> ((j & 3) * 8)) & 0xFF]; \
+  const uint32_t KI = 2 * f.K; /* the identity column, doubled */                      \
+  uint32_t kc[16];                                                                      \
+  _Pragma("unroll") for (int j = 0; j < 16; ++j) {                                      \
+    const bool act = ACTIVE;                                                            \
+    kc[j] = act ? (uint32_t)cls[(w[j >> 2] >> ((j & 3) * 8)) & 0xFF] : KI;              \
+  }                                                                                     \
   if (c < f.hot) {                                                                      \
     const uint32_t K2 = 2 * (f.K + 1); /* LDS rows: K classes + the identity column */ \
     uint32_t t = c;                                                                     \
     uint64_t bag = 0;                                                                   \
-    uint32_t kc[16];                                                                    \
     _Pragma("unroll") for (int j = 0; j < 16; ++j) {                                    \
-      const bool act = ACTIVE;                                                          \
-      kc[j] = act ? 2 * k[j] : 2 * f.K;                                                 \
-    }                                                                                   \
-    _Pragma("unroll") for (int j = 0; j < 16; ++j) {                                    \
-      const uint32_t e = core_entry(T, t, K2, kc[j]);                                   \
+      const uint32_t e = core_entry(t, K2, kc[j]);                                      \
       bag |= 1ull << (e & 63);                                                          \
       t = e >> 6;                                                                       \
     }                                                                                   \
     if ((bag >> 63) && t != f.hot) {                                                    \
       uint32_t x = c;                                                                   \
       for (int j = 0; j < 16; ++j) {                                                    \
-        const uint32_t e = core_entry(T, x, K2, kc[j]);                                 \
-        if ((e & 63) == 63) pend |= f.gout[(size_t)x * f.K + k[j]];                     \
+        const uint32_t e = core_entry(x, K2, kc[j]);                                    \
+        if ((e & 63) == 63) pend |= f.gout[(size_t)x * f.K + (kc[j] >> 1)];             \
         x = e >> 6;                                                                     \
       }                                                                                 \
     }                                                                                   \
@@ -389,7 +393,7 @@ __device__ __forceinline__ bool core_chunk16(uint32_t &c, uint64_t &mask, uint64
   RURE_CORE_CHUNK(true)
 #pragma unroll 1
   for (int j = 0; j < 16; ++j)
-    if (core_careful(c, mask, f, k[j], quit)) return true;
+    if (core_careful(c, mask, f, kc[j] >> 1, quit)) return true;
   return false;
 }
 
@@ -403,7 +407,7 @@ __device__ __forceinline__ bool core_chunk_masked(uint32_t &c, uint64_t &mask, u
   RURE_CORE_CHUNK((uint32_t)j >= k0 && (uint32_t)j < kend)
 #pragma unroll 1
   for (uint32_t j = k0; j < kend; ++j)
-    if (core_careful(c, mask, f, k[j], quit)) return true;
+    if (core_careful(c, mask, f, kc[j] >> 1, quit)) return true;
   return false;
 }
 #undef RURE_CORE_CHUNK
@@ -455,6 +459,8 @@ __global__ __launch_bounds__(1024) void set_core_kernel(BatchDev bt, SetCoreDev 
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   for (uint32_t i = threadIdx.x * 16; i < f.lds_bytes; i += blockDim.x * 16)
     *(uint4 *)(lds + i) = *(const uint4 *)(f.lds_image + i);
+  __syncthreads();
+  if (threadIdx.x < 256) lds[threadIdx.x] = (uint8_t)(2 * lds[threadIdx.x]);  // class map, doubled (K < 128)
   __syncthreads();
   const uint8_t *cls = lds;
   const uint16_t *T = (const uint16_t *)(lds + 256);

@@ -311,6 +311,7 @@ bool build_set_cores(const DenseDfa &d, size_t lds_budget, CoreSet *cs,
     cls[b] = (uint8_t)it.first->second;
   }
   const uint32_t K = (uint32_t)col_rep.size();
+  if (K > 127) return false;  // the kernel's LDS class map holds 2k in a byte
   if (lds_budget < 256 + 64 * 8 + 16 + 4 * (K + 1)) return false;
   // LDS rows have K + 1 entries: column K is the identity (same core, no
   // output), the class of the bytes outside a masked head / tail chunk
