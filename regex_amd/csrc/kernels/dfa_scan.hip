@@ -455,162 +455,49 @@ __device__ __forceinline__ uint64_t core_scan_one(const SetCoreDev &f, const uin
   return done ? mask : (mask | f.eof[c]);
 }
 
-// Two haystacks per lane, stepped together: the two lookup chains are
-// independent, so each one's LDS latency hides behind the other's (with one
-// chain per lane and the 16 waves per CU that the table's LDS allows, the
-// SIMDs idle ~40% of the time waiting on the chain).  A haystack spans
-// aligned blocks: its first and last blocks are stepped with the bytes
-// outside it masked to the identity column, the blocks between unmasked; a
-// chain with nothing to do in a step runs on stale data and is not committed.
-struct CoreLane {
-  const uint8_t *base;
-  uint64_t len, at;
-  uint64_t mask, codes;
-  uint32_t c;
-  bool done, quit;
-};
-
-__device__ __forceinline__ void core_lane_init(CoreLane &L, const SetCoreDev &f, const uint8_t *base, uint64_t len,
-                                               uint64_t start, bool valid) {
-  L.base = base;
-  L.len = len;
-  L.mask = 0;
-  L.codes = 0;
-  L.quit = false;
-  if (!valid || start > len) {
-    L.c = f.dead;
-    L.done = true;
-    L.at = len;
-  } else {
-    L.c = f.start[fwd_flag_index(base, len, start)];
-    L.done = L.c == f.dead;
-    L.at = start;
-  }
-}
-
-// classes of the bytes [k0, kend) of block v (MASKED), the identity elsewhere
-template <bool MASKED>
-__device__ __forceinline__ void core_classes(uint32_t kc[16], const uint8_t *cls, uint4 v, uint32_t k0, uint32_t kend,
-                                             uint32_t KI) {
-  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+// Ascending bitonic sort of the wave's 64 * R keys, key r of lane l being
+// element r * 64 + l: partners 64 or more apart are in the lane's own
+// registers, nearer ones one __shfl_xor away.
+template <int R>
+__device__ __forceinline__ void wave_sort(uint32_t key[R], uint32_t lane) {
 #pragma unroll
-  for (int j = 0; j < 16; ++j) kc[j] = cls[(w[j >> 2] >> ((j & 3) * 8)) & 0xFF];
-  if (MASKED) {
+  for (uint32_t k = 2; k <= 64u * R; k <<= 1) {
 #pragma unroll
-    for (int j = 0; j < 16; ++j) kc[j] = ((uint32_t)j >= k0 && (uint32_t)j < kend) ? kc[j] : KI;
-  }
-}
-
-// Commits one chain's step: the hot result, or (the step left the hot cores,
-// or started outside them) the bytes [k0, kend) again on the global tables.
-__device__ __forceinline__ void core_commit(CoreLane &L, const SetCoreDev &f, const uint32_t kc[16], uint32_t t,
-                                            uint64_t bag, uint32_t k0, uint32_t kend) {
-  const uint32_t K2 = 2 * (f.K + 1);
-  if (L.c < f.hot && t != f.hot) {
-    if (bag >> 63) {  // code 63: the mask is in the global table
-      uint32_t x = L.c;
-      for (int j = 0; j < 16; ++j) {
-        const uint32_t e = core_entry(x, K2, kc[j]);
-        if ((e & 63) == 63) L.mask |= f.gout[(size_t)x * f.K + (kc[j] >> 1)];
-        x = e >> 6;
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      if (j >= 64) {
+        const uint32_t jr = j >> 6;
+#pragma unroll
+        for (uint32_t r = 0; r < (uint32_t)R; ++r) {
+          if (r & jr) continue;
+          const bool up = ((r * 64 + lane) & k) == 0;
+          const uint32_t a = key[r], b = key[r | jr];
+          key[r] = up ? min(a, b) : max(a, b);
+          key[r | jr] = up ? max(a, b) : min(a, b);
+        }
+      } else {
+#pragma unroll
+        for (uint32_t r = 0; r < (uint32_t)R; ++r) {
+          const uint32_t o = __shfl_xor(key[r], (int)j);
+          const bool up = ((r * 64 + lane) & k) == 0, lower = (lane & j) == 0;
+          key[r] = (up == lower) ? min(key[r], o) : max(key[r], o);
+        }
       }
     }
-    L.codes |= bag;
-    L.c = t;
-    if (t == f.dead) L.done = true;
-    else if (t == f.quit) { L.quit = true; L.done = true; }
-    return;
-  }
-  for (uint32_t j = k0; j < kend; ++j)
-    if (core_careful(L.c, L.mask, f, kc[j] >> 1, L.quit)) { L.done = true; return; }
-}
-
-template <bool MASKED>
-__device__ __forceinline__ void core_pair_step(CoreLane &A, CoreLane &B, const SetCoreDev &f, const uint8_t *cls,
-                                               uint4 va, uint4 vb, uint32_t k0a, uint32_t kea, uint32_t k0b,
-                                               uint32_t keb, bool acta, bool actb) {
-  const uint32_t KI = 2 * f.K, K2 = 2 * (f.K + 1);
-  uint32_t ka[16], kb[16];
-  core_classes<MASKED>(ka, cls, va, k0a, kea, KI);
-  core_classes<MASKED>(kb, cls, vb, k0b, keb, KI);
-  uint32_t ta = min(A.c, f.hot), tb = min(B.c, f.hot);  // row hot: the sink
-  uint64_t baga = 0, bagb = 0;
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const uint32_t ea = core_entry(ta, K2, ka[j]);
-    const uint32_t eb = core_entry(tb, K2, kb[j]);
-    baga |= 1ull << (ea & 63);
-    bagb |= 1ull << (eb & 63);
-    ta = ea >> 6;
-    tb = eb >> 6;
-    __builtin_amdgcn_sched_barrier(0);  // keep the two chains interleaved step by step
-  }
-  if (acta) core_commit(A, f, ka, ta, baga, MASKED ? k0a : 0, MASKED ? kea : 16);
-  if (actb) core_commit(B, f, kb, tb, bagb, MASKED ? k0b : 0, MASKED ? keb : 16);
-}
-
-// the block holding byte L.at and the bytes of it inside the haystack
-__device__ __forceinline__ bool core_edge(const CoreLane &L, uint4 &v, uint32_t &k0, uint32_t &kend) {
-  if (L.done || L.at >= L.len) { v = make_uint4(0, 0, 0, 0); k0 = kend = 0; return false; }
-  const uintptr_t a = (uintptr_t)(L.base + L.at);
-  k0 = (uint32_t)(a & 15);
-  kend = L.len - L.at < 16 - k0 ? k0 + (uint32_t)(L.len - L.at) : 16;
-  v = *(const uint4 *)(a & ~(uintptr_t)15);
-  return true;
-}
-
-__device__ __forceinline__ uint64_t core_finish(const CoreLane &L, const SetCoreDev &f, const uint64_t *MT,
-                                                uint32_t *qf) {
-  if (L.quit) { note_quit(qf); return QUITMARK; }
-  uint64_t mask = L.mask, bb = L.codes & 0x7FFFFFFFFFFFFFFEull;  // codes 1..62: the LDS code table
-  while (bb) {
-    mask |= MT[__builtin_ctzll(bb)];
-    bb &= bb - 1;
-  }
-  return L.done ? mask : (mask | f.eof[L.c]);
-}
-
-__device__ __forceinline__ void core_scan_pair(CoreLane &A, CoreLane &B, const SetCoreDev &f, const uint8_t *cls) {
-  uint4 va, vb;
-  uint32_t k0a, kea, k0b, keb;
-  // first blocks (masked)
-  bool aa = core_edge(A, va, k0a, kea), ab = core_edge(B, vb, k0b, keb);
-  if (aa || ab) {
-    core_pair_step<true>(A, B, f, cls, va, vb, k0a, kea, k0b, keb, aa, ab);
-    if (aa) A.at += kea - k0a;
-    if (ab) B.at += keb - k0b;
-  }
-  // whole blocks (A.at, B.at are block-aligned now), the next one's load in flight
-  bool fa = !A.done && A.at + 16 <= A.len, fb = !B.done && B.at + 16 <= B.len;
-  va = fa ? *(const uint4 *)(A.base + A.at) : make_uint4(0, 0, 0, 0);
-  vb = fb ? *(const uint4 *)(B.base + B.at) : make_uint4(0, 0, 0, 0);
-  while (fa || fb) {
-    uint4 na = make_uint4(0, 0, 0, 0), nb = make_uint4(0, 0, 0, 0);
-    if (fa && A.at + 32 <= A.len) na = *(const uint4 *)(A.base + A.at + 16);
-    if (fb && B.at + 32 <= B.len) nb = *(const uint4 *)(B.base + B.at + 16);
-    core_pair_step<false>(A, B, f, cls, va, vb, 0, 16, 0, 16, fa, fb);
-    if (fa) A.at += 16;
-    if (fb) B.at += 16;
-    fa = !A.done && A.at + 16 <= A.len;
-    fb = !B.done && B.at + 16 <= B.len;
-    va = na;
-    vb = nb;
-  }
-  // last blocks (masked)
-  aa = core_edge(A, va, k0a, kea);
-  ab = core_edge(B, vb, k0b, keb);
-  if (aa || ab) {
-    core_pair_step<true>(A, B, f, cls, va, vb, k0a, kea, k0b, keb, aa, ab);
-    if (aa) A.at += kea - k0a;
-    if (ab) B.at += keb - k0b;
   }
 }
 
-// MODE: 0 = fixed stride, 1 = offsets; one haystack per lane (grid-stride).
+// MODE: 0 = fixed stride (one haystack per lane, grid-stride), 1 = offsets.
+// Offset batches: a wave's time per round is its longest lane's, so each wave
+// takes 64 * kCoreRounds haystacks, sorts them by the number of blocks they
+// span (wave_sort) and scans them in kCoreRounds rounds of 64 similar ones
+// (C4's 40-160 byte lines: 66% of the lanes' block steps were useful with one
+// haystack per lane in index order, 95% sorted in groups of 512).
 // (Tried: offsets as one byte stream cut into equal units per lane, each lane
 // scanning the haystacks that start in its unit — equal bytes per lane, but
-// every load of a wave then hits 64 distant regions: C4 1.22 vs 0.79 ms.)
-template <int MODE>
+// every load of a wave then hits 64 distant regions: C4 1.22 vs 0.79 ms; two
+// haystacks per lane with interleaved chains: 0.72 vs 0.68 ms, the shorter
+// one's chain idles.)
+template <int MODE, int kCoreRounds = 8>
 __global__ __launch_bounds__(1024) void set_core_kernel(BatchDev bt, SetCoreDev f, uint64_t *out) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   for (uint32_t i = threadIdx.x * 16; i < f.lds_bytes; i += blockDim.x * 16)
@@ -620,29 +507,38 @@ __global__ __launch_bounds__(1024) void set_core_kernel(BatchDev bt, SetCoreDev 
   __syncthreads();
   const uint8_t *cls = lds;
   const uint64_t *MT = (const uint64_t *)(lds + f.mt_off);
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
-  // haystacks h and h + nthreads per lane (two chains), grid-stride by 2x
-  for (uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; h < bt.count; h += 2 * nthreads) {
-    const uint64_t h2 = h + nthreads;
-    const bool v2 = h2 < bt.count;
-    const uint8_t *b1, *b2 = bt.hay;
-    uint64_t l1, l2 = 0;
-    if (MODE == 0) {
-      b1 = bt.hay + h * bt.stride;
-      l1 = bt.length;
-      if (v2) { b2 = bt.hay + h2 * bt.stride; l2 = bt.length; }
-    } else {
-      const uint64_t o0 = bt.offs[h], o1 = bt.offs[h + 1];
-      b1 = bt.hay + o0;
-      l1 = o1 - o0;
-      if (v2) { const uint64_t p0 = bt.offs[h2], p1 = bt.offs[h2 + 1]; b2 = bt.hay + p0; l2 = p1 - p0; }
+  if (MODE == 0) {
+    for (uint64_t h = tid; h < bt.count; h += nthreads)
+      out[h] = core_scan_one(f, cls, MT, bt.hay + h * bt.stride, bt.length, bt.start, bt.quit_flag);
+    return;
+  }
+  constexpr uint32_t G = 64 * kCoreRounds;  // haystacks per wave and group
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint64_t h0 = (tid >> 6) * G; h0 < bt.count; h0 += (nthreads >> 6) * G) {  // wave-uniform
+    uint32_t key[kCoreRounds];
+#pragma unroll
+    for (int r = 0; r < kCoreRounds; ++r) {
+      const uint64_t h = h0 + r * 64 + lane;
+      uint32_t blocks = 0x7FFFFF;  // past the batch: sorts last
+      if (h < bt.count) {
+        const uint64_t o0 = bt.offs[h], o1 = bt.offs[h + 1];
+        blocks = (uint32_t)min<uint64_t>(((o1 + 15) >> 4) - (o0 >> 4), 0x7FFFFE);
+      }
+      key[r] = blocks << 9 | (r * 64 + lane);
     }
-    CoreLane A, B;
-    core_lane_init(A, f, b1, l1, bt.start, true);
-    core_lane_init(B, f, b2, l2, bt.start, v2);
-    core_scan_pair(A, B, f, cls);
-    out[h] = core_finish(A, f, MT, bt.quit_flag);
-    if (v2) out[h2] = core_finish(B, f, MT, bt.quit_flag);
+    wave_sort<kCoreRounds>(key, lane);
+#pragma unroll 1
+    for (int r = 0; r < kCoreRounds; ++r) {
+      const uint64_t h = h0 + (key[0] & (G - 1));
+      if (h < bt.count) {
+        const uint64_t o0 = bt.offs[h], o1 = bt.offs[h + 1];
+        out[h] = core_scan_one(f, cls, MT, bt.hay + o0, o1 - o0, bt.start, bt.quit_flag);
+      }
+#pragma unroll
+      for (int q = 0; q + 1 < kCoreRounds; ++q) key[q] = key[q + 1];  // next round's key to the front
+    }
   }
 }
 
@@ -698,6 +594,11 @@ hipError_t launch_set_cores(const BatchDev &b, const SetCoreDev &f, uint64_t *ou
     hipLaunchKernelGGL(kern, dim3(grid), dim3(bs), f.lds_bytes, st, b, f, out);
     return hipGetLastError();
   };
+  int rounds = 8;
+  if (const char *v = getenv("RURE_AMD_CORE_ROUNDS")) rounds = atoi(v);
+  if (mode == 1 && rounds == 1) return go(set_core_kernel<1, 1>);
+  if (mode == 1 && rounds == 2) return go(set_core_kernel<1, 2>);
+  if (mode == 1 && rounds == 4) return go(set_core_kernel<1, 4>);
   if (mode == 1) return go(set_core_kernel<1>);
   return go(set_core_kernel<0>);
 }
