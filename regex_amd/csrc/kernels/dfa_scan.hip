@@ -358,7 +358,7 @@ __device__ __forceinline__ uint32_t core_entry(uint32_t t, uint32_t K2, uint32_t
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};                                           \
   const uint32_t KI = 2 * f.K; /* the identity column, doubled */                      \
   uint32_t kc[16];                                                                      \
-  _Pragma("unroll") for (int j = 0; j < 16; ++j) kc[j] = cls[(w[j >> 2] >> ((j & 3) * 8)) & 0xFF]; \
+  _Pragma("unroll") for (int j = 0; j < 16; ++j) kc[j] = (EXP & 4) ? (((w[j >> 2] >> ((j & 3) * 8)) & 0x3F) << 1) : cls[(w[j >> 2] >> ((j & 3) * 8)) & 0xFF]; \
   _Pragma("unroll") for (int j = 0; j < 16; ++j) { /* a select, not a branch per byte */ \
     const bool act = ACTIVE;                                                            \
     kc[j] = act ? kc[j] : KI;                                                           \
@@ -368,7 +368,7 @@ __device__ __forceinline__ uint32_t core_entry(uint32_t t, uint32_t K2, uint32_t
     uint32_t t = c;                                                                     \
     uint64_t bag = 0;                                                                   \
     _Pragma("unroll") for (int j = 0; j < 16; ++j) {                                    \
-      const uint32_t e = core_entry(t, K2, kc[j]);                                      \
+      const uint32_t e = core_entry((EXP & 1) ? (t & f.dead) : t, K2, kc[j]);            \
       bag |= 1ull << (e & 63);                                                          \
       t = e >> 6;                                                                       \
     }                                                                                   \
@@ -389,6 +389,7 @@ __device__ __forceinline__ uint32_t core_entry(uint32_t t, uint32_t K2, uint32_t
     }                                                                                   \
   }
 
+template <int EXP>
 __device__ __forceinline__ bool core_chunk16(uint32_t &c, uint64_t &mask, uint64_t &codes, const SetCoreDev &f,
                                              const uint8_t *cls, uint4 v, bool &quit) {
   RURE_CORE_CHUNK(true)
@@ -402,6 +403,7 @@ __device__ __forceinline__ bool core_chunk16(uint32_t &c, uint64_t &mask, uint64
 // head and the tail of a line (lines start anywhere) cost one pass of the
 // same branch-free lookup chain instead of up to 15 single steps each; the
 // inactive bytes leave the core and the bag unchanged.
+template <int EXP>
 __device__ __forceinline__ bool core_chunk_masked(uint32_t &c, uint64_t &mask, uint64_t &codes, const SetCoreDev &f,
                                                   const uint8_t *cls, uint4 v, uint32_t k0, uint32_t kend,
                                                   bool &quit) {
@@ -416,6 +418,7 @@ __device__ __forceinline__ bool core_chunk_masked(uint32_t &c, uint64_t &mask, u
 // One haystack's set scan with the core-form tables (the per-lane body of
 // set_core_kernel): head / full / tail 16-byte chunks, the next block's load
 // in flight while one is stepped.
+template <int EXP>
 __device__ __forceinline__ uint64_t core_scan_one(const SetCoreDev &f, const uint8_t *cls, const uint64_t *MT,
                                                   const uint8_t *base, uint64_t len, uint64_t at, uint32_t *qf) {
   uint64_t mask = 0, codes = 0;
@@ -427,24 +430,26 @@ __device__ __forceinline__ uint64_t core_scan_one(const SetCoreDev &f, const uin
     const uintptr_t a = (uintptr_t)(base + at);
     const uint32_t k0 = (uint32_t)(a & 15);
     const uint32_t kend = len - at < 16 - k0 ? k0 + (uint32_t)(len - at) : 16;
-    done = core_chunk_masked(c, mask, codes, f, cls, *(const uint4 *)(a & ~(uintptr_t)15), k0, kend, quit);
+    done = core_chunk_masked<EXP>(c, mask, codes, f, cls, *(const uint4 *)(a & ~(uintptr_t)15), k0, kend, quit);
     at += kend - k0;
   }
   // the next block's load is in flight while this one is stepped (the
   // per-lane streams are latency-bound: one round trip per block otherwise).
   // (Tried: 128-byte windows loaded at once, 8 unrolled chunk steps: 1.21 vs
   // 0.79 ms on C4 — the unrolled chunk code outgrows the instruction cache.)
+  if (EXP & 16) done = true;
   uint4 cur = make_uint4(0, 0, 0, 0);
   if (!done && at < len) cur = *(const uint4 *)(base + at);
   while (!done && at + 16 <= len) {
     uint4 nxt = make_uint4(0, 0, 0, 0);
-    if (at + 16 < len) nxt = *(const uint4 *)(base + at + 16);
-    done = core_chunk16(c, mask, codes, f, cls, cur, quit);
+    if (!(EXP & 2) && at + 16 < len) nxt = *(const uint4 *)(base + at + 16);
+    if (EXP & 2) nxt = cur;
+    done = core_chunk16<EXP>(c, mask, codes, f, cls, cur, quit);
     cur = nxt;
     at += 16;
   }
   if (!done && at < len)  // tail: at is 16-byte aligned here
-    done = core_chunk_masked(c, mask, codes, f, cls, cur, 0, (uint32_t)(len - at), quit);
+    done = core_chunk_masked<EXP>(c, mask, codes, f, cls, cur, 0, (uint32_t)(len - at), quit);
   if (quit) note_quit(qf);
   if (quit) return QUITMARK;
   uint64_t bb = codes & 0x7FFFFFFFFFFFFFFEull;  // codes 1..62: the LDS code table
@@ -455,49 +460,15 @@ __device__ __forceinline__ uint64_t core_scan_one(const SetCoreDev &f, const uin
   return done ? mask : (mask | f.eof[c]);
 }
 
-// Ascending bitonic sort of the wave's 64 * R keys, key r of lane l being
-// element r * 64 + l: partners 64 or more apart are in the lane's own
-// registers, nearer ones one __shfl_xor away.
-template <int R>
-__device__ __forceinline__ void wave_sort(uint32_t key[R], uint32_t lane) {
-#pragma unroll
-  for (uint32_t k = 2; k <= 64u * R; k <<= 1) {
-#pragma unroll
-    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      if (j >= 64) {
-        const uint32_t jr = j >> 6;
-#pragma unroll
-        for (uint32_t r = 0; r < (uint32_t)R; ++r) {
-          if (r & jr) continue;
-          const bool up = ((r * 64 + lane) & k) == 0;
-          const uint32_t a = key[r], b = key[r | jr];
-          key[r] = up ? min(a, b) : max(a, b);
-          key[r | jr] = up ? max(a, b) : min(a, b);
-        }
-      } else {
-#pragma unroll
-        for (uint32_t r = 0; r < (uint32_t)R; ++r) {
-          const uint32_t o = __shfl_xor(key[r], (int)j);
-          const bool up = ((r * 64 + lane) & k) == 0, lower = (lane & j) == 0;
-          key[r] = (up == lower) ? min(key[r], o) : max(key[r], o);
-        }
-      }
-    }
-  }
-}
-
-// MODE: 0 = fixed stride (one haystack per lane, grid-stride), 1 = offsets.
-// Offset batches: a wave's time per round is its longest lane's, so each wave
-// takes 64 * kCoreRounds haystacks, sorts them by the number of blocks they
-// span (wave_sort) and scans them in kCoreRounds rounds of 64 similar ones
-// (C4's 40-160 byte lines: 66% of the lanes' block steps were useful with one
-// haystack per lane in index order, 95% sorted in groups of 512).
-// (Tried: offsets as one byte stream cut into equal units per lane, each lane
-// scanning the haystacks that start in its unit — equal bytes per lane, but
-// every load of a wave then hits 64 distant regions: C4 1.22 vs 0.79 ms; two
-// haystacks per lane with interleaved chains: 0.72 vs 0.68 ms, the shorter
-// one's chain idles.)
-template <int MODE, int kCoreRounds = 8>
+// MODE: 0 = fixed stride, 1 = offsets; one haystack per lane (grid-stride).
+// Tried on C4 and dropped: offsets as one byte stream cut into equal units per
+// lane, each lane scanning the haystacks that start in its unit (1.22 vs
+// 0.79 ms: every load of a wave hits 64 distant regions); two haystacks per
+// lane with interleaved chains (0.72 vs 0.68 ms: the shorter one's chain
+// idles); each wave sorting 128-512 haystacks by length into rounds of 64
+// similar ones (0.73-0.87 vs 0.68 ms although 80-95% instead of 66% of the
+// lanes' block steps are then useful: the wave's loads spread over more lines).
+template <int MODE, int EXP = 0>
 __global__ __launch_bounds__(1024) void set_core_kernel(BatchDev bt, SetCoreDev f, uint64_t *out) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   for (uint32_t i = threadIdx.x * 16; i < f.lds_bytes; i += blockDim.x * 16)
@@ -507,38 +478,13 @@ __global__ __launch_bounds__(1024) void set_core_kernel(BatchDev bt, SetCoreDev 
   __syncthreads();
   const uint8_t *cls = lds;
   const uint64_t *MT = (const uint64_t *)(lds + f.mt_off);
-  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
-  if (MODE == 0) {
-    for (uint64_t h = tid; h < bt.count; h += nthreads)
-      out[h] = core_scan_one(f, cls, MT, bt.hay + h * bt.stride, bt.length, bt.start, bt.quit_flag);
-    return;
-  }
-  constexpr uint32_t G = 64 * kCoreRounds;  // haystacks per wave and group
-  const uint32_t lane = threadIdx.x & 63;
-  for (uint64_t h0 = (tid >> 6) * G; h0 < bt.count; h0 += (nthreads >> 6) * G) {  // wave-uniform
-    uint32_t key[kCoreRounds];
-#pragma unroll
-    for (int r = 0; r < kCoreRounds; ++r) {
-      const uint64_t h = h0 + r * 64 + lane;
-      uint32_t blocks = 0x7FFFFF;  // past the batch: sorts last
-      if (h < bt.count) {
-        const uint64_t o0 = bt.offs[h], o1 = bt.offs[h + 1];
-        blocks = (uint32_t)min<uint64_t>(((o1 + 15) >> 4) - (o0 >> 4), 0x7FFFFE);
-      }
-      key[r] = blocks << 9 | (r * 64 + lane);
-    }
-    wave_sort<kCoreRounds>(key, lane);
-#pragma unroll 1
-    for (int r = 0; r < kCoreRounds; ++r) {
-      const uint64_t h = h0 + (key[0] & (G - 1));
-      if (h < bt.count) {
-        const uint64_t o0 = bt.offs[h], o1 = bt.offs[h + 1];
-        out[h] = core_scan_one(f, cls, MT, bt.hay + o0, o1 - o0, bt.start, bt.quit_flag);
-      }
-#pragma unroll
-      for (int q = 0; q + 1 < kCoreRounds; ++q) key[q] = key[q + 1];  // next round's key to the front
-    }
+  for (uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; h < bt.count; h += nthreads) {
+    const uint8_t *base;
+    uint64_t len;
+    if (MODE == 0) { base = bt.hay + h * bt.stride; len = bt.length; }
+    else { const uint64_t o0 = bt.offs[h], o1 = bt.offs[h + 1]; base = bt.hay + o0; len = o1 - o0; }
+    out[h] = core_scan_one<EXP>(f, cls, MT, base, len, bt.start, bt.quit_flag);
   }
 }
 
@@ -594,11 +540,18 @@ hipError_t launch_set_cores(const BatchDev &b, const SetCoreDev &f, uint64_t *ou
     hipLaunchKernelGGL(kern, dim3(grid), dim3(bs), f.lds_bytes, st, b, f, out);
     return hipGetLastError();
   };
-  int rounds = 8;
-  if (const char *v = getenv("RURE_AMD_CORE_ROUNDS")) rounds = atoi(v);
-  if (mode == 1 && rounds == 1) return go(set_core_kernel<1, 1>);
-  if (mode == 1 && rounds == 2) return go(set_core_kernel<1, 2>);
-  if (mode == 1 && rounds == 4) return go(set_core_kernel<1, 4>);
+  int exp = 0;
+  if (const char *v = getenv("RURE_AMD_CORE_EXP")) exp = atoi(v);
+  if (mode == 1) switch (exp) {
+    case 1: return go(set_core_kernel<1, 1>);
+    case 16: return go(set_core_kernel<1, 16>);
+    case 2: return go(set_core_kernel<1, 2>);
+    case 3: return go(set_core_kernel<1, 3>);
+    case 4: return go(set_core_kernel<1, 4>);
+    case 5: return go(set_core_kernel<1, 5>);
+    case 7: return go(set_core_kernel<1, 7>);
+    default: break;
+  }
   if (mode == 1) return go(set_core_kernel<1>);
   return go(set_core_kernel<0>);
 }
