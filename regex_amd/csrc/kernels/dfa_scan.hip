@@ -358,7 +358,7 @@ __device__ __forceinline__ uint32_t core_entry(uint32_t t, uint32_t K2, uint32_t
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};                                           \
   const uint32_t KI = 2 * f.K; /* the identity column, doubled */                      \
   uint32_t kc[16];                                                                      \
-  _Pragma("unroll") for (int j = 0; j < 16; ++j) kc[j] = (EXP & 4) ? (((w[j >> 2] >> ((j & 3) * 8)) & 0x3F) << 1) : cls[(w[j >> 2] >> ((j & 3) * 8)) & 0xFF]; \
+  _Pragma("unroll") for (int j = 0; j < 16; ++j) kc[j] = cls[(w[j >> 2] >> ((j & 3) * 8)) & 0xFF]; \
   _Pragma("unroll") for (int j = 0; j < 16; ++j) { /* a select, not a branch per byte */ \
     const bool act = ACTIVE;                                                            \
     kc[j] = act ? kc[j] : KI;                                                           \
@@ -368,7 +368,7 @@ __device__ __forceinline__ uint32_t core_entry(uint32_t t, uint32_t K2, uint32_t
     uint32_t t = c;                                                                     \
     uint64_t bag = 0;                                                                   \
     _Pragma("unroll") for (int j = 0; j < 16; ++j) {                                    \
-      const uint32_t e = core_entry((EXP & 1) ? (t & f.dead) : t, K2, kc[j]);            \
+      const uint32_t e = core_entry(t, K2, kc[j]);                                      \
       bag |= 1ull << (e & 63);                                                          \
       t = e >> 6;                                                                       \
     }                                                                                   \
@@ -389,7 +389,6 @@ __device__ __forceinline__ uint32_t core_entry(uint32_t t, uint32_t K2, uint32_t
     }                                                                                   \
   }
 
-template <int EXP>
 __device__ __forceinline__ bool core_chunk16(uint32_t &c, uint64_t &mask, uint64_t &codes, const SetCoreDev &f,
                                              const uint8_t *cls, uint4 v, bool &quit) {
   RURE_CORE_CHUNK(true)
@@ -403,7 +402,6 @@ __device__ __forceinline__ bool core_chunk16(uint32_t &c, uint64_t &mask, uint64
 // head and the tail of a line (lines start anywhere) cost one pass of the
 // same branch-free lookup chain instead of up to 15 single steps each; the
 // inactive bytes leave the core and the bag unchanged.
-template <int EXP>
 __device__ __forceinline__ bool core_chunk_masked(uint32_t &c, uint64_t &mask, uint64_t &codes, const SetCoreDev &f,
                                                   const uint8_t *cls, uint4 v, uint32_t k0, uint32_t kend,
                                                   bool &quit) {
@@ -415,41 +413,63 @@ __device__ __forceinline__ bool core_chunk_masked(uint32_t &c, uint64_t &mask, u
 }
 #undef RURE_CORE_CHUNK
 
+// byte k (0..15) of a block
+__device__ __forceinline__ uint32_t block_byte(uint4 v, uint32_t k) {
+  const uint32_t q = k >> 2;
+  const uint32_t w = q == 0 ? v.x : q == 1 ? v.y : q == 2 ? v.z : v.w;
+  return (w >> ((k & 3) * 8)) & 0xFF;
+}
+
+// fwd_flag_index (dfa_device.hpp) from the bytes around `at`: prev = text[at-1]
+// (at > 0), cur = text[at] (at < len).
+__device__ __forceinline__ uint32_t fwd_flag_index_bytes(uint64_t len, uint64_t at, uint32_t prev, uint32_t cur) {
+  const bool start = at == 0, end = len == 0;
+  const bool start_line = at == 0 || prev == '\n';
+  const bool wl = at > 0 && word_byte((uint8_t)prev);
+  const bool wn = at < len && word_byte((uint8_t)cur);
+  return (start ? 1u : 0u) | (end ? 2u : 0u) | (start_line ? 4u : 0u) | (end ? 8u : 0u) | (wl != wn ? 16u : 32u) |
+         (wl ? 64u : 0u);
+}
+
 // One haystack's set scan with the core-form tables (the per-lane body of
 // set_core_kernel): head / full / tail 16-byte chunks, the next block's load
-// in flight while one is stepped.
-template <int EXP>
+// in flight while one is stepped.  The caller has loaded (a line ahead) hb =
+// the aligned block holding text[at] and b1 = the block after it (used only
+// if the haystack continues past hb); ST = the start cores in LDS.
 __device__ __forceinline__ uint64_t core_scan_one(const SetCoreDev &f, const uint8_t *cls, const uint64_t *MT,
-                                                  const uint8_t *base, uint64_t len, uint64_t at, uint32_t *qf) {
+                                                  const uint16_t *ST, const uint8_t *base, uint64_t len, uint64_t at,
+                                                  uint4 hb, uint4 b1, uint32_t *qf) {
   uint64_t mask = 0, codes = 0;
   bool quit = false, done;
   uint32_t c;
+  const uint32_t k0 = (uint32_t)((uintptr_t)(base + at) & 15);
   if (at > len) { c = f.dead; done = true; }
-  else { c = f.start[fwd_flag_index(base, len, at)]; done = c == f.dead; }
-  if (!done && at < len && (((uintptr_t)(base + at)) & 15)) {  // head: the rest of one aligned block
-    const uintptr_t a = (uintptr_t)(base + at);
-    const uint32_t k0 = (uint32_t)(a & 15);
+  else {
+    const uint32_t prev = at > 0 ? base[at - 1] : 0u;
+    const uint32_t cur = at < len ? block_byte(hb, k0) : 0u;
+    c = ST[fwd_flag_index_bytes(len, at, prev, cur)];
+    done = c == f.dead;
+  }
+  uint4 cur = hb;
+  if (!done && at < len && k0) {  // head: the rest of one aligned block
     const uint32_t kend = len - at < 16 - k0 ? k0 + (uint32_t)(len - at) : 16;
-    done = core_chunk_masked<EXP>(c, mask, codes, f, cls, *(const uint4 *)(a & ~(uintptr_t)15), k0, kend, quit);
+    done = core_chunk_masked(c, mask, codes, f, cls, hb, k0, kend, quit);
     at += kend - k0;
+    cur = b1;
   }
   // the next block's load is in flight while this one is stepped (the
   // per-lane streams are latency-bound: one round trip per block otherwise).
   // (Tried: 128-byte windows loaded at once, 8 unrolled chunk steps: 1.21 vs
-  // 0.79 ms on C4 — the unrolled chunk code outgrows the instruction cache.)
-  if (EXP & 16) done = true;
-  uint4 cur = make_uint4(0, 0, 0, 0);
-  if (!done && at < len) cur = *(const uint4 *)(base + at);
+  // 0.79 ms on C4.)
   while (!done && at + 16 <= len) {
     uint4 nxt = make_uint4(0, 0, 0, 0);
-    if (!(EXP & 2) && at + 16 < len) nxt = *(const uint4 *)(base + at + 16);
-    if (EXP & 2) nxt = cur;
-    done = core_chunk16<EXP>(c, mask, codes, f, cls, cur, quit);
+    if (at + 16 < len) nxt = *(const uint4 *)(base + at + 16);
+    done = core_chunk16(c, mask, codes, f, cls, cur, quit);
     cur = nxt;
     at += 16;
   }
   if (!done && at < len)  // tail: at is 16-byte aligned here
-    done = core_chunk_masked<EXP>(c, mask, codes, f, cls, cur, 0, (uint32_t)(len - at), quit);
+    done = core_chunk_masked(c, mask, codes, f, cls, cur, 0, (uint32_t)(len - at), quit);
   if (quit) note_quit(qf);
   if (quit) return QUITMARK;
   uint64_t bb = codes & 0x7FFFFFFFFFFFFFFEull;  // codes 1..62: the LDS code table
@@ -468,23 +488,64 @@ __device__ __forceinline__ uint64_t core_scan_one(const SetCoreDev &f, const uin
 // idles); each wave sorting 128-512 haystacks by length into rounds of 64
 // similar ones (0.73-0.87 vs 0.68 ms although 80-95% instead of 66% of the
 // lanes' block steps are then useful: the wave's loads spread over more lines).
-template <int MODE, int EXP = 0>
+// LDS byte offset of the start cores (128 x u16) after the table image
+__host__ __device__ inline uint32_t core_start_off(uint32_t lds_bytes) { return (lds_bytes + 15) & ~15u; }
+
+template <int MODE>
 __global__ __launch_bounds__(1024) void set_core_kernel(BatchDev bt, SetCoreDev f, uint64_t *out) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   for (uint32_t i = threadIdx.x * 16; i < f.lds_bytes; i += blockDim.x * 16)
     *(uint4 *)(lds + i) = *(const uint4 *)(f.lds_image + i);
+  uint16_t *ST = (uint16_t *)(lds + core_start_off(f.lds_bytes));
+  if (threadIdx.x < 128) ST[threadIdx.x] = f.start[threadIdx.x];
   __syncthreads();
   if (threadIdx.x < 256) lds[threadIdx.x] = (uint8_t)(2 * lds[threadIdx.x]);  // class map, doubled (K < 128)
   __syncthreads();
   const uint8_t *cls = lds;
   const uint64_t *MT = (const uint64_t *)(lds + f.mt_off);
   const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; h < bt.count; h += nthreads) {
-    const uint8_t *base;
-    uint64_t len;
-    if (MODE == 0) { base = bt.hay + h * bt.stride; len = bt.length; }
-    else { const uint64_t o0 = bt.offs[h], o1 = bt.offs[h + 1]; base = bt.hay + o0; len = o1 - o0; }
-    out[h] = core_scan_one<EXP>(f, cls, MT, base, len, bt.start, bt.quit_flag);
+  const uint64_t at = bt.start;
+  // A line's prologue is a chain of dependent loads (its offsets, then the
+  // block holding its first byte): the lane loads the offsets two grid
+  // strides ahead and the first two blocks one stride ahead, after the
+  // current line's first body block (vector loads complete in order, so a
+  // wait for that block does not wait for the prefetches), with clamped
+  // addresses and no branches (a load under a branch is waited for at the
+  // branch's end).  The start cores are read from LDS.
+  auto line = [&](uint64_t h, uint64_t &o0, uint64_t &o1) {
+    if (MODE == 0) { o0 = h * bt.stride; o1 = h < bt.count ? o0 + bt.length : o0; return; }
+    const uint64_t hc = h < bt.count ? h : bt.count - 1;
+    o0 = bt.offs[hc];
+    o1 = h < bt.count ? bt.offs[hc + 1] : o0;
+  };
+  // the block holding text[at] and the one after it (if the line continues)
+  auto blocks = [&](uint64_t o0, uint64_t o1, uint4 &b0, uint4 &b1) {
+    const uint8_t *p = bt.hay + o0 + at;
+    const uint8_t *a = p - ((uintptr_t)p & 15);
+    const bool any = at < o1 - o0, more = any && (uint64_t)(a + 16 - p) < o1 - o0 - at;
+    if (MODE == 0) {
+      b0 = b1 = make_uint4(0, 0, 0, 0);
+      if (at < bt.length) { b0 = *(const uint4 *)a; b1 = *(const uint4 *)(more ? a + 16 : a); }
+      return;
+    }
+    const uint4 *q0 = any ? (const uint4 *)a : (const uint4 *)bt.offs;  // offs: 16 readable bytes
+    b0 = *q0;
+    b1 = *(more ? (const uint4 *)(a + 16) : q0);
+  };
+  uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (h >= bt.count) return;
+  uint64_t a0, a1, b0, b1;
+  uint4 x0, x1;
+  line(h, a0, a1);
+  line(h + nthreads, b0, b1);
+  blocks(a0, a1, x0, x1);
+  for (; h < bt.count; h += nthreads) {
+    uint64_t c0, c1;
+    uint4 y0, y1;
+    line(h + 2 * nthreads, c0, c1);
+    blocks(b0, b1, y0, y1);
+    out[h] = core_scan_one(f, cls, MT, ST, bt.hay + a0, a1 - a0, at, x0, x1, bt.quit_flag);
+    a0 = b0; a1 = b1; b0 = c0; b1 = c1; x0 = y0; x1 = y1;
   }
 }
 
@@ -526,32 +587,22 @@ hipError_t launch_set_cores(const BatchDev &b, const SetCoreDev &f, uint64_t *ou
   // as the LDS table allows
   int bs = 1024;
   if (const char *v = getenv("RURE_AMD_CORE_BS")) bs = std::max(64, std::min(1024, atoi(v)));
-  const int per_cu = std::max<int>(1, std::min<int>(2048 / bs, (int)((160u * 1024u) / std::max<uint32_t>(f.lds_bytes, 1))));
+  const int per_cu =
+      std::max<int>(1, std::min<int>(2048 / bs, (int)((160u * 1024u) / (core_start_off(f.lds_bytes) + 256))));
   const int mode = b.offs ? 1 : 0;
   const uint64_t items = b.count;
   const uint64_t blocks = (items + bs - 1) / bs;
   const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)cus * per_cu));
   hipError_t e;
+  const uint32_t lds = core_start_off(f.lds_bytes) + 256;  // + the start cores
   auto go = [&](auto kern) -> hipError_t {
-    if (f.lds_bytes > 64 * 1024 &&
-        (e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)f.lds_bytes)) !=
+    if (lds > 64 * 1024 &&
+        (e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) !=
             hipSuccess)
       return e;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(bs), f.lds_bytes, st, b, f, out);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(bs), lds, st, b, f, out);
     return hipGetLastError();
   };
-  int exp = 0;
-  if (const char *v = getenv("RURE_AMD_CORE_EXP")) exp = atoi(v);
-  if (mode == 1) switch (exp) {
-    case 1: return go(set_core_kernel<1, 1>);
-    case 16: return go(set_core_kernel<1, 16>);
-    case 2: return go(set_core_kernel<1, 2>);
-    case 3: return go(set_core_kernel<1, 3>);
-    case 4: return go(set_core_kernel<1, 4>);
-    case 5: return go(set_core_kernel<1, 5>);
-    case 7: return go(set_core_kernel<1, 7>);
-    default: break;
-  }
   if (mode == 1) return go(set_core_kernel<1>);
   return go(set_core_kernel<0>);
 }
