@@ -436,9 +436,22 @@ __device__ __forceinline__ uint32_t fwd_flag_index_bytes(uint64_t len, uint64_t 
 // in flight while one is stepped.  The caller has loaded (a line ahead) hb =
 // the aligned block holding text[at] and b1 = the block after it (used only
 // if the haystack continues past hb); ST = the start cores in LDS.
+// diagnostic stamps (set_core_kernel's PROF build, RURE_AMD_CORE_PROF=1)
+__device__ __forceinline__ uint64_t core_stamp() {
+  uint64_t t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+
+template <bool PROF, typename PF>
 __device__ __forceinline__ uint64_t core_scan_one(const SetCoreDev &f, const uint8_t *cls, const uint64_t *MT,
-                                                  const uint16_t *ST, const uint8_t *base, uint64_t len, uint64_t at,
-                                                  uint4 hb, uint4 b1, uint32_t *qf) {
+                                                  const uint16_t *ST, const uint64_t *HE, const uint8_t *base,
+                                                  uint64_t len, uint64_t at, uint4 hb, uint4 b1, uint32_t *qf,
+                                                  uint64_t *acc, PF prefetch) {
+  uint64_t t0 = 0;
+  if (PROF) t0 = core_stamp();
   uint64_t mask = 0, codes = 0;
   bool quit = false, done;
   uint32_t c;
@@ -457,6 +470,8 @@ __device__ __forceinline__ uint64_t core_scan_one(const SetCoreDev &f, const uin
     at += kend - k0;
     cur = b1;
   }
+  uint64_t t1 = 0;
+  if (PROF) { t1 = core_stamp(); acc[0] += t1 - t0; }
   // the next block's load is in flight while this one is stepped (the
   // per-lane streams are latency-bound: one round trip per block otherwise).
   // (Tried: 128-byte windows loaded at once, 8 unrolled chunk steps: 1.21 vs
@@ -468,16 +483,26 @@ __device__ __forceinline__ uint64_t core_scan_one(const SetCoreDev &f, const uin
     cur = nxt;
     at += 16;
   }
+  uint64_t t2 = 0;
+  if (PROF) { t2 = core_stamp(); acc[1] += t2 - t1; }
+  // The next lines' prologue loads go out here: vector loads complete in
+  // order, so a wait for any later load would wait for them too, and from here
+  // to the next line's first wait this line issues no more loads.
+  prefetch();
   if (!done && at < len)  // tail: at is 16-byte aligned here
     done = core_chunk_masked(c, mask, codes, f, cls, cur, 0, (uint32_t)(len - at), quit);
   if (quit) note_quit(qf);
   if (quit) return QUITMARK;
+  uint64_t t3 = 0;
+  if (PROF) { t3 = core_stamp(); acc[2] += t3 - t2; }
   uint64_t bb = codes & 0x7FFFFFFFFFFFFFFEull;  // codes 1..62: the LDS code table
   while (bb) {
     mask |= MT[__builtin_ctzll(bb)];
     bb &= bb - 1;
   }
-  return done ? mask : (mask | f.eof[c]);
+  const uint64_t r = done ? mask : (mask | (c < f.hot ? HE[c] : f.eof[c]));
+  if (PROF) { (void)__builtin_amdgcn_readfirstlane((uint32_t)r); acc[3] += core_stamp() - t3; }
+  return r;
 }
 
 // MODE: 0 = fixed stride, 1 = offsets; one haystack per lane (grid-stride).
@@ -488,16 +513,24 @@ __device__ __forceinline__ uint64_t core_scan_one(const SetCoreDev &f, const uin
 // idles); each wave sorting 128-512 haystacks by length into rounds of 64
 // similar ones (0.73-0.87 vs 0.68 ms although 80-95% instead of 66% of the
 // lanes' block steps are then useful: the wave's loads spread over more lines).
-// LDS byte offset of the start cores (128 x u16) after the table image
+// LDS byte offset of the start cores (128 x u16) after the table image; the
+// hot cores' EOF masks follow them
 __host__ __device__ inline uint32_t core_start_off(uint32_t lds_bytes) { return (lds_bytes + 15) & ~15u; }
+__host__ __device__ inline uint32_t core_lds_total(uint32_t lds_bytes, uint32_t hot) {
+  return core_start_off(lds_bytes) + 256 + 8 * hot;
+}
 
-template <int MODE>
-__global__ __launch_bounds__(1024) void set_core_kernel(BatchDev bt, SetCoreDev f, uint64_t *out) {
+template <int MODE, bool PROF = false>
+__global__ __launch_bounds__(1024) void set_core_kernel(BatchDev bt, SetCoreDev f, uint64_t *out,
+                                                        uint64_t *prof = nullptr) {
+  uint64_t acc[5] = {0, 0, 0, 0, 0};
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   for (uint32_t i = threadIdx.x * 16; i < f.lds_bytes; i += blockDim.x * 16)
     *(uint4 *)(lds + i) = *(const uint4 *)(f.lds_image + i);
   uint16_t *ST = (uint16_t *)(lds + core_start_off(f.lds_bytes));
+  uint64_t *HE = (uint64_t *)(lds + core_start_off(f.lds_bytes) + 256);
   if (threadIdx.x < 128) ST[threadIdx.x] = f.start[threadIdx.x];
+  for (uint32_t i = threadIdx.x; i < f.hot; i += blockDim.x) HE[i] = f.eof[i];
   __syncthreads();
   if (threadIdx.x < 256) lds[threadIdx.x] = (uint8_t)(2 * lds[threadIdx.x]);  // class map, doubled (K < 128)
   __syncthreads();
@@ -512,11 +545,12 @@ __global__ __launch_bounds__(1024) void set_core_kernel(BatchDev bt, SetCoreDev 
   // wait for that block does not wait for the prefetches), with clamped
   // addresses and no branches (a load under a branch is waited for at the
   // branch's end).  The start cores are read from LDS.
+  // (past the batch: the last line's offsets, never scanned)
   auto line = [&](uint64_t h, uint64_t &o0, uint64_t &o1) {
-    if (MODE == 0) { o0 = h * bt.stride; o1 = h < bt.count ? o0 + bt.length : o0; return; }
     const uint64_t hc = h < bt.count ? h : bt.count - 1;
+    if (MODE == 0) { o0 = hc * bt.stride; o1 = o0 + bt.length; return; }
     o0 = bt.offs[hc];
-    o1 = h < bt.count ? bt.offs[hc + 1] : o0;
+    o1 = bt.offs[hc + 1];
   };
   // the block holding text[at] and the one after it (if the line continues)
   auto blocks = [&](uint64_t o0, uint64_t o1, uint4 &b0, uint4 &b1) {
@@ -542,10 +576,19 @@ __global__ __launch_bounds__(1024) void set_core_kernel(BatchDev bt, SetCoreDev 
   for (; h < bt.count; h += nthreads) {
     uint64_t c0, c1;
     uint4 y0, y1;
-    line(h + 2 * nthreads, c0, c1);
-    blocks(b0, b1, y0, y1);
-    out[h] = core_scan_one(f, cls, MT, ST, bt.hay + a0, a1 - a0, at, x0, x1, bt.quit_flag);
+    auto prefetch = [&]() {
+      uint64_t tl = 0;
+      if (PROF) tl = core_stamp();
+      line(h + 2 * nthreads, c0, c1);
+      blocks(b0, b1, y0, y1);
+      if (PROF) acc[4] += core_stamp() - tl;
+    };
+    out[h] = core_scan_one<PROF>(f, cls, MT, ST, HE, bt.hay + a0, a1 - a0, at, x0, x1, bt.quit_flag, acc, prefetch);
     a0 = b0; a1 = b1; b0 = c0; b1 = c1; x0 = y0; x1 = y1;
+  }
+  if (PROF && (threadIdx.x & 63) == 0) {
+    const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    for (int k = 0; k < 5; ++k) prof[w * 5 + k] = acc[k];
   }
 }
 
@@ -588,21 +631,41 @@ hipError_t launch_set_cores(const BatchDev &b, const SetCoreDev &f, uint64_t *ou
   int bs = 1024;
   if (const char *v = getenv("RURE_AMD_CORE_BS")) bs = std::max(64, std::min(1024, atoi(v)));
   const int per_cu =
-      std::max<int>(1, std::min<int>(2048 / bs, (int)((160u * 1024u) / (core_start_off(f.lds_bytes) + 256))));
+      std::max<int>(1, std::min<int>(2048 / bs, (int)((160u * 1024u) / core_lds_total(f.lds_bytes, f.hot))));
   const int mode = b.offs ? 1 : 0;
   const uint64_t items = b.count;
   const uint64_t blocks = (items + bs - 1) / bs;
   const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)cus * per_cu));
   hipError_t e;
-  const uint32_t lds = core_start_off(f.lds_bytes) + 256;  // + the start cores
+  const uint32_t lds = core_lds_total(f.lds_bytes, f.hot);  // + the start cores and hot EOF masks
   auto go = [&](auto kern) -> hipError_t {
     if (lds > 64 * 1024 &&
         (e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) !=
             hipSuccess)
       return e;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(bs), lds, st, b, f, out);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(bs), lds, st, b, f, out, (uint64_t *)nullptr);
     return hipGetLastError();
   };
+  if (mode == 1 && getenv("RURE_AMD_CORE_PROF")) {  // diagnostic: per-phase clock stamps
+    const uint64_t nw = (uint64_t)grid * bs / 64;
+    uint64_t *prof = nullptr;
+    if ((e = hipMalloc(&prof, nw * 5 * 8)) != hipSuccess) return e;
+    (void)hipMemsetAsync(prof, 0, nw * 5 * 8, st);
+    auto kern = set_core_kernel<1, true>;
+    if ((e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess)
+      return e;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(bs), lds, st, b, f, out, prof);
+    std::vector<uint64_t> hp(nw * 5);
+    (void)hipMemcpyAsync(hp.data(), prof, nw * 5 * 8, hipMemcpyDeviceToHost, st);
+    (void)hipStreamSynchronize(st);
+    (void)hipFree(prof);
+    double sum[5] = {0, 0, 0, 0, 0};
+    for (uint64_t w = 0; w < nw; ++w)
+      for (int k = 0; k < 5; ++k) sum[k] += (double)hp[w * 5 + k];
+    fprintf(stderr, "core_prof per wave (memtime ticks): prologue+head %.0f body %.0f tail %.0f finish %.0f prefetch %.0f\n",
+            sum[0] / nw, sum[1] / nw, sum[2] / nw, sum[3] / nw, sum[4] / nw);
+    return hipGetLastError();
+  }
   if (mode == 1) return go(set_core_kernel<1>);
   return go(set_core_kernel<0>);
 }
