@@ -495,10 +495,17 @@ __device__ __forceinline__ uint64_t core_scan_one(const SetCoreDev &f, const uin
   if (quit) return QUITMARK;
   uint64_t t3 = 0;
   if (PROF) { t3 = core_stamp(); acc[2] += t3 - t2; }
-  uint64_t bb = codes & 0x7FFFFFFFFFFFFFFEull;  // codes 1..62: the LDS code table
+  // codes 1..62: the LDS code table, four lookups in flight per round (MT[0]
+  // is 0: a lane out of codes reads it)
+  uint64_t bb = codes & 0x7FFFFFFFFFFFFFFEull;
   while (bb) {
-    mask |= MT[__builtin_ctzll(bb)];
-    bb &= bb - 1;
+    uint32_t i[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      i[q] = bb ? (uint32_t)__builtin_ctzll(bb) : 0u;
+      bb &= bb - 1;
+    }
+    mask |= MT[i[0]] | MT[i[1]] | MT[i[2]] | MT[i[3]];
   }
   const uint64_t r = done ? mask : (mask | (c < f.hot ? HE[c] : f.eof[c]));
   if (PROF) { (void)__builtin_amdgcn_readfirstlane((uint32_t)r); acc[3] += core_stamp() - t3; }
