@@ -220,7 +220,8 @@ def profiled_traffic(config, b_alg):
     PMC pass of this same command (profiles/<tag>_summary.json, written by
     tools/gpu_profile.sh + tools/summarize_profile.py: FETCH_SIZE KB x 1024 x 2,
     MI355X_MICROARCH.md HBM section).  PMC counters cannot be read from inside
-    the timed process, so the newest summary whose workload matches is used."""
+    the timed process, so the newest summary whose workload matches is used
+    (by its `generated_utc` stamp: file times do not survive a checkout)."""
     import glob
     best = None
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json"))):
@@ -231,8 +232,9 @@ def profiled_traffic(config, b_alg):
         strip = lambda c: {k: v for k, v in (c or {}).items() if k != "parallelism"}
         if strip(d.get("bench_config")) != strip(config) or not d.get("hbm_read_bytes_per_launch"):
             continue
-        if best is None or os.path.getmtime(p) >= best[0]:
-            best = (os.path.getmtime(p), p, d)
+        key = (d.get("generated_utc", ""), os.path.basename(p))
+        if best is None or key >= best[0]:
+            best = (key, p, d)
     if best is None:
         return None
     d = best[2]

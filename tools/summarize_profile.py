@@ -27,8 +27,10 @@ def main(tag, kernel_substr="rure_amd::"):
     bench = json.loads(open(os.path.join(src, "bench_trace.json")).read().strip().splitlines()[-1])
     roof = bench.get("roofline", {})
     alg = roof.get("alg_bytes_per_launch")
+    import datetime
     out = {
         "tag": tag,
+        "generated_utc": datetime.datetime.now(datetime.timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ"),
         "kernel": ks[0]["Name"] if ks else None,
         "calls": int(ks[0]["Calls"]) if ks else 0,
         "avg_ns": float(ks[0]["AverageNs"]) if ks else None,
