@@ -215,7 +215,7 @@ def _short_kernel(name):
     return re.sub(r"\((rure_amd::BatchDev|unsigned|int|long|void\*).*$", "", name).replace("void ", "")
 
 
-def profiled_traffic(config, b_alg):
+def profiled_traffic(config, b_alg, kernel=None):
     """HBM bytes per launch of the scan kernel from the committed rocprofv3
     PMC pass of this same command (profiles/<tag>_summary.json, written by
     tools/gpu_profile.sh + tools/summarize_profile.py: FETCH_SIZE KB x 1024 x 2,
@@ -231,6 +231,8 @@ def profiled_traffic(config, b_alg):
             continue
         strip = lambda c: {k: v for k, v in (c or {}).items() if k != "parallelism"}
         if strip(d.get("bench_config")) != strip(config) or not d.get("hbm_read_bytes_per_launch"):
+            continue
+        if kernel is not None and kernel not in (d.get("kernel") or ""):
             continue
         key = (d.get("generated_utc", ""), os.path.basename(p))
         if best is None or key >= best[0]:
@@ -527,6 +529,13 @@ def run_c3(ctx):
                     strip_matches=nsp_sharded, variant_counts=got, known_answers_ok=ok,
                     cut_recomputations=stats["recomputed"], roofline=roofline_c3(my_bytes - (N + W - 1) // W,
                                                                                  var_ms, len(variants), config),
+                    roofline_strip=roofline_c3_strip((N + W - 1) // W, strip_ms, config),
+                    roofline_step={"bound": "hbm", "achieved": round(my_bytes / sec / 1e9, 1),
+                                   "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                   "frac": round(my_bytes / sec / 1e9 / HBM_PEAK_GBS, 4),
+                                   "ms": round(sec * 1e3, 4), "alg_bytes_per_step": int(my_bytes),
+                                   "what": "whole step: strip pass + 9 variant passes (+ exit exchange), "
+                                           "driver-visible time incl. launch gaps"},
                     **extra)
 
 
@@ -543,7 +552,23 @@ def roofline_c3(var_bytes, var_ms, nvar, config):
          "frac": round(a / HBM_PEAK_GBS, 4), "traffic": None, "kernel_ms": round(ms, 4),
          "alg_bytes_per_launch": int(per),
          "kernel": "variant find_iter pass (iter_spec_sa_tile_kernel + fix/emit/count kernels)"}
-    tr = profiled_traffic(config, per)
+    tr = profiled_traffic(config, per, kernel="iter_spec_sa_tile")
+    if tr is not None:
+        r["traffic"] = tr["bytes"]
+        r["traffic_source"] = tr["source"]
+    return r
+
+
+def roofline_c3_strip(strip_bytes, strip_ms, config):
+    """The strip pass (lexer engine: iter_spec_lex_tile_kernel + its tail,
+    fix, emit and count kernels): algorithmic bytes = the raw text; traffic =
+    HBM bytes per launch of the lexer kernel from the committed PMC pass."""
+    a = strip_bytes / strip_ms / 1e6
+    r = {"bound": "hbm", "achieved": round(a, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": round(a / HBM_PEAK_GBS, 4), "traffic": None, "kernel_ms": round(strip_ms, 4),
+         "alg_bytes_per_launch": int(strip_bytes),
+         "kernel": "strip find_iter pass (iter_spec_lex_tile_kernel + tail/fix/emit/count kernels)"}
+    tr = profiled_traffic(config, strip_bytes, kernel="iter_spec_lex_tile")
     if tr is not None:
         r["traffic"] = tr["bytes"]
         r["traffic_source"] = tr["source"]

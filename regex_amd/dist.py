@@ -47,6 +47,9 @@ def gather_records(rec, group=None):
 def _all_gather_flat(out, inp, group=None):
     """all_gather into one (world * rows, ...) tensor (no per-part copies);
     backends without the flat collective get the list form."""
+    if not dist.is_initialized():  # one process, no group: the gather is a copy
+        out.copy_(inp)
+        return
     try:
         dist.all_gather_into_tensor(out, inp, group=group)
     except (RuntimeError, NotImplementedError, AttributeError):
@@ -64,7 +67,7 @@ class RecordGather(object):
 
     def __init__(self, capacity, device, group=None):
         self.group = group
-        self.world = dist.get_world_size(group)
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.cap = int(capacity)
         self.send = torch.zeros((self.cap + 1, 3), dtype=torch.int64, device=device)
         self.recv = torch.empty((self.world * (self.cap + 1), 3), dtype=torch.int64, device=device)
