@@ -2,6 +2,9 @@
 #include "dfa_build.hpp"
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <unordered_map>
@@ -41,6 +44,7 @@ class Builder {
   }
 
   bool build(DenseDfa *out, std::string *err) {
+    const auto t_begin = std::chrono::steady_clock::now();
     // raw state 0 = DEAD, raw state 1 = QUIT (always allocated, maybe unused)
     keys_.push_back(std::string());
     keys_.push_back(std::string());
@@ -84,13 +88,14 @@ class Builder {
         }
         core_.emplace(key.substr(0, cut), s);
       }
-      for (int c = 0; c < ncls; ++c) trans_cls_[s * ncls + c] = step(key, rep[c]);
+      step_row(key, ncls, rep, &trans_cls_[s * ncls]);
       uint64_t mask = 0;
       bool m = step_eof(key, &mask);
       eof_match_.push_back(m ? 1 : 0);
       eof_mask_.push_back(mask);
     }
     const int nraw = (int)keys_.size();
+    const auto t_built = std::chrono::steady_clock::now();
     // Expand to 256 columns (QUIT override for non-ASCII bytes when the
     // program has a Unicode word boundary, dfa.rs:1487-1496).
     std::vector<uint32_t> t256((size_t)nraw * 256);
@@ -100,6 +105,12 @@ class Builder {
             (quit_ && b >= 0x80 && s != 0) ? 1u : trans_cls_[(size_t)s * ncls + p_.byte_classes[b]];
     minimise(nraw, t256, out);
     out->raw_states = nraw;
+    if (getenv("RURE_AMD_TIMING")) {  // diagnostic: construction and minimisation times
+      const auto t_end = std::chrono::steady_clock::now();
+      fprintf(stderr, "dfa_build: %d raw states, %d classes, %d states: construct %.3f s, minimise %.3f s\n", nraw,
+              ncls, out->nstates, std::chrono::duration<double>(t_built - t_begin).count(),
+              std::chrono::duration<double>(t_end - t_built).count());
+    }
     return true;
   }
 
@@ -147,6 +158,30 @@ class Builder {
         case OP_SPLIT: stack_.push_back(in.y); stack_.push_back(in.x); break;
       }
     }
+  }
+
+  // follow(ip, q, ef2) for the step's flags (only start_line varies: the
+  // byte is '\n' or not) from a cached closure list: within one step q is a
+  // union of closures under the same flags, so an ip already in q has its
+  // whole closure in q, and the DFS that stops at such ips adds exactly the
+  // closure's other ips in the closure's own DFS order.
+  std::vector<std::vector<uint32_t>> closure_[2];
+  std::vector<uint8_t> closure_done_[2];
+  void follow_cached(uint32_t ip, SparseSet &q, int nl) {
+    if (closure_done_[nl].empty()) {
+      closure_done_[nl].assign(p_.insts.size(), 0);
+      closure_[nl].resize(p_.insts.size());
+    }
+    if (!closure_done_[nl][ip]) {
+      SparseSet tmp(p_.insts.size() + 1);
+      EmptyFlags ef;
+      ef.start_line = nl != 0;
+      follow(ip, tmp, ef);
+      closure_[nl][ip].assign(tmp.dense.begin(), tmp.dense.begin() + tmp.n);
+      closure_done_[nl][ip] = 1;
+    }
+    for (uint32_t x : closure_[nl][ip])
+      if (!q.contains(x)) q.insert(x);
   }
 
   // dfa.rs:1196-1244 plus interning; returns raw id (0 = DEAD).  `now`
@@ -260,13 +295,61 @@ class Builder {
         // far fewer states (no subset-of-patterns-seen in the state).
         if (is_set_ && in.x < 64) m_now |= 1ull << in.x;
       } else if (in.op == OP_BYTES) {
-        if (b < 256 && in.lo <= b && b <= in.hi) follow(in.x, *qnext, ef2);
+        if (b < 256 && in.lo <= b && b <= in.hi) follow_cached(in.x, *qnext, ef2.start_line ? 1 : 0);
       }
     }
     if (b == 256 && is_set_) std::swap(qcur, qnext);  // dfa.rs:1004-1015
     *res = qnext;
     *sf = sflags;
     if (now) *now = m_now;
+  }
+
+  // One state's row over the byte classes.  The step on byte b depends only
+  // on b's '\n'-ness and word-ness (the look-around flags) and on which Byte
+  // instructions of the (flag-dependent) thread list accept b; classes that
+  // agree on all of that share one exec (Unicode classes: a state's hundreds
+  // of UTF-8 range instructions split the 100+ classes into few groups).
+  void step_row(const std::string &key, int ncls, const uint8_t *rep, uint32_t *row) {
+    const uint8_t flags = (uint8_t)key[0];
+    std::unordered_map<std::string, uint32_t> memo;
+    std::vector<std::string> sig(ncls);
+    for (int combo = 0; combo < 4; ++combo) {
+      const bool nl = combo & 1, w = (combo >> 1) & 1;
+      bool any = false;
+      for (int c = 0; c < ncls && !any; ++c)
+        any = (rep[c] == '\n') == nl && is_word_byte(rep[c]) == w;
+      if (!any) continue;
+      // the thread list the byte instructions are read from (exec's first
+      // follow when the state holds empty-width instructions)
+      SparseSet &q = qa_;
+      load(key, q);
+      if (flags & SF_EMPTY) {
+        EmptyFlags ef;
+        if (nl) ef.end_line = true;
+        if (((flags & SF_WORD) != 0) == w) ef.nwb = true; else ef.wb = true;
+        qb_.clear();
+        for (size_t k = 0; k < q.n; ++k) follow(q.dense[k], qb_, ef);
+        std::swap(qa_, qb_);
+      }
+      SparseSet &qq = qa_;
+      for (int c = 0; c < ncls; ++c) sig[c].clear();
+      for (size_t k = 0; k < qq.n; ++k) {
+        const Inst &in = p_.insts[qq.dense[k]];
+        if (in.op == OP_MATCH && !cont_) break;
+        if (in.op != OP_BYTES) continue;
+        const int c0 = p_.byte_classes[in.lo], c1 = p_.byte_classes[in.hi];
+        for (int c = c0; c <= c1; ++c) sig[c].append((const char *)&k, 4);
+      }
+      for (int c = 0; c < ncls; ++c) {
+        if ((rep[c] == '\n') != nl || is_word_byte(rep[c]) != w) continue;
+        sig[c].push_back((char)combo);
+        auto it = memo.find(sig[c]);
+        if (it != memo.end()) { row[c] = it->second; continue; }
+        const uint32_t t = step(key, rep[c]);
+        memo.emplace(sig[c], t);
+        row[c] = t;
+      }
+    }
   }
 
   uint32_t step(const std::string &key, uint8_t b) {
