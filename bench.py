@@ -62,6 +62,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive measurement (C2)")
     ap.add_argument("--no-parity", action="store_true", help="skip the whole-batch oracle check (C2)")
+    ap.add_argument("--c3-separate", action="store_true",
+                    help="C3: one find_iter pass per variant instead of the fused multi-regex pass")
     return ap.parse_args()
 
 
@@ -482,9 +484,27 @@ def run_c3(ctx):
     def strip_pass():
         span_raw(0, rk, None)
 
+    # the 9 variants over the rank's span in one call: they are all finite
+    # sets of 8-byte strings, so rure_amd_find_iter_span_multi reads the
+    # stream once for all of them (each variant's matches, count and exit are
+    # exactly its own find_iter_span's: tests/test_gpu_multi.py)
+    VP = ctypes.c_void_p
+    nv = P - 1
+    m_res = (VP * nv)(*[passes[j][0]._re for j in range(1, P)])
+    m_cnt = (VP * nv)(*[VP(pcount[j:].data_ptr()) for j in range(1, P)])
+    m_out = (VP * nv)(*[VP(passes[j][3].data_ptr()) for j in range(1, P)])
+    m_cap = (ctypes.c_size_t * nv)(*[passes[j][3].shape[0] for j in range(1, P)])
+    m_exit = (VP * nv)(*[VP(pexit[j].data_ptr()) for j in range(1, P)])
+    v_lo, v_hi = span_bounds(M, W, rk)
+
     def variant_pass():
-        for j in range(1, P):
-            span_raw(j, rk, None)
+        if ctx.args.c3_separate:
+            for j in range(1, P):
+                span_raw(j, rk, None)
+            return
+        rc = NN.rure_amd_find_iter_span_multi(m_res, nv, VP(seq.data_ptr()), M, v_lo, v_hi, None, m_cnt, m_out,
+                                              m_cap, m_exit, sp)
+        assert rc == 0
 
     def step():
         strip_pass()
@@ -527,8 +547,10 @@ def run_c3(ctx):
                     variant_passes_ms=round(var_ms, 3),
                     variant_GBps=round((my_bytes - (N + W - 1) // W) / var_ms / 1e6, 1),
                     strip_matches=nsp_sharded, variant_counts=got, known_answers_ok=ok,
+                    variant_engine="separate passes" if ctx.args.c3_separate else "one fused pass",
                     cut_recomputations=stats["recomputed"], roofline=roofline_c3(my_bytes - (N + W - 1) // W,
-                                                                                 var_ms, len(variants), config),
+                                                                                 var_ms, len(variants), config,
+                                                                                 fused=not ctx.args.c3_separate),
                     roofline_strip=roofline_c3_strip((N + W - 1) // W, strip_ms, config),
                     roofline_step={"bound": "hbm", "achieved": round(my_bytes / sec / 1e9, 1),
                                    "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -539,20 +561,24 @@ def run_c3(ctx):
                     **extra)
 
 
-def roofline_c3(var_bytes, var_ms, nvar, config):
-    """Pass-level roofline of one variant find_iter pass (the Shift-And
-    spec kernel plus its fix/emit/count kernels, HIP events on the launch
-    stream): algorithmic bytes = the stripped span one pass reads.  traffic =
-    HBM bytes per launch of the spec kernel (only the variant passes run it)
-    from the committed PMC pass of this command."""
+def roofline_c3(var_bytes, var_ms, nvar, config, fused=True):
+    """Roofline of the variant phase (HIP events on the launch stream).
+    Fused (default): one Shift-And pass reads the stripped span once for all
+    variants (iter_spec_sa_multi_tile_kernel), then each variant's fix / emit
+    / count kernels: algorithmic bytes = the span, time = the whole phase.
+    Separate (--c3-separate): one pass per variant, figures per pass.
+    traffic = HBM bytes per launch of the spec kernel from the committed PMC
+    pass of this command."""
     per = var_bytes / nvar
-    ms = var_ms / nvar
+    ms = var_ms if fused else var_ms / nvar
     a = per / ms / 1e6
     r = {"bound": "hbm", "achieved": round(a, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
          "frac": round(a / HBM_PEAK_GBS, 4), "traffic": None, "kernel_ms": round(ms, 4),
          "alg_bytes_per_launch": int(per),
-         "kernel": "variant find_iter pass (iter_spec_sa_tile_kernel + fix/emit/count kernels)"}
-    tr = profiled_traffic(config, per, kernel="iter_spec_sa_tile")
+         "kernel": ("variant phase: one fused pass (iter_spec_sa_multi_tile_kernel) + per-variant "
+                    "fix/emit/count kernels" if fused else
+                    "variant find_iter pass (iter_spec_sa_tile_kernel + fix/emit/count kernels)")}
+    tr = profiled_traffic(config, per, kernel="iter_spec_sa_multi_tile" if fused else "iter_spec_sa_tile")
     if tr is not None:
         r["traffic"] = tr["bytes"]
         r["traffic_source"] = tr["source"]

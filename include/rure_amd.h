@@ -180,6 +180,17 @@ typedef struct rure_amd_iter_state {
 int rure_amd_find_iter_span(rure *re, const uint8_t *haystack, size_t length, size_t lo, size_t hi,
                             const rure_amd_iter_state *entry, uint64_t *count, rure_match *matches,
                             size_t capacity, rure_amd_iter_state *exit, void *stream);
+/* rure_amd_find_iter_span for n regexes over the same span [lo, hi) of one
+ * haystack: regex i's results go to count[i], matches[i] (capacity[i]
+ * records) and exit[i], entered with entry[i] (NULL entry array or element:
+ * a fresh start) — host arrays of device pointers; each regex's output is
+ * exactly its own rure_amd_find_iter_span's.  Regexes that are finite sets of
+ * strings of one common length (the regex-dna variants) are scanned together
+ * in one pass over the text; otherwise each runs its own pass. */
+int rure_amd_find_iter_span_multi(rure *const *res, size_t n, const uint8_t *haystack, size_t length, size_t lo,
+                                  size_t hi, const rure_amd_iter_state *const *entry, uint64_t *const *count,
+                                  rure_match *const *matches, const size_t *capacity,
+                                  rure_amd_iter_state *const *exit, void *stream);
 
 /* Batched replacen with a literal replacement (bytes::Regex::replacen's
  * no-expansion path, re_bytes.rs:489-512): in every haystack the first

@@ -601,6 +601,43 @@ class Regex(object):
         return info, trans.reshape(n, 256), eof, start
 
 
+def find_iter_span_multi(regexes, haystack, lo, hi, length=None, entries=None, capacities=None, stream=None):
+    """Regex.find_iter_span for several regexes over the same span [lo, hi)
+    (rure_amd_find_iter_span_multi: finite string sets of one common length,
+    e.g. the regex-dna variants, are scanned in one pass over the text).
+    entries: None or a list of (3,) device exits (None items: fresh starts).
+    Returns [(count, matches, exit), ...] in the order of `regexes`, each
+    exactly what that regex's find_iter_span returns.  With capacities given
+    the outputs are not resized (a count above its capacity: truncated)."""
+    import torch
+    k = len(regexes)
+    dev = haystack.device
+    n = haystack.numel() if length is None else length
+    caps = list(capacities) if capacities is not None else [max(1024, (hi - lo) // 64)] * k
+    counts = [torch.zeros((1,), dtype=torch.int64, device=dev) for _ in range(k)]
+    exits = [torch.empty((3,), dtype=torch.int64, device=dev) for _ in range(k)]
+    VP = ctypes.c_void_p
+    res = (VP * k)(*[r._re for r in regexes])
+    ent = None
+    if entries is not None:
+        ent = (VP * k)(*[VP(e.data_ptr()) if e is not None else None for e in entries])
+    while True:
+        outs = [torch.empty((max(c, 1), 2), dtype=torch.int64, device=dev) for c in caps]
+        _check(N.rure_amd_find_iter_span_multi(res, k, VP(haystack.data_ptr()), n, lo, hi, ent,
+                                               (VP * k)(*[VP(c.data_ptr()) for c in counts]),
+                                               (VP * k)(*[VP(o.data_ptr()) for o in outs]),
+                                               (ctypes.c_size_t * k)(*caps),
+                                               (VP * k)(*[VP(x.data_ptr()) for x in exits]), _stream_ptr(stream)),
+               "find_iter_span_multi")
+        if capacities is not None:
+            return [(counts[i], outs[i], exits[i]) for i in range(k)]
+        (stream or torch.cuda.current_stream()).synchronize()
+        tot = [int(c.item()) for c in counts]
+        if all(t <= c for t, c in zip(tot, caps)):
+            return [(counts[i], outs[i][: tot[i]], exits[i]) for i in range(k)]
+        caps = [max(t, c) for t, c in zip(tot, caps)]
+
+
 def _read_caps(caps):
     out = []
     m = N.RureMatch()

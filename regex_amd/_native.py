@@ -141,6 +141,8 @@ rure_amd_find_iter_batch = _sig("rure_amd_find_iter_batch", ctypes.c_int, VP, ct
                                 c_size, VP, VP)
 rure_amd_find_iter_span = _sig("rure_amd_find_iter_span", ctypes.c_int, VP, VP, c_size, c_size, c_size, VP, VP,
                                VP, c_size, VP, VP)
+rure_amd_find_iter_span_multi = _sig("rure_amd_find_iter_span_multi", ctypes.c_int, VP, c_size, VP, c_size, c_size,
+                                     c_size, VP, VP, VP, VP, VP, VP)
 rure_amd_literals_export = _sig("rure_amd_literals_export", ctypes.c_int64, VP, VP, VP, c_size)
 rure_amd_shiftand_export = _sig("rure_amd_shiftand_export", ctypes.c_int64, VP, VP, VP, VP, VP)
 rure_amd_uses_dfa = _sig("rure_amd_uses_dfa", ctypes.c_int, VP)

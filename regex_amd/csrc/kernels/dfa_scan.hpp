@@ -211,6 +211,11 @@ struct IterSpan {
 hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaDev &r, const NfaDev *nf,
                             bool chunked, uint64_t chunk, const IterOut &o, hipStream_t st, int cus,
                             const IterSpan *span = nullptr);
+// Several Shift-And regexes over one span in one speculative pass, then each
+// regex's own passes; hipErrorNotSupported (nothing launched) if they do not
+// qualify (iter_scan.hip).
+hipError_t launch_find_iter_multi(const BatchDev &b, int nre, const FwdDfaDev *const *f, const RevDfaDev *const *r,
+                                  uint64_t chunk, const IterOut *o, hipStream_t st, int cus, const IterSpan *spn);
 
 // One search per haystack over few long fixed-stride haystacks, chunked
 // (iter_scan.hip); f must be the find_iter DFA (with strip).

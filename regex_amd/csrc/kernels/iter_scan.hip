@@ -25,6 +25,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <rocprim/rocprim.hpp>
+#include <vector>
 #include <stdint.h>
 
 #include "dfa_device.hpp"
@@ -785,6 +786,238 @@ __global__ __launch_bounds__(256) void iter_spec_sa_tile_kernel(BatchDev b, Geo 
   }
 }
 
+// ------------------------------------------------------------------------
+// Several Shift-And regexes over one text in one pass (rure_amd_find_iter_
+// span_multi; regex-dna's 9 variants read the stripped stream once instead of
+// 9 times).  Every regex keeps its own bits (packed into NW 64-bit words: a
+// word's sequences step together, the init bits re-arm each sequence's first
+// bit whatever the previous one shifted in), its own greedy iteration state
+// and its own unit records, so the per-regex passes after this one (fix,
+// walk, emit) are unchanged and each regex's matches are exactly its own
+// find_iter's.  All regexes share one string length L and the unit geometry.
+constexpr int kSaMultiMax = 12;
+struct SaMulti {
+  uint64_t *image;                    // [256][NW] combined masks (device, built by sa_multi_image_kernel)
+  uint64_t init[4], facc[4];          // per word: init bits, final bits of all its regexes
+  uint64_t len;                       // the common string length L
+  uint32_t nre;
+  uint32_t word[kSaMultiMax];         // word of regex x
+  uint32_t shift[kSaMultiMax];        // bit offset of regex x in its word
+  uint64_t fin[kSaMultiMax];          // final bits of regex x (in its word)
+  uint32_t nonempty[kSaMultiMax];
+  const uint64_t *sa_image[kSaMultiMax];  // each regex's own 256 masks
+  Unit *units[kSaMultiMax];
+  uint64_t *slots[kSaMultiMax];
+  uint32_t *counts[kSaMultiMax];
+  uint32_t *dirty[kSaMultiMax];
+};
+
+template <int NW>
+__global__ void sa_multi_image_kernel(SaMulti m) {
+  const uint32_t c = threadIdx.x;  // 256 threads: one byte value each
+  uint64_t wv[NW];
+#pragma unroll
+  for (int x = 0; x < NW; ++x) wv[x] = 0;
+  for (uint32_t q = 0; q < m.nre; ++q) {
+    const uint64_t v = m.sa_image[q][c] << m.shift[q];
+#pragma unroll
+    for (int x = 0; x < NW; ++x)
+      if (m.word[q] == (uint32_t)x) wv[x] |= v;
+  }
+#pragma unroll
+  for (int x = 0; x < NW; ++x) m.image[c * NW + x] = wv[x];
+}
+
+// sa_block for every regex of the pass: the bits of 16 bytes (k0..kend) and,
+// in the rare block holding string ends, each regex's greedy iteration.
+template <int NW>
+__device__ __forceinline__ void sam_block(uint64_t (&D)[NW], const uint64_t *B, const SaMulti &m, const uint32_t w[4],
+                                          uint32_t k0, uint32_t kend, int64_t bp, uint64_t c1,
+                                          uint64_t (&p)[kSaMultiMax], uint64_t (&lm)[kSaMultiMax],
+                                          uint32_t (&n)[kSaMultiMax], uint64_t u, uint32_t nslots) {
+  uint64_t D0[NW];
+  uint64_t acc = 0;
+#pragma unroll
+  for (int x = 0; x < NW; ++x) D0[x] = D[x];
+  if (k0 == 0 && kend == 16) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const uint64_t *row = B + ((w[j >> 2] >> (8 * (j & 3))) & 0xFF) * NW;
+#pragma unroll
+      for (int x = 0; x < NW; ++x) {
+        D[x] = ((D[x] << 1) | m.init[x]) & row[x];
+        acc |= D[x] & m.facc[x];
+      }
+    }
+  } else {
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) {
+      const uint64_t *row = B + ((w[j >> 2] >> (8 * (j & 3))) & 0xFF) * NW;
+      const bool act = j >= k0 && j < kend;
+#pragma unroll
+      for (int x = 0; x < NW; ++x) {
+        const uint64_t Dn = ((D[x] << 1) | m.init[x]) & row[x];
+        D[x] = act ? Dn : D[x];
+        acc |= act ? (Dn & m.facc[x]) : 0ull;
+      }
+    }
+  }
+  if (!acc) return;
+  // rare: the block holds string ends; walk it byte by byte
+  uint64_t E[NW];
+#pragma unroll
+  for (int x = 0; x < NW; ++x) E[x] = D0[x];
+#pragma unroll 1
+  for (uint32_t j = k0; j < kend; ++j) {
+    const uint64_t *row = B + ((w[j >> 2] >> (8 * (j & 3))) & 0xFF) * NW;
+    uint64_t any = 0;
+#pragma unroll
+    for (int x = 0; x < NW; ++x) {
+      E[x] = ((E[x] << 1) | m.init[x]) & row[x];
+      any |= E[x] & m.facc[x];
+    }
+    if (!any) continue;
+    const uint64_t e = (uint64_t)bp + j + 1, st = e - m.len;
+#pragma unroll
+    for (int q = 0; q < kSaMultiMax; ++q) {
+      if ((uint32_t)q >= m.nre) break;
+      uint64_t ew = E[0];
+#pragma unroll
+      for (int x = 1; x < NW; ++x) ew = m.word[q] == (uint32_t)x ? E[x] : ew;
+      if ((ew & m.fin[q]) && st >= p[q] && st < c1) {
+        if (n[q] < nslots) *(ulonglong2 *)&m.slots[q][(u * nslots + n[q]) * 2] = make_ulonglong2(st, e);
+        ++n[q];
+        p[q] = lm[q] = e;
+      }
+    }
+  }
+}
+
+template <int NW>
+__global__ __launch_bounds__(256) void iter_spec_sa_multi_tile_kernel(BatchDev b, Geo g, uint64_t nunits, SaMulti m) {
+  __shared__ uint64_t B[256 * NW];
+  __shared__ __attribute__((aligned(16))) uint4 stage[4][64 * 8];
+  for (uint32_t i = threadIdx.x; i < 256 * NW; i += blockDim.x) B[i] = m.image[i];
+  __syncthreads();
+  const uint64_t L = m.len, C = g.chunk, nk = g.nk;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint4 *buf = stage[w];
+  const int src_h = lane >> 3, src_seg = lane & 7, sw = (lane >> 1) & 7;
+  const uint64_t ngroups = (nunits + 63) / 64, nwaves = (uint64_t)gridDim.x * 4;
+  const bool single = b.count == 1;
+  auto hk = [&](uint64_t uu, uint64_t &h, uint64_t &k) {
+    if (single) { h = 0; k = uu; } else { h = uu / nk; k = uu - h * nk; }
+  };
+  for (uint64_t gi = (uint64_t)blockIdx.x * 4 + w; gi < ngroups; gi += nwaves) {
+    const uint64_t u = gi * 64 + lane;
+    uint64_t h, k;
+    hk(u, h, k);
+    const bool valid = u < nunits;
+    const bool full = valid && k + 1 < nk;
+    const uint8_t *src[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      uint64_t us = gi * 64 + 8 * j + src_h, hs, ks;
+      hk(us, hs, ks);
+      if (us >= nunits || ks + 1 >= nk) hs = ks = 0;  // absent / ragged units re-read unit 0 (full)
+      src[j] = b.hay + hs * b.stride + b.start + ks * C + 16 * src_seg;
+    }
+    const uint8_t *base = b.hay + h * b.stride;
+    const uint64_t len = b.length, c0 = b.start + k * C;
+    const uint64_t c1 = k + 1 == nk ? g.end : c0 + C;
+    uint64_t p[kSaMultiMax], lm[kSaMultiMax];
+    uint32_t n[kSaMultiMax];
+#pragma unroll
+    for (int q = 0; q < kSaMultiMax; ++q) { p[q] = c0; lm[q] = NONE; n[q] = 0; }
+    uint64_t D[NW];
+#pragma unroll
+    for (int x = 0; x < NW; ++x) D[x] = 0;
+    uint4 first = make_uint4(0, 0, 0, 0);
+    uint4 n0, n1, n2, n3, n4, n5, n6, n7;
+#define RURE_LOAD_TILE(a)                                                                                     \
+  n0 = *(const uint4 *)(src[0] + (a)); n1 = *(const uint4 *)(src[1] + (a));                                  \
+  n2 = *(const uint4 *)(src[2] + (a)); n3 = *(const uint4 *)(src[3] + (a));                                  \
+  n4 = *(const uint4 *)(src[4] + (a)); n5 = *(const uint4 *)(src[5] + (a));                                  \
+  n6 = *(const uint4 *)(src[6] + (a)); n7 = *(const uint4 *)(src[7] + (a));
+#define RURE_STAGE(kk, v) buf[(8 * (kk) + src_h) * 8 + (src_seg ^ (((8 * (kk) + src_h) >> 1) & 7))] = (v);
+    RURE_LOAD_TILE(0)
+    for (uint64_t at = 0; at < C; at += 128) {
+      RURE_STAGE(0, n0) RURE_STAGE(1, n1) RURE_STAGE(2, n2) RURE_STAGE(3, n3)
+      RURE_STAGE(4, n4) RURE_STAGE(5, n5) RURE_STAGE(6, n6) RURE_STAGE(7, n7)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const uint64_t an = at + 128 < C ? at + 128 : at;
+      RURE_LOAD_TILE(an)
+      if (full) {
+        uint4 cur = buf[lane * 8 + sw];
+        if (at == 0) first = cur;
+#pragma unroll 1
+        for (int mm = 0; mm < 8; ++mm) {
+          const uint4 nx = buf[lane * 8 + ((mm + 1 < 8 ? mm + 1 : 7) ^ sw)];
+          const uint32_t wd[4] = {cur.x, cur.y, cur.z, cur.w};
+          sam_block<NW>(D, B, m, wd, 0, 16, (int64_t)(c0 + at + 16 * mm), c1, p, lm, n, u, g.slots);
+          cur = nx;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+#undef RURE_LOAD_TILE
+#undef RURE_STAGE
+    uint4 nxt;
+    nxt.x = __shfl_down(first.x, 1);
+    nxt.y = __shfl_down(first.y, 1);
+    nxt.z = __shfl_down(first.z, 1);
+    nxt.w = __shfl_down(first.w, 1);
+    if (!valid) continue;
+    if (full) {
+      // strings starting before the cut end in [c1, c1 + L - 1)
+      const uint64_t qend = min(len, c1 + L - 1);
+      uint64_t q = c1;
+      if (q < qend && lane < 63 && k + 2 < nk) {  // the next unit is full: lane + 1 holds its first block
+        const uint32_t wd[4] = {nxt.x, nxt.y, nxt.z, nxt.w};
+        const uint32_t kend = qend - q < 16 ? (uint32_t)(qend - q) : 16;
+        sam_block<NW>(D, B, m, wd, 0, kend, (int64_t)q, c1, p, lm, n, u, g.slots);
+        q += 16;
+      }
+      for (; q < qend; q += 16) {  // from memory (aligned: c1 is)
+        const uint4 v = *(const uint4 *)(base + q);
+        const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+        const uint32_t kend = qend - q < 16 ? (uint32_t)(qend - q) : 16;
+        sam_block<NW>(D, B, m, wd, 0, kend, (int64_t)q, c1, p, lm, n, u, g.slots);
+      }
+    } else {
+      // ragged last unit of its haystack: the per-lane loop
+      const uint64_t qend = c1 >= len ? len : min(len, c1 + L - 1);
+      for (uintptr_t a = (uintptr_t)(base + c0) & ~(uintptr_t)15; c0 < qend && a < (uintptr_t)(base + qend); a += 16) {
+        const uint4 v = *(const uint4 *)a;
+        const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+        const int64_t bp = (int64_t)(a - (uintptr_t)base);
+        const uint32_t k0 = bp < (int64_t)c0 ? (uint32_t)((int64_t)c0 - bp) : 0;
+        const uint32_t kend = (int64_t)qend - bp < 16 ? (uint32_t)((int64_t)qend - bp) : 16;
+        sam_block<NW>(D, B, m, wd, k0, kend, bp, c1, p, lm, n, u, g.slots);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kSaMultiMax; ++q) {
+      if ((uint32_t)q >= m.nre) break;
+      Unit U;
+      U.entry = {c0, NONE};
+      U.exit = {p[q], lm[q]};
+      U.spec_exit = U.exit;
+      U.spec_count = n[q];
+      const bool clean = p[q] < c1 || (p[q] == c1 && (lm[q] != c1 || m.nonempty[q]));
+      U.flags = clean ? (U_SPEC_CLEAN | U_CLEAN) : 0;
+      U.skip = U.pad = 0;
+      m.units[q][u] = U;
+      m.counts[q][u] = n[q];
+      if (!clean) atomicOr(m.dirty[q], 1u);  // the fix pass has work
+    }
+  }
+}
+
 // Pass 1 with the lexer table (FwdDfaDev::lex_image, host build_lex), for
 // patterns whose matches all end in terminal states and start at the first
 // byte of F (the regex-dna strip pattern `>[^\n]*\n|\n`): the iteration is a
@@ -1529,6 +1762,183 @@ hipError_t launch_long_scan(int mode, const BatchDev &b, const FwdDfaDev &f, con
   }
 }
 
+// Unit geometry of a chunked find_iter: units of `chunk` bytes per haystack
+// (offset batches: one unit per haystack); returns the number of units.
+static uint64_t iter_geo(const BatchDev &b, uint64_t chunk, uint64_t hi, Geo *g) {
+  const uint64_t lim = std::min<uint64_t>(b.length, hi);
+  const uint64_t span = (!b.offs && lim > b.start) ? lim - b.start : 0;
+  g->chunk = chunk;
+  g->end = hi;
+  g->nk = (b.offs || span <= chunk) ? 1 : (span + chunk - 1) / chunk;
+  if (b.offs) g->chunk = ~0ull >> 2;
+  g->slots = b.offs ? 16 : unit_slots(std::min<uint64_t>(g->chunk, span ? span : 1));
+  return b.count * g->nk;
+}
+
+// Scratch of one chunked find_iter: units, slots, counts (n + 1), offsets
+// (n + 1), repair queue, its length and the dirty flag; one allocation.
+struct IterScratch {
+  uint8_t *buf = nullptr;
+  Unit *units;
+  uint64_t *slots, *off, *queue;
+  uint32_t *counts, *dirty;
+  unsigned long long *qlen;
+};
+
+static hipError_t iter_scratch(uint64_t nunits, uint32_t nslots, hipStream_t st, IterScratch *sc) {
+  const size_t sz_units = nunits * sizeof(Unit), sz_slots = nunits * (size_t)nslots * 16;
+  const size_t sz_counts = (nunits + 1) * 4, sz_off = (nunits + 1) * 8, sz_queue = nunits * 8;
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t total = al(sz_units) + al(sz_slots) + al(sz_counts) + al(sz_off) + al(sz_queue) + 256;
+  hipError_t e;
+  if ((e = hipMallocAsync((void **)&sc->buf, total, st)) != hipSuccess) return e;
+  uint8_t *buf = sc->buf;
+  sc->units = (Unit *)buf;
+  sc->slots = (uint64_t *)(buf + al(sz_units));
+  sc->counts = (uint32_t *)(buf + al(sz_units) + al(sz_slots));
+  sc->off = (uint64_t *)(buf + al(sz_units) + al(sz_slots) + al(sz_counts));
+  sc->queue = (uint64_t *)(buf + al(sz_units) + al(sz_slots) + al(sz_counts) + al(sz_off));
+  sc->qlen = (unsigned long long *)(buf + total - 256);
+  sc->dirty = (uint32_t *)(buf + total - 256 + 8);
+  if ((e = hipMemsetAsync(sc->counts + nunits, 0, 4, st)) != hipSuccess) return e;
+  return hipMemsetAsync(sc->qlen, 0, 16, st);  // qlen, dirty
+}
+
+static int iter_bs() {
+  int bs = 256;
+  if (const char *v = getenv("RURE_AMD_ITER_BS")) bs = std::max(64, std::min(1024, atoi(v)));
+  return bs;
+}
+
+static bool sa_usable(const FwdDfaDev &f) {
+  const char *sa_env = getenv("RURE_AMD_SA"), *lit_env = getenv("RURE_AMD_LIT");
+  return f.sa_len && !(sa_env && sa_env[0] == '0') && !(lit_env && lit_env[0] == '1');
+}
+
+static bool sa_tile_ok(const BatchDev &b, const Geo &g) {
+  const char *sa_env = getenv("RURE_AMD_SA");
+  return !b.offs && g.nk >= 2 && (g.chunk % 128) == 0 && (b.count == 1 || (b.stride % 16) == 0) &&
+         (((uintptr_t)(b.hay + b.start)) & 15) == 0 && !(sa_env && sa_env[0] == '2');
+}
+
+// The passes after the speculative one (same for every engine): a span's
+// entry, the repairs (fix, walk), the output offsets, emission, per-haystack
+// counts and a span's exit.
+static hipError_t iter_post(const BatchDev &b, const Geo &g, uint64_t nunits, const FwdDfaDev &f, const RevDfaDev &r,
+                            const IterScratch &sc, const IterOut &o, const IterSpan *spn, hipStream_t st, int cus) {
+  hipError_t e;
+  const int bs = iter_bs();
+  const size_t lb = iter_lds_bytes(f, r);
+  const int per_cu = std::max<int>(1, std::min<int>(2048 / bs, (int)((160u * 1024u) / std::max<size_t>(lb, 1))));
+  const int grid = grid_cap(nunits, bs, cus, per_cu);
+  if ((e = allow_lds(iter_fix_kernel, lb)) != hipSuccess || (e = allow_lds(iter_emit_kernel, lb)) != hipSuccess)
+    return e;
+  if (spn && spn->entry) {
+    FwdDfaDev fw = f;
+    fw.hot = 0;
+    RevDfaDev rw = r;
+    rw.hot = 0;
+    hipLaunchKernelGGL(iter_entry_kernel, dim3(1), dim3(64), 0, st, b, g, nunits, fw, rw, sc.units, sc.counts,
+                       (const uint64_t *)sc.slots, spn->entry, sc.queue, sc.qlen);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  if (g.nk > 1) {
+    hipLaunchKernelGGL(iter_fix_kernel, dim3(grid), dim3(bs), lb, st, b, g, nunits, f, r, sc.units, sc.counts,
+                       (const uint64_t *)sc.slots, sc.queue, sc.qlen, (const uint32_t *)sc.dirty);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    FwdDfaDev fw = f;
+    fw.hot = 0;
+    RevDfaDev rw = r;
+    rw.hot = 0;
+    hipLaunchKernelGGL(iter_walk_kernel, dim3(1), dim3(64), 0, st, b, g, nunits, fw, rw, sc.units, sc.counts,
+                       (const uint64_t *)sc.slots, sc.queue, sc.qlen);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  if ((e = scan_counts(sc.counts, sc.off, nunits, st)) != hipSuccess) return e;
+  hipLaunchKernelGGL(iter_emit_kernel, dim3(grid), dim3(bs), lb, st, b, g, nunits, f, r, sc.units, sc.slots, sc.off,
+                     o.matches, o.cap);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(iter_counts_kernel, dim3(grid_cap(b.count, 256, cus, 4)), dim3(256), 0, st, b.count, g.nk,
+                     sc.off, o.counts, o.total);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if (spn && spn->exit) {
+    hipLaunchKernelGGL(iter_exit_kernel, dim3(1), dim3(64), 0, st, (const Unit *)sc.units, nunits, spn->exit,
+                       spn->tail, f.nonempty);
+    e = hipGetLastError();
+  }
+  return e;
+}
+
+// Several Shift-And regexes over the same span in one speculative pass
+// (iter_spec_sa_multi_tile_kernel), then each regex's own passes.  Returns
+// hipErrorNotSupported (nothing launched) when they do not qualify: every
+// regex on the Shift-And engine with one string length, the tile geometry,
+// at most kSaMultiMax regexes in at most 4 words of 64 bits.
+hipError_t launch_find_iter_multi(const BatchDev &b, int nre, const FwdDfaDev *const *f, const RevDfaDev *const *r,
+                                  uint64_t chunk, const IterOut *o, hipStream_t st, int cus, const IterSpan *spn) {
+  if (nre < 1 || nre > kSaMultiMax || b.count == 0) return hipErrorNotSupported;
+  Geo g;
+  const uint64_t nunits = iter_geo(b, chunk, spn ? spn[0].hi : ~0ull, &g);
+  if (!sa_tile_ok(b, g)) return hipErrorNotSupported;
+  SaMulti m{};
+  m.nre = (uint32_t)nre;
+  m.len = f[0]->sa_len;
+  uint32_t word = 0, used = 0;
+  for (int q = 0; q < nre; ++q) {
+    if (!sa_usable(*f[q]) || f[q]->sa_len != m.len || f[q]->sa_bits > 64) return hipErrorNotSupported;
+    if (spn && spn[q].hi != spn[0].hi) return hipErrorNotSupported;
+    if (used + f[q]->sa_bits > 64) { ++word; used = 0; }
+    if (word >= 4) return hipErrorNotSupported;
+    m.word[q] = word;
+    m.shift[q] = used;
+    m.fin[q] = f[q]->sa_final << used;
+    m.init[word] |= f[q]->sa_init << used;
+    m.facc[word] |= m.fin[q];
+    m.nonempty[q] = f[q]->nonempty;
+    m.sa_image[q] = f[q]->sa_image;
+    used += f[q]->sa_bits;
+  }
+  const int nw = (int)word + 1;
+  hipError_t e = hipSuccess;
+  std::vector<IterScratch> sc(nre);
+  uint64_t *img = nullptr;
+  int made = 0;
+  do {
+    if ((e = hipMallocAsync((void **)&img, 256 * 4 * 8, st)) != hipSuccess) break;
+    m.image = img;
+    for (; made < nre; ++made) {
+      if ((e = iter_scratch(nunits, g.slots, st, &sc[made])) != hipSuccess) break;
+      m.units[made] = sc[made].units;
+      m.slots[made] = sc[made].slots;
+      m.counts[made] = sc[made].counts;
+      m.dirty[made] = sc[made].dirty;
+    }
+    if (e != hipSuccess) break;
+    const dim3 sg(grid_cap((nunits + 63) / 64, 4, cus, 4));
+    switch (nw) {
+      case 1: hipLaunchKernelGGL(sa_multi_image_kernel<1>, dim3(1), dim3(256), 0, st, m);
+              hipLaunchKernelGGL(iter_spec_sa_multi_tile_kernel<1>, sg, dim3(256), 0, st, b, g, nunits, m); break;
+      case 2: hipLaunchKernelGGL(sa_multi_image_kernel<2>, dim3(1), dim3(256), 0, st, m);
+              hipLaunchKernelGGL(iter_spec_sa_multi_tile_kernel<2>, sg, dim3(256), 0, st, b, g, nunits, m); break;
+      case 3: hipLaunchKernelGGL(sa_multi_image_kernel<3>, dim3(1), dim3(256), 0, st, m);
+              hipLaunchKernelGGL(iter_spec_sa_multi_tile_kernel<3>, sg, dim3(256), 0, st, b, g, nunits, m); break;
+      default: hipLaunchKernelGGL(sa_multi_image_kernel<4>, dim3(1), dim3(256), 0, st, m);
+               hipLaunchKernelGGL(iter_spec_sa_multi_tile_kernel<4>, sg, dim3(256), 0, st, b, g, nunits, m); break;
+    }
+    if ((e = hipGetLastError()) != hipSuccess) break;
+    for (int q = 0; q < nre && e == hipSuccess; ++q) e = iter_post(b, g, nunits, *f[q], *r[q], sc[q], o[q], spn ? &spn[q] : nullptr, st, cus);
+  } while (false);
+  for (int q = 0; q < made; ++q) {
+    hipError_t e2 = hipFreeAsync(sc[q].buf, st);
+    if (e == hipSuccess) e = e2;
+  }
+  if (img) {
+    hipError_t e2 = hipFreeAsync(img, st);
+    if (e == hipSuccess) e = e2;
+  }
+  return e;
+}
+
 hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaDev &r, const NfaDev *nf,
                             bool chunked, uint64_t chunk, const IterOut &o, hipStream_t st, int cus,
                             const IterSpan *spn) {
@@ -1538,39 +1948,20 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
     return hipMemsetAsync(o.total, 0, 8, st);
   }
   if (chunked) {
-    const uint64_t lim = std::min<uint64_t>(b.length, hi);
-    uint64_t span = (!b.offs && lim > b.start) ? lim - b.start : 0;
     Geo g;
-    g.chunk = chunk;
-    g.end = hi;
-    g.nk = (b.offs || span <= chunk) ? 1 : (span + chunk - 1) / chunk;
-    if (b.offs) g.chunk = ~0ull >> 2;
-    const uint64_t nunits = b.count * g.nk;
-    // scratch: units, slots, counts (n + 1), offsets (n + 1), queue, qlen
-    g.slots = b.offs ? 16 : unit_slots(std::min<uint64_t>(g.chunk, span ? span : 1));
-    const size_t sz_units = nunits * sizeof(Unit), sz_slots = nunits * (size_t)g.slots * 16;
-    const size_t sz_counts = (nunits + 1) * 4, sz_off = (nunits + 1) * 8, sz_queue = nunits * 8;
-    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    const size_t total = al(sz_units) + al(sz_slots) + al(sz_counts) + al(sz_off) + al(sz_queue) + 256;
-    uint8_t *buf = nullptr;
-    if ((e = hipMallocAsync((void **)&buf, total, st)) != hipSuccess) return e;
-    Unit *units = (Unit *)buf;
-    uint64_t *slots = (uint64_t *)(buf + al(sz_units));
-    uint32_t *counts = (uint32_t *)(buf + al(sz_units) + al(sz_slots));
-    uint64_t *off = (uint64_t *)(buf + al(sz_units) + al(sz_slots) + al(sz_counts));
-    uint64_t *queue = (uint64_t *)(buf + al(sz_units) + al(sz_slots) + al(sz_counts) + al(sz_off));
-    unsigned long long *qlen = (unsigned long long *)(buf + total - 256);
-    uint32_t *dirty = (uint32_t *)(buf + total - 256 + 8);
+    const uint64_t nunits = iter_geo(b, chunk, hi, &g);
+    IterScratch sc;
+    if ((e = iter_scratch(nunits, g.slots, st, &sc)) != hipSuccess) return e;
     // threads per block: the hot tables are staged once per block, so larger
     // blocks let more waves share one LDS copy (occupancy of these latency-
     // bound per-lane scans); RURE_AMD_ITER_BS overrides (tuning)
-    int bs = 256;
-    if (const char *v = getenv("RURE_AMD_ITER_BS")) bs = std::max(64, std::min(1024, atoi(v)));
+    const int bs = iter_bs();
     const int per_cu = std::max<int>(1, std::min<int>(2048 / bs, (int)((160u * 1024u) / std::max<size_t>(iter_lds_bytes(*f, r), 1))));
     const int grid = grid_cap(nunits, bs, cus, per_cu);
+    Unit *units = sc.units;
+    uint64_t *slots = sc.slots;
+    uint32_t *counts = sc.counts, *dirty = sc.dirty;
     do {
-      if ((e = hipMemsetAsync(counts + nunits, 0, 4, st)) != hipSuccess) break;
-      if ((e = hipMemsetAsync(qlen, 0, 16, st)) != hipSuccess) break;  // qlen, dirty
       const size_t lb = iter_lds_bytes(*f, r);
       if ((e = allow_lds(iter_spec_kernel, lb)) != hipSuccess || (e = allow_lds(iter_spec_burst_kernel, lb)) != hipSuccess || (e = allow_lds(iter_fix_kernel, lb)) != hipSuccess ||
           (e = allow_lds(iter_emit_kernel, lb)) != hipSuccess)
@@ -1583,10 +1974,8 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
       const char *lit_env = getenv("RURE_AMD_LIT");
       const bool use_lit = f->lit_n && (lit_env ? lit_env[0] == '1' : !f->all);
       // Shift-And engine for equal-length string sets; RURE_AMD_SA=0 disables
-      const char *sa_env = getenv("RURE_AMD_SA");
-      const bool use_sa = f->sa_len && !(sa_env && sa_env[0] == '0') && !(lit_env && lit_env[0] == '1');
-      const bool sa_tile = !b.offs && g.nk >= 2 && (g.chunk % 128) == 0 && (b.count == 1 || (b.stride % 16) == 0) &&
-                           (((uintptr_t)(b.hay + b.start)) & 15) == 0 && !(sa_env && sa_env[0] == '2');
+      const bool use_sa = sa_usable(*f);
+      const bool sa_tile = sa_tile_ok(b, g);
       // Lexer engine (terminal matches + first-byte rule); RURE_AMD_LEX=0 disables
       const char *lex_env = getenv("RURE_AMD_LEX");
       const bool use_lex = f->lex_bytes && !(lex_env && lex_env[0] == '0') && !b.offs && g.nk >= 2 &&
@@ -1635,41 +2024,9 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
                            units, slots, counts, dirty);
       }
       if ((e = hipGetLastError()) != hipSuccess) break;
-      if (spn && spn->entry) {
-        FwdDfaDev fw = *f;
-        fw.hot = 0;
-        RevDfaDev rw = r;
-        rw.hot = 0;
-        hipLaunchKernelGGL(iter_entry_kernel, dim3(1), dim3(64), 0, st, b, g, nunits, fw, rw, units, counts,
-                           (const uint64_t *)slots, spn->entry, queue, qlen);
-        if ((e = hipGetLastError()) != hipSuccess) break;
-      }
-      if (g.nk > 1) {
-        hipLaunchKernelGGL(iter_fix_kernel, dim3(grid), dim3(bs), iter_lds_bytes(*f, r), st, b, g, nunits, *f, r, units,
-                           counts, (const uint64_t *)slots, queue, qlen, (const uint32_t *)dirty);
-        if ((e = hipGetLastError()) != hipSuccess) break;
-        FwdDfaDev fw = *f;
-        fw.hot = 0;
-        RevDfaDev rw = r;
-        rw.hot = 0;
-        hipLaunchKernelGGL(iter_walk_kernel, dim3(1), dim3(64), 0, st, b, g, nunits, fw, rw, units, counts,
-                           (const uint64_t *)slots, queue, qlen);
-        if ((e = hipGetLastError()) != hipSuccess) break;
-      }
-      if ((e = scan_counts(counts, off, nunits, st)) != hipSuccess) break;
-      hipLaunchKernelGGL(iter_emit_kernel, dim3(grid), dim3(bs), iter_lds_bytes(*f, r), st, b, g, nunits, *f, r, units, slots,
-                         off, o.matches, o.cap);
-      if ((e = hipGetLastError()) != hipSuccess) break;
-      hipLaunchKernelGGL(iter_counts_kernel, dim3(grid_cap(b.count, 256, cus, 4)), dim3(256), 0, st, b.count, g.nk,
-                         off, o.counts, o.total);
-      if ((e = hipGetLastError()) != hipSuccess) break;
-      if (spn && spn->exit) {
-        hipLaunchKernelGGL(iter_exit_kernel, dim3(1), dim3(64), 0, st, (const Unit *)units, nunits, spn->exit,
-                           spn->tail, f->nonempty);
-        e = hipGetLastError();
-      }
+      e = iter_post(b, g, nunits, *f, r, sc, o, spn, st, cus);
     } while (false);
-    hipError_t e2 = hipFreeAsync(buf, st);
+    hipError_t e2 = hipFreeAsync(sc.buf, st);
     return e != hipSuccess ? e : e2;
   }
   // one wavefront per haystack (assertions, DFA quit, or no DFA)

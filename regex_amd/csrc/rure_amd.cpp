@@ -1960,6 +1960,63 @@ int rure_amd_find_iter_span(rure *re, const uint8_t *haystack, size_t length, si
   return run_find_iter(re, t, b, o, st, &err, &sp) == hipSuccess ? RURE_AMD_OK : RURE_AMD_ERR_HIP;
 }
 
+int rure_amd_find_iter_span_multi(rure *const *res, size_t n, const uint8_t *haystack, size_t length, size_t lo,
+                                  size_t hi, const rure_amd_iter_state *const *entry, uint64_t *const *count,
+                                  rure_match *const *matches, const size_t *capacity,
+                                  rure_amd_iter_state *const *exit, void *stream) {
+  if (!res || !count || !exit || (!matches && n) || (!capacity && n) || (!haystack && length) || lo > hi ||
+      hi > length)
+    return RURE_AMD_ERR_ARG;
+  for (size_t i = 0; i < n; ++i)
+    if (!res[i] || !count[i] || !exit[i] || (!matches[i] && capacity[i])) return RURE_AMD_ERR_ARG;
+  if (n == 0) return RURE_AMD_OK;
+  hipStream_t st = (hipStream_t)stream;
+  BatchDev b;
+  b.hay = haystack;
+  b.offs = nullptr;
+  b.stride = length;
+  b.length = length;
+  b.count = 1;
+  b.start = lo;
+  const uint64_t hcut = hi == length ? ~0ull : (uint64_t)hi, tail = hi == length ? (uint64_t)length : ~0ull;
+  // the fused pass: every regex on the chunked Shift-And path
+  std::vector<const FwdDfaDev *> fs(n);
+  std::vector<const RevDfaDev *> rs(n);
+  std::vector<IterOut> os(n);
+  std::vector<IterSpan> sps(n);
+  std::string err;
+  bool fused = n > 1 && hi > lo;
+  int cus = 0;
+  for (size_t i = 0; i < n && fused; ++i) {
+    DevTables *t = regex_device(res[i], &err);
+    if (!t) return err.rfind("HIP", 0) == 0 ? RURE_AMD_ERR_HIP : RURE_AMD_ERR_DFA;
+    const FwdDfaDev *fi = nullptr;
+    if (t->has_dfa && !t->quit_possible && res[i]->nfa_ok && res[i]->nt.looks_used == 0) fi = iter_device(res[i], *t, &err);
+    if (!fi || !fi->sa_len) { fused = false; break; }
+    fs[i] = fi;
+    rs[i] = &t->r;
+    cus = t->cus;
+    os[i] = IterOut{count[i], (uint64_t *)matches[i], capacity[i], count[i]};
+    sps[i] = IterSpan{hcut, entry ? (const uint64_t *)entry[i] : nullptr, (uint64_t *)exit[i], tail};
+  }
+  if (fused) {
+    // the unit size of run_find_iter (one haystack: the span over the lanes in flight)
+    const uint64_t span = std::min<uint64_t>(length, hcut) - lo;
+    uint64_t per_cu = 1024;
+    if (const char *v = getenv("RURE_AMD_ITER_LANES")) per_cu = std::max(64, atoi(v));
+    const uint64_t chunk = odd_lines(std::max<uint64_t>(4096, (span + (uint64_t)cus * per_cu - 1) / ((uint64_t)cus * per_cu)));
+    hipError_t e = launch_find_iter_multi(b, (int)n, fs.data(), rs.data(), chunk, os.data(), st, cus, sps.data());
+    if (e == hipSuccess) return RURE_AMD_OK;
+    if (e != hipErrorNotSupported) return RURE_AMD_ERR_HIP;
+  }
+  for (size_t i = 0; i < n; ++i) {
+    int rc = rure_amd_find_iter_span(res[i], haystack, length, lo, hi, entry ? entry[i] : nullptr, count[i],
+                                     matches[i], capacity[i], exit[i], stream);
+    if (rc != RURE_AMD_OK) return rc;
+  }
+  return RURE_AMD_OK;
+}
+
 int rure_amd_replace_batch(rure *re, const rure_amd_batch *batch, const uint8_t *rep, size_t rep_len, size_t limit,
                            uint8_t *out, uint64_t *out_offsets, size_t out_capacity, uint64_t *total, void *stream) {
   BatchDev b;
