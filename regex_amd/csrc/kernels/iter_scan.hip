@@ -795,15 +795,19 @@ __global__ __launch_bounds__(256) void iter_spec_sa_tile_kernel(BatchDev b, Geo 
 // and its own unit records, so the per-regex passes after this one (fix,
 // walk, emit) are unchanged and each regex's matches are exactly its own
 // find_iter's.  All regexes share one string length L and the unit geometry.
-constexpr int kSaMultiMax = 12;
+constexpr int kSaMultiMax = 12, kSaMultiWords = 8;
+// Regexes of at most 32 bits each, packed into 32-bit words (a regex never
+// straddles two words, so a byte's step is one v_lshl_or + one v_and per
+// word, with no carries between words).
 struct SaMulti {
-  uint64_t *image;                    // [256][NW] combined masks (device, built by sa_multi_image_kernel)
-  uint64_t init[4], facc[4];          // per word: init bits, final bits of all its regexes
+  uint32_t *image;                    // [256][NW] combined masks (device, built by sa_multi_image_kernel)
+  uint32_t init[kSaMultiWords], facc[kSaMultiWords];  // per word: init bits, final bits of its regexes
+  uint32_t fany;                      // the OR of facc
   uint64_t len;                       // the common string length L
   uint32_t nre;
   uint32_t word[kSaMultiMax];         // word of regex x
   uint32_t shift[kSaMultiMax];        // bit offset of regex x in its word
-  uint64_t fin[kSaMultiMax];          // final bits of regex x (in its word)
+  uint32_t fin[kSaMultiMax];          // final bits of regex x (in its word)
   uint32_t nonempty[kSaMultiMax];
   const uint64_t *sa_image[kSaMultiMax];  // each regex's own 256 masks
   Unit *units[kSaMultiMax];
@@ -812,65 +816,88 @@ struct SaMulti {
   uint32_t *dirty[kSaMultiMax];
 };
 
+// LDS rows of NWP = 4 or 8 words (16-byte reads)
+template <int NW> struct SamPitch { static constexpr int v = NW <= 4 ? 4 : 8; };
+
 template <int NW>
 __global__ void sa_multi_image_kernel(SaMulti m) {
   const uint32_t c = threadIdx.x;  // 256 threads: one byte value each
-  uint64_t wv[NW];
+  uint32_t wv[NW];
 #pragma unroll
   for (int x = 0; x < NW; ++x) wv[x] = 0;
   for (uint32_t q = 0; q < m.nre; ++q) {
-    const uint64_t v = m.sa_image[q][c] << m.shift[q];
+    const uint32_t v = (uint32_t)m.sa_image[q][c] << m.shift[q];
 #pragma unroll
     for (int x = 0; x < NW; ++x)
       if (m.word[q] == (uint32_t)x) wv[x] |= v;
   }
 #pragma unroll
-  for (int x = 0; x < NW; ++x) m.image[c * NW + x] = wv[x];
+  for (int x = 0; x < SamPitch<NW>::v; ++x) m.image[c * SamPitch<NW>::v + x] = x < NW ? wv[x] : 0u;
 }
 
 // sa_block for every regex of the pass: the bits of 16 bytes (k0..kend) and,
-// in the rare block holding string ends, each regex's greedy iteration.
+// in the rare block holding string ends, each regex's greedy iteration.  The
+// iteration state is kept relative to the unit start (p, lm: u32 offsets;
+// kNoLm = none) to spare registers.
+constexpr uint32_t kNoLm = 0xFFFFFFFFu;
 template <int NW>
-__device__ __forceinline__ void sam_block(uint64_t (&D)[NW], const uint64_t *B, const SaMulti &m, const uint32_t w[4],
-                                          uint32_t k0, uint32_t kend, int64_t bp, uint64_t c1,
-                                          uint64_t (&p)[kSaMultiMax], uint64_t (&lm)[kSaMultiMax],
+__device__ __forceinline__ void sam_row(const uint32_t *B, uint32_t c, uint32_t (&row)[NW]) {
+  const uint4 *r = (const uint4 *)(B + c * SamPitch<NW>::v);
+  const uint4 a = r[0];
+  const uint32_t t[8] = {a.x, a.y, a.z, a.w, 0, 0, 0, 0};
+  uint32_t u[8] = {t[0], t[1], t[2], t[3], 0, 0, 0, 0};
+  if (NW > 4) { const uint4 b2 = r[1]; u[4] = b2.x; u[5] = b2.y; u[6] = b2.z; u[7] = b2.w; }
+#pragma unroll
+  for (int x = 0; x < NW; ++x) row[x] = u[x];
+}
+
+template <int NW>
+__device__ __forceinline__ void sam_block(uint32_t (&D)[NW], const uint32_t *B, const SaMulti &m, const uint32_t w[4],
+                                          uint32_t k0, uint32_t kend, int64_t bp, uint64_t c0, uint64_t c1,
+                                          uint32_t (&p)[kSaMultiMax], uint32_t (&lm)[kSaMultiMax],
                                           uint32_t (&n)[kSaMultiMax], uint64_t u, uint32_t nslots) {
-  uint64_t D0[NW];
-  uint64_t acc = 0;
+  uint32_t D0[NW];
+  uint32_t acc = 0;
 #pragma unroll
   for (int x = 0; x < NW; ++x) D0[x] = D[x];
+  // acc: the OR of every word's bits after every byte; the words share one
+  // layout of final bits in practice (8-bit sequences), and a bit that is
+  // final only in another word just sends the block down the exact walk
   if (k0 == 0 && kend == 16) {
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-      const uint64_t *row = B + ((w[j >> 2] >> (8 * (j & 3))) & 0xFF) * NW;
+      uint32_t row[NW];
+      sam_row<NW>(B, (w[j >> 2] >> (8 * (j & 3))) & 0xFF, row);
 #pragma unroll
       for (int x = 0; x < NW; ++x) {
         D[x] = ((D[x] << 1) | m.init[x]) & row[x];
-        acc |= D[x] & m.facc[x];
+        acc |= D[x];
       }
     }
   } else {
 #pragma unroll
     for (uint32_t j = 0; j < 16; ++j) {
-      const uint64_t *row = B + ((w[j >> 2] >> (8 * (j & 3))) & 0xFF) * NW;
+      uint32_t row[NW];
+      sam_row<NW>(B, (w[j >> 2] >> (8 * (j & 3))) & 0xFF, row);
       const bool act = j >= k0 && j < kend;
 #pragma unroll
       for (int x = 0; x < NW; ++x) {
-        const uint64_t Dn = ((D[x] << 1) | m.init[x]) & row[x];
+        const uint32_t Dn = ((D[x] << 1) | m.init[x]) & row[x];
         D[x] = act ? Dn : D[x];
-        acc |= act ? (Dn & m.facc[x]) : 0ull;
+        acc |= act ? Dn : 0u;
       }
     }
   }
-  if (!acc) return;
+  if (!(acc & m.fany)) return;
   // rare: the block holds string ends; walk it byte by byte
-  uint64_t E[NW];
+  uint32_t E[NW];
 #pragma unroll
   for (int x = 0; x < NW; ++x) E[x] = D0[x];
 #pragma unroll 1
   for (uint32_t j = k0; j < kend; ++j) {
-    const uint64_t *row = B + ((w[j >> 2] >> (8 * (j & 3))) & 0xFF) * NW;
-    uint64_t any = 0;
+    uint32_t row[NW];
+    sam_row<NW>(B, (w[j >> 2] >> (8 * (j & 3))) & 0xFF, row);
+    uint32_t any = 0;
 #pragma unroll
     for (int x = 0; x < NW; ++x) {
       E[x] = ((E[x] << 1) | m.init[x]) & row[x];
@@ -881,13 +908,13 @@ __device__ __forceinline__ void sam_block(uint64_t (&D)[NW], const uint64_t *B, 
 #pragma unroll
     for (int q = 0; q < kSaMultiMax; ++q) {
       if ((uint32_t)q >= m.nre) break;
-      uint64_t ew = E[0];
+      uint32_t ew = E[0];
 #pragma unroll
       for (int x = 1; x < NW; ++x) ew = m.word[q] == (uint32_t)x ? E[x] : ew;
-      if ((ew & m.fin[q]) && st >= p[q] && st < c1) {
+      if ((ew & m.fin[q]) && st >= c0 + p[q] && st < c1) {
         if (n[q] < nslots) *(ulonglong2 *)&m.slots[q][(u * nslots + n[q]) * 2] = make_ulonglong2(st, e);
         ++n[q];
-        p[q] = lm[q] = e;
+        p[q] = lm[q] = (uint32_t)(e - c0);
       }
     }
   }
@@ -895,9 +922,9 @@ __device__ __forceinline__ void sam_block(uint64_t (&D)[NW], const uint64_t *B, 
 
 template <int NW>
 __global__ __launch_bounds__(256) void iter_spec_sa_multi_tile_kernel(BatchDev b, Geo g, uint64_t nunits, SaMulti m) {
-  __shared__ uint64_t B[256 * NW];
+  __shared__ __attribute__((aligned(16))) uint32_t B[256 * SamPitch<NW>::v];
   __shared__ __attribute__((aligned(16))) uint4 stage[4][64 * 8];
-  for (uint32_t i = threadIdx.x; i < 256 * NW; i += blockDim.x) B[i] = m.image[i];
+  for (uint32_t i = threadIdx.x; i < 256 * SamPitch<NW>::v; i += blockDim.x) B[i] = m.image[i];
   __syncthreads();
   const uint64_t L = m.len, C = g.chunk, nk = g.nk;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -925,11 +952,10 @@ __global__ __launch_bounds__(256) void iter_spec_sa_multi_tile_kernel(BatchDev b
     const uint8_t *base = b.hay + h * b.stride;
     const uint64_t len = b.length, c0 = b.start + k * C;
     const uint64_t c1 = k + 1 == nk ? g.end : c0 + C;
-    uint64_t p[kSaMultiMax], lm[kSaMultiMax];
-    uint32_t n[kSaMultiMax];
+    uint32_t p[kSaMultiMax], lm[kSaMultiMax], n[kSaMultiMax];
 #pragma unroll
-    for (int q = 0; q < kSaMultiMax; ++q) { p[q] = c0; lm[q] = NONE; n[q] = 0; }
-    uint64_t D[NW];
+    for (int q = 0; q < kSaMultiMax; ++q) { p[q] = 0; lm[q] = kNoLm; n[q] = 0; }
+    uint32_t D[NW];
 #pragma unroll
     for (int x = 0; x < NW; ++x) D[x] = 0;
     uint4 first = make_uint4(0, 0, 0, 0);
@@ -956,7 +982,7 @@ __global__ __launch_bounds__(256) void iter_spec_sa_multi_tile_kernel(BatchDev b
         for (int mm = 0; mm < 8; ++mm) {
           const uint4 nx = buf[lane * 8 + ((mm + 1 < 8 ? mm + 1 : 7) ^ sw)];
           const uint32_t wd[4] = {cur.x, cur.y, cur.z, cur.w};
-          sam_block<NW>(D, B, m, wd, 0, 16, (int64_t)(c0 + at + 16 * mm), c1, p, lm, n, u, g.slots);
+          sam_block<NW>(D, B, m, wd, 0, 16, (int64_t)(c0 + at + 16 * mm), c0, c1, p, lm, n, u, g.slots);
           cur = nx;
         }
       }
@@ -979,14 +1005,14 @@ __global__ __launch_bounds__(256) void iter_spec_sa_multi_tile_kernel(BatchDev b
       if (q < qend && lane < 63 && k + 2 < nk) {  // the next unit is full: lane + 1 holds its first block
         const uint32_t wd[4] = {nxt.x, nxt.y, nxt.z, nxt.w};
         const uint32_t kend = qend - q < 16 ? (uint32_t)(qend - q) : 16;
-        sam_block<NW>(D, B, m, wd, 0, kend, (int64_t)q, c1, p, lm, n, u, g.slots);
+        sam_block<NW>(D, B, m, wd, 0, kend, (int64_t)q, c0, c1, p, lm, n, u, g.slots);
         q += 16;
       }
       for (; q < qend; q += 16) {  // from memory (aligned: c1 is)
         const uint4 v = *(const uint4 *)(base + q);
         const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
         const uint32_t kend = qend - q < 16 ? (uint32_t)(qend - q) : 16;
-        sam_block<NW>(D, B, m, wd, 0, kend, (int64_t)q, c1, p, lm, n, u, g.slots);
+        sam_block<NW>(D, B, m, wd, 0, kend, (int64_t)q, c0, c1, p, lm, n, u, g.slots);
       }
     } else {
       // ragged last unit of its haystack: the per-lane loop
@@ -997,18 +1023,19 @@ __global__ __launch_bounds__(256) void iter_spec_sa_multi_tile_kernel(BatchDev b
         const int64_t bp = (int64_t)(a - (uintptr_t)base);
         const uint32_t k0 = bp < (int64_t)c0 ? (uint32_t)((int64_t)c0 - bp) : 0;
         const uint32_t kend = (int64_t)qend - bp < 16 ? (uint32_t)((int64_t)qend - bp) : 16;
-        sam_block<NW>(D, B, m, wd, k0, kend, bp, c1, p, lm, n, u, g.slots);
+        sam_block<NW>(D, B, m, wd, k0, kend, bp, c0, c1, p, lm, n, u, g.slots);
       }
     }
 #pragma unroll
     for (int q = 0; q < kSaMultiMax; ++q) {
       if ((uint32_t)q >= m.nre) break;
+      const uint64_t pq = c0 + p[q], lq = lm[q] == kNoLm ? NONE : c0 + lm[q];
       Unit U;
       U.entry = {c0, NONE};
-      U.exit = {p[q], lm[q]};
+      U.exit = {pq, lq};
       U.spec_exit = U.exit;
       U.spec_count = n[q];
-      const bool clean = p[q] < c1 || (p[q] == c1 && (lm[q] != c1 || m.nonempty[q]));
+      const bool clean = pq < c1 || (pq == c1 && (lq != c1 || m.nonempty[q]));
       U.flags = clean ? (U_SPEC_CLEAN | U_CLEAN) : 0;
       U.skip = U.pad = 0;
       m.units[q][u] = U;
@@ -1880,20 +1907,24 @@ hipError_t launch_find_iter_multi(const BatchDev &b, int nre, const FwdDfaDev *c
   Geo g;
   const uint64_t nunits = iter_geo(b, chunk, spn ? spn[0].hi : ~0ull, &g);
   if (!sa_tile_ok(b, g)) return hipErrorNotSupported;
+  // every regex's scratch is live at once: fewer speculative slots per unit
+  // (a unit with more matches is re-run by the emit pass instead of copied)
+  g.slots = std::min<uint32_t>(g.slots, 32);
   SaMulti m{};
   m.nre = (uint32_t)nre;
   m.len = f[0]->sa_len;
   uint32_t word = 0, used = 0;
   for (int q = 0; q < nre; ++q) {
-    if (!sa_usable(*f[q]) || f[q]->sa_len != m.len || f[q]->sa_bits > 64) return hipErrorNotSupported;
+    if (!sa_usable(*f[q]) || f[q]->sa_len != m.len || f[q]->sa_bits > 32) return hipErrorNotSupported;
     if (spn && spn[q].hi != spn[0].hi) return hipErrorNotSupported;
-    if (used + f[q]->sa_bits > 64) { ++word; used = 0; }
-    if (word >= 4) return hipErrorNotSupported;
+    if (used + f[q]->sa_bits > 32) { ++word; used = 0; }
+    if (word >= (uint32_t)kSaMultiWords) return hipErrorNotSupported;
     m.word[q] = word;
     m.shift[q] = used;
-    m.fin[q] = f[q]->sa_final << used;
-    m.init[word] |= f[q]->sa_init << used;
+    m.fin[q] = (uint32_t)f[q]->sa_final << used;
+    m.init[word] |= (uint32_t)f[q]->sa_init << used;
     m.facc[word] |= m.fin[q];
+    m.fany |= m.fin[q];
     m.nonempty[q] = f[q]->nonempty;
     m.sa_image[q] = f[q]->sa_image;
     used += f[q]->sa_bits;
@@ -1901,10 +1932,10 @@ hipError_t launch_find_iter_multi(const BatchDev &b, int nre, const FwdDfaDev *c
   const int nw = (int)word + 1;
   hipError_t e = hipSuccess;
   std::vector<IterScratch> sc(nre);
-  uint64_t *img = nullptr;
+  uint32_t *img = nullptr;
   int made = 0;
   do {
-    if ((e = hipMallocAsync((void **)&img, 256 * 4 * 8, st)) != hipSuccess) break;
+    if ((e = hipMallocAsync((void **)&img, 256 * kSaMultiWords * 4, st)) != hipSuccess) break;
     m.image = img;
     for (; made < nre; ++made) {
       if ((e = iter_scratch(nunits, g.slots, st, &sc[made])) != hipSuccess) break;
@@ -1915,16 +1946,17 @@ hipError_t launch_find_iter_multi(const BatchDev &b, int nre, const FwdDfaDev *c
     }
     if (e != hipSuccess) break;
     const dim3 sg(grid_cap((nunits + 63) / 64, 4, cus, 4));
+#define RURE_SAM(NWc)                                                                            \
+  case NWc:                                                                                      \
+    hipLaunchKernelGGL(sa_multi_image_kernel<NWc>, dim3(1), dim3(256), 0, st, m);                \
+    hipLaunchKernelGGL(iter_spec_sa_multi_tile_kernel<NWc>, sg, dim3(256), 0, st, b, g, nunits, m); \
+    break;
     switch (nw) {
-      case 1: hipLaunchKernelGGL(sa_multi_image_kernel<1>, dim3(1), dim3(256), 0, st, m);
-              hipLaunchKernelGGL(iter_spec_sa_multi_tile_kernel<1>, sg, dim3(256), 0, st, b, g, nunits, m); break;
-      case 2: hipLaunchKernelGGL(sa_multi_image_kernel<2>, dim3(1), dim3(256), 0, st, m);
-              hipLaunchKernelGGL(iter_spec_sa_multi_tile_kernel<2>, sg, dim3(256), 0, st, b, g, nunits, m); break;
-      case 3: hipLaunchKernelGGL(sa_multi_image_kernel<3>, dim3(1), dim3(256), 0, st, m);
-              hipLaunchKernelGGL(iter_spec_sa_multi_tile_kernel<3>, sg, dim3(256), 0, st, b, g, nunits, m); break;
-      default: hipLaunchKernelGGL(sa_multi_image_kernel<4>, dim3(1), dim3(256), 0, st, m);
-               hipLaunchKernelGGL(iter_spec_sa_multi_tile_kernel<4>, sg, dim3(256), 0, st, b, g, nunits, m); break;
+      RURE_SAM(1) RURE_SAM(2) RURE_SAM(3) RURE_SAM(4) RURE_SAM(5) RURE_SAM(6) RURE_SAM(7) RURE_SAM(8)
+      default: e = hipErrorNotSupported;
     }
+#undef RURE_SAM
+    if (e != hipSuccess) break;
     if ((e = hipGetLastError()) != hipSuccess) break;
     for (int q = 0; q < nre && e == hipSuccess; ++q) e = iter_post(b, g, nunits, *f[q], *r[q], sc[q], o[q], spn ? &spn[q] : nullptr, st, cus);
   } while (false);

@@ -26,11 +26,11 @@ def pairs(m):
 
 
 def variants():
-    return [R.Regex(v["re"]) for v in known_counts()["variants"]]
+    return [R.Regex(v["re"]) for v in known_counts()["regexdna"]["variants"]]
 
 
 def stripped(copies):
-    kc = known_counts()
+    kc = known_counts()["regexdna"]
     seq = R.Regex(kc["strip"]).replace_all(corpus("regexdna"), b"")
     return seq * copies
 
@@ -89,7 +89,7 @@ def test_multi_not_fusable(cuda):
 
 @pytest.mark.parametrize("k", [1, 2, 4, 9])
 def test_multi_counts_known_answers(cuda, k):
-    kc = known_counts()
+    kc = known_counts()["regexdna"]
     seq = stripped(1)
     res = variants()[:k]
     h = dev(seq, cuda)
