@@ -864,15 +864,30 @@ __device__ __forceinline__ void sam_block(uint32_t (&D)[NW], const uint32_t *B, 
   // layout of final bits in practice (8-bit sequences), and a bit that is
   // final only in another word just sends the block down the exact walk
   if (k0 == 0 && kend == 16) {
+    // rows of the next 4 bytes are read while these 4 are stepped (the row
+    // reads do not depend on D); acc is folded per byte so no D is kept
+    uint32_t ra[4][NW], rb[4][NW];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      uint32_t row[NW];
-      sam_row<NW>(B, (w[j >> 2] >> (8 * (j & 3))) & 0xFF, row);
+    for (int jj = 0; jj < 4; ++jj) sam_row<NW>(B, (w[0] >> (8 * jj)) & 0xFF, ra[jj]);
 #pragma unroll
-      for (int x = 0; x < NW; ++x) {
-        D[x] = ((D[x] << 1) | m.init[x]) & row[x];
-        acc |= D[x];
+    for (int q = 0; q < 4; ++q) {
+      if (q + 1 < 4) {
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) sam_row<NW>(B, (w[q + 1] >> (8 * jj)) & 0xFF, rb[jj]);
       }
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+#pragma unroll
+        for (int x = 0; x < NW; ++x) {
+          D[x] = ((D[x] << 1) | m.init[x]) & ra[jj][x];
+          acc |= D[x];
+        }
+        asm volatile("" : "+v"(acc));
+      }
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+        for (int x = 0; x < NW; ++x) ra[jj][x] = rb[jj][x];
     }
   } else {
 #pragma unroll
@@ -1909,7 +1924,7 @@ hipError_t launch_find_iter_multi(const BatchDev &b, int nre, const FwdDfaDev *c
   if (!sa_tile_ok(b, g)) return hipErrorNotSupported;
   // every regex's scratch is live at once: fewer speculative slots per unit
   // (a unit with more matches is re-run by the emit pass instead of copied)
-  g.slots = std::min<uint32_t>(g.slots, 32);
+  g.slots = std::min<uint32_t>(g.slots, 16);
   SaMulti m{};
   m.nre = (uint32_t)nre;
   m.len = f[0]->sa_len;

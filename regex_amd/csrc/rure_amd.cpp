@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <array>
 #include <cstdio>
 #include <cstdlib>
@@ -401,7 +402,21 @@ struct Blob {
   }
 };
 
+// The scans take their scratch from the stream-ordered allocator; keep up to
+// 4 GiB of freed blocks in the device's pool instead of returning them to
+// the driver at every synchronisation (a multi-regex find_iter holds one
+// scratch per regex at once), once per device.
+static void keep_pool(int dev) {
+  static std::atomic<uint32_t> done{0};
+  if (dev < 0 || dev >= 32 || (done.fetch_or(1u << dev) & (1u << dev))) return;
+  hipMemPool_t pool;
+  if (hipDeviceGetDefaultMemPool(&pool, dev) != hipSuccess) return;
+  uint64_t thr = 4ull << 30;
+  (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+}
+
 int device_cus(int dev) {
+  keep_pool(dev);
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return 256;
   return prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
