@@ -864,30 +864,17 @@ __device__ __forceinline__ void sam_block(uint32_t (&D)[NW], const uint32_t *B, 
   // layout of final bits in practice (8-bit sequences), and a bit that is
   // final only in another word just sends the block down the exact walk
   if (k0 == 0 && kend == 16) {
-    // rows of the next 4 bytes are read while these 4 are stepped (the row
-    // reads do not depend on D); acc is folded per byte so no D is kept
-    uint32_t ra[4][NW], rb[4][NW];
+    // acc is folded per byte, so no D is kept for a later OR tree
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) sam_row<NW>(B, (w[0] >> (8 * jj)) & 0xFF, ra[jj]);
+    for (int j = 0; j < 16; ++j) {
+      uint32_t row[NW];
+      sam_row<NW>(B, (w[j >> 2] >> (8 * (j & 3))) & 0xFF, row);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (q + 1 < 4) {
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) sam_row<NW>(B, (w[q + 1] >> (8 * jj)) & 0xFF, rb[jj]);
+      for (int x = 0; x < NW; ++x) {
+        D[x] = ((D[x] << 1) | m.init[x]) & row[x];
+        acc |= D[x];
       }
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-#pragma unroll
-        for (int x = 0; x < NW; ++x) {
-          D[x] = ((D[x] << 1) | m.init[x]) & ra[jj][x];
-          acc |= D[x];
-        }
-        asm volatile("" : "+v"(acc));
-      }
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj)
-#pragma unroll
-        for (int x = 0; x < NW; ++x) ra[jj][x] = rb[jj][x];
+      asm volatile("" : "+v"(acc));
     }
   } else {
 #pragma unroll
@@ -936,7 +923,7 @@ __device__ __forceinline__ void sam_block(uint32_t (&D)[NW], const uint32_t *B, 
 }
 
 template <int NW>
-__global__ __launch_bounds__(256) void iter_spec_sa_multi_tile_kernel(BatchDev b, Geo g, uint64_t nunits, SaMulti m) {
+__global__ __launch_bounds__(256, 3) void iter_spec_sa_multi_tile_kernel(BatchDev b, Geo g, uint64_t nunits, SaMulti m) {
   __shared__ __attribute__((aligned(16))) uint32_t B[256 * SamPitch<NW>::v];
   __shared__ __attribute__((aligned(16))) uint4 stage[4][64 * 8];
   for (uint32_t i = threadIdx.x; i < 256 * SamPitch<NW>::v; i += blockDim.x) B[i] = m.image[i];
