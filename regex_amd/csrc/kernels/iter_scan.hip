@@ -857,26 +857,55 @@ __device__ __forceinline__ void sam_block(uint32_t (&D)[NW], const uint32_t *B, 
                                           uint32_t (&p)[kSaMultiMax], uint32_t (&lm)[kSaMultiMax],
                                           uint32_t (&n)[kSaMultiMax], uint64_t u, uint32_t nslots) {
   uint32_t D0[NW];
-  uint32_t acc = 0;
 #pragma unroll
   for (int x = 0; x < NW; ++x) D0[x] = D[x];
-  // acc: the OR of every word's bits after every byte; the words share one
-  // layout of final bits in practice (8-bit sequences), and a bit that is
-  // final only in another word just sends the block down the exact walk
   if (k0 == 0 && kend == 16) {
-    // acc is folded per byte, so no D is kept for a later OR tree
+    // Whole block: fm = the bytes after which some word holds a final bit
+    // (with 9 variants ~57% of wave-blocks hold one somewhere), and Dm = the
+    // words after the last such byte, so a block with one such byte (almost
+    // all of them) settles its matches without a second walk.
+    uint32_t fm = 0, Dm[NW];
+#pragma unroll
+    for (int x = 0; x < NW; ++x) Dm[x] = 0;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       uint32_t row[NW];
       sam_row<NW>(B, (w[j >> 2] >> (8 * (j & 3))) & 0xFF, row);
+      uint32_t t = 0;
 #pragma unroll
       for (int x = 0; x < NW; ++x) {
         D[x] = ((D[x] << 1) | m.init[x]) & row[x];
-        acc |= D[x];
+        t |= D[x];
       }
-      asm volatile("" : "+v"(acc));
+      const bool hit = (t & m.fany) != 0;
+      fm |= hit ? (1u << j) : 0u;
+#pragma unroll
+      for (int x = 0; x < NW; ++x) {
+        Dm[x] = hit ? D[x] : Dm[x];
+        asm volatile("" : "+v"(Dm[x]));  // per byte: no copies of D kept for later selects
+      }
+      asm volatile("" : "+v"(fm));
+    }
+    if (!fm) return;
+    if (__builtin_popcount(fm) == 1) {
+      const uint32_t j = __builtin_ctz(fm);
+      const uint64_t e = (uint64_t)bp + j + 1, st = e - m.len;
+#pragma unroll
+      for (int q = 0; q < kSaMultiMax; ++q) {
+        if ((uint32_t)q >= m.nre) break;
+        uint32_t ew = Dm[0];
+#pragma unroll
+        for (int x = 1; x < NW; ++x) ew = m.word[q] == (uint32_t)x ? Dm[x] : ew;
+        if ((ew & m.fin[q]) && st >= c0 + p[q] && st < c1) {
+          if (n[q] < nslots) *(ulonglong2 *)&m.slots[q][(u * nslots + n[q]) * 2] = make_ulonglong2(st, e);
+          ++n[q];
+          p[q] = lm[q] = (uint32_t)(e - c0);
+        }
+      }
+      return;
     }
   } else {
+    uint32_t acc = 0;
 #pragma unroll
     for (uint32_t j = 0; j < 16; ++j) {
       uint32_t row[NW];
@@ -889,8 +918,8 @@ __device__ __forceinline__ void sam_block(uint32_t (&D)[NW], const uint32_t *B, 
         acc |= act ? Dn : 0u;
       }
     }
+    if (!(acc & m.fany)) return;
   }
-  if (!(acc & m.fany)) return;
   // rare: the block holds string ends; walk it byte by byte
   uint32_t E[NW];
 #pragma unroll
@@ -923,7 +952,7 @@ __device__ __forceinline__ void sam_block(uint32_t (&D)[NW], const uint32_t *B, 
 }
 
 template <int NW>
-__global__ __launch_bounds__(256, 3) void iter_spec_sa_multi_tile_kernel(BatchDev b, Geo g, uint64_t nunits, SaMulti m) {
+__global__ __launch_bounds__(256) void iter_spec_sa_multi_tile_kernel(BatchDev b, Geo g, uint64_t nunits, SaMulti m) {
   __shared__ __attribute__((aligned(16))) uint32_t B[256 * SamPitch<NW>::v];
   __shared__ __attribute__((aligned(16))) uint4 stage[4][64 * 8];
   for (uint32_t i = threadIdx.x; i < 256 * SamPitch<NW>::v; i += blockDim.x) B[i] = m.image[i];
