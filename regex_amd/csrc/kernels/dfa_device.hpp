@@ -334,4 +334,69 @@ __device__ __forceinline__ int dfa_find_cut(const FwdDfaDev &f, const RevDfaDev 
   return 1;
 }
 
+// Literal engine (find_iter pass 1 and find / is_match batches): the first
+// literal, in leftmost-first priority order, that occurs at position i, or -1.
+// The caller guarantees i + lit_k <= len (i below len + 1 - lit_minlen).
+__device__ __forceinline__ int lit_verify(const FwdDfaDev &f, const uint8_t *lds, const uint8_t *base, uint64_t len,
+                                          uint64_t i) {
+  uint32_t key = 0;
+  for (uint32_t j = 0; j < f.lit_k; ++j) key |= (uint32_t)base[i + j] << (8 * j);
+  const uint32_t *keys = (const uint32_t *)(lds + kLitKeys);
+  for (uint32_t x = 0; x < f.lit_n; ++x) {
+    if (keys[x] != key) continue;
+    const uint32_t ln = lds[kLitLens + x];
+    if (i + ln > len) continue;
+    const uint8_t *lb = lds + kLitBytes + x * kLitLen;
+    uint32_t j = f.lit_k;
+    while (j < ln && base[i + j] == lb[j]) ++j;
+    if (j == ln) return (int)x;
+  }
+  return -1;
+}
+
+
+// Candidate starts of the 64 positions [a, a + 64) (a 16-byte aligned):
+// bit j = the hash of the lit_k bytes at a + j is in the prefix bitmap (and,
+// K8, the hash of bytes 4..7 in the second one).  Blocks at or past hi_blk
+// read as zeros; each position is tested on its own, so the 64 LDS probes are
+// independent (no dependent chain per byte).
+template <bool K4, bool K8>
+__device__ __forceinline__ uint64_t lit_cands64(uintptr_t a, uintptr_t hi_blk, const uint32_t *bitmap,
+                                                const uint32_t *bitmap2, uint32_t kmask) {
+  // 64 positions per step: 4 blocks and the first word after them
+  uint32_t d[18];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (a + 16 * k < hi_blk) v = *(const uint4 *)(a + 16 * k);
+    d[4 * k] = v.x;
+    d[4 * k + 1] = v.y;
+    d[4 * k + 2] = v.z;
+    d[4 * k + 3] = v.w;
+  }
+  if (a + 64 < hi_blk) {
+    const uint2 t2 = *(const uint2 *)(a + 64);
+    d[16] = t2.x;
+    d[17] = t2.y;
+  } else {
+    d[16] = d[17] = 0u;
+  }
+  uint32_t clo = 0, chi = 0;
+#pragma unroll
+  for (int j = 0; j < 64; ++j) {
+    const uint32_t w = (j & 3) ? __builtin_amdgcn_alignbyte(d[(j >> 2) + 1], d[j >> 2], j & 3) : d[j >> 2];
+    const uint32_t hh = lit_hash(K4 ? w : (w & kmask));
+    uint32_t bit = (bitmap[hh >> 5] >> (hh & 31)) & 1u;
+    if (K8) {  // bytes 4..7 too: candidates of a small alphabet (DNA) stay rare
+      const uint32_t w2 =
+          (j & 3) ? __builtin_amdgcn_alignbyte(d[(j >> 2) + 2], d[(j >> 2) + 1], j & 3) : d[(j >> 2) + 1];
+      const uint32_t h2 = lit_hash(w2);
+      bit &= (bitmap2[h2 >> 5] >> (h2 & 31)) & 1u;
+    }
+    if (j < 32) clo |= bit << j;
+    else chi |= bit << (j - 32);
+  }
+  return ((uint64_t)chi << 32) | clo;
+}
+
 }  // namespace rure_amd

@@ -92,6 +92,97 @@ __global__ __launch_bounds__(256) void dfa_fwd_kernel(BatchDev bt, FwdDfaDev f, 
   }
 }
 
+static std::atomic<int> g_last_fwd_path{-1};
+int last_fwd_path() { return g_last_fwd_path.load(); }
+
+// ------------------------------------------------------- literal engine
+// MatchType::Literal for find / is_match batches (exec.rs:601-625 find_literals,
+// dispatched by exec.rs:1148-1166 when the regex is a complete finite string
+// set).  The regex's literals (host/literals.hpp, leftmost-first priority
+// order, non-empty, no look-around) live in the find_iter DFA's literal image;
+// f must be that DFA.  One lane per haystack walks 64 start positions per
+// step through the prefix-hash bitmap (lit_cands64: 64 independent LDS probes
+// instead of a dependent DFA chain) and stops at the first position where a
+// literal occurs: the leftmost start, and there the first literal in priority
+// order is the leftmost-first match.  No reverse scan: the literal's length
+// gives the end.
+template <int MODE, bool STRIDED, bool K4, bool K8>
+__global__ __launch_bounds__(256) void lit_find_kernel(BatchDev bt, FwdDfaDev f, void *out) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  for (uint32_t i = threadIdx.x * 16; i < f.lit_bytes; i += blockDim.x * 16)
+    *(uint4 *)(lds + i) = *(const uint4 *)(f.lit_image + i);
+  __syncthreads();
+  const uint32_t *bitmap = (const uint32_t *)lds;
+  const uint32_t *bitmap2 = (const uint32_t *)(lds + kLitBitmap2);
+  const uint32_t kmask = K4 ? 0xFFFFFFFFu : ((1u << (8 * f.lit_k)) - 1);
+  const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; h < bt.count; h += nthreads) {
+    const uint8_t *base;
+    uint64_t len;
+    if (STRIDED) {
+      base = bt.hay + h * bt.stride;
+      len = bt.length;
+    } else {
+      const uint64_t o0 = bt.offs[h], o1 = bt.offs[h + 1];
+      base = bt.hay + o0;
+      len = o1 - o0;
+    }
+    uint64_t ms = NONE, me = NONE;
+    // candidate starts [start, iend): room for the shortest literal
+    const uint64_t iend = len + 1 >= f.lit_minlen ? len + 1 - f.lit_minlen : 0;
+    if (iend > bt.start) {
+      const uintptr_t hi_blk = (uintptr_t)(base + len);
+      const uintptr_t aend = (uintptr_t)(base + iend);
+      for (uintptr_t a = (uintptr_t)(base + bt.start) & ~(uintptr_t)15; a < aend && ms == NONE; a += 64) {
+        uint64_t cand = lit_cands64<K4, K8>(a, hi_blk, bitmap, bitmap2, kmask);
+        const int64_t p0 = (int64_t)(a - (uintptr_t)base);
+        while (cand) {
+          const int j = __builtin_ctzll(cand);
+          cand &= cand - 1;
+          const int64_t i = p0 + j;
+          if (i < (int64_t)bt.start || (uint64_t)i >= iend) continue;
+          const int x = lit_verify(f, lds, base, len, (uint64_t)i);
+          if (x < 0) continue;
+          ms = (uint64_t)i;
+          me = ms + lds[kLitLens + x];
+          break;
+        }
+      }
+    }
+    if (MODE == MODE_ISMATCH) {
+      ((uint8_t *)out)[h] = ms != NONE ? 1 : 0;
+    } else {
+      ((uint64_t *)out)[2 * h] = ms;
+      ((uint64_t *)out)[2 * h + 1] = me;
+    }
+  }
+}
+
+template <int MODE, bool STRIDED>
+static hipError_t launch_lit_find_m(const BatchDev &b, const FwdDfaDev &f, void *out, hipStream_t st, int grid) {
+  if (f.lit_k8)
+    hipLaunchKernelGGL((lit_find_kernel<MODE, STRIDED, true, true>), dim3(grid), dim3(256), kLitImage, st, b, f, out);
+  else if (f.lit_k == 4)
+    hipLaunchKernelGGL((lit_find_kernel<MODE, STRIDED, true, false>), dim3(grid), dim3(256), kLitImage, st, b, f, out);
+  else
+    hipLaunchKernelGGL((lit_find_kernel<MODE, STRIDED, false, false>), dim3(grid), dim3(256), kLitImage, st, b, f,
+                       out);
+  return hipGetLastError();
+}
+
+hipError_t launch_lit_find(int mode, const BatchDev &b, const FwdDfaDev &f, void *out, hipStream_t st) {
+  if (!f.lit_n || (mode != MODE_FIND && mode != MODE_ISMATCH)) return hipErrorInvalidValue;
+  const uint64_t blocks = (b.count + 255) / 256;
+  const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)f.cus * 32));
+  g_last_fwd_path.store(-3);
+  const bool strided = b.offs == nullptr;
+  if (mode == MODE_FIND)
+    return strided ? launch_lit_find_m<MODE_FIND, true>(b, f, out, st, grid)
+                   : launch_lit_find_m<MODE_FIND, false>(b, f, out, st, grid);
+  return strided ? launch_lit_find_m<MODE_ISMATCH, true>(b, f, out, st, grid)
+                 : launch_lit_find_m<MODE_ISMATCH, false>(b, f, out, st, grid);
+}
+
 // ------------------------------------------------------- coalesced tiles
 // Fixed-stride batches (stride % 16 == 0, search start 0, hot set <= 63
 // states): a wave owns 64 consecutive haystacks and walks them in lockstep
@@ -677,8 +768,6 @@ hipError_t launch_set_cores(const BatchDev &b, const SetCoreDev &f, uint64_t *ou
   return go(set_core_kernel<0>);
 }
 
-static std::atomic<int> g_last_fwd_path{-1};
-int last_fwd_path() { return g_last_fwd_path.load(); }
 
 // ------------------------------------------------------- anchored reverse
 // MatchType::DfaAnchoredReverse (exec.rs:1175-1177): a regex anchored at the

@@ -224,10 +224,15 @@ hipError_t launch_long_scan(int mode, const BatchDev &b, const FwdDfaDev &f, con
 
 hipError_t launch_dfa_fwd(int mode, const BatchDev &b, const FwdDfaDev &f, const RevDfaDev &r, void *out,
                           hipStream_t st, int grid);
+// MatchType::Literal (exec.rs:601-625, 1148-1166) for MODE_FIND / MODE_ISMATCH
+// batches of a regex that is a finite string set: f = the find_iter DFA
+// (lit_n > 0); same output layout as launch_dfa_fwd; last_fwd_path() = -3.
+hipError_t launch_lit_find(int mode, const BatchDev &b, const FwdDfaDev &f, void *out, hipStream_t st);
 // Which forward-scan kernel the last launch_dfa_fwd call launched (tests
 // assert the instantiation the bench times): 0 = dfa_fwd_kernel (per-lane
 // streaming), 1 / 2 / 4 = dfa_fwd_tile_kernel with that many bytes per
-// dependent LDS lookup.
+// dependent LDS lookup, -2 = the anchored reverse scan, -3 = the literal
+// engine.
 int last_fwd_path();
 // Multi-GPU gather (gather_scan.hip): records (3 u64: base + haystack, start,
 // end) of the haystacks whose find result holds a match, first `cap`; *count.

@@ -1699,6 +1699,23 @@ bool rure_set_matches(rure_set *rs, const uint8_t *hay, size_t len, size_t start
 }
 
 // ------------------------------------------------------------------ batches
+// MatchType::Literal (exec.rs:1148-1166 -> find_literals, exec.rs:601-625):
+// a regex that is a finite string set answers find / is_match from its
+// literals instead of the DFA when the forward DFA does not fit the u8 LDS
+// image (> 255 states; then the DFA kernels take global-table steps) —
+// batches of many haystacks only (few long ones keep the chunked DFA scan).
+// RURE_AMD_LIT=1 / 0 forces the literal engine on / off.
+static const FwdDfaDev *literal_engine(rure *re, DevTables &t, const BatchDev &b) {
+  if (!re->lit_ok) return nullptr;
+  uint64_t chunk;
+  const char *env = getenv("RURE_AMD_LIT");
+  if (env ? env[0] != '1' : (t.has_dfa && t.f.all)) return nullptr;
+  if (long_batch(b, t, &chunk)) return nullptr;
+  std::string err;
+  const FwdDfaDev *fi = iter_device(re, t, &err);
+  return fi && fi->lit_n ? fi : nullptr;
+}
+
 int rure_amd_find_batch(rure *re, const rure_amd_batch *batch, rure_match *out, void *stream) {
   static_assert(sizeof(rure_match) == 16, "rure_match layout");
   BatchDev b;
@@ -1707,6 +1724,8 @@ int rure_amd_find_batch(rure *re, const rure_amd_batch *batch, rure_match *out, 
   std::string err;
   DevTables *t = regex_device(re, &err);
   if (!t) return err.rfind("HIP", 0) == 0 ? RURE_AMD_ERR_HIP : RURE_AMD_ERR_DFA;
+  if (const FwdDfaDev *lit = literal_engine(re, *t, b))
+    return launch_lit_find(MODE_FIND, b, *lit, out, (hipStream_t)stream) == hipSuccess ? RURE_AMD_OK : RURE_AMD_ERR_HIP;
   int grid = grid_for(b.count, t->f.lds_bytes, t->cus);
   uint64_t chunk;
   const FwdDfaDev *iter = long_batch(b, *t, &chunk) ? iter_device(re, *t, &err) : nullptr;
@@ -1747,6 +1766,9 @@ int rure_amd_is_match_batch(rure *re, const rure_amd_batch *batch, uint8_t *out,
   std::string err;
   DevTables *t = regex_device(re, &err);
   if (!t) return err.rfind("HIP", 0) == 0 ? RURE_AMD_ERR_HIP : RURE_AMD_ERR_DFA;
+  if (const FwdDfaDev *lit = literal_engine(re, *t, b))
+    return launch_lit_find(MODE_ISMATCH, b, *lit, out, (hipStream_t)stream) == hipSuccess ? RURE_AMD_OK
+                                                                                      : RURE_AMD_ERR_HIP;
   int grid = grid_for(b.count, t->f.lds_bytes, t->cus);
   uint64_t chunk;
   const FwdDfaDev *iter = long_batch(b, *t, &chunk) ? iter_device(re, *t, &err) : nullptr;

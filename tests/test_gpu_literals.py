@@ -157,3 +157,99 @@ def test_literal_ragged_and_start(cuda):
                 exp.append((s, e))
             c, m = re.find_iter_batch(dev(t, cuda), stride=len(t), length=len(t), count=1, start=start)
             assert pairs(m) == exp, (pat, start)
+
+
+# ---------------------------------------------------------------------------
+# find / is_match batches through the literal engine (lit_find_kernel,
+# MatchType::Literal: exec.rs:601-625, 1148-1166): the leftmost start, and
+# there the first literal in priority order, bit-equal to the oracle's
+# leftmost-first find (the restated reference DFA) per haystack; strided and
+# offset batches, start > 0, haystacks shorter than the shortest literal,
+# matches at the very end of a haystack and odd lengths.
+def _haystacks(pat, n, maxlen, seed):
+    rng = random.Random(seed ^ zlib.crc32(pat.encode()))
+    alpha = [b"a", b"b", b"c", b"d", b"x", b"g", b"t", b"foo", b"bar", b"0", b"1", b"2", b"3", "é".encode(),
+             b"Holm", b"holm", b" ", b"aaaaaaaa", b"Sherlock", b"Watson", b"agggtaaa", b"tttaccct", b"\xff"]
+    out = []
+    for i in range(n):
+        k = rng.randrange(0, maxlen)
+        s = b"".join(rng.choice(alpha) for _ in range(k))[:k]
+        out.append(s)
+    return out
+
+
+def _offsets_batch(hs, cuda):
+    import torch
+    offs = np.zeros(len(hs) + 1, dtype=np.int64)
+    offs[1:] = np.cumsum([len(h) for h in hs])
+    buf = b"".join(hs)
+    return buf, offs, dev(buf, cuda), torch.from_numpy(offs).to(cuda)
+
+
+@pytest.mark.parametrize("pat", PATTERNS)
+def test_literal_find_batch_offsets(cuda, pat):
+    from regex_amd import _native as NN
+    re = R.Regex(pat)
+    o = OracleRegex(re)
+    hs = _haystacks(pat, 3000, 200, 1)
+    buf, offs, dbuf, doffs = _offsets_batch(hs, cuda)
+    for start in (0, 3):
+        got = re.find_batch(dbuf, offsets=doffs, start=start).cpu().numpy().astype(np.uint64)
+        assert NN.rure_amd_last_fwd_path() == -3
+        exp = [o.find(h, start) if start <= len(h) else None for h in hs]
+        for i, (h, e) in enumerate(zip(hs, exp)):
+            g = None if got[i, 0] == np.uint64(2**64 - 1) else (int(got[i, 0]), int(got[i, 1]))
+            assert g == e, (pat, i, h, start)
+        m = re.is_match_batch(dbuf, offsets=doffs, start=start).cpu().numpy()
+        assert [bool(x) for x in m] == [e is not None for e in exp], (pat, start)
+
+
+@pytest.mark.parametrize("pat", [r"Sherlock|Holmes|Watson", r"a|ab", r"agggtaaa|tttaccct", r"aa"])
+def test_literal_find_batch_strided(cuda, pat):
+    re = R.Regex(pat)
+    o = OracleRegex(re)
+    L, S = 333, 336
+    hs = _haystacks(pat, 5000, L, 2)
+    rows = [h[:L].ljust(L, b"z") for h in hs]
+    buf = b"".join(r.ljust(S, b"\0") for r in rows)
+    got = re.find_batch(dev(buf, cuda), stride=S, length=L, count=len(rows)).cpu().numpy().astype(np.uint64)
+    exp, _ = o.find_batch(np.frombuffer(buf, dtype=np.uint8).copy(), S, L, len(rows), nthreads=4)
+    assert np.array_equal(got, exp.astype(np.uint64)), pat
+    m = re.is_match_batch(dev(buf, cuda), stride=S, length=L, count=len(rows)).cpu().numpy()
+    assert np.array_equal(m, o.is_match_batch(np.frombuffer(buf, dtype=np.uint8).copy(), S, L, len(rows), 4)), pat
+
+
+def test_literal_find_default_dispatch(cuda, monkeypatch):
+    """64 words (a forward DFA beyond the u8 LDS image) take the literal
+    engine without RURE_AMD_LIT; RURE_AMD_LIT=0 gives the DFA the same
+    answers."""
+    from regex_amd import _native as NN
+    monkeypatch.delenv("RURE_AMD_LIT", raising=False)
+    text = corpus("sherlock")
+    words = sorted(set(w for w in text.decode("latin-1").split() if w.isalpha() and 5 <= len(w) <= 12))
+    rng = np.random.default_rng(11)
+    pat = "|".join(rng.choice(words, 64, replace=False))
+    re = R.Regex(pat)
+    assert len(re.literals()) == 64
+    L = 2000
+    n = len(text) // L
+    buf = text[: n * L]
+    d = dev(buf, cuda)
+    got = re.find_batch(d, stride=L, length=L, count=n).cpu().numpy()
+    path = NN.rure_amd_last_fwd_path()
+    monkeypatch.setenv("RURE_AMD_LIT", "0")
+    ref = re.find_batch(d, stride=L, length=L, count=n).cpu().numpy()
+    assert NN.rure_amd_last_fwd_path() != -3
+    assert np.array_equal(got, ref)
+    exp, _ = R_oracle_find(re, buf, L, n)
+    assert np.array_equal(got.astype(np.uint64), exp)
+    assert (got[:, 0] >= 0).sum() > n // 4
+    info = re.dfa_info(0)
+    assert info and info["states"] > 300, info  # beyond the u8 LDS image
+    assert path == -3
+
+
+def R_oracle_find(re, buf, L, n):
+    o = OracleRegex(re)
+    exp, st = o.find_batch(np.frombuffer(buf, dtype=np.uint8).copy(), L, L, n, nthreads=4)
+    return exp.astype(np.uint64), st
