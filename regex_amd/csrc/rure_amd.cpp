@@ -487,6 +487,7 @@ struct rure {
   DenseDfa dfwd_iter;
   PackedFwd pf_iter;
   bool lit_ok = false;      // the regex is a finite string set (literal find_iter engine)
+  bool lits_done = false;   // lit_ok / lits computed (build_iter_dfa or literal_engine)
   uint32_t fb_n = 0;        // first-byte start rule (first_byte_rule): |F| or 0
   uint8_t fb_bytes[4] = {0, 0, 0, 0};
   std::vector<uint8_t> lex;   // lexer table (build_lex), empty if none
@@ -946,7 +947,8 @@ bool build_iter_dfa(rure *re) {
     lim.strip = true;
     std::string e;
     re->iter_ok = build_dense_dfa(re->fwd, lim, &re->dfwd_iter, &e) && pack_forward(re->dfwd_iter, &re->pf_iter, &e, true);
-    re->lit_ok = extract_literals(re->nfa, kLitMax, kLitLen, &re->lits);
+    if (!re->lits_done) re->lit_ok = extract_literals(re->nfa, kLitMax, kLitLen, &re->lits);
+    re->lits_done = true;
     if (re->iter_ok)
       re->fb_n = first_byte_rule(re->dfwd_iter, re->pf_iter.ustart1, !can_match_empty(re->nfa), re->fb_bytes);
     if (re->iter_ok) build_lex(re->dfwd_iter, re->pf_iter.ustart1, re->fb_n, &re->lex, &re->lex_s0);
@@ -1700,17 +1702,29 @@ bool rure_set_matches(rure_set *rs, const uint8_t *hay, size_t len, size_t start
 
 // ------------------------------------------------------------------ batches
 // MatchType::Literal (exec.rs:1148-1166 -> find_literals, exec.rs:601-625):
-// a regex that is a finite string set answers find / is_match from its
-// literals instead of the DFA when the forward DFA does not fit the u8 LDS
-// image (> 255 states; then the DFA kernels take global-table steps) —
-// batches of many haystacks only (few long ones keep the chunked DFA scan).
-// RURE_AMD_LIT=1 / 0 forces the literal engine on / off.
+// a regex that is a finite string set can answer find / is_match from its
+// literals instead of the DFA.  On the GPU that wins for a few literals
+// (tools/lit_find_bench.py, find over 262144 x 2000 B of sherlock text,
+// literal engine vs DFA: 1 word 0.19 vs 0.22 ms, 3 words 0.19 vs 0.32,
+// 4 words 0.24 vs 0.30, 8 words 0.24 vs 0.29, 2 rare words 0.29 vs 0.29;
+// 16 words 0.30 vs 0.25 and 64 words 0.76 vs 0.63 favour the DFA, whose
+// lookups stay one LDS read per byte while candidate verification grows with
+// the literal count), so by default it runs for at most kLitFindMax
+// literals, on batches of many haystacks (few long ones keep the chunked DFA
+// scan).  RURE_AMD_LIT=1 / 0 forces it on / off.
+static constexpr size_t kLitFindMax = 8;
 static const FwdDfaDev *literal_engine(rure *re, DevTables &t, const BatchDev &b) {
-  if (!re->lit_ok) return nullptr;
   uint64_t chunk;
   const char *env = getenv("RURE_AMD_LIT");
-  if (env ? env[0] != '1' : (t.has_dfa && t.f.all)) return nullptr;
+  if (env && env[0] != '1') return nullptr;
   if (long_batch(b, t, &chunk)) return nullptr;
+  {
+    // the literal set alone (cheap) before any find_iter DFA is built
+    std::lock_guard<std::mutex> g(re->mu);
+    if (!re->iter_built && !re->lits_done) re->lit_ok = extract_literals(re->nfa, kLitMax, kLitLen, &re->lits);
+    re->lits_done = true;
+    if (!re->lit_ok || (!env && re->lits.lits.size() > kLitFindMax)) return nullptr;
+  }
   std::string err;
   const FwdDfaDev *fi = iter_device(re, t, &err);
   return fi && fi->lit_n ? fi : nullptr;

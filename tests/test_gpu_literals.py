@@ -219,34 +219,39 @@ def test_literal_find_batch_strided(cuda, pat):
     assert np.array_equal(m, o.is_match_batch(np.frombuffer(buf, dtype=np.uint8).copy(), S, L, len(rows), 4)), pat
 
 
-def test_literal_find_default_dispatch(cuda, monkeypatch):
-    """64 words (a forward DFA beyond the u8 LDS image) take the literal
-    engine without RURE_AMD_LIT; RURE_AMD_LIT=0 gives the DFA the same
-    answers."""
+@pytest.mark.parametrize("nwords", [3, 64])
+def test_literal_find_default_dispatch(cuda, monkeypatch, nwords):
+    """Without RURE_AMD_LIT a set of at most 8 literals takes the literal
+    engine and a larger one the DFA (measured faster there); RURE_AMD_LIT=0
+    (the DFA) gives the same answers, and both equal the oracle."""
     from regex_amd import _native as NN
     monkeypatch.delenv("RURE_AMD_LIT", raising=False)
     text = corpus("sherlock")
-    words = sorted(set(w for w in text.decode("latin-1").split() if w.isalpha() and 5 <= len(w) <= 12))
-    rng = np.random.default_rng(11)
-    pat = "|".join(rng.choice(words, 64, replace=False))
+    if nwords == 3:
+        pat = r"Sherlock|Holmes|Watson"
+    else:
+        words = sorted(set(w for w in text.decode("latin-1").split() if w.isalpha() and 5 <= len(w) <= 12))
+        rng = np.random.default_rng(11)
+        pat = "|".join(rng.choice(words, nwords, replace=False))
     re = R.Regex(pat)
-    assert len(re.literals()) == 64
     L = 2000
     n = len(text) // L
     buf = text[: n * L]
     d = dev(buf, cuda)
     got = re.find_batch(d, stride=L, length=L, count=n).cpu().numpy()
     path = NN.rure_amd_last_fwd_path()
+    gm = re.is_match_batch(d, stride=L, length=L, count=n).cpu().numpy()
+    assert (path == -3) == (nwords <= 8), path
+    assert NN.rure_amd_last_fwd_path() == path
+    assert len(re.literals()) == nwords
     monkeypatch.setenv("RURE_AMD_LIT", "0")
     ref = re.find_batch(d, stride=L, length=L, count=n).cpu().numpy()
     assert NN.rure_amd_last_fwd_path() != -3
     assert np.array_equal(got, ref)
+    assert np.array_equal(gm, re.is_match_batch(d, stride=L, length=L, count=n).cpu().numpy())
     exp, _ = R_oracle_find(re, buf, L, n)
     assert np.array_equal(got.astype(np.uint64), exp)
     assert (got[:, 0] >= 0).sum() > n // 4
-    info = re.dfa_info(0)
-    assert info and info["states"] > 300, info  # beyond the u8 LDS image
-    assert path == -3
 
 
 def R_oracle_find(re, buf, L, n):

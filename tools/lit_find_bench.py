@@ -26,7 +26,11 @@ buf[: n * L].copy_(one.repeat(reps)[: n * L])
 words = sorted(set(w for w in text.decode("latin-1").split() if w.isalpha() and 5 <= len(w) <= 12))
 rng = np.random.default_rng(7)
 pats = {
+    "Holmes": r"Holmes",
     "Sherlock|Holmes|Watson": r"Sherlock|Holmes|Watson",
+    "2 rare words": "|".join(w + "zq" for w in rng.choice(words, 2, replace=False)),
+    "4 words": "|".join(rng.choice(words, 4, replace=False)),
+    "8 words": "|".join(rng.choice(words, 8, replace=False)),
     "16 words": "|".join(rng.choice(words, 16, replace=False)),
     "64 words": "|".join(rng.choice(words, 64, replace=False)),
     "64 rare words": "|".join(w + "zq" for w in rng.choice(words, 64, replace=False)),
