@@ -25,8 +25,6 @@
 #include <cstdlib>
 #include <cstring>
 #include <rocprim/rocprim.hpp>
-#include <map>
-#include <mutex>
 #include <vector>
 #include <stdint.h>
 
@@ -1880,56 +1878,6 @@ static hipError_t iter_post(const BatchDev &b, const Geo &g, uint64_t nunits, co
   return e;
 }
 
-// Side streams (per device, created once) for work that forks off a caller's
-// stream and joins back into it.
-static constexpr int kSideStreams = 4;
-static hipError_t side_streams(hipStream_t out[kSideStreams]) {
-  static std::mutex mu;
-  static std::map<int, std::vector<hipStream_t>> per_dev;
-  int d = 0;
-  hipError_t e = hipGetDevice(&d);
-  if (e != hipSuccess) return e;
-  std::lock_guard<std::mutex> g(mu);
-  std::vector<hipStream_t> &v = per_dev[d];
-  while (v.size() < (size_t)kSideStreams) {
-    hipStream_t s;
-    if ((e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) != hipSuccess) return e;
-    v.push_back(s);
-  }
-  for (int i = 0; i < kSideStreams; ++i) out[i] = v[i];
-  return hipSuccess;
-}
-
-// Run body(q, stream) for q < n, regex q on side stream q % kSideStreams,
-// forked from st after the work already queued there and joined back into st
-// (everything queued on st later waits for all of it).  The post passes of
-// the fused multi-regex pass are short, latency-bound kernels (fix, walk,
-// scan, emit, counts, exit per regex): run one regex after another they cost
-// more than the fused speculative pass saves; side by side they overlap.
-template <typename F>
-static hipError_t post_forked(int n, hipStream_t st, F body) {
-  hipStream_t side[kSideStreams];
-  hipError_t e = side_streams(side);
-  if (e != hipSuccess) return e;
-  const int ns = std::min(n, kSideStreams);
-  hipEvent_t fork = nullptr, join[kSideStreams] = {};
-  if ((e = hipEventCreateWithFlags(&fork, hipEventDisableTiming)) != hipSuccess) return e;
-  e = hipEventRecord(fork, st);
-  for (int i = 0; i < ns && e == hipSuccess; ++i) e = hipStreamWaitEvent(side[i], fork, 0);
-  for (int q = 0; q < n && e == hipSuccess; ++q) e = body(q, side[q % kSideStreams]);
-  // join even after a failure, so st never runs ahead of queued side work
-  for (int i = 0; i < ns; ++i) {
-    hipError_t e2 = hipEventCreateWithFlags(&join[i], hipEventDisableTiming);
-    if (e2 == hipSuccess) e2 = hipEventRecord(join[i], side[i]);
-    if (e2 == hipSuccess) e2 = hipStreamWaitEvent(st, join[i], 0);
-    if (e == hipSuccess) e = e2;
-  }
-  (void)hipEventDestroy(fork);
-  for (int i = 0; i < ns; ++i)
-    if (join[i]) (void)hipEventDestroy(join[i]);
-  return e;
-}
-
 // Several Shift-And regexes over the same span in one speculative pass
 // (iter_spec_sa_multi_tile_kernel), then each regex's own passes.  Returns
 // hipErrorNotSupported (nothing launched) when they do not qualify: every
@@ -1992,9 +1940,11 @@ hipError_t launch_find_iter_multi(const BatchDev &b, int nre, const FwdDfaDev *c
 #undef RURE_SAM
     if (e != hipSuccess) break;
     if ((e = hipGetLastError()) != hipSuccess) break;
-    e = post_forked(nre, st, [&](int q, hipStream_t sq) {
-      return iter_post(b, g, nunits, *f[q], *r[q], sc[q], o[q], spn ? &spn[q] : nullptr, sq, cus);
-    });
+    // each regex's post passes in turn (running them on side streams forked
+    // from st measured no faster: C3 variant phase 2.58 vs 2.48 ms,
+    // profiles/r02h_c3_summary.json vs r02g)
+    for (int q = 0; q < nre && e == hipSuccess; ++q)
+      e = iter_post(b, g, nunits, *f[q], *r[q], sc[q], o[q], spn ? &spn[q] : nullptr, st, cus);
   } while (false);
   for (int q = 0; q < made; ++q) {
     hipError_t e2 = hipFreeAsync(sc[q].buf, st);
