@@ -1471,8 +1471,9 @@ __global__ void iter_exit_kernel(const Unit *units, uint64_t nunits, uint64_t *e
 }
 
 // Pass 4: write every unit's matches at its offset.  Units whose speculation
-// held copy their slot buffer; the 64 lanes of a wave copy one unit at a time
-// (coalesced 16-byte records).  Units that were repaired, or had more matches
+// held copy their slot buffer: each lane its own unit's when it holds at most
+// 4 records, else the 64 lanes of a wave one unit at a time (coalesced
+// 16-byte records).  Units that were repaired, or had more matches
 // than slots, re-run their iteration (the block stages the hot tables only
 // then).
 __global__ __launch_bounds__(1024) void iter_emit_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
@@ -1497,7 +1498,23 @@ __global__ __launch_bounds__(1024) void iter_emit_kernel(BatchDev b, Geo g, uint
         skip = (fl & U_COPY) ? units[u].skip : 0;  // loaded by every lane at once, not per copied unit
       }
     }
-    uint64_t m = __ballot(copy);
+    // A unit with at most 4 records (almost every unit: the copy loop below
+    // is a chain of dependent load -> store rounds, one unit per round) copies
+    // its own records, every lane at once; larger ones go one at a time with
+    // the whole wave.
+    const bool own = copy && cnt <= 4;
+    if (own) {
+      const uint32_t nw = 2 * (uint32_t)min(cnt, cap - o0);
+      const uint64_t *src = slots + (u * g.slots + skip) * 2;
+      uint64_t *dst = out + 2 * o0;
+      uint64_t v[8];
+#pragma unroll
+      for (uint32_t k = 0; k < 8; ++k) v[k] = k < nw ? src[k] : 0;
+#pragma unroll
+      for (uint32_t k = 0; k < 8; ++k)
+        if (k < nw) dst[k] = v[k];
+    }
+    uint64_t m = __ballot(copy && !own);
     while (m) {
       const int l = __builtin_ctzll(m);
       m &= m - 1;
