@@ -445,7 +445,7 @@ def run_c3(ctx):
     P, W, rk = len(passes), ctx.world, ctx.rank
     pcount = torch.zeros((P,), dtype=torch.int64, device=ctx.dev)
     pexit = torch.zeros((P, 3), dtype=torch.int64, device=ctx.dev)
-    sp = R._stream_ptr(ctx.stream)
+    spv = [R._stream_ptr(ctx.stream)]
     stats = {"recomputed": 0}
 
     def span_raw(j, i, entry):
@@ -454,7 +454,7 @@ def run_c3(ctx):
         ent = ctypes.c_void_p(entry.data_ptr()) if entry is not None else None
         rc = NN.rure_amd_find_iter_span(re_._re, ctypes.c_void_p(buf.data_ptr()), L, lo, hi, ent,
                                         ctypes.c_void_p(pcount[j:].data_ptr()), ctypes.c_void_p(out.data_ptr()),
-                                        out.shape[0], ctypes.c_void_p(pexit[j].data_ptr()), sp)
+                                        out.shape[0], ctypes.c_void_p(pexit[j].data_ptr()), spv[0])
         assert rc == 0
 
     def repair(j):
@@ -503,7 +503,7 @@ def run_c3(ctx):
                 span_raw(j, rk, None)
             return
         rc = NN.rure_amd_find_iter_span_multi(m_res, nv, VP(seq.data_ptr()), M, v_lo, v_hi, None, m_cnt, m_out,
-                                              m_cap, m_exit, sp)
+                                              m_cap, m_exit, spv[0])
         assert rc == 0
 
     def step():
@@ -529,10 +529,19 @@ def run_c3(ctx):
         ok = ok and g == v["count"] * copies + seam * (copies - 1)
     ctx.ramp(variant_pass)
     sec = ctx.timed(step)
+    # host time to enqueue one variant phase (no sync inside): the phase is
+    # ~100 launches and stream-ordered allocations behind one long kernel
+    torch.cuda.synchronize()
+    hts = []
+    for _ in range(ctx.args.steps):
+        t0 = time.perf_counter()
+        variant_pass()
+        hts.append(time.perf_counter() - t0)
+        torch.cuda.synchronize()
     strip_ms = ctx.kernel_ms(strip_pass)
     var_ms = ctx.kernel_ms(variant_pass)
     scanned = N + len(variants) * M
-    extra = {}
+    extra = {"variant_host_enqueue_ms": round(float(np.median(hts)) * 1e3, 3)}
     if ctx.rank == 0 and not ctx.args.no_cpu:
         extra["cpu_baseline"] = cpu_baseline_c3(variants, seq, M, got, ctx.args)
     my_bytes = sum(span_bounds(L, W, rk)[1] - span_bounds(L, W, rk)[0] for _, _, L, _ in passes)
