@@ -252,4 +252,14 @@ hipError_t launch_dfa_anchored_rev(int mode, const BatchDev &b, const RevDfaDev 
                                    int grid);
 hipError_t launch_dfa_set(const BatchDev &b, const SetDfaDev &f, uint64_t *out, hipStream_t st, int grid);
 
+// Scratch from the stream-ordered allocator, cached per (device, stream)
+// (rure_amd.cpp): a freed block goes back to its stream's cache instead of to
+// hipFreeAsync — which on this ROCm waits for the stream's queued work when it
+// returns a large block (1-2 ms host stalls, one per freed scratch: the C3
+// variant phase spent more host time freeing than the GPU spent scanning) —
+// and an allocation on the same stream reuses it (stream order makes that
+// safe).  Same signatures as hipMallocAsync / hipFreeAsync.
+hipError_t scratch_malloc(void **p, size_t bytes, hipStream_t st);
+hipError_t scratch_free(void *p, hipStream_t st);
+
 }  // namespace rure_amd

@@ -129,7 +129,7 @@ __global__ __launch_bounds__(256) void one_match_write_kernel(const uint64_t *fo
 hipError_t launch_find_to_iter(const uint64_t *found, uint64_t n, uint64_t *counts, uint64_t *matches, uint64_t cap,
                                uint64_t *total, hipStream_t st) {
   uint64_t *buf = nullptr;
-  hipError_t e = hipMallocAsync((void **)&buf, (n + 1) * 16, st);
+  hipError_t e = scratch_malloc((void **)&buf, (n + 1) * 16, st);
   if (e != hipSuccess) return e;
   const uint32_t g = (uint32_t)std::min<uint64_t>((n + 255) / 256 ? (n + 255) / 256 : 1, 8192);
   e = hipMemsetAsync(buf + n, 0, 8, st);
@@ -143,7 +143,7 @@ hipError_t launch_find_to_iter(const uint64_t *found, uint64_t n, uint64_t *coun
                        total);
     e = hipGetLastError();
   }
-  hipError_t e2 = hipFreeAsync(buf, st);
+  hipError_t e2 = scratch_free(buf, st);
   return e != hipSuccess ? e : e2;
 }
 
@@ -160,7 +160,7 @@ hipError_t launch_compact_matches(const uint64_t *found, uint64_t n, uint64_t ba
   if (nb > 0x7fffffffull) return hipErrorInvalidValue;
   const bool scan = nb > 4096;
   uint64_t *blk = nullptr;
-  hipError_t e = hipMallocAsync((void **)&blk, nb * 8 * (scan ? 2 : 1), st);
+  hipError_t e = scratch_malloc((void **)&blk, nb * 8 * (scan ? 2 : 1), st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(compact_count_kernel, dim3((uint32_t)nb), dim3(256), 0, st, found, n, blk);
   e = hipGetLastError();
@@ -170,7 +170,7 @@ hipError_t launch_compact_matches(const uint64_t *found, uint64_t n, uint64_t ba
                        scan ? blk + nb : nullptr, rec, cap, count);
     e = hipGetLastError();
   }
-  hipError_t e2 = hipFreeAsync(blk, st);
+  hipError_t e2 = scratch_free(blk, st);
   return e != hipSuccess ? e : e2;
 }
 

@@ -1658,9 +1658,9 @@ hipError_t scan_counts(const uint32_t *counts, uint64_t *off, uint64_t n, hipStr
                                          rocprim::plus<uint64_t>(), st);
   if (e != hipSuccess) return e;
   void *buf = nullptr;
-  if ((e = hipMallocAsync(&buf, tmp, st)) != hipSuccess) return e;
+  if ((e = scratch_malloc(&buf, tmp, st)) != hipSuccess) return e;
   e = rocprim::exclusive_scan(buf, tmp, counts, off, (uint64_t)0, (size_t)(n + 1), rocprim::plus<uint64_t>(), st);
-  hipError_t e2 = hipFreeAsync(buf, st);
+  hipError_t e2 = scratch_free(buf, st);
   return e != hipSuccess ? e : e2;
 }
 
@@ -1758,7 +1758,7 @@ hipError_t long_scan_m(const BatchDev &b, const FwdDfaDev &f, const RevDfaDev &r
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   const size_t sz_u = MODE == MODE_FIND ? nunits * 16 : 0, sz_b = b.count * 8;
   uint8_t *buf = nullptr;
-  hipError_t e = hipMallocAsync((void **)&buf, al(sz_u) + al(sz_b), st);
+  hipError_t e = scratch_malloc((void **)&buf, al(sz_u) + al(sz_b), st);
   if (e != hipSuccess) return e;
   uint64_t *ures = (uint64_t *)buf;
   unsigned long long *best = (unsigned long long *)(buf + al(sz_u));
@@ -1773,7 +1773,7 @@ hipError_t long_scan_m(const BatchDev &b, const FwdDfaDev &f, const RevDfaDev &r
                        (const uint64_t *)ures, (const unsigned long long *)best, out);
     e = hipGetLastError();
   } while (false);
-  hipError_t e2 = hipFreeAsync(buf, st);
+  hipError_t e2 = scratch_free(buf, st);
   return e != hipSuccess ? e : e2;
 }
 
@@ -1817,7 +1817,7 @@ static hipError_t iter_scratch(uint64_t nunits, uint32_t nslots, hipStream_t st,
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   const size_t total = al(sz_units) + al(sz_slots) + al(sz_counts) + al(sz_off) + al(sz_queue) + 256;
   hipError_t e;
-  if ((e = hipMallocAsync((void **)&sc->buf, total, st)) != hipSuccess) return e;
+  if ((e = scratch_malloc((void **)&sc->buf, total, st)) != hipSuccess) return e;
   uint8_t *buf = sc->buf;
   sc->units = (Unit *)buf;
   sc->slots = (uint64_t *)(buf + al(sz_units));
@@ -1934,7 +1934,7 @@ hipError_t launch_find_iter_multi(const BatchDev &b, int nre, const FwdDfaDev *c
   uint32_t *img = nullptr;
   int made = 0;
   do {
-    if ((e = hipMallocAsync((void **)&img, 256 * kSaMultiWords * 4, st)) != hipSuccess) break;
+    if ((e = scratch_malloc((void **)&img, 256 * kSaMultiWords * 4, st)) != hipSuccess) break;
     m.image = img;
     for (; made < nre; ++made) {
       if ((e = iter_scratch(nunits, g.slots, st, &sc[made])) != hipSuccess) break;
@@ -1964,11 +1964,11 @@ hipError_t launch_find_iter_multi(const BatchDev &b, int nre, const FwdDfaDev *c
       e = iter_post(b, g, nunits, *f[q], *r[q], sc[q], o[q], spn ? &spn[q] : nullptr, st, cus);
   } while (false);
   for (int q = 0; q < made; ++q) {
-    hipError_t e2 = hipFreeAsync(sc[q].buf, st);
+    hipError_t e2 = scratch_free(sc[q].buf, st);
     if (e == hipSuccess) e = e2;
   }
   if (img) {
-    hipError_t e2 = hipFreeAsync(img, st);
+    hipError_t e2 = scratch_free(img, st);
     if (e == hipSuccess) e = e2;
   }
   return e;
@@ -2061,7 +2061,7 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
       if ((e = hipGetLastError()) != hipSuccess) break;
       e = iter_post(b, g, nunits, *f, r, sc, o, spn, st, cus);
     } while (false);
-    hipError_t e2 = hipFreeAsync(sc.buf, st);
+    hipError_t e2 = scratch_free(sc.buf, st);
     return e != hipSuccess ? e : e2;
   }
   // one wavefront per haystack (assertions, DFA quit, or no DFA)
@@ -2072,7 +2072,7 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
   const size_t sz_counts = (b.count + 1) * 4, sz_off = (b.count + 1) * 8;
   const size_t sz_scr = use_lds ? 0 : wb * (size_t)grid;
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-  if ((e = hipMallocAsync((void **)&buf, al(sz_counts) + al(sz_off) + al(sz_scr), st)) != hipSuccess) return e;
+  if ((e = scratch_malloc((void **)&buf, al(sz_counts) + al(sz_off) + al(sz_scr), st)) != hipSuccess) return e;
   uint32_t *counts = (uint32_t *)buf;
   uint64_t *off = (uint64_t *)(buf + al(sz_counts));
   uint8_t *scr = use_lds ? nullptr : buf + al(sz_counts) + al(sz_off);
@@ -2102,7 +2102,7 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
                        (uint64_t)1, off, o.counts, o.total);
     e = hipGetLastError();
   } while (false);
-  hipError_t e2 = hipFreeAsync(buf, st);
+  hipError_t e2 = scratch_free(buf, st);
   return e != hipSuccess ? e : e2;
 }
 

@@ -222,9 +222,9 @@ hipError_t exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, hip
   hipError_t e = rocprim::exclusive_scan(nullptr, tmp, in, out, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), st);
   if (e != hipSuccess) return e;
   void *buf = nullptr;
-  if ((e = hipMallocAsync(&buf, tmp, st)) != hipSuccess) return e;
+  if ((e = scratch_malloc(&buf, tmp, st)) != hipSuccess) return e;
   e = rocprim::exclusive_scan(buf, tmp, in, out, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), st);
-  hipError_t e2 = hipFreeAsync(buf, st);
+  hipError_t e2 = scratch_free(buf, st);
   return e != hipSuccess ? e : e2;
 }
 

@@ -415,6 +415,97 @@ static void keep_pool(int dev) {
   (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
 }
 
+// ---------------------------------------------------------- scratch cache
+// See dfa_scan.hpp scratch_malloc.  Blocks are rounded up (4 KiB, then
+// 64 KiB multiples) and reused on the stream that freed them when at most
+// twice the request; a stream keeps at most kScratchCacheMax bytes cached
+// (beyond that frees go to hipFreeAsync), and an allocation that fails
+// returns every cached block to the pool and retries once.
+}  // namespace
+
+namespace {
+constexpr size_t kScratchCacheMax = 8ull << 30;
+struct ScratchCache {
+  std::mutex mu;
+  std::map<std::pair<int, hipStream_t>, std::multimap<size_t, void *>> free_blocks;
+  std::map<std::pair<int, hipStream_t>, size_t> cached;
+  std::unordered_map<void *, size_t> sizes;  // every block made here (live or cached)
+};
+ScratchCache &scratch_cache() {
+  static ScratchCache *c = new ScratchCache();  // never destroyed: frees may run at exit
+  return *c;
+}
+size_t scratch_round(size_t n) { return n <= 4096 ? 4096 : (n + 65535) & ~(size_t)65535; }
+}  // namespace
+
+hipError_t rure_amd::scratch_malloc(void **p, size_t bytes, hipStream_t st) {
+  if (!p) return hipErrorInvalidValue;
+  int d = 0;
+  hipError_t e = hipGetDevice(&d);
+  if (e != hipSuccess) return e;
+  const size_t n = scratch_round(bytes);
+  const auto key = std::make_pair(d, st);
+  ScratchCache &c = scratch_cache();
+  {
+    std::lock_guard<std::mutex> g(c.mu);
+    auto it = c.free_blocks.find(key);
+    if (it != c.free_blocks.end()) {
+      auto b = it->second.lower_bound(n);
+      if (b != it->second.end() && b->first <= 2 * n) {
+        *p = b->second;
+        c.cached[key] -= b->first;
+        it->second.erase(b);
+        return hipSuccess;
+      }
+    }
+  }
+  void *q = nullptr;
+  e = hipMallocAsync(&q, n, st);
+  if (e == hipErrorOutOfMemory) {
+    (void)hipGetLastError();
+    std::lock_guard<std::mutex> g(c.mu);
+    for (auto &kv : c.free_blocks) {
+      for (auto &blk : kv.second) {
+        c.sizes.erase(blk.second);
+        (void)hipFreeAsync(blk.second, kv.first.second);
+      }
+      kv.second.clear();
+      c.cached[kv.first] = 0;
+    }
+  }
+  if (e == hipErrorOutOfMemory) e = hipMallocAsync(&q, n, st);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> g(c.mu);
+  c.sizes[q] = n;
+  *p = q;
+  return hipSuccess;
+}
+
+hipError_t rure_amd::scratch_free(void *p, hipStream_t st) {
+  if (!p) return hipSuccess;
+  int d = 0;
+  hipError_t e = hipGetDevice(&d);
+  if (e != hipSuccess) return e;
+  const auto key = std::make_pair(d, st);
+  ScratchCache &c = scratch_cache();
+  {
+    std::lock_guard<std::mutex> g(c.mu);
+    auto it = c.sizes.find(p);
+    if (it != c.sizes.end()) {
+      size_t &cached = c.cached[key];
+      if (cached + it->second <= kScratchCacheMax) {
+        cached += it->second;
+        c.free_blocks[key].emplace(it->second, p);
+        return hipSuccess;
+      }
+      c.sizes.erase(it);
+    }
+  }
+  return hipFreeAsync(p, st);
+}
+
+namespace {
+
 int device_cus(int dev) {
   keep_pool(dev);
   hipDeviceProp_t prop;
@@ -832,10 +923,10 @@ hipError_t run_pike(int mode, bool fallback, const BatchDev &b, const DevTables 
   size_t wb = nfa_wave_bytes(t.n.nleaves);
   if (wb <= kNfaLdsMax) return launch_pike(mode, fallback, b, t.n, out, nullptr, st, grid);
   void *scratch = nullptr;
-  hipError_t e = hipMallocAsync(&scratch, wb * (size_t)grid, st);
+  hipError_t e = scratch_malloc(&scratch, wb * (size_t)grid, st);
   if (e != hipSuccess) return e;
   e = launch_pike(mode, fallback, b, t.n, out, scratch, st, grid);
-  hipError_t e2 = hipFreeAsync(scratch, st);
+  hipError_t e2 = scratch_free(scratch, st);
   return e != hipSuccess ? e : e2;
 }
 
@@ -1158,12 +1249,12 @@ hipError_t run_regex(int mode, const BatchDev &b, const DevTables &t, void *out,
   if (!t.quit_possible) return run_dfa_step(mode, b, t, out, st, dfa_grid, nullptr);
   // the DFA kernels flag a quit; the Pike VM fallback returns at once without
   BatchDev bq = b;
-  hipError_t e = hipMallocAsync((void **)&bq.quit_flag, 4, st);
+  hipError_t e = scratch_malloc((void **)&bq.quit_flag, 4, st);
   if (e == hipSuccess) e = hipMemsetAsync(bq.quit_flag, 0, 4, st);
   if (e == hipSuccess) e = run_dfa_step(mode, bq, t, out, st, dfa_grid, nullptr);
   if (e == hipSuccess) e = run_pike(mode, true, bq, t, out, st);
   if (bq.quit_flag) {
-    hipError_t e2 = hipFreeAsync(bq.quit_flag, st);
+    hipError_t e2 = scratch_free(bq.quit_flag, st);
     if (e == hipSuccess) e = e2;
   }
   return e;
@@ -1182,8 +1273,8 @@ bool adapt_cores(rure_set *rs, DevTables *t, const BatchDev &b, hipStream_t st, 
   unsigned int *visits = nullptr;
   uint16_t *mid = nullptr;
   const size_t nm = cs.masks.size() + 1;
-  if (!hip_ok(hipMallocAsync((void **)&visits, (cs.ncores + nm) * 4, st), err)) return false;
-  if (!hip_ok(hipMallocAsync((void **)&mid, cs.mid.size() * 2, st), err)) return false;
+  if (!hip_ok(scratch_malloc((void **)&visits, (cs.ncores + nm) * 4, st), err)) return false;
+  if (!hip_ok(scratch_malloc((void **)&mid, cs.mid.size() * 2, st), err)) return false;
   std::vector<unsigned int> h(cs.ncores + nm);
   SetCoreDev pc = t->c;
   pc.mid = mid;
@@ -1191,7 +1282,7 @@ bool adapt_cores(rure_set *rs, DevTables *t, const BatchDev &b, hipStream_t st, 
             hip_ok(hipMemcpyAsync(mid, cs.mid.data(), cs.mid.size() * 2, hipMemcpyHostToDevice, st), err) &&
             hip_ok(launch_core_profile(b, pc, sample, visits, visits + cs.ncores, st, t->cus), err) &&
             hip_ok(hipMemcpyAsync(h.data(), visits, h.size() * 4, hipMemcpyDeviceToHost, st), err) &&
-            hip_ok(hipFreeAsync(visits, st), err) && hip_ok(hipFreeAsync(mid, st), err) &&
+            hip_ok(scratch_free(visits, st), err) && hip_ok(scratch_free(mid, st), err) &&
             hip_ok(hipStreamSynchronize(st), err);
   if (!ok) return false;
   std::vector<uint64_t> w(cs.ncores, 0);
@@ -1233,13 +1324,13 @@ hipError_t run_set(const BatchDev &b, const DevTables &t, uint64_t *out, hipStre
   if (!t.quit_possible)
     return t.use_cores ? launch_set_cores(b, t.c, out, st, t.cus) : launch_dfa_set(b, t.s, out, st, dfa_grid);
   BatchDev bq = b;  // quit flag: see run_regex
-  hipError_t e = hipMallocAsync((void **)&bq.quit_flag, 4, st);
+  hipError_t e = scratch_malloc((void **)&bq.quit_flag, 4, st);
   if (e == hipSuccess) e = hipMemsetAsync(bq.quit_flag, 0, 4, st);
   if (e == hipSuccess)
     e = t.use_cores ? launch_set_cores(bq, t.c, out, st, t.cus) : launch_dfa_set(bq, t.s, out, st, dfa_grid);
   if (e == hipSuccess) e = run_pike(MODE_SET, true, bq, t, out, st);
   if (bq.quit_flag) {
-    hipError_t e2 = hipFreeAsync(bq.quit_flag, st);
+    hipError_t e2 = scratch_free(bq.quit_flag, st);
     if (e == hipSuccess) e = e2;
   }
   return e;
@@ -1258,7 +1349,7 @@ hipError_t run_captures(const BatchDev &b, const DevTables &t, uint64_t *slots, 
   hipError_t e = hipSuccess;
   uint64_t *found = nullptr;
   if (!t.n.anchored) {
-    if ((e = hipMallocAsync((void **)&found, b.count * 16, st)) != hipSuccess) return e;
+    if ((e = scratch_malloc((void **)&found, b.count * 16, st)) != hipSuccess) return e;
     e = t.has_dfa ? run_dfa_step(MODE_FIND, b, t, found, st, dfa_grid, nullptr)
                   : run_pike(MODE_FIND, false, b, t, found, st);
   }
@@ -1269,10 +1360,10 @@ hipError_t run_captures(const BatchDev &b, const DevTables &t, uint64_t *slots, 
   if (!in_lds) g = std::min<size_t>(g, (256u << 20) / wb);  // bound the scratch (wide programs: MiBs per wave)
   const int grid = (int)std::max<size_t>(1, g);
   void *scratch = nullptr;
-  if (e == hipSuccess && !in_lds) e = hipMallocAsync(&scratch, wb * (size_t)grid, st);
+  if (e == hipSuccess && !in_lds) e = scratch_malloc(&scratch, wb * (size_t)grid, st);
   if (e == hipSuccess) e = launch_captures(b, t.n, found, slots, ns, scratch, st, grid);
-  if (scratch) { hipError_t e2 = hipFreeAsync(scratch, st); if (e == hipSuccess) e = e2; }
-  if (found) { hipError_t e2 = hipFreeAsync(found, st); if (e == hipSuccess) e = e2; }
+  if (scratch) { hipError_t e2 = scratch_free(scratch, st); if (e == hipSuccess) e = e2; }
+  if (found) { hipError_t e2 = scratch_free(found, st); if (e == hipSuccess) e = e2; }
   return e;
 }
 
@@ -1531,10 +1622,10 @@ bool captures_call(rure *re, const uint8_t *hay, size_t len, size_t start, uint6
   if (len && !hip_ok(hipMemcpyAsync(re->stage.hay, hay, len, hipMemcpyHostToDevice, st), &err)) die(err);
   BatchDev b{re->stage.hay, nullptr, len, len, 1, start};
   uint64_t *dev = re->stage.res;
-  if (ns > 64 && !hip_ok(hipMallocAsync((void **)&dev, (size_t)ns * 8, st), &err)) die(err);
+  if (ns > 64 && !hip_ok(scratch_malloc((void **)&dev, (size_t)ns * 8, st), &err)) die(err);
   if (!hip_ok(run_captures(b, *t, dev, ns, st, 1), &err)) die(err);
   if (!hip_ok(hipMemcpyAsync(slots, dev, (size_t)ns * 8, hipMemcpyDeviceToHost, st), &err)) die(err);
-  if (dev != re->stage.res && !hip_ok(hipFreeAsync(dev, st), &err)) die(err);
+  if (dev != re->stage.res && !hip_ok(scratch_free(dev, st), &err)) die(err);
   if (!hip_ok(hipStreamSynchronize(st), &err)) die(err);
   if (slots[0] == kQuit || slots[1] == kQuit) die("internal error: unresolved DFA quit");
   return slots[0] != ~0ull && slots[1] != ~0ull;
@@ -1822,14 +1913,14 @@ int set_batch_group(rure_set *g, const rure_amd_batch *batch, const BatchDev &b,
                     size_t w, hipStream_t st) {
   void *tmp = nullptr;
   const bool single = g->single != nullptr;
-  if (hipMallocAsync(&tmp, b.count * (single ? 1 : 8), st) != hipSuccess) return RURE_AMD_ERR_HIP;
+  if (scratch_malloc(&tmp, b.count * (single ? 1 : 8), st) != hipSuccess) return RURE_AMD_ERR_HIP;
   int rc = single ? rure_amd_is_match_batch(g->single, batch, (uint8_t *)tmp, st)
                   : set_batch_word(g, b, (uint64_t *)tmp, st);
   if (rc == RURE_AMD_OK &&
       launch_mask_column(single ? (const uint8_t *)tmp : nullptr, single ? nullptr : (const uint64_t *)tmp, b.count,
                          mask, words, w, st) != hipSuccess)
     rc = RURE_AMD_ERR_HIP;
-  if (hipFreeAsync(tmp, st) != hipSuccess && rc == RURE_AMD_OK) rc = RURE_AMD_ERR_HIP;
+  if (scratch_free(tmp, st) != hipSuccess && rc == RURE_AMD_OK) rc = RURE_AMD_ERR_HIP;
   return rc;
 }
 
@@ -1872,11 +1963,11 @@ hipError_t run_find_iter(rure *re, DevTables *t, const BatchDev &b, const IterOu
   // forward scan's); from 0 the chunked path below answers the same.
   if (!sp && t->anchored_rev && b.start > 0 && b.count) {
     uint64_t *found = nullptr;
-    hipError_t e = hipMallocAsync((void **)&found, b.count * 16, st);
+    hipError_t e = scratch_malloc((void **)&found, b.count * 16, st);
     if (e != hipSuccess) return e;
     e = run_regex(MODE_FIND, b, *t, found, st, grid_for(b.count, t->r.lds_bytes, t->cus));
     if (e == hipSuccess) e = launch_find_to_iter(found, b.count, o.counts, o.matches, o.cap, o.total, st);
-    hipError_t e2 = hipFreeAsync(found, st);
+    hipError_t e2 = scratch_free(found, st);
     return e != hipSuccess ? e : e2;
   }
   // Chunked speculative iteration needs a DFA that cannot quit and a pattern
@@ -1910,10 +2001,10 @@ struct IterBufs {
   uint64_t nm = 0;
   hipStream_t st = nullptr;
   ~IterBufs() {
-    if (counts) (void)hipFreeAsync(counts, st);
-    if (moff) (void)hipFreeAsync(moff, st);
-    if (m) (void)hipFreeAsync(m, st);
-    if (total) (void)hipFreeAsync(total, st);
+    if (counts) (void)scratch_free(counts, st);
+    if (moff) (void)scratch_free(moff, st);
+    if (m) (void)scratch_free(m, st);
+    if (total) (void)scratch_free(total, st);
   }
 };
 
@@ -1921,14 +2012,14 @@ hipError_t iter_to_device(rure *re, DevTables *t, const BatchDev &b, hipStream_t
   ib->st = st;
   hipError_t e;
   const size_t n = b.count;
-  if ((e = hipMallocAsync((void **)&ib->counts, (n + 1) * 8, st)) != hipSuccess) return e;
-  if ((e = hipMallocAsync((void **)&ib->moff, (n + 1) * 8, st)) != hipSuccess) return e;
-  if ((e = hipMallocAsync((void **)&ib->total, 8, st)) != hipSuccess) return e;
+  if ((e = scratch_malloc((void **)&ib->counts, (n + 1) * 8, st)) != hipSuccess) return e;
+  if ((e = scratch_malloc((void **)&ib->moff, (n + 1) * 8, st)) != hipSuccess) return e;
+  if ((e = scratch_malloc((void **)&ib->total, 8, st)) != hipSuccess) return e;
   if ((e = hipMemsetAsync(ib->counts, 0, (n + 1) * 8, st)) != hipSuccess) return e;
   const uint64_t bytes = b.offs ? 0 : (uint64_t)b.count * b.length;
   uint64_t cap = std::max<uint64_t>(1024, bytes / 64 + 2 * n);
   for (int pass = 0; pass < 2; ++pass) {
-    if ((e = hipMallocAsync((void **)&ib->m, cap * 16, st)) != hipSuccess) return e;
+    if ((e = scratch_malloc((void **)&ib->m, cap * 16, st)) != hipSuccess) return e;
     IterOut o{ib->counts, ib->m, cap, ib->total};
     if ((e = run_find_iter(re, t, b, o, st, err)) != hipSuccess) return e;
     uint64_t tot = 0;
@@ -1936,7 +2027,7 @@ hipError_t iter_to_device(rure *re, DevTables *t, const BatchDev &b, hipStream_t
     if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
     ib->nm = tot;
     if (tot <= cap) break;
-    (void)hipFreeAsync(ib->m, st);
+    (void)scratch_free(ib->m, st);
     ib->m = nullptr;
     cap = tot;
   }
@@ -2086,9 +2177,9 @@ int rure_amd_replace_batch(rure *re, const rure_amd_batch *batch, const uint8_t 
   uint8_t *drep = nullptr;
   const uint64_t lim = limit == 0 ? ~0ull : (uint64_t)limit;  // replacen: 0 = all
   hipError_t e = iter_to_device(re, t, b, st, &ib, &err);
-  if (e == hipSuccess) e = hipMallocAsync((void **)&shift, std::max<uint64_t>(ib.nm, 1) * 8, st);
-  if (e == hipSuccess) e = hipMallocAsync((void **)&olen, (b.count + 1) * 8, st);
-  if (e == hipSuccess) e = hipMallocAsync((void **)&drep, std::max<size_t>(rep_len, 1), st);
+  if (e == hipSuccess) e = scratch_malloc((void **)&shift, std::max<uint64_t>(ib.nm, 1) * 8, st);
+  if (e == hipSuccess) e = scratch_malloc((void **)&olen, (b.count + 1) * 8, st);
+  if (e == hipSuccess) e = scratch_malloc((void **)&drep, std::max<size_t>(rep_len, 1), st);
   if (e == hipSuccess && rep_len) e = hipMemcpyAsync(drep, rep, rep_len, hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = hipMemsetAsync(olen + b.count, 0, 8, st);
   if (e == hipSuccess)
@@ -2100,9 +2191,9 @@ int rure_amd_replace_batch(rure *re, const rure_amd_batch *batch, const uint8_t 
     e = launch_replace_copy(b, out_offsets, ib.counts, ib.moff, ib.m, shift, lim, drep, rep_len, out, out_capacity,
                             hint, st, t->cus);
   }
-  if (shift) (void)hipFreeAsync(shift, st);
-  if (olen) (void)hipFreeAsync(olen, st);
-  if (drep) (void)hipFreeAsync(drep, st);
+  if (shift) (void)scratch_free(shift, st);
+  if (olen) (void)scratch_free(olen, st);
+  if (drep) (void)scratch_free(drep, st);
   return e == hipSuccess ? RURE_AMD_OK : RURE_AMD_ERR_HIP;
 }
 
@@ -2120,16 +2211,16 @@ int rure_amd_split_batch(rure *re, const rure_amd_batch *batch, size_t limit, ui
   IterBufs ib;
   uint64_t *fields = nullptr, *foff = nullptr;
   hipError_t e = iter_to_device(re, t, b, st, &ib, &err);
-  if (e == hipSuccess) e = hipMallocAsync((void **)&fields, (b.count + 1) * 8, st);
-  if (e == hipSuccess) e = hipMallocAsync((void **)&foff, (b.count + 1) * 8, st);
+  if (e == hipSuccess) e = scratch_malloc((void **)&fields, (b.count + 1) * 8, st);
+  if (e == hipSuccess) e = scratch_malloc((void **)&foff, (b.count + 1) * 8, st);
   if (e == hipSuccess) e = hipMemsetAsync(fields + b.count, 0, 8, st);
   if (e == hipSuccess)
     e = launch_split(b, ib.counts, ib.moff, ib.m, (uint64_t)limit, fields, foff, (uint64_t *)pieces, capacity, ib.nm,
                      st, t->cus);
   if (e == hipSuccess) e = hipMemcpyAsync(counts, fields, b.count * 8, hipMemcpyDeviceToDevice, st);
   if (e == hipSuccess) e = hipMemcpyAsync(total, foff + b.count, 8, hipMemcpyDeviceToDevice, st);
-  if (fields) (void)hipFreeAsync(fields, st);
-  if (foff) (void)hipFreeAsync(foff, st);
+  if (fields) (void)scratch_free(fields, st);
+  if (foff) (void)scratch_free(foff, st);
   return e == hipSuccess ? RURE_AMD_OK : RURE_AMD_ERR_HIP;
 }
 
