@@ -337,7 +337,9 @@ int rure_amd_set_uses_dfa(rure_set *re);
  * find / is_match / shortest_match launch of this process used — 0 = the
  * per-lane streaming kernel, 1 / 2 / 4 = the coalesced-tile kernel with that
  * many bytes per dependent table lookup, -2 = the reverse DFA from the end
- * (DfaAnchoredReverse); -1 before the first launch. */
+ * (DfaAnchoredReverse), -3 = the literal engine (MatchType::Literal), -4 =
+ * the chunked cut-bounded scan (long haystacks, small batches split into
+ * units); -1 before the first launch. */
 int rure_amd_last_fwd_path(void);
 
 #ifdef __cplusplus

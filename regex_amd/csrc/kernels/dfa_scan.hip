@@ -94,6 +94,7 @@ __global__ __launch_bounds__(256) void dfa_fwd_kernel(BatchDev bt, FwdDfaDev f, 
 
 static std::atomic<int> g_last_fwd_path{-1};
 int last_fwd_path() { return g_last_fwd_path.load(); }
+void note_fwd_path(int path) { g_last_fwd_path.store(path); }
 
 // ------------------------------------------------------- literal engine
 // MatchType::Literal for find / is_match batches (exec.rs:601-625 find_literals,

@@ -232,8 +232,9 @@ hipError_t launch_lit_find(int mode, const BatchDev &b, const FwdDfaDev &f, void
 // assert the instantiation the bench times): 0 = dfa_fwd_kernel (per-lane
 // streaming), 1 / 2 / 4 = dfa_fwd_tile_kernel with that many bytes per
 // dependent LDS lookup, -2 = the anchored reverse scan, -3 = the literal
-// engine.
+// engine, -4 = the chunked long scan (launch_long_scan).
 int last_fwd_path();
+void note_fwd_path(int path);
 // Multi-GPU gather (gather_scan.hip): records (3 u64: base + haystack, start,
 // end) of the haystacks whose find result holds a match, first `cap`; *count.
 hipError_t launch_compact_matches(const uint64_t *found, uint64_t n, uint64_t base, uint64_t *rec, uint64_t cap,

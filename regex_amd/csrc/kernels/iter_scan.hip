@@ -1781,6 +1781,7 @@ hipError_t long_scan_m(const BatchDev &b, const FwdDfaDev &f, const RevDfaDev &r
 
 hipError_t launch_long_scan(int mode, const BatchDev &b, const FwdDfaDev &f, const RevDfaDev &r, uint64_t chunk,
                             void *out, hipStream_t st, int cus) {
+  note_fwd_path(-4);
   switch (mode) {
     case MODE_FIND: return long_scan_m<MODE_FIND>(b, f, r, chunk, out, st, cus);
     case MODE_ISMATCH: return long_scan_m<MODE_ISMATCH>(b, f, r, chunk, out, st, cus);

@@ -1214,7 +1214,22 @@ uint64_t odd_lines(uint64_t bytes) {
 bool long_batch(const BatchDev &b, const DevTables &t, uint64_t *chunk) {
   if (b.offs || !t.has_dfa || t.quit_possible || b.count == 0) return false;
   const uint64_t span = b.length > b.start ? b.length - b.start : 0;
-  if (span < (256u << 10) || b.count >= (uint64_t)t.cus * 128) return false;
+  if (span < (256u << 10) || b.count >= (uint64_t)t.cus * 128) {
+    // Small batches of medium haystacks (C1: 1024 x 1 KiB): one lane per
+    // haystack runs count / 256 workgroups on a 256-CU chip, each lane a
+    // dependent chain over its whole haystack; units of >= 128 B spread the
+    // searches over about one wave per CU.  End-anchored regexes keep the
+    // reverse scan (it reads O(match) bytes); single calls and batches of
+    // fewer than 64 haystacks keep one lane each.  RURE_AMD_SPLIT=0 turns it off.
+    const char *sv = getenv("RURE_AMD_SPLIT");
+    if ((sv && sv[0] == '0') || t.anchored_rev || span < 512 || b.count < 64 || b.count > (uint64_t)t.cus * 16)
+      return false;
+    const uint64_t per_h = ((uint64_t)t.cus * 64 + b.count - 1) / b.count;
+    const uint64_t c = odd_lines(std::max<uint64_t>(128, (span + per_h - 1) / per_h));
+    if (c >= span) return false;
+    *chunk = c;
+    return true;
+  }
   // 16 waves per CU: per-lane streams need latency hiding (RURE_AMD_LONG_LANES
   // per CU overrides, tuning)
   uint64_t per_cu = 1024;

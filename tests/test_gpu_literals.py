@@ -234,7 +234,7 @@ def test_literal_find_default_dispatch(cuda, monkeypatch, nwords):
         rng = np.random.default_rng(11)
         pat = "|".join(rng.choice(words, nwords, replace=False))
     re = R.Regex(pat)
-    L = 2000
+    L = 256  # below the small-batch split (rure_amd.cpp long_batch: >= 512 B)
     n = len(text) // L
     buf = text[: n * L]
     d = dev(buf, cuda)
@@ -251,7 +251,7 @@ def test_literal_find_default_dispatch(cuda, monkeypatch, nwords):
     assert np.array_equal(gm, re.is_match_batch(d, stride=L, length=L, count=n).cpu().numpy())
     exp, _ = R_oracle_find(re, buf, L, n)
     assert np.array_equal(got.astype(np.uint64), exp)
-    assert (got[:, 0] >= 0).sum() > n // 4
+    assert (got[:, 0] >= 0).sum() > n // 8
 
 
 def R_oracle_find(re, buf, L, n):
