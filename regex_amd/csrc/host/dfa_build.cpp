@@ -32,7 +32,7 @@ struct SparseSet {
 class Builder {
  public:
   Builder(const Program &p, const DfaBuildLimits &lim)
-      : p_(p), lim_(lim), qa_(p.insts.size() + 1), qb_(p.insts.size() + 1) {
+      : p_(p), lim_(lim), qa_(p.insts.size() + 1), qb_(p.insts.size() + 1), qc_(p.insts.size() + 1) {
     is_set_ = p.matches.size() > 1;
     strip_ = lim.strip && p.dotstar_end > 0;
     cont_ = p.is_reverse || is_set_;  // dfa.rs:1557-1559
@@ -41,6 +41,7 @@ class Builder {
       if (i.op == OP_EMPTY && i.look >= LOOK_WORD_BOUNDARY) word_matters_ = true;
     quit_ = p.has_unicode_word_boundary;
     stack_.reserve(p.insts.size() + 1);
+    stamp_.assign(p.insts.size() + 1, 0);
   }
 
   bool build(DenseDfa *out, std::string *err) {
@@ -117,8 +118,14 @@ class Builder {
  private:
   const Program &p_;
   DfaBuildLimits lim_;
-  SparseSet qa_, qb_;
+  SparseSet qa_, qb_, qc_;
   std::vector<uint32_t> stack_;
+  // step_row's cache across states: (flags, slots, target ips) -> raw state
+  std::unordered_map<std::string, uint32_t> step_cache_;
+  std::string tkey_;
+  std::vector<std::string> sig_;   // step_row scratch: per class, the accepting threads' targets
+  std::vector<uint32_t> stamp_;
+  uint32_t stamp_gen_ = 0;
   bool is_set_, cont_, word_matters_, quit_, strip_ = false;
   std::vector<uint32_t> strip_raw_;  // raw state (from 2) -> stripped raw state
   std::vector<std::string> keys_;
@@ -172,8 +179,12 @@ class Builder {
       closure_done_[nl].assign(p_.insts.size(), 0);
       closure_[nl].resize(p_.insts.size());
     }
+    if (q.contains(ip)) return;  // its whole closure is in q already (above)
     if (!closure_done_[nl][ip]) {
-      SparseSet tmp(p_.insts.size() + 1);
+      // one scratch set for every closure (clear() is O(1)): a set sized for
+      // the program per closure cost a program-sized allocation each time
+      SparseSet &tmp = qc_;
+      tmp.clear();
       EmptyFlags ef;
       ef.start_line = nl != 0;
       follow(ip, tmp, ef);
@@ -186,8 +197,10 @@ class Builder {
 
   // dfa.rs:1196-1244 plus interning; returns raw id (0 = DEAD).  `now`
   // (sets only): Match slots reached by the step that produced this state.
+  std::vector<uint32_t> kips_;  // intern's scratch: the key's instruction pointers
+  std::string kbuf_;            // intern's scratch key
   uint32_t intern(const SparseSet &q, uint8_t sflags, uint64_t now = 0) {
-    std::string key(1, '\0');
+    kips_.clear();
     for (size_t k = 0; k < q.n; ++k) {
       uint32_t ip = q.dense[k];
       const Inst &in = p_.insts[ip];
@@ -198,21 +211,24 @@ class Builder {
         case OP_EMPTY: sflags |= SF_EMPTY; push = true; break;
         case OP_MATCH: push = true; stop = !cont_; break;
       }
-      if (push) key.append((const char *)&ip, 4);
+      if (push) kips_.push_back(ip);
       if (stop) break;
     }
+    if (kips_.empty() && !now && !(sflags & SF_MATCH)) return 0;
+    std::string &key = kbuf_;
+    key.resize(1 + 4 * kips_.size() + (now ? 12 : 0));
+    key[0] = (char)sflags;
+    if (!kips_.empty()) memcpy(&key[1], kips_.data(), 4 * kips_.size());
     if (now) {
       const uint32_t sep = 0xFFFFFFFFu;
-      key.append((const char *)&sep, 4);
-      key.append((const char *)&now, 8);
+      memcpy(&key[1 + 4 * kips_.size()], &sep, 4);
+      memcpy(&key[5 + 4 * kips_.size()], &now, 8);
     }
-    if (key.size() == 1 && !(sflags & SF_MATCH)) return 0;
-    key[0] = (char)sflags;
     auto it = ids_.find(key);
     if (it != ids_.end()) return it->second;
     uint32_t id = (uint32_t)keys_.size();
     ids_.emplace(key, id);
-    keys_.push_back(std::move(key));
+    keys_.push_back(key);
     return id;
   }
 
@@ -311,8 +327,12 @@ class Builder {
   // of UTF-8 range instructions split the 100+ classes into few groups).
   void step_row(const std::string &key, int ncls, const uint8_t *rep, uint32_t *row) {
     const uint8_t flags = (uint8_t)key[0];
-    std::unordered_map<std::string, uint32_t> memo;
-    std::vector<std::string> sig(ncls);
+    std::unordered_map<std::string, uint32_t> memo[4];
+    std::vector<std::string> &sig = sig_;
+    sig.resize(ncls);
+    uint8_t mflag = 0;
+    uint64_t m_now = 0;
+    bool scanned = false;
     for (int combo = 0; combo < 4; ++combo) {
       const bool nl = combo & 1, w = (combo >> 1) & 1;
       bool any = false;
@@ -320,33 +340,80 @@ class Builder {
         any = (rep[c] == '\n') == nl && is_word_byte(rep[c]) == w;
       if (!any) continue;
       // the thread list the byte instructions are read from (exec's first
-      // follow when the state holds empty-width instructions)
-      SparseSet &q = qa_;
-      load(key, q);
-      if (flags & SF_EMPTY) {
-        EmptyFlags ef;
-        if (nl) ef.end_line = true;
-        if (((flags & SF_WORD) != 0) == w) ef.nwb = true; else ef.wb = true;
-        qb_.clear();
-        for (size_t k = 0; k < q.n; ++k) follow(q.dense[k], qb_, ef);
-        std::swap(qa_, qb_);
+      // follow when the state holds empty-width instructions; without them
+      // it is the state's own list for every combination)
+      if (!scanned || (flags & SF_EMPTY)) {
+        SparseSet &q = qa_;
+        load(key, q);
+        if (flags & SF_EMPTY) {
+          EmptyFlags ef;
+          if (nl) ef.end_line = true;
+          if (((flags & SF_WORD) != 0) == w) ef.nwb = true; else ef.wb = true;
+          qb_.clear();
+          for (size_t k = 0; k < q.n; ++k) follow(q.dense[k], qb_, ef);
+          std::swap(qa_, qb_);
+        }
+        SparseSet &qq = qa_;
+        // exec_byte's second half (dfa.rs:966-1003) read off qq once: the
+        // match flag and set slots of the threads before the first Match
+        // (all of them for sets / reverse), and per class the targets of the
+        // Byte threads that accept it, in priority order
+        mflag = 0;
+        m_now = 0;
+        for (int c = 0; c < ncls; ++c) sig[c].clear();
+        for (size_t k = 0; k < qq.n; ++k) {
+          const Inst &in = p_.insts[qq.dense[k]];
+          if (in.op == OP_MATCH) {
+            mflag = SF_MATCH;
+            if (!cont_) break;
+            if (is_set_ && in.x < 64) m_now |= 1ull << in.x;
+            continue;
+          }
+          if (in.op != OP_BYTES) continue;
+          const int c0 = p_.byte_classes[in.lo], c1 = p_.byte_classes[in.hi];
+          const uint32_t x = in.x;
+          for (int c = c0; c <= c1; ++c) sig[c].append((const char *)&x, 4);
+        }
+        scanned = true;
       }
-      SparseSet &qq = qa_;
-      for (int c = 0; c < ncls; ++c) sig[c].clear();
-      for (size_t k = 0; k < qq.n; ++k) {
-        const Inst &in = p_.insts[qq.dense[k]];
-        if (in.op == OP_MATCH && !cont_) break;
-        if (in.op != OP_BYTES) continue;
-        const int c0 = p_.byte_classes[in.lo], c1 = p_.byte_classes[in.hi];
-        for (int c = c0; c <= c1; ++c) sig[c].append((const char *)&k, 4);
-      }
+      const uint8_t sflags = (uint8_t)(mflag | (w && word_matters_ ? SF_WORD : 0));
+      const uint64_t now = is_set_ ? m_now : 0;
       for (int c = 0; c < ncls; ++c) {
         if ((rep[c] == '\n') != nl || is_word_byte(rep[c]) != w) continue;
-        sig[c].push_back((char)combo);
-        auto it = memo.find(sig[c]);
-        if (it != memo.end()) { row[c] = it->second; continue; }
-        const uint32_t t = step(key, rep[c]);
-        memo.emplace(sig[c], t);
+        auto it = memo[combo].find(sig[c]);
+        if (it != memo[combo].end()) { row[c] = it->second; continue; }
+        // The step on this class is the union, in order, of the closures
+        // (under start_line = the byte is '\n') of the accepting threads'
+        // targets, so it is a function of (that target list, the flags, the
+        // set slots): cached across states (a repeated target adds nothing).
+        std::string &tk = tkey_;
+        tk.assign(1, (char)(sflags | (nl ? 0x80 : 0)));
+        tk.append((const char *)&now, 8);
+        ++stamp_gen_;
+        const size_t nk = sig[c].size() / 4;
+        for (size_t j = 0; j < nk; ++j) {
+          uint32_t x;
+          memcpy(&x, sig[c].data() + 4 * j, 4);
+          if (stamp_[x] == stamp_gen_) continue;
+          stamp_[x] = stamp_gen_;
+          tk.append((const char *)&x, 4);
+        }
+        uint32_t t;
+        auto st = step_cache_.find(tk);
+        if (st != step_cache_.end()) {
+          t = st->second;
+        } else {
+          SparseSet &nx = qb_;
+          nx.clear();
+          for (size_t j = 9; j < tk.size(); j += 4) {
+            uint32_t x;
+            memcpy(&x, tk.data() + j, 4);
+            follow_cached(x, nx, nl ? 1 : 0);
+          }
+          t = intern(nx, sflags, now);
+          step_cache_.emplace(tk, t);
+        }
+        memo[combo].emplace(sig[c], t);
         row[c] = t;
       }
     }

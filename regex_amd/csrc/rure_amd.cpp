@@ -21,6 +21,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "host/dfa_build.hpp"
@@ -655,9 +656,14 @@ bool build_regex(rure *re) {
   std::string nerr;
   re->nfa_ok = build_nfa_tables(re->nfa, &re->nt, &nerr);
   DfaBuildLimits lim;
-  std::string err;
-  if (!build_dense_dfa(re->fwd, lim, &re->dfwd, &err) || !build_dense_dfa(re->rev, lim, &re->drev, &err) ||
-      !pack_forward(re->dfwd, &re->pf, &err) || !pack_forward(re->drev, &re->pr, &err, true)) {
+  std::string err, rerr;
+  // the forward and reverse automata are independent: build them on two threads
+  bool rev_ok = false;
+  std::thread rt([&] { rev_ok = build_dense_dfa(re->rev, lim, &re->drev, &rerr); });
+  const bool fwd_ok = build_dense_dfa(re->fwd, lim, &re->dfwd, &err);
+  rt.join();
+  if (fwd_ok && !rev_ok) err = rerr;
+  if (!fwd_ok || !rev_ok || !pack_forward(re->dfwd, &re->pf, &err) || !pack_forward(re->drev, &re->pr, &err, true)) {
     re->dfa_err = err.empty() ? "reverse DFA too large" : err;
     re->dfa_ok = false;
     if (!re->nfa_ok) re->dfa_err += "; " + nerr;
