@@ -540,101 +540,161 @@ def run_c3(ctx):
         torch.cuda.synchronize()
     strip_ms = ctx.kernel_ms(strip_pass)
     var_ms = ctx.kernel_ms(variant_pass)
-    scanned = N + len(variants) * M
+    # the dominant kernel of each phase timed live (HIP events the library
+    # records around the speculative kernel on the launch stream)
+    lex_ms, lex_n = kernel_timer_ms(strip_pass, ctx.args.steps)
+    spec_ms, spec_n = kernel_timer_ms(variant_pass, ctx.args.steps)
+    fused = not ctx.args.c3_separate
+    strip_bytes = (N + W - 1) // W
+    scanned = N + len(variants) * M   # regex-bytes: the stripped stream once per variant
+    var_bytes = v_hi - v_lo      # the rank's span of the stripped stream
     extra = {"variant_host_enqueue_ms": round(float(np.median(hts)) * 1e3, 3)}
     if ctx.rank == 0 and not ctx.args.no_cpu:
-        extra["cpu_baseline"] = cpu_baseline_c3(variants, seq, M, got, ctx.args)
-    my_bytes = sum(span_bounds(L, W, rk)[1] - span_bounds(L, W, rk)[0] for _, _, L, _ in passes)
+        extra["cpu_baseline"] = cpu_baseline_c3(strip, raw, variants, seq, M, got, ctx.args)
+    # bytes the step must move: the raw text read by the strip pass, the
+    # stripped stream read once by the fused variant pass (9 times when
+    # separate), and the match records written (16 B each)
+    var_matches = sum(got) // W
+    step_bytes = strip_bytes + var_bytes * (1 if fused else len(variants)) + 16 * (nsp_sharded // W + var_matches)
     config = {"workload": "C3: regex-dna x%d (%d B raw, %d B stripped): strip find_iter + 9 variant find_iter"
                           % (copies, N, M),
               "parallelism": "span%d (one logical stream cut into %d contiguous spans, exit exchange per step)"
                              % (W, W)}
+    # value: haystack bytes per second, each haystack (raw text, stripped
+    # stream) counted once; regex_bytes_GBps counts the stripped stream once
+    # per variant (the 9 find_iter the reference runs)
     return ctx.line("haystack GB/s scanned, batched bytes::Regex::find_iter (regex-dna)",
-                    scanned / sec / 1e9, "GB/s", sec * 1e3, "u8",
+                    (N + M) / sec / 1e9, "GB/s", sec * 1e3, "u8",
                     "examples/regexdna-input.txt replicated", config, scaling="strong",
-                    strip_pass_ms=round(strip_ms, 3), strip_GBps=round(N / W / strip_ms / 1e6, 1),
-                    variant_passes_ms=round(var_ms, 3),
-                    variant_GBps=round((my_bytes - (N + W - 1) // W) / var_ms / 1e6, 1),
+                    regex_bytes_GBps=round(scanned / sec / 1e9, 1),
+                    strip_pass_ms=round(strip_ms, 3), strip_GBps=round(strip_bytes / strip_ms / 1e6, 1),
+                    variant_phase_ms=round(var_ms, 3),
+                    variant_phase_GBps=round(var_bytes / var_ms / 1e6, 1),
                     strip_matches=nsp_sharded, variant_counts=got, known_answers_ok=ok,
                     variant_engine="separate passes" if ctx.args.c3_separate else "one fused pass",
-                    cut_recomputations=stats["recomputed"], roofline=roofline_c3(my_bytes - (N + W - 1) // W,
-                                                                                 var_ms, len(variants), config,
-                                                                                 fused=not ctx.args.c3_separate),
-                    roofline_strip=roofline_c3_strip((N + W - 1) // W, strip_ms, config),
-                    roofline_step={"bound": "hbm", "achieved": round(my_bytes / sec / 1e9, 1),
+                    cut_recomputations=stats["recomputed"],
+                    roofline=roofline_kernel(var_bytes, spec_ms, spec_n, config,
+                                             "iter_spec_sa_multi_tile" if fused else "iter_spec_sa_tile",
+                                             "variant speculative kernel (%s)" %
+                                             ("iter_spec_sa_multi_tile_kernel: one read of the stripped span "
+                                              "for all 9 variants" if fused else
+                                              "iter_spec_sa_tile_kernel, one launch per variant")),
+                    roofline_strip=roofline_kernel(strip_bytes, lex_ms, lex_n, config,
+                                                   "iter_spec_lex_tile",
+                                                   "strip speculative kernel (iter_spec_lex_tile_kernel: one read "
+                                                   "of the raw text)"),
+                    roofline_variant_phase={"bound": "hbm", "achieved": round(var_bytes / var_ms / 1e6, 1),
+                                            "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                            "frac": round(var_bytes / var_ms / 1e6 / HBM_PEAK_GBS, 4),
+                                            "ms": round(var_ms, 4), "alg_bytes": int(var_bytes),
+                                            "what": "whole variant phase (speculative kernel + each variant's "
+                                                    "fix/walk/emit/count kernels), HIP events"},
+                    roofline_step={"bound": "hbm", "achieved": round(step_bytes / sec / 1e9, 1),
                                    "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                   "frac": round(my_bytes / sec / 1e9 / HBM_PEAK_GBS, 4),
-                                   "ms": round(sec * 1e3, 4), "alg_bytes_per_step": int(my_bytes),
-                                   "what": "whole step: strip pass + 9 variant passes (+ exit exchange), "
-                                           "driver-visible time incl. launch gaps"},
+                                   "frac": round(step_bytes / sec / 1e9 / HBM_PEAK_GBS, 4),
+                                   "ms": round(sec * 1e3, 4), "alg_bytes_per_step": int(step_bytes),
+                                   "what": "whole step: raw text read once (strip), stripped stream read %s, "
+                                           "match records written; driver-visible time incl. launch gaps"
+                                           % ("once (fused variant pass)" if fused else "once per variant")},
                     **extra)
 
 
-def roofline_c3(var_bytes, var_ms, nvar, config, fused=True):
-    """Roofline of the variant phase (HIP events on the launch stream).
-    Fused (default): one Shift-And pass reads the stripped span once for all
-    variants (iter_spec_sa_multi_tile_kernel), then each variant's fix / emit
-    / count kernels: algorithmic bytes = the span, time = the whole phase.
-    Separate (--c3-separate): one pass per variant, figures per pass.
-    traffic = HBM bytes per launch of the spec kernel from the committed PMC
-    pass of this command."""
-    per = var_bytes / nvar
-    ms = var_ms if fused else var_ms / nvar
-    a = per / ms / 1e6
+def kernel_timer_ms(fn, steps):
+    """Average duration of the find_iter speculative kernel of fn() over
+    `steps` calls (rure_amd_kernel_timer: HIP events on the launch stream)."""
+    import ctypes
+    from regex_amd import _native as NN
+    NN.rure_amd_kernel_timer(1)
+    for _ in range(steps):
+        fn()
+    n = ctypes.c_uint64(0)
+    ms = NN.rure_amd_kernel_timer_read(ctypes.byref(n))
+    NN.rure_amd_kernel_timer(0)
+    return float(ms), int(n.value)
+
+
+def roofline_kernel(alg_bytes, ms, launches, config, kernel, what):
+    """Roofline of one kernel: algorithmic bytes per launch / its average
+    launch duration (live HIP events); traffic = HBM bytes per launch from the
+    committed PMC pass of this command (profiles/*_summary.json)."""
+    a = alg_bytes / ms / 1e6 if ms > 0 else 0.0
     r = {"bound": "hbm", "achieved": round(a, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
          "frac": round(a / HBM_PEAK_GBS, 4), "traffic": None, "kernel_ms": round(ms, 4),
-         "alg_bytes_per_launch": int(per),
-         "kernel": ("variant phase: one fused pass (iter_spec_sa_multi_tile_kernel) + per-variant "
-                    "fix/emit/count kernels" if fused else
-                    "variant find_iter pass (iter_spec_sa_tile_kernel + fix/emit/count kernels)")}
-    tr = profiled_traffic(config, per, kernel="iter_spec_sa_multi_tile" if fused else "iter_spec_sa_tile")
+         "launches_timed": launches, "alg_bytes_per_launch": int(alg_bytes), "kernel": what}
+    tr = profiled_traffic(config, alg_bytes, kernel=kernel)
     if tr is not None:
         r["traffic"] = tr["bytes"]
         r["traffic_source"] = tr["source"]
     return r
 
 
-def roofline_c3_strip(strip_bytes, strip_ms, config):
-    """The strip pass (lexer engine: iter_spec_lex_tile_kernel + its tail,
-    fix, emit and count kernels): algorithmic bytes = the raw text; traffic =
-    HBM bytes per launch of the lexer kernel from the committed PMC pass."""
-    a = strip_bytes / strip_ms / 1e6
-    r = {"bound": "hbm", "achieved": round(a, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-         "frac": round(a / HBM_PEAK_GBS, 4), "traffic": None, "kernel_ms": round(strip_ms, 4),
-         "alg_bytes_per_launch": int(strip_bytes),
-         "kernel": "strip find_iter pass (iter_spec_lex_tile_kernel + tail/fix/emit/count kernels)"}
-    tr = profiled_traffic(config, strip_bytes, kernel="iter_spec_lex_tile")
-    if tr is not None:
-        r["traffic"] = tr["bytes"]
-        r["traffic_source"] = tr["source"]
-    return r
-
-
-def cpu_baseline_c3(variants, seq, M, gpu_counts, args):
-    """Oracle find_iter (restated lazy DFA + re_trait.rs:197-221 iteration),
-    single-threaded like the reference's find_iter, over the first 16 MiB of
-    the stripped stream for each of the 9 variants; counts re-checked against
-    the GPU's find_iter of the same slice."""
+def cpu_baseline_c3(strip, raw, variants, seq, M, gpu_counts, args):
+    """The C3 step on the CPU the way the reference's shootout runs it
+    (examples/shootout-regex-dna-bytes.rs): the strip replace_all on one
+    thread (:21), then the 9 variant find_iter counts on one thread each
+    (:37-42), with the oracle (restated lazy DFA + re_trait.rs:197-221
+    iteration) as the engine.  Sample: the first `copies` whole copies of the
+    input (about 32 MiB raw), repeated for --cpu-seconds; its stripped output
+    and variant counts are checked against the GPU's."""
+    import threading
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle_py import OracleRegex
-    import regex_amd as R
-    S = min(M, 16 << 20)
-    piece = bytes(seq[:S].cpu().numpy())
+    copies = max(1, (32 << 20) // len(raw))
+    text = raw * copies
+    R_ = len(text)
+    o_strip = OracleRegex(strip)
     os_ = [OracleRegex(v) for v in variants]
-    t0 = time.perf_counter()
-    exp = [len(o.find_iter(piece)) for o in os_]
-    passes, elapsed = 1, time.perf_counter() - t0
-    while elapsed < args.cpu_seconds and passes < 64:
+
+    def strip_once(cap=None):
+        sp = o_strip.find_iter_array(text, cap=cap)
+        # replace_all(.., "") = the bytes outside the matches
+        a = np.frombuffer(text, dtype=np.uint8)
+        d = np.zeros(R_ + 1, dtype=np.int32)
+        np.add.at(d, sp[:, 0].astype(np.int64), 1)
+        np.add.at(d, sp[:, 1].astype(np.int64), -1)
+        keep = np.cumsum(d[:R_]) == 0
+        return sp.shape[0], a[keep].tobytes()
+
+    nstrip, stripped = strip_once()
+    S = len(stripped)
+    res = [None] * len(os_)
+
+    def var_thread(i, cap):
+        res[i] = os_[i].find_iter_array(stripped, cap=cap).shape[0]
+
+    def variants_once(caps):
+        th = [threading.Thread(target=var_thread, args=(i, caps[i])) for i in range(len(os_))]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        return list(res)
+
+    exp = variants_once([None] * len(os_))
+    caps = [c + 16 for c in exp]
+    t_strip = t_var = 0.0
+    passes = 0
+    while (t_strip + t_var) < args.cpu_seconds and passes < 64:
         t0 = time.perf_counter()
-        for o in os_:
-            o.find_iter(piece)
-        elapsed += time.perf_counter() - t0
+        strip_once(nstrip + 16)
+        t1 = time.perf_counter()
+        variants_once(caps)
+        t2 = time.perf_counter()
+        t_strip += t1 - t0
+        t_var += t2 - t1
         passes += 1
+    gpu_strip = bytes(seq[:S].cpu().numpy())
     got = [int(v.find_iter_batch(seq[:S + 16], stride=S, length=S, count=1)[0][0]) for v in variants]
-    return {"value": round(S * len(variants) * passes / elapsed / 1e9, 3), "unit": "GB/s", "cores": 1,
-            "kind": "port", "sample": "%d passes of the 9 variant find_iter over the first %d MiB of the stripped "
-                                      "stream" % (passes, S >> 20),
-            "parity_on_sample": exp == got}
+    sec = (t_strip + t_var) / passes
+    return {"value": round((R_ + S) / sec / 1e9, 3), "unit": "GB/s", "cores": len(os_),
+            "kind": "port",
+            "regex_bytes_GBps": round((R_ + len(os_) * S) / sec / 1e9, 3),
+            "strip_GBps_1thread": round(R_ * passes / t_strip / 1e9, 3),
+            "variants_GBps_9threads": round(len(os_) * S * passes / t_var / 1e9, 3),
+            "sample": "%d passes over %d copies of the input (%.1f MiB raw -> %.1f MiB stripped): strip "
+                      "replace_all on 1 thread, then the 9 variant find_iter on 9 threads (one per variant, "
+                      "shootout-regex-dna-bytes.rs:37-42)" % (passes, copies, R_ / 2**20, S / 2**20),
+            "parity_on_sample": bool(gpu_strip == stripped and exp == got)}
 
 
 # ------------------------------------------------------------------ C4

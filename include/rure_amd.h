@@ -229,6 +229,13 @@ int rure_amd_captures_batch(rure *re, const rure_amd_batch *batch, size_t *slots
 /* Number of capture groups including group 0 (= rure_captures_len). */
 size_t rure_amd_captures_len(rure *re);
 
+/* Returns the device scratch this library keeps cached for reuse (blocks
+ * of the stream-ordered allocator freed by earlier batched calls; at most
+ * max(256 MiB, 2 x the peak of live scratch) are kept) to the allocator.
+ * Also done when the last rure / rure_set is freed.  Safe at any time: each
+ * block is freed after the kernels that last used it. */
+void rure_amd_release_scratch(void);
+
 /* Diagnostics (host only, no GPU needed). */
 typedef struct rure_amd_dfa_info {
   int32_t ok;            /* 1 if the automaton was materialized */
@@ -341,6 +348,13 @@ int rure_amd_set_uses_dfa(rure_set *re);
  * the chunked cut-bounded scan (long haystacks, small batches split into
  * units); -1 before the first launch. */
 int rure_amd_last_fwd_path(void);
+/* Diagnostics (bench): rure_amd_kernel_timer(1) resets and starts timing the
+ * speculative kernel of every find_iter pass (the dominant kernel of a pass:
+ * iter_spec_*; HIP events on the launch stream), (0) stops;
+ * rure_amd_kernel_timer_read waits for the timed launches and returns their
+ * average duration in ms (*launches = how many; -1 on a HIP error). */
+int rure_amd_kernel_timer(int on);
+double rure_amd_kernel_timer_read(uint64_t *launches);
 
 #ifdef __cplusplus
 }

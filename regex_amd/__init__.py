@@ -15,9 +15,16 @@ import ctypes
 
 from . import _native as N
 
-__all__ = ["Regex", "RegexSet", "Error", "NoExpand", "NONE"]
+__all__ = ["Regex", "RegexSet", "Error", "NoExpand", "NONE", "release_scratch"]
 
 NONE = N.NONE
+
+
+def release_scratch():
+    """Returns the device scratch the library keeps cached between batched
+    calls to the allocator (rure_amd_release_scratch); also happens when the
+    last Regex / RegexSet is freed."""
+    N.rure_amd_release_scratch()
 
 
 class Error(Exception):
@@ -726,6 +733,13 @@ class RegexSet(object):
         if out is None:
             shape = (b.count,) if len(self) <= 64 else (b.count, w)
             out = torch.empty(shape, dtype=torch.int64, device=haystack.device)
+        elif (out.dtype != torch.int64 or not out.is_contiguous() or not out.is_cuda
+              or out.numel() < b.count * w):
+            # the kernels write count * words int64 words: anything smaller
+            # (e.g. an (n,) tensor for a set of more than 64 patterns) would
+            # be written out of bounds
+            raise ValueError("out must be a contiguous int64 CUDA tensor of at least %d x %d words"
+                             % (b.count, w))
         _check(N.rure_amd_set_matches_batch_words(self._set, ctypes.byref(b), ctypes.c_void_p(out.data_ptr()), w,
                                                   _stream_ptr(stream)), "matches_batch")
         return out

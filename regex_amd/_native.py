@@ -152,6 +152,9 @@ rure_amd_first_byte_export = _sig("rure_amd_first_byte_export", ctypes.c_int, VP
 rure_amd_lex_export = _sig("rure_amd_lex_export", ctypes.c_int64, VP, VP, c_size, VP)
 rure_amd_set_matches_batch_words = _sig("rure_amd_set_matches_batch_words", ctypes.c_int, VP,
                                         ctypes.POINTER(RureBatch), VP, c_size, VP)
+rure_amd_release_scratch = _sig("rure_amd_release_scratch", None)
+rure_amd_kernel_timer = _sig("rure_amd_kernel_timer", ctypes.c_int, ctypes.c_int)
+rure_amd_kernel_timer_read = _sig("rure_amd_kernel_timer_read", ctypes.c_double, VP)
 rure_amd_compact_matches = _sig("rure_amd_compact_matches", ctypes.c_int, VP, c_size, ctypes.c_uint64, VP, c_size,
                                 VP, VP)
 

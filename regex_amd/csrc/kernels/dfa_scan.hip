@@ -26,6 +26,8 @@
 #include <atomic>
 #include <algorithm>
 #include <cstdlib>
+#include <mutex>
+#include <vector>
 
 #include "dfa_device.hpp"
 
@@ -95,6 +97,66 @@ __global__ __launch_bounds__(256) void dfa_fwd_kernel(BatchDev bt, FwdDfaDev f, 
 static std::atomic<int> g_last_fwd_path{-1};
 int last_fwd_path() { return g_last_fwd_path.load(); }
 void note_fwd_path(int path) { g_last_fwd_path.store(path); }
+
+// Kernel timer (bench diagnostics, rure_amd_kernel_timer): while on, the
+// launches a caller brackets with ktimer_begin / ktimer_end (the find_iter
+// speculative kernels) get a HIP event pair on their own stream, so the
+// bench can report that kernel's average duration measured live.
+namespace {
+struct KTimer {
+  std::mutex mu;
+  bool on = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+  size_t used = 0;
+};
+KTimer &ktimer() {
+  static KTimer *t = new KTimer();
+  return *t;
+}
+}  // namespace
+
+void ktimer_begin(hipStream_t st) {
+  KTimer &t = ktimer();
+  std::lock_guard<std::mutex> g(t.mu);
+  if (!t.on) return;
+  if (t.used == t.ev.size()) {
+    std::pair<hipEvent_t, hipEvent_t> p{nullptr, nullptr};
+    if (hipEventCreate(&p.first) != hipSuccess || hipEventCreate(&p.second) != hipSuccess) return;
+    t.ev.push_back(p);
+  }
+  (void)hipEventRecord(t.ev[t.used].first, st);
+}
+
+void ktimer_end(hipStream_t st) {
+  KTimer &t = ktimer();
+  std::lock_guard<std::mutex> g(t.mu);
+  if (!t.on || t.used >= t.ev.size()) return;
+  (void)hipEventRecord(t.ev[t.used].second, st);
+  ++t.used;
+}
+
+int ktimer_set(int on) {
+  KTimer &t = ktimer();
+  std::lock_guard<std::mutex> g(t.mu);
+  t.on = on != 0;
+  t.used = 0;
+  return 0;
+}
+
+double ktimer_read(uint64_t *launches) {
+  KTimer &t = ktimer();
+  std::lock_guard<std::mutex> g(t.mu);
+  double sum = 0;
+  for (size_t i = 0; i < t.used; ++i) {
+    float ms = 0;
+    if (hipEventSynchronize(t.ev[i].second) != hipSuccess ||
+        hipEventElapsedTime(&ms, t.ev[i].first, t.ev[i].second) != hipSuccess)
+      return -1.0;
+    sum += ms;
+  }
+  if (launches) *launches = t.used;
+  return t.used ? sum / (double)t.used : 0.0;
+}
 
 // ------------------------------------------------------- literal engine
 // MatchType::Literal for find / is_match batches (exec.rs:601-625 find_literals,

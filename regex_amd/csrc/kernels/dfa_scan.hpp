@@ -235,6 +235,11 @@ hipError_t launch_lit_find(int mode, const BatchDev &b, const FwdDfaDev &f, void
 // engine, -4 = the chunked long scan (launch_long_scan).
 int last_fwd_path();
 void note_fwd_path(int path);
+// Kernel timer (rure_amd_kernel_timer): HIP event pairs around bracketed launches.
+void ktimer_begin(hipStream_t st);
+void ktimer_end(hipStream_t st);
+int ktimer_set(int on);
+double ktimer_read(uint64_t *launches);
 // Multi-GPU gather (gather_scan.hip): records (3 u64: base + haystack, start,
 // end) of the haystacks whose find result holds a match, first `cap`; *count.
 hipError_t launch_compact_matches(const uint64_t *found, uint64_t n, uint64_t base, uint64_t *rec, uint64_t cap,

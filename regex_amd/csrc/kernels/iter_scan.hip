@@ -740,7 +740,7 @@ __global__ __launch_bounds__(256) void iter_spec_sa_tile_kernel(BatchDev b, Geo 
 // ------------------------------------------------------------------------
 // Several Shift-And regexes over one text in one pass (rure_amd_find_iter_
 // span_multi; regex-dna's 9 variants read the stripped stream once instead of
-// 9 times).  Every regex keeps its own bits (packed into NW 64-bit words: a
+// 9 times).  Every regex keeps its own bits (packed into NW 32-bit words: a
 // word's sequences step together, the init bits re-arm each sequence's first
 // bit whatever the previous one shifted in), its own greedy iteration state
 // and its own unit records, so the per-regex passes after this one (fix,
@@ -1900,7 +1900,8 @@ static hipError_t iter_post(const BatchDev &b, const Geo &g, uint64_t nunits, co
 // (iter_spec_sa_multi_tile_kernel), then each regex's own passes.  Returns
 // hipErrorNotSupported (nothing launched) when they do not qualify: every
 // regex on the Shift-And engine with one string length, the tile geometry,
-// at most kSaMultiMax regexes in at most 4 words of 64 bits.
+// at most kSaMultiMax regexes in at most kSaMultiWords (8) words of 32 bits,
+// at most 32 bits per regex (a regex never straddles two words).
 hipError_t launch_find_iter_multi(const BatchDev &b, int nre, const FwdDfaDev *const *f, const RevDfaDev *const *r,
                                   uint64_t chunk, const IterOut *o, hipStream_t st, int cus, const IterSpan *spn) {
   if (nre < 1 || nre > kSaMultiMax || b.count == 0) return hipErrorNotSupported;
@@ -1949,7 +1950,9 @@ hipError_t launch_find_iter_multi(const BatchDev &b, int nre, const FwdDfaDev *c
 #define RURE_SAM(NWc)                                                                            \
   case NWc:                                                                                      \
     hipLaunchKernelGGL(sa_multi_image_kernel<NWc>, dim3(1), dim3(256), 0, st, m);                \
+    ktimer_begin(st);                                                                            \
     hipLaunchKernelGGL(iter_spec_sa_multi_tile_kernel<NWc>, sg, dim3(256), 0, st, b, g, nunits, m); \
+    ktimer_end(st);                                                                              \
     break;
     switch (nw) {
       RURE_SAM(1) RURE_SAM(2) RURE_SAM(3) RURE_SAM(4) RURE_SAM(5) RURE_SAM(6) RURE_SAM(7) RURE_SAM(8)
@@ -2017,9 +2020,11 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
       const bool use_lex = f->lex_bytes && !(lex_env && lex_env[0] == '0') && !b.offs && g.nk >= 2 &&
                            (g.chunk % 128) == 0 && (b.count == 1 || (b.stride % 16) == 0) &&
                            (((uintptr_t)(b.hay + b.start)) & 15) == 0;
+      ktimer_begin(st);  // bench diagnostics: the speculative kernel's duration
       if (use_lex) {
         hipLaunchKernelGGL(iter_spec_lex_tile_kernel, dim3(grid_cap((nunits + 63) / 64, 4, cus, 4)), dim3(256), 0,
                            st, b, g, nunits, *f, units, slots, counts);
+        ktimer_end(st);
         if ((e = hipGetLastError()) != hipSuccess) break;
         if ((e = allow_lds(iter_lex_tail_kernel, lb)) != hipSuccess) break;
         if (!(getenv("RURE_AMD_LEX_TAIL") && getenv("RURE_AMD_LEX_TAIL")[0] == '0'))
@@ -2059,6 +2064,7 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
         hipLaunchKernelGGL(iter_spec_kernel, dim3(grid), dim3(bs), iter_lds_bytes(*f, r), st, b, g, nunits, *f, r,
                            units, slots, counts, dirty);
       }
+      if (!use_lex) ktimer_end(st);
       if ((e = hipGetLastError()) != hipSuccess) break;
       e = iter_post(b, g, nunits, *f, r, sc, o, spn, st, cus);
     } while (false);

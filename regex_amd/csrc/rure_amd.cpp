@@ -403,40 +403,65 @@ struct Blob {
   }
 };
 
-// The scans take their scratch from the stream-ordered allocator; keep up to
-// 4 GiB of freed blocks in the device's pool instead of returning them to
-// the driver at every synchronisation (a multi-regex find_iter holds one
-// scratch per regex at once), once per device.
-static void keep_pool(int dev) {
-  static std::atomic<uint32_t> done{0};
-  if (dev < 0 || dev >= 32 || (done.fetch_or(1u << dev) & (1u << dev))) return;
-  hipMemPool_t pool;
-  if (hipDeviceGetDefaultMemPool(&pool, dev) != hipSuccess) return;
-  uint64_t thr = 4ull << 30;
-  (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
-}
-
 // ---------------------------------------------------------- scratch cache
 // See dfa_scan.hpp scratch_malloc.  Blocks are rounded up (4 KiB, then
-// 64 KiB multiples) and reused on the stream that freed them when at most
-// twice the request; a stream keeps at most kScratchCacheMax bytes cached
-// (beyond that frees go to hipFreeAsync), and an allocation that fails
-// returns every cached block to the pool and retries once.
-}  // namespace
-
-namespace {
-constexpr size_t kScratchCacheMax = 8ull << 30;
+// 64 KiB multiples).  A freed block is cached per device with an event
+// recorded on the freeing stream; an allocation of at most half its size on
+// any stream of that device waits for that event (hipStreamWaitEvent) and
+// reuses it, so reuse is ordered after the previous user's kernels whatever
+// stream either used (a destroyed and recreated stream handle, the per-thread
+// default stream).  The cache holds at most max(kScratchMinCap, 2 x the peak
+// of live scratch bytes), at most kScratchMaxCap (RURE_AMD_SCRATCH_CAP
+// overrides, bytes); beyond that a free goes to hipFreeAsync.  Cached blocks
+// are returned by rure_amd_release_scratch(), when the last rure / rure_set
+// is freed, and before a retry when an allocation fails.
+constexpr size_t kScratchMinCap = 256ull << 20, kScratchMaxCap = 8ull << 30;
+struct ScratchBlock {
+  size_t n;
+  int dev;
+  hipEvent_t ev;   // recorded at the last free (nullptr: never freed yet)
+};
 struct ScratchCache {
   std::mutex mu;
-  std::map<std::pair<int, hipStream_t>, std::multimap<size_t, void *>> free_blocks;
-  std::map<std::pair<int, hipStream_t>, size_t> cached;
-  std::unordered_map<void *, size_t> sizes;  // every block made here (live or cached)
+  std::map<int, std::multimap<size_t, std::pair<void *, ScratchBlock>>> free_blocks;
+  std::unordered_map<void *, ScratchBlock> live;
+  size_t cached = 0, live_bytes = 0, peak_live = 0;
 };
 ScratchCache &scratch_cache() {
   static ScratchCache *c = new ScratchCache();  // never destroyed: frees may run at exit
   return *c;
 }
 size_t scratch_round(size_t n) { return n <= 4096 ? 4096 : (n + 65535) & ~(size_t)65535; }
+size_t scratch_cap(const ScratchCache &c) {
+  if (const char *v = getenv("RURE_AMD_SCRATCH_CAP")) return (size_t)strtoull(v, nullptr, 10);
+  return std::min(kScratchMaxCap, std::max(kScratchMinCap, 2 * c.peak_live));
+}
+// Returns every cached block (caller holds c.mu).  The frees are ordered
+// after the block's last use through its event on the legacy default stream,
+// which every device has.
+void scratch_drop_all(ScratchCache &c) {
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  for (auto &kv : c.free_blocks) {
+    if (kv.second.empty()) continue;
+    (void)hipSetDevice(kv.first);
+    for (auto &blk : kv.second) {
+      hipEvent_t ev = blk.second.second.ev;
+      if (ev) (void)hipStreamWaitEvent(nullptr, ev, 0);
+      (void)hipFreeAsync(blk.second.first, nullptr);
+      if (ev) (void)hipEventDestroy(ev);
+    }
+    kv.second.clear();
+    // hand the freed blocks back to the driver, not only to the pool (the
+    // wait is for the blocks' last users, as hipFree of the tables waits)
+    hipMemPool_t pool;
+    if (hipStreamSynchronize(nullptr) == hipSuccess && hipDeviceGetDefaultMemPool(&pool, kv.first) == hipSuccess)
+      (void)hipMemPoolTrimTo(pool, 0);
+  }
+  (void)hipSetDevice(cur);
+  c.cached = 0;
+}
+std::atomic<long> g_live_handles{0};   // rure + rure_set objects alive
 }  // namespace
 
 hipError_t rure_amd::scratch_malloc(void **p, size_t bytes, hipStream_t st) {
@@ -445,61 +470,67 @@ hipError_t rure_amd::scratch_malloc(void **p, size_t bytes, hipStream_t st) {
   hipError_t e = hipGetDevice(&d);
   if (e != hipSuccess) return e;
   const size_t n = scratch_round(bytes);
-  const auto key = std::make_pair(d, st);
   ScratchCache &c = scratch_cache();
   {
     std::lock_guard<std::mutex> g(c.mu);
-    auto it = c.free_blocks.find(key);
-    if (it != c.free_blocks.end()) {
-      auto b = it->second.lower_bound(n);
-      if (b != it->second.end() && b->first <= 2 * n) {
-        *p = b->second;
-        c.cached[key] -= b->first;
-        it->second.erase(b);
-        return hipSuccess;
+    auto &fb = c.free_blocks[d];
+    auto b = fb.lower_bound(n);
+    if (b != fb.end() && b->first <= 2 * n) {
+      void *q = b->second.first;
+      ScratchBlock blk = b->second.second;
+      fb.erase(b);
+      c.cached -= blk.n;
+      if (blk.ev && (e = hipStreamWaitEvent(st, blk.ev, 0)) != hipSuccess) {
+        c.live[q] = blk;  // still owned: the caller's failure path frees it
+        return e;
       }
+      c.live[q] = blk;
+      c.live_bytes += blk.n;
+      c.peak_live = std::max(c.peak_live, c.live_bytes);
+      *p = q;
+      return hipSuccess;
     }
   }
   void *q = nullptr;
   e = hipMallocAsync(&q, n, st);
   if (e == hipErrorOutOfMemory) {
     (void)hipGetLastError();
-    std::lock_guard<std::mutex> g(c.mu);
-    for (auto &kv : c.free_blocks) {
-      for (auto &blk : kv.second) {
-        c.sizes.erase(blk.second);
-        (void)hipFreeAsync(blk.second, kv.first.second);
-      }
-      kv.second.clear();
-      c.cached[kv.first] = 0;
+    {
+      std::lock_guard<std::mutex> g(c.mu);
+      scratch_drop_all(c);
     }
+    e = hipMallocAsync(&q, n, st);
   }
-  if (e == hipErrorOutOfMemory) e = hipMallocAsync(&q, n, st);
   if (e != hipSuccess) return e;
   std::lock_guard<std::mutex> g(c.mu);
-  c.sizes[q] = n;
+  c.live[q] = ScratchBlock{n, d, nullptr};
+  c.live_bytes += n;
+  c.peak_live = std::max(c.peak_live, c.live_bytes);
   *p = q;
   return hipSuccess;
 }
 
 hipError_t rure_amd::scratch_free(void *p, hipStream_t st) {
   if (!p) return hipSuccess;
-  int d = 0;
-  hipError_t e = hipGetDevice(&d);
-  if (e != hipSuccess) return e;
-  const auto key = std::make_pair(d, st);
   ScratchCache &c = scratch_cache();
   {
     std::lock_guard<std::mutex> g(c.mu);
-    auto it = c.sizes.find(p);
-    if (it != c.sizes.end()) {
-      size_t &cached = c.cached[key];
-      if (cached + it->second <= kScratchCacheMax) {
-        cached += it->second;
-        c.free_blocks[key].emplace(it->second, p);
-        return hipSuccess;
+    auto it = c.live.find(p);
+    if (it != c.live.end()) {
+      ScratchBlock blk = it->second;
+      c.live.erase(it);
+      c.live_bytes -= blk.n;
+      if (c.cached + blk.n <= scratch_cap(c)) {
+        hipError_t e = hipSuccess;
+        if (!blk.ev) e = hipEventCreateWithFlags(&blk.ev, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventRecord(blk.ev, st);
+        if (e == hipSuccess) {
+          c.free_blocks[blk.dev].emplace(blk.n, std::make_pair(p, blk));
+          c.cached += blk.n;
+          return hipSuccess;
+        }
       }
-      c.sizes.erase(it);
+      if (blk.ev) (void)hipEventDestroy(blk.ev);
     }
   }
   return hipFreeAsync(p, st);
@@ -507,8 +538,22 @@ hipError_t rure_amd::scratch_free(void *p, hipStream_t st) {
 
 namespace {
 
+void scratch_release() {
+  ScratchCache &c = scratch_cache();
+  std::lock_guard<std::mutex> g(c.mu);
+  scratch_drop_all(c);
+}
+
+void handle_created() { g_live_handles.fetch_add(1); }
+void handle_freed() {
+  if (g_live_handles.fetch_sub(1) == 1) scratch_release();
+}
+
+}  // namespace
+
+namespace {
+
 int device_cus(int dev) {
-  keep_pool(dev);
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return 256;
   return prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
@@ -1217,7 +1262,7 @@ uint64_t odd_lines(uint64_t bytes) {
 // Few long haystacks: one lane per haystack would leave the chip idle, so the
 // search is split into chunks (launch_long_scan).  Needs a DFA that cannot
 // quit (the Pike VM fallback is per haystack).
-bool long_batch(const BatchDev &b, const DevTables &t, uint64_t *chunk) {
+bool long_batch(int mode, const BatchDev &b, const DevTables &t, uint64_t *chunk) {
   if (b.offs || !t.has_dfa || t.quit_possible || b.count == 0) return false;
   const uint64_t span = b.length > b.start ? b.length - b.start : 0;
   if (span < (256u << 10) || b.count >= (uint64_t)t.cus * 128) {
@@ -1227,8 +1272,13 @@ bool long_batch(const BatchDev &b, const DevTables &t, uint64_t *chunk) {
     // searches over about one wave per CU.  End-anchored regexes keep the
     // reverse scan (it reads O(match) bytes); single calls and batches of
     // fewer than 64 haystacks keep one lane each.  RURE_AMD_SPLIT=0 turns it off.
+    // Only is_match: a unit stops at its first match there, while a find /
+    // shortest_match unit scans on until the DFA dies, so a pattern that never
+    // dies ([^\n]* over text without newlines) would cost every unit the rest
+    // of its haystack (about units / 2 times the unsplit work).
     const char *sv = getenv("RURE_AMD_SPLIT");
-    if ((sv && sv[0] == '0') || t.anchored_rev || span < 512 || b.count < 64 || b.count > (uint64_t)t.cus * 16)
+    if ((sv && sv[0] == '0') || mode != MODE_ISMATCH || t.anchored_rev || span < 512 || b.count < 64 ||
+        b.count > (uint64_t)t.cus * 16)
       return false;
     const uint64_t per_h = ((uint64_t)t.cus * 64 + b.count - 1) / b.count;
     const uint64_t c = odd_lines(std::max<uint64_t>(128, (span + per_h - 1) / per_h));
@@ -1255,7 +1305,7 @@ bool long_batch(const BatchDev &b, const DevTables &t, uint64_t *chunk) {
 hipError_t run_dfa_step(int mode, const BatchDev &b, const DevTables &t, void *out, hipStream_t st, int dfa_grid,
                         const FwdDfaDev *iter) {
   uint64_t chunk = 0;
-  const bool long_fwd = iter && long_batch(b, t, &chunk);
+  const bool long_fwd = iter && long_batch(mode, b, t, &chunk);
   if (t.anchored_rev && !(long_fwd && b.start == 0)) return launch_dfa_anchored_rev(mode, b, t.r, out, st, dfa_grid);
   if (long_fwd) return launch_long_scan(mode, b, *iter, t.r, chunk, out, st, t.cus);
   return launch_dfa_fwd(mode, b, t.f, t.r, out, st, dfa_grid);
@@ -1265,7 +1315,7 @@ hipError_t run_regex(int mode, const BatchDev &b, const DevTables &t, void *out,
                      const FwdDfaDev *iter = nullptr) {
   if (!t.has_dfa) return run_pike(mode, false, b, t, out, st);
   uint64_t chunk = 0;
-  if (iter && long_batch(b, t, &chunk) && !(t.anchored_rev && b.start != 0))
+  if (iter && long_batch(mode, b, t, &chunk) && !(t.anchored_rev && b.start != 0))
     return launch_long_scan(mode, b, *iter, t.r, chunk, out, st, t.cus);
   if (!t.quit_possible) return run_dfa_step(mode, b, t, out, st, dfa_grid, nullptr);
   // the DFA kernels flag a quit; the Pike VM fallback returns at once without
@@ -1410,7 +1460,7 @@ bool single_call(rure *re, int mode, const uint8_t *hay, size_t len, size_t star
   if (!t) die(err);
   uint64_t chunk;
   BatchDev probe{nullptr, nullptr, len, len, 1, start};
-  const FwdDfaDev *iter = long_batch(probe, *t, &chunk) ? iter_device(re, *t, &err) : nullptr;  // locks re->mu
+  const FwdDfaDev *iter = long_batch(mode, probe, *t, &chunk) ? iter_device(re, *t, &err) : nullptr;  // locks re->mu
   std::lock_guard<std::mutex> g(re->mu);
   int d = 0;
   if (!hip_ok(hipGetDevice(&d), &err)) die(err);
@@ -1544,6 +1594,7 @@ rure *rure_compile(const uint8_t *pattern, size_t length, uint32_t flags, rure_o
   o.reverse = true;
   if (!compile_program(es, o, &re->rev, &err)) { if (error) error->msg = err; return nullptr; }
   re->fwd.dfa_size_limit = re->rev.dfa_size_limit = re->opts.dfa_size_limit;
+  handle_created();
   return re.release();
 }
 
@@ -1574,6 +1625,7 @@ void rure_free(rure *re) {
     (void)hipSetDevice(cur);
   }
   delete re;
+  handle_freed();
 }
 
 // ---------------------------------------------------------------- searches
@@ -1766,6 +1818,7 @@ rure_set *rure_compile_set(const uint8_t **patterns, const size_t *lens, size_t 
     }
     rs->groups.push_back(g);
   }
+  handle_created();
   return rs.release();
 }
 
@@ -1782,7 +1835,10 @@ void rure_set_free(rure_set *rs) {
     (void)hipSetDevice(cur);
   }
   delete rs;
+  handle_freed();
 }
+
+void rure_amd_release_scratch(void) { scratch_release(); }
 
 size_t rure_set_len(rure_set *rs) { return rs->exprs.size(); }
 
@@ -1825,11 +1881,11 @@ bool rure_set_matches(rure_set *rs, const uint8_t *hay, size_t len, size_t start
 // literals, on batches of many haystacks (few long ones keep the chunked DFA
 // scan).  RURE_AMD_LIT=1 / 0 forces it on / off.
 static constexpr size_t kLitFindMax = 8;
-static const FwdDfaDev *literal_engine(rure *re, DevTables &t, const BatchDev &b) {
+static const FwdDfaDev *literal_engine(int mode, rure *re, DevTables &t, const BatchDev &b) {
   uint64_t chunk;
   const char *env = getenv("RURE_AMD_LIT");
   if (env && env[0] != '1') return nullptr;
-  if (long_batch(b, t, &chunk)) return nullptr;
+  if (!env && long_batch(mode, b, t, &chunk)) return nullptr;  // RURE_AMD_LIT=1 forces the literal engine
   {
     // the literal set alone (cheap) before any find_iter DFA is built
     std::lock_guard<std::mutex> g(re->mu);
@@ -1850,11 +1906,11 @@ int rure_amd_find_batch(rure *re, const rure_amd_batch *batch, rure_match *out, 
   std::string err;
   DevTables *t = regex_device(re, &err);
   if (!t) return err.rfind("HIP", 0) == 0 ? RURE_AMD_ERR_HIP : RURE_AMD_ERR_DFA;
-  if (const FwdDfaDev *lit = literal_engine(re, *t, b))
+  if (const FwdDfaDev *lit = literal_engine(MODE_FIND, re, *t, b))
     return launch_lit_find(MODE_FIND, b, *lit, out, (hipStream_t)stream) == hipSuccess ? RURE_AMD_OK : RURE_AMD_ERR_HIP;
   int grid = grid_for(b.count, t->f.lds_bytes, t->cus);
   uint64_t chunk;
-  const FwdDfaDev *iter = long_batch(b, *t, &chunk) ? iter_device(re, *t, &err) : nullptr;
+  const FwdDfaDev *iter = long_batch(MODE_FIND, b, *t, &chunk) ? iter_device(re, *t, &err) : nullptr;
   if (run_regex(MODE_FIND, b, *t, out, (hipStream_t)stream, grid, iter) != hipSuccess) return RURE_AMD_ERR_HIP;
   return RURE_AMD_OK;
 }
@@ -1892,12 +1948,12 @@ int rure_amd_is_match_batch(rure *re, const rure_amd_batch *batch, uint8_t *out,
   std::string err;
   DevTables *t = regex_device(re, &err);
   if (!t) return err.rfind("HIP", 0) == 0 ? RURE_AMD_ERR_HIP : RURE_AMD_ERR_DFA;
-  if (const FwdDfaDev *lit = literal_engine(re, *t, b))
+  if (const FwdDfaDev *lit = literal_engine(MODE_ISMATCH, re, *t, b))
     return launch_lit_find(MODE_ISMATCH, b, *lit, out, (hipStream_t)stream) == hipSuccess ? RURE_AMD_OK
                                                                                       : RURE_AMD_ERR_HIP;
   int grid = grid_for(b.count, t->f.lds_bytes, t->cus);
   uint64_t chunk;
-  const FwdDfaDev *iter = long_batch(b, *t, &chunk) ? iter_device(re, *t, &err) : nullptr;
+  const FwdDfaDev *iter = long_batch(MODE_ISMATCH, b, *t, &chunk) ? iter_device(re, *t, &err) : nullptr;
   if (run_regex(MODE_ISMATCH, b, *t, out, (hipStream_t)stream, grid, iter) != hipSuccess) return RURE_AMD_ERR_HIP;
   return RURE_AMD_OK;
 }
@@ -1911,7 +1967,7 @@ int rure_amd_shortest_match_batch(rure *re, const rure_amd_batch *batch, size_t 
   if (!t) return err.rfind("HIP", 0) == 0 ? RURE_AMD_ERR_HIP : RURE_AMD_ERR_DFA;
   int grid = grid_for(b.count, t->f.lds_bytes, t->cus);
   uint64_t chunk;
-  const FwdDfaDev *iter = long_batch(b, *t, &chunk) ? iter_device(re, *t, &err) : nullptr;
+  const FwdDfaDev *iter = long_batch(MODE_SHORTEST, b, *t, &chunk) ? iter_device(re, *t, &err) : nullptr;
   if (run_regex(MODE_SHORTEST, b, *t, end, (hipStream_t)stream, grid, iter) != hipSuccess) return RURE_AMD_ERR_HIP;
   return RURE_AMD_OK;
 }
@@ -2401,6 +2457,9 @@ int rure_amd_uses_dfa(rure *re) {
 }
 
 int rure_amd_last_fwd_path(void) { return rure_amd::last_fwd_path(); }
+
+int rure_amd_kernel_timer(int on) { return rure_amd::ktimer_set(on); }
+double rure_amd_kernel_timer_read(uint64_t *launches) { return rure_amd::ktimer_read(launches); }
 
 int rure_amd_set_uses_dfa(rure_set *rs) {
   if (!rs) return RURE_AMD_ERR_ARG;

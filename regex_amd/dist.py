@@ -84,6 +84,10 @@ class RecordGather(object):
     def step(self, found, base, stream=None):
         if found.is_cuda:
             self.compact(found, base, stream)
+            # the collective runs on torch's current stream: order it after
+            # the compaction when that ran on another stream
+            if stream is not None and stream != torch.cuda.current_stream(found.device):
+                torch.cuda.current_stream(found.device).wait_stream(stream)
         else:  # CPU rehearsal (gloo tests): the same layout from torch ops
             rec = compact_matches(found, base)
             k = rec.shape[0]

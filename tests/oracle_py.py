@@ -147,6 +147,17 @@ class OracleRegex(object):
                 return [(int(buf[2 * i]), int(buf[2 * i + 1])) for i in range(n)]
             cap = n
 
+    def find_iter_array(self, text, start=0, cap=None):
+        """find_iter as an (n, 2) uint64 array (no per-match Python objects;
+        the bench's CPU baseline).  `cap`: expected matches (rerun if short)."""
+        cap = cap if cap is not None else len(text) // 32 + 1024
+        while True:
+            buf = np.empty(2 * max(cap, 1), dtype=np.uint64)
+            n = orc_find_iter_at(self._r, self._c, text, len(text), start, buf.ctypes.data, cap)
+            if n <= cap:
+                return buf[: 2 * n].reshape(n, 2)
+            cap = n
+
     def matches(self, text, start=0, nfa=False):
         m = np.zeros(max(self.n, 1), dtype=np.uint8)
         f = orc_many_matches_nfa if nfa else orc_many_matches_at

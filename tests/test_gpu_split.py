@@ -1,6 +1,8 @@
 """Small batches of medium haystacks (BASELINE C1's shape, 1024 x 1 KiB) are
 split into units of >= 128 B scanned with the cut-bounded search
 (rure_amd.cpp long_batch, long_scan_kernel) instead of one lane per haystack.
+is_match takes it (find / shortest_match units would scan on until the DFA
+dies: a never-dying pattern costs every unit the rest of its haystack);
 is_match / find / shortest_match must equal the oracle and the unsplit
 kernels (RURE_AMD_SPLIT=0) bit for bit, with matches crossing every unit cut,
 Unicode and invalid UTF-8 bytes, start > 0 and ragged strides."""
@@ -38,9 +40,9 @@ def test_split_small_batch(cuda, monkeypatch, pat, shape):
     o = OracleRegex(re)
     for start in (0, 7):
         got_f = re.find_batch(d, stride=S, length=L, count=n, start=start).cpu().numpy()
-        got_m = re.is_match_batch(d, stride=S, length=L, count=n, start=start).cpu().numpy()
         got_s = re.shortest_match_batch(d, stride=S, length=L, count=n, start=start).cpu().numpy()
-        if pat in SPLIT_PATS:
+        got_m = re.is_match_batch(d, stride=S, length=L, count=n, start=start).cpu().numpy()
+        if pat in SPLIT_PATS:  # only is_match takes the split (a find unit scans until the DFA dies)
             assert N.rure_amd_last_fwd_path() == -4, (pat, shape)
         monkeypatch.setenv("RURE_AMD_SPLIT", "0")
         ref_f = re.find_batch(d, stride=S, length=L, count=n, start=start).cpu().numpy()
