@@ -4,7 +4,8 @@ ARCH ?= gfx950
 CXXFLAGS = -O3 -std=c++17 -fPIC -Wall -Wno-unused-function
 LIB = regex_amd/lib/librure_amd.so
 HOST_SRC = regex_amd/csrc/host/syntax.cpp regex_amd/csrc/host/compile.cpp regex_amd/csrc/host/dfa_build.cpp \
-           regex_amd/csrc/host/nfa_build.cpp regex_amd/csrc/host/literals.cpp
+           regex_amd/csrc/host/nfa_build.cpp regex_amd/csrc/host/literals.cpp \
+           regex_amd/csrc/host/literal_sets.cpp
 RT_SRC = regex_amd/csrc/rure_amd.cpp
 KERNEL_SRC = regex_amd/csrc/kernels/dfa_scan.hip regex_amd/csrc/kernels/nfa_scan.hip regex_amd/csrc/kernels/iter_scan.hip \
              regex_amd/csrc/kernels/replace_scan.hip regex_amd/csrc/kernels/gather_scan.hip

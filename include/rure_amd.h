@@ -336,6 +336,35 @@ int64_t rure_amd_literals_export(rure *re, uint32_t *lens, uint8_t *bytes, size_
  * class sequence and the string length.  Returns the state width in bits, 0
  * when the regex is not a set of equal-length strings that fits 64 bits. */
 int64_t rure_amd_shiftand_export(rure *re, uint64_t *mask, uint64_t *init, uint64_t *fin, uint32_t *len);
+/* Literal sets and the reference's engine choice (host only).
+ * rure_amd_literals_syntax: regex-syntax's Expr::prefixes (which 0) /
+ * suffixes (which 1) of a pattern (regex-syntax/src/literals.rs:285-304)
+ * with the given limits (the reference's defaults: 250 bytes, 10 class
+ * members), serialized as records {u8 cut, u32 length, bytes}; returns the
+ * serialized size (copied only when cap suffices).  rure_amd_literals_op on
+ * such records: 0 unambiguous_prefixes, 1 longest_common_prefix (raw bytes),
+ * 2 longest_common_suffix (raw bytes), 3 unambiguous_suffixes.
+ * rure_amd_exec_literals_export: the unambiguous prefix (which 0) / suffix
+ * (which 1) set the reference's Exec builds for this regex (exec.rs:308-321).
+ * rure_amd_match_info_get: its MatchType (exec.rs:1130-1210; codes:
+ * 0 Literal(Unanchored), 1 Literal(AnchoredStart), 2 Literal(AnchoredEnd),
+ * 3 Dfa, 4 DfaAnchoredReverse, 5 DfaSuffix, 6 Nfa, 7 Nothing), the two
+ * LiteralSearchers' matcher kind (0 Empty, 1 Bytes, 2 one literal,
+ * 3 several), len(), complete(), lcp / lcs character lengths and the lcs. */
+typedef struct rure_amd_match_info {
+  int32_t match_type;
+  int32_t prefix_matcher, suffix_matcher;
+  uint32_t prefix_len, suffix_len;
+  uint8_t prefix_complete, suffix_complete, pad[2];
+  uint32_t lcp_chars, lcs_chars;
+  uint32_t lcs_bytes;
+  uint8_t lcs[256];
+} rure_amd_match_info;
+int64_t rure_amd_literals_syntax(const uint8_t *pattern, size_t length, uint32_t flags, int which,
+                                 size_t limit_size, size_t limit_class, uint8_t *out, size_t cap);
+int64_t rure_amd_literals_op(int op, const uint8_t *in, size_t in_len, uint8_t *out, size_t cap);
+int64_t rure_amd_exec_literals_export(rure *re, int which, uint8_t *out, size_t cap);
+int rure_amd_match_info_get(rure *re, rure_amd_match_info *info);
 /* 1 if batched searches of this regex run the DFA kernels, 0 if only the
  * Pike VM kernel (automaton too large), negative on error. */
 int rure_amd_uses_dfa(rure *re);

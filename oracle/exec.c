@@ -57,7 +57,15 @@ orc_regex *orc_regex_new(orc_prog *nfa, orc_prog *fwd, orc_prog *rev) {
   r->nfa = nfa;
   r->fwd = fwd;
   r->rev = rev;
+  r->mt = -1;
   return r;
+}
+
+static void lits_free(orc_lits *l) {
+  for (size_t i = 0; i < l->n; ++i) free(l->lit[i]);
+  free(l->lit);
+  free(l->len);
+  memset(l, 0, sizeof(*l));
 }
 
 void orc_regex_free(orc_regex *r) {
@@ -65,7 +73,37 @@ void orc_regex_free(orc_regex *r) {
   orc_prog_free(r->nfa);
   orc_prog_free(r->fwd);
   orc_prog_free(r->rev);
+  lits_free(&r->pre);
+  lits_free(&r->suf);
+  free(r->lcs);
   free(r);
+}
+
+static void lits_parse(orc_lits *l, const uint8_t *b, size_t n, int matcher) {
+  lits_free(l);
+  l->matcher = matcher;
+  for (size_t i = 0; i + 5 <= n;) {
+    uint32_t k;
+    memcpy(&k, b + i + 1, 4);
+    l->lit = (uint8_t **)realloc(l->lit, (l->n + 1) * sizeof(uint8_t *));
+    l->len = (size_t *)realloc(l->len, (l->n + 1) * sizeof(size_t));
+    l->lit[l->n] = (uint8_t *)malloc(k ? k : 1);
+    memcpy(l->lit[l->n], b + i + 5, k);
+    l->len[l->n] = k;
+    l->n++;
+    i += 5 + k;
+  }
+}
+
+void orc_regex_set_exec(orc_regex *r, int match_type, const uint8_t *pre, size_t pre_len, int pre_matcher,
+                        const uint8_t *suf, size_t suf_len, int suf_matcher, const uint8_t *lcs, size_t lcs_len) {
+  r->mt = match_type;
+  lits_parse(&r->pre, pre, pre_len, pre_matcher);
+  lits_parse(&r->suf, suf, suf_len, suf_matcher);
+  free(r->lcs);
+  r->lcs = (uint8_t *)malloc(lcs_len ? lcs_len : 1);
+  memcpy(r->lcs, lcs, lcs_len);
+  r->lcs_len = lcs_len;
 }
 
 orc_cache *orc_cache_new(const orc_regex *r) {
@@ -149,11 +187,140 @@ static int find_dfa_forward(const orc_regex *r, orc_cache *c, const uint8_t *tex
   return R_MATCH;
 }
 
+/* Leftmost occurrence of `needle` in hay[0..n) (memmem), -1 if none. */
+static long find_sub(const uint8_t *hay, size_t n, const uint8_t *needle, size_t k) {
+  if (k == 0) return 0;
+  for (size_t i = 0; i + k <= n; ++i)
+    if (hay[i] == needle[0] && memcmp(hay + i, needle, k) == 0) return (long)i;
+  return -1;
+}
+
+/* LiteralSearcher::find (src/literals.rs:92-103) over hay[0..n): Empty
+ * matches the empty string at 0; Bytes the first byte of the set; one
+ * literal its first occurrence; several (Teddy / Aho-Corasick) the leftmost
+ * occurrence of any (the set is unambiguous: no member is a substring of
+ * another, so one literal at most occurs at a position and the occurrence
+ * that ends first is the leftmost). */
+static int lits_find(const orc_lits *l, const uint8_t *hay, size_t n, size_t *s, size_t *e) {
+  if (l->matcher == 0) { *s = *e = 0; return 1; }
+  long best = -1;
+  size_t blen = 0;
+  for (size_t j = 0; j < l->n; ++j) {
+    size_t nj = n;  /* only occurrences starting before the best so far */
+    if (best >= 0) {
+      size_t cap = (size_t)best + l->len[j];
+      cap = cap ? cap - 1 : 0;
+      if (cap < nj) nj = cap;
+    }
+    long i = find_sub(hay, nj, l->lit[j], l->len[j]);
+    if (i >= 0 && (best < 0 || i < best)) { best = i; blen = l->len[j]; }
+  }
+  if (best < 0) return 0;
+  *s = (size_t)best;
+  *e = (size_t)best + blen;
+  return 1;
+}
+
+/* find_start / find_end (literals.rs:105-128): the first literal of iter()
+ * (Empty yields none) that the text starts / ends with. */
+static int lits_find_start(const orc_lits *l, const uint8_t *hay, size_t n, size_t *s, size_t *e) {
+  if (l->matcher == 0) return 0;
+  for (size_t j = 0; j < l->n; ++j)
+    if (l->len[j] <= n && memcmp(hay, l->lit[j], l->len[j]) == 0) { *s = 0; *e = l->len[j]; return 1; }
+  return 0;
+}
+static int lits_find_end(const orc_lits *l, const uint8_t *hay, size_t n, size_t *s, size_t *e) {
+  if (l->matcher == 0) return 0;
+  for (size_t j = 0; j < l->n; ++j)
+    if (l->len[j] <= n && memcmp(hay + n - l->len[j], l->lit[j], l->len[j]) == 0) {
+      *s = n - l->len[j];
+      *e = n;
+      return 1;
+    }
+  return 0;
+}
+
+/* exec.rs:601-625 find_literals */
+static int find_literals(const orc_regex *r, const uint8_t *text, size_t len, size_t start, size_t *ms, size_t *me) {
+  size_t s, e;
+  int ok;
+  if (r->mt == 0) ok = lits_find(&r->pre, text + start, len - start, &s, &e);
+  else if (r->mt == 1) ok = lits_find_start(&r->pre, text + start, len - start, &s, &e);
+  else ok = lits_find_end(&r->suf, text + start, len - start, &s, &e);
+  if (!ok) return 0;
+  *ms = start + s;
+  *me = start + e;
+  return 1;
+}
+
+/* exec.rs:725-756 exec_dfa_reverse_suffix.  Returns R_MATCH / R_NOMATCH /
+ * R_QUIT, or -1 for None (the reverse scan reached its slice start: give up
+ * to the forward DFA).  Each reverse scan sees only text[start..end], the
+ * previous suffix occurrence's end to this one's (its look-around at both
+ * slice edges is that of a text edge). */
+static int exec_dfa_reverse_suffix(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t len,
+                                   size_t original_start, size_t *ms, size_t *me) {
+  size_t start = original_start, end = start;
+  while (end <= len) {
+    start = end;
+    long i = find_sub(text + end, len - end, r->lcs, r->lcs_len);
+    if (i < 0) return R_NOMATCH;
+    end += (size_t)i + r->lcs_len;
+    size_t pos, consumed;
+    int k = orc_dfa_reverse(r->rev, c->rev, 0, text + start, end - start, end - start, &pos, &consumed);
+    c->st.rev_bytes += consumed;
+    if ((k == R_MATCH || k == R_NOMATCH) && pos == 0) return -1;
+    if (k == R_MATCH) { *ms = pos + start; *me = end; return R_MATCH; }
+    if (k == R_NOMATCH) continue;
+    return R_QUIT;
+  }
+  return R_NOMATCH;
+}
+
+/* exec.rs:764-794 find_dfa_reverse_suffix */
+static int find_dfa_reverse_suffix(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t len, size_t start,
+                                   size_t *ms, size_t *me) {
+  size_t s0, e0;
+  int k = exec_dfa_reverse_suffix(r, c, text, len, start, &s0, &e0);
+  if (k < 0) return find_dfa_forward(r, c, text, len, start, ms, me);
+  if (k != R_MATCH) return k;
+  /* the suffix occurrence is the earliest possible end: run the forward DFA
+   * from the match start for the leftmost-first end */
+  size_t end, stop;
+  int k2 = orc_dfa_forward(r->fwd, c->fwd, 0, text, len, s0, &end, &stop);
+  c->st.fwd_bytes += stop - s0;
+  if (k2 == R_QUIT) return R_QUIT;
+  if (k2 != R_MATCH) return R_NOMATCH;  /* the reference panics here ("BUG: reverse match implies ...") */
+  *ms = s0;
+  *me = end;
+  return R_MATCH;
+}
+
+/* exec.rs:700-710 shortest_dfa_reverse_suffix (end of the shortest match) */
+static int shortest_dfa_reverse_suffix(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t len,
+                                       size_t start, size_t *end) {
+  size_t s0, e0, stop;
+  int k = exec_dfa_reverse_suffix(r, c, text, len, start, &s0, &e0);
+  if (k < 0) {
+    k = orc_dfa_forward(r->fwd, c->fwd, 1, text, len, start, end, &stop);
+    c->st.fwd_bytes += stop - start;
+    return k;
+  }
+  if (k == R_MATCH) *end = e0;
+  return k;
+}
+
+static int is_literal(const orc_regex *r) { return r->mt >= 0 && r->mt <= 2; }
+static int use_anchored_rev(const orc_regex *r) { return r->mt < 0 ? anchored_rev(r) : r->mt == 4; }
+
 int orc_find_at(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t len, size_t start, size_t *ms,
                 size_t *me) {
   if (start > len) return 0;
-  int k = anchored_rev(r) ? find_dfa_anchored_reverse(r, c, 0, text, len, start, ms, me)
-                          : find_dfa_forward(r, c, text, len, start, ms, me);
+  if (is_literal(r)) return find_literals(r, text, len, start, ms, me);
+  if (r->mt == 6) return orc_find_nfa(r, c, text, len, start, ms, me);
+  int k = r->mt == 5 ? find_dfa_reverse_suffix(r, c, text, len, start, ms, me)
+          : use_anchored_rev(r) ? find_dfa_anchored_reverse(r, c, 0, text, len, start, ms, me)
+                                : find_dfa_forward(r, c, text, len, start, ms, me);
   if (k == R_MATCH) return 1;
   if (k == R_NOMATCH) return 0;
   c->st.quits++;
@@ -180,11 +347,18 @@ int orc_captures_at(const orc_regex *r, orc_cache *c, const uint8_t *text, size_
     if (nslots == 2) { slots[0] = ms; slots[1] = me; }
     return 1;
   }
-  if (r->nfa->anchored_start) return orc_captures_nfa(r, c, text, len, start, slots, nslots) &&
-                                     slots[0] != SIZE_MAX && slots[1] != SIZE_MAX;
   size_t ms, me;
-  int k = anchored_rev(r) ? find_dfa_anchored_reverse(r, c, 0, text, len, start, &ms, &me)
-                          : find_dfa_forward(r, c, text, len, start, &ms, &me);
+  int k;
+  if (is_literal(r)) {
+    k = find_literals(r, text, len, start, &ms, &me) ? R_MATCH : R_NOMATCH;
+  } else if (r->mt == 6 || ((r->mt < 0 || r->mt == 3) && r->nfa->anchored_start)) {
+    return orc_captures_nfa(r, c, text, len, start, slots, nslots) && slots[0] != SIZE_MAX &&
+           slots[1] != SIZE_MAX;
+  } else {
+    k = r->mt == 5 ? find_dfa_reverse_suffix(r, c, text, len, start, &ms, &me)
+        : use_anchored_rev(r) ? find_dfa_anchored_reverse(r, c, 0, text, len, start, &ms, &me)
+                              : find_dfa_forward(r, c, text, len, start, &ms, &me);
+  }
   if (k == R_NOMATCH) return 0;
   size_t n = len;
   if (k == R_MATCH) {
@@ -214,7 +388,16 @@ int orc_shortest_match_at(const orc_regex *r, orc_cache *c, const uint8_t *text,
   if (start > len) return 0;
   size_t e, stop;
   int k;
-  if (anchored_rev(r)) {
+  if (is_literal(r)) {
+    size_t s;
+    if (!find_literals(r, text, len, start, &s, &e)) return 0;
+    *end = e;
+    return 1;
+  }
+  if (r->mt == 6) return orc_shortest_nfa(r, c, text, len, start, end);
+  if (r->mt == 5) {
+    k = shortest_dfa_reverse_suffix(r, c, text, len, start, &e);
+  } else if (use_anchored_rev(r)) {
     size_t s;
     k = find_dfa_anchored_reverse(r, c, 1, text, len, start, &s, &e);
   } else {
@@ -231,7 +414,17 @@ int orc_is_match_at(const orc_regex *r, orc_cache *c, const uint8_t *text, size_
   if (start > len) return 0;
   size_t e, stop;
   int k;
-  if (anchored_rev(r)) {
+  if (is_literal(r)) {
+    size_t s;
+    return find_literals(r, text, len, start, &s, &e);
+  }
+  if (r->mt == 6) {
+    uint8_t m[1] = {0};
+    return orc_pike_exec(r->nfa, c->pike, m, 1, NULL, 0, 1, text, len, start);
+  }
+  if (r->mt == 5) {
+    k = shortest_dfa_reverse_suffix(r, c, text, len, start, &e);
+  } else if (use_anchored_rev(r)) {
     size_t s;
     k = find_dfa_anchored_reverse(r, c, 1, text, len, start, &s, &e);
   } else {

@@ -8,7 +8,9 @@
  *   dispatch            src/exec.rs       (find_dfa_forward, shortest_dfa, many_matches_at,
  *                                          NFA fallback on DFA Quit)
  *   iteration           src/re_trait.rs:197-221
- * Literal prefilters (src/literals.rs) are result-neutral and omitted.
+ * The engine choice (exec.rs:1130-1210) is restated where it is observable:
+ * MatchType::Literal searches the literal sets (exec.rs:601-625) and
+ * DfaSuffix scans for the suffix literal first (exec.rs:725-794).
  *
  * The Program (src/prog.rs contract) is supplied by the caller as flat
  * 12-byte instruction records (the product's host compiler exports them via
@@ -42,6 +44,17 @@ void orc_prog_free(orc_prog *p);
 /* rev may be NULL for sets.  Takes ownership of the programs. */
 orc_regex *orc_regex_new(orc_prog *nfa, orc_prog *fwd, orc_prog *rev);
 void orc_regex_free(orc_regex *r);
+
+/* The reference's engine choice for a single regex (src/exec.rs:1130-1210;
+ * the product computes it, rure_amd_match_info_get) and the literal sets it
+ * rests on, serialized as records {u8 cut, u32 len, bytes}: the unambiguous
+ * prefixes (nfa.prefixes) and suffixes with their searchers' matcher kinds
+ * (0 Empty, 1 Bytes, 2 one literal, 3 several), and suffixes.lcs().
+ * match_type: 0 Literal(Unanchored), 1 Literal(AnchoredStart),
+ * 2 Literal(AnchoredEnd), 3 Dfa, 4 DfaAnchoredReverse, 5 DfaSuffix, 6 Nfa.
+ * Without this call the oracle dispatches as for Dfa / DfaAnchoredReverse. */
+void orc_regex_set_exec(orc_regex *r, int match_type, const uint8_t *pre, size_t pre_len, int pre_matcher,
+                        const uint8_t *suf, size_t suf_len, int suf_matcher, const uint8_t *lcs, size_t lcs_len);
 
 orc_cache *orc_cache_new(const orc_regex *r);
 void orc_cache_free(orc_cache *c);

@@ -65,8 +65,20 @@ void orc_pike_cache_free(orc_pike_cache *c);
 int orc_pike_exec(const orc_prog *p, orc_pike_cache *c, uint8_t *matches, size_t nmatches, size_t *slots,
                   size_t nslots, int quit_after_match, const uint8_t *text, size_t len, size_t start);
 
+/* A literal set (src/literals.rs LiteralSearcher): literals in order. */
+typedef struct {
+  int matcher;          /* 0 Empty, 1 Bytes, 2 one literal, 3 several (Teddy / AC) */
+  size_t n;
+  uint8_t **lit;
+  size_t *len;
+} orc_lits;
+
 struct orc_regex {
   orc_prog *nfa, *fwd, *rev;
+  int mt;               /* MatchType code (orc_regex_set_exec), -1: not set (Dfa dispatch) */
+  orc_lits pre, suf;    /* nfa.prefixes, suffixes (exec.rs:308-321) */
+  uint8_t *lcs;         /* suffixes.lcs() (DfaSuffix) */
+  size_t lcs_len;
 };
 
 struct orc_cache {

@@ -20,6 +20,54 @@ __all__ = ["Regex", "RegexSet", "Error", "NoExpand", "NONE", "release_scratch"]
 NONE = N.NONE
 
 
+def _ser_lits(lits):
+    out = bytearray()
+    for v, cut in lits:
+        out += bytes([1 if cut else 0]) + len(v).to_bytes(4, "little") + bytes(v)
+    return bytes(out)
+
+
+def _de_lits(buf):
+    out, i = [], 0
+    while i < len(buf):
+        cut, n = buf[i] != 0, int.from_bytes(buf[i + 1:i + 5], "little")
+        out.append((bytes(buf[i + 5:i + 5 + n]), cut))
+        i += 5 + n
+    return out
+
+
+def _call_out(fn, *args):
+    n = fn(*args, None, 0)
+    if n < 0:
+        raise ValueError("literal extraction failed (%d)" % n)
+    buf = ctypes.create_string_buffer(max(n, 1))
+    fn(*args, buf, n)
+    return buf.raw[:n]
+
+
+def syntax_literals(pattern, which="prefixes", unicode=True, limit_size=250, limit_class=10):
+    """regex-syntax's Expr::prefixes / suffixes (regex-syntax/src/literals.rs)
+    of a pattern, as [(bytes, cut), ...] in the reference's order (host only)."""
+    if isinstance(pattern, str):
+        pattern = pattern.encode("utf-8")
+    return _de_lits(_call_out(N.rure_amd_literals_syntax, pattern, len(pattern),
+                              N.FLAG_UNICODE if unicode else 0, 0 if which == "prefixes" else 1,
+                              limit_size, limit_class))
+
+
+def literals_op(op, lits):
+    """Literals::unambiguous_prefixes ("unambiguous_prefixes" / "unambiguous_suffixes",
+    -> [(bytes, cut)]), longest_common_prefix / _suffix ("lcp" / "lcs" -> bytes)."""
+    code = {"unambiguous_prefixes": 0, "lcp": 1, "lcs": 2, "unambiguous_suffixes": 3}[op]
+    raw = _ser_lits(lits)
+    out = _call_out(N.rure_amd_literals_op, code, raw, len(raw))
+    return out if op in ("lcp", "lcs") else _de_lits(out)
+
+
+MATCH_TYPES = ["Literal(Unanchored)", "Literal(AnchoredStart)", "Literal(AnchoredEnd)", "Dfa",
+               "DfaAnchoredReverse", "DfaSuffix", "Nfa", "Nothing"]
+
+
 def release_scratch():
     """Returns the device scratch the library keeps cached between batched
     calls to the allocator (rure_amd_release_scratch); also happens when the
@@ -517,6 +565,20 @@ class Regex(object):
             cap = t
 
     # ----------------------------------------------------------- diagnostics
+    def match_info(self):
+        """The reference's engine choice for this regex (exec.rs:1130-1210)
+        and the literal searchers it rests on."""
+        i = N.MatchInfo()
+        _check(N.rure_amd_match_info_get(self._re, ctypes.byref(i)), "match_info")
+        return {"match_type": MATCH_TYPES[i.match_type], "prefix_matcher": i.prefix_matcher,
+                "suffix_matcher": i.suffix_matcher, "prefix_len": i.prefix_len, "suffix_len": i.suffix_len,
+                "prefix_complete": bool(i.prefix_complete), "suffix_complete": bool(i.suffix_complete),
+                "lcp_chars": i.lcp_chars, "lcs_chars": i.lcs_chars, "lcs": bytes(i.lcs[:i.lcs_bytes])}
+
+    def exec_literals(self, which="prefixes"):
+        """The unambiguous prefix / suffix literal set the reference builds (exec.rs:308-321)."""
+        return _de_lits(_call_out(N.rure_amd_exec_literals_export, self._re, 0 if which == "prefixes" else 1))
+
     def dfa_info(self, which=0):
         info = N.DfaInfo()
         rc = N.rure_amd_dfa_info_get(self._re, which, ctypes.byref(info))

@@ -152,6 +152,20 @@ rure_amd_first_byte_export = _sig("rure_amd_first_byte_export", ctypes.c_int, VP
 rure_amd_lex_export = _sig("rure_amd_lex_export", ctypes.c_int64, VP, VP, c_size, VP)
 rure_amd_set_matches_batch_words = _sig("rure_amd_set_matches_batch_words", ctypes.c_int, VP,
                                         ctypes.POINTER(RureBatch), VP, c_size, VP)
+class MatchInfo(ctypes.Structure):
+    _fields_ = [("match_type", ctypes.c_int32), ("prefix_matcher", ctypes.c_int32),
+                ("suffix_matcher", ctypes.c_int32), ("prefix_len", ctypes.c_uint32),
+                ("suffix_len", ctypes.c_uint32), ("prefix_complete", ctypes.c_uint8),
+                ("suffix_complete", ctypes.c_uint8), ("pad", ctypes.c_uint8 * 2),
+                ("lcp_chars", ctypes.c_uint32), ("lcs_chars", ctypes.c_uint32),
+                ("lcs_bytes", ctypes.c_uint32), ("lcs", ctypes.c_uint8 * 256)]
+
+
+rure_amd_literals_syntax = _sig("rure_amd_literals_syntax", ctypes.c_int64, ctypes.c_char_p, c_size, ctypes.c_uint32,
+                                ctypes.c_int, c_size, c_size, VP, c_size)
+rure_amd_literals_op = _sig("rure_amd_literals_op", ctypes.c_int64, ctypes.c_int, ctypes.c_char_p, c_size, VP, c_size)
+rure_amd_exec_literals_export = _sig("rure_amd_exec_literals_export", ctypes.c_int64, VP, ctypes.c_int, VP, c_size)
+rure_amd_match_info_get = _sig("rure_amd_match_info_get", ctypes.c_int, VP, VP)
 rure_amd_release_scratch = _sig("rure_amd_release_scratch", None)
 rure_amd_kernel_timer = _sig("rure_amd_kernel_timer", ctypes.c_int, ctypes.c_int)
 rure_amd_kernel_timer_read = _sig("rure_amd_kernel_timer_read", ctypes.c_double, VP)

@@ -27,6 +27,7 @@
 #include "host/dfa_build.hpp"
 #include "host/nfa_build.hpp"
 #include "host/literals.hpp"
+#include "host/literal_sets.hpp"
 #include "host/program.hpp"
 #include "host/syntax.hpp"
 #include "host/unicode_tables.h"
@@ -609,6 +610,7 @@ struct rure {
   uint32_t flags = 0;
   rure_options opts;
   Expr expr;
+  ExecLiterals xl;          // the reference's literal sets and MatchType (host/literal_sets.hpp)
   Program nfa, fwd, rev;
   std::mutex mu;
   bool built = false, dfa_ok = false;
@@ -1594,6 +1596,7 @@ rure *rure_compile(const uint8_t *pattern, size_t length, uint32_t flags, rure_o
   o.reverse = true;
   if (!compile_program(es, o, &re->rev, &err)) { if (error) error->msg = err; return nullptr; }
   re->fwd.dfa_size_limit = re->rev.dfa_size_limit = re->opts.dfa_size_limit;
+  re->xl = exec_literals(re->expr);
   handle_created();
   return re.release();
 }
@@ -2457,6 +2460,91 @@ int rure_amd_uses_dfa(rure *re) {
 }
 
 int rure_amd_last_fwd_path(void) { return rure_amd::last_fwd_path(); }
+
+namespace {
+void ser_lits(const std::vector<Lit> &ls, std::string *o) {
+  for (const Lit &l : ls) {
+    o->push_back((char)(l.cut ? 1 : 0));
+    const uint32_t n = (uint32_t)l.v.size();
+    o->append((const char *)&n, 4);
+    o->append(l.v);
+  }
+}
+bool de_lits(const uint8_t *in, size_t n, std::vector<Lit> *ls) {
+  size_t i = 0;
+  while (i < n) {
+    if (i + 5 > n) return false;
+    Lit l;
+    l.cut = in[i] != 0;
+    uint32_t k;
+    memcpy(&k, in + i + 1, 4);
+    i += 5;
+    if (i + k > n) return false;
+    l.v.assign((const char *)in + i, k);
+    i += k;
+    ls->push_back(l);
+  }
+  return true;
+}
+int64_t put_out(const std::string &s, uint8_t *out, size_t cap) {
+  if (out && cap >= s.size()) memcpy(out, s.data(), s.size());
+  return (int64_t)s.size();
+}
+}  // namespace
+
+int64_t rure_amd_literals_syntax(const uint8_t *pattern, size_t length, uint32_t flags, int which, size_t limit_size,
+                                 size_t limit_class, uint8_t *out, size_t cap) {
+  Expr e;
+  std::string err;
+  if (!parse_regex(std::string((const char *)pattern, length), syntax_flags(flags), &e, &err)) return RURE_AMD_ERR_ARG;
+  Literals l;
+  l.limit_size = limit_size;
+  l.limit_class = limit_class;
+  if (which == 0) l.union_prefixes(e);
+  else l.union_suffixes(e);
+  std::string o;
+  ser_lits(l.lits, &o);
+  return put_out(o, out, cap);
+}
+
+int64_t rure_amd_literals_op(int op, const uint8_t *in, size_t in_len, uint8_t *out, size_t cap) {
+  Literals l;
+  if ((in_len && !in) || !de_lits(in, in_len, &l.lits)) return RURE_AMD_ERR_ARG;
+  std::string o;
+  switch (op) {
+    case 0: ser_lits(l.unambiguous_prefixes().lits, &o); break;
+    case 1: o = l.longest_common_prefix(); break;
+    case 2: o = l.longest_common_suffix(); break;
+    case 3: ser_lits(l.unambiguous_suffixes().lits, &o); break;
+    default: return RURE_AMD_ERR_ARG;
+  }
+  return put_out(o, out, cap);
+}
+
+int rure_amd_match_info_get(rure *re, rure_amd_match_info *info) {
+  if (!re || !info) return RURE_AMD_ERR_ARG;
+  memset(info, 0, sizeof(*info));
+  const ExecLiterals &x = re->xl;
+  info->match_type = x.match_type;
+  info->prefix_matcher = x.prefixes.matcher;
+  info->suffix_matcher = x.suffixes.matcher;
+  info->prefix_len = (uint32_t)x.prefixes.len;
+  info->suffix_len = (uint32_t)x.suffixes.len;
+  info->prefix_complete = x.prefixes.complete ? 1 : 0;
+  info->suffix_complete = x.suffixes.complete ? 1 : 0;
+  info->lcp_chars = (uint32_t)x.prefixes.lcp_chars;
+  info->lcs_chars = (uint32_t)x.suffixes.lcs_chars;
+  info->lcs_bytes = (uint32_t)std::min<size_t>(x.suffixes.lcs.size(), sizeof(info->lcs));
+  memcpy(info->lcs, x.suffixes.lcs.data(), info->lcs_bytes);
+  return RURE_AMD_OK;
+}
+
+int64_t rure_amd_exec_literals_export(rure *re, int which, uint8_t *out, size_t cap) {
+  if (!re) return RURE_AMD_ERR_ARG;
+  std::string o;
+  ser_lits(which == 0 ? re->xl.prefixes.lits.lits : re->xl.suffixes.lits.lits, &o);
+  return put_out(o, out, cap);
+}
 
 int rure_amd_kernel_timer(int on) { return rure_amd::ktimer_set(on); }
 double rure_amd_kernel_timer_read(uint64_t *launches) { return rure_amd::ktimer_read(launches); }

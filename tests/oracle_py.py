@@ -32,6 +32,8 @@ orc_prog_new = _sig("orc_prog_new", VP, VP, ctypes.c_uint32, ctypes.c_uint32, VP
                     ctypes.c_int, ctypes.c_int, ctypes.c_uint32, SZ)
 orc_regex_new = _sig("orc_regex_new", VP, VP, VP, VP)
 orc_regex_free = _sig("orc_regex_free", None, VP)
+orc_regex_set_exec = _sig("orc_regex_set_exec", None, VP, ctypes.c_int, ctypes.c_char_p, SZ, ctypes.c_int,
+                          ctypes.c_char_p, SZ, ctypes.c_int, ctypes.c_char_p, SZ)
 orc_cache_new = _sig("orc_cache_new", VP, VP)
 orc_cache_free = _sig("orc_cache_free", None, VP)
 orc_find_at = _sig("orc_find_at", ctypes.c_int, VP, VP, ctypes.c_char_p, SZ, SZ, ctypes.POINTER(SZ),
@@ -67,7 +69,10 @@ def _prog(info_insts, dfa_size_limit=2 << 20):
 class OracleRegex(object):
     """Oracle over the programs of a regex_amd.Regex (or RegexSet)."""
 
-    def __init__(self, re_obj, dfa_size_limit=2 << 20):
+    def __init__(self, re_obj, dfa_size_limit=2 << 20, dispatch=True):
+        """dispatch: restate the reference's engine choice for a single regex
+        (exec.rs:1130-1210: Literal / DfaSuffix arms, with the literal sets
+        the product's host code computes); False: the DFA arms only."""
         self.is_set = hasattr(re_obj, "_set") and not hasattr(re_obj, "_re")
         if self.is_set:
             fwd = _prog(re_obj.program(0), dfa_size_limit)
@@ -83,6 +88,14 @@ class OracleRegex(object):
             nfa = _prog(re_obj.program(2), dfa_size_limit)
             self.ncaps = re_obj.program(2)[0].ncaptures
         self._r = orc_regex_new(nfa, fwd, rev)
+        if dispatch and not self.is_set:
+            import regex_amd as R
+            mi = re_obj.match_info()
+            pre = R._ser_lits(re_obj.exec_literals("prefixes"))
+            suf = R._ser_lits(re_obj.exec_literals("suffixes"))
+            self.match_type = R.MATCH_TYPES.index(mi["match_type"])
+            orc_regex_set_exec(self._r, self.match_type, pre, len(pre), mi["prefix_matcher"], suf, len(suf),
+                               mi["suffix_matcher"], mi["lcs"], len(mi["lcs"]))
         self._c = orc_cache_new(self._r)
 
     def __del__(self):
