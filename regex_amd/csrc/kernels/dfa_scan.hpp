@@ -92,6 +92,27 @@ constexpr uint32_t kLitBitmap2 = kLitBytes + kLitMax * kLitLen;  // second bitma
 constexpr uint32_t kLitImage = kLitBitmap2 + 8192;
 __host__ __device__ inline uint32_t lit_hash(uint32_t key) { return (key * 0x9E3779B1u) >> 16; }
 
+// The reference's engine choice where it differs from the forward DFA
+// (host/literal_sets.hpp): MatchType::Literal over the reference's literal
+// sets (exec.rs:601-625) and DfaSuffix (exec.rs:725-794).  Literal lists:
+// `n` literals, literal i = bytes[off[i] .. off[i + 1]), in the searcher's
+// iteration order; matcher 0 = Empty (literals.rs:92-96: every search finds
+// the empty string at its start).
+struct LitListDev {
+  const uint8_t *bytes;
+  const uint32_t *off;
+  uint32_t n;
+  int32_t matcher;
+};
+// mt: host/literal_sets.hpp MatchTypeCode (0-2 the Literal types, 5 DfaSuffix)
+enum { MT_LIT_UNANCHORED = 0, MT_LIT_ANCHORED_START = 1, MT_LIT_ANCHORED_END = 2 };
+struct MatchDev {
+  int32_t mt;             // MT_* code
+  LitListDev pre, suf;    // nfa.prefixes, suffixes
+  const uint8_t *lcs;     // suffixes.lcs() (DfaSuffix)
+  uint32_t lcs_len;
+};
+
 struct RevDfaDev {
   const uint8_t *lds_image;   // hot table (same layout as FwdDfaDev::lds_image)
   uint32_t lds_bytes;
@@ -210,7 +231,7 @@ struct IterSpan {
 };
 hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaDev &r, const NfaDev *nf,
                             bool chunked, uint64_t chunk, const IterOut &o, hipStream_t st, int cus,
-                            const IterSpan *span = nullptr);
+                            const IterSpan *span = nullptr, const MatchDev *mt = nullptr);
 // Several Shift-And regexes over one span in one speculative pass, then each
 // regex's own passes; hipErrorNotSupported (nothing launched) if they do not
 // qualify (iter_scan.hip).
@@ -224,6 +245,13 @@ hipError_t launch_long_scan(int mode, const BatchDev &b, const FwdDfaDev &f, con
 
 hipError_t launch_dfa_fwd(int mode, const BatchDev &b, const FwdDfaDev &f, const RevDfaDev &r, void *out,
                           hipStream_t st, int grid);
+// find / is_match / shortest_match of a batch under the reference's Literal
+// or DfaSuffix match type (match_types.hip): one lane per haystack, global
+// DFA tables for DfaSuffix's reverse / forward scans; same output layout and
+// quit markers as launch_dfa_fwd (the Pike VM pass resolves quits);
+// last_fwd_path() = -5.
+hipError_t launch_lane_search(int mode, const BatchDev &b, const MatchDev &m, const FwdDfaDev &f,
+                              const RevDfaDev &r, void *out, hipStream_t st, int cus);
 // MatchType::Literal (exec.rs:601-625, 1148-1166) for MODE_FIND / MODE_ISMATCH
 // batches of a regex that is a finite string set: f = the find_iter DFA
 // (lit_n > 0); same output layout as launch_dfa_fwd; last_fwd_path() = -3.
@@ -258,13 +286,15 @@ hipError_t launch_dfa_anchored_rev(int mode, const BatchDev &b, const RevDfaDev 
                                    int grid);
 hipError_t launch_dfa_set(const BatchDev &b, const SetDfaDev &f, uint64_t *out, hipStream_t st, int grid);
 
-// Scratch from the stream-ordered allocator, cached per (device, stream)
-// (rure_amd.cpp): a freed block goes back to its stream's cache instead of to
-// hipFreeAsync — which on this ROCm waits for the stream's queued work when it
-// returns a large block (1-2 ms host stalls, one per freed scratch: the C3
-// variant phase spent more host time freeing than the GPU spent scanning) —
-// and an allocation on the same stream reuses it (stream order makes that
-// safe).  Same signatures as hipMallocAsync / hipFreeAsync.
+// Scratch device memory for the scans, cached by the library (rure_amd.cpp):
+// a freed block is kept with an event recorded on the freeing stream and
+// reused, after a wait on that event, by the next allocation of at most twice
+// its size on any stream of the device — freeing to the driver (hipFree,
+// hipFreeAsync) waits for queued work: 1-2 ms host stalls, one per freed
+// scratch, made the C3 variant phase spend more host time freeing than the
+// GPU spent scanning.  The cache is bounded and released on request
+// (rure_amd_release_scratch).  Same signatures as hipMallocAsync /
+// hipFreeAsync (the memory is usable on any stream once the call returns).
 hipError_t scratch_malloc(void **p, size_t bytes, hipStream_t st);
 hipError_t scratch_free(void *p, hipStream_t st);
 

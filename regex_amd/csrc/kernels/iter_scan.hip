@@ -29,6 +29,7 @@
 #include <stdint.h>
 
 #include "dfa_device.hpp"
+#include "match_device.hpp"
 #include "nfa_device.hpp"
 
 namespace rure_amd {
@@ -1565,7 +1566,7 @@ template <bool EMIT>
 __global__ __launch_bounds__(64) void iter_wave_kernel(BatchDev b, FwdDfaDev f, RevDfaDev r, NfaDev nf, int has_dfa,
                                                        uint32_t *counts, const uint64_t *off, uint64_t *out,
                                                        uint64_t cap, uint8_t *scratch, const uint64_t *entry,
-                                                       uint64_t hi, uint64_t *exit) {
+                                                       uint64_t hi, uint64_t *exit, MatchDev m) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_mem[];
   uint8_t *mem = scratch ? scratch + (size_t)blockIdx.x * nfa_wave_bytes(nf.nleaves) : lds_mem;
   pike::Lists W;
@@ -1602,10 +1603,14 @@ __global__ __launch_bounds__(64) void iter_wave_kernel(BatchDev b, FwdDfaDev f, 
     while (p <= len && (!EMIT || n < cnt)) {
       uint64_t s = NONE, e = NONE;
       int k = 2;
-      if (has_dfa) {
+      if (has_dfa || m.mt >= 0) {
         uint64_t s0 = NONE, e0 = NONE;
         int k0 = 0;
-        if (lane == 0) k0 = dfa_find(fg, r, nullptr, nullptr, base, len, p, &s0, &e0);
+        // one search: the reference's Literal / DfaSuffix search (m.mt >= 0,
+        // match_device.hpp) or find_dfa_forward
+        if (lane == 0)
+          k0 = m.mt >= 0 ? mt_search<MODE_FIND>(m, fg, r, base, len, p, &s0, &e0)
+                         : dfa_find(fg, r, nullptr, nullptr, base, len, p, &s0, &e0);
         k = __shfl(k0, 0);
         s = __shfl(s0, 0);
         e = __shfl(e0, 0);
@@ -1980,7 +1985,7 @@ hipError_t launch_find_iter_multi(const BatchDev &b, int nre, const FwdDfaDev *c
 
 hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaDev &r, const NfaDev *nf,
                             bool chunked, uint64_t chunk, const IterOut &o, hipStream_t st, int cus,
-                            const IterSpan *spn) {
+                            const IterSpan *spn, const MatchDev *mtd) {
   const uint64_t hi = spn ? spn->hi : ~0ull;
   hipError_t e = hipSuccess;
   if (b.count == 0) {
@@ -2086,6 +2091,7 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
   const size_t lds = use_lds ? wb : 0;
   FwdDfaDev fz{};
   const FwdDfaDev &fa = f ? *f : fz;
+  const MatchDev md = mtd ? *mtd : MatchDev{-1, {}, {}, nullptr, 0};
   do {
     if (lds > 64 * 1024) {
       if ((e = hipFuncSetAttribute((const void *)iter_wave_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2098,12 +2104,12 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
     if ((e = hipMemsetAsync(counts + b.count, 0, 4, st)) != hipSuccess) break;
     hipLaunchKernelGGL(iter_wave_kernel<false>, dim3(grid), dim3(64), lds, st, b, fa, r, *nf, f ? 1 : 0, counts,
                        (const uint64_t *)nullptr, (uint64_t *)nullptr, (uint64_t)0, scr,
-                       spn ? spn->entry : (const uint64_t *)nullptr, hi, spn ? spn->exit : (uint64_t *)nullptr);
+                       spn ? spn->entry : (const uint64_t *)nullptr, hi, spn ? spn->exit : (uint64_t *)nullptr, md);
     if ((e = hipGetLastError()) != hipSuccess) break;
     if ((e = scan_counts(counts, off, b.count, st)) != hipSuccess) break;
     hipLaunchKernelGGL(iter_wave_kernel<true>, dim3(grid), dim3(64), lds, st, b, fa, r, *nf, f ? 1 : 0, counts,
                        (const uint64_t *)off, o.matches, o.cap, scr,
-                       spn ? spn->entry : (const uint64_t *)nullptr, hi, (uint64_t *)nullptr);
+                       spn ? spn->entry : (const uint64_t *)nullptr, hi, (uint64_t *)nullptr, md);
     if ((e = hipGetLastError()) != hipSuccess) break;
     hipLaunchKernelGGL(iter_counts_kernel, dim3(grid_cap(b.count, 256, cus, 4)), dim3(256), 0, st, b.count,
                        (uint64_t)1, off, o.counts, o.total);

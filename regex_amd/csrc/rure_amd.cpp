@@ -72,6 +72,13 @@ struct DevTables {
   bool has_dfa = false;     // the DFA materialised (else: Pike VM only)
   bool quit_possible = false;  // the DFA can quit (Unicode \b): Pike VM fallback pass
   bool anchored_rev = false;   // MatchType::DfaAnchoredReverse (exec.rs:1175-1177)
+  // The reference's match type where its searches differ from a forward DFA
+  // search (literal_sets.hpp): Literal(AnchoredStart), Literal(Unanchored)
+  // chosen from complete suffixes (its prefix searcher may be Empty or
+  // partial), DfaSuffix.  Those searches run match_types.hip / the wave
+  // iteration with `m`.
+  MatchDev m{-1, {}, {}, nullptr, 0};
+  bool mt_lane = false;
   int cus = 256;
 };
 
@@ -406,16 +413,19 @@ struct Blob {
 
 // ---------------------------------------------------------- scratch cache
 // See dfa_scan.hpp scratch_malloc.  Blocks are rounded up (4 KiB, then
-// 64 KiB multiples).  A freed block is cached per device with an event
-// recorded on the freeing stream; an allocation of at most half its size on
-// any stream of that device waits for that event (hipStreamWaitEvent) and
-// reuses it, so reuse is ordered after the previous user's kernels whatever
-// stream either used (a destroyed and recreated stream handle, the per-thread
-// default stream).  The cache holds at most max(kScratchMinCap, 2 x the peak
-// of live scratch bytes), at most kScratchMaxCap (RURE_AMD_SCRATCH_CAP
-// overrides, bytes); beyond that a free goes to hipFreeAsync.  Cached blocks
-// are returned by rure_amd_release_scratch(), when the last rure / rure_set
-// is freed, and before a retry when an allocation fails.
+// 64 KiB multiples) and come from hipMalloc.  A freed block is cached per
+// device with an event recorded on the freeing stream; an allocation of at
+// most half its size on any stream of that device waits for that event
+// (hipStreamWaitEvent) and reuses it, so reuse is ordered after the previous
+// user's kernels whatever stream either used (a destroyed and recreated
+// stream handle, the per-thread default stream).  The cache holds at most
+// max(kScratchMinCap, 2 x the peak of live scratch bytes), at most
+// kScratchMaxCap (RURE_AMD_SCRATCH_CAP overrides, bytes); a block freed
+// beyond that is returned to the driver once its event has completed.
+// Cached blocks go back to the driver on rure_amd_release_scratch(), when the
+// last rure / rure_set is freed, and before a retry when an allocation fails.
+// (The stream-ordered pool of hipMallocAsync kept freed memory mapped even
+// after hipMemPoolTrimTo on this ROCm: tools/scratch_diag.py.)
 constexpr size_t kScratchMinCap = 256ull << 20, kScratchMaxCap = 8ull << 30;
 struct ScratchBlock {
   size_t n;
@@ -437,27 +447,23 @@ size_t scratch_cap(const ScratchCache &c) {
   if (const char *v = getenv("RURE_AMD_SCRATCH_CAP")) return (size_t)strtoull(v, nullptr, 10);
   return std::min(kScratchMaxCap, std::max(kScratchMinCap, 2 * c.peak_live));
 }
-// Returns every cached block (caller holds c.mu).  The frees are ordered
-// after the block's last use through its event on the legacy default stream,
-// which every device has.
+// Returns a block to the driver after its last use.
+void scratch_release_block(void *p, const ScratchBlock &b) {
+  if (b.ev) {
+    (void)hipEventSynchronize(b.ev);
+    (void)hipEventDestroy(b.ev);
+  }
+  (void)hipFree(p);
+}
+// Returns every cached block (caller holds c.mu).
 void scratch_drop_all(ScratchCache &c) {
   int cur = 0;
   (void)hipGetDevice(&cur);
   for (auto &kv : c.free_blocks) {
     if (kv.second.empty()) continue;
     (void)hipSetDevice(kv.first);
-    for (auto &blk : kv.second) {
-      hipEvent_t ev = blk.second.second.ev;
-      if (ev) (void)hipStreamWaitEvent(nullptr, ev, 0);
-      (void)hipFreeAsync(blk.second.first, nullptr);
-      if (ev) (void)hipEventDestroy(ev);
-    }
+    for (auto &blk : kv.second) scratch_release_block(blk.second.first, blk.second.second);
     kv.second.clear();
-    // hand the freed blocks back to the driver, not only to the pool (the
-    // wait is for the blocks' last users, as hipFree of the tables waits)
-    hipMemPool_t pool;
-    if (hipStreamSynchronize(nullptr) == hipSuccess && hipDeviceGetDefaultMemPool(&pool, kv.first) == hipSuccess)
-      (void)hipMemPoolTrimTo(pool, 0);
   }
   (void)hipSetDevice(cur);
   c.cached = 0;
@@ -481,26 +487,22 @@ hipError_t rure_amd::scratch_malloc(void **p, size_t bytes, hipStream_t st) {
       ScratchBlock blk = b->second.second;
       fb.erase(b);
       c.cached -= blk.n;
-      if (blk.ev && (e = hipStreamWaitEvent(st, blk.ev, 0)) != hipSuccess) {
-        c.live[q] = blk;  // still owned: the caller's failure path frees it
-        return e;
-      }
       c.live[q] = blk;
       c.live_bytes += blk.n;
       c.peak_live = std::max(c.peak_live, c.live_bytes);
       *p = q;
-      return hipSuccess;
+      return blk.ev ? hipStreamWaitEvent(st, blk.ev, 0) : hipSuccess;
     }
   }
   void *q = nullptr;
-  e = hipMallocAsync(&q, n, st);
+  e = hipMalloc(&q, n);
   if (e == hipErrorOutOfMemory) {
     (void)hipGetLastError();
     {
       std::lock_guard<std::mutex> g(c.mu);
       scratch_drop_all(c);
     }
-    e = hipMallocAsync(&q, n, st);
+    e = hipMalloc(&q, n);
   }
   if (e != hipSuccess) return e;
   std::lock_guard<std::mutex> g(c.mu);
@@ -514,27 +516,25 @@ hipError_t rure_amd::scratch_malloc(void **p, size_t bytes, hipStream_t st) {
 hipError_t rure_amd::scratch_free(void *p, hipStream_t st) {
   if (!p) return hipSuccess;
   ScratchCache &c = scratch_cache();
+  ScratchBlock blk{0, 0, nullptr};
   {
     std::lock_guard<std::mutex> g(c.mu);
     auto it = c.live.find(p);
-    if (it != c.live.end()) {
-      ScratchBlock blk = it->second;
-      c.live.erase(it);
-      c.live_bytes -= blk.n;
-      if (c.cached + blk.n <= scratch_cap(c)) {
-        hipError_t e = hipSuccess;
-        if (!blk.ev) e = hipEventCreateWithFlags(&blk.ev, hipEventDisableTiming);
-        if (e == hipSuccess) e = hipEventRecord(blk.ev, st);
-        if (e == hipSuccess) {
-          c.free_blocks[blk.dev].emplace(blk.n, std::make_pair(p, blk));
-          c.cached += blk.n;
-          return hipSuccess;
-        }
-      }
-      if (blk.ev) (void)hipEventDestroy(blk.ev);
+    if (it == c.live.end()) return hipErrorInvalidValue;  // not a scratch block
+    blk = it->second;
+    c.live.erase(it);
+    c.live_bytes -= blk.n;
+    hipError_t e = hipSuccess;
+    if (!blk.ev) e = hipEventCreateWithFlags(&blk.ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(blk.ev, st);
+    if (e == hipSuccess && c.cached + blk.n <= scratch_cap(c)) {
+      c.free_blocks[blk.dev].emplace(blk.n, std::make_pair(p, blk));
+      c.cached += blk.n;
+      return hipSuccess;
     }
   }
-  return hipFreeAsync(p, st);
+  scratch_release_block(p, blk);
+  return hipSuccess;
 }
 
 namespace {
@@ -807,6 +807,30 @@ bool upload_blob(const Blob &b, DevTables *t, std::string *err) {
   return true;
 }
 
+// A literal list (bytes, n + 1 u32 offsets) into an upload blob.
+struct LitOffsets { size_t bytes, off; uint32_t n; };
+LitOffsets add_litlist(Blob &b, const Literals &l) {
+  std::string cat;
+  std::vector<uint32_t> off{0};
+  for (const Lit &x : l.lits) {
+    cat += x.v;
+    off.push_back((uint32_t)cat.size());
+  }
+  cat.resize(cat.size() + 16, 0);
+  LitOffsets o;
+  o.bytes = b.add(cat.data(), cat.size());
+  o.off = b.add(off.data(), off.size() * 4);
+  o.n = (uint32_t)l.lits.size();
+  return o;
+}
+
+// Whether the reference's match type makes this regex's searches differ from
+// a forward DFA search (DevTables::mt_lane).
+bool needs_mt_lane(const ExecLiterals &x) {
+  return x.match_type == MT_DFA_SUFFIX || x.match_type == MT_LITERAL_ANCHORED_START ||
+         (x.match_type == MT_LITERAL_UNANCHORED && !x.prefixes.complete);
+}
+
 // Upload (once per device) and return device descriptors.
 DevTables *regex_device(rure *re, std::string *err) {
   if (!build_regex(re)) { if (err) *err = re->dfa_err; return nullptr; }
@@ -838,9 +862,27 @@ DevTables *regex_device(rure *re, std::string *err) {
     o_rstart = b.add(rstart.data(), 256);
     o_rlds = b.add(re->pr.lds.data(), re->pr.lds.size());
   }
+  const bool mt_lane = needs_mt_lane(re->xl);
+  LitOffsets lp{}, ls{};
+  size_t o_lcs = 0;
+  if (mt_lane) {
+    lp = add_litlist(b, re->xl.prefixes.lits);
+    ls = add_litlist(b, re->xl.suffixes.lits);
+    std::string lcs = re->xl.suffixes.lcs;
+    lcs.resize(lcs.size() + 16, 0);
+    o_lcs = b.add(lcs.data(), lcs.size());
+  }
   if (!upload_blob(b, &t, err)) return nullptr;
   uint8_t *base = (uint8_t *)t.blob;
   if (re->nfa_ok) fix_nfa(&t.n, base, no, re->nt, true);
+  if (mt_lane) {
+    t.mt_lane = true;
+    t.m.mt = re->xl.match_type;
+    t.m.pre = LitListDev{base + lp.bytes, (const uint32_t *)(base + lp.off), lp.n, re->xl.prefixes.matcher};
+    t.m.suf = LitListDev{base + ls.bytes, (const uint32_t *)(base + ls.off), ls.n, re->xl.suffixes.matcher};
+    t.m.lcs = base + o_lcs;
+    t.m.lcs_len = (uint32_t)re->xl.suffixes.lcs.size();
+  }
   if (re->dfa_ok) {
     const DenseDfa &fw = re->dfwd;
     t.has_dfa = true;
@@ -1313,8 +1355,28 @@ hipError_t run_dfa_step(int mode, const BatchDev &b, const DevTables &t, void *o
   return launch_dfa_fwd(mode, b, t.f, t.r, out, st, dfa_grid);
 }
 
+// The Literal / DfaSuffix match types (DevTables::mt_lane): literal searches
+// need no DFA; DfaSuffix steps the DFA tables (without them the reference's
+// DFA would have quit too: the Pike VM answers).
+bool lane_search_ok(const DevTables &t) { return t.mt_lane && (t.m.mt != MT_DFA_SUFFIX || t.has_dfa); }
+
+hipError_t run_lane_search(int mode, const BatchDev &b, const DevTables &t, void *out, hipStream_t st) {
+  if (!t.quit_possible || t.m.mt != MT_DFA_SUFFIX) return launch_lane_search(mode, b, t.m, t.f, t.r, out, st, t.cus);
+  BatchDev bq = b;  // quit flag: see run_regex
+  hipError_t e = scratch_malloc((void **)&bq.quit_flag, 4, st);
+  if (e == hipSuccess) e = hipMemsetAsync(bq.quit_flag, 0, 4, st);
+  if (e == hipSuccess) e = launch_lane_search(mode, bq, t.m, t.f, t.r, out, st, t.cus);
+  if (e == hipSuccess) e = run_pike(mode, true, bq, t, out, st);
+  if (bq.quit_flag) {
+    hipError_t e2 = scratch_free(bq.quit_flag, st);
+    if (e == hipSuccess) e = e2;
+  }
+  return e;
+}
+
 hipError_t run_regex(int mode, const BatchDev &b, const DevTables &t, void *out, hipStream_t st, int dfa_grid,
                      const FwdDfaDev *iter = nullptr) {
+  if (lane_search_ok(t)) return run_lane_search(mode, b, t, out, st);
   if (!t.has_dfa) return run_pike(mode, false, b, t, out, st);
   uint64_t chunk = 0;
   if (iter && long_batch(mode, b, t, &chunk) && !(t.anchored_rev && b.start != 0))
@@ -1423,8 +1485,9 @@ hipError_t run_captures(const BatchDev &b, const DevTables &t, uint64_t *slots, 
   uint64_t *found = nullptr;
   if (!t.n.anchored) {
     if ((e = scratch_malloc((void **)&found, b.count * 16, st)) != hipSuccess) return e;
-    e = t.has_dfa ? run_dfa_step(MODE_FIND, b, t, found, st, dfa_grid, nullptr)
-                  : run_pike(MODE_FIND, false, b, t, found, st);
+    e = lane_search_ok(t) ? launch_lane_search(MODE_FIND, b, t.m, t.f, t.r, found, st, t.cus)
+        : t.has_dfa       ? run_dfa_step(MODE_FIND, b, t, found, st, dfa_grid, nullptr)
+                          : run_pike(MODE_FIND, false, b, t, found, st);
   }
   const size_t wb = caps_wave_bytes(t.n.nleaves, ns);
   const bool in_lds = wb <= kNfaLdsMax;
@@ -1888,6 +1951,7 @@ static const FwdDfaDev *literal_engine(int mode, rure *re, DevTables &t, const B
   uint64_t chunk;
   const char *env = getenv("RURE_AMD_LIT");
   if (env && env[0] != '1') return nullptr;
+  if (t.mt_lane) return nullptr;  // the reference's literal searcher differs from the regex's strings
   if (!env && long_batch(mode, b, t, &chunk)) return nullptr;  // RURE_AMD_LIT=1 forces the literal engine
   {
     // the literal set alone (cheap) before any find_iter DFA is built
@@ -2050,6 +2114,11 @@ hipError_t run_find_iter(rure *re, DevTables *t, const BatchDev &b, const IterOu
     hipError_t e2 = scratch_free(found, st);
     return e != hipSuccess ? e : e2;
   }
+  // The reference's Literal / DfaSuffix searches (DevTables::mt_lane): every
+  // search of the iteration is one of those, on a wave per haystack (lane 0
+  // searches, the wave runs the Pike VM where a DfaSuffix scan quits).
+  if (lane_search_ok(*t) && re->nfa_ok)
+    return launch_find_iter(b, t->has_dfa ? &t->f : nullptr, t->r, &t->n, false, 0, o, st, t->cus, sp, &t->m);
   // Chunked speculative iteration needs a DFA that cannot quit and a pattern
   // without assertions (see iter_scan.hip); otherwise one wave per haystack.
   const FwdDfaDev *fi = nullptr;
