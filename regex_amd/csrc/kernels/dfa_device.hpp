@@ -221,6 +221,22 @@ __device__ __forceinline__ uint64_t rev_scan(const RevDfaDev &r, const uint8_t *
   return rs;
 }
 
+// Whether the 128 bytes of v hold one of the prefix first bytes (pfx_rep).
+__device__ __forceinline__ uint32_t has_byte(uint32_t w, uint32_t rep) {
+  const uint32_t x = w ^ rep;
+  return (x - 0x01010101u) & ~x & 0x80808080u;
+}
+__device__ __forceinline__ bool prefix_hit(const FwdDfaDev &f, const uint4 *v) {
+  uint32_t acc = 0;
+  for (uint32_t i = 0; i < f.pfx_n; ++i) {
+    const uint32_t rep = f.pfx_rep[i];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      acc |= has_byte(v[k].x, rep) | has_byte(v[k].y, rep) | has_byte(v[k].z, rep) | has_byte(v[k].w, rep);
+  }
+  return acc != 0;
+}
+
 // One lane's forward scan of text[at..end) (dfa.rs:576-764): 16-byte
 // chunks through the LDS fast table, 128-byte bursts per lane.  No EOF step.
 template <int MODE>
@@ -242,6 +258,18 @@ __device__ __forceinline__ void fwd_range(LaneState &L, const FwdDfaDev &f, cons
     uint4 v[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = p[k];
+    if (f.pfx_n && L.s + 1 == f.ustart1) {
+      // start-state prefix skip (dfa.rs:700-711): bursts without a prefix
+      // first byte cannot start a match, and the state stays the start state
+      while (!prefix_hit(f, v)) {
+        at += 128;
+        if (at + 128 > end) break;
+        p = (const uint4 *)(base + at);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = p[k];
+      }
+      if (at + 128 > end) break;
+    }
 #pragma unroll
     for (int k = 0; k < 8; ++k)
       if (!L.done) chunk16<MODE>(L, f, lds, v[k], at + 16 * k);

@@ -82,6 +82,14 @@ struct FwdDfaDev {
   // match ended at it (EMIT), 3 = EMIT only.
   const uint8_t *lex_image;
   uint32_t lex_bytes, lex_s0;
+  // The start-state prefix skip (dfa.rs:700-711, 1504-1506 prefix_at): when
+  // the regex has prefix literals (literal_sets.hpp, dfa.prefixes) whose
+  // first bytes are at most 4 (pfx_rep[i] = byte * 0x01010101), every match
+  // starts with one of them, so a scan in the start state (ustart1 - 1: the
+  // start does not depend on look-behind) jumps over the 128-byte bursts
+  // that hold none of those bytes (fwd_range); pfx_n = 0: off.
+  uint32_t pfx_n;
+  uint32_t pfx_rep[4];
 };
 constexpr uint32_t kLexMaxRows = 24;  // lexer table rows (iter_spec_lex_tile_kernel's static LDS)
 
@@ -232,11 +240,25 @@ struct IterSpan {
 hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaDev &r, const NfaDev *nf,
                             bool chunked, uint64_t chunk, const IterOut &o, hipStream_t st, int cus,
                             const IterSpan *span = nullptr, const MatchDev *mt = nullptr);
+// The k-mer probe engine of launch_find_iter_multi: the regexes' strings all
+// have one length len <= 8 over an alphabet of at most 4 bytes whose codes
+// (b >> shift) & 3 are distinct.  bitmap: 2048 u32, bit c set iff the L-mer
+// with code c (2 bits per byte, first byte lowest) is a string of some regex;
+// mask: 4^len u16, regex q's bit set iff its strings hold it; lut / present:
+// the byte of each code (verification of probe hits on the text).
+struct KmerDev {
+  const uint32_t *bitmap;
+  const uint16_t *mask;
+  uint32_t shift, lut, present, cmask;
+  uint64_t len;
+};
 // Several Shift-And regexes over one span in one speculative pass, then each
 // regex's own passes; hipErrorNotSupported (nothing launched) if they do not
-// qualify (iter_scan.hip).
+// qualify (iter_scan.hip).  km (may be null): the k-mer probe engine for the
+// pass instead of the Shift-And words.
 hipError_t launch_find_iter_multi(const BatchDev &b, int nre, const FwdDfaDev *const *f, const RevDfaDev *const *r,
-                                  uint64_t chunk, const IterOut *o, hipStream_t st, int cus, const IterSpan *spn);
+                                  uint64_t chunk, const IterOut *o, hipStream_t st, int cus, const IterSpan *spn,
+                                  const KmerDev *km = nullptr);
 
 // One search per haystack over few long fixed-stride haystacks, chunked
 // (iter_scan.hip); f must be the find_iter DFA (with strip).

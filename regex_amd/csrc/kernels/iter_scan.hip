@@ -766,6 +766,8 @@ struct SaMulti {
   uint64_t *slots[kSaMultiMax];
   uint32_t *counts[kSaMultiMax];
   uint32_t *dirty[kSaMultiMax];
+  KmerDev km;                         // k-mer probe engine (km.bitmap != nullptr)
+  uint32_t pbits;                     // per-regex state: search position bits (multi_record)
 };
 
 // LDS rows of NWP = 4 or 8 words (16-byte reads)
@@ -787,11 +789,25 @@ __global__ void sa_multi_image_kernel(SaMulti m) {
   for (int x = 0; x < SamPitch<NW>::v; ++x) m.image[c * SamPitch<NW>::v + x] = x < NW ? wv[x] : 0u;
 }
 
-// sa_block for every regex of the pass: the bits of 16 bytes (k0..kend) and,
-// in the rare block holding string ends, each regex's greedy iteration.  The
-// iteration state is kept relative to the unit start (p, lm: u32 offsets;
-// kNoLm = none) to spare registers.
-constexpr uint32_t kNoLm = 0xFFFFFFFFu;
+// Each regex's greedy iteration state in the fused pass, one u32 per regex
+// and lane (registers bound the kernel's occupancy): the end of its last
+// match relative to the unit start (its next search starts there) in the low
+// m.pbits bits, its match count above (the host checks both fit).  The last
+// match end equals the search position once a match was seen (nonempty
+// strings), so it needs no register of its own.
+template <int MQ>
+__device__ __forceinline__ void multi_record(const SaMulti &m, uint32_t (&pn)[MQ], int q, uint64_t st, uint64_t e,
+                                             uint64_t c0, uint64_t c1, uint64_t u, uint32_t nslots) {
+  const uint32_t pmask = (1u << m.pbits) - 1u;
+  const uint32_t pq = pn[q] & pmask, nq = pn[q] >> m.pbits;
+  if (st >= c0 + pq && st < c1) {
+    if (nq < nslots) *(ulonglong2 *)&m.slots[q][(u * nslots + nq) * 2] = make_ulonglong2(st, e);
+    pn[q] = (uint32_t)(e - c0) | ((nq + 1) << m.pbits);
+  }
+}
+
+// sam_block for every regex of the pass: the bits of 16 bytes (k0..kend) and,
+// in the rare block holding string ends, each regex's greedy iteration.
 template <int NW>
 __device__ __forceinline__ void sam_row(const uint32_t *B, uint32_t c, uint32_t (&row)[NW]) {
   const uint4 *r = (const uint4 *)(B + c * SamPitch<NW>::v);
@@ -803,11 +819,10 @@ __device__ __forceinline__ void sam_row(const uint32_t *B, uint32_t c, uint32_t 
   for (int x = 0; x < NW; ++x) row[x] = u[x];
 }
 
-template <int NW>
+template <int NW, int MQ>
 __device__ __forceinline__ void sam_block(uint32_t (&D)[NW], const uint32_t *B, const SaMulti &m, const uint32_t w[4],
                                           uint32_t k0, uint32_t kend, int64_t bp, uint64_t c0, uint64_t c1,
-                                          uint32_t (&p)[kSaMultiMax], uint32_t (&lm)[kSaMultiMax],
-                                          uint32_t (&n)[kSaMultiMax], uint64_t u, uint32_t nslots) {
+                                          uint32_t (&pn)[MQ], uint64_t u, uint32_t nslots) {
   uint32_t D0[NW];
 #pragma unroll
   for (int x = 0; x < NW; ++x) D0[x] = D[x];
@@ -843,16 +858,12 @@ __device__ __forceinline__ void sam_block(uint32_t (&D)[NW], const uint32_t *B, 
       const uint32_t j = __builtin_ctz(fm);
       const uint64_t e = (uint64_t)bp + j + 1, st = e - m.len;
 #pragma unroll
-      for (int q = 0; q < kSaMultiMax; ++q) {
+      for (int q = 0; q < MQ; ++q) {
         if ((uint32_t)q >= m.nre) break;
         uint32_t ew = Dm[0];
 #pragma unroll
         for (int x = 1; x < NW; ++x) ew = m.word[q] == (uint32_t)x ? Dm[x] : ew;
-        if ((ew & m.fin[q]) && st >= c0 + p[q] && st < c1) {
-          if (n[q] < nslots) *(ulonglong2 *)&m.slots[q][(u * nslots + n[q]) * 2] = make_ulonglong2(st, e);
-          ++n[q];
-          p[q] = lm[q] = (uint32_t)(e - c0);
-        }
+        if (ew & m.fin[q]) multi_record<MQ>(m, pn, q, st, e, c0, c1, u, nslots);
       }
       return;
     }
@@ -889,65 +900,131 @@ __device__ __forceinline__ void sam_block(uint32_t (&D)[NW], const uint32_t *B, 
     if (!any) continue;
     const uint64_t e = (uint64_t)bp + j + 1, st = e - m.len;
 #pragma unroll
-    for (int q = 0; q < kSaMultiMax; ++q) {
+    for (int q = 0; q < MQ; ++q) {
       if ((uint32_t)q >= m.nre) break;
       uint32_t ew = E[0];
 #pragma unroll
       for (int x = 1; x < NW; ++x) ew = m.word[q] == (uint32_t)x ? E[x] : ew;
-      if ((ew & m.fin[q]) && st >= c0 + p[q] && st < c1) {
-        if (n[q] < nslots) *(ulonglong2 *)&m.slots[q][(u * nslots + n[q]) * 2] = make_ulonglong2(st, e);
-        ++n[q];
-        p[q] = lm[q] = (uint32_t)(e - c0);
-      }
+      if (ew & m.fin[q]) multi_record<MQ>(m, pn, q, st, e, c0, c1, u, nslots);
     }
   }
 }
 
-template <int NW>
-__global__ __launch_bounds__(256) void iter_spec_sa_multi_tile_kernel(BatchDev b, Geo g, uint64_t nunits, SaMulti m) {
-  __shared__ __attribute__((aligned(16))) uint32_t B[256 * SamPitch<NW>::v];
+// The k-mer probe engine's block step (KmerDev): the 2-bit codes of the 16
+// bytes (code(b) = (b >> shift) & 3, four bytes per VALU op) join the
+// previous block's in a 64-bit window register; the L-mer ending at each
+// byte is one independent probe of the LDS bitmap of the strings' codes (no
+// dependent chain).  Probe hits (rare: ~1 per 2 KiB on the regex-dna stream)
+// are verified on the text bytes (exact whatever the input: a byte outside
+// the alphabet fails) and the code's regex mask drives each regex's greedy
+// iteration exactly as sam_block does.  Rp: the previous block's codes
+// (garbage before a unit's first block: the windows reaching into it start
+// before the unit and are not the unit's).
+template <int MQ>
+__device__ __forceinline__ void kmer_block(uint32_t &Rp, const uint32_t *B, const SaMulti &m, const uint32_t w[4],
+                                           uint32_t k0, uint32_t kend, int64_t bp, uint64_t c0, uint64_t c1,
+                                           uint32_t (&pn)[MQ], uint64_t u, uint32_t nslots, const uint8_t *base) {
+  const KmerDev &km = m.km;
+  uint32_t cw = 0;
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+    uint32_t c4 = (w[x] >> km.shift) & 0x03030303u;
+    c4 = (c4 | (c4 >> 6)) & 0x000F000Fu;
+    c4 = (c4 | (c4 >> 12)) & 0xFFu;
+    cw |= c4 << (8 * x);
+  }
+  const uint32_t L = (uint32_t)m.len, cmask = km.cmask;
+  uint32_t cm = 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    // codes of bytes j - L + 1 .. j: bits [2 (16 + j - L + 1), ...) of cw:Rp
+    const uint32_t sh = 2 * (17 + j - L);
+    const uint32_t code = (sh >= 32 ? (cw >> (sh - 32)) : __builtin_amdgcn_alignbit(cw, Rp, sh)) & cmask;
+    cm |= ((B[code >> 5] >> (code & 31)) & 1u) << j;
+  }
+  Rp = cw;
+  cm &= ((kend >= 32 ? 0u : (1u << kend)) - 1u) & ~((1u << k0) - 1u);
+  if (!cm) return;
+#pragma unroll 1
+  while (cm) {
+    const uint32_t j = __builtin_ctz(cm);
+    cm &= cm - 1;
+    const uint64_t e = (uint64_t)bp + j + 1, st = e - L;
+    if ((int64_t)e < (int64_t)L || st < c0) continue;  // starts before the unit: not its match
+    uint32_t code = 0;
+    bool ok = true;
+    for (uint32_t i = 0; i < L; ++i) {
+      const uint32_t bb = base[st + i], c = (bb >> km.shift) & 3u;
+      ok = ok && ((km.present >> c) & 1u) && ((km.lut >> (8 * c)) & 0xFFu) == bb;
+      code |= c << (2 * i);
+    }
+    if (!ok) continue;
+    const uint32_t mask = km.mask[code];
+#pragma unroll
+    for (int q = 0; q < MQ; ++q) {
+      if ((uint32_t)q >= m.nre) break;
+      if ((mask >> q) & 1u) multi_record<MQ>(m, pn, q, st, e, c0, c1, u, nslots);
+    }
+  }
+}
+
+// One regex-set step of a block for the tile kernel below: the Shift-And
+// words (KMER = false) or the k-mer probes (KMER = true; D[0] holds Rp).
+template <int NW, bool KMER, int MQ>
+__device__ __forceinline__ void multi_block(uint32_t (&D)[NW], const uint32_t *B, const SaMulti &m,
+                                            const uint32_t w[4], uint32_t k0, uint32_t kend, int64_t bp, uint64_t c0,
+                                            uint64_t c1, uint32_t (&pn)[MQ], uint64_t u, uint32_t nslots,
+                                            const uint8_t *base) {
+  if (KMER) kmer_block<MQ>(D[0], B, m, w, k0, kend, bp, c0, c1, pn, u, nslots, base);
+  else sam_block<NW, MQ>(D, B, m, w, k0, kend, bp, c0, c1, pn, u, nslots);
+}
+
+// The fused speculative pass over ONE haystack span (b.count == 1): the
+// coalesced tile layout of iter_spec_sa_tile_kernel (a wave owns 64
+// consecutive units; each load covers 8 units x one 128-byte line, staged
+// through a swizzled LDS buffer), each lane running every regex of the pass
+// over its unit.  MQ >= m.nre bounds the per-regex state arrays.
+template <int NW, bool KMER, int MQ>
+__device__ __forceinline__ void multi_tile_body(const BatchDev &b, const Geo &g, uint64_t nunits, const SaMulti &m) {
+  __shared__ __attribute__((aligned(16))) uint32_t B[KMER ? 2048 : 256 * SamPitch<NW>::v];
   __shared__ __attribute__((aligned(16))) uint4 stage[4][64 * 8];
-  for (uint32_t i = threadIdx.x; i < 256 * SamPitch<NW>::v; i += blockDim.x) B[i] = m.image[i];
+  if (KMER) {
+    for (uint32_t i = threadIdx.x; i < 2048; i += blockDim.x) B[i] = m.km.bitmap[i];
+  } else {
+    for (uint32_t i = threadIdx.x; i < 256 * SamPitch<NW>::v; i += blockDim.x) B[i] = m.image[i];
+  }
   __syncthreads();
   const uint64_t L = m.len, C = g.chunk, nk = g.nk;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   uint4 *buf = stage[w];
   const int src_h = lane >> 3, src_seg = lane & 7, sw = (lane >> 1) & 7;
   const uint64_t ngroups = (nunits + 63) / 64, nwaves = (uint64_t)gridDim.x * 4;
-  const bool single = b.count == 1;
-  auto hk = [&](uint64_t uu, uint64_t &h, uint64_t &k) {
-    if (single) { h = 0; k = uu; } else { h = uu / nk; k = uu - h * nk; }
-  };
+  const uint8_t *const base = b.hay;  // one haystack
+  const uint64_t len = b.length;
   for (uint64_t gi = (uint64_t)blockIdx.x * 4 + w; gi < ngroups; gi += nwaves) {
-    const uint64_t u = gi * 64 + lane;
-    uint64_t h, k;
-    hk(u, h, k);
+    const uint64_t u = gi * 64 + lane, k = u;
     const bool valid = u < nunits;
     const bool full = valid && k + 1 < nk;
-    const uint8_t *src[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      uint64_t us = gi * 64 + 8 * j + src_h, hs, ks;
-      hk(us, hs, ks);
-      if (us >= nunits || ks + 1 >= nk) hs = ks = 0;  // absent / ragged units re-read unit 0 (full)
-      src[j] = b.hay + hs * b.stride + b.start + ks * C + 16 * src_seg;
-    }
-    const uint8_t *base = b.hay + h * b.stride;
-    const uint64_t len = b.length, c0 = b.start + k * C;
+    // tile sources: load j covers units gi*64 + 8 j + src_h (absent / ragged
+    // units re-read unit 0, which is full), addresses formed per load
+    const uint64_t us0 = gi * 64 + src_h;
+    const uint8_t *const src0 = base + b.start + 16 * src_seg;
+    const uint64_t c0 = b.start + k * C;
     const uint64_t c1 = k + 1 == nk ? g.end : c0 + C;
-    uint32_t p[kSaMultiMax], lm[kSaMultiMax], n[kSaMultiMax];
+    uint32_t pn[MQ];
 #pragma unroll
-    for (int q = 0; q < kSaMultiMax; ++q) { p[q] = 0; lm[q] = kNoLm; n[q] = 0; }
+    for (int q = 0; q < MQ; ++q) pn[q] = 0;
     uint32_t D[NW];
 #pragma unroll
     for (int x = 0; x < NW; ++x) D[x] = 0;
     uint4 first = make_uint4(0, 0, 0, 0);
     uint4 n0, n1, n2, n3, n4, n5, n6, n7;
+#define RURE_SRC(j, a) (src0 + ((us0 + 8 * (j) + 1 < nk) ? (us0 + 8 * (j)) * C : 0) + (a))
 #define RURE_LOAD_TILE(a)                                                                                     \
-  n0 = *(const uint4 *)(src[0] + (a)); n1 = *(const uint4 *)(src[1] + (a));                                  \
-  n2 = *(const uint4 *)(src[2] + (a)); n3 = *(const uint4 *)(src[3] + (a));                                  \
-  n4 = *(const uint4 *)(src[4] + (a)); n5 = *(const uint4 *)(src[5] + (a));                                  \
-  n6 = *(const uint4 *)(src[6] + (a)); n7 = *(const uint4 *)(src[7] + (a));
+  n0 = *(const uint4 *)RURE_SRC(0, a); n1 = *(const uint4 *)RURE_SRC(1, a);                                  \
+  n2 = *(const uint4 *)RURE_SRC(2, a); n3 = *(const uint4 *)RURE_SRC(3, a);                                  \
+  n4 = *(const uint4 *)RURE_SRC(4, a); n5 = *(const uint4 *)RURE_SRC(5, a);                                  \
+  n6 = *(const uint4 *)RURE_SRC(6, a); n7 = *(const uint4 *)RURE_SRC(7, a);
 #define RURE_STAGE(kk, v) buf[(8 * (kk) + src_h) * 8 + (src_seg ^ (((8 * (kk) + src_h) >> 1) & 7))] = (v);
     RURE_LOAD_TILE(0)
     for (uint64_t at = 0; at < C; at += 128) {
@@ -965,7 +1042,7 @@ __global__ __launch_bounds__(256) void iter_spec_sa_multi_tile_kernel(BatchDev b
         for (int mm = 0; mm < 8; ++mm) {
           const uint4 nx = buf[lane * 8 + ((mm + 1 < 8 ? mm + 1 : 7) ^ sw)];
           const uint32_t wd[4] = {cur.x, cur.y, cur.z, cur.w};
-          sam_block<NW>(D, B, m, wd, 0, 16, (int64_t)(c0 + at + 16 * mm), c0, c1, p, lm, n, u, g.slots);
+          multi_block<NW, KMER, MQ>(D, B, m, wd, 0, 16, (int64_t)(c0 + at + 16 * mm), c0, c1, pn, u, g.slots, base);
           cur = nx;
         }
       }
@@ -975,6 +1052,7 @@ __global__ __launch_bounds__(256) void iter_spec_sa_multi_tile_kernel(BatchDev b
     }
 #undef RURE_LOAD_TILE
 #undef RURE_STAGE
+#undef RURE_SRC
     uint4 nxt;
     nxt.x = __shfl_down(first.x, 1);
     nxt.y = __shfl_down(first.y, 1);
@@ -988,14 +1066,14 @@ __global__ __launch_bounds__(256) void iter_spec_sa_multi_tile_kernel(BatchDev b
       if (q < qend && lane < 63 && k + 2 < nk) {  // the next unit is full: lane + 1 holds its first block
         const uint32_t wd[4] = {nxt.x, nxt.y, nxt.z, nxt.w};
         const uint32_t kend = qend - q < 16 ? (uint32_t)(qend - q) : 16;
-        sam_block<NW>(D, B, m, wd, 0, kend, (int64_t)q, c0, c1, p, lm, n, u, g.slots);
+        multi_block<NW, KMER, MQ>(D, B, m, wd, 0, kend, (int64_t)q, c0, c1, pn, u, g.slots, base);
         q += 16;
       }
       for (; q < qend; q += 16) {  // from memory (aligned: c1 is)
         const uint4 v = *(const uint4 *)(base + q);
         const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
         const uint32_t kend = qend - q < 16 ? (uint32_t)(qend - q) : 16;
-        sam_block<NW>(D, B, m, wd, 0, kend, (int64_t)q, c0, c1, p, lm, n, u, g.slots);
+        multi_block<NW, KMER, MQ>(D, B, m, wd, 0, kend, (int64_t)q, c0, c1, pn, u, g.slots, base);
       }
     } else {
       // ragged last unit of its haystack: the per-lane loop
@@ -1006,23 +1084,25 @@ __global__ __launch_bounds__(256) void iter_spec_sa_multi_tile_kernel(BatchDev b
         const int64_t bp = (int64_t)(a - (uintptr_t)base);
         const uint32_t k0 = bp < (int64_t)c0 ? (uint32_t)((int64_t)c0 - bp) : 0;
         const uint32_t kend = (int64_t)qend - bp < 16 ? (uint32_t)((int64_t)qend - bp) : 16;
-        sam_block<NW>(D, B, m, wd, k0, kend, bp, c0, c1, p, lm, n, u, g.slots);
+        multi_block<NW, KMER, MQ>(D, B, m, wd, k0, kend, bp, c0, c1, pn, u, g.slots, base);
       }
     }
+    const uint32_t pmask = (1u << m.pbits) - 1u;
 #pragma unroll
-    for (int q = 0; q < kSaMultiMax; ++q) {
+    for (int q = 0; q < MQ; ++q) {
       if ((uint32_t)q >= m.nre) break;
-      const uint64_t pq = c0 + p[q], lq = lm[q] == kNoLm ? NONE : c0 + lm[q];
+      const uint32_t nq = pn[q] >> m.pbits;
+      const uint64_t pq = c0 + (pn[q] & pmask), lq = nq ? pq : NONE;
       Unit U;
       U.entry = {c0, NONE};
       U.exit = {pq, lq};
       U.spec_exit = U.exit;
-      U.spec_count = n[q];
+      U.spec_count = nq;
       const bool clean = pq < c1 || (pq == c1 && (lq != c1 || m.nonempty[q]));
       U.flags = clean ? (U_SPEC_CLEAN | U_CLEAN) : 0;
       U.skip = U.pad = 0;
       m.units[q][u] = U;
-      m.counts[q][u] = n[q];
+      m.counts[q][u] = nq;
       if (!clean) atomicOr(m.dirty[q], 1u);  // the fix pass has work
     }
   }
@@ -1373,12 +1453,11 @@ __device__ bool repair_unit(const BatchDev &b, const Geo &g, const FwdDfaDev &f,
 // parallel; repairs that change their own exit are queued for the walker.
 // Dirty exits are rare, so a block stages the hot tables into LDS only when
 // one of its units needs a repair.
-__global__ __launch_bounds__(1024) void iter_fix_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
-                                                       Unit *units, uint32_t *counts, const uint64_t *slots,
-                                                       uint64_t *queue, unsigned long long *qlen,
-                                                       const uint32_t *dirty) {
+__device__ __forceinline__ void fix_body(const BatchDev &b, const Geo &g, uint64_t nunits, const FwdDfaDev &f,
+                                         const RevDfaDev &r, Unit *units, uint32_t *counts, const uint64_t *slots,
+                                         uint64_t *queue, unsigned long long *qlen, const uint32_t *dirty,
+                                         uint8_t *lds) {
   if (*dirty == 0) return;  // every speculative exit was clean
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const uint8_t *rlds = nullptr;
   bool staged = false;
   for (uint64_t u0 = (uint64_t)blockIdx.x * blockDim.x; u0 + 1 < nunits; u0 += (uint64_t)gridDim.x * blockDim.x) {
@@ -1396,10 +1475,18 @@ __global__ __launch_bounds__(1024) void iter_fix_kernel(BatchDev b, Geo g, uint6
   }
 }
 
+__global__ __launch_bounds__(1024) void iter_fix_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
+                                                       Unit *units, uint32_t *counts, const uint64_t *slots,
+                                                       uint64_t *queue, unsigned long long *qlen,
+                                                       const uint32_t *dirty) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  fix_body(b, g, nunits, f, r, units, counts, slots, queue, qlen, dirty, lds);
+}
+
 // Pass 3 (one thread): propagate exits that changed, in unit order.
-__global__ void iter_walk_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r, Unit *units,
-                                 uint32_t *counts, const uint64_t *slots, uint64_t *queue, unsigned long long *qlen) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+__device__ __forceinline__ void walk_body(const BatchDev &b, const Geo &g, uint64_t nunits, const FwdDfaDev &f,
+                                          const RevDfaDev &r, Unit *units, uint32_t *counts, const uint64_t *slots,
+                                          uint64_t *queue, unsigned long long *qlen) {
   const uint64_t n = *qlen;
   if (n == 0) return;
   for (uint64_t i = 1; i < n; ++i) {  // insertion sort (the queue is short)
@@ -1440,6 +1527,12 @@ __global__ void iter_walk_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f
   }
 }
 
+__global__ void iter_walk_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r, Unit *units,
+                                 uint32_t *counts, const uint64_t *slots, uint64_t *queue, unsigned long long *qlen) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  walk_body(b, g, nunits, f, r, units, counts, slots, queue, qlen);
+}
+
 // Span entry (sharded / streamed find_iter): the first unit is entered with
 // the iteration state the previous span left.  Runs after the speculative
 // pass and before the parallel repairs, which read only the speculative
@@ -1460,15 +1553,19 @@ __global__ void iter_entry_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev 
 // A span that runs to the end of the text (`tail` = its length) iterated
 // without a cut; "fresh" then means equivalent to a fresh start at the text
 // end, where only an empty match at the end could differ.
-__global__ void iter_exit_kernel(const Unit *units, uint64_t nunits, uint64_t *exit, uint64_t tail,
-                                 uint32_t nonempty) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+__device__ __forceinline__ void exit_body(const Unit *units, uint64_t nunits, uint64_t *exit, uint64_t tail,
+                                          uint32_t nonempty) {
   const Unit U = units[nunits - 1];
   bool fresh = (U.flags & U_CLEAN) != 0;
   if (tail != ~0ull && U.exit.p >= tail) fresh = U.exit.p == tail && (U.exit.lm != tail || nonempty);
   exit[0] = U.exit.p;
   exit[1] = U.exit.lm;
   exit[2] = fresh ? 1 : 0;
+}
+__global__ void iter_exit_kernel(const Unit *units, uint64_t nunits, uint64_t *exit, uint64_t tail,
+                                 uint32_t nonempty) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  exit_body(units, nunits, exit, tail, nonempty);
 }
 
 // Pass 4: write every unit's matches at its offset.  Units whose speculation
@@ -1477,21 +1574,21 @@ __global__ void iter_exit_kernel(const Unit *units, uint64_t nunits, uint64_t *e
 // 16-byte records).  Units that were repaired, or had more matches
 // than slots, re-run their iteration (the block stages the hot tables only
 // then).
-__global__ __launch_bounds__(1024) void iter_emit_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
-                                                        const Unit *units, const uint64_t *slots, const uint64_t *off,
-                                                        uint64_t *out, uint64_t cap) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+__device__ __forceinline__ void emit_body(const BatchDev &b, const Geo &g, uint64_t nunits, const FwdDfaDev &f,
+                                          const RevDfaDev &r, const Unit *units, const uint64_t *slots,
+                                          const uint64_t *off, uint64_t *out, uint64_t cap, uint8_t *lds) {
   const uint8_t *rlds = nullptr;
   bool staged = false;
   const uint32_t lane = threadIdx.x & 63;
+  const uint64_t obase = off[0];  // off may be a segment of several regexes' shared scan
   for (uint64_t u0 = (uint64_t)blockIdx.x * blockDim.x; u0 < nunits; u0 += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t u = u0 + threadIdx.x;
     uint64_t o0 = 0, cnt = 0;
     uint32_t skip = 0;
     bool rerun = false, copy = false;
     if (u < nunits) {
-      o0 = off[u];
-      cnt = off[u + 1] - o0;
+      o0 = off[u] - obase;
+      cnt = off[u + 1] - off[u];
       if (cnt && o0 < cap) {
         const uint32_t fl = units[u].flags;
         rerun = ((fl & U_FIXED) && !(fl & U_COPY)) || cnt > g.slots;
@@ -1557,6 +1654,13 @@ __global__ __launch_bounds__(1024) void iter_emit_kernel(BatchDev b, Geo g, uint
       ++i;
     }
   }
+}
+
+__global__ __launch_bounds__(1024) void iter_emit_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
+                                                        const Unit *units, const uint64_t *slots, const uint64_t *off,
+                                                        uint64_t *out, uint64_t cap) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  emit_body(b, g, nunits, f, r, units, slots, off, out, cap, lds);
 }
 
 // ---------------------------------------------------- one wave per haystack
@@ -1649,11 +1753,15 @@ __global__ __launch_bounds__(64) void iter_wave_kernel(BatchDev b, FwdDfaDev f, 
 }
 
 // counts[h] = matches of haystack h, total = all matches.
-__global__ void iter_counts_kernel(uint64_t nh, uint64_t nk, const uint64_t *off, uint64_t *hcounts,
-                                   uint64_t *total) {
+__device__ __forceinline__ void counts_body(uint64_t nh, uint64_t nk, const uint64_t *off, uint64_t *hcounts,
+                                            uint64_t *total) {
   for (uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; h < nh; h += (uint64_t)gridDim.x * blockDim.x)
     hcounts[h] = off[(h + 1) * nk] - off[h * nk];
-  if (blockIdx.x == 0 && threadIdx.x == 0) *total = off[nh * nk];
+  if (blockIdx.x == 0 && threadIdx.x == 0) *total = off[nh * nk] - off[0];
+}
+__global__ void iter_counts_kernel(uint64_t nh, uint64_t nk, const uint64_t *off, uint64_t *hcounts,
+                                   uint64_t *total) {
+  counts_body(nh, nk, off, hcounts, total);
 }
 
 hipError_t scan_counts(const uint32_t *counts, uint64_t *off, uint64_t n, hipStream_t st) {
@@ -1901,6 +2009,82 @@ static hipError_t iter_post(const BatchDev &b, const Geo &g, uint64_t nunits, co
   return e;
 }
 
+template <int NW, int MQ>
+__global__ __launch_bounds__(256) void iter_spec_sa_multi_tile_kernel(BatchDev b, Geo g, uint64_t nunits, SaMulti m) {
+  multi_tile_body<NW, false, MQ>(b, g, nunits, m);
+}
+// The k-mer engine holds no Shift-And words: capped at 128 VGPRs for 4 waves
+// per SIMD (16 per CU; 146 VGPRs uncapped = 3 waves)
+template <int MQ>
+__global__ __launch_bounds__(256, 4) void iter_spec_kmer_multi_tile_kernel(BatchDev b, Geo g, uint64_t nunits,
+                                                                           SaMulti m) {
+  multi_tile_body<1, true, MQ>(b, g, nunits, m);
+}
+
+// The passes after a fused speculative pass for all its regexes at once:
+// one launch per pass, blockIdx.y = the regex, its buffers and tables in a
+// descriptor (the per-regex passes of iter_post took ~70 launches for the 9
+// regex-dna variants).  The regexes' unit counts are segments of one array
+// scanned once (emit / counts read their segment relative to its base).
+struct PostDesc {
+  FwdDfaDev f;
+  RevDfaDev r;
+  Unit *units;
+  uint32_t *counts;
+  const uint64_t *slots;
+  uint64_t *off, *queue;
+  unsigned long long *qlen;
+  const uint32_t *dirty;
+  uint64_t *out, cap, *hcounts, *total;
+  const uint64_t *entry;
+  uint64_t *exit, tail;
+  uint32_t nonempty;
+};
+
+__global__ void multi_entry_kernel(BatchDev b, Geo g, uint64_t nunits, const PostDesc *d) {
+  const PostDesc &P = d[blockIdx.y];
+  if (threadIdx.x != 0 || blockIdx.x != 0 || !P.entry || P.entry[2]) return;
+  FwdDfaDev fw = P.f;
+  fw.hot = 0;
+  RevDfaDev rw = P.r;
+  rw.hot = 0;
+  if (repair_unit(b, g, fw, rw, fw.lds_image /* unused: hot = 0 */, nullptr, 0, IterSt{P.entry[0], P.entry[1]},
+                  P.units, P.counts, P.slots) &&
+      g.nk > 1) {
+    const unsigned long long q = atomicAdd(P.qlen, 1ull);
+    P.queue[q] = 0;
+  }
+}
+
+__global__ __launch_bounds__(1024) void multi_fix_kernel(BatchDev b, Geo g, uint64_t nunits, const PostDesc *d) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const PostDesc &P = d[blockIdx.y];
+  fix_body(b, g, nunits, P.f, P.r, P.units, P.counts, P.slots, P.queue, P.qlen, P.dirty, lds);
+}
+
+__global__ void multi_walk_kernel(BatchDev b, Geo g, uint64_t nunits, const PostDesc *d) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const PostDesc &P = d[blockIdx.y];
+  if (*P.qlen == 0) return;
+  FwdDfaDev fw = P.f;
+  fw.hot = 0;
+  RevDfaDev rw = P.r;
+  rw.hot = 0;
+  walk_body(b, g, nunits, fw, rw, P.units, P.counts, P.slots, P.queue, P.qlen);
+}
+
+__global__ __launch_bounds__(1024) void multi_emit_kernel(BatchDev b, Geo g, uint64_t nunits, const PostDesc *d) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const PostDesc &P = d[blockIdx.y];
+  emit_body(b, g, nunits, P.f, P.r, P.units, P.slots, P.off, P.out, P.cap, lds);
+}
+
+__global__ void multi_counts_exit_kernel(BatchDev b, Geo g, uint64_t nunits, const PostDesc *d) {
+  const PostDesc &P = d[blockIdx.y];
+  counts_body(b.count, g.nk, P.off, P.hcounts, P.total);
+  if (P.exit && blockIdx.x == 0 && threadIdx.x == 0) exit_body(P.units, nunits, P.exit, P.tail, P.nonempty);
+}
+
 // Several Shift-And regexes over the same span in one speculative pass
 // (iter_spec_sa_multi_tile_kernel), then each regex's own passes.  Returns
 // hipErrorNotSupported (nothing launched) when they do not qualify: every
@@ -1908,8 +2092,9 @@ static hipError_t iter_post(const BatchDev &b, const Geo &g, uint64_t nunits, co
 // at most kSaMultiMax regexes in at most kSaMultiWords (8) words of 32 bits,
 // at most 32 bits per regex (a regex never straddles two words).
 hipError_t launch_find_iter_multi(const BatchDev &b, int nre, const FwdDfaDev *const *f, const RevDfaDev *const *r,
-                                  uint64_t chunk, const IterOut *o, hipStream_t st, int cus, const IterSpan *spn) {
-  if (nre < 1 || nre > kSaMultiMax || b.count == 0) return hipErrorNotSupported;
+                                  uint64_t chunk, const IterOut *o, hipStream_t st, int cus, const IterSpan *spn,
+                                  const KmerDev *km) {
+  if (nre < 1 || nre > kSaMultiMax || b.count != 1) return hipErrorNotSupported;
   Geo g;
   const uint64_t nunits = iter_geo(b, chunk, spn ? spn[0].hi : ~0ull, &g);
   if (!sa_tile_ok(b, g)) return hipErrorNotSupported;
@@ -1919,6 +2104,15 @@ hipError_t launch_find_iter_multi(const BatchDev &b, int nre, const FwdDfaDev *c
   SaMulti m{};
   m.nre = (uint32_t)nre;
   m.len = f[0]->sa_len;
+  // RURE_AMD_KMER=0 keeps the Shift-And words (A/B)
+  const char *kenv = getenv("RURE_AMD_KMER");
+  const bool kmer = km && km->bitmap && km->len == m.len && m.len <= 8 && !(kenv && kenv[0] == '0');
+  if (kmer) m.km = *km;
+  // packed per-regex state (multi_record): positions up to chunk + L, and at
+  // most one match per L bytes of a unit
+  m.pbits = 1;
+  while (m.pbits < 31 && (1ull << m.pbits) <= g.chunk + m.len + 1) ++m.pbits;
+  if (m.len == 0 || m.pbits > 24 || (g.chunk / m.len + 2) >= (1ull << (32 - m.pbits))) return hipErrorNotSupported;
   uint32_t word = 0, used = 0;
   for (int q = 0; q < nre; ++q) {
     if (!sa_usable(*f[q]) || f[q]->sa_len != m.len || f[q]->sa_bits > 32) return hipErrorNotSupported;
@@ -1936,51 +2130,105 @@ hipError_t launch_find_iter_multi(const BatchDev &b, int nre, const FwdDfaDev *c
     used += f[q]->sa_bits;
   }
   const int nw = (int)word + 1;
-  hipError_t e = hipSuccess;
-  std::vector<IterScratch> sc(nre);
-  uint32_t *img = nullptr;
-  int made = 0;
+  // one scratch for every regex: units, slots, the counts segments (one
+  // scan), offsets, walker queues, control words, the image, descriptors
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const uint64_t seg = nunits + 1;
+  const size_t sz_units = al(nunits * sizeof(Unit)), sz_slots = al(nunits * (size_t)g.slots * 16);
+  const size_t sz_counts = al(nre * seg * 4), sz_off = al(nre * seg * 8), sz_queue = al(nunits * 8);
+  const size_t sz_ctl = al((size_t)nre * 16), sz_img = al(256 * kSaMultiWords * 4), sz_desc = al(nre * sizeof(PostDesc));
+  const size_t total = nre * (sz_units + sz_slots + sz_queue) + sz_counts + sz_off + sz_ctl + sz_img + sz_desc;
+  uint8_t *buf = nullptr;
+  hipError_t e = scratch_malloc((void **)&buf, total, st);
+  if (e != hipSuccess) return e;
+  uint8_t *q0 = buf;
+  auto take = [&](size_t n) { uint8_t *r = q0; q0 += n; return r; };
+  uint32_t *counts_all = (uint32_t *)take(sz_counts);
+  uint64_t *off_all = (uint64_t *)take(sz_off);
+  uint8_t *ctl = take(sz_ctl);
+  m.image = (uint32_t *)take(sz_img);
+  PostDesc *ddesc = (PostDesc *)take(sz_desc);
+  std::vector<PostDesc> hd(nre);
+  size_t lb = 0;
+  bool entries = false;
+  for (int q = 0; q < nre; ++q) {
+    PostDesc &P = hd[q];
+    P.f = *f[q];
+    P.r = *r[q];
+    P.units = (Unit *)take(sz_units);
+    P.slots = (const uint64_t *)take(sz_slots);
+    P.queue = (uint64_t *)take(sz_queue);
+    P.counts = counts_all + q * seg;
+    P.off = off_all + q * seg;
+    P.qlen = (unsigned long long *)(ctl + 16 * q);
+    P.dirty = (const uint32_t *)(ctl + 16 * q + 8);
+    P.out = o[q].matches;
+    P.cap = o[q].cap;
+    P.hcounts = o[q].counts;
+    P.total = o[q].total;
+    P.entry = spn ? spn[q].entry : nullptr;
+    P.exit = spn ? spn[q].exit : nullptr;
+    P.tail = spn ? spn[q].tail : ~0ull;
+    P.nonempty = f[q]->nonempty;
+    entries = entries || P.entry;
+    m.units[q] = P.units;
+    m.slots[q] = (uint64_t *)P.slots;
+    m.counts[q] = P.counts;
+    m.dirty[q] = (uint32_t *)P.dirty;
+    lb = std::max(lb, iter_lds_bytes(*f[q], *r[q]));
+  }
   do {
-    if ((e = scratch_malloc((void **)&img, 256 * kSaMultiWords * 4, st)) != hipSuccess) break;
-    m.image = img;
-    for (; made < nre; ++made) {
-      if ((e = iter_scratch(nunits, g.slots, st, &sc[made])) != hipSuccess) break;
-      m.units[made] = sc[made].units;
-      m.slots[made] = sc[made].slots;
-      m.counts[made] = sc[made].counts;
-      m.dirty[made] = sc[made].dirty;
-    }
-    if (e != hipSuccess) break;
+    if ((e = hipMemsetAsync(counts_all, 0, nre * seg * 4, st)) != hipSuccess) break;
+    if ((e = hipMemsetAsync(ctl, 0, (size_t)nre * 16, st)) != hipSuccess) break;
+    if ((e = hipMemcpyAsync(ddesc, hd.data(), nre * sizeof(PostDesc), hipMemcpyHostToDevice, st)) != hipSuccess) break;
     const dim3 sg(grid_cap((nunits + 63) / 64, 4, cus, 4));
-#define RURE_SAM(NWc)                                                                            \
-  case NWc:                                                                                      \
-    hipLaunchKernelGGL(sa_multi_image_kernel<NWc>, dim3(1), dim3(256), 0, st, m);                \
-    ktimer_begin(st);                                                                            \
-    hipLaunchKernelGGL(iter_spec_sa_multi_tile_kernel<NWc>, sg, dim3(256), 0, st, b, g, nunits, m); \
-    ktimer_end(st);                                                                              \
+#define RURE_SAM(NWc)                                                                                   \
+  case NWc:                                                                                             \
+    hipLaunchKernelGGL(sa_multi_image_kernel<NWc>, dim3(1), dim3(256), 0, st, m);                       \
+    ktimer_begin(st);                                                                                   \
+    hipLaunchKernelGGL((iter_spec_sa_multi_tile_kernel<NWc, kSaMultiMax>), sg, dim3(256), 0, st, b, g,        \
+                       nunits, m);                                                                      \
+    ktimer_end(st);                                                                                     \
     break;
-    switch (nw) {
-      RURE_SAM(1) RURE_SAM(2) RURE_SAM(3) RURE_SAM(4) RURE_SAM(5) RURE_SAM(6) RURE_SAM(7) RURE_SAM(8)
-      default: e = hipErrorNotSupported;
+    if (kmer) {
+      ktimer_begin(st);
+      if (nre <= 4)
+        hipLaunchKernelGGL((iter_spec_kmer_multi_tile_kernel<4>), sg, dim3(256), 0, st, b, g, nunits, m);
+      else if (nre <= 9)
+        hipLaunchKernelGGL((iter_spec_kmer_multi_tile_kernel<9>), sg, dim3(256), 0, st, b, g, nunits, m);
+      else
+        hipLaunchKernelGGL((iter_spec_kmer_multi_tile_kernel<kSaMultiMax>), sg, dim3(256), 0, st, b, g,
+                           nunits, m);
+      ktimer_end(st);
+    } else {
+      switch (nw) {
+        RURE_SAM(1) RURE_SAM(2) RURE_SAM(3) RURE_SAM(4) RURE_SAM(5) RURE_SAM(6) RURE_SAM(7) RURE_SAM(8)
+        default: e = hipErrorNotSupported;
+      }
     }
 #undef RURE_SAM
     if (e != hipSuccess) break;
     if ((e = hipGetLastError()) != hipSuccess) break;
-    // each regex's post passes in turn (running them on side streams forked
-    // from st measured no faster: C3 variant phase 2.58 vs 2.48 ms,
-    // profiles/r02h_c3_summary.json vs r02g)
-    for (int q = 0; q < nre && e == hipSuccess; ++q)
-      e = iter_post(b, g, nunits, *f[q], *r[q], sc[q], o[q], spn ? &spn[q] : nullptr, st, cus);
+    // the passes of iter_post, each once for all regexes (blockIdx.y)
+    const int bs = iter_bs();
+    const int per_cu = std::max<int>(1, std::min<int>(2048 / bs, (int)((160u * 1024u) / std::max<size_t>(lb, 1))));
+    const uint32_t grid = (uint32_t)grid_cap(nunits, bs, cus, per_cu);
+    if ((e = allow_lds(multi_fix_kernel, lb)) != hipSuccess || (e = allow_lds(multi_emit_kernel, lb)) != hipSuccess)
+      break;
+    if (entries) hipLaunchKernelGGL(multi_entry_kernel, dim3(1, nre), dim3(64), 0, st, b, g, nunits, ddesc);
+    if (g.nk > 1) {
+      hipLaunchKernelGGL(multi_fix_kernel, dim3(grid, nre), dim3(bs), lb, st, b, g, nunits, ddesc);
+      hipLaunchKernelGGL(multi_walk_kernel, dim3(1, nre), dim3(64), 0, st, b, g, nunits, ddesc);
+    }
+    if ((e = hipGetLastError()) != hipSuccess) break;
+    if ((e = scan_counts(counts_all, off_all, nre * seg - 1, st)) != hipSuccess) break;
+    hipLaunchKernelGGL(multi_emit_kernel, dim3(grid, nre), dim3(bs), lb, st, b, g, nunits, ddesc);
+    hipLaunchKernelGGL(multi_counts_exit_kernel, dim3(grid_cap(b.count, 256, cus, 4), nre), dim3(256), 0, st, b, g,
+                       nunits, ddesc);
+    e = hipGetLastError();
   } while (false);
-  for (int q = 0; q < made; ++q) {
-    hipError_t e2 = scratch_free(sc[q].buf, st);
-    if (e == hipSuccess) e = e2;
-  }
-  if (img) {
-    hipError_t e2 = scratch_free(img, st);
-    if (e == hipSuccess) e = e2;
-  }
-  return e;
+  hipError_t e2 = scratch_free(buf, st);
+  return e != hipSuccess ? e : e2;
 }
 
 hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaDev &r, const NfaDev *nf,

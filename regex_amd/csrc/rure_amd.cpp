@@ -681,6 +681,8 @@ struct rure_iter {
 
 namespace {
 
+void kmer_forget(const rure *re);  // k-mer table cache (below)
+
 SyntaxFlags syntax_flags(uint32_t flags) {  // rure.rs:119-124
   SyntaxFlags f;
   f.casei = (flags & RURE_FLAG_CASEI) != 0;
@@ -831,6 +833,30 @@ bool needs_mt_lane(const ExecLiterals &x) {
          (x.match_type == MT_LITERAL_UNANCHORED && !x.prefixes.complete);
 }
 
+// FwdDfaDev::pfx_*: the start-state prefix skip (dfa.rs:700-711), for a
+// DFA whose start does not depend on look-behind, from the regex's prefix
+// literals (dfa.prefixes, exec.rs:308-311; not for anchored starts,
+// dfa.rs:1516-1522 has_prefix) when they have at most 4 first bytes.
+// RURE_AMD_PREFIX=0 turns it off (A/B).
+void set_prefix_skip(const rure *re, FwdDfaDev *f) {
+  f->pfx_n = 0;
+  const char *env = getenv("RURE_AMD_PREFIX");
+  if ((env && env[0] == '0') || !f->ustart1 || re->nfa.anchored_start) return;
+  const LitSearcher &p = re->xl.prefixes;
+  if (p.matcher == 0 || p.lits.lits.empty()) return;
+  bool seen[256] = {false};
+  uint32_t n = 0;
+  for (const Lit &l : p.lits.lits) {
+    if (l.v.empty()) return;
+    const uint8_t b = (uint8_t)l.v[0];
+    if (seen[b]) continue;
+    if (n == 4) return;
+    seen[b] = true;
+    f->pfx_rep[n++] = b * 0x01010101u;
+  }
+  f->pfx_n = n;
+}
+
 // Upload (once per device) and return device descriptors.
 DevTables *regex_device(rure *re, std::string *err) {
   if (!build_regex(re)) { if (err) *err = re->dfa_err; return nullptr; }
@@ -918,6 +944,7 @@ DevTables *regex_device(rure *re, std::string *err) {
     t.r.ustart1 = re->pr.ustart1;
     t.f.ustart1 = pf.ustart1;
     t.f.nonempty = can_match_empty(re->nfa) ? 0 : 1;
+    set_prefix_skip(re, &t.f);
     // a regex anchored at the end and not at the start runs the reverse DFA
     // from the end of the text (exec.rs:1175-1177, 671-688)
     t.anchored_rev = !re->nfa.anchored_start && re->nfa.anchored_end;
@@ -1264,6 +1291,7 @@ const FwdDfaDev *iter_device(rure *re, const DevTables &t, std::string *err) {
   f.all = pf.all;
   f.ustart1 = pf.ustart1;
   f.nonempty = can_match_empty(re->nfa) ? 0 : 1;
+  set_prefix_skip(re, &f);
   // RURE_AMD_FB=0 turns the first-byte start rule off (reverse scans)
   f.fb_n = getenv("RURE_AMD_FB") && getenv("RURE_AMD_FB")[0] == '0' ? 0 : re->fb_n;
   for (uint32_t i = 0; i < 4; ++i) f.fb_rep[i] = (i < re->fb_n ? re->fb_bytes[i] : re->fb_bytes[0]) * 0x01010101u;
@@ -1676,6 +1704,7 @@ rure *rure_compile_must(const char *pattern) {  // rure.rs:76-91
 
 void rure_free(rure *re) {
   if (!re) return;
+  kmer_forget(re);
   for (auto &kv : re->iter_dev) {
     int cur = 0;
     (void)hipGetDevice(&cur);
@@ -2251,6 +2280,119 @@ int rure_amd_find_iter_span(rure *re, const uint8_t *haystack, size_t length, si
   return run_find_iter(re, t, b, o, st, &err, &sp) == hipSuccess ? RURE_AMD_OK : RURE_AMD_ERR_HIP;
 }
 
+namespace {
+// k-mer probe tables of a regex list (KmerDev), built once per list and
+// device: every regex a finite set of strings of one length L <= 8 over an
+// alphabet of at most 4 bytes with distinct codes (b >> shift) & 3.
+struct KmerCacheEntry {
+  std::vector<const rure *> res;
+  int dev;
+  void *blob;
+  KmerDev km;
+};
+std::mutex g_kmer_mu;
+std::vector<KmerCacheEntry> g_kmer;
+
+bool build_kmer(rure *const *res, size_t n, std::vector<uint32_t> *bitmap, std::vector<uint16_t> *mask, KmerDev *km) {
+  if (n == 0 || n > 16) return false;
+  size_t L = 0;
+  bool seen[256] = {false};
+  std::vector<uint8_t> alpha;
+  for (size_t i = 0; i < n; ++i) {
+    rure *re = res[i];
+    if (!re->lit_ok || re->lits.lits.empty() || re->lits.minlen != re->lits.maxlen) return false;
+    if (L == 0) L = re->lits.minlen;
+    if (re->lits.minlen != L) return false;
+    for (const std::string &l : re->lits.lits)
+      for (unsigned char c : l)
+        if (!seen[c]) {
+          seen[c] = true;
+          alpha.push_back(c);
+        }
+  }
+  if (L == 0 || L > 8 || alpha.size() > 4) return false;
+  int shift = -1;
+  for (int sh = 0; sh <= 6 && shift < 0; ++sh) {
+    uint32_t used = 0;
+    bool ok = true;
+    for (uint8_t c : alpha) {
+      const uint32_t code = (c >> sh) & 3u;
+      if (used & (1u << code)) ok = false;
+      used |= 1u << code;
+    }
+    if (ok) shift = sh;
+  }
+  if (shift < 0) return false;
+  km->shift = (uint32_t)shift;
+  km->lut = 0;
+  km->present = 0;
+  for (uint8_t c : alpha) {
+    const uint32_t code = (c >> shift) & 3u;
+    km->lut |= (uint32_t)c << (8 * code);
+    km->present |= 1u << code;
+  }
+  km->len = L;
+  km->cmask = (uint32_t)((1ull << (2 * L)) - 1);
+  bitmap->assign(2048, 0);
+  mask->assign((size_t)1 << (2 * L), 0);
+  for (size_t i = 0; i < n; ++i)
+    for (const std::string &l : res[i]->lits.lits) {
+      uint32_t code = 0;
+      for (size_t j = 0; j < L; ++j) code |= (((uint8_t)l[j] >> shift) & 3u) << (2 * j);
+      (*bitmap)[code >> 5] |= 1u << (code & 31);
+      (*mask)[code] |= (uint16_t)(1u << i);
+    }
+  return true;
+}
+
+// The cached device tables for this regex list, or null (not eligible).
+const KmerDev *kmer_device(rure *const *res, size_t n) {
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> g(g_kmer_mu);
+  for (const KmerCacheEntry &e : g_kmer)
+    if (e.dev == d && e.res.size() == n && std::equal(e.res.begin(), e.res.end(), res)) return e.blob ? &e.km : nullptr;
+  KmerCacheEntry ent;
+  ent.res.assign(res, res + n);
+  ent.dev = d;
+  ent.blob = nullptr;
+  std::vector<uint32_t> bm;
+  std::vector<uint16_t> mk;
+  if (build_kmer(res, n, &bm, &mk, &ent.km)) {
+    Blob b;
+    const size_t ob = b.add(bm.data(), bm.size() * 4), om = b.add(mk.data(), mk.size() * 2);
+    DevTables tmp;
+    std::string err;
+    if (upload_blob(b, &tmp, &err)) {
+      ent.blob = tmp.blob;
+      ent.km.bitmap = (const uint32_t *)((uint8_t *)tmp.blob + ob);
+      ent.km.mask = (const uint16_t *)((uint8_t *)tmp.blob + om);
+    }
+  }
+  g_kmer.push_back(ent);
+  return g_kmer.back().blob ? &g_kmer.back().km : nullptr;
+}
+
+// rure_free: drop the k-mer tables of lists holding this regex.
+void kmer_forget(const rure *re) {
+  std::lock_guard<std::mutex> g(g_kmer_mu);
+  for (size_t i = 0; i < g_kmer.size();) {
+    if (std::find(g_kmer[i].res.begin(), g_kmer[i].res.end(), re) != g_kmer[i].res.end()) {
+      if (g_kmer[i].blob) {
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        (void)hipSetDevice(g_kmer[i].dev);
+        (void)hipFree(g_kmer[i].blob);
+        (void)hipSetDevice(cur);
+      }
+      g_kmer.erase(g_kmer.begin() + i);
+    } else {
+      ++i;
+    }
+  }
+}
+}  // namespace
+
 int rure_amd_find_iter_span_multi(rure *const *res, size_t n, const uint8_t *haystack, size_t length, size_t lo,
                                   size_t hi, const rure_amd_iter_state *const *entry, uint64_t *const *count,
                                   rure_match *const *matches, const size_t *capacity,
@@ -2296,7 +2438,8 @@ int rure_amd_find_iter_span_multi(rure *const *res, size_t n, const uint8_t *hay
     uint64_t per_cu = 1024;
     if (const char *v = getenv("RURE_AMD_ITER_LANES")) per_cu = std::max(64, atoi(v));
     const uint64_t chunk = odd_lines(std::max<uint64_t>(4096, (span + (uint64_t)cus * per_cu - 1) / ((uint64_t)cus * per_cu)));
-    hipError_t e = launch_find_iter_multi(b, (int)n, fs.data(), rs.data(), chunk, os.data(), st, cus, sps.data());
+    const KmerDev *km = kmer_device(res, n);
+    hipError_t e = launch_find_iter_multi(b, (int)n, fs.data(), rs.data(), chunk, os.data(), st, cus, sps.data(), km);
     if (e == hipSuccess) return RURE_AMD_OK;
     if (e != hipErrorNotSupported) return RURE_AMD_ERR_HIP;
   }

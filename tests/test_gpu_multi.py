@@ -96,3 +96,38 @@ def test_multi_counts_known_answers(cuda, k):
     got = R.find_iter_span_multi(res, h, 0, len(seq), length=len(seq))
     for i in range(k):
         assert int(got[i][0].item()) == kc["variants"][i]["count"], i
+
+
+@pytest.mark.parametrize("engine", ["kmer", "shiftand"])
+def test_multi_engines_mixed_bytes(cuda, monkeypatch, engine):
+    """The fused pass with the k-mer probe engine (default for the regex-dna
+    variants) and with the Shift-And words (RURE_AMD_KMER=0): text with
+    uppercase ACGT, IUB codes, 'n', bytes >= 0x80 and newlines between the
+    motifs — every regex's output equals its own single pass and the oracle."""
+    if engine == "shiftand":
+        monkeypatch.setenv("RURE_AMD_KMER", "0")
+    rng = np.random.default_rng(11)
+    motifs = [b"agggtaaa", b"tttaccct", b"cgggtaaa", b"tttacccg", b"aggggtaa", b"ggtaaaTT", b"AGGGTAAA"]
+    noise = np.frombuffer(b"acgtacgtACGTnNBDHKMRSVWY\n\x80\xff\xc3\xa9", dtype=np.uint8)
+    parts = [motifs[int(i)] if rng.random() < 0.4 else bytes(rng.choice(noise, size=int(rng.integers(1, 12))))
+             for i in rng.integers(0, len(motifs), size=150000)]
+    text = b"".join(parts)
+    res = variants()
+    h = dev(text, cuda)
+    got = check_same(res, h, len(text), 0, len(text))
+    for i, re in enumerate(res):
+        assert pairs(got[i][1]) == OracleRegex(re).find_iter(text), i
+    check_same(res, h, len(text), 13, len(text) - 5)
+
+
+def test_multi_kmer_known_answers(cuda):
+    """The regex-dna known answers through the k-mer engine over many copies."""
+    kc = known_counts()["regexdna"]
+    seq = stripped(40)
+    res = variants()
+    h = dev(seq, cuda)
+    got = R.find_iter_span_multi(res, h, 0, len(seq), length=len(seq))
+    one = stripped(1)
+    for v, re, g in zip(kc["variants"], res, got):
+        seam = len(OracleRegex(re).find_iter(one * 2)) - 2 * v["count"]
+        assert int(g[0].item()) == v["count"] * 40 + seam * 39, v["re"]
