@@ -555,6 +555,10 @@ def run_c3(ctx):
     # stripped stream read once by the fused variant pass (9 times when
     # separate), and the match records written (16 B each)
     var_matches = sum(got) // W
+    # the fused pass runs the k-mer probe engine when every variant is a set
+    # of 8-byte strings (all 9 are) unless RURE_AMD_KMER=0
+    kmer = os.environ.get("RURE_AMD_KMER", "1") != "0"
+    var_kernel = ("iter_spec_kmer_multi_tile" if kmer else "iter_spec_sa_multi_tile") if fused else "iter_spec_sa_tile"
     step_bytes = strip_bytes + var_bytes * (1 if fused else len(variants)) + 16 * (nsp_sharded // W + var_matches)
     config = {"workload": "C3: regex-dna x%d (%d B raw, %d B stripped): strip find_iter + 9 variant find_iter"
                           % (copies, N, M),
@@ -573,11 +577,10 @@ def run_c3(ctx):
                     strip_matches=nsp_sharded, variant_counts=got, known_answers_ok=ok,
                     variant_engine="separate passes" if ctx.args.c3_separate else "one fused pass",
                     cut_recomputations=stats["recomputed"],
-                    roofline=roofline_kernel(var_bytes, spec_ms, spec_n, config,
-                                             "iter_spec_sa_multi_tile" if fused else "iter_spec_sa_tile",
+                    roofline=roofline_kernel(var_bytes, spec_ms, spec_n, config, var_kernel,
                                              "variant speculative kernel (%s)" %
-                                             ("iter_spec_sa_multi_tile_kernel: one read of the stripped span "
-                                              "for all 9 variants" if fused else
+                                             ("%s_kernel: one read of the stripped span for all 9 variants"
+                                              % var_kernel if fused else
                                               "iter_spec_sa_tile_kernel, one launch per variant")),
                     roofline_strip=roofline_kernel(strip_bytes, lex_ms, lex_n, config,
                                                    "iter_spec_lex_tile",

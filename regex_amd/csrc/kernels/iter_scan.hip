@@ -920,7 +920,7 @@ __device__ __forceinline__ void sam_block(uint32_t (&D)[NW], const uint32_t *B, 
 // iteration exactly as sam_block does.  Rp: the previous block's codes
 // (garbage before a unit's first block: the windows reaching into it start
 // before the unit and are not the unit's).
-template <int MQ>
+template <int MQ, int KL>
 __device__ __forceinline__ void kmer_block(uint32_t &Rp, const uint32_t *B, const SaMulti &m, const uint32_t w[4],
                                            uint32_t k0, uint32_t kend, int64_t bp, uint64_t c0, uint64_t c1,
                                            uint32_t (&pn)[MQ], uint64_t u, uint32_t nslots, const uint8_t *base) {
@@ -933,14 +933,21 @@ __device__ __forceinline__ void kmer_block(uint32_t &Rp, const uint32_t *B, cons
     c4 = (c4 | (c4 >> 12)) & 0xFFu;
     cw |= c4 << (8 * x);
   }
-  const uint32_t L = (uint32_t)m.len, cmask = km.cmask;
+  // The window of the KL-mer ending at byte j starts at bit sh = 2 (17 + j -
+  // KL) of cw:Rp.  Its bitmap dword is bits [sh + 5, sh + 2 KL) (address:
+  // shifted to bit 2), its bit within the dword bits [sh, sh + 5) (v_bfe_u32
+  // reads only the low 5 bits of the offset).
+  constexpr uint32_t amask = ((1u << (2 * KL)) - 1u) >> 5 << 2;
+  const uint8_t *Bb = (const uint8_t *)B;
   uint32_t cm = 0;
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
-    // codes of bytes j - L + 1 .. j: bits [2 (16 + j - L + 1), ...) of cw:Rp
-    const uint32_t sh = 2 * (17 + j - L);
-    const uint32_t code = (sh >= 32 ? (cw >> (sh - 32)) : __builtin_amdgcn_alignbit(cw, Rp, sh)) & cmask;
-    cm |= ((B[code >> 5] >> (code & 31)) & 1u) << j;
+    constexpr int base_sh = 2 * (17 - KL);
+    const int sh = base_sh + 2 * j;
+    const uint32_t lo = sh >= 32 ? (cw >> (sh - 32)) : __builtin_amdgcn_alignbit(cw, Rp, sh);
+    const uint32_t hi = sh + 3 >= 32 ? (cw >> (sh + 3 - 32)) : __builtin_amdgcn_alignbit(cw, Rp, sh + 3);
+    const uint32_t word = *(const uint32_t *)(Bb + (hi & amask));
+    cm |= __builtin_amdgcn_ubfe(word, lo, 1) << j;
   }
   Rp = cw;
   cm &= ((kend >= 32 ? 0u : (1u << kend)) - 1u) & ~((1u << k0) - 1u);
@@ -949,11 +956,11 @@ __device__ __forceinline__ void kmer_block(uint32_t &Rp, const uint32_t *B, cons
   while (cm) {
     const uint32_t j = __builtin_ctz(cm);
     cm &= cm - 1;
-    const uint64_t e = (uint64_t)bp + j + 1, st = e - L;
-    if ((int64_t)e < (int64_t)L || st < c0) continue;  // starts before the unit: not its match
+    const uint64_t e = (uint64_t)bp + j + 1, st = e - KL;
+    if ((int64_t)e < (int64_t)KL || st < c0) continue;  // starts before the unit: not its match
     uint32_t code = 0;
     bool ok = true;
-    for (uint32_t i = 0; i < L; ++i) {
+    for (uint32_t i = 0; i < (uint32_t)KL; ++i) {
       const uint32_t bb = base[st + i], c = (bb >> km.shift) & 3u;
       ok = ok && ((km.present >> c) & 1u) && ((km.lut >> (8 * c)) & 0xFFu) == bb;
       code |= c << (2 * i);
@@ -975,7 +982,7 @@ __device__ __forceinline__ void multi_block(uint32_t (&D)[NW], const uint32_t *B
                                             const uint32_t w[4], uint32_t k0, uint32_t kend, int64_t bp, uint64_t c0,
                                             uint64_t c1, uint32_t (&pn)[MQ], uint64_t u, uint32_t nslots,
                                             const uint8_t *base) {
-  if (KMER) kmer_block<MQ>(D[0], B, m, w, k0, kend, bp, c0, c1, pn, u, nslots, base);
+  if (KMER) kmer_block<MQ, 8>(D[0], B, m, w, k0, kend, bp, c0, c1, pn, u, nslots, base);
   else sam_block<NW, MQ>(D, B, m, w, k0, kend, bp, c0, c1, pn, u, nslots);
 }
 
@@ -2106,7 +2113,7 @@ hipError_t launch_find_iter_multi(const BatchDev &b, int nre, const FwdDfaDev *c
   m.len = f[0]->sa_len;
   // RURE_AMD_KMER=0 keeps the Shift-And words (A/B)
   const char *kenv = getenv("RURE_AMD_KMER");
-  const bool kmer = km && km->bitmap && km->len == m.len && m.len <= 8 && !(kenv && kenv[0] == '0');
+  const bool kmer = km && km->bitmap && km->len == m.len && m.len == 8 && !(kenv && kenv[0] == '0');
   if (kmer) m.km = *km;
   // packed per-regex state (multi_record): positions up to chunk + L, and at
   // most one match per L bytes of a unit
