@@ -235,6 +235,9 @@ size_t rure_amd_captures_len(rure *re);
  * Also done when the last rure / rure_set is freed.  Safe at any time: each
  * block is freed after the kernels that last used it. */
 void rure_amd_release_scratch(void);
+// Scratch bookkeeping: bytes cached for reuse, bytes held by calls in
+// flight, and the number of rure / rure_set handles alive.
+void rure_amd_scratch_stats(size_t *cached, size_t *live, long *handles);
 
 /* Diagnostics (host only, no GPU needed). */
 typedef struct rure_amd_dfa_info {

@@ -75,6 +75,14 @@ def release_scratch():
     N.rure_amd_release_scratch()
 
 
+def scratch_stats():
+    """{"cached", "live", "handles"}: scratch bytes cached for reuse, bytes
+    held by calls in flight, rure / rure_set handles alive."""
+    c, l, h = N.c_size(0), N.c_size(0), ctypes.c_long(0)
+    N.rure_amd_scratch_stats(ctypes.byref(c), ctypes.byref(l), ctypes.byref(h))
+    return {"cached": c.value, "live": l.value, "handles": h.value}
+
+
 class Error(Exception):
     """Invalid pattern (regex-capi/src/error.rs:8-77)."""
 

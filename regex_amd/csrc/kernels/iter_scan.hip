@@ -910,29 +910,26 @@ __device__ __forceinline__ void sam_block(uint32_t (&D)[NW], const uint32_t *B, 
   }
 }
 
-// The k-mer probe engine's block step (KmerDev): the 2-bit codes of the 16
-// bytes (code(b) = (b >> shift) & 3, four bytes per VALU op) join the
-// previous block's in a 64-bit window register; the L-mer ending at each
-// byte is one independent probe of the LDS bitmap of the strings' codes (no
-// dependent chain).  Probe hits (rare: ~1 per 2 KiB on the regex-dna stream)
-// are verified on the text bytes (exact whatever the input: a byte outside
-// the alphabet fails) and the code's regex mask drives each regex's greedy
-// iteration exactly as sam_block does.  Rp: the previous block's codes
-// (garbage before a unit's first block: the windows reaching into it start
-// before the unit and are not the unit's).
-template <int MQ, int KL>
-__device__ __forceinline__ void kmer_block(uint32_t &Rp, const uint32_t *B, const SaMulti &m, const uint32_t w[4],
-                                           uint32_t k0, uint32_t kend, int64_t bp, uint64_t c0, uint64_t c1,
-                                           uint32_t (&pn)[MQ], uint64_t u, uint32_t nslots, const uint8_t *base) {
-  const KmerDev &km = m.km;
-  uint32_t cw = 0;
+// The k-mer probe engine (KmerDev): the 2-bit codes of a block's 16 bytes
+// (code(b) = (b >> shift) & 3, four bytes per VALU op) join the previous
+// block's in a 64-bit window register; the L-mer ending at each byte is one
+// independent probe of the LDS bitmap of the strings' codes (no dependent
+// chain).  Returns the probe hits (bit j: the L-mer ending at byte j).  Rp:
+// the previous block's codes (garbage before a unit's first block: the
+// windows reaching into it start before the unit and are dropped by
+// kmer_hit).
+template <int KL>
+__device__ __forceinline__ uint32_t kmer_probe(uint32_t &Rp, const uint32_t *B, const KmerDev &km,
+                                               const uint32_t w[4]) {
+  // four codes per word packed by one v_dot4_u32_u8 (byte weights 1, 4,
+  // 16, 64 on the codes left in place at bit `shift` of each byte)
+  const uint32_t M = 0x03030303u << km.shift;
+  uint32_t d[4];
 #pragma unroll
-  for (int x = 0; x < 4; ++x) {
-    uint32_t c4 = (w[x] >> km.shift) & 0x03030303u;
-    c4 = (c4 | (c4 >> 6)) & 0x000F000Fu;
-    c4 = (c4 | (c4 >> 12)) & 0xFFu;
-    cw |= c4 << (8 * x);
-  }
+  for (int x = 0; x < 4; ++x) d[x] = __builtin_amdgcn_udot4(w[x] & M, 0x40100401u, 0u, false);
+  uint32_t cw = d[0] >> km.shift;
+#pragma unroll
+  for (int x = 1; x < 4; ++x) cw |= d[x] << (8 * x - km.shift);
   // The window of the KL-mer ending at byte j starts at bit sh = 2 (17 + j -
   // KL) of cw:Rp.  Its bitmap dword is bits [sh + 5, sh + 2 KL) (address:
   // shifted to bit 2), its bit within the dword bits [sh, sh + 5) (v_bfe_u32
@@ -950,28 +947,49 @@ __device__ __forceinline__ void kmer_block(uint32_t &Rp, const uint32_t *B, cons
     cm |= __builtin_amdgcn_ubfe(word, lo, 1) << j;
   }
   Rp = cw;
+  return cm;
+}
+
+// One probe hit: the KL-mer ending before e.  Verified on the text bytes
+// (exact whatever the input: a byte outside the alphabet fails; the eight
+// loads issue together), then its code's regex mask drives each regex's
+// greedy iteration exactly as sam_block does.
+template <int MQ, int KL>
+__device__ __forceinline__ void kmer_hit(const SaMulti &m, uint64_t e, uint64_t c0, uint64_t c1,
+                                         uint32_t (&pn)[MQ], uint64_t u, uint32_t nslots, const uint8_t *base) {
+  const KmerDev &km = m.km;
+  if (e < (uint64_t)KL || e - KL < c0) return;  // starts before the unit: not its match
+  const uint64_t st = e - KL;
+  uint32_t code = 0, bad = 0;
+#pragma unroll
+  for (int i = 0; i < KL; ++i) {
+    const uint32_t bb = base[st + i], c = (bb >> km.shift) & 3u;
+    bad |= (((km.lut >> (8 * c)) & 0xFFu) ^ bb) | (~(km.present >> c) & 1u);
+    code |= c << (2 * i);
+  }
+  if (bad) return;
+  const uint32_t mask = km.mask[code];
+#pragma unroll
+  for (int q = 0; q < MQ; ++q) {
+    if ((uint32_t)q >= m.nre) break;
+    if ((mask >> q) & 1u) multi_record<MQ>(m, pn, q, st, e, c0, c1, u, nslots);
+  }
+}
+
+// The k-mer engine's step of one block with its hits settled at once (the
+// tail paths; the tile loop defers a line's hits to its end, see
+// multi_tile_body): bytes k0..kend of the block at bp.
+template <int MQ, int KL>
+__device__ __forceinline__ void kmer_block(uint32_t &Rp, const uint32_t *B, const SaMulti &m, const uint32_t w[4],
+                                           uint32_t k0, uint32_t kend, int64_t bp, uint64_t c0, uint64_t c1,
+                                           uint32_t (&pn)[MQ], uint64_t u, uint32_t nslots, const uint8_t *base) {
+  uint32_t cm = kmer_probe<KL>(Rp, B, m.km, w);
   cm &= ((kend >= 32 ? 0u : (1u << kend)) - 1u) & ~((1u << k0) - 1u);
-  if (!cm) return;
 #pragma unroll 1
   while (cm) {
     const uint32_t j = __builtin_ctz(cm);
     cm &= cm - 1;
-    const uint64_t e = (uint64_t)bp + j + 1, st = e - KL;
-    if ((int64_t)e < (int64_t)KL || st < c0) continue;  // starts before the unit: not its match
-    uint32_t code = 0;
-    bool ok = true;
-    for (uint32_t i = 0; i < (uint32_t)KL; ++i) {
-      const uint32_t bb = base[st + i], c = (bb >> km.shift) & 3u;
-      ok = ok && ((km.present >> c) & 1u) && ((km.lut >> (8 * c)) & 0xFFu) == bb;
-      code |= c << (2 * i);
-    }
-    if (!ok) continue;
-    const uint32_t mask = km.mask[code];
-#pragma unroll
-    for (int q = 0; q < MQ; ++q) {
-      if ((uint32_t)q >= m.nre) break;
-      if ((mask >> q) & 1u) multi_record<MQ>(m, pn, q, st, e, c0, c1, u, nslots);
-    }
+    kmer_hit<MQ, KL>(m, (uint64_t)bp + j + 1, c0, c1, pn, u, nslots, base);
   }
 }
 
@@ -1045,12 +1063,43 @@ __device__ __forceinline__ void multi_tile_body(const BatchDev &b, const Geo &g,
       if (full) {
         uint4 cur = buf[lane * 8 + sw];
         if (at == 0) first = cur;
+        if (KMER) {
+          // The line's probe hits collect in a 128-bit shift register (block
+          // mm at bits 16 mm) and are settled after the line: the block loop
+          // issues no global load, so nothing in it waits on the next
+          // line's tile loads in flight (one vmcnt counter, in order).
+          uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
 #pragma unroll 1
-        for (int mm = 0; mm < 8; ++mm) {
-          const uint4 nx = buf[lane * 8 + ((mm + 1 < 8 ? mm + 1 : 7) ^ sw)];
-          const uint32_t wd[4] = {cur.x, cur.y, cur.z, cur.w};
-          multi_block<NW, KMER, MQ>(D, B, m, wd, 0, 16, (int64_t)(c0 + at + 16 * mm), c0, c1, pn, u, g.slots, base);
-          cur = nx;
+          for (int mm = 0; mm < 8; ++mm) {
+            const uint4 nx = buf[lane * 8 + ((mm + 1 < 8 ? mm + 1 : 7) ^ sw)];
+            const uint32_t wd[4] = {cur.x, cur.y, cur.z, cur.w};
+            const uint32_t cm = kmer_probe<8>(D[0], B, m.km, wd);
+            h0 = __builtin_amdgcn_alignbit(h1, h0, 16);
+            h1 = __builtin_amdgcn_alignbit(h2, h1, 16);
+            h2 = __builtin_amdgcn_alignbit(h3, h2, 16);
+            h3 = __builtin_amdgcn_alignbit(cm, h3, 16);
+            cur = nx;
+          }
+          const uint32_t hw[4] = {h0, h1, h2, h3};
+#pragma unroll
+          for (int x = 0; x < 4; ++x) {
+            uint32_t hm = hw[x];
+#pragma unroll 1
+            while (hm) {
+              const uint32_t j = __builtin_ctz(hm);
+              hm &= hm - 1;
+              kmer_hit<MQ, 8>(m, c0 + at + 32 * x + j + 1, c0, c1, pn, u, g.slots, base);
+            }
+          }
+        } else {
+#pragma unroll 1
+          for (int mm = 0; mm < 8; ++mm) {
+            const uint4 nx = buf[lane * 8 + ((mm + 1 < 8 ? mm + 1 : 7) ^ sw)];
+            const uint32_t wd[4] = {cur.x, cur.y, cur.z, cur.w};
+            multi_block<NW, KMER, MQ>(D, B, m, wd, 0, 16, (int64_t)(c0 + at + 16 * mm), c0, c1, pn, u, g.slots,
+                                      base);
+            cur = nx;
+          }
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1577,8 +1626,7 @@ __global__ void iter_exit_kernel(const Unit *units, uint64_t nunits, uint64_t *e
 
 // Pass 4: write every unit's matches at its offset.  Units whose speculation
 // held copy their slot buffer: each lane its own unit's when it holds at most
-// 4 records, else the 64 lanes of a wave one unit at a time (coalesced
-// 16-byte records).  Units that were repaired, or had more matches
+// 4 records, else the wave's larger units eight at a time.  Units that were repaired, or had more matches
 // than slots, re-run their iteration (the block stages the hot tables only
 // then).
 __device__ __forceinline__ void emit_body(const BatchDev &b, const Geo &g, uint64_t nunits, const FwdDfaDev &f,
@@ -1619,26 +1667,43 @@ __device__ __forceinline__ void emit_body(const BatchDev &b, const Geo &g, uint6
       for (uint32_t k = 0; k < 8; ++k)
         if (k < nw) dst[k] = v[k];
     }
-    uint64_t m = __ballot(copy && !own);
-    while (m) {
-      const int l = __builtin_ctzll(m);
-      m &= m - 1;
-      const uint64_t uu = __shfl(u, l), oo = __shfl(o0, l);
-      const uint64_t cc = min(__shfl(cnt, l), cap - oo);
-      const uint32_t sk = __shfl(skip, l);
-      // `out` (rure_match records) is only guaranteed 8-byte aligned
-      const uint64_t *src = slots + (uu * g.slots + sk) * 2;
-      uint64_t *dst = out + 2 * oo;
-      // four loads in flight per lane before the stores
-      uint64_t i = lane;
-      for (; i + 192 < 2 * cc; i += 256) {
-        const uint64_t a0 = src[i], a1 = src[i + 64], a2 = src[i + 128], a3 = src[i + 192];
-        dst[i] = a0;
-        dst[i + 64] = a1;
-        dst[i + 128] = a2;
-        dst[i + 192] = a3;
+    // The wave's larger units eight at a time: lane l serves records
+    // l & 7, + 8, ... of unit 8 grp + (l >> 3), so each load instruction
+    // reads 8 units x 128 contiguous bytes (whole lines) and four rounds of
+    // loads are in flight before their stores.
+    const uint64_t wrec = (copy && !own) ? min(cnt, cap - o0) : 0;
+    const uint64_t wsrc = (u * g.slots + skip) * 2, wdst = 2 * o0;
+    const uint64_t busy = __ballot(wrec != 0);
+    const bool a16 = ((uintptr_t)out & 15) == 0;
+#pragma unroll 1
+    for (int grp = 0; grp < 8; ++grp) {
+      if (!((busy >> (8 * grp)) & 0xFFull)) continue;
+      const int ul = 8 * grp + (int)(lane >> 3);
+      const uint64_t cu = __shfl(wrec, ul), su = __shfl(wsrc, ul), du = __shfl(wdst, ul);
+      uint64_t mx = cu;
+      mx = max(mx, (uint64_t)__shfl_xor(mx, 8));
+      mx = max(mx, (uint64_t)__shfl_xor(mx, 16));
+      mx = max(mx, (uint64_t)__shfl_xor(mx, 32));
+      const ulonglong2 *src = (const ulonglong2 *)(slots + su);
+      uint64_t *dst = out + du;
+      for (uint64_t i = lane & 7; i < mx; i += 32) {
+        ulonglong2 v[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          if (i + 8 * t < cu) v[t] = src[i + 8 * t];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const uint64_t j = i + 8 * t;
+          if (j < cu) {
+            if (a16) {
+              *(ulonglong2 *)(dst + 2 * j) = v[t];
+            } else {
+              dst[2 * j] = v[t].x;
+              dst[2 * j + 1] = v[t].y;
+            }
+          }
+        }
       }
-      for (; i < 2 * cc; i += 64) dst[i] = src[i];
     }
     if (!__syncthreads_or(rerun)) continue;
     if (!staged) {

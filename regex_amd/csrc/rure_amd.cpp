@@ -1934,6 +1934,13 @@ void rure_set_free(rure_set *rs) {
 }
 
 void rure_amd_release_scratch(void) { scratch_release(); }
+void rure_amd_scratch_stats(size_t *cached, size_t *live, long *handles) {
+  ScratchCache &c = scratch_cache();
+  std::lock_guard<std::mutex> g(c.mu);
+  if (cached) *cached = c.cached;
+  if (live) *live = c.live_bytes;
+  if (handles) *handles = g_live_handles.load();
+}
 
 size_t rure_set_len(rure_set *rs) { return rs->exprs.size(); }
 
