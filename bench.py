@@ -25,6 +25,10 @@ Other configs (for DESIGN.md's table; same timing protocol):
   c4  RegexSet of 64 patterns over 10M synthetic log lines (one mask per line)
   c5  `\\w+@\\w+\\.\\w+` find over one 16 GiB haystack per GPU, one planted
       match in its last MiB; records gathered across ranks
+  big `[a-q][^u-z]{13}x` find over 256K x 4 KiB random a-w haystacks (an x
+      planted per 2 KiB):
+      a 73,725-state forward DFA (past the u16 tables) on the u32 big-DFA
+      kernel, with the Pike VM it replaces timed beside it
 
 Prints ONE JSON line (rank 0) with the roofline of the scan kernel (HIP
 events on the launch stream, algorithmic bytes per launch; HBM traffic from
@@ -53,7 +57,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "rehearsal"])
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "big", "rehearsal"])
     ap.add_argument("--haystacks", type=int, default=1 << 20)
     ap.add_argument("--length", type=int, default=4096)
     ap.add_argument("--match-frac", type=float, default=0.01)
@@ -907,6 +911,91 @@ def run_rehearsal(ctx):
                     gather_ok=ok, counts=counts)
 
 
+BIG_PATTERN = r"[a-q][^u-z]{13}x"
+
+
+def run_big(ctx):
+    """A forward DFA past the u16 tables (SURVEY §8 a7 / VERDICT r2 item 7):
+    `[a-q][^u-z]{13}x` builds 73,725 states, run by big_dfa.hip from u32
+    column tables (hot rows in LDS, the rest from L2 / Infinity Cache).  The
+    Pike VM that served such automata before is timed once beside it; parity
+    against the oracle on a sample."""
+    import regex_amd as R
+    from regex_amd import _native as NN
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_py import OracleRegex
+    torch, args = ctx.torch, ctx.args
+    n, L = 1 << 18, 4096
+    # letters a-w with an `x` planted about every 2 KiB: most haystacks are
+    # scanned to their end (a match needs the 14 bytes before an `x` to fit)
+    g = torch.Generator(device=ctx.dev).manual_seed(0xB16 + ctx.rank)
+    hay = (torch.randint(0, 23, (n * L + 16,), generator=g, device=ctx.dev, dtype=torch.uint8) + ord("a"))
+    xs = torch.randint(0, n * L, (n * L // 2048,), generator=g, device=ctx.dev)
+    hay[xs] = ord("x")
+    t0 = time.perf_counter()
+    re = R.Regex(BIG_PATTERN)
+    info = re.dfa_info(3)
+    build_s = time.perf_counter() - t0
+    out = torch.empty((n, 2), dtype=torch.int64, device=ctx.dev)
+
+    def scan():
+        re.find_batch(hay, stride=L, length=L, count=n, out=out, stream=ctx.stream)
+
+    ctx.ramp(scan)
+    assert NN.rure_amd_last_fwd_path() == -6, "big-DFA kernel not taken"
+    sec = ctx.timed(scan)
+    kms = ctx.kernel_ms(scan)
+    res = out.cpu().numpy()
+    # Pike VM on the same batch (RURE_AMD_BIG=0 is read per call), untimed
+    os.environ["RURE_AMD_BIG"] = "0"
+    pk = out.clone()
+    torch.cuda.synchronize()
+    tp = time.perf_counter()
+    re.find_batch(hay, stride=L, length=L, count=n, out=pk, stream=ctx.stream)
+    torch.cuda.synchronize()
+    pike_s = time.perf_counter() - tp
+    del os.environ["RURE_AMD_BIG"]
+    same = bool(torch.equal(pk, out))
+    # oracle parity on a sample of haystacks
+    o = OracleRegex(re)
+    sample = list(range(0, n, n // 512))
+    buf = hay[: n * L].view(n, L)
+    bad = 0
+    for i in sample:
+        e = o.find(bytes(buf[i].cpu().numpy()))
+        gg = None if res[i, 0] < 0 else (int(res[i, 0]), int(res[i, 1]))
+        bad += gg != e
+    if bad:
+        sys.stderr.write("PARITY FAILURE (big): %d of %d sampled haystacks differ\n" % (bad, len(sample)))
+        sys.exit(3)
+    m = res[:, 0] >= 0
+    fwd = np.where(m, np.minimum(res[:, 1] + 1, L), L).sum()
+    rev = (res[m, 1] - res[m, 0]).sum()
+    b_alg = float(fwd + rev + 16 * n)
+    config = {"workload": "big: find %s (%d-state forward DFA, u32 tables) over %d x %d B random lowercase "
+                          "haystacks per GPU (a-w, an x per 2 KiB)" % (BIG_PATTERN, info["states"], n, L),
+              "haystacks_per_gpu": n, "haystack_bytes": L, "parallelism": "dp%d" % ctx.world}
+    extra = {}
+    if ctx.rank == 0 and not args.no_cpu:
+        reps, t1 = 0, time.perf_counter()
+        cs = [bytes(buf[i].cpu().numpy()) for i in range(0, 2048)]
+        while time.perf_counter() - t1 < min(args.cpu_seconds, 5.0):
+            for h in cs:
+                o.find(h)
+            reps += 1
+        el = time.perf_counter() - t1
+        extra["cpu_baseline"] = {"value": round(len(cs) * L * reps / el / 1e9, 4), "unit": "GB/s", "cores": 1,
+                                 "kind": "port", "sample": "%d passes over the first 2048 haystacks, one thread, "
+                                                           "oracle lazy DFA" % reps}
+    return ctx.line("haystack GB/s scanned, batched bytes::Regex::find (DFA > 65535 states)",
+                    n * L * ctx.world / sec / 1e9, "GB/s", sec * 1e3, "u8", "synthetic (seeded random a-w, planted x)", config,
+                    dfa_states=info["states"], dfa_columns=info["byte_classes"], dfa_build_s=round(build_s, 3),
+                    matched_haystacks=int(m.sum()), kernel_ms=round(kms, 4),
+                    pike_vm_GBps=round(n * L / pike_s / 1e9, 2), pike_vm_agrees=same,
+                    parity={"haystacks_checked": len(sample), "mismatches": 0, "against": "oracle lazy DFA"},
+                    roofline=roofline(b_alg / (kms * 1e-3) / 1e9, kms, b_alg, config), **extra)
+
+
 def run_c1(ctx):
     """BASELINE configs[0]: the date regex `is_match` over 1K x 1 KiB ASCII
     buffers.  The batched GPU call (latency-bound at this size: one launch
@@ -958,7 +1047,7 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus))
     ctx = Ctx(args)
-    line = {"c1": run_c1, "c2": run_c2, "c3": run_c3, "c4": run_c4, "c5": run_c5,
+    line = {"c1": run_c1, "c2": run_c2, "c3": run_c3, "c4": run_c4, "c5": run_c5, "big": run_big,
             "rehearsal": run_rehearsal}[args.config](ctx)
     if ctx.rank == 0:
         print(json.dumps(line), flush=True)

@@ -254,7 +254,9 @@ typedef struct rure_amd_dfa_info {
   int32_t fast_stride;   /* bytes per dependent LDS lookup in the tile kernel (1, 2, 4) */
   int32_t fast_classes;  /* local byte classes of the multi-byte table (K) */
 } rure_amd_dfa_info;
-/* which: 0 = forward DFA, 1 = reverse DFA, 2 = find_iter forward DFA. */
+/* which: 0 = forward DFA, 1 = reverse DFA, 2 = find_iter forward DFA,
+ * 3 / 4 = the forward / reverse automata past the u16 tables (u32 column
+ * form, built when 0 / 1 exceed 65535 states; byte_classes = columns). */
 int rure_amd_dfa_info_get(rure *re, int which, rure_amd_dfa_info *info);
 int rure_amd_set_dfa_info_get(rure_set *re, rure_amd_dfa_info *info);
 

@@ -97,14 +97,26 @@ class Builder {
     }
     const int nraw = (int)keys_.size();
     const auto t_built = std::chrono::steady_clock::now();
-    // Expand to 256 columns (QUIT override for non-ASCII bytes when the
-    // program has a Unicode word boundary, dfa.rs:1487-1496).
-    std::vector<uint32_t> t256((size_t)nraw * 256);
+    // Columns: the byte classes, split at 0x80 when the program has a
+    // Unicode word boundary (non-ASCII bytes quit, dfa.rs:1487-1496).
+    std::vector<int> colrep;
+    {
+      std::vector<int> seen(512, -1);
+      for (int b = 0; b < 256; ++b) {
+        const int key = p_.byte_classes[b] * 2 + ((quit_ && b >= 0x80) ? 1 : 0);
+        if (seen[key] < 0) { seen[key] = (int)colrep.size(); colrep.push_back(b); }
+        out->colmap[b] = (uint8_t)seen[key];
+      }
+    }
+    const int ncol = (int)colrep.size();
+    std::vector<uint32_t> tc((size_t)nraw * ncol);
     for (int s = 0; s < nraw; ++s)
-      for (int b = 0; b < 256; ++b)
-        t256[(size_t)s * 256 + b] =
-            (quit_ && b >= 0x80 && s != 0) ? 1u : trans_cls_[(size_t)s * ncls + p_.byte_classes[b]];
-    minimise(nraw, t256, out);
+      for (int j = 0; j < ncol; ++j) {
+        const int b = colrep[j];
+        tc[(size_t)s * ncol + j] = (quit_ && b >= 0x80 && s != 0) ? 1u : trans_cls_[(size_t)s * ncls + p_.byte_classes[b]];
+      }
+    std::vector<uint32_t>().swap(trans_cls_);
+    minimise(nraw, tc, ncol, out);
     out->raw_states = nraw;
     if (getenv("RURE_AMD_TIMING")) {  // diagnostic: construction and minimisation times
       const auto t_end = std::chrono::steady_clock::now();
@@ -481,17 +493,10 @@ class Builder {
 
   // Moore partition refinement over byte columns; outputs preserved:
   // single: (match flag, EOF match, dead, quit); set: (EOF match mask, dead, quit).
-  void minimise(int n, const std::vector<uint32_t> &t, DenseDfa *out) {
-    // distinct byte columns: transitions depend on the byte only through its
-    // class (plus the QUIT split for non-ASCII bytes)
-    std::vector<int> colrep;
-    {
-      std::vector<int> seen(512, -1);
-      for (int b = 0; b < 256; ++b) {
-        int key = p_.byte_classes[b] * 2 + ((quit_ && b >= 0x80) ? 1 : 0);
-        if (seen[key] < 0) { seen[key] = b; colrep.push_back(b); }
-      }
-    }
+  // t: n raw states x ncol columns (out->colmap maps bytes to columns).
+  void minimise(int n, const std::vector<uint32_t> &t, int ncol, DenseDfa *out) {
+    std::vector<int> colbyte(ncol, 0);  // a byte of each column
+    for (int b = 255; b >= 0; --b) colbyte[out->colmap[b]] = b;
     std::vector<uint32_t> block(n), nb(n);
     auto out_key = [&](int s) {
       std::string k;
@@ -512,7 +517,10 @@ class Builder {
       return k;
     };
     size_t nblocks;
-    {
+    if (!lim_.minimise) {  // every raw state its own block (DEAD and QUIT included)
+      for (int s = 0; s < n; ++s) block[s] = (uint32_t)s;
+      nblocks = (size_t)n;
+    } else {
       std::unordered_map<std::string, uint32_t> m;
       for (int s = 0; s < n; ++s) {
         auto it = m.emplace(out_key(s), (uint32_t)m.size()).first;
@@ -520,12 +528,12 @@ class Builder {
       }
       nblocks = m.size();
     }
-    while (true) {
+    while (lim_.minimise) {
       std::unordered_map<std::string, uint32_t> m;
       m.reserve(n * 2);
       for (int s = 0; s < n; ++s) {
         std::string sig((const char *)&block[s], 4);
-        for (int b : colrep) sig.append((const char *)&block[t[(size_t)s * 256 + b]], 4);
+        for (int j = 0; j < ncol; ++j) sig.append((const char *)&block[t[(size_t)s * ncol + j]], 4);
         if (strip_) sig.append((const char *)&block[strip_of(s)], 4);
         auto it = m.emplace(sig, (uint32_t)m.size()).first;
         nb[s] = it->second;
@@ -566,9 +574,9 @@ class Builder {
         uint32_t b = dq.front(); dq.pop_front();
         order_normal.push_back(b);
         int s = rep[b];
-        for (int c : colrep) {
-          if (c >= 0x80) continue;
-          uint32_t nb2 = block[t[(size_t)s * 256 + c]];
+        for (int j = 0; j < ncol; ++j) {
+          if (colbyte[j] >= 0x80) continue;   // columns of ASCII bytes
+          uint32_t nb2 = block[t[(size_t)s * ncol + j]];
           if (!seen[nb2] && is_ordinary(nb2)) { seen[nb2] = 1; dq.push_back(nb2); }
         }
       }
@@ -584,7 +592,7 @@ class Builder {
           else if (!seen[b]) order_normal.push_back(b);
         }
         int s = rep[b];
-        for (int c : colrep) push(block[t[(size_t)s * 256 + c]]);
+        for (int j = 0; j < ncol; ++j) push(block[t[(size_t)s * ncol + j]]);
       }
     }
     int next = 0;
@@ -599,13 +607,25 @@ class Builder {
     out->nstates = next;
     out->is_set = is_set_;
     out->reverse = p_.is_reverse;
-    out->trans.assign((size_t)next * 256, 0);
+    out->ncol = (uint32_t)ncol;
     out->eof_match.assign(next, 0);
     out->eof_mask.assign(next, 0);
     out->now_mask.assign(next, 0);
+    if (lim_.columns) {
+      out->trans.clear();
+      out->ctrans.assign((size_t)next * ncol, 0);
+    } else {
+      out->trans.assign((size_t)next * 256, 0);
+      out->ctrans.clear();
+    }
     for (uint32_t b = 0; b < nblocks; ++b) {
       int s = rep[b], id = newid[b];
-      for (int c = 0; c < 256; ++c) out->trans[(size_t)id * 256 + c] = newid[block[t[(size_t)s * 256 + c]]];
+      if (lim_.columns) {
+        for (int j = 0; j < ncol; ++j) out->ctrans[(size_t)id * ncol + j] = newid[block[t[(size_t)s * ncol + j]]];
+      } else {
+        for (int c = 0; c < 256; ++c)
+          out->trans[(size_t)id * 256 + c] = newid[block[t[(size_t)s * ncol + out->colmap[c]]]];
+      }
       out->eof_match[id] = eof_match_[s];
       out->eof_mask[id] = eof_mask_[s];
       if (is_set_) out->now_mask[id] = now_of(keys_[s]);

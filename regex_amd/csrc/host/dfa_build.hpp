@@ -43,12 +43,23 @@ struct DenseDfa {
   // as s minus the `.*?` prefix, i.e. no new match may start from here on
   // (used to end a search once it crosses a chunk cut).
   std::vector<uint32_t> strip;
+  // Column form (DfaBuildLimits::columns, the u32 tables of automata past
+  // 65535 states): trans is empty and ctrans holds nstates * ncol next states,
+  // column colmap[b] for byte b (the byte classes, split at 0x80 when a
+  // Unicode word boundary makes non-ASCII bytes quit).
+  uint32_t ncol = 0;
+  uint8_t colmap[256] = {0};
+  std::vector<uint32_t> ctrans;
 };
 
 struct DfaBuildLimits {
   int max_raw_states = 1 << 16;
   bool strip = false;
+  bool columns = false;   // emit ctrans / colmap instead of the 256-wide trans
+  bool minimise = true;   // false: raw states kept (same language, more states)
 };
+// Raw-state budget of the u32 (column form) automata.
+constexpr int kBigDfaRawStates = 1 << 21;
 
 // Builds the DFA for `prog` (a forward DFA program with `.*?` unless anchored,
 // or a reverse program).  Returns false (with `err`) if the state budget is

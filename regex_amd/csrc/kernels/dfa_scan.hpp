@@ -308,6 +308,25 @@ hipError_t launch_dfa_anchored_rev(int mode, const BatchDev &b, const RevDfaDev 
                                    int grid);
 hipError_t launch_dfa_set(const BatchDev &b, const SetDfaDev &f, uint64_t *out, hipStream_t st, int grid);
 
+// An automaton past the u16 tables (more than 65535 states, host
+// kBigDfaRawStates budget): u32 next states in column form, trans[s * ncol +
+// colmap[b]], same state numbering as FwdDfaDev / RevDfaDev (no quit state:
+// programs with a Unicode word boundary keep the Pike VM).  The first `hot`
+// rows are staged in LDS (states in BFS order from the start states).
+struct BigDfaDev {
+  const uint32_t *trans;
+  const uint8_t *colmap;      // 256 bytes
+  const uint8_t *eof;         // nstates
+  const uint32_t *start;      // 128 start states by flag index
+  uint32_t ncol, nstates, hot, n_normal, n_match_end, dead, ustart1;
+};
+// find / is_match / shortest_match over a batch, one lane per haystack:
+// find_dfa_forward (exec.rs:632-662) with the big forward and reverse DFAs.
+hipError_t launch_big_dfa(int mode, const BatchDev &b, const BigDfaDev &f, const BigDfaDev &r, void *out,
+                          hipStream_t st, int cus);
+// Rows of a big forward DFA the kernel holds in LDS.
+uint32_t big_dfa_hot_rows(uint32_t ncol, uint32_t nstates);
+
 // Scratch device memory for the scans, cached by the library (rure_amd.cpp):
 // a freed block is kept with an event recorded on the freeing stream and
 // reused, after a wait on that event, by the next allocation of at most twice

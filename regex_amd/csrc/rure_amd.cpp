@@ -70,6 +70,8 @@ struct DevTables {
   bool cores_adapted = false;
   void *core_blob = nullptr;  // re-ranked core tables (adapt_cores)
   bool has_dfa = false;     // the DFA materialised (else: Pike VM only)
+  bool has_big = false;     // big (u32) forward / reverse automata: bf, br
+  BigDfaDev bf{}, br{};
   bool quit_possible = false;  // the DFA can quit (Unicode \b): Pike VM fallback pass
   bool anchored_rev = false;   // MatchType::DfaAnchoredReverse (exec.rs:1175-1177)
   // The reference's match type where its searches differ from a forward DFA
@@ -617,6 +619,10 @@ struct rure {
   std::string dfa_err;
   DenseDfa dfwd, drev;
   PackedFwd pf, pr;   // forward / reverse hot tables
+  // automata past the u16 tables (column form, u32; big_dfa.hip): batched
+  // find / is_match / shortest_match only, when dfa_ok is false
+  bool big_ok = false;
+  DenseDfa bfwd, brev;
   NfaTables nt;
   bool nfa_ok = false;
   std::map<int, DevTables> dev;
@@ -698,6 +704,32 @@ SyntaxFlags syntax_flags(uint32_t flags) {  // rure.rs:119-124
 // Builds the automata of a regex once: the DFAs (when they materialise
 // within budget) and always the Pike VM closure tables.  Returns whether a
 // search engine is available.
+// Automata past the u16 tables (more than 65535 states): both directions in
+// column form with the larger raw-state budget, for the big_dfa.hip kernels.
+// Programs with a Unicode word boundary (quit states) keep the Pike VM, and
+// so does a search the reference runs as DfaAnchoredReverse.
+void build_big_dfas(rure *re) {
+  re->big_ok = false;
+  if (!re->nfa_ok) return;
+  if (re->fwd.has_unicode_word_boundary || re->rev.has_unicode_word_boundary) return;
+  if (!re->nfa.anchored_start && re->nfa.anchored_end) return;
+  DfaBuildLimits lim;
+  lim.max_raw_states = kBigDfaRawStates;
+  lim.columns = true;
+  lim.minimise = false;   // construction already shares step targets; refinement doubled the build time
+  std::string e1, e2;
+  bool rok = false;
+  std::thread rt([&] { rok = build_dense_dfa(re->rev, lim, &re->brev, &e2); });
+  const bool fok = build_dense_dfa(re->fwd, lim, &re->bfwd, &e1);
+  rt.join();
+  if (!fok || !rok || re->bfwd.quit >= 0 || re->brev.quit >= 0) {
+    re->bfwd = DenseDfa();
+    re->brev = DenseDfa();
+    return;
+  }
+  re->big_ok = true;
+}
+
 bool build_regex(rure *re) {
   std::lock_guard<std::mutex> g(re->mu);
   if (re->built) return re->dfa_ok || re->nfa_ok;
@@ -715,6 +747,7 @@ bool build_regex(rure *re) {
   if (!fwd_ok || !rev_ok || !pack_forward(re->dfwd, &re->pf, &err) || !pack_forward(re->drev, &re->pr, &err, true)) {
     re->dfa_err = err.empty() ? "reverse DFA too large" : err;
     re->dfa_ok = false;
+    build_big_dfas(re);
     if (!re->nfa_ok) re->dfa_err += "; " + nerr;
     return re->nfa_ok;
   }
@@ -888,6 +921,16 @@ DevTables *regex_device(rure *re, std::string *err) {
     o_rstart = b.add(rstart.data(), 256);
     o_rlds = b.add(re->pr.lds.data(), re->pr.lds.size());
   }
+  size_t o_big[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (re->big_ok) {
+    const DenseDfa *bd[2] = {&re->bfwd, &re->brev};
+    for (int k = 0; k < 2; ++k) {
+      o_big[4 * k] = b.add(bd[k]->ctrans.data(), bd[k]->ctrans.size() * 4);
+      o_big[4 * k + 1] = b.add(bd[k]->colmap, 256);
+      o_big[4 * k + 2] = b.add(bd[k]->eof_match.data(), bd[k]->eof_match.size());
+      o_big[4 * k + 3] = b.add(bd[k]->start, 128 * 4);
+    }
+  }
   const bool mt_lane = needs_mt_lane(re->xl);
   LitOffsets lp{}, ls{};
   size_t o_lcs = 0;
@@ -948,6 +991,26 @@ DevTables *regex_device(rure *re, std::string *err) {
     // a regex anchored at the end and not at the start runs the reverse DFA
     // from the end of the text (exec.rs:1175-1177, 671-688)
     t.anchored_rev = !re->nfa.anchored_start && re->nfa.anchored_end;
+  }
+  if (re->big_ok) {
+    const DenseDfa *bd[2] = {&re->bfwd, &re->brev};
+    BigDfaDev *dst[2] = {&t.bf, &t.br};
+    for (int k = 0; k < 2; ++k) {
+      const DenseDfa &D = *bd[k];
+      BigDfaDev &x = *dst[k];
+      x.trans = (const uint32_t *)(base + o_big[4 * k]);
+      x.colmap = base + o_big[4 * k + 1];
+      x.eof = base + o_big[4 * k + 2];
+      x.start = (const uint32_t *)(base + o_big[4 * k + 3]);
+      x.ncol = D.ncol;
+      x.nstates = (uint32_t)D.nstates;
+      x.hot = k == 0 ? big_dfa_hot_rows(D.ncol, (uint32_t)D.nstates) : 0;
+      x.n_normal = (uint32_t)D.n_normal;
+      x.n_match_end = (uint32_t)D.n_match_end;
+      x.dead = (uint32_t)D.dead;
+      x.ustart1 = uniform_start(D);
+    }
+    t.has_big = true;
   }
   if (t.quit_possible && !re->nfa_ok) {
     (void)hipFree(t.blob);
@@ -1402,9 +1465,21 @@ hipError_t run_lane_search(int mode, const BatchDev &b, const DevTables &t, void
   return e;
 }
 
+// The big-DFA kernel runs one lane per haystack: for batches that fill the
+// device (a handful of long haystacks stay on the Pike VM, which spreads one
+// haystack over a wave).  RURE_AMD_BIG=2 forces it (tests), =0 keeps the
+// Pike VM (A/B; read per call).
+bool big_batch(const BatchDev &b, const DevTables &t) {
+  const char *env = getenv("RURE_AMD_BIG");
+  if (env && env[0] == '2') return true;
+  if (env && env[0] == '0') return false;
+  return b.count >= (uint64_t)t.cus * 64;
+}
+
 hipError_t run_regex(int mode, const BatchDev &b, const DevTables &t, void *out, hipStream_t st, int dfa_grid,
                      const FwdDfaDev *iter = nullptr) {
   if (lane_search_ok(t)) return run_lane_search(mode, b, t, out, st);
+  if (!t.has_dfa && t.has_big && big_batch(b, t)) return launch_big_dfa(mode, b, t.bf, t.br, out, st, t.cus);
   if (!t.has_dfa) return run_pike(mode, false, b, t, out, st);
   uint64_t chunk = 0;
   if (iter && long_batch(mode, b, t, &chunk) && !(t.anchored_rev && b.start != 0))
@@ -2527,6 +2602,13 @@ int rure_amd_split_batch(rure *re, const rure_amd_batch *batch, size_t limit, ui
 int rure_amd_dfa_info_get(rure *re, int which, rure_amd_dfa_info *info) {
   if (!re || !info) return RURE_AMD_ERR_ARG;
   memset(info, 0, sizeof(*info));
+  if (which == 3 || which == 4) {  // the big (u32 column form) automata
+    build_regex(re);
+    if (!re->big_ok) { info->ok = 0; return RURE_AMD_ERR_DFA; }
+    fill_info(which == 3 ? re->bfwd : re->brev, which == 3 ? re->fwd : re->rev, 0, info);
+    info->byte_classes = (int32_t)(which == 3 ? re->bfwd.ncol : re->brev.ncol);
+    return RURE_AMD_OK;
+  }
   if (!build_regex_dfas(re)) { info->ok = 0; return RURE_AMD_ERR_DFA; }
   if (which == 0) fill_info(re->dfwd, re->fwd, re->pf.hot, info, &re->pf);
   else if (which == 1) fill_info(re->drev, re->rev, re->pr.hot, info);
