@@ -9,7 +9,7 @@ HOST_SRC = regex_amd/csrc/host/syntax.cpp regex_amd/csrc/host/compile.cpp regex_
 RT_SRC = regex_amd/csrc/rure_amd.cpp
 KERNEL_SRC = regex_amd/csrc/kernels/dfa_scan.hip regex_amd/csrc/kernels/nfa_scan.hip regex_amd/csrc/kernels/iter_scan.hip \
              regex_amd/csrc/kernels/replace_scan.hip regex_amd/csrc/kernels/gather_scan.hip \
-             regex_amd/csrc/kernels/match_types.hip regex_amd/csrc/kernels/big_dfa.hip
+             regex_amd/csrc/kernels/match_types.hip regex_amd/csrc/kernels/big_dfa.hip regex_amd/csrc/kernels/set_multi.hip
 KERNEL_OBJ = $(patsubst regex_amd/csrc/kernels/%.hip,$(OBJDIR)/%.o,$(KERNEL_SRC))
 HDRS = $(wildcard regex_amd/csrc/host/*.hpp regex_amd/csrc/host/*.h regex_amd/csrc/kernels/*.hpp include/*.h)
 OBJDIR = regex_amd/build

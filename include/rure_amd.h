@@ -235,6 +235,12 @@ size_t rure_amd_captures_len(rure *re);
  * Also done when the last rure / rure_set is freed.  Safe at any time: each
  * block is freed after the kernels that last used it. */
 void rure_amd_release_scratch(void);
+/* Sets searched as several automata in one pass (set_multi.hip: the
+ * 64-pattern groups of a larger set): after the first batched call, the
+ * number of groups run together (0: one pass per group), the LDS image size
+ * and the smallest share of a profiled sample's visits that stayed in a
+ * group's LDS-resident cores (the rule that picks one pass, >= 0.995). */
+int rure_amd_set_multi_info(rure_set *rs, uint32_t *groups, uint32_t *lds_bytes, double *coverage);
 // Scratch bookkeeping: bytes cached for reuse, bytes held by calls in
 // flight, and the number of rure / rure_set handles alive.
 void rure_amd_scratch_stats(size_t *cached, size_t *live, long *handles);

@@ -863,6 +863,13 @@ class RegexSet(object):
     def nfa_tables(self):
         return _nfa_export(N.rure_amd_set_nfa_export, self._set)
 
+    def multi_info(self):
+        """After a batched call: {"groups", "lds_bytes", "coverage"} of the
+        one-pass multi-group kernel (groups 0: one pass per group)."""
+        g, l, c = ctypes.c_uint32(0), ctypes.c_uint32(0), ctypes.c_double(0)
+        N.rure_amd_set_multi_info(self._set, ctypes.byref(g), ctypes.byref(l), ctypes.byref(c))
+        return {"groups": g.value, "lds_bytes": l.value, "coverage": c.value}
+
     def dfa_info(self):
         info = N.DfaInfo()
         rc = N.rure_amd_set_dfa_info_get(self._set, ctypes.byref(info))

@@ -167,6 +167,8 @@ rure_amd_literals_op = _sig("rure_amd_literals_op", ctypes.c_int64, ctypes.c_int
 rure_amd_exec_literals_export = _sig("rure_amd_exec_literals_export", ctypes.c_int64, VP, ctypes.c_int, VP, c_size)
 rure_amd_match_info_get = _sig("rure_amd_match_info_get", ctypes.c_int, VP, VP)
 rure_amd_release_scratch = _sig("rure_amd_release_scratch", None)
+rure_amd_set_multi_info = _sig("rure_amd_set_multi_info", ctypes.c_int, VP, ctypes.POINTER(ctypes.c_uint32),
+                               ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_double))
 rure_amd_scratch_stats = _sig("rure_amd_scratch_stats", None, ctypes.POINTER(c_size), ctypes.POINTER(c_size),
                               ctypes.POINTER(ctypes.c_long))
 rure_amd_kernel_timer = _sig("rure_amd_kernel_timer", ctypes.c_int, ctypes.c_int)

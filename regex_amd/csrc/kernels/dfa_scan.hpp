@@ -21,6 +21,9 @@ struct BatchDev {
   // set (atomic OR) by the DFA kernels when a haystack's DFA quit; the Pike VM
   // fallback pass then runs, else it returns at once (nullptr: always runs)
   uint32_t *quit_flag = nullptr;
+  // set masks (the Pike VM's MODE_SET): words between consecutive haystacks'
+  // masks (the set groups of set_multi.hip write word g of `words`)
+  uint32_t out_stride = 1;
 };
 
 // Forward DFA on the device.  State ids: [0, hot) are in the LDS fast table
@@ -167,6 +170,32 @@ struct SetCoreDev {
   const uint16_t *mid;        // profile only: ncores x K mask id + 1 of gout (0: none)
 };
 hipError_t launch_set_cores(const BatchDev &b, const SetCoreDev &f, uint64_t *out, hipStream_t st, int cus);
+
+// Several core-form set automata run side by side over each haystack in one
+// pass (set_multi.hip): the groups of a set of more than 64 patterns (group
+// g = patterns 64 g .. 64 g + 63, mask word g), or a set split into smaller
+// groups (A/B, RURE_AMD_SET_CHAINS).  Each lane steps every group's chain
+// over the same bytes.  Per group, in the combined LDS image: a 256-entry u16
+// class map holding 2k (k = the byte's class), its hot
+// rows ((hot + 1) x (K + 1) u16, SetCoreDev layout), its 64 code masks, its
+// 128 start cores and its hot cores' EOF masks.
+constexpr int kMultiMaxGroups = 4;
+struct MultiGroupDev {
+  const uint16_t *gcore;
+  const uint64_t *gout;
+  const uint64_t *eof;
+  uint64_t all;
+  uint32_t K, hot, dead, quit;                          // quit = 0xFFFFFFFF if none
+  uint32_t cls_off, rows_off, mt_off, st_off, he_off;   // LDS byte offsets
+  uint32_t word, shift;                                 // where its mask goes
+};
+struct MultiCoreDev {
+  const uint8_t *lds_image;
+  uint32_t lds_bytes, G, words;
+  uint32_t split;   // groups share word 0 (a split set): a quit marks the whole word
+  MultiGroupDev g[kMultiMaxGroups];
+};
+hipError_t launch_set_multi(const BatchDev &b, const MultiCoreDev &f, uint64_t *out, hipStream_t st, int cus);
 hipError_t launch_core_profile(const BatchDev &b, const SetCoreDev &f, uint64_t count, unsigned int *visits,
                                unsigned int *mask_counts, hipStream_t st, int cus);
 

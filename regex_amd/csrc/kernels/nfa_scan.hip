@@ -50,7 +50,7 @@ __global__ __launch_bounds__(64) void pike_kernel(BatchDev bt, NfaDev nf, void *
     if (need && FALLBACK) {
       if (MODE == MODE_FIND) need = ((const uint64_t *)out)[2 * hh] == QUITMARK;
       else if (MODE == MODE_ISMATCH) need = ((const uint8_t *)out)[hh] == 2;
-      else need = ((const uint64_t *)out)[hh] == QUITMARK;
+      else need = ((const uint64_t *)out)[hh * bt.out_stride] == QUITMARK;
     }
     uint64_t todo = __ballot(need);
     while (todo) {
@@ -78,7 +78,7 @@ __global__ __launch_bounds__(64) void pike_kernel(BatchDev bt, NfaDev nf, void *
         } else if (MODE == MODE_SHORTEST) {
           ((uint64_t *)out)[h] = r1;
         } else {
-          ((uint64_t *)out)[h] = r0;
+          ((uint64_t *)out)[h * bt.out_stride] = r0;
         }
       }
     }

@@ -254,6 +254,7 @@ struct CoreSet {
   // = 1 + the index of gout's mask in `masks` (0: none), for the profile.
   uint64_t codemask[64] = {0};
   uint32_t mt_off = 0;
+  uint64_t hot_visits = 0;        // with visit weights: the visits to the hot cores
   std::vector<uint64_t> masks;
   std::vector<uint16_t> mid;
 };
@@ -272,7 +273,8 @@ size_t core_lds_budget() {
 // Without it, masks rank by the number of hot transitions reporting them.
 bool build_set_cores(const DenseDfa &d, size_t lds_budget, CoreSet *cs,
                      const std::vector<uint64_t> *weights = nullptr,
-                     const std::unordered_map<uint64_t, uint64_t> *mask_weights = nullptr) {
+                     const std::unordered_map<uint64_t, uint64_t> *mask_weights = nullptr,
+                     const std::vector<uint64_t> *state_weights = nullptr) {
   const int S = d.nstates;
   std::unordered_map<std::string, uint32_t> key_core;
   std::vector<uint32_t> core_of(S);
@@ -297,6 +299,12 @@ bool build_set_cores(const DenseDfa &d, size_t lds_budget, CoreSet *cs,
     for (int b = 0; b < 128; ++b) push(core_of[d.trans[(size_t)rep[c] * 256 + b]]);
   }
   for (uint32_t c = 0; c < nc; ++c) push(c);
+  std::vector<uint64_t> sw;
+  if (!weights && state_weights) {  // per-state visit counts summed per core
+    sw.assign(nc, 0);
+    for (int s2 = 0; s2 < S; ++s2) sw[core_of[s2]] += (*state_weights)[s2];
+    weights = &sw;
+  }
   if (weights) {
     std::vector<uint32_t> bfs = order;
     std::stable_sort(order.begin(), order.end(),
@@ -330,6 +338,9 @@ bool build_set_cores(const DenseDfa &d, size_t lds_budget, CoreSet *cs,
   const uint32_t KL = K + 1;
   // (the image: class map, (hot + 1) rows, the 64 code masks)
   uint32_t hot = (uint32_t)std::min<size_t>({(size_t)nc, 1023, (lds_budget - 256 - 64 * 8 - 16) / (2 * KL) - 1});
+  cs->hot_visits = 0;
+  if (weights)
+    for (uint32_t r = 0; r < hot; ++r) cs->hot_visits += (*weights)[order[r]];
   cs->K = K;
   cs->ncores = nc;
   cs->hot = hot;
@@ -666,7 +677,12 @@ struct rure_set {
   // groups' answers concatenated are the set's.  The combined programs are
   // still compiled (size limit, program export).
   std::vector<rure_set *> groups;
+  struct MultiSet *multi = nullptr;   // the groups as one pass (build_multi)
 };
+
+namespace {
+void free_multi(rure_set *rs);
+}  // namespace
 
 struct rure_captures {           // rure.rs Captures(Locations): 2 slots per group
   std::vector<uint64_t> slots;
@@ -1994,6 +2010,7 @@ rure_set *rure_compile_set(const uint8_t **patterns, const size_t *lens, size_t 
 
 void rure_set_free(rure_set *rs) {
   if (!rs) return;
+  free_multi(rs);
   if (rs->single) rure_free(rs->single);
   for (rure_set *g : rs->groups) rure_set_free(g);
   for (auto &kv : rs->dev) {
@@ -2164,6 +2181,307 @@ int set_batch_word(rure_set *rs, const BatchDev &b, uint64_t *mask, hipStream_t 
 }
 
 // Group g (patterns [64 g, 64 g + len)) into word g of mask (words per haystack).
+// ------------------------------------------------- sets as one pass (groups)
+// A set of more than 64 patterns is searched as its 64-pattern groups
+// (rure_set::groups), one pass over the batch per group.  With
+// RURE_AMD_SET_MULTI=1, build_multi puts every group's core-form automaton
+// in one LDS image and set_multi.hip steps all of them over each haystack
+// read once; RURE_AMD_SET_CHAINS=G (2..4) splits a set of at most 64
+// patterns into G groups the same way.  Measured (tools/bigset_bench.py,
+// DESIGN.md §4.3): the chains share the VALU and LDS issue slots the single
+// chain already saturates, and the split LDS holds fewer hot cores, so one
+// pass is slower (C4 as 2 chains 1.50 vs 0.64 ms; 100 patterns 4.95 vs
+// 1.39 ms per-group) though it reads the text once; per-group passes stay
+// the default.
+}  // namespace
+struct MultiSet {
+  bool built = false, ok = false;
+  std::vector<rure_set *> owned;   // split groups (RURE_AMD_SET_CHAINS), freed with the set
+  std::vector<rure_set *> parts;
+  std::vector<uint32_t> word, shift;
+  std::vector<CoreSet> cores;
+  std::vector<uint8_t> lds;
+  MultiCoreDev proto{};            // offsets and scalars; pointers filled per device
+  bool quit = false;               // some group can quit: Pike VM fallback passes
+  double coverage = 1.0;           // smallest share of sampled visits in a group's hot cores
+  std::map<int, std::pair<void *, MultiCoreDev>> dev;
+};
+namespace {
+
+int set_chains() {
+  const char *v = getenv("RURE_AMD_SET_CHAINS");
+  return v ? std::max(1, std::min(kMultiMaxGroups, atoi(v))) : 1;
+}
+
+int device_cus_cached() {
+  int d = 0;
+  (void)hipGetDevice(&d);
+  static std::mutex mu;
+  static std::map<int, int> cache;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cache.find(d);
+  if (it != cache.end()) return it->second;
+  return cache[d] = device_cus(d);
+}
+
+void free_multi(rure_set *rs) {
+  MultiSet *m = rs->multi;
+  if (!m) return;
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  for (auto &kv : m->dev) {
+    (void)hipSetDevice(kv.first);
+    (void)hipFree(kv.second.first);
+  }
+  (void)hipSetDevice(cur);
+  for (rure_set *x : m->owned) rure_set_free(x);
+  delete m;
+  rs->multi = nullptr;
+}
+
+bool multi_fail(int why) {  // diagnostic (RURE_AMD_MULTI_DEBUG): which rule declined one pass
+  if (getenv("RURE_AMD_MULTI_DEBUG")) fprintf(stderr, "set_multi: not built (%d)\n", why);
+  return false;
+}
+
+bool build_multi_locked(rure_set *rs, MultiSet *m, std::string *err, const std::vector<std::string> *sample,
+                        size_t sample_start) {
+  const char *on = getenv("RURE_AMD_SET_MULTI");
+  if (!(on && on[0] == '1')) return multi_fail(1);
+  if (!rs->groups.empty()) {
+    for (size_t g = 0; g < rs->groups.size(); ++g) {
+      m->parts.push_back(rs->groups[g]);
+      m->word.push_back((uint32_t)g);
+      m->shift.push_back(0);
+    }
+  } else {
+    const int G = set_chains();
+    const size_t n = rs->exprs.size();
+    if (G < 2 || n < (size_t)G) return multi_fail(2);
+    const size_t per = (n + G - 1) / G;
+    for (size_t lo = 0; lo < n; lo += per) {
+      const size_t cnt = std::min(per, n - lo);
+      std::vector<const uint8_t *> ps;
+      std::vector<size_t> ls;
+      for (size_t i = lo; i < lo + cnt; ++i) {
+        ps.push_back((const uint8_t *)rs->patterns[i].data());
+        ls.push_back(rs->patterns[i].size());
+      }
+      rure_error e;
+      rure_set *x = rure_compile_set(ps.data(), ls.data(), cnt, rs->flags, &rs->opts, &e);
+      if (!x) { if (err) *err = e.msg; return multi_fail(3); }
+      m->owned.push_back(x);
+      m->parts.push_back(x);
+      m->word.push_back(0);
+      m->shift.push_back((uint32_t)lo);
+    }
+  }
+  const int G = (int)m->parts.size();
+  if (G < 2 || G > kMultiMaxGroups) return multi_fail(4);
+  for (rure_set *x : m->parts)
+    if (x->single || !build_set_dfa(x)) return multi_fail(5);
+  // quit states (Unicode \b): the Pike VM redoes the words a lane quit in,
+  // with each group's NFA (one word each) or the whole set's (split sets)
+  if (rs->groups.empty() && !rs->nfa_ok) return multi_fail(6);  // (built by multi_device before the lock)
+  // which cores the batch visits (the hot LDS rows) and which masks it
+  // reports (the 62 LDS codes): each group's DFA run on the host over a
+  // sample of the first batch (one copy + sync, once per set, like
+  // adapt_cores)
+  std::vector<std::vector<uint64_t>> sw(G);
+  std::vector<std::unordered_map<uint64_t, uint64_t>> mw(G);
+  if (sample && !sample->empty()) {
+    for (int g = 0; g < G; ++g) {
+      const DenseDfa &d = m->parts[g]->dfa;
+      sw[g].assign(d.nstates, 0);
+      for (const std::string &line : *sample) {
+        const uint8_t *tx = (const uint8_t *)line.data();
+        const size_t len = line.size();
+        if (sample_start > len) continue;
+        uint32_t c = d.start[start_flag_index_fwd(tx, len, sample_start)];
+        for (size_t i = sample_start; i < len && (int)c != d.dead && (int)c != d.quit; ++i) {
+          c = d.trans[(size_t)c * 256 + tx[i]];
+          ++sw[g][c];
+          if (d.now_mask[c]) ++mw[g][d.now_mask[c]];
+        }
+      }
+    }
+  }
+  // one LDS image for all groups: each group's share of 159 KiB, shrunk
+  // until the image fits (class map 512 B, rows, code masks 512 B, start
+  // cores 256 B, hot EOF masks 8 B per hot core)
+  const size_t L = 159 * 1024;
+  size_t bud = L / G;
+  m->cores.assign(G, CoreSet());
+  auto al16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+  for (int tries = 0;; ++tries) {
+    size_t total = 0;
+    for (int g = 0; g < G; ++g) {
+      m->cores[g] = CoreSet();
+      const bool prof = sample && !sample->empty();
+      if (!build_set_cores(m->parts[g]->dfa, bud, &m->cores[g], nullptr, prof ? &mw[g] : nullptr,
+                           prof ? &sw[g] : nullptr))
+        return multi_fail(7);
+      const CoreSet &cs = m->cores[g];
+      total += 512 + al16((size_t)(cs.hot + 1) * (cs.K + 1) * 2) + 512 + 256 + al16(8 * (size_t)cs.hot);
+    }
+    if (total <= L) break;
+    if (tries > 16 || bud < 16 * 1024) return multi_fail(8);
+    bud -= 4 * 1024;
+  }
+  // The share of the sample's visits that stays in every group's LDS cores
+  // (the LDS is split between the groups), for rure_amd_set_multi_info.
+  m->coverage = 1.0;
+  if (sample && !sample->empty()) {
+    for (int g = 0; g < G; ++g) {
+      uint64_t tot = 0;
+      for (uint64_t v : sw[g]) tot += v;
+      const double cov = tot ? (double)m->cores[g].hot_visits / (double)tot : 1.0;
+      m->coverage = std::min(m->coverage, cov);
+    }
+  }
+  MultiCoreDev &P = m->proto;
+  P = MultiCoreDev{};
+  P.G = (uint32_t)G;
+  P.split = rs->groups.empty() ? 1u : 0u;
+  size_t cur = 0;
+  for (int g = 0; g < G; ++g) {
+    const CoreSet &cs = m->cores[g];
+    MultiGroupDev &d = P.g[g];
+    const size_t rows = (size_t)(cs.hot + 1) * (cs.K + 1) * 2;
+    d.K = cs.K;
+    d.hot = cs.hot;
+    d.dead = cs.dead;
+    d.quit = cs.quit;
+    if (cs.quit != 0xFFFFFFFFu) m->quit = true;
+    d.cls_off = (uint32_t)cur;
+    d.rows_off = (uint32_t)(cur + 512);
+    d.mt_off = (uint32_t)(d.rows_off + al16(rows));
+    d.st_off = d.mt_off + 512;
+    d.he_off = d.st_off + 256;
+    d.word = m->word[g];
+    d.shift = m->shift[g];
+    const size_t np = m->parts[g]->exprs.size();
+    d.all = np >= 64 ? ~0ull : ((1ull << np) - 1);
+    cur = d.he_off + al16(8 * (size_t)cs.hot);
+    m->lds.resize(cur, 0);
+    uint16_t *cm = (uint16_t *)(m->lds.data() + d.cls_off);
+    for (int b = 0; b < 256; ++b) cm[b] = (uint16_t)(2 * cs.lds[b]);
+    memcpy(m->lds.data() + d.rows_off, cs.lds.data() + 256, rows);
+    memcpy(m->lds.data() + d.mt_off, cs.codemask, 512);
+    memcpy(m->lds.data() + d.st_off, cs.start, 256);
+    memcpy(m->lds.data() + d.he_off, cs.eof.data(), 8 * (size_t)cs.hot);
+  }
+  m->lds.resize(al16(m->lds.size()), 0);
+  P.lds_bytes = (uint32_t)m->lds.size();
+  uint32_t words = 0;
+  for (int g = 0; g < G; ++g) words = std::max(words, P.g[g].word + 1);
+  P.words = words;
+  return true;
+}
+
+// Host copy of up to 4096 haystacks of the batch (the profile sample).
+std::vector<std::string> batch_sample(const BatchDev &b, hipStream_t st) {
+  std::vector<std::string> out;
+  const uint64_t n = std::min<uint64_t>(b.count, 4096);
+  if (!n) return out;
+  std::vector<uint64_t> offs(n + 1);
+  if (b.offs) {
+    if (hipMemcpyAsync(offs.data(), b.offs, (n + 1) * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      return out;
+  } else {
+    for (uint64_t i = 0; i <= n; ++i) offs[i] = i * b.stride;
+  }
+  const uint64_t lo = offs[0], hi = b.offs ? offs[n] : (n - 1) * b.stride + b.length;
+  std::vector<uint8_t> bytes(hi - lo);
+  if (hipMemcpyAsync(bytes.data(), b.hay + lo, hi - lo, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return out;
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint64_t a = offs[i] - lo, len = b.offs ? offs[i + 1] - offs[i] : b.length;
+    out.emplace_back((const char *)bytes.data() + a, len);
+  }
+  return out;
+}
+
+const MultiCoreDev *multi_device(rure_set *rs, std::string *err, const BatchDev &b, hipStream_t st) {
+  if (rs->groups.empty()) build_set(rs);  // split sets: the whole set's NFA (quit fallback); takes rs->mu
+  std::lock_guard<std::mutex> g(rs->mu);
+  if (!rs->multi) rs->multi = new MultiSet();
+  MultiSet *m = rs->multi;
+  if (!m->built) {
+    m->built = true;
+    const std::vector<std::string> sample = batch_sample(b, st);
+    m->ok = build_multi_locked(rs, m, err, &sample, b.start);
+  }
+  if (!m->ok) return nullptr;
+  int d = 0;
+  if (!hip_ok(hipGetDevice(&d), err)) return nullptr;
+  auto it = m->dev.find(d);
+  if (it != m->dev.end()) return &it->second.second;
+  Blob bl;
+  const int G = (int)m->parts.size();
+  size_t o_core[kMultiMaxGroups], o_out[kMultiMaxGroups], o_eof[kMultiMaxGroups];
+  for (int k = 0; k < G; ++k) {
+    const CoreSet &cs = m->cores[k];
+    o_core[k] = bl.add(cs.gcore.data(), cs.gcore.size() * 2);
+    o_out[k] = bl.add(cs.gout.data(), cs.gout.size() * 8);
+    o_eof[k] = bl.add(cs.eof.data(), cs.eof.size() * 8);
+  }
+  const size_t o_lds = bl.add(m->lds.data(), m->lds.size());
+  DevTables tmp;
+  if (!upload_blob(bl, &tmp, err)) return nullptr;
+  uint8_t *base = (uint8_t *)tmp.blob;
+  MultiCoreDev f = m->proto;
+  f.lds_image = base + o_lds;
+  for (int k = 0; k < G; ++k) {
+    f.g[k].gcore = (const uint16_t *)(base + o_core[k]);
+    f.g[k].gout = (const uint64_t *)(base + o_out[k]);
+    f.g[k].eof = (const uint64_t *)(base + o_eof[k]);
+  }
+  auto &slot = m->dev[d];
+  slot = std::make_pair(tmp.blob, f);
+  return &slot.second;
+}
+
+// The one-pass kernel, then (only where a lane quit: the Pike kernels read
+// the flag first) the Pike VM over the words marked QUITMARK.
+int run_set_multi(rure_set *rs, const BatchDev &b, const MultiCoreDev &f, uint64_t *mask, hipStream_t st) {
+  MultiSet *m = rs->multi;
+  const int cus = device_cus_cached();
+  if (getenv("RURE_AMD_MULTI_DEBUG")) {  // diagnostic: the combined image's layout
+    fprintf(stderr, "set_multi: G %u words %u split %u lds %u quit %d\n", f.G, f.words, f.split, f.lds_bytes,
+            (int)m->quit);
+    for (uint32_t g = 0; g < f.G; ++g)
+      fprintf(stderr, "  group %u: K %u hot %u dead %u quit %u cls %u rows %u mt %u st %u he %u word %u shift %u\n", g,
+              f.g[g].K, f.g[g].hot, f.g[g].dead, f.g[g].quit, f.g[g].cls_off, f.g[g].rows_off, f.g[g].mt_off,
+              f.g[g].st_off, f.g[g].he_off, f.g[g].word, f.g[g].shift);
+  }
+  if (!m->quit) return launch_set_multi(b, f, mask, st, cus) == hipSuccess ? RURE_AMD_OK : RURE_AMD_ERR_HIP;
+  std::string err;
+  BatchDev bq = b;
+  hipError_t e = scratch_malloc((void **)&bq.quit_flag, 4, st);
+  if (e == hipSuccess) e = hipMemsetAsync(bq.quit_flag, 0, 4, st);
+  if (e == hipSuccess) e = launch_set_multi(bq, f, mask, st, cus);
+  if (e == hipSuccess && f.split) {
+    const DevTables *t = set_device(rs, &err);
+    e = t ? run_pike(MODE_SET, true, bq, *t, mask, st) : hipErrorInvalidValue;
+  } else {
+    for (size_t g = 0; e == hipSuccess && g < m->parts.size(); ++g) {
+      const DevTables *t = set_device(m->parts[g], &err);
+      if (!t) { e = hipErrorInvalidValue; break; }
+      BatchDev bg = bq;
+      bg.out_stride = f.words;
+      e = run_pike(MODE_SET, true, bg, *t, mask + f.g[g].word, st);
+    }
+  }
+  if (bq.quit_flag) {
+    hipError_t e2 = scratch_free(bq.quit_flag, st);
+    if (e == hipSuccess) e = e2;
+  }
+  return e == hipSuccess ? RURE_AMD_OK : RURE_AMD_ERR_HIP;
+}
+
 int set_batch_group(rure_set *g, const rure_amd_batch *batch, const BatchDev &b, uint64_t *mask, size_t words,
                     size_t w, hipStream_t st) {
   void *tmp = nullptr;
@@ -2189,6 +2507,14 @@ int rure_amd_set_matches_batch_words(rure_set *rs, const rure_amd_batch *batch, 
   if (words < std::max<size_t>(1, (n + 63) / 64)) return RURE_AMD_ERR_ARG;
   if (b.count == 0) return RURE_AMD_OK;
   hipStream_t st = (hipStream_t)stream;
+  if (words <= (size_t)kMultiMaxGroups && (!rs->groups.empty() || set_chains() > 1)) {
+    std::string err;
+    if (const MultiCoreDev *md = multi_device(rs, &err, b, st)) {
+      MultiCoreDev f = *md;
+      f.words = (uint32_t)words;
+      return run_set_multi(rs, b, f, mask, st);
+    }
+  }
   if (words == 1 && n >= 2) return set_batch_word(rs, b, mask, st);
   if (hipMemsetAsync(mask, 0, b.count * words * 8, st) != hipSuccess) return RURE_AMD_ERR_HIP;
   if (n == 0) return RURE_AMD_OK;  // MatchType::Nothing (exec.rs:276-286)
@@ -2197,6 +2523,17 @@ int rure_amd_set_matches_batch_words(rure_set *rs, const rure_amd_batch *batch, 
     int rc = set_batch_group(rs->groups[g], batch, b, mask, words, g, st);
     if (rc != RURE_AMD_OK) return rc;
   }
+  return RURE_AMD_OK;
+}
+
+int rure_amd_set_multi_info(rure_set *rs, uint32_t *groups, uint32_t *lds_bytes, double *coverage) {
+  if (!rs) return RURE_AMD_ERR_ARG;
+  std::lock_guard<std::mutex> g(rs->mu);
+  const MultiSet *m = rs->multi;
+  const bool ok = m && m->built && m->ok;
+  if (groups) *groups = ok ? m->proto.G : 0;
+  if (lds_bytes) *lds_bytes = ok ? m->proto.lds_bytes : 0;
+  if (coverage) *coverage = m && m->built ? m->coverage : 0.0;
   return RURE_AMD_OK;
 }
 
