@@ -65,6 +65,8 @@ static void lits_free(orc_lits *l) {
   for (size_t i = 0; i < l->n; ++i) free(l->lit[i]);
   free(l->lit);
   free(l->len);
+  free(l->pair);
+  free(l->quad);
   memset(l, 0, sizeof(*l));
 }
 
@@ -79,6 +81,8 @@ void orc_regex_free(orc_regex *r) {
   free(r);
 }
 
+static inline uint32_t quad_hash(uint32_t w) { return (w * 0x9E3779B1u) >> 16; }
+
 static void lits_parse(orc_lits *l, const uint8_t *b, size_t n, int matcher) {
   lits_free(l);
   l->matcher = matcher;
@@ -92,6 +96,25 @@ static void lits_parse(orc_lits *l, const uint8_t *b, size_t n, int matcher) {
     l->len[l->n] = k;
     l->n++;
     i += 5 + k;
+  }
+  l->pair = (uint8_t *)calloc(65536 / 8, 1);
+  l->quad = (uint8_t *)calloc(65536 / 8, 1);
+  for (size_t j = 0; j < l->n; ++j) {
+    if (l->len[j] == 0) { l->any_empty = 1; continue; }
+    if (l->len[j] >= 4) {
+      uint32_t w;
+      memcpy(&w, l->lit[j], 4);
+      const uint32_t h = quad_hash(w);
+      l->quad[h >> 3] |= (uint8_t)(1u << (h & 7));
+      l->any_long = 1;
+      continue;
+    }
+    l->any_short = 1;
+    const uint8_t b0 = l->lit[j][0];
+    l->first[b0] = 1;
+    if (l->len[j] == 1) { l->single[b0] = 1; continue; }
+    const unsigned k = ((unsigned)b0 << 8) | l->lit[j][1];
+    l->pair[k >> 3] |= (uint8_t)(1u << (k & 7));
   }
 }
 
@@ -190,8 +213,13 @@ static int find_dfa_forward(const orc_regex *r, orc_cache *c, const uint8_t *tex
 /* Leftmost occurrence of `needle` in hay[0..n) (memmem), -1 if none. */
 static long find_sub(const uint8_t *hay, size_t n, const uint8_t *needle, size_t k) {
   if (k == 0) return 0;
-  for (size_t i = 0; i + k <= n; ++i)
-    if (hay[i] == needle[0] && memcmp(hay + i, needle, k) == 0) return (long)i;
+  for (size_t i = 0; i + k <= n;) {
+    const uint8_t *p = (const uint8_t *)memchr(hay + i, needle[0], n - k + 1 - i);
+    if (!p) return -1;
+    i = (size_t)(p - hay);
+    if (memcmp(p, needle, k) == 0) return (long)i;
+    ++i;
+  }
   return -1;
 }
 
@@ -199,26 +227,45 @@ static long find_sub(const uint8_t *hay, size_t n, const uint8_t *needle, size_t
  * matches the empty string at 0; Bytes the first byte of the set; one
  * literal its first occurrence; several (Teddy / Aho-Corasick) the leftmost
  * occurrence of any (the set is unambiguous: no member is a substring of
- * another, so one literal at most occurs at a position and the occurrence
- * that ends first is the leftmost). */
+ * another, so one literal at most occurs at a position; at a tie the first
+ * literal in order is taken).  One forward pass: a position is tested only
+ * when its first four bytes hash like a literal's (or its first bytes begin
+ * a literal of 1-3 bytes: lits_parse's tables), so a find_iter over a long
+ * text stays linear. */
+static int lit_at(const orc_lits *l, const uint8_t *hay, size_t n, size_t i, size_t *s, size_t *e) {
+  for (size_t j = 0; j < l->n; ++j) {
+    const size_t k = l->len[j];
+    if (k <= n - i && memcmp(hay + i, l->lit[j], k) == 0) {
+      *s = i;
+      *e = i + k;
+      return 1;
+    }
+  }
+  return 0;
+}
+
 static int lits_find(const orc_lits *l, const uint8_t *hay, size_t n, size_t *s, size_t *e) {
   if (l->matcher == 0) { *s = *e = 0; return 1; }
-  long best = -1;
-  size_t blen = 0;
-  for (size_t j = 0; j < l->n; ++j) {
-    size_t nj = n;  /* only occurrences starting before the best so far */
-    if (best >= 0) {
-      size_t cap = (size_t)best + l->len[j];
-      cap = cap ? cap - 1 : 0;
-      if (cap < nj) nj = cap;
+  if (l->any_empty) return lit_at(l, hay, n, 0, s, e);
+  for (size_t i = 0; i < n; ++i) {
+    int cand = 0;
+    if (l->any_long && i + 4 <= n) {
+      uint32_t w;
+      memcpy(&w, hay + i, 4);
+      const uint32_t h = quad_hash(w);
+      cand = (l->quad[h >> 3] >> (h & 7)) & 1;
     }
-    long i = find_sub(hay, nj, l->lit[j], l->len[j]);
-    if (i >= 0 && (best < 0 || i < best)) { best = i; blen = l->len[j]; }
+    if (!cand && l->any_short) {
+      const uint8_t b = hay[i];
+      if (l->single[b]) cand = 1;
+      else if (l->first[b] && i + 1 < n) {
+        const unsigned k = ((unsigned)b << 8) | hay[i + 1];
+        cand = (l->pair[k >> 3] >> (k & 7)) & 1;
+      }
+    }
+    if (cand && lit_at(l, hay, n, i, s, e)) return 1;
   }
-  if (best < 0) return 0;
-  *s = (size_t)best;
-  *e = (size_t)best + blen;
-  return 1;
+  return 0;
 }
 
 /* find_start / find_end (literals.rs:105-128): the first literal of iter()

@@ -71,6 +71,13 @@ typedef struct {
   size_t n;
   uint8_t **lit;
   size_t *len;
+  /* lits_find's prefilter (lits_parse): for literals of 1-3 bytes their
+   * first bytes, the one-byte literals and a bitmap of first byte pairs; for
+   * the longer ones a bitmap of a hash of their first four bytes; any_empty:
+   * some literal is empty (it occurs at every position) */
+  uint8_t first[256], single[256];
+  uint8_t *pair, *quad;
+  int any_empty, any_short, any_long;
 } orc_lits;
 
 struct orc_regex {

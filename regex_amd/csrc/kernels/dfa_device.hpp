@@ -239,7 +239,11 @@ __device__ __forceinline__ bool prefix_hit(const FwdDfaDev &f, const uint4 *v) {
 
 // One lane's forward scan of text[at..end) (dfa.rs:576-764): 16-byte
 // chunks through the LDS fast table, 128-byte bursts per lane.  No EOF step.
-template <int MODE>
+// PFX: with the start-state prefix skip (FwdDfaDev::pfx_*).  A separate
+// instantiation: the skip loop costs the scan ~58 VGPRs (long_scan_kernel
+// 82 -> 140, half the waves per SIMD), so kernels for regexes without a
+// prefix set are built without it.
+template <int MODE, bool PFX = false>
 __device__ __forceinline__ void fwd_range(LaneState &L, const FwdDfaDev &f, const uint8_t *lds, const uint8_t *base,
                                           uint64_t at, uint64_t end) {
   // head: the bytes up to the next 16-byte boundary come from one aligned
@@ -254,22 +258,24 @@ __device__ __forceinline__ void fwd_range(LaneState &L, const FwdDfaDev &f, cons
     for (; j < 16 && at < end && !L.done; ++j, ++at) step1<MODE>(L, f, lds, (w[j >> 2] >> ((j & 3) * 8)) & 0xFF, at);
   }
   while (!L.done && at + 128 <= end) {
+    if (PFX && f.pfx_n && L.s + 1 == f.ustart1) {
+      // start-state prefix skip (dfa.rs:700-711): bursts without a prefix
+      // first byte cannot start a match, and the state stays the start state
+      while (true) {
+        uint4 t[8];
+        const uint4 *q = (const uint4 *)(base + at);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) t[k] = q[k];
+        if (prefix_hit(f, t)) break;
+        at += 128;
+        if (at + 128 > end) break;
+      }
+      if (at + 128 > end) break;
+    }
     const uint4 *p = (const uint4 *)(base + at);
     uint4 v[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = p[k];
-    if (f.pfx_n && L.s + 1 == f.ustart1) {
-      // start-state prefix skip (dfa.rs:700-711): bursts without a prefix
-      // first byte cannot start a match, and the state stays the start state
-      while (!prefix_hit(f, v)) {
-        at += 128;
-        if (at + 128 > end) break;
-        p = (const uint4 *)(base + at);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = p[k];
-      }
-      if (at + 128 > end) break;
-    }
 #pragma unroll
     for (int k = 0; k < 8; ++k)
       if (!L.done) chunk16<MODE>(L, f, lds, v[k], at + 16 * k);
@@ -287,10 +293,10 @@ __device__ __forceinline__ void fwd_range(LaneState &L, const FwdDfaDev &f, cons
 }
 
 // Full forward scan of text[at..len] including the EOF step (dfa.rs:748-763).
-template <int MODE>
+template <int MODE, bool PFX = false>
 __device__ __forceinline__ void fwd_run(LaneState &L, const FwdDfaDev &f, const uint8_t *lds, const uint8_t *base,
                                         uint64_t len, uint64_t at) {
-  fwd_range<MODE>(L, f, lds, base, at, len);
+  fwd_range<MODE, PFX>(L, f, lds, base, at, len);
   if (!L.done && f.eof[L.s]) L.last = len;
 }
 

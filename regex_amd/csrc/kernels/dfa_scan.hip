@@ -68,7 +68,7 @@ __device__ __forceinline__ void finish_lane(const LaneState &L, const RevDfaDev 
   ((uint64_t *)out)[2 * h + 1] = me;
 }
 
-template <int MODE, bool STRIDED>
+template <int MODE, bool STRIDED, bool PFX>
 __global__ __launch_bounds__(256) void dfa_fwd_kernel(BatchDev bt, FwdDfaDev f, RevDfaDev r, void *out) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   for (uint32_t i = threadIdx.x * 16; i < f.lds_bytes; i += blockDim.x * 16)
@@ -89,7 +89,7 @@ __global__ __launch_bounds__(256) void dfa_fwd_kernel(BatchDev bt, FwdDfaDev f, 
     }
     LaneState L;
     lane_start(L, f, base, len, bt.start);
-    fwd_run<MODE>(L, f, lds, base, len, bt.start);
+    fwd_run<MODE, PFX>(L, f, lds, base, len, bt.start);
     finish_lane<MODE>(L, r, base, len, bt.start, h, out, bt.quit_flag);
   }
 }
@@ -895,7 +895,10 @@ hipError_t launch_dfa_anchored_rev(int mode, const BatchDev &b, const RevDfaDev 
 template <int MODE, bool STRIDED>
 static hipError_t launch_fwd(const BatchDev &b, const FwdDfaDev &f, const RevDfaDev &r, void *out,
                              hipStream_t st, int grid) {
-  hipLaunchKernelGGL((dfa_fwd_kernel<MODE, STRIDED>), dim3(grid), dim3(256), f.lds_bytes, st, b, f, r, out);
+  if (f.pfx_n)  // the start-state prefix skip (fwd_range<MODE, true>)
+    hipLaunchKernelGGL((dfa_fwd_kernel<MODE, STRIDED, true>), dim3(grid), dim3(256), f.lds_bytes, st, b, f, r, out);
+  else
+    hipLaunchKernelGGL((dfa_fwd_kernel<MODE, STRIDED, false>), dim3(grid), dim3(256), f.lds_bytes, st, b, f, r, out);
   return hipGetLastError();
 }
 

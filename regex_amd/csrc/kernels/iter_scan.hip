@@ -1873,7 +1873,7 @@ int grid_cap(uint64_t items, int threads, int cus, int per_cu) {
 // later-started ones are cut by the match or never outrank it), and the
 // reverse pass runs over text[start..end] as the reference's does.  The
 // earliest match end (shortest_match) is the minimum over units.
-template <int MODE>
+template <int MODE, bool PFX>
 __global__ __launch_bounds__(256) void long_scan_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
                                                         uint64_t *ures, unsigned long long *best) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -1885,14 +1885,14 @@ __global__ __launch_bounds__(256) void long_scan_kernel(BatchDev b, Geo g, uint6
     LaneState L;
     lane_start(L, f, base, len, c0);
     if (c1 > c0 && c1 - 1 <= len) {
-      fwd_range<MODE>(L, f, lds, base, c0, c1 - 1);
+      fwd_range<MODE, PFX>(L, f, lds, base, c0, c1 - 1);
       if (!L.done) {
         L.s = f.strip[L.s];
         if (L.s == f.dead) L.done = true;
       }
       fwd_range<MODE>(L, f, lds, base, c1 - 1, len);
     } else {
-      fwd_range<MODE>(L, f, lds, base, c0, len);
+      fwd_range<MODE, PFX>(L, f, lds, base, c0, len);
     }
     if (!L.done && f.eof[L.s]) L.last = len;
     if (L.last == NONE) continue;
@@ -1950,9 +1950,16 @@ hipError_t long_scan_m(const BatchDev &b, const FwdDfaDev &f, const RevDfaDev &r
   do {
     if ((e = hipMemsetAsync(best, MODE == MODE_ISMATCH ? 0 : 0xFF, sz_b, st)) != hipSuccess) break;
     const int per_cu = std::max<int>(1, std::min<int>(8, (int)((160u * 1024u) / std::max<size_t>(iter_lds_bytes(f, r), 1))));
-    if ((e = allow_lds(long_scan_kernel<MODE>, iter_lds_bytes(f, r))) != hipSuccess) break;
-    hipLaunchKernelGGL(long_scan_kernel<MODE>, dim3(grid_cap(nunits, 256, cus, per_cu)), dim3(256), iter_lds_bytes(f, r), st, b,
-                       g, nunits, f, r, ures, best);
+    const dim3 lg(grid_cap(nunits, 256, cus, per_cu));
+    if (f.pfx_n) {  // the start-state prefix skip (fwd_range<MODE, true>)
+      if ((e = allow_lds(long_scan_kernel<MODE, true>, iter_lds_bytes(f, r))) != hipSuccess) break;
+      hipLaunchKernelGGL((long_scan_kernel<MODE, true>), lg, dim3(256), iter_lds_bytes(f, r), st, b, g, nunits, f, r,
+                         ures, best);
+    } else {
+      if ((e = allow_lds(long_scan_kernel<MODE, false>, iter_lds_bytes(f, r))) != hipSuccess) break;
+      hipLaunchKernelGGL((long_scan_kernel<MODE, false>), lg, dim3(256), iter_lds_bytes(f, r), st, b, g, nunits, f, r,
+                         ures, best);
+    }
     if ((e = hipGetLastError()) != hipSuccess) break;
     hipLaunchKernelGGL(long_finish_kernel<MODE>, dim3(grid_cap(b.count, 256, cus, 4)), dim3(256), 0, st, b.count,
                        (const uint64_t *)ures, (const unsigned long long *)best, out);
