@@ -895,10 +895,10 @@ hipError_t launch_dfa_anchored_rev(int mode, const BatchDev &b, const RevDfaDev 
 template <int MODE, bool STRIDED>
 static hipError_t launch_fwd(const BatchDev &b, const FwdDfaDev &f, const RevDfaDev &r, void *out,
                              hipStream_t st, int grid) {
-  if (f.pfx_n)  // the start-state prefix skip (fwd_range<MODE, true>)
-    hipLaunchKernelGGL((dfa_fwd_kernel<MODE, STRIDED, true>), dim3(grid), dim3(256), f.lds_bytes, st, b, f, r, out);
-  else
-    hipLaunchKernelGGL((dfa_fwd_kernel<MODE, STRIDED, false>), dim3(grid), dim3(256), f.lds_bytes, st, b, f, r, out);
+  // no start-state prefix skip here: one lane per haystack, and the skip's
+  // registers cost more than it saves on every pattern measured
+  // (profiles/r03_prefix_ab.jsonl, "lines": 1.33 -> 1.81 ms for >[^\n]*\n)
+  hipLaunchKernelGGL((dfa_fwd_kernel<MODE, STRIDED, false>), dim3(grid), dim3(256), f.lds_bytes, st, b, f, r, out);
   return hipGetLastError();
 }
 

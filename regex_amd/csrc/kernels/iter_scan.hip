@@ -1951,7 +1951,11 @@ hipError_t long_scan_m(const BatchDev &b, const FwdDfaDev &f, const RevDfaDev &r
     if ((e = hipMemsetAsync(best, MODE == MODE_ISMATCH ? 0 : 0xFF, sz_b, st)) != hipSuccess) break;
     const int per_cu = std::max<int>(1, std::min<int>(8, (int)((160u * 1024u) / std::max<size_t>(iter_lds_bytes(f, r), 1))));
     const dim3 lg(grid_cap(nunits, 256, cus, per_cu));
-    if (f.pfx_n) {  // the start-state prefix skip (fwd_range<MODE, true>)
+    // the start-state prefix skip (fwd_range<MODE, true>) for one prefix
+    // first byte: measured faster there (Sherlock\s+\w+ 1.76 -> 1.54 ms per
+    // GiB, >[^\n]*\n 1.10 -> 0.31) and slower with two ((?i)holmes\w*:
+    // 1.46 -> 1.73 ms; profiles/r03_prefix_ab.jsonl)
+    if (f.pfx_n == 1) {
       if ((e = allow_lds(long_scan_kernel<MODE, true>, iter_lds_bytes(f, r))) != hipSuccess) break;
       hipLaunchKernelGGL((long_scan_kernel<MODE, true>), lg, dim3(256), iter_lds_bytes(f, r), st, b, g, nunits, f, r,
                          ures, best);
