@@ -40,7 +40,12 @@ $(ORACLE_LIB): $(ORACLE_SRC) $(wildcard oracle/*.h)
 	@mkdir -p oracle/build
 	gcc -O2 -std=c11 -fPIC -shared -Wall -o $@ $(ORACLE_SRC) -lpthread
 
+# diagnostic A/B library (tools/*): make ab AB=<name> ABFLAGS=-D...
+ab:
+	@mkdir -p regex_amd/build/ab_$(AB) regex_amd/lib
+	$(MAKE) LIB=regex_amd/lib/librure_amd_$(AB).so OBJDIR=regex_amd/build/ab_$(AB) CXXFLAGS="$(CXXFLAGS) $(ABFLAGS)" regex_amd/lib/librure_amd_$(AB).so
+
 clean:
 	rm -rf regex_amd/build regex_amd/lib oracle/build
 
-.PHONY: all clean
+.PHONY: all clean ab

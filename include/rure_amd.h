@@ -313,10 +313,11 @@ int rure_amd_dfa_strip_export(rure *re, uint32_t *strip);
  * instead of a reverse scan — else 0; negative on error. */
 int rure_amd_first_byte_export(rure *re, uint8_t *bytes);
 /* The find_iter lexer table (host only; iter_spec_lex_tile_kernel): u8
- * next-state rows of 304 bytes (256 used); *s0 = the start state's row; rows
- * above it: its twin, then the other restart twins (entering a twin = a match
- * ended at that byte).  Returns the table's size in bytes (0: no lexer
- * table), copies at most `cap`. */
+ * entries e = 4 row + code; the next entry after byte b is table[76 e + b];
+ * code (e & 3): 0 = an ordinary state, 1 = the start state (*s0 = its entry),
+ * 2 = its twin, 3 = another restart twin (entering a twin = a match ended at
+ * that byte).  Returns the table's size in bytes (0: no lexer table), copies
+ * at most `cap`. */
 int64_t rure_amd_lex_export(rure *re, uint8_t *table, size_t cap, uint32_t *s0);
 
 /* Export of the Pike VM closure tables the NFA kernel runs (host only):

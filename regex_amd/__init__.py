@@ -600,8 +600,9 @@ class Regex(object):
         return bytes(buf[:n]) if n > 0 else None
 
     def lex_table(self):
-        """The find_iter lexer table: ((rows, 304) uint8 next states, start
-        row), or None (see rure_amd.h rure_amd_lex_export)."""
+        """The find_iter lexer table: (flat uint8 table: the entry after byte
+        b from entry e is table[76 e + b], start entry), or None (see
+        rure_amd.h rure_amd_lex_export)."""
         import numpy as np
         n = N.rure_amd_lex_export(self._re, None, 0, None)
         if n <= 0:
@@ -609,7 +610,7 @@ class Regex(object):
         t = np.zeros(n, dtype=np.uint8)
         s0 = ctypes.c_uint32()
         N.rure_amd_lex_export(self._re, t.ctypes.data, n, ctypes.byref(s0))
-        return t.reshape(-1, 304), s0.value
+        return t, s0.value
 
     def program(self, which):
         """Compiled byte program (0 fwd DFA, 1 reverse DFA, 2 NFA): (info, insts)."""

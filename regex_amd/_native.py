@@ -9,6 +9,10 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "librure_amd.so")
+# A/B builds of the same library (tools/*: diagnostic variants under
+# regex_amd/lib/); never set in product use
+if os.environ.get("RURE_AMD_LIB_AB"):
+    LIB_PATH = os.path.join(_HERE, "lib", os.path.basename(os.environ["RURE_AMD_LIB_AB"]))
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(

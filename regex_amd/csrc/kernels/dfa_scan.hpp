@@ -80,8 +80,8 @@ struct FwdDfaDev {
   // a match state at byte x ends the search there and the next one starts at
   // x, so that transition goes to a twin of the start state's successor on
   // the same byte.  u8 rows of kRow bytes; states numbered [others, S0 =
-  // lex_s0, twin(S0), other twins]: clamp(s - (lex_s0 - 1), 0, 3) = the
-  // byte's flags: 1 = the state after it is the start state (Z), 2 = Z and a
+  // lex_s0, twin(S0), other twins] with the codes 0, 1, 2, 3 = the byte's
+  // flags: 1 = the state after it is the start state (Z), 2 = Z and a
   // match ended at it (EMIT), 3 = EMIT only.
   const uint8_t *lex_image;
   uint32_t lex_bytes, lex_s0;
@@ -95,6 +95,8 @@ struct FwdDfaDev {
   uint32_t pfx_rep[4];
 };
 constexpr uint32_t kLexMaxRows = 24;  // lexer table rows (iter_spec_lex_tile_kernel's static LDS)
+constexpr uint32_t kLexUnit = kRow / 4;  // lexer entry -> row address multiplier
+constexpr uint32_t kLexBytes = (kLexMaxRows * kRow + 3 * kLexUnit + 15) & ~15u;  // largest lexer image
 
 // Literal engine image layout (at most kLitMax literals of kLitLen bytes).
 constexpr uint32_t kLitMax = 64, kLitLen = 32;

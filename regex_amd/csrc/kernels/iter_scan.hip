@@ -50,6 +50,7 @@ enum : uint32_t {
   U_QUIT = 8,         // a search quit (cannot happen on the chunked path)
   U_COPY = 16,        // fixed, and its matches are slots[skip, skip + count)
   U_LEX_TAIL = 32,    // iter_spec_lex_tile_kernel: exit = the lexer's iteration state, the tail pass finishes
+  U_COMPACT = 64,     // slots hold uint2 (start - c0, end - c0) records (the lexer's; haystacks < 4 GiB)
 };
 
 struct IterSt {
@@ -68,6 +69,16 @@ struct Geo {  // unit -> (haystack, chunk) for fixed-stride batches
   uint64_t end;     // cut of the last unit (~0: the haystack end; a span's hi)
   uint32_t slots;   // speculative matches stored per unit
 };
+
+// Speculative record i of unit u (U_COMPACT: stored relative to c0).
+__device__ __forceinline__ ulonglong2 slot_rec(const uint64_t *slots, const Geo &g, uint64_t u, uint32_t i,
+                                               bool compact, uint64_t c0) {
+  if (compact) {
+    const uint2 r = ((const uint2 *)(slots + u * g.slots * 2))[i];
+    return make_ulonglong2(c0 + r.x, c0 + r.y);
+  }
+  return ((const ulonglong2 *)(slots + u * g.slots * 2))[i];
+}
 
 __device__ __forceinline__ void unit_bounds(const BatchDev &b, const Geo &g, uint64_t u, uint64_t *h,
                                             const uint8_t **base, uint64_t *len, uint64_t *c0, uint64_t *c1) {
@@ -1185,60 +1196,90 @@ __device__ __forceinline__ void multi_tile_body(const BatchDev &b, const Geo &g,
 // iter_spec_burst_kernel.
 // 16 lexer steps; FULL = false: only bytes [0, kend) (kend < 16), the rest
 // leave s unchanged and add no flags.  The chain per byte is one 24-bit
-// multiply-add and one LDS u8 read (as the tile kernel's); the flags come off
-// it: code = clamp(s - zb, 0, 3) (FwdDfaDev::lex_image numbering), two bits
-// per byte of the returned word.
+// multiply-add and one LDS u8 read (as the tile kernel's); the flags are the
+// entry's low two bits (FwdDfaDev::lex_image), two bits per byte of the
+// returned word.
 template <bool FULL>
-__device__ __forceinline__ uint32_t lex16(uint32_t &s, const uint32_t w[4], const uint8_t *tab, int32_t zb,
-                                          uint32_t kend) {
+__device__ __forceinline__ uint32_t lex16(uint32_t &s, const uint32_t w[4], const uint8_t *tab, uint32_t kend) {
   uint32_t m = 0;
 #pragma unroll
   for (uint32_t k = 0; k < 16; ++k) {
-    const uint32_t t = tab[__umul24(s, kRow) + ((w[k >> 2] >> (8 * (k & 3))) & 0xFF)];
+    const uint32_t t = tab[__umul24(s, kLexUnit) + ((w[k >> 2] >> (8 * (k & 3))) & 0xFF)];
     if (FULL || k < kend) {
-      m |= (uint32_t)min(max((int32_t)t - zb, 0), 3) << (2 * k);
+      m |= (t & 3u) << (2 * k);
       s = t;
     }
   }
   return m;
 }
 
-// The block's matches from its flag word (kend bytes): EMIT at byte j = a
-// match ended at bp + j; its start is the last earlier position where the
-// search may have begun its match (the state before the byte was the start
-// state — Z of the byte before — or a match ended there).
-__device__ __forceinline__ void lex_events(uint32_t m, uint32_t kend, uint64_t bp, uint32_t &cz, uint64_t &fc,
-                                           uint64_t &p, uint64_t &lm, uint32_t &n, uint64_t *myslots,
-                                           uint32_t nslots) {
+// The lexer's matches go to the unit's slots as uint2 (start - c0, end - c0)
+// records (U_COMPACT) through a queue of four in registers, flushed once per
+// tile with two 16-byte stores whatever it holds (LexQueue::flush): no store
+// in the block loop depends on the data, so the wait for the next tile's
+// loads counts a fixed number of younger stores.  A store whose count
+// depends on the data (one per match) made the compiler drain every store
+// before each tile's loads could be used (s_waitcnt vmcnt(0)): the kernel
+// ran 0.96 ms with them against 0.61 ms without (tools/lex_time.py A/B).
+// A fifth match in one tile flushes early, then waits for its stores.
+struct LexQueue {
+  uint32_t q0, q1, q2, q3;  // start | end << 16 (units of at most 64 KiB)
+  uint32_t qc, nf;          // queued; records flushed (written at [nf, nf + 4))
+  __device__ __forceinline__ void flush(uint2 *dst, uint32_t cap2) {
+    uint4 *d = (uint4 *)(dst + min(nf, cap2 - 4));  // past the slots: a re-run unit, slots unread
+    d[0] = make_uint4(q0 & 0xFFFFu, q0 >> 16, q1 & 0xFFFFu, q1 >> 16);
+    d[1] = make_uint4(q2 & 0xFFFFu, q2 >> 16, q3 & 0xFFFFu, q3 >> 16);
+    nf += qc;
+    qc = 0;
+  }
+  __device__ __forceinline__ void push(uint32_t r, uint2 *dst, uint32_t cap2) {
+    if (qc == 4) {
+      flush(dst, cap2);
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the tile's store count stays fixed
+    }
+    q0 = qc == 0 ? r : q0;
+    q1 = qc == 1 ? r : q1;
+    q2 = qc == 2 ? r : q2;
+    q3 = qc == 3 ? r : q3;
+    ++qc;
+  }
+};
+
+// The block's matches from its flag word: EMIT at byte j = a match ended at
+// bp + j; its start is the last earlier position where the search may have
+// begun its match (the state before the byte was the start state — Z of the
+// byte before — or a match ended there).  Positions are relative to the unit
+// start c0 (fc: the last such position before the block; last: the end of
+// the last match).  For a partial block (kend < 16, the walk's last) the
+// candidate at bp + kend enters fc harmlessly.
+__device__ __forceinline__ void lex_events(uint32_t m, uint32_t bp, uint32_t &cz, uint32_t &fc, uint32_t &last,
+                                           uint32_t &n, LexQueue &Q, uint2 *dst, uint32_t cap2) {
   uint32_t E = (m >> 1) & 0x55555555u;
   const uint32_t Z = (m ^ (m >> 1)) & 0x55555555u;
-  const uint32_t zlast = (Z >> (2 * kend - 2)) & 1u;
-  const uint32_t zmask = kend == 16 ? 0xFFFFFFFFu : (1u << (2 * kend - 2)) - 1u;  // Z of bytes 0 .. kend - 2
-  const uint32_t A = E | ((Z & zmask) << 2) | cz;
+  const uint32_t A = E | (Z << 2) | cz;
   while (E) {
     const uint32_t j = __builtin_ctz(E);
     E &= E - 1;
     const uint32_t below = A & ((1u << j) - 1u);
-    const uint64_t st = below ? bp + ((31 - __builtin_clz(below)) >> 1) : fc;
-    const uint64_t x = bp + (j >> 1);
-    if (n < nslots) *(ulonglong2 *)&myslots[2 * n] = make_ulonglong2(st, x);
+    const uint32_t st = below ? bp + ((31 - __builtin_clz(below)) >> 1) : fc;
+    const uint32_t x = bp + (j >> 1);
+    Q.push(st | (x << 16), dst, cap2);
     ++n;
-    p = lm = x;
+    last = x;
   }
   if (A) fc = bp + ((31 - __builtin_clz(A)) >> 1);
-  cz = zlast;
+  cz = (Z >> 30) & 1u;
 }
 
 __global__ __launch_bounds__(256) void iter_spec_lex_tile_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f,
                                                                  Unit *units, uint64_t *slots, uint32_t *counts) {
-  // the table first in LDS (address 0): the chain's address is one 24-bit
-  // multiply-add; 24 rows + the tile stage = 39 KB, 4 blocks (16 waves) per CU
-  __shared__ __attribute__((aligned(16))) uint8_t tab[kLexMaxRows * kRow];
+  // the chain's address is one 24-bit multiply-add; 24 rows + the tile stage
+  // = 39.5 KB, 4 blocks (16 waves) per CU
+  __shared__ __attribute__((aligned(16))) uint8_t tab[kLexBytes];
   __shared__ __attribute__((aligned(16))) uint4 stage[4][64 * 8];
   for (uint32_t i = threadIdx.x * 16; i < f.lex_bytes; i += blockDim.x * 16)
     *(uint4 *)(tab + i) = *(const uint4 *)(f.lex_image + i);
   __syncthreads();
-  const int32_t zb = (int32_t)f.lex_s0 - 1;
   const uint64_t C = g.chunk, nk = g.nk;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   uint4 *buf = stage[w];
@@ -1269,8 +1310,14 @@ __global__ __launch_bounds__(256) void iter_spec_lex_tile_kernel(BatchDev b, Geo
     // the lexer covers [c0, lim): the byte at c1 - 1 (where the search is cut)
     // and the end of the text are left to the tail pass
     const uint64_t lim = valid ? min(c1 - 1, len) : c0;
-    uint64_t *myslots = slots + u * g.slots * 2;
-    uint64_t p = c0, lm = NONE, fc = c0;
+    // compact records: twice the slots fit the unit's slot bytes (the
+    // queue's flush may write four past the last record)
+    uint2 *const dst = (uint2 *)(slots + u * g.slots * 2);
+    const uint32_t cap2 = 2 * g.slots;
+    LexQueue Q;
+    Q.q0 = Q.q1 = Q.q2 = Q.q3 = 0;
+    Q.qc = Q.nf = 0;
+    uint32_t fc = 0, last = 0;  // relative to c0 (lex_events)
     uint32_t n = 0, s = f.lex_s0, cz = 1;
     bool frozen = false;  // a byte >= 0x80 was seen: the rest is the tail pass's
     uint4 n0, n1, n2, n3, n4, n5, n6, n7;
@@ -1280,6 +1327,10 @@ __global__ __launch_bounds__(256) void iter_spec_lex_tile_kernel(BatchDev b, Geo
   n4 = RURE_LD(4, a); n5 = RURE_LD(5, a); n6 = RURE_LD(6, a); n7 = RURE_LD(7, a);
 #define RURE_STAGE(kk, v) buf[(8 * (kk) + src_h) * 8 + (src_seg ^ (((8 * (kk) + src_h) >> 1) & 7))] = (v);
     RURE_LOAD_TILE(0)
+    // an empty flush: the loop is entered, as it loops back, with the two
+    // flush stores younger than the tile loads (the wait for the loads then
+    // leaves them in flight: vmcnt(2), not vmcnt(0))
+    Q.flush(dst, cap2);
     for (uint64_t at = 0; at < C; at += 128) {
       RURE_STAGE(0, n0) RURE_STAGE(1, n1) RURE_STAGE(2, n2) RURE_STAGE(3, n3)
       RURE_STAGE(4, n4) RURE_STAGE(5, n5) RURE_STAGE(6, n6) RURE_STAGE(7, n7)
@@ -1304,7 +1355,7 @@ __global__ __launch_bounds__(256) void iter_spec_lex_tile_kernel(BatchDev b, Geo
           frozen = frozen || hi8;
           mw[m] = 0;
           if (!frozen) {
-            mw[m] = lex16<true>(s, wd, tab, zb, 16);
+            mw[m] = lex16<true>(s, wd, tab, 16);
             act += 16;
           }
         }
@@ -1321,16 +1372,17 @@ __global__ __launch_bounds__(256) void iter_spec_lex_tile_kernel(BatchDev b, Geo
           frozen = frozen || (hi8 & 0x80808080u);
           mw[m] = 0;
           if (!frozen && kend) {
-            mw[m] = kend == 16 ? lex16<true>(s, wd, tab, zb, 16) : lex16<false>(s, wd, tab, zb, kend);
+            mw[m] = kend == 16 ? lex16<true>(s, wd, tab, 16) : lex16<false>(s, wd, tab, kend);
             act += kend;
           }
         }
       }
-#pragma unroll 1
-      for (int m = 0; m < 8 && 16u * m < act; ++m) {
-        const uint32_t kend = min(act - 16u * m, 16u);
-        lex_events(mw[m], kend, t0 + 16 * m, cz, fc, p, lm, n, myslots, g.slots);
-      }
+      // unrolled: a loop over m indexes mw[] dynamically (a select chain
+      // of 7 per block)
+#pragma unroll
+      for (int m = 0; m < 8; ++m)
+        if (16u * m < act) lex_events(mw[m], (uint32_t)at + 16 * m, cz, fc, last, n, Q, dst, cap2);
+      Q.flush(dst, cap2);  // every lane, every tile (slots are padded to whole groups)
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1343,10 +1395,10 @@ __global__ __launch_bounds__(256) void iter_spec_lex_tile_kernel(BatchDev b, Geo
     // RURE_AMD_LEX_TAIL=0: a diagnostic that leaves the lexer's matches alone)
     Unit U;
     U.entry = {c0, NONE};
-    U.exit = {p, lm};
+    U.exit = n ? IterSt{c0 + last, c0 + last} : IterSt{c0, NONE};
     U.spec_exit = U.exit;
     U.spec_count = n;
-    U.flags = U_LEX_TAIL | U_SPEC_CLEAN | U_CLEAN;
+    U.flags = U_LEX_TAIL | U_COMPACT | U_SPEC_CLEAN | U_CLEAN;
     U.skip = U.pad = 0;
     units[u] = U;
     counts[u] = n;
@@ -1370,14 +1422,20 @@ __global__ __launch_bounds__(256) void iter_lex_tail_kernel(BatchDev b, Geo g, u
     UnitIter it;
     it.init(U.exit, c1);
     uint64_t ms, me;
+    const bool compact = (U.flags & U_COMPACT) != 0;
     while (it.next(f, r, lds, rlds, base, len, &ms, &me)) {
-      if (n < g.slots) *(ulonglong2 *)&slots[(u * g.slots + n) * 2] = make_ulonglong2(ms, me);
+      if (n < g.slots) {
+        if (compact)  // the host keeps haystacks below 4 GiB on this path
+          ((uint2 *)(slots + u * g.slots * 2))[n] = make_uint2((uint32_t)(ms - c0), (uint32_t)(me - c0));
+        else
+          *(ulonglong2 *)&slots[(u * g.slots + n) * 2] = make_ulonglong2(ms, me);
+      }
       ++n;
     }
     U.exit = it.exit;
     U.spec_exit = it.exit;
     U.spec_count = n;
-    U.flags = (it.clean ? (U_SPEC_CLEAN | U_CLEAN) : 0) | (it.quit ? U_QUIT : 0);
+    U.flags = (it.clean ? (U_SPEC_CLEAN | U_CLEAN) : 0) | (it.quit ? U_QUIT : 0) | (U.flags & U_COMPACT);
     units[u] = U;
     counts[u] = n;
     if (!(U.flags & U_SPEC_CLEAN)) atomicOr(dirty, 1u);  // the fix pass has work
@@ -1397,18 +1455,21 @@ __device__ int64_t join_speculation(const Unit &U, uint64_t c0, IterSt E, const 
                                     uint64_t j) {
   const uint32_t n = U.spec_count;
   if (n > g.slots || E.p < c0) return -1;
-  const uint64_t *sl = slots + j * g.slots * 2;
+  const bool cp = (U.flags & U_COMPACT) != 0;
+  auto rec = [&](uint32_t i) { return slot_rec(slots, g, j, i, cp, c0); };
   uint32_t lo = 0, hi = n;  // last i in [0, n] with p_i <= E.p (p_i strictly increasing)
   while (lo < hi) {
     const uint32_t mid = (lo + hi + 1) >> 1;
-    const uint64_t s = sl[2 * (mid - 1)], e = sl[2 * (mid - 1) + 1];
+    const ulonglong2 r = rec(mid - 1);
+    const uint64_t s = r.x, e = r.y;
     if ((s == e ? e + 1 : e) <= E.p) lo = mid;
     else hi = mid - 1;
   }
   const uint32_t i = lo;
   uint64_t pi = c0, lmi = NONE;
   if (i > 0) {
-    const uint64_t s = sl[2 * (i - 1)], e = sl[2 * (i - 1) + 1];
+    const ulonglong2 r = rec(i - 1);
+    const uint64_t s = r.x, e = r.y;
     pi = s == e ? e + 1 : e;
     lmi = e;
   }
@@ -1416,10 +1477,11 @@ __device__ int64_t join_speculation(const Unit &U, uint64_t c0, IterSt E, const 
     // same search start, different last match: S's search from p_i yielded
     // its match i directly (no empty match skipped) when S had no last match
     // (i == 0) or match i starts at p_i
-    if (!(i == 0 || (i < n && sl[2 * i] == pi))) return -1;
+    if (!(i == 0 || (i < n && rec(i).x == pi))) return -1;
   }
   if (i < n) {
-    const uint64_t s = sl[2 * i], e = sl[2 * i + 1];
+    const ulonglong2 r = rec(i);
+    const uint64_t s = r.x, e = r.y;
     if (s < E.p || (s == e && e == E.lm)) return -1;
     return i;
   }
@@ -1638,9 +1700,9 @@ __device__ __forceinline__ void emit_body(const BatchDev &b, const Geo &g, uint6
   const uint64_t obase = off[0];  // off may be a segment of several regexes' shared scan
   for (uint64_t u0 = (uint64_t)blockIdx.x * blockDim.x; u0 < nunits; u0 += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t u = u0 + threadIdx.x;
-    uint64_t o0 = 0, cnt = 0;
+    uint64_t o0 = 0, cnt = 0, cbase = 0;
     uint32_t skip = 0;
-    bool rerun = false, copy = false;
+    bool rerun = false, copy = false, compact = false;
     if (u < nunits) {
       o0 = off[u] - obase;
       cnt = off[u + 1] - off[u];
@@ -1649,6 +1711,12 @@ __device__ __forceinline__ void emit_body(const BatchDev &b, const Geo &g, uint6
         rerun = ((fl & U_FIXED) && !(fl & U_COPY)) || cnt > g.slots;
         copy = !rerun;
         skip = (fl & U_COPY) ? units[u].skip : 0;  // loaded by every lane at once, not per copied unit
+        compact = (fl & U_COMPACT) != 0;
+        if (compact) {
+          uint64_t hh, ll, c1;
+          const uint8_t *bb;
+          unit_bounds(b, g, u, &hh, &bb, &ll, &cbase, &c1);
+        }
       }
     }
     // A unit with at most 4 records (almost every unit: the copy loop below
@@ -1658,11 +1726,17 @@ __device__ __forceinline__ void emit_body(const BatchDev &b, const Geo &g, uint6
     const bool own = copy && cnt <= 4;
     if (own) {
       const uint32_t nw = 2 * (uint32_t)min(cnt, cap - o0);
-      const uint64_t *src = slots + (u * g.slots + skip) * 2;
       uint64_t *dst = out + 2 * o0;
       uint64_t v[8];
+      if (compact) {
+        const uint32_t *src = (const uint32_t *)(slots + u * g.slots * 2) + 2 * skip;
 #pragma unroll
-      for (uint32_t k = 0; k < 8; ++k) v[k] = k < nw ? src[k] : 0;
+        for (uint32_t k = 0; k < 8; ++k) v[k] = k < nw ? cbase + src[k] : 0;
+      } else {
+        const uint64_t *src = slots + (u * g.slots + skip) * 2;
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) v[k] = k < nw ? src[k] : 0;
+      }
 #pragma unroll
       for (uint32_t k = 0; k < 8; ++k)
         if (k < nw) dst[k] = v[k];
@@ -1673,6 +1747,8 @@ __device__ __forceinline__ void emit_body(const BatchDev &b, const Geo &g, uint6
     // loads are in flight before their stores.
     const uint64_t wrec = (copy && !own) ? min(cnt, cap - o0) : 0;
     const uint64_t wsrc = (u * g.slots + skip) * 2, wdst = 2 * o0;
+    // compact units: the record base (c0) rides along; ~0 marks u64 records
+    const uint64_t wcb = compact ? cbase : ~0ull, wsrc32 = u * g.slots * 4 + 2 * skip;
     const uint64_t busy = __ballot(wrec != 0);
     const bool a16 = ((uintptr_t)out & 15) == 0;
 #pragma unroll 1
@@ -1680,17 +1756,28 @@ __device__ __forceinline__ void emit_body(const BatchDev &b, const Geo &g, uint6
       if (!((busy >> (8 * grp)) & 0xFFull)) continue;
       const int ul = 8 * grp + (int)(lane >> 3);
       const uint64_t cu = __shfl(wrec, ul), su = __shfl(wsrc, ul), du = __shfl(wdst, ul);
+      const uint64_t cb = __shfl(wcb, ul), su32 = __shfl(wsrc32, ul);
       uint64_t mx = cu;
       mx = max(mx, (uint64_t)__shfl_xor(mx, 8));
       mx = max(mx, (uint64_t)__shfl_xor(mx, 16));
       mx = max(mx, (uint64_t)__shfl_xor(mx, 32));
       const ulonglong2 *src = (const ulonglong2 *)(slots + su);
+      const uint2 *src32 = (const uint2 *)((const uint32_t *)slots + su32);
       uint64_t *dst = out + du;
       for (uint64_t i = lane & 7; i < mx; i += 32) {
         ulonglong2 v[4];
+        if (cb != ~0ull) {
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
-          if (i + 8 * t < cu) v[t] = src[i + 8 * t];
+          for (int t = 0; t < 4; ++t)
+            if (i + 8 * t < cu) {
+              const uint2 r = src32[i + 8 * t];
+              v[t] = make_ulonglong2(cb + r.x, cb + r.y);
+            }
+        } else {
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            if (i + 8 * t < cu) v[t] = src[i + 8 * t];
+        }
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           const uint64_t j = i + 8 * t;
@@ -2009,7 +2096,9 @@ struct IterScratch {
 };
 
 static hipError_t iter_scratch(uint64_t nunits, uint32_t nslots, hipStream_t st, IterScratch *sc) {
-  const size_t sz_units = nunits * sizeof(Unit), sz_slots = nunits * (size_t)nslots * 16;
+  // slots for whole groups of 64 units: the lexer's lanes past the last unit
+  // flush their (empty) record queues unconditionally
+  const size_t sz_units = nunits * sizeof(Unit), sz_slots = ((nunits + 63) & ~(uint64_t)63) * (size_t)nslots * 16;
   const size_t sz_counts = (nunits + 1) * 4, sz_off = (nunits + 1) * 8, sz_queue = nunits * 8;
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   const size_t total = al(sz_units) + al(sz_slots) + al(sz_counts) + al(sz_off) + al(sz_queue) + 256;
@@ -2353,9 +2442,13 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
       const bool sa_tile = sa_tile_ok(b, g);
       // Lexer engine (terminal matches + first-byte rule); RURE_AMD_LEX=0 disables
       const char *lex_env = getenv("RURE_AMD_LEX");
+      // (haystacks below 4 GiB: the lexer's records are u32 offsets from the
+      // unit start, U_COMPACT; units of at most 64 KiB: its record queue
+      // packs two u16 per register)
       const bool use_lex = f->lex_bytes && !(lex_env && lex_env[0] == '0') && !b.offs && g.nk >= 2 &&
                            (g.chunk % 128) == 0 && (b.count == 1 || (b.stride % 16) == 0) &&
-                           (((uintptr_t)(b.hay + b.start)) & 15) == 0;
+                           (((uintptr_t)(b.hay + b.start)) & 15) == 0 && b.length < (1ull << 32) &&
+                           g.chunk <= 65536;
       ktimer_begin(st);  // bench diagnostics: the speculative kernel's duration
       if (use_lex) {
         hipLaunchKernelGGL(iter_spec_lex_tile_kernel, dim3(grid_cap((nunits + 63) / 64, 4, cus, 4)), dim3(256), 0,

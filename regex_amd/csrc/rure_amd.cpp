@@ -444,6 +444,7 @@ struct ScratchBlock {
   size_t n;
   int dev;
   hipEvent_t ev;   // recorded at the last free (nullptr: never freed yet)
+  hipStream_t st;  // the stream of the last free
 };
 struct ScratchCache {
   std::mutex mu;
@@ -504,7 +505,13 @@ hipError_t rure_amd::scratch_malloc(void **p, size_t bytes, hipStream_t st) {
       c.live_bytes += blk.n;
       c.peak_live = std::max(c.peak_live, c.live_bytes);
       *p = q;
-      return blk.ev ? hipStreamWaitEvent(st, blk.ev, 0) : hipSuccess;
+      // Reuse on the stream that freed it is ordered by the stream itself
+      // (hipStreamDestroy completes a stream's work before its handle can be
+      // handed out again); the wait is a barrier packet that cost the
+      // latency-bound C1 step ~5 us.  hipStreamPerThread names a different
+      // stream on every thread, so it always waits.
+      if (!blk.ev || (st == blk.st && st != hipStreamPerThread)) return hipSuccess;
+      return hipStreamWaitEvent(st, blk.ev, 0);
     }
   }
   void *q = nullptr;
@@ -519,7 +526,7 @@ hipError_t rure_amd::scratch_malloc(void **p, size_t bytes, hipStream_t st) {
   }
   if (e != hipSuccess) return e;
   std::lock_guard<std::mutex> g(c.mu);
-  c.live[q] = ScratchBlock{n, d, nullptr};
+  c.live[q] = ScratchBlock{n, d, nullptr, nullptr};
   c.live_bytes += n;
   c.peak_live = std::max(c.peak_live, c.live_bytes);
   *p = q;
@@ -529,7 +536,7 @@ hipError_t rure_amd::scratch_malloc(void **p, size_t bytes, hipStream_t st) {
 hipError_t rure_amd::scratch_free(void *p, hipStream_t st) {
   if (!p) return hipSuccess;
   ScratchCache &c = scratch_cache();
-  ScratchBlock blk{0, 0, nullptr};
+  ScratchBlock blk{0, 0, nullptr, nullptr};
   {
     std::lock_guard<std::mutex> g(c.mu);
     auto it = c.live.find(p);
@@ -540,6 +547,7 @@ hipError_t rure_amd::scratch_free(void *p, hipStream_t st) {
     hipError_t e = hipSuccess;
     if (!blk.ev) e = hipEventCreateWithFlags(&blk.ev, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventRecord(blk.ev, st);
+    blk.st = st;
     if (e == hipSuccess && c.cached + blk.n <= scratch_cap(c)) {
       c.free_blocks[blk.dev].emplace(blk.n, std::make_pair(p, blk));
       c.cached += blk.n;
@@ -1220,13 +1228,19 @@ static bool build_lex(const DenseDfa &d, uint32_t ustart1, uint32_t fb_n, std::v
     if (twin[t] < 0) { twin[t] = (int)rows.size(); rows.push_back(t); }
   }
   if (rows.size() > kLexMaxRows || plain[s0] < 1) return false;
-  img->assign(rows.size() * kRow, 0);
+  // entries 4 row + code (dfa_scan.hpp FwdDfaDev::lex_image): codes 0 for the
+  // rows below S0, 1 for S0, 2 for twin(S0), 3 for the other twins
+  const uint32_t ps0 = (uint32_t)plain[s0];
+  auto code = [&](uint32_t r) -> uint32_t { return r < ps0 ? 0 : r == ps0 ? 1 : r == ps0 + 1 ? 2 : 3; };
+  auto entry = [&](uint32_t r) -> uint8_t { return (uint8_t)(4 * r + code(r)); };
+  img->assign(((rows.size() - 1) * kRow + 3 * kLexUnit + 256 + 15) & ~(size_t)15, 0);
   for (size_t i = 0; i < rows.size(); ++i)
     for (int c = 0; c < 256; ++c) {
       const uint32_t t = d.trans[(size_t)rows[i] * 256 + c];
-      (*img)[i * kRow + c] = (uint8_t)(is_match(t) ? twin[d.trans[(size_t)s0 * 256 + c]] : plain[t]);
+      const int to = is_match(t) ? twin[d.trans[(size_t)s0 * 256 + c]] : plain[t];
+      (*img)[(size_t)entry((uint32_t)i) * kLexUnit + c] = entry((uint32_t)to);
     }
-  *s0_idx = (uint32_t)plain[s0];
+  *s0_idx = entry(ps0);
   return true;
 }
 

@@ -24,12 +24,13 @@ def lex_walk(lex, t, c0, end):
             return out, p, lm, True
         m = 0
         for k in range(kend):
-            s = int(tab[s, t[bp + k]])
-            m |= min(max(s - (s0 - 1), 0), 3) << (2 * k)
+            s = int(tab[76 * s + t[bp + k]])
+            m |= (s & 3) << (2 * k)
         E = (m >> 1) & 0x55555555
         Z = (m ^ (m >> 1)) & 0x55555555
-        zlast = (Z >> (2 * kend - 2)) & 1
-        A = E | ((Z & ((1 << (2 * kend - 2)) - 1)) << 2) | cz
+        zlast = (Z >> 30) & 1
+        # (a partial block is the walk's last: its bit 2 kend only reaches fc)
+        A = (E | (Z << 2) | cz) & 0xFFFFFFFF
         while E:
             j = (E & -E).bit_length() - 1
             E &= E - 1
