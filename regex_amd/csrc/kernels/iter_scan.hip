@@ -1822,6 +1822,7 @@ __global__ __launch_bounds__(1024) void iter_emit_kernel(BatchDev b, Geo g, uint
   emit_body(b, g, nunits, f, r, units, slots, off, out, cap, lds);
 }
 
+
 // ---------------------------------------------------- one wave per haystack
 // exec.rs:473-514 per search: the DFA on lane 0; the Pike VM on the whole
 // wave when the DFA quits (or when there is no DFA).
@@ -1984,9 +1985,9 @@ __global__ __launch_bounds__(256) void long_scan_kernel(BatchDev b, Geo g, uint6
     if (!L.done && f.eof[L.s]) L.last = len;
     if (L.last == NONE) continue;
     if (MODE == MODE_ISMATCH) {
-      best[h] = 1;
+      ((uint8_t *)best)[h] = 1;  // best = the u8 output itself (long_scan_m)
     } else if (MODE == MODE_SHORTEST) {
-      atomicMin(&best[h], (unsigned long long)L.last);
+      atomicMin(&best[h], (unsigned long long)L.last);  // the u64 output itself
     } else {
       uint64_t ms, me = L.last;
       if (me == b.start) ms = me;  // exec.rs:647
@@ -2028,14 +2029,21 @@ hipError_t long_scan_m(const BatchDev &b, const FwdDfaDev &f, const RevDfaDev &r
   g.nk = span <= chunk ? 1 : (span + chunk - 1) / chunk;
   const uint64_t nunits = b.count * g.nk;
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-  const size_t sz_u = MODE == MODE_FIND ? nunits * 16 : 0, sz_b = b.count * 8;
+  // is_match / shortest_match write the output directly (a byte store / an
+  // atomic min per haystack): no scratch and no finish pass — the scratch
+  // cache's event per call had cost the latency-bound C1 step ~5 us
+  const size_t sz_u = MODE == MODE_FIND ? nunits * 16 : 0, sz_b = MODE == MODE_FIND ? b.count * 8 : 0;
   uint8_t *buf = nullptr;
-  hipError_t e = scratch_malloc((void **)&buf, al(sz_u) + al(sz_b), st);
+  hipError_t e = MODE == MODE_FIND ? scratch_malloc((void **)&buf, al(sz_u) + al(sz_b), st) : hipSuccess;
   if (e != hipSuccess) return e;
   uint64_t *ures = (uint64_t *)buf;
-  unsigned long long *best = (unsigned long long *)(buf + al(sz_u));
+  unsigned long long *best = MODE == MODE_FIND ? (unsigned long long *)(buf + al(sz_u)) : (unsigned long long *)out;
   do {
-    if ((e = hipMemsetAsync(best, MODE == MODE_ISMATCH ? 0 : 0xFF, sz_b, st)) != hipSuccess) break;
+    if (MODE == MODE_FIND)
+      e = hipMemsetAsync(best, 0xFF, sz_b, st);
+    else
+      e = hipMemsetAsync(out, MODE == MODE_ISMATCH ? 0 : 0xFF, b.count * (MODE == MODE_ISMATCH ? 1 : 8), st);
+    if (e != hipSuccess) break;
     const int per_cu = std::max<int>(1, std::min<int>(8, (int)((160u * 1024u) / std::max<size_t>(iter_lds_bytes(f, r), 1))));
     const dim3 lg(grid_cap(nunits, 256, cus, per_cu));
     // the start-state prefix skip (fwd_range<MODE, true>) for one prefix
@@ -2052,11 +2060,13 @@ hipError_t long_scan_m(const BatchDev &b, const FwdDfaDev &f, const RevDfaDev &r
                          ures, best);
     }
     if ((e = hipGetLastError()) != hipSuccess) break;
-    hipLaunchKernelGGL(long_finish_kernel<MODE>, dim3(grid_cap(b.count, 256, cus, 4)), dim3(256), 0, st, b.count,
-                       (const uint64_t *)ures, (const unsigned long long *)best, out);
-    e = hipGetLastError();
+    if (MODE == MODE_FIND) {
+      hipLaunchKernelGGL(long_finish_kernel<MODE>, dim3(grid_cap(b.count, 256, cus, 4)), dim3(256), 0, st, b.count,
+                         (const uint64_t *)ures, (const unsigned long long *)best, out);
+      e = hipGetLastError();
+    }
   } while (false);
-  hipError_t e2 = scratch_free(buf, st);
+  hipError_t e2 = buf ? scratch_free(buf, st) : hipSuccess;
   return e != hipSuccess ? e : e2;
 }
 
