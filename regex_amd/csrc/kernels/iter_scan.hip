@@ -50,7 +50,8 @@ enum : uint32_t {
   U_QUIT = 8,         // a search quit (cannot happen on the chunked path)
   U_COPY = 16,        // fixed, and its matches are slots[skip, skip + count)
   U_LEX_TAIL = 32,    // iter_spec_lex_tile_kernel: exit = the lexer's iteration state, the tail pass finishes
-  U_COMPACT = 64,     // slots hold uint2 (start - c0, end - c0) records (the lexer's; haystacks < 4 GiB)
+  U_COMPACT = 64,     // the lexer's slots: its pad (= its count) records as u32 start - c0 | end - c0 << 16,
+                      // then the tail pass's as absolute ulonglong2 from the back of the slot area
 };
 
 struct IterSt {
@@ -60,7 +61,7 @@ struct IterSt {
 struct Unit {
   IterSt entry, exit, spec_exit;
   uint32_t spec_count, flags;
-  uint32_t skip, pad;  // U_COPY: speculative matches dropped at the front
+  uint32_t skip, pad;  // U_COPY: speculative matches dropped at the front; pad: U_COMPACT's lexer count
 };
 
 struct Geo {  // unit -> (haystack, chunk) for fixed-stride batches
@@ -70,14 +71,19 @@ struct Geo {  // unit -> (haystack, chunk) for fixed-stride batches
   uint32_t slots;   // speculative matches stored per unit
 };
 
-// Speculative record i of unit u (U_COMPACT: stored relative to c0).
+// Speculative record i of unit u (U_COMPACT: the first nlex as u16 pairs
+// relative to c0, the rest absolute from the back of the unit's slots).
 __device__ __forceinline__ ulonglong2 slot_rec(const uint64_t *slots, const Geo &g, uint64_t u, uint32_t i,
-                                               bool compact, uint64_t c0) {
+                                               bool compact, uint64_t c0, uint32_t nlex) {
+  const ulonglong2 *r16 = (const ulonglong2 *)(slots + u * g.slots * 2);
   if (compact) {
-    const uint2 r = ((const uint2 *)(slots + u * g.slots * 2))[i];
-    return make_ulonglong2(c0 + r.x, c0 + r.y);
+    if (i < nlex) {
+      const uint32_t v = ((const uint32_t *)r16)[i];
+      return make_ulonglong2(c0 + (v & 0xFFFFu), c0 + (v >> 16));
+    }
+    return r16[g.slots - 1 - (i - nlex)];
   }
-  return ((const ulonglong2 *)(slots + u * g.slots * 2))[i];
+  return r16[i];
 }
 
 __device__ __forceinline__ void unit_bounds(const BatchDev &b, const Geo &g, uint64_t u, uint64_t *h,
@@ -1213,9 +1219,9 @@ __device__ __forceinline__ uint32_t lex16(uint32_t &s, const uint32_t w[4], cons
   return m;
 }
 
-// The lexer's matches go to the unit's slots as uint2 (start - c0, end - c0)
-// records (U_COMPACT) through a queue of four in registers, flushed once per
-// tile with two 16-byte stores whatever it holds (LexQueue::flush): no store
+// The lexer's matches go to the unit's slots as u32 (start - c0 | end - c0 <<
+// 16) records (U_COMPACT) through a queue of four in registers, flushed once
+// per tile with one 16-byte store whatever it holds (LexQueue::flush): no store
 // in the block loop depends on the data, so the wait for the next tile's
 // loads counts a fixed number of younger stores.  A store whose count
 // depends on the data (one per match) made the compiler drain every store
@@ -1225,16 +1231,14 @@ __device__ __forceinline__ uint32_t lex16(uint32_t &s, const uint32_t w[4], cons
 struct LexQueue {
   uint32_t q0, q1, q2, q3;  // start | end << 16 (units of at most 64 KiB)
   uint32_t qc, nf;          // queued; records flushed (written at [nf, nf + 4))
-  __device__ __forceinline__ void flush(uint2 *dst, uint32_t cap2) {
-    uint4 *d = (uint4 *)(dst + min(nf, cap2 - 4));  // past the slots: a re-run unit, slots unread
-    d[0] = make_uint4(q0 & 0xFFFFu, q0 >> 16, q1 & 0xFFFFu, q1 >> 16);
-    d[1] = make_uint4(q2 & 0xFFFFu, q2 >> 16, q3 & 0xFFFFu, q3 >> 16);
+  __device__ __forceinline__ void flush(uint32_t *dst, uint32_t cap4) {
+    *(uint4 *)(dst + min(nf, cap4 - 4)) = make_uint4(q0, q1, q2, q3);  // past the slots: a re-run unit, slots unread
     nf += qc;
     qc = 0;
   }
-  __device__ __forceinline__ void push(uint32_t r, uint2 *dst, uint32_t cap2) {
+  __device__ __forceinline__ void push(uint32_t r, uint32_t *dst, uint32_t cap4) {
     if (qc == 4) {
-      flush(dst, cap2);
+      flush(dst, cap4);
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the tile's store count stays fixed
     }
     q0 = qc == 0 ? r : q0;
@@ -1253,7 +1257,7 @@ struct LexQueue {
 // the last match).  For a partial block (kend < 16, the walk's last) the
 // candidate at bp + kend enters fc harmlessly.
 __device__ __forceinline__ void lex_events(uint32_t m, uint32_t bp, uint32_t &cz, uint32_t &fc, uint32_t &last,
-                                           uint32_t &n, LexQueue &Q, uint2 *dst, uint32_t cap2) {
+                                           uint32_t &n, LexQueue &Q, uint32_t *dst, uint32_t cap4) {
   uint32_t E = (m >> 1) & 0x55555555u;
   const uint32_t Z = (m ^ (m >> 1)) & 0x55555555u;
   const uint32_t A = E | (Z << 2) | cz;
@@ -1263,7 +1267,7 @@ __device__ __forceinline__ void lex_events(uint32_t m, uint32_t bp, uint32_t &cz
     const uint32_t below = A & ((1u << j) - 1u);
     const uint32_t st = below ? bp + ((31 - __builtin_clz(below)) >> 1) : fc;
     const uint32_t x = bp + (j >> 1);
-    Q.push(st | (x << 16), dst, cap2);
+    Q.push(st | (x << 16), dst, cap4);
     ++n;
     last = x;
   }
@@ -1310,10 +1314,10 @@ __global__ __launch_bounds__(256) void iter_spec_lex_tile_kernel(BatchDev b, Geo
     // the lexer covers [c0, lim): the byte at c1 - 1 (where the search is cut)
     // and the end of the text are left to the tail pass
     const uint64_t lim = valid ? min(c1 - 1, len) : c0;
-    // compact records: twice the slots fit the unit's slot bytes (the
-    // queue's flush may write four past the last record)
-    uint2 *const dst = (uint2 *)(slots + u * g.slots * 2);
-    const uint32_t cap2 = 2 * g.slots;
+    // compact records: four per slot of the unit's slot bytes (the queue's
+    // flush may write four past the last record)
+    uint32_t *const dst = (uint32_t *)(slots + u * g.slots * 2);
+    const uint32_t cap4 = 4 * g.slots;
     LexQueue Q;
     Q.q0 = Q.q1 = Q.q2 = Q.q3 = 0;
     Q.qc = Q.nf = 0;
@@ -1330,7 +1334,7 @@ __global__ __launch_bounds__(256) void iter_spec_lex_tile_kernel(BatchDev b, Geo
     // an empty flush: the loop is entered, as it loops back, with the two
     // flush stores younger than the tile loads (the wait for the loads then
     // leaves them in flight: vmcnt(2), not vmcnt(0))
-    Q.flush(dst, cap2);
+    Q.flush(dst, cap4);
     for (uint64_t at = 0; at < C; at += 128) {
       RURE_STAGE(0, n0) RURE_STAGE(1, n1) RURE_STAGE(2, n2) RURE_STAGE(3, n3)
       RURE_STAGE(4, n4) RURE_STAGE(5, n5) RURE_STAGE(6, n6) RURE_STAGE(7, n7)
@@ -1381,8 +1385,8 @@ __global__ __launch_bounds__(256) void iter_spec_lex_tile_kernel(BatchDev b, Geo
       // of 7 per block)
 #pragma unroll
       for (int m = 0; m < 8; ++m)
-        if (16u * m < act) lex_events(mw[m], (uint32_t)at + 16 * m, cz, fc, last, n, Q, dst, cap2);
-      Q.flush(dst, cap2);  // every lane, every tile (slots are padded to whole groups)
+        if (16u * m < act) lex_events(mw[m], (uint32_t)at + 16 * m, cz, fc, last, n, Q, dst, cap4);
+      Q.flush(dst, cap4);  // every lane, every tile (slots are padded to whole groups)
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1399,7 +1403,8 @@ __global__ __launch_bounds__(256) void iter_spec_lex_tile_kernel(BatchDev b, Geo
     U.spec_exit = U.exit;
     U.spec_count = n;
     U.flags = U_LEX_TAIL | U_COMPACT | U_SPEC_CLEAN | U_CLEAN;
-    U.skip = U.pad = 0;
+    U.skip = 0;
+    U.pad = n;  // the lexer's records (u16 pairs); the tail pass's go to the back
     units[u] = U;
     counts[u] = n;
   }
@@ -1425,10 +1430,9 @@ __global__ __launch_bounds__(256) void iter_lex_tail_kernel(BatchDev b, Geo g, u
     const bool compact = (U.flags & U_COMPACT) != 0;
     while (it.next(f, r, lds, rlds, base, len, &ms, &me)) {
       if (n < g.slots) {
-        if (compact)  // the host keeps haystacks below 4 GiB on this path
-          ((uint2 *)(slots + u * g.slots * 2))[n] = make_uint2((uint32_t)(ms - c0), (uint32_t)(me - c0));
-        else
-          *(ulonglong2 *)&slots[(u * g.slots + n) * 2] = make_ulonglong2(ms, me);
+        // compact units: absolute records from the back (slot_rec)
+        const uint64_t k = compact ? g.slots - 1 - (n - U.pad) : n;
+        *(ulonglong2 *)&slots[(u * g.slots + k) * 2] = make_ulonglong2(ms, me);
       }
       ++n;
     }
@@ -1456,7 +1460,7 @@ __device__ int64_t join_speculation(const Unit &U, uint64_t c0, IterSt E, const 
   const uint32_t n = U.spec_count;
   if (n > g.slots || E.p < c0) return -1;
   const bool cp = (U.flags & U_COMPACT) != 0;
-  auto rec = [&](uint32_t i) { return slot_rec(slots, g, j, i, cp, c0); };
+  auto rec = [&](uint32_t i) { return slot_rec(slots, g, j, i, cp, c0, U.pad); };
   uint32_t lo = 0, hi = n;  // last i in [0, n] with p_i <= E.p (p_i strictly increasing)
   while (lo < hi) {
     const uint32_t mid = (lo + hi + 1) >> 1;
@@ -1691,6 +1695,9 @@ __global__ void iter_exit_kernel(const Unit *units, uint64_t nunits, uint64_t *e
 // 4 records, else the wave's larger units eight at a time.  Units that were repaired, or had more matches
 // than slots, re-run their iteration (the block stages the hot tables only
 // then).
+// LEX: compact (lexer) units may occur (iter_emit_kernel; the multi-regex
+// passes never produce them, and the extra paths cost their kernel spills)
+template <bool LEX>
 __device__ __forceinline__ void emit_body(const BatchDev &b, const Geo &g, uint64_t nunits, const FwdDfaDev &f,
                                           const RevDfaDev &r, const Unit *units, const uint64_t *slots,
                                           const uint64_t *off, uint64_t *out, uint64_t cap, uint8_t *lds) {
@@ -1701,7 +1708,7 @@ __device__ __forceinline__ void emit_body(const BatchDev &b, const Geo &g, uint6
   for (uint64_t u0 = (uint64_t)blockIdx.x * blockDim.x; u0 < nunits; u0 += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t u = u0 + threadIdx.x;
     uint64_t o0 = 0, cnt = 0, cbase = 0;
-    uint32_t skip = 0;
+    uint32_t skip = 0, nlex = 0;
     bool rerun = false, copy = false, compact = false;
     if (u < nunits) {
       o0 = off[u] - obase;
@@ -1711,11 +1718,12 @@ __device__ __forceinline__ void emit_body(const BatchDev &b, const Geo &g, uint6
         rerun = ((fl & U_FIXED) && !(fl & U_COPY)) || cnt > g.slots;
         copy = !rerun;
         skip = (fl & U_COPY) ? units[u].skip : 0;  // loaded by every lane at once, not per copied unit
-        compact = (fl & U_COMPACT) != 0;
+        compact = LEX && (fl & U_COMPACT) != 0;
         if (compact) {
           uint64_t hh, ll, c1;
           const uint8_t *bb;
           unit_bounds(b, g, u, &hh, &bb, &ll, &cbase, &c1);
+          nlex = units[u].pad;
         }
       }
     }
@@ -1729,9 +1737,13 @@ __device__ __forceinline__ void emit_body(const BatchDev &b, const Geo &g, uint6
       uint64_t *dst = out + 2 * o0;
       uint64_t v[8];
       if (compact) {
-        const uint32_t *src = (const uint32_t *)(slots + u * g.slots * 2) + 2 * skip;
 #pragma unroll
-        for (uint32_t k = 0; k < 8; ++k) v[k] = k < nw ? cbase + src[k] : 0;
+        for (uint32_t k = 0; k < 4; ++k)
+          if (2 * k < nw) {
+            const ulonglong2 r = slot_rec(slots, g, u, skip + k, true, cbase, nlex);
+            v[2 * k] = r.x;
+            v[2 * k + 1] = r.y;
+          }
       } else {
         const uint64_t *src = slots + (u * g.slots + skip) * 2;
 #pragma unroll
@@ -1747,8 +1759,13 @@ __device__ __forceinline__ void emit_body(const BatchDev &b, const Geo &g, uint6
     // loads are in flight before their stores.
     const uint64_t wrec = (copy && !own) ? min(cnt, cap - o0) : 0;
     const uint64_t wsrc = (u * g.slots + skip) * 2, wdst = 2 * o0;
-    // compact units: the record base (c0) rides along; ~0 marks u64 records
-    const uint64_t wcb = compact ? cbase : ~0ull, wsrc32 = u * g.slots * 4 + 2 * skip;
+    // compact units: the record base (c0) rides along (~0 marks u64 records),
+    // the lexer's records are u32 from the unit's slot start, the tail's u64
+    // from its end
+    const uint64_t wcb = compact ? cbase : ~0ull, wsrc32 = u * g.slots * 4 + skip;
+    const uint64_t wlex = compact ? (nlex > skip ? nlex - skip : 0) : 0;
+    const uint64_t wend = (u * g.slots + g.slots - 1) * 2;  // u64 index of the unit's last slot
+    const uint64_t wtail0 = compact && skip > nlex ? skip - nlex : 0;
     const uint64_t busy = __ballot(wrec != 0);
     const bool a16 = ((uintptr_t)out & 15) == 0;
 #pragma unroll 1
@@ -1757,22 +1774,29 @@ __device__ __forceinline__ void emit_body(const BatchDev &b, const Geo &g, uint6
       const int ul = 8 * grp + (int)(lane >> 3);
       const uint64_t cu = __shfl(wrec, ul), su = __shfl(wsrc, ul), du = __shfl(wdst, ul);
       const uint64_t cb = __shfl(wcb, ul), su32 = __shfl(wsrc32, ul);
+      const uint64_t nl = __shfl(wlex, ul), se = __shfl(wend, ul), t0 = __shfl(wtail0, ul);
       uint64_t mx = cu;
       mx = max(mx, (uint64_t)__shfl_xor(mx, 8));
       mx = max(mx, (uint64_t)__shfl_xor(mx, 16));
       mx = max(mx, (uint64_t)__shfl_xor(mx, 32));
       const ulonglong2 *src = (const ulonglong2 *)(slots + su);
-      const uint2 *src32 = (const uint2 *)((const uint32_t *)slots + su32);
+      const uint32_t *src32 = (const uint32_t *)slots + su32;
       uint64_t *dst = out + du;
       for (uint64_t i = lane & 7; i < mx; i += 32) {
         ulonglong2 v[4];
-        if (cb != ~0ull) {
+        if (LEX && cb != ~0ull) {
 #pragma unroll
-          for (int t = 0; t < 4; ++t)
-            if (i + 8 * t < cu) {
-              const uint2 r = src32[i + 8 * t];
-              v[t] = make_ulonglong2(cb + r.x, cb + r.y);
+          for (int t = 0; t < 4; ++t) {
+            const uint64_t j = i + 8 * t;
+            if (j < cu) {
+              if (j < nl) {
+                const uint32_t r = src32[j];
+                v[t] = make_ulonglong2(cb + (r & 0xFFFFu), cb + (r >> 16));
+              } else {  // the tail pass's records, backwards from the last slot
+                v[t] = *(const ulonglong2 *)(slots + se - 2 * (t0 + j - nl));
+              }
             }
+          }
         } else {
 #pragma unroll
           for (int t = 0; t < 4; ++t)
@@ -1819,7 +1843,7 @@ __global__ __launch_bounds__(1024) void iter_emit_kernel(BatchDev b, Geo g, uint
                                                         const Unit *units, const uint64_t *slots, const uint64_t *off,
                                                         uint64_t *out, uint64_t cap) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  emit_body(b, g, nunits, f, r, units, slots, off, out, cap, lds);
+  emit_body<true>(b, g, nunits, f, r, units, slots, off, out, cap, lds);
 }
 
 
@@ -2258,7 +2282,7 @@ __global__ void multi_walk_kernel(BatchDev b, Geo g, uint64_t nunits, const Post
 __global__ __launch_bounds__(1024) void multi_emit_kernel(BatchDev b, Geo g, uint64_t nunits, const PostDesc *d) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const PostDesc &P = d[blockIdx.y];
-  emit_body(b, g, nunits, P.f, P.r, P.units, P.slots, P.off, P.out, P.cap, lds);
+  emit_body<false>(b, g, nunits, P.f, P.r, P.units, P.slots, P.off, P.out, P.cap, lds);
 }
 
 __global__ void multi_counts_exit_kernel(BatchDev b, Geo g, uint64_t nunits, const PostDesc *d) {
