@@ -537,7 +537,7 @@ typedef struct {
   const uint8_t *buf;
   const uint64_t *offs;
   size_t stride, length, lo, hi;
-  int mode;  /* 0 find, 1 is_match, 2 set */
+  int mode;  /* 0 find, 1 is_match, 2 set, 3 shortest_match */
   uint64_t *out;
   uint8_t *out8;
   orc_stats st;
@@ -558,6 +558,9 @@ static void *worker(void *arg) {
       else { j->out[2 * i] = UINT64_MAX; j->out[2 * i + 1] = UINT64_MAX; }
     } else if (j->mode == 1) {
       j->out8[i] = (uint8_t)orc_is_match_at(j->r, c, t, len, 0);
+    } else if (j->mode == 3) {  /* shortest_match: the end, UINT64_MAX for none */
+      size_t e;
+      j->out[i] = orc_shortest_match_at(j->r, c, t, len, 0, &e) ? (uint64_t)e : UINT64_MAX;
     } else {
       uint32_t nm = j->r->fwd->nmatches;
       memset(matches, 0, sizeof(matches));
@@ -607,6 +610,10 @@ int orc_find_batch(const orc_regex *r, const uint8_t *buf, const uint64_t *offs,
 int orc_is_match_batch(const orc_regex *r, const uint8_t *buf, const uint64_t *offs, size_t stride, size_t length,
                        size_t n, int nthreads, uint8_t *out) {
   return run_batch(r, buf, offs, stride, length, n, nthreads, 1, NULL, out, NULL);
+}
+int orc_shortest_batch(const orc_regex *r, const uint8_t *buf, const uint64_t *offs, size_t stride, size_t length,
+                       size_t n, int nthreads, uint64_t *out) {
+  return run_batch(r, buf, offs, stride, length, n, nthreads, 3, out, NULL, NULL);
 }
 int orc_set_batch(const orc_regex *r, const uint8_t *buf, const uint64_t *offs, size_t stride, size_t length,
                   size_t n, int nthreads, uint64_t *masks) {

@@ -107,6 +107,9 @@ int orc_find_batch(const orc_regex *r, const uint8_t *buf, const uint64_t *offs,
                    size_t n, int nthreads, uint64_t *out_pairs, orc_stats *stats);
 int orc_is_match_batch(const orc_regex *r, const uint8_t *buf, const uint64_t *offs, size_t stride,
                        size_t length, size_t n, int nthreads, uint8_t *out);
+/* shortest_match (exec.rs:382-420) per haystack: the end, UINT64_MAX for none. */
+int orc_shortest_batch(const orc_regex *r, const uint8_t *buf, const uint64_t *offs, size_t stride, size_t length,
+                       size_t n, int nthreads, uint64_t *out);
 int orc_set_batch(const orc_regex *r, const uint8_t *buf, const uint64_t *offs, size_t stride, size_t length,
                   size_t n, int nthreads, uint64_t *masks);
 

@@ -54,6 +54,7 @@ orc_cache_stats = _sig("orc_cache_stats", None, VP, ctypes.POINTER(Stats))
 orc_find_batch = _sig("orc_find_batch", ctypes.c_int, VP, VP, VP, SZ, SZ, SZ, ctypes.c_int, VP,
                       ctypes.POINTER(Stats))
 orc_is_match_batch = _sig("orc_is_match_batch", ctypes.c_int, VP, VP, VP, SZ, SZ, SZ, ctypes.c_int, VP)
+orc_shortest_batch = _sig("orc_shortest_batch", ctypes.c_int, VP, VP, VP, SZ, SZ, SZ, ctypes.c_int, VP)
 orc_set_batch = _sig("orc_set_batch", ctypes.c_int, VP, VP, VP, SZ, SZ, SZ, ctypes.c_int, VP)
 
 NONE = (1 << 64) - 1
@@ -193,6 +194,13 @@ class OracleRegex(object):
     def is_match_batch(self, buf, stride, length, n, nthreads=1, offsets=None):
         out = np.zeros(n, dtype=np.uint8)
         orc_is_match_batch(self._r, buf.ctypes.data, offsets.ctypes.data if offsets is not None else None,
+                           stride, length, n, nthreads, out.ctypes.data)
+        return out
+
+    def shortest_batch(self, buf, stride, length, n, nthreads=1, offsets=None):
+        """shortest_match end per haystack (uint64, 2**64 - 1 for none)."""
+        out = np.zeros(n, dtype=np.uint64)
+        orc_shortest_batch(self._r, buf.ctypes.data, offsets.ctypes.data if offsets is not None else None,
                            stride, length, n, nthreads, out.ctypes.data)
         return out
 
