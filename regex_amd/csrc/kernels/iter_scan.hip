@@ -1700,7 +1700,8 @@ __global__ void iter_exit_kernel(const Unit *units, uint64_t nunits, uint64_t *e
 template <bool LEX>
 __device__ __forceinline__ void emit_body(const BatchDev &b, const Geo &g, uint64_t nunits, const FwdDfaDev &f,
                                           const RevDfaDev &r, const Unit *units, const uint64_t *slots,
-                                          const uint64_t *off, uint64_t *out, uint64_t cap, uint8_t *lds) {
+                                          const uint64_t *off, uint64_t *out, uint64_t cap, uint8_t *lds,
+                                          bool copies = true) {
   const uint8_t *rlds = nullptr;
   bool staged = false;
   const uint32_t lane = threadIdx.x & 63;
@@ -1716,7 +1717,7 @@ __device__ __forceinline__ void emit_body(const BatchDev &b, const Geo &g, uint6
       if (cnt && o0 < cap) {
         const uint32_t fl = units[u].flags;
         rerun = ((fl & U_FIXED) && !(fl & U_COPY)) || cnt > g.slots;
-        copy = !rerun;
+        copy = !rerun && copies;  // copies = false: iter_copy_out_kernel wrote them
         skip = (fl & U_COPY) ? units[u].skip : 0;  // loaded by every lane at once, not per copied unit
         compact = LEX && (fl & U_COMPACT) != 0;
         if (compact) {
@@ -1841,9 +1842,86 @@ __device__ __forceinline__ void emit_body(const BatchDev &b, const Geo &g, uint6
 
 __global__ __launch_bounds__(1024) void iter_emit_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
                                                         const Unit *units, const uint64_t *slots, const uint64_t *off,
-                                                        uint64_t *out, uint64_t cap) {
+                                                        uint64_t *out, uint64_t cap, int copies) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  emit_body<true>(b, g, nunits, f, r, units, slots, off, out, cap, lds);
+  emit_body<true>(b, g, nunits, f, r, units, slots, off, out, cap, lds, copies != 0);
+}
+
+// The copies of a lexer pass in output order: block k writes output records
+// [k R, (k + 1) R) — one contiguous range, 16 B per lane per store — reading
+// them from the few units that hold them (their slots: u16 pairs, the tail
+// pass's records from the back), kCopyUnits units staged at a time.
+// emit_body's unit-ordered copy writes 64
+// units' ranges at once (8 x 128 B per store instruction, scattered over
+// the whole output): 0.31 ms for the strip's 35 M records.  Units that are
+// re-run (no valid slots) are left to iter_emit_kernel.
+constexpr uint32_t kCopyRecs = 4096;  // output records per block (256 threads x 16)
+constexpr uint32_t kCopyUnits = 64;   // units staged per round (the strip's 4096 records span ~31)
+__global__ __launch_bounds__(256) void iter_copy_out_kernel(BatchDev b, Geo g, uint64_t nunits, const Unit *units,
+                                                            const uint64_t *slots, const uint64_t *off,
+                                                            uint64_t *out, uint64_t cap) {
+  __shared__ uint64_t soff[kCopyUnits + 1];
+  __shared__ uint64_t sbase[kCopyUnits];
+  __shared__ uint32_t sskip[kCopyUnits], snlex[kCopyUnits], sok[kCopyUnits];
+  const uint64_t obase = off[0];
+  const uint64_t total = min(off[nunits] - obase, cap);
+  for (uint64_t r0 = (uint64_t)blockIdx.x * kCopyRecs; r0 < total; r0 += (uint64_t)gridDim.x * kCopyRecs) {
+    // the unit holding record r0: last u with off[u] - obase <= r0 (a
+    // 256-ary search, two or three rounds over the unit offsets)
+    uint64_t lo = 0, hi = nunits;  // answer in [lo, hi)
+    while (hi - lo > 1) {
+      const uint64_t step = (hi - lo + 255) / 256;
+      const uint64_t c = lo + threadIdx.x * step;
+      const bool le = c < hi && off[c] - obase <= r0;
+      // the largest probe with off <= r0
+      const uint64_t best = __syncthreads_count(le);  // probes are monotone: the first `best` hold
+      const uint64_t nlo = lo + (best ? best - 1 : 0) * step;
+      hi = min(hi, nlo + step);
+      lo = nlo;
+      __syncthreads();
+    }
+    // the units from u0 on, kCopyUnits at a time, into LDS; each round
+    // writes the block's records that fall into them (offsets are sorted)
+    const uint64_t rend = min(total, r0 + kCopyRecs);
+    for (uint64_t u0 = lo;; u0 += kCopyUnits) {
+      const uint64_t uu = u0 + threadIdx.x;
+      if (threadIdx.x <= kCopyUnits) soff[threadIdx.x] = uu <= nunits ? off[uu] - obase : ~0ull;
+      if (threadIdx.x < kCopyUnits && uu < nunits) {
+        const Unit U = units[uu];
+        const uint64_t cnt = off[uu + 1] - off[uu];
+        sok[threadIdx.x] = !(((U.flags & U_FIXED) && !(U.flags & U_COPY)) || cnt > g.slots);
+        sskip[threadIdx.x] = (U.flags & U_COPY) ? U.skip : 0;
+        snlex[threadIdx.x] = (U.flags & U_COMPACT) ? U.pad : 0xFFFFFFFFu;  // ~0: u64 slots
+        uint64_t hh, ll, c0, c1;
+        const uint8_t *bb;
+        unit_bounds(b, g, uu, &hh, &bb, &ll, &c0, &c1);
+        sbase[threadIdx.x] = c0;
+      }
+      __syncthreads();
+      const uint64_t lo_r = soff[0], hi_r = soff[kCopyUnits];
+#pragma unroll 4
+      for (uint32_t k = 0; k < kCopyRecs / 256; ++k) {
+        const uint64_t rr = r0 + k * 256 + threadIdx.x;
+        if (rr >= rend || rr < lo_r || rr >= hi_r) continue;
+        uint32_t a = 0, z = kCopyUnits;  // last j with soff[j] <= rr
+        while (z - a > 1) {
+          const uint32_t m = (a + z) >> 1;
+          if (soff[m] <= rr) a = m;
+          else z = m;
+        }
+        if (!sok[a]) continue;  // re-run by iter_emit_kernel
+        const uint64_t u = u0 + a;
+        const uint32_t i = sskip[a] + (uint32_t)(rr - soff[a]);
+        const uint32_t nl = snlex[a];
+        const ulonglong2 v = nl != 0xFFFFFFFFu ? slot_rec(slots, g, u, i, true, sbase[a], nl)
+                                               : slot_rec(slots, g, u, i, false, 0, 0);
+        *(ulonglong2 *)(out + 2 * rr) = v;
+      }
+      __syncthreads();
+      if (hi_r >= rend) break;
+    }
+    __syncthreads();
+  }
 }
 
 
@@ -2171,7 +2249,8 @@ static bool sa_tile_ok(const BatchDev &b, const Geo &g) {
 // entry, the repairs (fix, walk), the output offsets, emission, per-haystack
 // counts and a span's exit.
 static hipError_t iter_post(const BatchDev &b, const Geo &g, uint64_t nunits, const FwdDfaDev &f, const RevDfaDev &r,
-                            const IterScratch &sc, const IterOut &o, const IterSpan *spn, hipStream_t st, int cus) {
+                            const IterScratch &sc, const IterOut &o, const IterSpan *spn, hipStream_t st, int cus,
+                            bool dense = false) {
   hipError_t e;
   const int bs = iter_bs();
   const size_t lb = iter_lds_bytes(f, r);
@@ -2201,8 +2280,17 @@ static hipError_t iter_post(const BatchDev &b, const Geo &g, uint64_t nunits, co
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   if ((e = scan_counts(sc.counts, sc.off, nunits, st)) != hipSuccess) return e;
+  // a lexer pass (match-dense): its copies in output order first, then the
+  // emit pass only re-runs units (needs a 16-byte aligned output)
+  dense = dense && (((uintptr_t)o.matches) & 15) == 0;
+  if (dense) {
+    hipLaunchKernelGGL(iter_copy_out_kernel, dim3((unsigned)std::min<uint64_t>((nunits * 16) / kCopyRecs + 1, (uint64_t)cus * 8)),
+                       dim3(256), 0, st, b, g, nunits, (const Unit *)sc.units, (const uint64_t *)sc.slots,
+                       (const uint64_t *)sc.off, o.matches, o.cap);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(iter_emit_kernel, dim3(grid), dim3(bs), lb, st, b, g, nunits, f, r, sc.units, sc.slots, sc.off,
-                     o.matches, o.cap);
+                     o.matches, o.cap, dense ? 0 : 1);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(iter_counts_kernel, dim3(grid_cap(b.count, 256, cus, 4)), dim3(256), 0, st, b.count, g.nk,
                      sc.off, o.counts, o.total);
@@ -2529,7 +2617,7 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
       }
       if (!use_lex) ktimer_end(st);
       if ((e = hipGetLastError()) != hipSuccess) break;
-      e = iter_post(b, g, nunits, *f, r, sc, o, spn, st, cus);
+      e = iter_post(b, g, nunits, *f, r, sc, o, spn, st, cus, use_lex);
     } while (false);
     hipError_t e2 = scratch_free(sc.buf, st);
     return e != hipSuccess ? e : e2;
