@@ -545,10 +545,8 @@ hipError_t rure_amd::scratch_free(void *p, hipStream_t st) {
     c.live.erase(it);
     c.live_bytes -= blk.n;
     hipError_t e = hipSuccess;
-#ifndef RURE_AMD_DIAG_SCRATCH_NOEVENT  // diagnostic A/B build only (unsafe across streams)
     if (!blk.ev) e = hipEventCreateWithFlags(&blk.ev, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventRecord(blk.ev, st);
-#endif
     blk.st = st;
     if (e == hipSuccess && c.cached + blk.n <= scratch_cap(c)) {
       c.free_blocks[blk.dev].emplace(blk.n, std::make_pair(p, blk));
