@@ -177,16 +177,6 @@ __device__ __forceinline__ const uint8_t *stage_tables(const FwdDfaDev &f, const
   return r.lds_bytes ? rl : nullptr;
 }
 
-// The post passes (fix, emit) need the tables only for the rare units they
-// re-run: they read the LDS images in place from global memory (same
-// layout, L2-resident) instead of staging them, so those kernels launch
-// without dynamic LDS at full occupancy (a staged block held 1-3 per CU).
-__device__ __forceinline__ void table_view(const FwdDfaDev &f, const RevDfaDev &r, const uint8_t *&tl,
-                                           const uint8_t *&rl) {
-  tl = f.lds_image;
-  rl = r.lds_bytes ? r.lds_image : nullptr;
-}
-
 // Pass 1: speculative iteration of every unit.
 __global__ __launch_bounds__(1024) void iter_spec_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
                                                         Unit *units, uint64_t *slots, uint32_t *counts, uint32_t *dirty) {
@@ -1584,29 +1574,23 @@ __device__ bool repair_unit(const BatchDev &b, const Geo &g, const FwdDfaDev &f,
 // Pass 2: units entered through a dirty speculative exit are repaired in
 // parallel; repairs that change their own exit are queued for the walker.
 // Dirty exits are rare, so a block stages the hot tables into LDS only when
-// one of its units needs a repair (lds = nullptr: the images are read in
-// place, table_view).
+// one of its units needs a repair.
 __device__ __forceinline__ void fix_body(const BatchDev &b, const Geo &g, uint64_t nunits, const FwdDfaDev &f,
                                          const RevDfaDev &r, Unit *units, uint32_t *counts, const uint64_t *slots,
                                          uint64_t *queue, unsigned long long *qlen, const uint32_t *dirty,
                                          uint8_t *lds) {
   if (*dirty == 0) return;  // every speculative exit was clean
-  const uint8_t *tl = lds, *rlds = nullptr;
+  const uint8_t *rlds = nullptr;
   bool staged = false;
   for (uint64_t u0 = (uint64_t)blockIdx.x * blockDim.x; u0 + 1 < nunits; u0 += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t u = u0 + threadIdx.x;
     const bool need = u + 1 < nunits && (u + 1) % g.nk != 0 && !(units[u].flags & U_SPEC_CLEAN);
-    if (!lds) {
-      if (!need) continue;
-      table_view(f, r, tl, rlds);
-    } else {
-      if (!__syncthreads_or(need)) continue;
-      if (!staged) {
-        rlds = stage_tables(f, r, lds);
-        staged = true;
-      }
+    if (!__syncthreads_or(need)) continue;
+    if (!staged) {
+      rlds = stage_tables(f, r, lds);
+      staged = true;
     }
-    if (need && repair_unit(b, g, f, r, tl, rlds, u + 1, units[u].spec_exit, units, counts, slots)) {
+    if (need && repair_unit(b, g, f, r, lds, rlds, u + 1, units[u].spec_exit, units, counts, slots)) {
       const unsigned long long q = atomicAdd(qlen, 1ull);
       queue[q] = u + 1;
     }
@@ -1617,7 +1601,8 @@ __global__ __launch_bounds__(1024) void iter_fix_kernel(BatchDev b, Geo g, uint6
                                                        Unit *units, uint32_t *counts, const uint64_t *slots,
                                                        uint64_t *queue, unsigned long long *qlen,
                                                        const uint32_t *dirty) {
-  fix_body(b, g, nunits, f, r, units, counts, slots, queue, qlen, dirty, nullptr);  // tables in place
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  fix_body(b, g, nunits, f, r, units, counts, slots, queue, qlen, dirty, lds);
 }
 
 // Pass 3 (one thread): propagate exits that changed, in unit order.
@@ -1832,18 +1817,12 @@ __device__ __forceinline__ void emit_body(const BatchDev &b, const Geo &g, uint6
         }
       }
     }
-    const uint8_t *tl = lds;
-    if (!lds) {  // the images in place (table_view)
-      if (!rerun) continue;
-      table_view(f, r, tl, rlds);
-    } else {
-      if (!__syncthreads_or(rerun)) continue;
-      if (!staged) {
-        rlds = stage_tables(f, r, lds);
-        staged = true;
-      }
-      if (!rerun) continue;
+    if (!__syncthreads_or(rerun)) continue;
+    if (!staged) {
+      rlds = stage_tables(f, r, lds);
+      staged = true;
     }
+    if (!rerun) continue;
     const Unit U = units[u];
     uint64_t h, len, c0, c1;
     const uint8_t *base;
@@ -1851,7 +1830,7 @@ __device__ __forceinline__ void emit_body(const BatchDev &b, const Geo &g, uint6
     UnitIter it;
     it.init(U.entry, c1);
     uint64_t s, e, i = 0;
-    while (i < cnt && it.next(f, r, tl, rlds, base, len, &s, &e)) {
+    while (i < cnt && it.next(f, r, lds, rlds, base, len, &s, &e)) {
       if (o0 + i < cap) {
         out[2 * (o0 + i)] = s;
         out[2 * (o0 + i) + 1] = e;
@@ -1864,7 +1843,8 @@ __device__ __forceinline__ void emit_body(const BatchDev &b, const Geo &g, uint6
 __global__ __launch_bounds__(1024) void iter_emit_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
                                                         const Unit *units, const uint64_t *slots, const uint64_t *off,
                                                         uint64_t *out, uint64_t cap, int copies) {
-  emit_body<true>(b, g, nunits, f, r, units, slots, off, out, cap, nullptr, copies != 0);  // tables in place
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  emit_body<true>(b, g, nunits, f, r, units, slots, off, out, cap, lds, copies != 0);
 }
 
 // The copies of a lexer pass in output order: block k writes output records
@@ -2273,9 +2253,11 @@ static hipError_t iter_post(const BatchDev &b, const Geo &g, uint64_t nunits, co
                             bool dense = false) {
   hipError_t e;
   const int bs = iter_bs();
-  // no dynamic LDS: fix and emit read the table images in place (table_view)
-  const size_t lb = 0;
-  const int grid = grid_cap(nunits, bs, cus, 2048 / bs);
+  const size_t lb = iter_lds_bytes(f, r);
+  const int per_cu = std::max<int>(1, std::min<int>(2048 / bs, (int)((160u * 1024u) / std::max<size_t>(lb, 1))));
+  const int grid = grid_cap(nunits, bs, cus, per_cu);
+  if ((e = allow_lds(iter_fix_kernel, lb)) != hipSuccess || (e = allow_lds(iter_emit_kernel, lb)) != hipSuccess)
+    return e;
   if (spn && spn->entry) {
     FwdDfaDev fw = f;
     fw.hot = 0;
@@ -2369,8 +2351,9 @@ __global__ void multi_entry_kernel(BatchDev b, Geo g, uint64_t nunits, const Pos
 }
 
 __global__ __launch_bounds__(1024) void multi_fix_kernel(BatchDev b, Geo g, uint64_t nunits, const PostDesc *d) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const PostDesc &P = d[blockIdx.y];
-  fix_body(b, g, nunits, P.f, P.r, P.units, P.counts, P.slots, P.queue, P.qlen, P.dirty, nullptr);
+  fix_body(b, g, nunits, P.f, P.r, P.units, P.counts, P.slots, P.queue, P.qlen, P.dirty, lds);
 }
 
 __global__ void multi_walk_kernel(BatchDev b, Geo g, uint64_t nunits, const PostDesc *d) {
@@ -2385,8 +2368,9 @@ __global__ void multi_walk_kernel(BatchDev b, Geo g, uint64_t nunits, const Post
 }
 
 __global__ __launch_bounds__(1024) void multi_emit_kernel(BatchDev b, Geo g, uint64_t nunits, const PostDesc *d) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const PostDesc &P = d[blockIdx.y];
-  emit_body<false>(b, g, nunits, P.f, P.r, P.units, P.slots, P.off, P.out, P.cap, nullptr);
+  emit_body<false>(b, g, nunits, P.f, P.r, P.units, P.slots, P.off, P.out, P.cap, lds);
 }
 
 __global__ void multi_counts_exit_kernel(BatchDev b, Geo g, uint64_t nunits, const PostDesc *d) {
@@ -2521,16 +2505,18 @@ hipError_t launch_find_iter_multi(const BatchDev &b, int nre, const FwdDfaDev *c
     if ((e = hipGetLastError()) != hipSuccess) break;
     // the passes of iter_post, each once for all regexes (blockIdx.y)
     const int bs = iter_bs();
-    // no dynamic LDS: fix and emit read the table images in place (table_view)
-    const uint32_t grid = (uint32_t)grid_cap(nunits, bs, cus, 2048 / bs);
+    const int per_cu = std::max<int>(1, std::min<int>(2048 / bs, (int)((160u * 1024u) / std::max<size_t>(lb, 1))));
+    const uint32_t grid = (uint32_t)grid_cap(nunits, bs, cus, per_cu);
+    if ((e = allow_lds(multi_fix_kernel, lb)) != hipSuccess || (e = allow_lds(multi_emit_kernel, lb)) != hipSuccess)
+      break;
     if (entries) hipLaunchKernelGGL(multi_entry_kernel, dim3(1, nre), dim3(64), 0, st, b, g, nunits, ddesc);
     if (g.nk > 1) {
-      hipLaunchKernelGGL(multi_fix_kernel, dim3(grid, nre), dim3(bs), 0, st, b, g, nunits, ddesc);
+      hipLaunchKernelGGL(multi_fix_kernel, dim3(grid, nre), dim3(bs), lb, st, b, g, nunits, ddesc);
       hipLaunchKernelGGL(multi_walk_kernel, dim3(1, nre), dim3(64), 0, st, b, g, nunits, ddesc);
     }
     if ((e = hipGetLastError()) != hipSuccess) break;
     if ((e = scan_counts(counts_all, off_all, nre * seg - 1, st)) != hipSuccess) break;
-    hipLaunchKernelGGL(multi_emit_kernel, dim3(grid, nre), dim3(bs), 0, st, b, g, nunits, ddesc);
+    hipLaunchKernelGGL(multi_emit_kernel, dim3(grid, nre), dim3(bs), lb, st, b, g, nunits, ddesc);
     hipLaunchKernelGGL(multi_counts_exit_kernel, dim3(grid_cap(b.count, 256, cus, 4), nre), dim3(256), 0, st, b, g,
                        nunits, ddesc);
     e = hipGetLastError();
