@@ -67,6 +67,10 @@ class Builder {
         if (err) *err = "DFA state budget exceeded (" + std::to_string(lim_.max_raw_states) + " states)";
         return false;
       }
+      if (lim_.max_bytes && key_bytes_ + trans_cls_.size() * 4 > lim_.max_bytes) {
+        if (err) *err = "DFA construction memory budget exceeded (" + std::to_string(lim_.max_bytes) + " bytes)";
+        return false;
+      }
       std::string key = keys_[s];  // copy: keys_ may grow
       if (strip_) strip_raw_.push_back(strip_key(key));
       trans_cls_.resize((s + 1) * ncls);
@@ -130,6 +134,10 @@ class Builder {
  private:
   const Program &p_;
   DfaBuildLimits lim_;
+  // host memory held per interned state key beyond its bytes (two strings,
+  // the hash node): the estimate max_bytes is checked against
+  static constexpr size_t kKeyOverhead = 128;
+  size_t key_bytes_ = 0;
   SparseSet qa_, qb_, qc_;
   std::vector<uint32_t> stack_;
   // step_row's cache across states: (flags, slots, target ips) -> raw state
@@ -241,6 +249,7 @@ class Builder {
     uint32_t id = (uint32_t)keys_.size();
     ids_.emplace(key, id);
     keys_.push_back(key);
+    key_bytes_ += 2 * key.size() + kKeyOverhead;
     return id;
   }
 
@@ -257,6 +266,7 @@ class Builder {
     auto it = ids_.find(k);
     if (it != ids_.end()) return it->second;
     uint32_t id = (uint32_t)keys_.size();
+    key_bytes_ += 2 * k.size() + kKeyOverhead;
     ids_.emplace(k, id);
     keys_.push_back(std::move(k));
     return id;

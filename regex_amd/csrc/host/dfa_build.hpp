@@ -57,9 +57,12 @@ struct DfaBuildLimits {
   bool strip = false;
   bool columns = false;   // emit ctrans / colmap instead of the 256-wide trans
   bool minimise = true;   // false: raw states kept (same language, more states)
+  size_t max_bytes = 0;   // construction memory budget (state keys + rows, estimated); 0 = none
 };
 // Raw-state budget of the u32 (column form) automata.
 constexpr int kBigDfaRawStates = 1 << 21;
+// Construction memory budget of the u32 automata (RURE_AMD_BIG_BYTES overrides).
+constexpr size_t kBigDfaBytes = (size_t)1 << 30;
 
 // Builds the DFA for `prog` (a forward DFA program with `.*?` unless anchored,
 // or a reverse program).  Returns false (with `err`) if the state budget is

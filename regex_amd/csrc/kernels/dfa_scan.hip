@@ -39,7 +39,8 @@ __device__ __forceinline__ void note_quit(uint32_t *flag) {
 
 template <int MODE>
 __device__ __forceinline__ void finish_lane(const LaneState &L, const RevDfaDev &r, const uint8_t *base,
-                                            uint64_t len, uint64_t lo, uint64_t h, void *out, uint32_t *qf) {
+                                            uint64_t len, uint64_t lo, uint64_t h, void *out, uint32_t *qf,
+                                            const uint8_t *rlds = nullptr) {
   if (L.quit) note_quit(qf);
   if (MODE == MODE_ISMATCH) {
     ((uint8_t *)out)[h] = L.quit ? 2 : (L.last != NONE ? 1 : 0);
@@ -57,7 +58,7 @@ __device__ __forceinline__ void finish_lane(const LaneState &L, const RevDfaDev 
     if (me == lo) {
       ms = lo;                              // exec.rs:647
     } else {
-      const uint64_t rs = rev_scan(r, nullptr, base, len, lo, me);
+      const uint64_t rs = rev_scan(r, rlds, base, len, lo, me);
       if (rs == QUITMARK) note_quit(qf);
       if (rs == QUITMARK) ms = me = QUITMARK;
       else if (rs == NONE) ms = me = NONE;  // exec.rs:656-660: reverse NoMatch -> no match
@@ -832,6 +833,159 @@ hipError_t launch_set_cores(const BatchDev &b, const SetCoreDev &f, uint64_t *ou
 }
 
 
+// ------------------------------------------------------- ragged line batches
+// find / is_match / shortest_match over offset batches (log lines, text
+// lines): one lane per line, the line walked in 16-byte blocks as the set
+// kernel walks its lines.  The head and tail blocks of a line (lines start
+// and end anywhere) run the same branch-free 16-lookup chain with the bytes
+// outside the line sent to the identity column kIdCol, instead of single
+// steps with one global byte load each; a line's prologue (its offsets, then
+// the blocks holding its first bytes) is a chain of dependent loads, so the
+// lane loads the offsets two lines ahead and the first two blocks one line
+// ahead, issued after the current line's body loop.  Every step is
+// dfa.rs:576-764's: a block that leaves the hot states (match, dead, quit or
+// cold state) is redone byte by byte against the full table.
+
+// One 16-byte block of a line; the bytes [k0, kend) belong to the line, byte
+// j sits at haystack position pos0 + j.
+template <int MODE, bool MASKED>
+__device__ __forceinline__ void line_block(LaneState &L, const FwdDfaDev &f, const uint8_t *lds, uint4 v,
+                                           uint64_t pos0, uint32_t k0, uint32_t kend) {
+  if (L.s < f.hot) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t t = L.s;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      uint32_t b = (w[j >> 2] >> ((j & 3) * 8)) & 0xFF;
+      if (MASKED) b = ((uint32_t)j >= k0 && (uint32_t)j < kend) ? b : kIdCol;
+      t = lds[__umul24(t, kRow) + b];
+    }
+    if (t != f.hot) { L.s = t; return; }
+  }
+#pragma unroll 1
+  for (uint32_t j = k0; j < kend && !L.done; ++j) step1<MODE>(L, f, lds, block_byte(v, j), pos0 + j);
+}
+
+// LDS layout of dfa_line_kernel: the forward hot table, the start states
+// (128 x u16), then for find the reverse DFA's hot table (the reverse scan of
+// each match steps in LDS instead of the global u16 table).
+__host__ __device__ inline uint32_t line_rev_off(uint32_t f_bytes) { return core_start_off(f_bytes) + 256; }
+__host__ __device__ inline uint32_t line_lds_total(int mode, uint32_t f_bytes, uint32_t r_bytes) {
+  return line_rev_off(f_bytes) + (mode == MODE_FIND ? ((r_bytes + 15) & ~15u) : 0u);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(1024) void dfa_line_kernel(BatchDev bt, FwdDfaDev f, RevDfaDev r, void *out) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  for (uint32_t i = threadIdx.x * 16; i < f.lds_bytes; i += blockDim.x * 16)
+    *(uint4 *)(lds + i) = *(const uint4 *)(f.lds_image + i);
+  uint8_t *rlds = lds + line_rev_off(f.lds_bytes);
+  if (MODE == MODE_FIND)
+    for (uint32_t i = threadIdx.x * 16; i < r.lds_bytes; i += blockDim.x * 16)
+      *(uint4 *)(rlds + i) = *(const uint4 *)(r.lds_image + i);
+  uint16_t *ST = (uint16_t *)(lds + core_start_off(f.lds_bytes));
+  if (threadIdx.x < 128) ST[threadIdx.x] = f.start[threadIdx.x];
+  __syncthreads();
+  const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t at0 = bt.start;
+  auto line = [&](uint64_t h, uint64_t &o0, uint64_t &o1) {
+    const uint64_t hc = h < bt.count ? h : bt.count - 1;  // past the batch: the last line, never scanned
+    o0 = bt.offs[hc];
+    o1 = bt.offs[hc + 1];
+  };
+  // the block holding text[at0] and the one after it (if the line continues),
+  // clamped addresses, no branches
+  auto blocks = [&](uint64_t o0, uint64_t o1, uint4 &b0, uint4 &b1) {
+    const uint8_t *p = bt.hay + o0 + at0;
+    const uint8_t *a = p - ((uintptr_t)p & 15);
+    const bool any = at0 < o1 - o0, more = any && (uint64_t)(a + 16 - p) < o1 - o0 - at0;
+    const uint4 *q0 = any ? (const uint4 *)a : (const uint4 *)bt.offs;  // offs: 16 readable bytes
+    b0 = *q0;
+    b1 = *(more ? (const uint4 *)(a + 16) : q0);
+  };
+  uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (h >= bt.count) return;
+  uint64_t a0, a1, b0, b1;
+  uint4 x0, x1;
+  line(h, a0, a1);
+  line(h + nthreads, b0, b1);
+  blocks(a0, a1, x0, x1);
+  for (; h < bt.count; h += nthreads) {
+    uint64_t c0, c1;
+    uint4 y0, y1;
+    const uint8_t *base = bt.hay + a0;
+    const uint64_t len = a1 - a0;
+    uint64_t at = at0;
+    LaneState L;
+    L.last = NONE;
+    L.quit = false;
+    L.fast = false;
+    L.t = 0;
+    L.done = false;
+    const uint32_t k0 = (uint32_t)((uintptr_t)(base + at) & 15);
+    if (at > len) {
+      L.s = f.dead;
+      L.done = true;
+    } else {
+      if (f.ustart1) {
+        L.s = f.ustart1 - 1;
+      } else {
+        const uint32_t prev = at > 0 ? base[at - 1] : 0u;
+        const uint32_t cur = at < len ? block_byte(x0, k0) : 0u;
+        L.s = ST[fwd_flag_index_bytes(len, at, prev, cur)];
+      }
+      if (L.s >= f.n_normal) L.done = true;  // dead start state (dfa.rs:484)
+    }
+    uint4 cur = x0;
+    if (!L.done && at < len && k0) {  // head: the rest of one aligned block
+      const uint32_t kend = len - at < 16 - k0 ? k0 + (uint32_t)(len - at) : 16;
+      line_block<MODE, true>(L, f, lds, x0, at - k0, k0, kend);
+      at += kend - k0;
+      cur = x1;
+    }
+    while (!L.done && at + 16 <= len) {  // at is 16-byte aligned here
+      uint4 nxt = make_uint4(0, 0, 0, 0);
+      if (at + 16 < len) nxt = *(const uint4 *)(base + at + 16);
+      line_block<MODE, false>(L, f, lds, cur, at, 0, 16);
+      cur = nxt;
+      at += 16;
+    }
+    // the next lines' prologue loads (vector loads complete in order: issued
+    // here, no later wait of this line waits for them)
+    line(h + 2 * nthreads, c0, c1);
+    blocks(b0, b1, y0, y1);
+    if (!L.done && at < len) line_block<MODE, true>(L, f, lds, cur, at, 0, (uint32_t)(len - at));
+    if (!L.done && f.eof[L.s]) L.last = len;  // dfa.rs:748-763
+    finish_lane<MODE>(L, r, base, len, at0, h, out, bt.quit_flag, rlds);
+    a0 = b0; a1 = b1; b0 = c0; b1 = c1; x0 = y0; x1 = y1;
+  }
+}
+
+// whether dfa_line_kernel serves an offsets batch (RURE_AMD_LINES=0: the
+// one-lane-per-haystack dfa_fwd_kernel, A/B)
+static bool line_path_ok(const BatchDev &b, const FwdDfaDev &f) {
+  if (b.offs == nullptr || f.all || b.count == 0) return false;
+  const char *v = getenv("RURE_AMD_LINES");
+  return !(v && v[0] == '0');
+}
+
+template <int MODE>
+static hipError_t launch_lines_m(const BatchDev &b, const FwdDfaDev &f, const RevDfaDev &r, void *out,
+                                 hipStream_t st) {
+  const uint32_t lds = line_lds_total(MODE, f.lds_bytes, r.lds_bytes);
+  const int bs = 1024;
+  const int per_cu = std::max<int>(1, std::min<int>(2, (int)((160u * 1024u) / lds)));
+  const uint64_t blocks = (b.count + bs - 1) / bs;
+  const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (uint64_t)f.cus * per_cu));
+  auto kern = dfa_line_kernel<MODE>;
+  hipError_t e;
+  if (lds > 64 * 1024 &&
+      (e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess)
+    return e;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(bs), lds, st, b, f, r, out);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------- anchored reverse
 // MatchType::DfaAnchoredReverse (exec.rs:1175-1177): a regex anchored at the
 // end and not at the start matches only at the end of the text, so the
@@ -956,6 +1110,14 @@ hipError_t launch_dfa_fwd(int mode, const BatchDev &b, const FwdDfaDev &f, const
       case MODE_FIND: return launch_tile<MODE_FIND>(b, f, r, out, st, tgrid);
       case MODE_ISMATCH: return launch_tile<MODE_ISMATCH>(b, f, r, out, st, tgrid);
       default: return launch_tile<MODE_SHORTEST>(b, f, r, out, st, tgrid);
+    }
+  }
+  if (line_path_ok(b, f)) {
+    g_last_fwd_path.store(-8);
+    switch (mode) {
+      case MODE_FIND: return launch_lines_m<MODE_FIND>(b, f, r, out, st);
+      case MODE_ISMATCH: return launch_lines_m<MODE_ISMATCH>(b, f, r, out, st);
+      default: return launch_lines_m<MODE_SHORTEST>(b, f, r, out, st);
     }
   }
   g_last_fwd_path.store(0);

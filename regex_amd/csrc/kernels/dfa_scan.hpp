@@ -11,6 +11,9 @@ namespace rure_amd {
 // model over the C2 haystacks gives 4.15 LDS cycles per lookup
 // wave-instruction at 304 vs 4.67 at 260 and 4.86 at 256 (2 = conflict free).
 constexpr uint32_t kRow = 304;
+// Column of the forward hot rows (in the padding) holding the row's own
+// number: the identity step for bytes outside a masked block.
+constexpr uint32_t kIdCol = 256;
 
 enum { MODE_FIND = 0, MODE_ISMATCH = 1, MODE_SHORTEST = 2 };
 

@@ -71,6 +71,9 @@ struct DevTables {
   void *core_blob = nullptr;  // re-ranked core tables (adapt_cores)
   bool has_dfa = false;     // the DFA materialised (else: Pike VM only)
   bool has_big = false;     // big (u32) forward / reverse automata: bf, br
+  bool big_tried = false;   // big automata built (lazily, big_device) or found not to build
+  void *big_blob = nullptr; // their device copy
+  struct rure *owner = nullptr;  // the regex (big_device builds its automata on first need)
   BigDfaDev bf{}, br{};
   bool quit_possible = false;  // the DFA can quit (Unicode \b): Pike VM fallback pass
   bool anchored_rev = false;   // MatchType::DfaAnchoredReverse (exec.rs:1175-1177)
@@ -218,11 +221,15 @@ bool pack_forward(const DenseDfa &d, PackedFwd *p, std::string *err, bool all = 
   p->hot = hot;
   size_t lds_bytes = ((size_t)(hot + 1) * kRow + 15) & ~(size_t)15;
   p->lds.assign(lds_bytes, 0);
-  for (uint32_t s = 0; s <= hot; ++s)
+  for (uint32_t s = 0; s <= hot; ++s) {
     for (int b = 0; b < 256; ++b) {
       uint32_t t = (s < hot) ? d.trans[(size_t)s * 256 + b] : hot;
       p->lds[(size_t)s * kRow + b] = (uint8_t)(t < hot ? t : hot);
     }
+    // column 256 (row padding): the identity, for the bytes outside a masked
+    // head / tail block of the line kernel (dfa_line_kernel)
+    p->lds[(size_t)s * kRow + kIdCol] = (uint8_t)s;
+  }
   build_stride_image(d, p);
   p->full.resize((size_t)d.nstates * 256);
   for (size_t i = 0; i < p->full.size(); ++i) p->full[i] = (uint16_t)d.trans[i];
@@ -640,7 +647,7 @@ struct rure {
   PackedFwd pf, pr;   // forward / reverse hot tables
   // automata past the u16 tables (column form, u32; big_dfa.hip): batched
   // find / is_match / shortest_match only, when dfa_ok is false
-  bool big_ok = false;
+  bool big_ok = false, big_built = false;
   DenseDfa bfwd, brev;
   NfaTables nt;
   bool nfa_ok = false;
@@ -739,6 +746,8 @@ void build_big_dfas(rure *re) {
   if (!re->nfa.anchored_start && re->nfa.anchored_end) return;
   DfaBuildLimits lim;
   lim.max_raw_states = kBigDfaRawStates;
+  lim.max_bytes = kBigDfaBytes;
+  if (const char *v = getenv("RURE_AMD_BIG_BYTES")) lim.max_bytes = (size_t)std::max(1ll, atoll(v));
   lim.columns = true;
   lim.minimise = false;   // construction already shares step targets; refinement doubled the build time
   std::string e1, e2;
@@ -770,8 +779,7 @@ bool build_regex(rure *re) {
   if (fwd_ok && !rev_ok) err = rerr;
   if (!fwd_ok || !rev_ok || !pack_forward(re->dfwd, &re->pf, &err) || !pack_forward(re->drev, &re->pr, &err, true)) {
     re->dfa_err = err.empty() ? "reverse DFA too large" : err;
-    re->dfa_ok = false;
-    build_big_dfas(re);
+    re->dfa_ok = false;   // the big automata are built on first need (big_device)
     if (!re->nfa_ok) re->dfa_err += "; " + nerr;
     return re->nfa_ok;
   }
@@ -945,16 +953,6 @@ DevTables *regex_device(rure *re, std::string *err) {
     o_rstart = b.add(rstart.data(), 256);
     o_rlds = b.add(re->pr.lds.data(), re->pr.lds.size());
   }
-  size_t o_big[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (re->big_ok) {
-    const DenseDfa *bd[2] = {&re->bfwd, &re->brev};
-    for (int k = 0; k < 2; ++k) {
-      o_big[4 * k] = b.add(bd[k]->ctrans.data(), bd[k]->ctrans.size() * 4);
-      o_big[4 * k + 1] = b.add(bd[k]->colmap, 256);
-      o_big[4 * k + 2] = b.add(bd[k]->eof_match.data(), bd[k]->eof_match.size());
-      o_big[4 * k + 3] = b.add(bd[k]->start, 128 * 4);
-    }
-  }
   const bool mt_lane = needs_mt_lane(re->xl);
   LitOffsets lp{}, ls{};
   size_t o_lcs = 0;
@@ -1016,32 +1014,64 @@ DevTables *regex_device(rure *re, std::string *err) {
     // from the end of the text (exec.rs:1175-1177, 671-688)
     t.anchored_rev = !re->nfa.anchored_start && re->nfa.anchored_end;
   }
-  if (re->big_ok) {
-    const DenseDfa *bd[2] = {&re->bfwd, &re->brev};
-    BigDfaDev *dst[2] = {&t.bf, &t.br};
-    for (int k = 0; k < 2; ++k) {
-      const DenseDfa &D = *bd[k];
-      BigDfaDev &x = *dst[k];
-      x.trans = (const uint32_t *)(base + o_big[4 * k]);
-      x.colmap = base + o_big[4 * k + 1];
-      x.eof = base + o_big[4 * k + 2];
-      x.start = (const uint32_t *)(base + o_big[4 * k + 3]);
-      x.ncol = D.ncol;
-      x.nstates = (uint32_t)D.nstates;
-      x.hot = k == 0 ? big_dfa_hot_rows(D.ncol, (uint32_t)D.nstates) : 0;
-      x.n_normal = (uint32_t)D.n_normal;
-      x.n_match_end = (uint32_t)D.n_match_end;
-      x.dead = (uint32_t)D.dead;
-      x.ustart1 = uniform_start(D);
-    }
-    t.has_big = true;
-  }
+  t.owner = re;
   if (t.quit_possible && !re->nfa_ok) {
     (void)hipFree(t.blob);
     if (err) *err = "the DFA can quit and the NFA tables could not be built";
     return nullptr;
   }
   return &(re->dev[d] = t);
+}
+
+// Automata past the u16 tables, built and uploaded on the first batch that
+// would run them (big_batch): their construction can take seconds and
+// hundreds of MB of host memory (bounded by kBigDfaBytes), which a regex
+// searched on the Pike VM only (few long haystacks) never needs.  Returns
+// whether t now has them.
+bool big_device(const DevTables &tc) {
+  DevTables &t = const_cast<DevTables &>(tc);  // the regex's own entry of rure::dev
+  rure *re = t.owner;
+  if (!re) return false;
+  std::lock_guard<std::mutex> g(re->mu);
+  if (t.big_tried) return t.has_big;
+  t.big_tried = true;
+  if (!re->big_built) {
+    re->big_built = true;
+    build_big_dfas(re);
+  }
+  if (!re->big_ok) return false;
+  Blob b;
+  size_t o_big[8];
+  const DenseDfa *bd[2] = {&re->bfwd, &re->brev};
+  for (int k = 0; k < 2; ++k) {
+    o_big[4 * k] = b.add(bd[k]->ctrans.data(), bd[k]->ctrans.size() * 4);
+    o_big[4 * k + 1] = b.add(bd[k]->colmap, 256);
+    o_big[4 * k + 2] = b.add(bd[k]->eof_match.data(), bd[k]->eof_match.size());
+    o_big[4 * k + 3] = b.add(bd[k]->start, 128 * 4);
+  }
+  DevTables tmp;
+  std::string err;
+  if (!upload_blob(b, &tmp, &err)) return false;
+  uint8_t *base = (uint8_t *)tmp.blob;
+  BigDfaDev *dst[2] = {&t.bf, &t.br};
+  for (int k = 0; k < 2; ++k) {
+    const DenseDfa &D = *bd[k];
+    BigDfaDev &x = *dst[k];
+    x.trans = (const uint32_t *)(base + o_big[4 * k]);
+    x.colmap = base + o_big[4 * k + 1];
+    x.eof = base + o_big[4 * k + 2];
+    x.start = (const uint32_t *)(base + o_big[4 * k + 3]);
+    x.ncol = D.ncol;
+    x.nstates = (uint32_t)D.nstates;
+    x.hot = k == 0 ? big_dfa_hot_rows(D.ncol, (uint32_t)D.nstates) : 0;
+    x.n_normal = (uint32_t)D.n_normal;
+    x.n_match_end = (uint32_t)D.n_match_end;
+    x.dead = (uint32_t)D.dead;
+    x.ustart1 = uniform_start(D);
+  }
+  t.big_blob = tmp.blob;
+  t.has_big = true;
+  return true;
 }
 
 DevTables *set_device(rure_set *rs, std::string *err) {
@@ -1509,7 +1539,7 @@ bool big_batch(const BatchDev &b, const DevTables &t) {
 hipError_t run_regex(int mode, const BatchDev &b, const DevTables &t, void *out, hipStream_t st, int dfa_grid,
                      const FwdDfaDev *iter = nullptr) {
   if (lane_search_ok(t)) return run_lane_search(mode, b, t, out, st);
-  if (!t.has_dfa && t.has_big && big_batch(b, t)) return launch_big_dfa(mode, b, t.bf, t.br, out, st, t.cus);
+  if (!t.has_dfa && big_batch(b, t) && big_device(t)) return launch_big_dfa(mode, b, t.bf, t.br, out, st, t.cus);
   if (!t.has_dfa) return run_pike(mode, false, b, t, out, st);
   uint64_t chunk = 0;
   if (iter && long_batch(mode, b, t, &chunk) && !(t.anchored_rev && b.start != 0))
@@ -1822,6 +1852,7 @@ void rure_free(rure *re) {
     (void)hipGetDevice(&cur);
     (void)hipSetDevice(kv.first);
     (void)hipFree(kv.second.blob);
+    if (kv.second.big_blob) (void)hipFree(kv.second.big_blob);
     (void)hipSetDevice(cur);
   }
   delete re;
@@ -2393,11 +2424,14 @@ bool build_multi_locked(rure_set *rs, MultiSet *m, std::string *err, const std::
   return true;
 }
 
-// Host copy of up to 4096 haystacks of the batch (the profile sample).
+// Host copy of the first haystacks of the batch (the profile sample): at most
+// 4096 of them, each cut to its first 4 KiB, at most 4 MiB in all (so a few
+// huge haystacks cost a bounded copy).
 std::vector<std::string> batch_sample(const BatchDev &b, hipStream_t st) {
   std::vector<std::string> out;
   const uint64_t n = std::min<uint64_t>(b.count, 4096);
   if (!n) return out;
+  constexpr uint64_t kPerHay = 4096, kTotal = 4u << 20;
   std::vector<uint64_t> offs(n + 1);
   if (b.offs) {
     if (hipMemcpyAsync(offs.data(), b.offs, (n + 1) * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -2406,14 +2440,17 @@ std::vector<std::string> batch_sample(const BatchDev &b, hipStream_t st) {
   } else {
     for (uint64_t i = 0; i <= n; ++i) offs[i] = i * b.stride;
   }
-  const uint64_t lo = offs[0], hi = b.offs ? offs[n] : (n - 1) * b.stride + b.length;
-  std::vector<uint8_t> bytes(hi - lo);
-  if (hipMemcpyAsync(bytes.data(), b.hay + lo, hi - lo, hipMemcpyDeviceToHost, st) != hipSuccess ||
-      hipStreamSynchronize(st) != hipSuccess)
-    return out;
-  for (uint64_t i = 0; i < n; ++i) {
-    const uint64_t a = offs[i] - lo, len = b.offs ? offs[i + 1] - offs[i] : b.length;
-    out.emplace_back((const char *)bytes.data() + a, len);
+  std::vector<uint8_t> buf;
+  uint64_t total = 0;
+  for (uint64_t i = 0; i < n && total < kTotal; ++i) {
+    const uint64_t len = b.offs ? offs[i + 1] - offs[i] : b.length;
+    const uint64_t take = std::min<uint64_t>({len, kPerHay, kTotal - total});
+    buf.resize(take);
+    if (take && (hipMemcpyAsync(buf.data(), b.hay + offs[i], take, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                 hipStreamSynchronize(st) != hipSuccess))
+      return out;
+    out.emplace_back((const char *)buf.data(), take);
+    total += take;
   }
   return out;
 }
@@ -2425,6 +2462,12 @@ const MultiCoreDev *multi_device(rure_set *rs, std::string *err, const BatchDev 
   MultiSet *m = rs->multi;
   if (!m->built) {
     m->built = true;
+    // opt-in (RURE_AMD_SET_MULTI=1): the default path never samples
+    const char *on = getenv("RURE_AMD_SET_MULTI");
+    if (!(on && on[0] == '1')) {
+      m->ok = false;
+      return nullptr;
+    }
     const std::vector<std::string> sample = batch_sample(b, st);
     m->ok = build_multi_locked(rs, m, err, &sample, b.start);
   }
@@ -2778,13 +2821,18 @@ bool build_kmer(rure *const *res, size_t n, std::vector<uint32_t> *bitmap, std::
   return true;
 }
 
-// The cached device tables for this regex list, or null (not eligible).
-const KmerDev *kmer_device(rure *const *res, size_t n) {
+// The cached device tables for this regex list, copied into *out while the
+// cache lock is held (an entry's address does not outlive the lock: another
+// thread's push_back or kmer_forget moves the vector).  False: not eligible.
+bool kmer_device(rure *const *res, size_t n, KmerDev *out) {
   int d = 0;
-  if (hipGetDevice(&d) != hipSuccess) return nullptr;
+  if (hipGetDevice(&d) != hipSuccess) return false;
   std::lock_guard<std::mutex> g(g_kmer_mu);
   for (const KmerCacheEntry &e : g_kmer)
-    if (e.dev == d && e.res.size() == n && std::equal(e.res.begin(), e.res.end(), res)) return e.blob ? &e.km : nullptr;
+    if (e.dev == d && e.res.size() == n && std::equal(e.res.begin(), e.res.end(), res)) {
+      if (e.blob) *out = e.km;
+      return e.blob != nullptr;
+    }
   KmerCacheEntry ent;
   ent.res.assign(res, res + n);
   ent.dev = d;
@@ -2803,7 +2851,8 @@ const KmerDev *kmer_device(rure *const *res, size_t n) {
     }
   }
   g_kmer.push_back(ent);
-  return g_kmer.back().blob ? &g_kmer.back().km : nullptr;
+  if (ent.blob) *out = ent.km;
+  return ent.blob != nullptr;
 }
 
 // rure_free: drop the k-mer tables of lists holding this regex.
@@ -2857,6 +2906,10 @@ int rure_amd_find_iter_span_multi(rure *const *res, size_t n, const uint8_t *hay
     DevTables *t = regex_device(res[i], &err);
     if (!t) return err.rfind("HIP", 0) == 0 ? RURE_AMD_ERR_HIP : RURE_AMD_ERR_DFA;
     const FwdDfaDev *fi = nullptr;
+    // a regex the reference searches with its own match type (Literal /
+    // DfaSuffix, lane_search_ok) iterates on its own path, as in
+    // rure_amd_find_iter_span: the fused pass is a forward-DFA iteration
+    if (lane_search_ok(*t)) { fused = false; break; }
     if (t->has_dfa && !t->quit_possible && res[i]->nfa_ok && res[i]->nt.looks_used == 0) fi = iter_device(res[i], *t, &err);
     if (!fi || !fi->sa_len) { fused = false; break; }
     fs[i] = fi;
@@ -2871,7 +2924,8 @@ int rure_amd_find_iter_span_multi(rure *const *res, size_t n, const uint8_t *hay
     uint64_t per_cu = 1024;
     if (const char *v = getenv("RURE_AMD_ITER_LANES")) per_cu = std::max(64, atoi(v));
     const uint64_t chunk = odd_lines(std::max<uint64_t>(4096, (span + (uint64_t)cus * per_cu - 1) / ((uint64_t)cus * per_cu)));
-    const KmerDev *km = kmer_device(res, n);
+    KmerDev kmv;
+    const KmerDev *km = kmer_device(res, n, &kmv) ? &kmv : nullptr;
     hipError_t e = launch_find_iter_multi(b, (int)n, fs.data(), rs.data(), chunk, os.data(), st, cus, sps.data(), km);
     if (e == hipSuccess) return RURE_AMD_OK;
     if (e != hipErrorNotSupported) return RURE_AMD_ERR_HIP;
@@ -2954,7 +3008,14 @@ int rure_amd_dfa_info_get(rure *re, int which, rure_amd_dfa_info *info) {
   if (!re || !info) return RURE_AMD_ERR_ARG;
   memset(info, 0, sizeof(*info));
   if (which == 3 || which == 4) {  // the big (u32 column form) automata
-    build_regex(re);
+    if (!build_regex(re) || re->dfa_ok) { info->ok = 0; return RURE_AMD_ERR_DFA; }  // only where the u16 DFA fails
+    {
+      std::lock_guard<std::mutex> g(re->mu);
+      if (!re->big_built) {
+        re->big_built = true;
+        build_big_dfas(re);
+      }
+    }
     if (!re->big_ok) { info->ok = 0; return RURE_AMD_ERR_DFA; }
     fill_info(which == 3 ? re->bfwd : re->brev, which == 3 ? re->fwd : re->rev, 0, info);
     info->byte_classes = (int32_t)(which == 3 ? re->bfwd.ncol : re->brev.ncol);
