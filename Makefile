@@ -38,7 +38,7 @@ $(LIB): $(HOST_OBJ) $(OBJDIR)/rure_amd.o $(KERNEL_OBJ)
 
 $(ORACLE_LIB): $(ORACLE_SRC) $(wildcard oracle/*.h)
 	@mkdir -p oracle/build
-	gcc -O2 -std=c11 -fPIC -shared -Wall -o $@ $(ORACLE_SRC) -lpthread
+	gcc -O3 -std=c11 -fPIC -shared -Wall -o $@ $(ORACLE_SRC) -lpthread
 
 # diagnostic A/B library (tools/*): make ab AB=<name> ABFLAGS=-D...
 ab:

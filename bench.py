@@ -384,10 +384,24 @@ def cpu_baseline(re, hay, res, n, L, args):
         passes += 1
     gbps = S * L * passes / elapsed / 1e9
     parity = bool(np.array_equal(exp.astype(np.int64), res[:S]))
+    # a measured one-thread rate, on the first 4096 haystacks
+    S1 = min(S, 4096)
+    p1, e1 = 0, 0.0
+    while e1 < max(2.0, args.cpu_seconds / 4) and p1 < 256:
+        t0 = time.perf_counter()
+        o.find_batch(buf, L, L, S1, nthreads=1)
+        e1 += time.perf_counter() - t0
+        p1 += 1
+    one = S1 * L * p1 / e1 / 1e9
     d = {"value": round(gbps, 3), "unit": "GB/s", "kind": "port",
          "sample": "%d passes over the first %d haystacks x %d B (%.0f MiB) of the same batch" %
                    (passes, S, L, S * L / 2**20),
-         "per_core_GBps": round(gbps / threads, 3),
+         "engine_path": "lazy DFA forward + reverse (dfa.rs:576-866 via exec.rs:632-662; the date regex has no "
+                        "literal prefixes: MatchType::Dfa)",
+         "per_core_GBps": round(one, 3),
+         "one_thread": {"value": round(one, 3), "unit": "GB/s",
+                        "sample": "%d passes over the first %d haystacks (%.0f MiB), 1 thread" %
+                                  (p1, S1, S1 * L / 2**20)},
          "parity_on_sample": parity, "fwd_bytes_per_pass": int(st["fwd_bytes"])}
     d.update(cpu_info(threads))
     return d
@@ -544,6 +558,7 @@ def run_c3(ctx):
         torch.cuda.synchronize()
     strip_ms = ctx.kernel_ms(strip_pass)
     var_ms = ctx.kernel_ms(variant_pass)
+    pipe = shootout_pipeline(ctx, big, N, copies, kc, variants) if W == 1 else None
     # the dominant kernel of each phase timed live (HIP events the library
     # records around the speculative kernel on the launch stream)
     lex_ms, lex_n = kernel_timer_ms(strip_pass, ctx.args.steps)
@@ -581,6 +596,7 @@ def run_c3(ctx):
                     strip_matches=nsp_sharded, variant_counts=got, known_answers_ok=ok,
                     variant_engine="separate passes" if ctx.args.c3_separate else "one fused pass",
                     cut_recomputations=stats["recomputed"],
+                    **({} if pipe is None else pipe),
                     roofline=roofline_kernel(var_bytes, spec_ms, spec_n, config, var_kernel,
                                              "variant speculative kernel (%s)" %
                                              ("%s_kernel: one read of the stripped span for all 9 variants"
@@ -604,6 +620,47 @@ def run_c3(ctx):
                                            "match records written; driver-visible time incl. launch gaps"
                                            % ("once (fused variant pass)" if fused else "once per variant")},
                     **extra)
+
+
+def shootout_pipeline(ctx, big, N, copies, kc, variants):
+    """The whole regex-dna program (examples/shootout-regex-dna-bytes.rs:16-66)
+    on the device through the C ABI (regex_amd/shootout.py): strip
+    replace_all, the 9 variant counts in one fused pass, the 11 IUB
+    substitutions chained; timed end to end (host syncs included: each
+    replacement reads its output length back to size the next buffer).
+    Known answers: the lengths of examples/regexdna-output.txt x copies, and
+    each variant's count x copies plus the matches across copy seams."""
+    import regex_amd as R
+    from regex_amd.shootout import RegexDna
+    from oracle_py import OracleRegex
+    torch = ctx.torch
+    dna = RegexDna()
+    out = dna.run(big, N, stream=ctx.stream)
+    one = R.Regex(kc["strip"]).replace_all(corpus_regexdna(), b"")
+    ok = out["ilen"] == kc["input_len"] * copies and out["clen"] == kc["stripped_len"] * copies and \
+        out["slen"] == kc["substituted_len"] * copies
+    for v, got in zip(kc["variants"], out["counts"]):
+        seam = len(OracleRegex(R.Regex(v["re"])).find_iter(one * 2)) - 2 * v["count"]
+        ok = ok and got == v["count"] * copies + seam * (copies - 1)
+    times = []
+    for _ in range(max(1, ctx.args.steps)):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        dna.run(big, N, stream=ctx.stream)
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    ms = float(np.median(times)) * 1e3
+    return {"pipeline_ms": round(ms, 3), "pipeline_GBps": round(N / ms / 1e6, 1),
+            "pipeline_known_answers_ok": bool(ok),
+            "pipeline": {"what": "shootout-regex-dna-bytes.rs end to end on the device (regex_amd/shootout.py): "
+                                 "strip replace_all + 9 variant counts (one fused pass) + 11 IUB replace_all, "
+                                 "median of %d runs, host syncs included" % len(times),
+                         "lengths": [out["ilen"], out["clen"], out["slen"]], "counts": out["counts"]}}
+
+
+def corpus_regexdna():
+    from golden_data import corpus
+    return corpus("regexdna")
 
 
 def kernel_timer_ms(fn, steps):
@@ -657,8 +714,10 @@ def cpu_baseline_c3(strip, raw, variants, seq, M, gpu_counts, args):
         # replace_all(.., "") = the bytes outside the matches
         a = np.frombuffer(text, dtype=np.uint8)
         d = np.zeros(R_ + 1, dtype=np.int32)
-        np.add.at(d, sp[:, 0].astype(np.int64), 1)
-        np.add.at(d, sp[:, 1].astype(np.int64), -1)
+        # the spans are disjoint and non-empty here: starts (and ends) are
+        # distinct, so plain fancy-index updates (np.add.at is ~10x slower)
+        d[sp[:, 0].astype(np.int64)] += 1
+        d[sp[:, 1].astype(np.int64)] -= 1
         keep = np.cumsum(d[:R_]) == 0
         return sp.shape[0], a[keep].tobytes()
 
@@ -701,6 +760,15 @@ def cpu_baseline_c3(strip, raw, variants, seq, M, gpu_counts, args):
             "sample": "%d passes over %d copies of the input (%.1f MiB raw -> %.1f MiB stripped): strip "
                       "replace_all on 1 thread, then the 9 variant find_iter on 9 threads (one per variant, "
                       "shootout-regex-dna-bytes.rs:37-42)" % (passes, copies, R_ / 2**20, S / 2**20),
+            "engine_path": {"strip": "MatchType::Dfa with the start-state prefix skip: SingleByteSet {'>', '\\n'} "
+                                     "via memchr2 (dfa.rs:700-711, literals.rs:353-361), then a reverse DFA per "
+                                     "match (exec.rs:632-662)",
+                            "variants": "MatchType::Literal(Unanchored) (exec.rs:1148-1155): the literal searcher "
+                                        "(Teddy / Aho-Corasick in the reference; here one forward pass with a "
+                                        "4-byte hash prefilter, literals.rs:92-103), no DFA"},
+            "reference_published": {"strip_MBps": 343, "source": "bench/log/05/rust:42 (regex-dna strip "
+                                    "`>[^\\n]*\\n|\\n` on the reference's own machine)",
+                                    "ratio_of_strip_1thread": round(R_ * passes / t_strip / 1e9 * 1e3 / 343, 3)},
             "parity_on_sample": bool(gpu_strip == stripped and exp == got)}
 
 
@@ -751,8 +819,19 @@ def cpu_baseline_c4(rs, buf, offs, out, args):
         elapsed += time.perf_counter() - t0
         passes += 1
     got = out[:S].cpu().numpy().view(np.uint64)
+    # the engine path the reference takes on these lines: its 2 MiB lazy-DFA
+    # cache outgrows dfa_size_limit, and after three flushes clear_cache
+    # refuses to flush again within 10 x (states) bytes of the last flush
+    # (dfa.rs:1282-1293, flush_count never resets), so the DFA quits and the
+    # line is answered by the Pike VM (exec.rs:1019-1030)
+    _, st = o.set_batch(hb, 0, 0, S, nthreads=threads, offsets=so, stats=True)
     d = {"value": round(int(so[-1]) * passes / elapsed / 1e9, 3), "unit": "GB/s",
          "kind": "port", "lines_per_s": round(S * passes / elapsed, 1),
+         "engine_path": {"lines": S, "dfa_quits_to_pike_vm": int(st["quits"]),
+                         "lazy_dfa_cache_flushes": int(st["flushes"]),
+                         "cached_states_at_end": int(st["states"]), "threads": threads,
+                         "what": "DfaMany lazy DFA (dfa.rs:525-570) with the reference's 2 MiB cache and flush "
+                                 "policy; a line whose DFA quits is re-run on the Pike VM (pikevm.rs)"},
          "sample": "%d passes over the first %d lines (%.0f MiB) of the same batch" % (passes, S, so[-1] / 2**20),
          "parity_on_sample": bool(np.array_equal(exp, got))}
     d.update(cpu_info(threads))
@@ -838,6 +917,8 @@ def cpu_baseline_c5(re, hay, pos, plant, ctx):
     return {"value": round(S * passes / elapsed / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
             "sample": "%d passes of find over the shard's last %d MiB (one sequential scan, as the reference's "
                       "single-haystack find)" % (passes, S >> 20),
+            "engine_path": "MatchType::Dfa (Unicode \\w: no literal prefixes or suffixes): lazy DFA forward + "
+                           "reverse (exec.rs:632-662)",
             "parity_on_sample": [int(x) for x in exp[0]] == [int(x) for x in sub[0].cpu()] ==
                                 [pos - lo + 1, pos - lo + len(plant) - 1]}
 

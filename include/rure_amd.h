@@ -30,7 +30,7 @@ typedef struct rure rure;                  /* rure.h:29 */
 typedef struct rure_set rure_set;          /* rure.h:36 */
 typedef struct rure_options rure_options;  /* rure.h:47 */
 typedef struct rure_iter rure_iter;        /* rure.h:106 */
-typedef struct rure_error rure_error;      /* rure.h:127 */
+typedef struct rure_error rure_error;      /* rure.h:130 */
 typedef struct rure_captures rure_captures;                      /* rure.h:95 */
 typedef struct rure_iter_capture_names rure_iter_capture_names;  /* rure.h:117 */
 

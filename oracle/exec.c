@@ -193,11 +193,15 @@ static int find_dfa_anchored_reverse(const orc_regex *r, orc_cache *c, int quit_
   return R_MATCH;
 }
 
+/* The forward DFA's prefix literals (dfa.prefixes = nfa.prefixes,
+ * exec.rs:308-311), when the product exported them (orc_regex_set_exec). */
+static const orc_lits *dfa_prefixes(const orc_regex *r) { return r->mt >= 0 ? &r->pre : NULL; }
+
 /* exec.rs:632-662 find_dfa_forward */
 static int find_dfa_forward(const orc_regex *r, orc_cache *c, const uint8_t *text, size_t len, size_t start,
                             size_t *ms, size_t *me) {
   size_t end, stop;
-  int k = orc_dfa_forward(r->fwd, c->fwd, 0, text, len, start, &end, &stop);
+  int k = orc_dfa_forward_pfx(r->fwd, c->fwd, 0, dfa_prefixes(r), text, len, start, &end, &stop);
   c->st.fwd_bytes += stop - start;
   if (k != R_MATCH) return k;
   if (end == start) { *ms = start; *me = start; return R_MATCH; }
@@ -244,8 +248,35 @@ static int lit_at(const orc_lits *l, const uint8_t *hay, size_t n, size_t i, siz
   return 0;
 }
 
-static int lits_find(const orc_lits *l, const uint8_t *hay, size_t n, size_t *s, size_t *e) {
+/* memchr / memchr2 / memchr3 (SingleByteSet::find, literals.rs:353-361):
+ * the first byte of hay[0..n) in {a, b, c} (k of them), SWAR 8 bytes a step */
+static inline uint64_t zero_bytes(uint64_t x) { return (x - 0x0101010101010101ull) & ~x & 0x8080808080808080ull; }
+static long memchr_k(const uint8_t *hay, size_t n, int k, uint8_t a, uint8_t b, uint8_t c) {
+  const uint64_t ra = 0x0101010101010101ull * a, rb = 0x0101010101010101ull * b, rc = 0x0101010101010101ull * c;
+  size_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t w;
+    memcpy(&w, hay + i, 8);
+    uint64_t z = zero_bytes(w ^ ra);
+    if (k > 1) z |= zero_bytes(w ^ rb);
+    if (k > 2) z |= zero_bytes(w ^ rc);
+    if (z) break;  /* (the SWAR test can flag a byte after a true hit only: rescan bytewise) */
+  }
+  for (; i < n; ++i)
+    if (hay[i] == a || (k > 1 && hay[i] == b) || (k > 2 && hay[i] == c)) return (long)i;
+  return -1;
+}
+
+int orc_lits_find(const orc_lits *l, const uint8_t *hay, size_t n, size_t *s, size_t *e) {
   if (l->matcher == 0) { *s = *e = 0; return 1; }
+  if (l->matcher == 1 && l->n <= 3 && !l->any_empty) {  /* Bytes: every literal is one byte */
+    const uint8_t a = l->lit[0][0], b = l->n > 1 ? l->lit[1][0] : a, c = l->n > 2 ? l->lit[2][0] : a;
+    const long i = memchr_k(hay, n, (int)l->n, a, b, c);
+    if (i < 0) return 0;
+    *s = (size_t)i;
+    *e = (size_t)i + 1;
+    return 1;
+  }
   if (l->any_empty) return lit_at(l, hay, n, 0, s, e);
   for (size_t i = 0; i < n; ++i) {
     int cand = 0;
@@ -291,7 +322,7 @@ static int lits_find_end(const orc_lits *l, const uint8_t *hay, size_t n, size_t
 static int find_literals(const orc_regex *r, const uint8_t *text, size_t len, size_t start, size_t *ms, size_t *me) {
   size_t s, e;
   int ok;
-  if (r->mt == 0) ok = lits_find(&r->pre, text + start, len - start, &s, &e);
+  if (r->mt == 0) ok = orc_lits_find(&r->pre, text + start, len - start, &s, &e);
   else if (r->mt == 1) ok = lits_find_start(&r->pre, text + start, len - start, &s, &e);
   else ok = lits_find_end(&r->suf, text + start, len - start, &s, &e);
   if (!ok) return 0;
@@ -334,7 +365,7 @@ static int find_dfa_reverse_suffix(const orc_regex *r, orc_cache *c, const uint8
   /* the suffix occurrence is the earliest possible end: run the forward DFA
    * from the match start for the leftmost-first end */
   size_t end, stop;
-  int k2 = orc_dfa_forward(r->fwd, c->fwd, 0, text, len, s0, &end, &stop);
+  int k2 = orc_dfa_forward_pfx(r->fwd, c->fwd, 0, dfa_prefixes(r), text, len, s0, &end, &stop);
   c->st.fwd_bytes += stop - s0;
   if (k2 == R_QUIT) return R_QUIT;
   if (k2 != R_MATCH) return R_NOMATCH;  /* the reference panics here ("BUG: reverse match implies ...") */
@@ -349,7 +380,7 @@ static int shortest_dfa_reverse_suffix(const orc_regex *r, orc_cache *c, const u
   size_t s0, e0, stop;
   int k = exec_dfa_reverse_suffix(r, c, text, len, start, &s0, &e0);
   if (k < 0) {
-    k = orc_dfa_forward(r->fwd, c->fwd, 1, text, len, start, end, &stop);
+    k = orc_dfa_forward_pfx(r->fwd, c->fwd, 1, dfa_prefixes(r), text, len, start, end, &stop);
     c->st.fwd_bytes += stop - start;
     return k;
   }
@@ -448,7 +479,7 @@ int orc_shortest_match_at(const orc_regex *r, orc_cache *c, const uint8_t *text,
     size_t s;
     k = find_dfa_anchored_reverse(r, c, 1, text, len, start, &s, &e);
   } else {
-    k = orc_dfa_forward(r->fwd, c->fwd, 1, text, len, start, &e, &stop);
+    k = orc_dfa_forward_pfx(r->fwd, c->fwd, 1, dfa_prefixes(r), text, len, start, &e, &stop);
     c->st.fwd_bytes += stop - start;
   }
   if (k == R_MATCH) { *end = e; return 1; }
@@ -475,7 +506,7 @@ int orc_is_match_at(const orc_regex *r, orc_cache *c, const uint8_t *text, size_
     size_t s;
     k = find_dfa_anchored_reverse(r, c, 1, text, len, start, &s, &e);
   } else {
-    k = orc_dfa_forward(r->fwd, c->fwd, 1, text, len, start, &e, &stop);
+    k = orc_dfa_forward_pfx(r->fwd, c->fwd, 1, dfa_prefixes(r), text, len, start, &e, &stop);
     c->st.fwd_bytes += stop - start;
   }
   if (k == R_MATCH) return 1;
@@ -570,7 +601,7 @@ static void *worker(void *arg) {
       j->out[i] = m;
     }
   }
-  j->st = c->st;
+  orc_cache_stats(c, &j->st);  /* counters, plus this thread's cache flushes and final state count */
   orc_cache_free(c);
   return NULL;
 }
@@ -596,6 +627,8 @@ static int run_batch(const orc_regex *r, const uint8_t *buf, const uint64_t *off
       stats->fwd_bytes += jobs[k].st.fwd_bytes;
       stats->rev_bytes += jobs[k].st.rev_bytes;
       stats->quits += jobs[k].st.quits;
+      stats->flushes += jobs[k].st.flushes;
+      stats->states += jobs[k].st.states;
     }
   }
   free(jobs);
@@ -618,4 +651,8 @@ int orc_shortest_batch(const orc_regex *r, const uint8_t *buf, const uint64_t *o
 int orc_set_batch(const orc_regex *r, const uint8_t *buf, const uint64_t *offs, size_t stride, size_t length,
                   size_t n, int nthreads, uint64_t *masks) {
   return run_batch(r, buf, offs, stride, length, n, nthreads, 2, masks, NULL, NULL);
+}
+int orc_set_batch_stats(const orc_regex *r, const uint8_t *buf, const uint64_t *offs, size_t stride, size_t length,
+                        size_t n, int nthreads, uint64_t *masks, orc_stats *stats) {
+  return run_batch(r, buf, offs, stride, length, n, nthreads, 2, masks, NULL, stats);
 }

@@ -14,8 +14,10 @@
  *   start_state/start_flags   dfa.rs:1370-1464
  *   add_state                 dfa.rs:1479-1512
  *   StateFlags/Byte/varints   dfa.rs:1648-1697, 1791-1831
- * Literal prefixes are not modelled (has_prefix() is false), which the
- * reference documents as result-neutral.
+ *   prefix_at / has_prefix    dfa.rs:700-711, 1520-1522, 1562-1579
+ * The prefix skip runs when the caller passes the program's prefix literals
+ * (orc_dfa_forward_pfx); it is result-neutral (the reference documents it
+ * so) and makes the timed CPU baseline the reference's engine path.
  */
 #include <stdlib.h>
 #include <string.h>
@@ -188,6 +190,7 @@ typedef struct {
   uint32_t last_match_si;
   size_t last_cache_flush;
   orc_dfa_cache *cache;
+  const orc_lits *pre;  /* prefix searcher when has_prefix (dfa.rs:1562-1566), else NULL */
 } Fsm;
 
 typedef struct { int kind; size_t v; } DResult;  /* kind: 0 Match, 1 NoMatch, 2 Quit */
@@ -289,7 +292,7 @@ static uint32_t restore_state(Fsm *f, uint8_t *data, uint32_t len) {  /* dfa.rs:
   return add_state(f, data, len);
 }
 
-static uint32_t start_ptr(const Fsm *f, uint32_t si) { (void)f; return si; }  /* no prefixes */
+static uint32_t start_ptr(const Fsm *f, uint32_t si) { return f->pre ? si | STATE_START : si; }  /* dfa.rs:1573-1579 */
 
 static uint8_t *dup_state(const orc_state *st) {
   uint8_t *d = (uint8_t *)malloc(st->len ? st->len : 1);
@@ -503,18 +506,23 @@ static DResult exec_at(Fsm *f, const uint8_t *text, size_t len, size_t *stop) {
   DResult result = {R_NOMATCH, f->at};
   uint32_t prev_si = f->start, nsi = f->start;
   size_t at = f->at;
+  /* the table and class map in locals (next_si, dfa.rs:873-900); the table
+   * moves only when the slow path adds a state, so it is reloaded per round */
+  const uint8_t *cls = f->prog->byte_classes;
+  const uint32_t *T;
   while (at < len) {
+    T = f->cache->trans;
     while (nsi <= STATE_MAX && at < len) {
-      prev_si = next_si(f, nsi, text, at);
+      prev_si = T[(nsi) + cls[text[at]]];
       at += 1;
       if (prev_si > STATE_MAX || at + 2 >= len) { uint32_t t = prev_si; prev_si = nsi; nsi = t; break; }
-      nsi = next_si(f, prev_si, text, at);
+      nsi = T[(prev_si) + cls[text[at]]];
       at += 1;
       if (nsi > STATE_MAX) break;
-      prev_si = next_si(f, nsi, text, at);
+      prev_si = T[(nsi) + cls[text[at]]];
       at += 1;
       if (prev_si > STATE_MAX) { uint32_t t = prev_si; prev_si = nsi; nsi = t; break; }
-      nsi = next_si(f, prev_si, text, at);
+      nsi = T[(prev_si) + cls[text[at]]];
       at += 1;
     }
     if (nsi & STATE_MATCH) {
@@ -526,14 +534,24 @@ static DResult exec_at(Fsm *f, const uint8_t *text, size_t len, size_t *stop) {
       if (f->prog->nmatches > 1 && just_matches(f, nsi)) { *stop = at; return result; }
       size_t cur = at;
       while ((nsi & ~STATE_MATCH) == prev_si && at + 2 < len) {
-        nsi = next_si(f, nsi & ~STATE_MATCH, text, at);
+        nsi = T[(nsi & ~STATE_MATCH) + cls[text[at]]];
         at += 1;
       }
       if (at > cur) { result.kind = R_MATCH; result.v = at - 2; }
     } else if (nsi & STATE_START) {
-      /* unreachable: no literal prefixes (has_prefix() == false) */
+      /* dfa.rs:700-711: in the start state, skip to the next prefix occurrence */
       nsi &= ~STATE_START;
       prev_si = nsi;
+      if (f->pre) {
+        size_t s, e;
+        if (!orc_lits_find(f->pre, text + at, len - at, &s, &e)) {
+          *stop = len;
+          result.kind = R_NOMATCH;
+          result.v = len;
+          return result;
+        }
+        at += s;
+      }
     } else if (nsi >= STATE_UNKNOWN) {
       if (nsi == STATE_QUIT) { *stop = at; result.kind = R_QUIT; return result; }
       int byte = text[at - 1];
@@ -575,19 +593,22 @@ static DResult exec_at_reverse(Fsm *f, const uint8_t *text, size_t len, size_t *
   uint32_t prev_si = f->start, nsi = f->start;
   size_t at = f->at;
   const size_t at0 = f->at;
+  const uint8_t *cls = f->prog->byte_classes;
+  const uint32_t *T;
   while (at > 0) {
+    T = f->cache->trans;
     while (nsi <= STATE_MAX && at > 0) {
       at -= 1;
-      prev_si = next_si(f, nsi, text, at);
+      prev_si = T[(nsi) + cls[text[at]]];
       if (prev_si > STATE_MAX || at <= 4) { uint32_t t = prev_si; prev_si = nsi; nsi = t; break; }
       at -= 1;
-      nsi = next_si(f, prev_si, text, at);
+      nsi = T[(prev_si) + cls[text[at]]];
       if (nsi > STATE_MAX) break;
       at -= 1;
-      prev_si = next_si(f, nsi, text, at);
+      prev_si = T[(nsi) + cls[text[at]]];
       if (prev_si > STATE_MAX) { uint32_t t = prev_si; prev_si = nsi; nsi = t; break; }
       at -= 1;
-      nsi = next_si(f, prev_si, text, at);
+      nsi = T[(prev_si) + cls[text[at]]];
     }
     if (nsi & STATE_MATCH) {
       nsi &= ~STATE_MATCH;
@@ -598,7 +619,7 @@ static DResult exec_at_reverse(Fsm *f, const uint8_t *text, size_t len, size_t *
       size_t cur = at;
       while ((nsi & ~STATE_MATCH) == prev_si && at >= 2) {
         at -= 1;
-        nsi = next_si(f, nsi & ~STATE_MATCH, text, at);
+        nsi = T[(nsi & ~STATE_MATCH) + cls[text[at]]];
       }
       if (at < cur) { result.kind = R_MATCH; result.v = at + 2; }
     } else if (nsi >= STATE_UNKNOWN) {
@@ -642,13 +663,21 @@ static void fsm_init(Fsm *f, const orc_prog *p, orc_dfa_cache *c, int qam, size_
   f->last_match_si = STATE_UNKNOWN;
   f->last_cache_flush = at;
   f->cache = c;
+  f->pre = NULL;
 }
 
 /* Fsm::forward (dfa.rs:459-489).  Returns kind, *pos = value, *stop = scan end. */
 int orc_dfa_forward(const orc_prog *p, orc_dfa_cache *c, int quit_after_match, const uint8_t *text, size_t len,
                     size_t at, size_t *pos, size_t *stop) {
+  return orc_dfa_forward_pfx(p, c, quit_after_match, NULL, text, len, at, pos, stop);
+}
+
+int orc_dfa_forward_pfx(const orc_prog *p, orc_dfa_cache *c, int quit_after_match, const orc_lits *pre,
+                        const uint8_t *text, size_t len, size_t at, size_t *pos, size_t *stop) {
   Fsm f;
   fsm_init(&f, p, c, quit_after_match, at);
+  /* has_prefix (dfa.rs:1562-1566) */
+  if (pre && pre->matcher != 0 && pre->n > 0 && !p->is_reverse && !p->anchored_start) f.pre = pre;
   EmptyFlags ef;
   uint8_t sf;
   start_flags(text, len, at, &ef, &sf);

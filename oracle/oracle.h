@@ -105,6 +105,11 @@ void orc_cache_reset_stats(orc_cache *c);
  * contiguous split), haystack i = [offs[i], offs[i+1]) or fixed stride. */
 int orc_find_batch(const orc_regex *r, const uint8_t *buf, const uint64_t *offs, size_t stride, size_t length,
                    size_t n, int nthreads, uint64_t *out_pairs, orc_stats *stats);
+/* orc_set_batch with the engine statistics summed over the threads: DFA
+ * quits (lines answered by the Pike VM after the cache thrashed, dfa.rs:
+ * 1282-1293), cache flushes, and the threads' final cached-state counts. */
+int orc_set_batch_stats(const orc_regex *r, const uint8_t *buf, const uint64_t *offs, size_t stride, size_t length,
+                        size_t n, int nthreads, uint64_t *masks, orc_stats *stats);
 int orc_is_match_batch(const orc_regex *r, const uint8_t *buf, const uint64_t *offs, size_t stride,
                        size_t length, size_t n, int nthreads, uint8_t *out);
 /* shortest_match (exec.rs:382-420) per haystack: the end, UINT64_MAX for none. */

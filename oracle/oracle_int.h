@@ -80,6 +80,15 @@ typedef struct {
   int any_empty, any_short, any_long;
 } orc_lits;
 
+/* LiteralSearcher::find (src/literals.rs:92-103) over hay[0..n) (exec.c). */
+int orc_lits_find(const orc_lits *l, const uint8_t *hay, size_t n, size_t *s, size_t *e);
+/* Fsm::forward with the program's prefix literals (dfa.prefixes, exec.rs:
+ * 308-311): in a start state the scan jumps to the next prefix occurrence
+ * (dfa.rs:700-711 prefix_at, has_prefix dfa.rs:1562-1566).  pre NULL: none
+ * (orc_dfa_forward). */
+int orc_dfa_forward_pfx(const orc_prog *p, orc_dfa_cache *c, int quit_after_match, const orc_lits *pre,
+                        const uint8_t *text, size_t len, size_t at, size_t *pos, size_t *stop);
+
 struct orc_regex {
   orc_prog *nfa, *fwd, *rev;
   int mt;               /* MatchType code (orc_regex_set_exec), -1: not set (Dfa dispatch) */

@@ -243,7 +243,8 @@ hipError_t launch_captures(const BatchDev &b, const NfaDev &n, const uint64_t *f
 hipError_t exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, hipStream_t st);
 hipError_t launch_replace_plan(const BatchDev &b, const uint64_t *counts, const uint64_t *moff, const uint64_t *m,
                                uint64_t limit, uint64_t rep_len, int64_t *shift, uint64_t *out_len, hipStream_t st,
-                               int cus);
+                               int cus,
+                               uint64_t nm);
 hipError_t launch_replace_copy(const BatchDev &b, const uint64_t *ooff, const uint64_t *counts, const uint64_t *moff,
                                const uint64_t *m, const int64_t *shift, uint64_t limit, const uint8_t *rep,
                                uint64_t rep_len, uint8_t *out, uint64_t cap, uint64_t total_hint, hipStream_t st,

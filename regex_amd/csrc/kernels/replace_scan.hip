@@ -19,6 +19,7 @@
 // SplitN rule for a limit (its last field is the remainder of the text).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <rocprim/rocprim.hpp>
 #include <stdint.h>
@@ -49,7 +50,50 @@ __device__ __forceinline__ uint64_t upper_idx(const uint64_t *a, uint64_t lo, ui
   return lo;
 }
 
+// The layout of replacen as a segmented scan over all matches of the batch
+// (one thread per match, so a haystack with 35 M matches is as parallel as
+// 35 M haystacks): val[g] = len(match g) - rep_len when g is among its
+// haystack's first `limit` matches, else 0; S = exclusive scan of val over
+// nm + 1 entries; shift[g] = S[g] - S[moff[h]] (bytes removed before match g
+// minus its replacements so far, within haystack h) and out_len[h] = len_h -
+// (S[moff[h] + k_h] - S[moff[h]]).
+__global__ __launch_bounds__(256) void replace_vals_kernel(uint64_t n, const uint64_t *counts, const uint64_t *moff,
+                                                           const uint64_t *m, uint64_t limit, uint64_t rep_len,
+                                                           int64_t *val) {
+  const uint64_t nm = moff[n];
+  for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g <= nm; g += (uint64_t)gridDim.x * blockDim.x) {
+    int64_t v = 0;
+    if (g < nm) {
+      const uint64_t h = upper_idx(moff, 0, n + 1, g) - 1;
+      const uint64_t k = counts[h] < limit ? counts[h] : limit;
+      if (g - moff[h] < k) v = (int64_t)(m[2 * g + 1] - m[2 * g]) - (int64_t)rep_len;
+    }
+    val[g] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void replace_shift_kernel(BatchDev bt, const uint64_t *counts, const uint64_t *moff,
+                                                            uint64_t limit, const int64_t *S, int64_t *shift,
+                                                            uint64_t *out_len) {
+  const uint64_t n = bt.count, nm = moff[n];
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < nm + n; g += stride) {
+    if (g < nm) {
+      const uint64_t h = upper_idx(moff, 0, n + 1, g) - 1;
+      shift[g] = S[g] - S[moff[h]];
+    } else {
+      const uint64_t h = g - nm;
+      uint64_t base, len;
+      hay_of(bt, h, &base, &len);
+      const uint64_t k = counts[h] < limit ? counts[h] : limit;
+      out_len[h] = (uint64_t)((int64_t)len - (S[moff[h] + k] - S[moff[h]]));
+    }
+  }
+}
+
 // One wave per haystack: shift_j for its first k matches and the output length.
+// (Replaced by replace_vals / replace_shift: a haystack's matches were one
+// wave's sequential loop, 0.4 s for the regex-dna strip's 35 M matches.)
 __global__ __launch_bounds__(256) void replace_plan_kernel(BatchDev bt, const uint64_t *counts, const uint64_t *moff,
                                                            const uint64_t *m, uint64_t limit, uint64_t rep_len,
                                                            int64_t *shift, uint64_t *out_len) {
@@ -230,10 +274,37 @@ hipError_t exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, hip
 
 hipError_t launch_replace_plan(const BatchDev &b, const uint64_t *counts, const uint64_t *moff, const uint64_t *m,
                                uint64_t limit, uint64_t rep_len, int64_t *shift, uint64_t *out_len, hipStream_t st,
-                               int cus) {
-  hipLaunchKernelGGL(replace_plan_kernel, dim3(grid_for_items(b.count, 4, cus)), dim3(256), 0, st, b, counts, moff, m,
-                     limit, rep_len, shift, out_len);
-  return hipGetLastError();
+                               int cus, uint64_t nm) {
+  if (getenv("RURE_AMD_REPLACE_WAVE")) {  // the previous wave-per-haystack plan (A/B)
+    hipLaunchKernelGGL(replace_plan_kernel, dim3(grid_for_items(b.count, 4, cus)), dim3(256), 0, st, b, counts, moff,
+                       m, limit, rep_len, shift, out_len);
+    return hipGetLastError();
+  }
+  int64_t *val = nullptr, *S = nullptr;
+  hipError_t e = scratch_malloc((void **)&val, (nm + 1) * 8, st);
+  if (e == hipSuccess) e = scratch_malloc((void **)&S, (nm + 1) * 8, st);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(replace_vals_kernel, dim3(grid_for_items(nm + 1, 256, cus)), dim3(256), 0, st, b.count, counts,
+                       moff, m, limit, rep_len, val);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) {
+    size_t tmp = 0;
+    e = rocprim::exclusive_scan(nullptr, tmp, val, S, (int64_t)0, (size_t)(nm + 1), rocprim::plus<int64_t>(), st);
+    void *buf = nullptr;
+    if (e == hipSuccess) e = scratch_malloc(&buf, tmp, st);
+    if (e == hipSuccess)
+      e = rocprim::exclusive_scan(buf, tmp, val, S, (int64_t)0, (size_t)(nm + 1), rocprim::plus<int64_t>(), st);
+    if (buf) { hipError_t e2 = scratch_free(buf, st); if (e == hipSuccess) e = e2; }
+  }
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(replace_shift_kernel, dim3(grid_for_items(nm + b.count, 256, cus)), dim3(256), 0, st, b, counts,
+                       moff, limit, S, shift, out_len);
+    e = hipGetLastError();
+  }
+  if (val) { hipError_t e2 = scratch_free(val, st); if (e == hipSuccess) e = e2; }
+  if (S) { hipError_t e2 = scratch_free(S, st); if (e == hipSuccess) e = e2; }
+  return e;
 }
 
 hipError_t launch_replace_copy(const BatchDev &b, const uint64_t *ooff, const uint64_t *counts, const uint64_t *moff,

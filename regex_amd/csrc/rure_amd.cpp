@@ -445,7 +445,7 @@ struct Blob {
 // Cached blocks go back to the driver on rure_amd_release_scratch(), when the
 // last rure / rure_set is freed, and before a retry when an allocation fails.
 // (The stream-ordered pool of hipMallocAsync kept freed memory mapped even
-// after hipMemPoolTrimTo on this ROCm: tools/scratch_diag.py.)
+// after hipMemPoolTrimTo on this ROCm, measured in round 3.)
 constexpr size_t kScratchMinCap = 256ull << 20, kScratchMaxCap = 8ull << 30;
 struct ScratchBlock {
   size_t n;
@@ -2962,7 +2962,7 @@ int rure_amd_replace_batch(rure *re, const rure_amd_batch *batch, const uint8_t 
   if (e == hipSuccess && rep_len) e = hipMemcpyAsync(drep, rep, rep_len, hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = hipMemsetAsync(olen + b.count, 0, 8, st);
   if (e == hipSuccess)
-    e = launch_replace_plan(b, ib.counts, ib.moff, ib.m, lim, rep_len, shift, olen, st, t->cus);
+    e = launch_replace_plan(b, ib.counts, ib.moff, ib.m, lim, rep_len, shift, olen, st, t->cus, ib.nm);
   if (e == hipSuccess) e = exclusive_scan_u64(olen, out_offsets, b.count + 1, st);
   if (e == hipSuccess) e = hipMemcpyAsync(total, out_offsets + b.count, 8, hipMemcpyDeviceToDevice, st);
   if (e == hipSuccess && out_capacity) {

@@ -34,7 +34,8 @@ SUBSTS = [(b"B", b"(c|g|t)"), (b"D", b"(a|g|t)"), (b"H", b"(a|c|t)"), (b"K", b"(
 
 
 class RegexDna(object):
-    """Compiled once; run() many times (the bench's pipeline field)."""
+    """Compiled once; run() many times (bench.py times run() as the C3 line's
+    pipeline_ms field, with its known-answer check)."""
 
     def __init__(self):
         self.strip = Regex(STRIP)

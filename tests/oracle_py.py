@@ -56,6 +56,7 @@ orc_find_batch = _sig("orc_find_batch", ctypes.c_int, VP, VP, VP, SZ, SZ, SZ, ct
 orc_is_match_batch = _sig("orc_is_match_batch", ctypes.c_int, VP, VP, VP, SZ, SZ, SZ, ctypes.c_int, VP)
 orc_shortest_batch = _sig("orc_shortest_batch", ctypes.c_int, VP, VP, VP, SZ, SZ, SZ, ctypes.c_int, VP)
 orc_set_batch = _sig("orc_set_batch", ctypes.c_int, VP, VP, VP, SZ, SZ, SZ, ctypes.c_int, VP)
+orc_set_batch_stats = _sig("orc_set_batch_stats", ctypes.c_int, VP, VP, VP, SZ, SZ, SZ, ctypes.c_int, VP, VP)
 
 NONE = (1 << 64) - 1
 
@@ -204,8 +205,11 @@ class OracleRegex(object):
                            stride, length, n, nthreads, out.ctypes.data)
         return out
 
-    def set_batch(self, buf, stride, length, n, nthreads=1, offsets=None):
+    def set_batch(self, buf, stride, length, n, nthreads=1, offsets=None, stats=False):
         out = np.zeros(n, dtype=np.uint64)
-        orc_set_batch(self._r, buf.ctypes.data, offsets.ctypes.data if offsets is not None else None,
-                      stride, length, n, nthreads, out.ctypes.data)
+        st = Stats()
+        orc_set_batch_stats(self._r, buf.ctypes.data, offsets.ctypes.data if offsets is not None else None,
+                            stride, length, n, nthreads, out.ctypes.data, ctypes.byref(st))
+        if stats:
+            return out, {k: getattr(st, k) for k, _ in Stats._fields_}
         return out

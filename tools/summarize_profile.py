@@ -25,7 +25,16 @@ def main(tag, kernel_substr="rure_amd::"):
     fetch = [float(r["Counter_Value"]) for r in pmc
              if ks and r["Kernel_Name"] == ks[0]["Name"] and r["Counter_Name"] == "FETCH_SIZE"]
     bench = json.loads(open(os.path.join(src, "bench_trace.json")).read().strip().splitlines()[-1])
+    # the bench line's roofline entry for the dominant kernel (the C3 line
+    # carries one per phase: roofline = the variant kernel, roofline_strip =
+    # the lexer, which reads the raw text, not the stripped stream)
     roof = bench.get("roofline", {})
+    if ks:
+        kid = re.sub(r"_kernel.*$", "", short(ks[0]["Name"]).split("::")[-1])
+        for k, v in bench.items():
+            if k.startswith("roofline") and isinstance(v, dict) and kid in str(v.get("kernel", "")):
+                roof = v
+                break
     alg = roof.get("alg_bytes_per_launch")
     import datetime
     out = {
