@@ -6,7 +6,8 @@ LIB = regex_amd/lib/librure_amd.so
 HOST_SRC = regex_amd/csrc/host/syntax.cpp regex_amd/csrc/host/compile.cpp regex_amd/csrc/host/dfa_build.cpp \
            regex_amd/csrc/host/nfa_build.cpp regex_amd/csrc/host/literals.cpp \
            regex_amd/csrc/host/literal_sets.cpp
-RT_SRC = regex_amd/csrc/rure_amd.cpp
+RT_SRC = regex_amd/csrc/build.cpp regex_amd/csrc/dispatch.cpp regex_amd/csrc/scratch.cpp regex_amd/csrc/capi.cpp
+RT_OBJ = $(patsubst regex_amd/csrc/%.cpp,$(OBJDIR)/rt_%.o,$(RT_SRC))
 KERNEL_SRC = regex_amd/csrc/kernels/dfa_scan.hip regex_amd/csrc/kernels/nfa_scan.hip regex_amd/csrc/kernels/iter_scan.hip \
              regex_amd/csrc/kernels/replace_scan.hip regex_amd/csrc/kernels/gather_scan.hip \
              regex_amd/csrc/kernels/match_types.hip regex_amd/csrc/kernels/big_dfa.hip regex_amd/csrc/kernels/set_multi.hip
@@ -24,7 +25,7 @@ $(OBJDIR)/%.o: regex_amd/csrc/host/%.cpp $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(CXXFLAGS) -c $< -o $@
 
-$(OBJDIR)/rure_amd.o: $(RT_SRC) $(HDRS)
+$(OBJDIR)/rt_%.o: regex_amd/csrc/%.cpp $(HDRS) regex_amd/csrc/runtime.hpp
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(CXXFLAGS) -c $< -o $@
 
@@ -32,7 +33,7 @@ $(OBJDIR)/%.o: regex_amd/csrc/kernels/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(CXXFLAGS) --offload-arch=$(ARCH) -c $< -o $@
 
-$(LIB): $(HOST_OBJ) $(OBJDIR)/rure_amd.o $(KERNEL_OBJ)
+$(LIB): $(HOST_OBJ) $(RT_OBJ) $(KERNEL_OBJ)
 	@mkdir -p regex_amd/lib
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^
 

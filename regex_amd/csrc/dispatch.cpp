@@ -1,0 +1,832 @@
+// The reference's engine dispatch over batches (src/exec.rs:382-420, 473-514,
+// 998-1038, re_trait.rs:197-221): which kernel answers which search, the DFA
+// -> quit -> Pike VM fallback, sets in 64-pattern groups, the find_iter
+// passes and the k-mer table cache.
+#include "runtime.hpp"
+
+namespace rt {
+
+int device_cus(int dev) {
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return 256;
+  return prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+}
+
+int grid_for(size_t count, uint32_t lds_bytes, int cus) {
+  size_t blocks = (count + 255) / 256;
+  uint32_t per_cu = 8;
+  if (lds_bytes > 0) per_cu = std::max<uint32_t>(1, std::min<uint32_t>(8, (160u * 1024u) / lds_bytes));
+  size_t cap = (size_t)cus * per_cu;
+  if (blocks > cap) blocks = cap;
+  if (blocks == 0) blocks = 1;
+  return (int)blocks;
+}
+
+
+int pike_grid(size_t count, bool fallback, const NfaDev &n, int cus) {
+  size_t units = fallback ? (count + 63) / 64 : count;
+  size_t wb = nfa_wave_bytes(n.nleaves);
+  size_t per_cu = wb <= kNfaLdsMax ? std::max<size_t>(1, std::min<size_t>(32, (160u * 1024u) / wb)) : 4;
+  size_t g = std::min(units, (size_t)cus * per_cu);
+  return (int)std::max<size_t>(g, 1);
+}
+
+// Pike VM pass: all haystacks (no DFA) or only those the DFA quit on.
+hipError_t run_pike(int mode, bool fallback, const BatchDev &b, const DevTables &t, void *out, hipStream_t st) {
+  int grid = pike_grid(b.count, fallback, t.n, t.cus);
+  size_t wb = nfa_wave_bytes(t.n.nleaves);
+  if (wb <= kNfaLdsMax) return launch_pike(mode, fallback, b, t.n, out, nullptr, st, grid);
+  void *scratch = nullptr;
+  hipError_t e = scratch_malloc(&scratch, wb * (size_t)grid, st);
+  if (e != hipSuccess) return e;
+  e = launch_pike(mode, fallback, b, t.n, out, scratch, st, grid);
+  hipError_t e2 = scratch_free(scratch, st);
+  return e != hipSuccess ? e : e2;
+}
+
+
+// The engine dispatch of exec.rs:473-514 / 382-420 for a batch: DFA, and the
+// Pike VM where the DFA quits (or instead of it when it does not fit).
+// Chunk sizes are an odd number of 128-byte lines: lanes that scan chunks in
+// lockstep then read addresses with different low bits, instead of hammering
+// the few HBM channels a power-of-two chunk would map them all to.
+uint64_t odd_lines(uint64_t bytes) {
+  uint64_t lines = (bytes + 127) / 128;
+  if ((lines & 1) == 0) ++lines;
+  return lines * 128;
+}
+
+// Few long haystacks: one lane per haystack would leave the chip idle, so the
+// search is split into chunks (launch_long_scan).  Needs a DFA that cannot
+// quit (the Pike VM fallback is per haystack).
+bool long_batch(int mode, const BatchDev &b, const DevTables &t, uint64_t *chunk) {
+  if (b.offs || !t.has_dfa || t.quit_possible || b.count == 0) return false;
+  const uint64_t span = b.length > b.start ? b.length - b.start : 0;
+  if (span < (256u << 10) || b.count >= (uint64_t)t.cus * 128) {
+    // Small batches of medium haystacks (C1: 1024 x 1 KiB): one lane per
+    // haystack runs count / 256 workgroups on a 256-CU chip, each lane a
+    // dependent chain over its whole haystack; units of >= 128 B spread the
+    // searches over about one wave per CU.  End-anchored regexes keep the
+    // reverse scan (it reads O(match) bytes); single calls and batches of
+    // fewer than 64 haystacks keep one lane each.  RURE_AMD_SPLIT=0 turns it off.
+    // Only is_match: a unit stops at its first match there, while a find /
+    // shortest_match unit scans on until the DFA dies, so a pattern that never
+    // dies ([^\n]* over text without newlines) would cost every unit the rest
+    // of its haystack (about units / 2 times the unsplit work).
+    const char *sv = getenv("RURE_AMD_SPLIT");
+    if ((sv && sv[0] == '0') || mode != MODE_ISMATCH || t.anchored_rev || span < 512 || b.count < 64 ||
+        b.count > (uint64_t)t.cus * 16)
+      return false;
+    const uint64_t per_h = ((uint64_t)t.cus * 64 + b.count - 1) / b.count;
+    const uint64_t c = odd_lines(std::max<uint64_t>(128, (span + per_h - 1) / per_h));
+    if (c >= span) return false;
+    *chunk = c;
+    return true;
+  }
+  // 16 waves per CU: per-lane streams need latency hiding (RURE_AMD_LONG_LANES
+  // per CU overrides, tuning)
+  uint64_t per_cu = 1024;
+  if (const char *v = getenv("RURE_AMD_LONG_LANES")) per_cu = std::max(64, atoi(v));
+  const uint64_t target = (uint64_t)t.cus * per_cu;
+  const uint64_t per_h = (target + b.count - 1) / b.count;
+  uint64_t c = std::max<uint64_t>(16u << 10, (span + per_h - 1) / per_h);
+  *chunk = odd_lines(c);
+  return true;
+}
+
+// The DFA step of find / is_match / shortest_match (the quit marker where the
+// DFA quit): the forward DFA (+ reverse for find), or for DfaAnchoredReverse
+// regexes the reverse DFA from the end of each haystack.  Long haystacks
+// searched from their start take the chunked forward scan for either (the
+// two answer alike at start 0: only the look-behind at `start` differs).
+hipError_t run_dfa_step(int mode, const BatchDev &b, const DevTables &t, void *out, hipStream_t st, int dfa_grid,
+                        const FwdDfaDev *iter) {
+  uint64_t chunk = 0;
+  const bool long_fwd = iter && long_batch(mode, b, t, &chunk);
+  if (t.anchored_rev && !(long_fwd && b.start == 0)) return launch_dfa_anchored_rev(mode, b, t.r, out, st, dfa_grid);
+  if (long_fwd) return launch_long_scan(mode, b, *iter, t.r, chunk, out, st, t.cus);
+  return launch_dfa_fwd(mode, b, t.f, t.r, out, st, dfa_grid);
+}
+
+// The Literal / DfaSuffix match types (DevTables::mt_lane): literal searches
+// need no DFA; DfaSuffix steps the DFA tables (without them the reference's
+// DFA would have quit too: the Pike VM answers).
+bool lane_search_ok(const DevTables &t) { return t.mt_lane && (t.m.mt != MT_DFA_SUFFIX || t.has_dfa); }
+
+hipError_t run_lane_search(int mode, const BatchDev &b, const DevTables &t, void *out, hipStream_t st) {
+  if (!t.quit_possible || t.m.mt != MT_DFA_SUFFIX) return launch_lane_search(mode, b, t.m, t.f, t.r, out, st, t.cus);
+  BatchDev bq = b;  // quit flag: see run_regex
+  hipError_t e = scratch_malloc((void **)&bq.quit_flag, 4, st);
+  if (e == hipSuccess) e = hipMemsetAsync(bq.quit_flag, 0, 4, st);
+  if (e == hipSuccess) e = launch_lane_search(mode, bq, t.m, t.f, t.r, out, st, t.cus);
+  if (e == hipSuccess) e = run_pike(mode, true, bq, t, out, st);
+  if (bq.quit_flag) {
+    hipError_t e2 = scratch_free(bq.quit_flag, st);
+    if (e == hipSuccess) e = e2;
+  }
+  return e;
+}
+
+// The big-DFA kernel runs one lane per haystack: for batches that fill the
+// device (a handful of long haystacks stay on the Pike VM, which spreads one
+// haystack over a wave).  RURE_AMD_BIG=2 forces it (tests), =0 keeps the
+// Pike VM (A/B; read per call).
+bool big_batch(const BatchDev &b, const DevTables &t) {
+  const char *env = getenv("RURE_AMD_BIG");
+  if (env && env[0] == '2') return true;
+  if (env && env[0] == '0') return false;
+  return b.count >= (uint64_t)t.cus * 64;
+}
+
+hipError_t run_regex(int mode, const BatchDev &b, const DevTables &t, void *out, hipStream_t st, int dfa_grid,
+                     const FwdDfaDev *iter) {
+  if (lane_search_ok(t)) return run_lane_search(mode, b, t, out, st);
+  if (!t.has_dfa && big_batch(b, t) && big_device(t)) return launch_big_dfa(mode, b, t.bf, t.br, out, st, t.cus);
+  if (!t.has_dfa) return run_pike(mode, false, b, t, out, st);
+  uint64_t chunk = 0;
+  if (iter && long_batch(mode, b, t, &chunk) && !(t.anchored_rev && b.start != 0))
+    return launch_long_scan(mode, b, *iter, t.r, chunk, out, st, t.cus);
+  if (!t.quit_possible) return run_dfa_step(mode, b, t, out, st, dfa_grid, nullptr);
+  // the DFA kernels flag a quit; the Pike VM fallback returns at once without
+  BatchDev bq = b;
+  hipError_t e = scratch_malloc((void **)&bq.quit_flag, 4, st);
+  if (e == hipSuccess) e = hipMemsetAsync(bq.quit_flag, 0, 4, st);
+  if (e == hipSuccess) e = run_dfa_step(mode, bq, t, out, st, dfa_grid, nullptr);
+  if (e == hipSuccess) e = run_pike(mode, true, bq, t, out, st);
+  if (bq.quit_flag) {
+    hipError_t e2 = scratch_free(bq.quit_flag, st);
+    if (e == hipSuccess) e = e2;
+  }
+  return e;
+}
+
+
+// exec.rs:998-1038 many_matches_at for a batch.
+hipError_t run_set(const BatchDev &b, const DevTables &t, uint64_t *out, hipStream_t st, int dfa_grid) {
+  if (!t.has_dfa) return run_pike(MODE_SET, false, b, t, out, st);
+  if (!t.quit_possible)
+    return t.use_cores ? launch_set_cores(b, t.c, out, st, t.cus) : launch_dfa_set(b, t.s, out, st, dfa_grid);
+  BatchDev bq = b;  // quit flag: see run_regex
+  hipError_t e = scratch_malloc((void **)&bq.quit_flag, 4, st);
+  if (e == hipSuccess) e = hipMemsetAsync(bq.quit_flag, 0, 4, st);
+  if (e == hipSuccess)
+    e = t.use_cores ? launch_set_cores(bq, t.c, out, st, t.cus) : launch_dfa_set(bq, t.s, out, st, dfa_grid);
+  if (e == hipSuccess) e = run_pike(MODE_SET, true, bq, t, out, st);
+  if (bq.quit_flag) {
+    hipError_t e2 = scratch_free(bq.quit_flag, st);
+    if (e == hipSuccess) e = e2;
+  }
+  return e;
+}
+
+// exec.rs:524-596 read_captures_at for a batch.  One group (two slots): the
+// plain find.  Otherwise the DFA's (start, end) per haystack (the quit marker
+// kept, not resolved), then the Pike VM with slots: from the match start over
+// the text up to two characters past the match end, or over the whole
+// haystack where the DFA quit and for anchored-start programs.  A regex whose
+// DFA does not materialise takes its bounds from the Pike VM (the reference's
+// lazy DFA would have produced them).
+hipError_t run_captures(const BatchDev &b, const DevTables &t, uint64_t *slots, uint32_t ns, hipStream_t st,
+                        int dfa_grid) {
+  if (ns <= 2) return run_regex(MODE_FIND, b, t, slots, st, dfa_grid);
+  hipError_t e = hipSuccess;
+  uint64_t *found = nullptr;
+  if (!t.n.anchored) {
+    if ((e = scratch_malloc((void **)&found, b.count * 16, st)) != hipSuccess) return e;
+    e = lane_search_ok(t) ? launch_lane_search(MODE_FIND, b, t.m, t.f, t.r, found, st, t.cus)
+        : t.has_dfa       ? run_dfa_step(MODE_FIND, b, t, found, st, dfa_grid, nullptr)
+                          : run_pike(MODE_FIND, false, b, t, found, st);
+  }
+  const size_t wb = caps_wave_bytes(t.n.nleaves, ns);
+  const bool in_lds = wb <= kNfaLdsMax;
+  const size_t per_cu = in_lds ? std::max<size_t>(1, std::min<size_t>(32, (160u * 1024u) / wb)) : 4;
+  size_t g = std::min<size_t>(b.count, (size_t)t.cus * per_cu);
+  if (!in_lds) g = std::min<size_t>(g, (256u << 20) / wb);  // bound the scratch (wide programs: MiBs per wave)
+  const int grid = (int)std::max<size_t>(1, g);
+  void *scratch = nullptr;
+  if (e == hipSuccess && !in_lds) e = scratch_malloc(&scratch, wb * (size_t)grid, st);
+  if (e == hipSuccess) e = launch_captures(b, t.n, found, slots, ns, scratch, st, grid);
+  if (scratch) { hipError_t e2 = scratch_free(scratch, st); if (e == hipSuccess) e = e2; }
+  if (found) { hipError_t e2 = scratch_free(found, st); if (e == hipSuccess) e = e2; }
+  return e;
+}
+
+bool to_batch(const rure_amd_batch *b, BatchDev *o) {
+  if (!b || (!b->haystack && b->count > 0)) return false;
+  o->hay = b->haystack;
+  o->offs = b->offsets;
+  o->stride = b->stride;
+  o->length = b->length;
+  o->count = b->count;
+  o->start = b->start;
+  o->quit_flag = nullptr;
+  return true;
+}
+
+
+// Runs one regex over one host haystack on the GPU (single-call entry points).
+// mode: MODE_FIND / MODE_ISMATCH / MODE_SHORTEST.  Returns false if no match.
+bool single_call(rure *re, int mode, const uint8_t *hay, size_t len, size_t start, uint64_t *r0, uint64_t *r1) {
+  std::string err;
+  DevTables *t = regex_device(re, &err);
+  if (!t) die(err);
+  uint64_t chunk;
+  BatchDev probe{nullptr, nullptr, len, len, 1, start};
+  const FwdDfaDev *iter = long_batch(mode, probe, *t, &chunk) ? iter_device(re, *t, &err) : nullptr;  // locks re->mu
+  std::lock_guard<std::mutex> g(re->mu);
+  int d = 0;
+  if (!hip_ok(hipGetDevice(&d), &err)) die(err);
+  if (!re->stage.ensure(d, len, &err)) die(err);
+  hipStream_t st = re->stage.stream;
+  if (len && !hip_ok(hipMemcpyAsync(re->stage.hay, hay, len, hipMemcpyHostToDevice, st), &err)) die(err);
+  BatchDev b{re->stage.hay, nullptr, len, len, 1, start};
+  if (!hip_ok(run_regex(mode, b, *t, re->stage.res, st, 1, iter), &err)) die(err);
+  uint64_t out[2] = {~0ull, ~0ull};
+  size_t nbytes = mode == MODE_FIND ? 16 : mode == MODE_SHORTEST ? 8 : 1;
+  if (!hip_ok(hipMemcpyAsync(out, re->stage.res, nbytes, hipMemcpyDeviceToHost, st), &err)) die(err);
+  if (!hip_ok(hipStreamSynchronize(st), &err)) die(err);
+  if (mode == MODE_ISMATCH) {
+    uint8_t v = (uint8_t)(out[0] & 0xFF);
+    if (v > 1) die("internal error: unresolved DFA quit");
+    return v == 1;
+  }
+  if (out[0] == kQuit || (mode == MODE_FIND && out[1] == kQuit)) die("internal error: unresolved DFA quit");
+  if (out[0] == ~0ull) return false;
+  *r0 = out[0];
+  if (r1) *r1 = out[1];
+  return true;
+}
+
+uint64_t set_single_call(rure_set *rs, const uint8_t *hay, size_t len, size_t start) {
+  std::string err;
+  DevTables *t = set_device(rs, &err);
+  if (!t) die(err);
+  std::lock_guard<std::mutex> g(rs->mu);
+  int d = 0;
+  if (!hip_ok(hipGetDevice(&d), &err)) die(err);
+  if (!rs->stage.ensure(d, len, &err)) die(err);
+  hipStream_t st = rs->stage.stream;
+  if (len && !hip_ok(hipMemcpyAsync(rs->stage.hay, hay, len, hipMemcpyHostToDevice, st), &err)) die(err);
+  BatchDev b{rs->stage.hay, nullptr, 0, len, 1, start};
+  if (!hip_ok(run_set(b, *t, rs->stage.res, st, 1), &err)) die(err);
+  uint64_t out = 0;
+  if (!hip_ok(hipMemcpyAsync(&out, rs->stage.res, 8, hipMemcpyDeviceToHost, st), &err)) die(err);
+  if (!hip_ok(hipStreamSynchronize(st), &err)) die(err);
+  if (out == kQuit) die("internal error: unresolved DFA quit");
+  return out;
+}
+
+
+// ------------------------------------------------------------------ batches
+// MatchType::Literal (exec.rs:1148-1166 -> find_literals, exec.rs:601-625):
+// a regex that is a finite string set can answer find / is_match from its
+// literals instead of the DFA.  On the GPU that wins for a few literals
+// (tools/lit_find_bench.py, find over 262144 x 2000 B of sherlock text,
+// literal engine vs DFA: 1 word 0.19 vs 0.22 ms, 3 words 0.19 vs 0.32,
+// 4 words 0.24 vs 0.30, 8 words 0.24 vs 0.29, 2 rare words 0.29 vs 0.29;
+// 16 words 0.30 vs 0.25 and 64 words 0.76 vs 0.63 favour the DFA, whose
+// lookups stay one LDS read per byte while candidate verification grows with
+// the literal count), so by default it runs for at most kLitFindMax
+// literals, on batches of many haystacks (few long ones keep the chunked DFA
+// scan).  RURE_AMD_LIT=1 / 0 forces it on / off.
+static constexpr size_t kLitFindMax = 8;
+const FwdDfaDev *literal_engine(int mode, rure *re, DevTables &t, const BatchDev &b) {
+  uint64_t chunk;
+  const char *env = getenv("RURE_AMD_LIT");
+  if (env && env[0] != '1') return nullptr;
+  if (t.mt_lane) return nullptr;  // the reference's literal searcher differs from the regex's strings
+  if (!env && long_batch(mode, b, t, &chunk)) return nullptr;  // RURE_AMD_LIT=1 forces the literal engine
+  {
+    // the literal set alone (cheap) before any find_iter DFA is built
+    std::lock_guard<std::mutex> g(re->mu);
+    if (!re->iter_built && !re->lits_done) re->lit_ok = extract_literals(re->nfa, kLitMax, kLitLen, &re->lits);
+    re->lits_done = true;
+    if (!re->lit_ok || (!env && re->lits.lits.size() > kLitFindMax)) return nullptr;
+  }
+  std::string err;
+  const FwdDfaDev *fi = iter_device(re, t, &err);
+  return fi && fi->lit_n ? fi : nullptr;
+}
+
+
+// One set of at most 64 patterns (>= 2) into one mask word per haystack.
+int set_batch_word(rure_set *rs, const BatchDev &b, uint64_t *mask, hipStream_t stream) {
+  std::string err;
+  DevTables *t = set_device(rs, &err);
+  if (!t) return err.rfind("HIP", 0) == 0 ? RURE_AMD_ERR_HIP : RURE_AMD_ERR_DFA;
+  if (t->use_cores && !t->cores_adapted && !adapt_cores(rs, t, b, stream, &err)) return RURE_AMD_ERR_HIP;
+  int grid = grid_for(b.count, t->s.lds_bytes, t->cus);
+  if (run_set(b, *t, mask, stream, grid) != hipSuccess) return RURE_AMD_ERR_HIP;
+  return RURE_AMD_OK;
+}
+
+// Group g (patterns [64 g, 64 g + len)) into word g of mask (words per haystack).
+// ------------------------------------------------- sets as one pass (groups)
+// A set of more than 64 patterns is searched as its 64-pattern groups
+// (rure_set::groups), one pass over the batch per group.  With
+// RURE_AMD_SET_MULTI=1, build_multi puts every group's core-form automaton
+// in one LDS image and set_multi.hip steps all of them over each haystack
+// read once; RURE_AMD_SET_CHAINS=G (2..4) splits a set of at most 64
+// patterns into G groups the same way.  Measured (tools/bigset_bench.py,
+// DESIGN.md §4.3): the chains share the VALU and LDS issue slots the single
+// chain already saturates, and the split LDS holds fewer hot cores, so one
+// pass is slower (C4 as 2 chains 1.50 vs 0.64 ms; 100 patterns 4.95 vs
+// 1.39 ms per-group) though it reads the text once; per-group passes stay
+// the default.
+
+
+int set_chains() {
+  const char *v = getenv("RURE_AMD_SET_CHAINS");
+  return v ? std::max(1, std::min(kMultiMaxGroups, atoi(v))) : 1;
+}
+
+int device_cus_cached() {
+  int d = 0;
+  (void)hipGetDevice(&d);
+  static std::mutex mu;
+  static std::map<int, int> cache;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cache.find(d);
+  if (it != cache.end()) return it->second;
+  return cache[d] = device_cus(d);
+}
+
+void free_multi(rure_set *rs) {
+  MultiSet *m = rs->multi;
+  if (!m) return;
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  for (auto &kv : m->dev) {
+    (void)hipSetDevice(kv.first);
+    (void)hipFree(kv.second.first);
+  }
+  (void)hipSetDevice(cur);
+  for (rure_set *x : m->owned) rure_set_free(x);
+  delete m;
+  rs->multi = nullptr;
+}
+
+bool multi_fail(int why) {  // diagnostic (RURE_AMD_MULTI_DEBUG): which rule declined one pass
+  if (getenv("RURE_AMD_MULTI_DEBUG")) fprintf(stderr, "set_multi: not built (%d)\n", why);
+  return false;
+}
+
+bool build_multi_locked(rure_set *rs, MultiSet *m, std::string *err, const std::vector<std::string> *sample,
+                        size_t sample_start) {
+  const char *on = getenv("RURE_AMD_SET_MULTI");
+  if (!(on && on[0] == '1')) return multi_fail(1);
+  if (!rs->groups.empty()) {
+    for (size_t g = 0; g < rs->groups.size(); ++g) {
+      m->parts.push_back(rs->groups[g]);
+      m->word.push_back((uint32_t)g);
+      m->shift.push_back(0);
+    }
+  } else {
+    const int G = set_chains();
+    const size_t n = rs->exprs.size();
+    if (G < 2 || n < (size_t)G) return multi_fail(2);
+    const size_t per = (n + G - 1) / G;
+    for (size_t lo = 0; lo < n; lo += per) {
+      const size_t cnt = std::min(per, n - lo);
+      std::vector<const uint8_t *> ps;
+      std::vector<size_t> ls;
+      for (size_t i = lo; i < lo + cnt; ++i) {
+        ps.push_back((const uint8_t *)rs->patterns[i].data());
+        ls.push_back(rs->patterns[i].size());
+      }
+      rure_error e;
+      rure_set *x = rure_compile_set(ps.data(), ls.data(), cnt, rs->flags, &rs->opts, &e);
+      if (!x) { if (err) *err = e.msg; return multi_fail(3); }
+      m->owned.push_back(x);
+      m->parts.push_back(x);
+      m->word.push_back(0);
+      m->shift.push_back((uint32_t)lo);
+    }
+  }
+  const int G = (int)m->parts.size();
+  if (G < 2 || G > kMultiMaxGroups) return multi_fail(4);
+  for (rure_set *x : m->parts)
+    if (x->single || !build_set_dfa(x)) return multi_fail(5);
+  // quit states (Unicode \b): the Pike VM redoes the words a lane quit in,
+  // with each group's NFA (one word each) or the whole set's (split sets)
+  if (rs->groups.empty() && !rs->nfa_ok) return multi_fail(6);  // (built by multi_device before the lock)
+  // which cores the batch visits (the hot LDS rows) and which masks it
+  // reports (the 62 LDS codes): each group's DFA run on the host over a
+  // sample of the first batch (one copy + sync, once per set, like
+  // adapt_cores)
+  std::vector<std::vector<uint64_t>> sw(G);
+  std::vector<std::unordered_map<uint64_t, uint64_t>> mw(G);
+  if (sample && !sample->empty()) {
+    for (int g = 0; g < G; ++g) {
+      const DenseDfa &d = m->parts[g]->dfa;
+      sw[g].assign(d.nstates, 0);
+      for (const std::string &line : *sample) {
+        const uint8_t *tx = (const uint8_t *)line.data();
+        const size_t len = line.size();
+        if (sample_start > len) continue;
+        uint32_t c = d.start[start_flag_index_fwd(tx, len, sample_start)];
+        for (size_t i = sample_start; i < len && (int)c != d.dead && (int)c != d.quit; ++i) {
+          c = d.trans[(size_t)c * 256 + tx[i]];
+          ++sw[g][c];
+          if (d.now_mask[c]) ++mw[g][d.now_mask[c]];
+        }
+      }
+    }
+  }
+  // one LDS image for all groups: each group's share of 159 KiB, shrunk
+  // until the image fits (class map 512 B, rows, code masks 512 B, start
+  // cores 256 B, hot EOF masks 8 B per hot core)
+  const size_t L = 159 * 1024;
+  size_t bud = L / G;
+  m->cores.assign(G, CoreSet());
+  auto al16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+  for (int tries = 0;; ++tries) {
+    size_t total = 0;
+    for (int g = 0; g < G; ++g) {
+      m->cores[g] = CoreSet();
+      const bool prof = sample && !sample->empty();
+      if (!build_set_cores(m->parts[g]->dfa, bud, &m->cores[g], nullptr, prof ? &mw[g] : nullptr,
+                           prof ? &sw[g] : nullptr))
+        return multi_fail(7);
+      const CoreSet &cs = m->cores[g];
+      total += 512 + al16((size_t)(cs.hot + 1) * (cs.K + 1) * 2) + 512 + 256 + al16(8 * (size_t)cs.hot);
+    }
+    if (total <= L) break;
+    if (tries > 16 || bud < 16 * 1024) return multi_fail(8);
+    bud -= 4 * 1024;
+  }
+  // The share of the sample's visits that stays in every group's LDS cores
+  // (the LDS is split between the groups), for rure_amd_set_multi_info.
+  m->coverage = 1.0;
+  if (sample && !sample->empty()) {
+    for (int g = 0; g < G; ++g) {
+      uint64_t tot = 0;
+      for (uint64_t v : sw[g]) tot += v;
+      const double cov = tot ? (double)m->cores[g].hot_visits / (double)tot : 1.0;
+      m->coverage = std::min(m->coverage, cov);
+    }
+  }
+  MultiCoreDev &P = m->proto;
+  P = MultiCoreDev{};
+  P.G = (uint32_t)G;
+  P.split = rs->groups.empty() ? 1u : 0u;
+  size_t cur = 0;
+  for (int g = 0; g < G; ++g) {
+    const CoreSet &cs = m->cores[g];
+    MultiGroupDev &d = P.g[g];
+    const size_t rows = (size_t)(cs.hot + 1) * (cs.K + 1) * 2;
+    d.K = cs.K;
+    d.hot = cs.hot;
+    d.dead = cs.dead;
+    d.quit = cs.quit;
+    if (cs.quit != 0xFFFFFFFFu) m->quit = true;
+    d.cls_off = (uint32_t)cur;
+    d.rows_off = (uint32_t)(cur + 512);
+    d.mt_off = (uint32_t)(d.rows_off + al16(rows));
+    d.st_off = d.mt_off + 512;
+    d.he_off = d.st_off + 256;
+    d.word = m->word[g];
+    d.shift = m->shift[g];
+    const size_t np = m->parts[g]->exprs.size();
+    d.all = np >= 64 ? ~0ull : ((1ull << np) - 1);
+    cur = d.he_off + al16(8 * (size_t)cs.hot);
+    m->lds.resize(cur, 0);
+    uint16_t *cm = (uint16_t *)(m->lds.data() + d.cls_off);
+    for (int b = 0; b < 256; ++b) cm[b] = (uint16_t)(2 * cs.lds[b]);
+    memcpy(m->lds.data() + d.rows_off, cs.lds.data() + 256, rows);
+    memcpy(m->lds.data() + d.mt_off, cs.codemask, 512);
+    memcpy(m->lds.data() + d.st_off, cs.start, 256);
+    memcpy(m->lds.data() + d.he_off, cs.eof.data(), 8 * (size_t)cs.hot);
+  }
+  m->lds.resize(al16(m->lds.size()), 0);
+  P.lds_bytes = (uint32_t)m->lds.size();
+  uint32_t words = 0;
+  for (int g = 0; g < G; ++g) words = std::max(words, P.g[g].word + 1);
+  P.words = words;
+  return true;
+}
+
+// Host copy of the first haystacks of the batch (the profile sample): at most
+// 4096 of them, each cut to its first 4 KiB, at most 4 MiB in all (so a few
+// huge haystacks cost a bounded copy).
+std::vector<std::string> batch_sample(const BatchDev &b, hipStream_t st) {
+  std::vector<std::string> out;
+  const uint64_t n = std::min<uint64_t>(b.count, 4096);
+  if (!n) return out;
+  constexpr uint64_t kPerHay = 4096, kTotal = 4u << 20;
+  std::vector<uint64_t> offs(n + 1);
+  if (b.offs) {
+    if (hipMemcpyAsync(offs.data(), b.offs, (n + 1) * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      return out;
+  } else {
+    for (uint64_t i = 0; i <= n; ++i) offs[i] = i * b.stride;
+  }
+  std::vector<uint8_t> buf;
+  uint64_t total = 0;
+  for (uint64_t i = 0; i < n && total < kTotal; ++i) {
+    const uint64_t len = b.offs ? offs[i + 1] - offs[i] : b.length;
+    const uint64_t take = std::min<uint64_t>({len, kPerHay, kTotal - total});
+    buf.resize(take);
+    if (take && (hipMemcpyAsync(buf.data(), b.hay + offs[i], take, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                 hipStreamSynchronize(st) != hipSuccess))
+      return out;
+    out.emplace_back((const char *)buf.data(), take);
+    total += take;
+  }
+  return out;
+}
+
+const MultiCoreDev *multi_device(rure_set *rs, std::string *err, const BatchDev &b, hipStream_t st) {
+  if (rs->groups.empty()) build_set(rs);  // split sets: the whole set's NFA (quit fallback); takes rs->mu
+  std::lock_guard<std::mutex> g(rs->mu);
+  if (!rs->multi) rs->multi = new MultiSet();
+  MultiSet *m = rs->multi;
+  if (!m->built) {
+    m->built = true;
+    // opt-in (RURE_AMD_SET_MULTI=1): the default path never samples
+    const char *on = getenv("RURE_AMD_SET_MULTI");
+    if (!(on && on[0] == '1')) {
+      m->ok = false;
+      return nullptr;
+    }
+    const std::vector<std::string> sample = batch_sample(b, st);
+    m->ok = build_multi_locked(rs, m, err, &sample, b.start);
+  }
+  if (!m->ok) return nullptr;
+  int d = 0;
+  if (!hip_ok(hipGetDevice(&d), err)) return nullptr;
+  auto it = m->dev.find(d);
+  if (it != m->dev.end()) return &it->second.second;
+  Blob bl;
+  const int G = (int)m->parts.size();
+  size_t o_core[kMultiMaxGroups], o_out[kMultiMaxGroups], o_eof[kMultiMaxGroups];
+  for (int k = 0; k < G; ++k) {
+    const CoreSet &cs = m->cores[k];
+    o_core[k] = bl.add(cs.gcore.data(), cs.gcore.size() * 2);
+    o_out[k] = bl.add(cs.gout.data(), cs.gout.size() * 8);
+    o_eof[k] = bl.add(cs.eof.data(), cs.eof.size() * 8);
+  }
+  const size_t o_lds = bl.add(m->lds.data(), m->lds.size());
+  DevTables tmp;
+  if (!upload_blob(bl, &tmp, err)) return nullptr;
+  uint8_t *base = (uint8_t *)tmp.blob;
+  MultiCoreDev f = m->proto;
+  f.lds_image = base + o_lds;
+  for (int k = 0; k < G; ++k) {
+    f.g[k].gcore = (const uint16_t *)(base + o_core[k]);
+    f.g[k].gout = (const uint64_t *)(base + o_out[k]);
+    f.g[k].eof = (const uint64_t *)(base + o_eof[k]);
+  }
+  auto &slot = m->dev[d];
+  slot = std::make_pair(tmp.blob, f);
+  return &slot.second;
+}
+
+// The one-pass kernel, then (only where a lane quit: the Pike kernels read
+// the flag first) the Pike VM over the words marked QUITMARK.
+int run_set_multi(rure_set *rs, const BatchDev &b, const MultiCoreDev &f, uint64_t *mask, hipStream_t st) {
+  MultiSet *m = rs->multi;
+  const int cus = device_cus_cached();
+  if (getenv("RURE_AMD_MULTI_DEBUG")) {  // diagnostic: the combined image's layout
+    fprintf(stderr, "set_multi: G %u words %u split %u lds %u quit %d\n", f.G, f.words, f.split, f.lds_bytes,
+            (int)m->quit);
+    for (uint32_t g = 0; g < f.G; ++g)
+      fprintf(stderr, "  group %u: K %u hot %u dead %u quit %u cls %u rows %u mt %u st %u he %u word %u shift %u\n", g,
+              f.g[g].K, f.g[g].hot, f.g[g].dead, f.g[g].quit, f.g[g].cls_off, f.g[g].rows_off, f.g[g].mt_off,
+              f.g[g].st_off, f.g[g].he_off, f.g[g].word, f.g[g].shift);
+  }
+  if (!m->quit) return launch_set_multi(b, f, mask, st, cus) == hipSuccess ? RURE_AMD_OK : RURE_AMD_ERR_HIP;
+  std::string err;
+  BatchDev bq = b;
+  hipError_t e = scratch_malloc((void **)&bq.quit_flag, 4, st);
+  if (e == hipSuccess) e = hipMemsetAsync(bq.quit_flag, 0, 4, st);
+  if (e == hipSuccess) e = launch_set_multi(bq, f, mask, st, cus);
+  if (e == hipSuccess && f.split) {
+    const DevTables *t = set_device(rs, &err);
+    e = t ? run_pike(MODE_SET, true, bq, *t, mask, st) : hipErrorInvalidValue;
+  } else {
+    for (size_t g = 0; e == hipSuccess && g < m->parts.size(); ++g) {
+      const DevTables *t = set_device(m->parts[g], &err);
+      if (!t) { e = hipErrorInvalidValue; break; }
+      BatchDev bg = bq;
+      bg.out_stride = f.words;
+      e = run_pike(MODE_SET, true, bg, *t, mask + f.g[g].word, st);
+    }
+  }
+  if (bq.quit_flag) {
+    hipError_t e2 = scratch_free(bq.quit_flag, st);
+    if (e == hipSuccess) e = e2;
+  }
+  return e == hipSuccess ? RURE_AMD_OK : RURE_AMD_ERR_HIP;
+}
+
+int set_batch_group(rure_set *g, const rure_amd_batch *batch, const BatchDev &b, uint64_t *mask, size_t words,
+                    size_t w, hipStream_t st) {
+  void *tmp = nullptr;
+  const bool single = g->single != nullptr;
+  if (scratch_malloc(&tmp, b.count * (single ? 1 : 8), st) != hipSuccess) return RURE_AMD_ERR_HIP;
+  int rc = single ? rure_amd_is_match_batch(g->single, batch, (uint8_t *)tmp, st)
+                  : set_batch_word(g, b, (uint64_t *)tmp, st);
+  if (rc == RURE_AMD_OK &&
+      launch_mask_column(single ? (const uint8_t *)tmp : nullptr, single ? nullptr : (const uint64_t *)tmp, b.count,
+                         mask, words, w, st) != hipSuccess)
+    rc = RURE_AMD_ERR_HIP;
+  if (scratch_free(tmp, st) != hipSuccess && rc == RURE_AMD_OK) rc = RURE_AMD_ERR_HIP;
+  return rc;
+}
+
+
+
+// The batched find_iter (re_trait.rs:197-221) on one stream.
+hipError_t run_find_iter(rure *re, DevTables *t, const BatchDev &b, const IterOut &o, hipStream_t st,
+                         std::string *err, const IterSpan *sp) {
+  // DfaAnchoredReverse regexes match only at the end of the text, so the
+  // iteration (re_trait.rs:197-221) yields at most the first search's match
+  // (the next search starts at the end, where an empty match is the one just
+  // reported or skipped).  Searched from `start` > 0, that first search is
+  // the reverse DFA over text[start..] (its look-behind differs from the
+  // forward scan's); from 0 the chunked path below answers the same.
+  if (!sp && t->anchored_rev && b.start > 0 && b.count) {
+    uint64_t *found = nullptr;
+    hipError_t e = scratch_malloc((void **)&found, b.count * 16, st);
+    if (e != hipSuccess) return e;
+    e = run_regex(MODE_FIND, b, *t, found, st, grid_for(b.count, t->r.lds_bytes, t->cus));
+    if (e == hipSuccess) e = launch_find_to_iter(found, b.count, o.counts, o.matches, o.cap, o.total, st);
+    hipError_t e2 = scratch_free(found, st);
+    return e != hipSuccess ? e : e2;
+  }
+  // The reference's Literal / DfaSuffix searches (DevTables::mt_lane): every
+  // search of the iteration is one of those, on a wave per haystack (lane 0
+  // searches, the wave runs the Pike VM where a DfaSuffix scan quits).
+  if (lane_search_ok(*t) && re->nfa_ok)
+    return launch_find_iter(b, t->has_dfa ? &t->f : nullptr, t->r, &t->n, false, 0, o, st, t->cus, sp, &t->m);
+  // Chunked speculative iteration needs a DFA that cannot quit and a pattern
+  // without assertions (see iter_scan.hip); otherwise one wave per haystack.
+  const FwdDfaDev *fi = nullptr;
+  if (t->has_dfa && !t->quit_possible && re->nfa_ok && re->nt.looks_used == 0) fi = iter_device(re, *t, err);
+  if (fi) {
+    uint64_t chunk = ~0ull >> 2;
+    const uint64_t lim = sp ? std::min<uint64_t>(b.length, sp->hi) : b.length;
+    if (!b.offs && lim > b.start && b.count) {
+      const uint64_t span = lim - b.start;
+      // lanes in flight: 16 waves per CU (tools/iter_sweep.py);
+      // RURE_AMD_ITER_LANES (per CU) overrides (tuning)
+      uint64_t per_cu = 1024;
+      if (const char *v = getenv("RURE_AMD_ITER_LANES")) per_cu = std::max(64, atoi(v));
+      const uint64_t target = (uint64_t)t->cus * per_cu;
+      const uint64_t per_h = (target + b.count - 1) / b.count;
+      chunk = odd_lines(std::max<uint64_t>(4096, (span + per_h - 1) / per_h));
+    }
+    return launch_find_iter(b, fi, t->r, &t->n, true, chunk, o, st, t->cus, sp);
+  }
+  if (!re->nfa_ok) return hipErrorInvalidValue;
+  return launch_find_iter(b, t->has_dfa ? &t->f : nullptr, t->r, &t->n, false, 0, o, st, t->cus, sp);
+}
+
+
+hipError_t iter_to_device(rure *re, DevTables *t, const BatchDev &b, hipStream_t st, IterBufs *ib, std::string *err) {
+  ib->st = st;
+  hipError_t e;
+  const size_t n = b.count;
+  if ((e = scratch_malloc((void **)&ib->counts, (n + 1) * 8, st)) != hipSuccess) return e;
+  if ((e = scratch_malloc((void **)&ib->moff, (n + 1) * 8, st)) != hipSuccess) return e;
+  if ((e = scratch_malloc((void **)&ib->total, 8, st)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(ib->counts, 0, (n + 1) * 8, st)) != hipSuccess) return e;
+  const uint64_t bytes = b.offs ? 0 : (uint64_t)b.count * b.length;
+  uint64_t cap = std::max<uint64_t>(1024, bytes / 64 + 2 * n);
+  for (int pass = 0; pass < 2; ++pass) {
+    if ((e = scratch_malloc((void **)&ib->m, cap * 16, st)) != hipSuccess) return e;
+    IterOut o{ib->counts, ib->m, cap, ib->total};
+    if ((e = run_find_iter(re, t, b, o, st, err)) != hipSuccess) return e;
+    uint64_t tot = 0;
+    if ((e = hipMemcpyAsync(&tot, ib->total, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+    ib->nm = tot;
+    if (tot <= cap) break;
+    (void)scratch_free(ib->m, st);
+    ib->m = nullptr;
+    cap = tot;
+  }
+  return exclusive_scan_u64(ib->counts, ib->moff, n + 1, st);
+}
+
+
+// k-mer probe tables of a regex list (KmerDev), built once per list and
+// device: every regex a finite set of strings of one length L <= 8 over an
+// alphabet of at most 4 bytes with distinct codes (b >> shift) & 3.
+struct KmerCacheEntry {
+  std::vector<const rure *> res;
+  int dev;
+  void *blob;
+  KmerDev km;
+};
+std::mutex g_kmer_mu;
+std::vector<KmerCacheEntry> g_kmer;
+
+bool build_kmer(rure *const *res, size_t n, std::vector<uint32_t> *bitmap, std::vector<uint16_t> *mask, KmerDev *km) {
+  if (n == 0 || n > 16) return false;
+  size_t L = 0;
+  bool seen[256] = {false};
+  std::vector<uint8_t> alpha;
+  for (size_t i = 0; i < n; ++i) {
+    rure *re = res[i];
+    if (!re->lit_ok || re->lits.lits.empty() || re->lits.minlen != re->lits.maxlen) return false;
+    if (L == 0) L = re->lits.minlen;
+    if (re->lits.minlen != L) return false;
+    for (const std::string &l : re->lits.lits)
+      for (unsigned char c : l)
+        if (!seen[c]) {
+          seen[c] = true;
+          alpha.push_back(c);
+        }
+  }
+  if (L == 0 || L > 8 || alpha.size() > 4) return false;
+  int shift = -1;
+  for (int sh = 0; sh <= 6 && shift < 0; ++sh) {
+    uint32_t used = 0;
+    bool ok = true;
+    for (uint8_t c : alpha) {
+      const uint32_t code = (c >> sh) & 3u;
+      if (used & (1u << code)) ok = false;
+      used |= 1u << code;
+    }
+    if (ok) shift = sh;
+  }
+  if (shift < 0) return false;
+  km->shift = (uint32_t)shift;
+  km->lut = 0;
+  km->present = 0;
+  for (uint8_t c : alpha) {
+    const uint32_t code = (c >> shift) & 3u;
+    km->lut |= (uint32_t)c << (8 * code);
+    km->present |= 1u << code;
+  }
+  km->len = L;
+  km->cmask = (uint32_t)((1ull << (2 * L)) - 1);
+  bitmap->assign(2048, 0);
+  mask->assign((size_t)1 << (2 * L), 0);
+  for (size_t i = 0; i < n; ++i)
+    for (const std::string &l : res[i]->lits.lits) {
+      uint32_t code = 0;
+      for (size_t j = 0; j < L; ++j) code |= (((uint8_t)l[j] >> shift) & 3u) << (2 * j);
+      (*bitmap)[code >> 5] |= 1u << (code & 31);
+      (*mask)[code] |= (uint16_t)(1u << i);
+    }
+  return true;
+}
+
+// The cached device tables for this regex list, copied into *out while the
+// cache lock is held (an entry's address does not outlive the lock: another
+// thread's push_back or kmer_forget moves the vector).  False: not eligible.
+bool kmer_device(rure *const *res, size_t n, KmerDev *out) {
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess) return false;
+  std::lock_guard<std::mutex> g(g_kmer_mu);
+  for (const KmerCacheEntry &e : g_kmer)
+    if (e.dev == d && e.res.size() == n && std::equal(e.res.begin(), e.res.end(), res)) {
+      if (e.blob) *out = e.km;
+      return e.blob != nullptr;
+    }
+  KmerCacheEntry ent;
+  ent.res.assign(res, res + n);
+  ent.dev = d;
+  ent.blob = nullptr;
+  std::vector<uint32_t> bm;
+  std::vector<uint16_t> mk;
+  if (build_kmer(res, n, &bm, &mk, &ent.km)) {
+    Blob b;
+    const size_t ob = b.add(bm.data(), bm.size() * 4), om = b.add(mk.data(), mk.size() * 2);
+    DevTables tmp;
+    std::string err;
+    if (upload_blob(b, &tmp, &err)) {
+      ent.blob = tmp.blob;
+      ent.km.bitmap = (const uint32_t *)((uint8_t *)tmp.blob + ob);
+      ent.km.mask = (const uint16_t *)((uint8_t *)tmp.blob + om);
+    }
+  }
+  g_kmer.push_back(ent);
+  if (ent.blob) *out = ent.km;
+  return ent.blob != nullptr;
+}
+
+// rure_free: drop the k-mer tables of lists holding this regex.
+void kmer_forget(const rure *re) {
+  std::lock_guard<std::mutex> g(g_kmer_mu);
+  for (size_t i = 0; i < g_kmer.size();) {
+    if (std::find(g_kmer[i].res.begin(), g_kmer[i].res.end(), re) != g_kmer[i].res.end()) {
+      if (g_kmer[i].blob) {
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        (void)hipSetDevice(g_kmer[i].dev);
+        (void)hipFree(g_kmer[i].blob);
+        (void)hipSetDevice(cur);
+      }
+      g_kmer.erase(g_kmer.begin() + i);
+    } else {
+      ++i;
+    }
+  }
+}
+
+}  // namespace rt

@@ -362,7 +362,7 @@ hipError_t launch_big_dfa(int mode, const BatchDev &b, const BigDfaDev &f, const
 // Rows of a big forward DFA the kernel holds in LDS.
 uint32_t big_dfa_hot_rows(uint32_t ncol, uint32_t nstates);
 
-// Scratch device memory for the scans, cached by the library (rure_amd.cpp):
+// Scratch device memory for the scans, cached by the library (scratch.cpp):
 // a freed block is kept with an event recorded on the freeing stream and
 // reused, after a wait on that event, by the next allocation of at most twice
 // its size on any stream of the device — freeing to the driver (hipFree,

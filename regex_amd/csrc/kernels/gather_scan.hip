@@ -104,7 +104,7 @@ __global__ __launch_bounds__(256) void mask_column_kernel(const uint8_t *s8, con
 }
 
 // find_iter of a regex whose every match ends at the end of the text
-// (DfaAnchoredReverse): at most the find result (rure_amd.cpp run_find_iter).
+// (DfaAnchoredReverse): at most the find result (dispatch.cpp run_find_iter).
 __global__ __launch_bounds__(256) void one_match_counts_kernel(const uint64_t *found, uint64_t n, uint64_t *cnt) {
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
     cnt[i] = found[2 * i] != ~(uint64_t)0 ? 1 : 0;

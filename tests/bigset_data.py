@@ -1,6 +1,6 @@
 """Pattern sets of more than 64 patterns (RegexSet has no size bound in the
 reference: re_set.rs:86-213, compile.rs:162-198, rure.rs:468-566).  The GPU
-runs them in groups of 64 consecutive patterns (rure_amd.cpp, rure_set)."""
+runs them in groups of 64 consecutive patterns (runtime.hpp, rure_set)."""
 from regex_amd.workloads import C4_PATTERNS
 
 EXTRA = [

@@ -234,7 +234,7 @@ def test_literal_find_default_dispatch(cuda, monkeypatch, nwords):
         rng = np.random.default_rng(11)
         pat = "|".join(rng.choice(words, nwords, replace=False))
     re = R.Regex(pat)
-    L = 256  # below the small-batch split (rure_amd.cpp long_batch: >= 512 B)
+    L = 256  # below the small-batch split (dispatch.cpp long_batch: >= 512 B)
     n = len(text) // L
     buf = text[: n * L]
     d = dev(buf, cuda)

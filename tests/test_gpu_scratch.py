@@ -1,4 +1,4 @@
-"""Scratch memory hygiene (rure_amd.cpp scratch cache): device scratch kept
+"""Scratch memory hygiene (scratch.cpp scratch cache): device scratch kept
 between batched calls goes back to the allocator on rure_amd_release_scratch()
 and when the last rure / rure_set is freed, so the device's free memory
 returns to where it was."""

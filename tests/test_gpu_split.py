@@ -1,6 +1,6 @@
 """Small batches of medium haystacks (BASELINE C1's shape, 1024 x 1 KiB) are
 split into units of >= 128 B scanned with the cut-bounded search
-(rure_amd.cpp long_batch, long_scan_kernel) instead of one lane per haystack.
+(dispatch.cpp long_batch, long_scan_kernel) instead of one lane per haystack.
 is_match takes it (find / shortest_match units would scan on until the DFA
 dies: a never-dying pattern costs every unit the rest of its haystack);
 is_match / find / shortest_match must equal the oracle and the unsplit

@@ -1,5 +1,5 @@
 """Sets of more than 64 patterns on the CPU: the grouped evaluation the GPU
-uses (64 consecutive patterns per group, rure_amd.cpp rure_set::groups) gives
+uses (64 consecutive patterns per group, runtime.hpp rure_set::groups) gives
 the combined set's answer.  Checked with the oracle (restated DfaMany /
 Pike VM, dfa.rs:525-570, pikevm.rs:150-180) over the combined program versus
 the oracle over each group's own program, on log lines and odd haystacks."""

@@ -1,4 +1,4 @@
-"""Host side of the Shift-And find_iter engine (rure_amd.cpp build_shiftand,
+"""Host side of the Shift-And find_iter engine (build.cpp build_shiftand,
 used by iter_spec_sa_kernel): the class sequences merged from a string set
 must recognise exactly the set.  The automaton is stepped here as the kernel
 steps it (D = ((D << 1) | init) & mask[b]; a final bit after byte q = a string
