@@ -21,13 +21,14 @@ ORACLE_SRC = $(wildcard oracle/*.c)
 
 all: $(LIB) $(ORACLE_LIB)
 
+# host code: no device pass (hipcc would otherwise also compile it for a default GPU)
 $(OBJDIR)/%.o: regex_amd/csrc/host/%.cpp $(HDRS)
 	@mkdir -p $(OBJDIR)
-	$(HIPCC) $(CXXFLAGS) -c $< -o $@
+	$(HIPCC) $(CXXFLAGS) --offload-host-only -c $< -o $@
 
 $(OBJDIR)/rt_%.o: regex_amd/csrc/%.cpp $(HDRS) regex_amd/csrc/runtime.hpp
 	@mkdir -p $(OBJDIR)
-	$(HIPCC) $(CXXFLAGS) -c $< -o $@
+	$(HIPCC) $(CXXFLAGS) --offload-host-only -c $< -o $@
 
 $(OBJDIR)/%.o: regex_amd/csrc/kernels/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
