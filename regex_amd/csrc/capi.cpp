@@ -691,7 +691,7 @@ int rure_amd_replace_batch(rure *re, const rure_amd_batch *batch, const uint8_t 
   if (e == hipSuccess && out_capacity) {
     const uint64_t hint = b.offs ? out_capacity : std::min<uint64_t>(out_capacity, b.count * b.length + ib.nm * rep_len);
     e = launch_replace_copy(b, out_offsets, ib.counts, ib.moff, ib.m, shift, lim, drep, rep_len, out, out_capacity,
-                            hint, st, t->cus);
+                            hint, st, t->cus, ib.nm);
   }
   if (shift) (void)scratch_free(shift, st);
   if (olen) (void)scratch_free(olen, st);

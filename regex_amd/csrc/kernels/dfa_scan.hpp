@@ -248,7 +248,8 @@ hipError_t launch_replace_plan(const BatchDev &b, const uint64_t *counts, const 
 hipError_t launch_replace_copy(const BatchDev &b, const uint64_t *ooff, const uint64_t *counts, const uint64_t *moff,
                                const uint64_t *m, const int64_t *shift, uint64_t limit, const uint8_t *rep,
                                uint64_t rep_len, uint8_t *out, uint64_t cap, uint64_t total_hint, hipStream_t st,
-                               int cus);
+                               int cus,
+                               uint64_t nm);
 hipError_t launch_split(const BatchDev &b, const uint64_t *counts, const uint64_t *moff, const uint64_t *m,
                         uint64_t lim, uint64_t *fields, uint64_t *foff, uint64_t *pieces, uint64_t cap,
                         uint64_t nmatches, hipStream_t st, int cus);

@@ -19,6 +19,7 @@
 // SplitN rule for a limit (its last field is the remainder of the text).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <rocprim/rocprim.hpp>
@@ -122,58 +123,319 @@ __global__ __launch_bounds__(256) void replace_plan_kernel(BatchDev bt, const ui
   }
 }
 
-__global__ __launch_bounds__(256) void replace_copy_kernel(BatchDev bt, const uint64_t *ooff, const uint64_t *counts,
-                                                           const uint64_t *moff, const uint64_t *m,
-                                                           const int64_t *shift, uint64_t limit, const uint8_t *rep,
-                                                           uint64_t rep_len, uint8_t *out, uint64_t cap) {
-  const uint64_t n = bt.count;
-  const uint64_t total = ooff[n] < cap ? ooff[n] : cap;
-  const uint64_t nblk = (total + 15) / 16;
-  for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nblk; q += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t p0 = q * 16;
-    uint64_t h = upper_idx(ooff, 0, n + 1, p0) - 1;  // ooff[h] <= p0 < ooff[h+1]
-    uint8_t v[16];
-    uint64_t hh = ~0ull, base = 0, k = 0, m0 = 0, jj = 0;  // jj = matches whose replacement starts <= position
-    for (int i = 0; i < 16; ++i) {
-      const uint64_t p = p0 + i;
-      if (p >= total) { v[i] = 0; continue; }
-      while (p >= ooff[h + 1]) ++h;  // haystacks with empty output are skipped
-      const uint64_t loc = p - ooff[h];
-      if (h != hh) {
-        hh = h;
-        uint64_t len;
-        hay_of(bt, h, &base, &len);
-        k = counts[h] < limit ? counts[h] : limit;
-        m0 = moff[h];
-        uint64_t lo = 0, hi = k;
-        while (lo < hi) {
-          const uint64_t mid = (lo + hi) >> 1;
-          if ((uint64_t)((int64_t)m[2 * (m0 + mid)] - shift[m0 + mid]) <= loc) lo = mid + 1;
-          else hi = mid;
-        }
-        jj = lo;
-      }
-      while (jj < k && (uint64_t)((int64_t)m[2 * (m0 + jj)] - shift[m0 + jj]) <= loc) ++jj;
-      uint8_t c;
-      if (jj == 0) {
-        c = bt.hay[base + loc];
-      } else {
-        const uint64_t j = m0 + jj - 1;
-        const uint64_t r = (uint64_t)((int64_t)m[2 * j] - shift[j]);
-        c = loc - r < rep_len ? rep[loc - r] : bt.hay[base + m[2 * j + 1] + (loc - r - rep_len)];
-      }
-      v[i] = c;
+// 16 bytes from an arbitrary address, as two aligned 16-byte loads and a
+// funnel shift (the second load is the aligned block holding p[15], so it
+// stays inside the buffer's 16-byte-rounded end whenever p[0..16) does).
+__device__ __forceinline__ uint4 load16u(const uint8_t *p) {
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t off = (uint32_t)(a & 15);
+  const uint4 x = *(const uint4 *)(a - off);
+  if (off == 0) return x;
+  const uint4 y = *(const uint4 *)(a - off + 16);
+  const uint64_t w0 = ((uint64_t)x.y << 32) | x.x, w1 = ((uint64_t)x.w << 32) | x.z;
+  const uint64_t w2 = ((uint64_t)y.y << 32) | y.x, w3 = ((uint64_t)y.w << 32) | y.z;
+  uint64_t r0, r1;
+  const uint32_t sh = off * 8;
+  if (sh < 64) {
+    r0 = (w0 >> sh) | (w1 << (64 - sh));
+    r1 = (w1 >> sh) | (w2 << (64 - sh));
+  } else if (sh == 64) {
+    r0 = w1;
+    r1 = w2;
+  } else {
+    const uint32_t s2 = sh - 64;
+    r0 = (w1 >> s2) | (w2 << (64 - s2));
+    r1 = (w2 >> s2) | (w3 << (64 - s2));
+  }
+  return make_uint4((uint32_t)r0, (uint32_t)(r0 >> 32), (uint32_t)r1, (uint32_t)(r1 >> 32));
+}
+
+// replace_copy_kernel: a wave writes a 1 KiB window of the output per step,
+// lane l its 16-byte block l (coalesced stores).  Every match's replacement
+// start in global output coordinates (G, replace_index_kernel) is counted
+// per window and the counts prefix-summed (widx[w] = matches with G below
+// window w), so a lane searches only the few matches of its own window: a
+// binary search over all matches per block or per window is a chain of ~25
+// dependent loads (the kernel took 12-25 ms per regex-dna substitution).
+constexpr uint32_t kWin = 1024;
+
+__global__ __launch_bounds__(256) void replace_g_kernel(uint64_t n, const uint64_t *ooff, const uint64_t *moff,
+                                                        const uint64_t *m, const int64_t *shift, uint64_t *G) {
+  const uint64_t nm = moff[n];
+  for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < nm; g += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t h = n == 1 ? 0 : upper_idx(moff, 0, n + 1, g) - 1;
+    G[g] = ooff[h] + (uint64_t)((int64_t)m[2 * g] - shift[g]);
+  }
+}
+
+// widx[w] = the first match with G >= w * kWin (G is non-decreasing), for w
+// in [0, nent): one independent binary search per window (a scatter from the
+// matches would leave one thread to fill the windows of a long match-free
+// stretch).
+__global__ __launch_bounds__(256) void replace_widx_kernel(uint64_t n, const uint64_t *moff, const uint64_t *G,
+                                                           uint64_t nent, uint64_t *widx) {
+  const uint64_t nm = moff[n];
+  for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nent; w += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t x = w * kWin;
+    uint64_t lo = 0, hi = nm;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (G[mid] < x) lo = mid + 1;
+      else hi = mid;
     }
-    if (p0 + 16 <= total) {
-      uint4 w;
-      w.x = v[0] | (v[1] << 8) | (v[2] << 16) | ((uint32_t)v[3] << 24);
-      w.y = v[4] | (v[5] << 8) | (v[6] << 16) | ((uint32_t)v[7] << 24);
-      w.z = v[8] | (v[9] << 8) | (v[10] << 16) | ((uint32_t)v[11] << 24);
-      w.w = v[12] | (v[13] << 8) | (v[14] << 16) | ((uint32_t)v[15] << 24);
-      *(uint4 *)(out + p0) = w;
+    widx[w] = lo;
+  }
+}
+
+// One output block at global position p0 (window w): the byte-by-byte
+// path (a replacement edge, a haystack edge or the output end) or, when
+// `fast`, one 16-byte load of the text.  Split in two so that the kernel can
+// run four blocks' dependent load chains side by side.
+struct CopyCtx {
+  BatchDev bt;
+  const uint64_t *ooff, *counts, *moff, *m, *G, *widx;
+  const int64_t *shift;
+  uint64_t limit, rep_len, total, cap;
+  const uint8_t *rep;
+  __device__ __forceinline__ uint64_t R(uint64_t j) const { return (uint64_t)((int64_t)m[2 * j] - shift[j]); }
+};
+
+struct BlockPlan {
+  uint64_t h, jj, src;  // haystack, matches passed, text source (fast)
+  bool fast;
+};
+
+__device__ __forceinline__ BlockPlan plan_block(const CopyCtx &c, uint64_t w, uint64_t p0) {
+  BlockPlan b;
+  uint64_t lo = c.widx[w], hi = c.widx[w + 1];
+  while (lo < hi) {  // matches with G <= p0 among the window's few
+    const uint64_t mid = (lo + hi) >> 1;
+    if (c.G[mid] <= p0) lo = mid + 1;
+    else hi = mid;
+  }
+  const uint64_t n = c.bt.count;
+  b.h = n == 1 ? 0 : upper_idx(c.ooff, 0, n + 1, p0) - 1;
+  const uint64_t hbeg = c.ooff[b.h], hend = c.ooff[b.h + 1];
+  const uint64_t k = c.counts[b.h] < c.limit ? c.counts[b.h] : c.limit;
+  const uint64_t m0 = c.moff[b.h];
+  // matches of this haystack with R <= loc; only its first k are replaced
+  // (matches past the limit keep their text: their G, still increasing,
+  // counts above k and is clamped)
+  uint64_t jj = lo > m0 ? lo - m0 : 0;
+  b.jj = jj > k ? k : jj;
+  const uint64_t loc = p0 - hbeg;
+  b.fast = false;
+  b.src = 0;
+  if (p0 + 16 <= hend && p0 + 16 <= c.total) {
+    const uint64_t nextR = b.jj < k ? c.R(m0 + b.jj) : ~0ull;
+    const uint64_t r = b.jj ? c.R(m0 + b.jj - 1) : 0;
+    if (loc + 16 <= nextR && (b.jj == 0 || loc - r >= c.rep_len)) {
+      uint64_t base, len;
+      hay_of(c.bt, b.h, &base, &len);
+      b.src = base + (b.jj ? c.m[2 * (m0 + b.jj - 1) + 1] + (loc - r - c.rep_len) : loc);
+      b.fast = true;
+    }
+  }
+  return b;
+}
+
+// A block with replacement edges inside one haystack: the (at most four)
+// matches it can touch are loaded together, then each byte's source address
+// is computed on its own, so the 16 byte loads are independent (a walk per
+// byte was a chain of three dependent loads per byte).  False: the generic
+// walk must do it (a haystack or output edge, or more edges in the block).
+__device__ __forceinline__ bool copy_block_edges(const CopyCtx &c, uint64_t p0, const BlockPlan &b, uint8_t *out) {
+  const uint64_t hbeg = c.ooff[b.h], hend = c.ooff[b.h + 1];
+  if (p0 + 16 > hend || p0 + 16 > c.total) return false;
+  const uint64_t k = c.counts[b.h] < c.limit ? c.counts[b.h] : c.limit, m0 = c.moff[b.h];
+  const uint64_t loc = p0 - hbeg;
+  uint64_t base, len;
+  hay_of(c.bt, b.h, &base, &len);
+  // matches jj - 1 + t, t = 0..4: replacement starts and match ends
+  uint64_t Rt[5], Et[5];
+#pragma unroll
+  for (int t = 0; t < 5; ++t) {
+    const int64_t j = (int64_t)b.jj - 1 + t;
+    const bool ok = j >= 0 && (uint64_t)j < k;
+    Rt[t] = ok ? c.R(m0 + (uint64_t)j) : ~0ull;
+    Et[t] = ok ? c.m[2 * (m0 + (uint64_t)j) + 1] : 0;
+  }
+  if (Rt[4] <= loc + 15) return false;  // more than three replacements start in the block
+  uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const uint64_t lc = loc + i;
+    const int idx = (Rt[1] <= lc) + (Rt[2] <= lc) + (Rt[3] <= lc);  // Rt[0] <= loc when jj > 0
+    uint8_t ch;
+    if (b.jj == 0 && idx == 0) {
+      ch = c.bt.hay[base + lc];
     } else {
-      for (int i = 0; i < 16 && p0 + i < total; ++i) out[p0 + i] = v[i];
+      // the last match passed is jj - 1 + idx, i.e. Rt[idx]
+      const uint64_t rr = Rt[idx], off = lc - rr;
+      ch = off < c.rep_len ? c.rep[off] : c.bt.hay[base + Et[idx] + (off - c.rep_len)];
     }
+    w[i >> 2] |= (uint32_t)ch << (8 * (i & 3));
+  }
+  *(uint4 *)(out + p0) = make_uint4(w[0], w[1], w[2], w[3]);
+  return true;
+}
+
+__device__ __noinline__ void copy_block_slow(const CopyCtx &c, uint64_t p0, const BlockPlan &b, uint8_t *out) {
+  if (copy_block_edges(c, p0, b, out)) return;
+  uint8_t v[16];
+  uint64_t hh = b.h, he = c.ooff[b.h + 1], bb, ln;
+  hay_of(c.bt, hh, &bb, &ln);
+  uint64_t kk = c.counts[hh] < c.limit ? c.counts[hh] : c.limit, mm = c.moff[hh], j2 = b.jj;
+  for (int i = 0; i < 16; ++i) {
+    const uint64_t p = p0 + i;
+    uint8_t ch = 0;
+    if (p < c.total) {
+      if (p >= he) {  // the next haystack (empty outputs skipped)
+        while (p >= c.ooff[hh + 1]) ++hh;
+        he = c.ooff[hh + 1];
+        hay_of(c.bt, hh, &bb, &ln);
+        kk = c.counts[hh] < c.limit ? c.counts[hh] : c.limit;
+        mm = c.moff[hh];
+        j2 = 0;
+      }
+      const uint64_t lc = p - c.ooff[hh];
+      while (j2 < kk && c.R(mm + j2) <= lc) ++j2;
+      if (j2 == 0) {
+        ch = c.bt.hay[bb + lc];
+      } else {
+        const uint64_t j = mm + j2 - 1;
+        const uint64_t rr = c.R(j);
+        ch = lc - rr < c.rep_len ? c.rep[lc - rr] : c.bt.hay[bb + c.m[2 * j + 1] + (lc - rr - c.rep_len)];
+      }
+    }
+    v[i] = ch;
+  }
+  if (p0 + 16 <= c.total) {
+    uint4 x;
+    x.x = v[0] | (v[1] << 8) | (v[2] << 16) | ((uint32_t)v[3] << 24);
+    x.y = v[4] | (v[5] << 8) | (v[6] << 16) | ((uint32_t)v[7] << 24);
+    x.z = v[8] | (v[9] << 8) | (v[10] << 16) | ((uint32_t)v[11] << 24);
+    x.w = v[12] | (v[13] << 8) | (v[14] << 16) | ((uint32_t)v[15] << 24);
+    *(uint4 *)(out + p0) = x;
+  } else {
+    for (int i = 0; i < 16 && p0 + i < c.total; ++i) out[p0 + i] = v[i];
+  }
+}
+
+// A wave writes 4 KiB per step: lane l the 16-byte block l of each of four
+// 1 KiB windows (coalesced stores), the four blocks' load chains (window
+// index, its matches, the text) in flight together.
+constexpr uint32_t kCopyILP = 4;
+
+__global__ __launch_bounds__(256) void replace_copy_kernel(CopyCtx c, uint8_t *out) {
+  const uint64_t n = c.bt.count;
+  c.total = c.ooff[n] < c.cap ? c.ooff[n] : c.cap;
+  const uint64_t nwin = (c.total + kWin - 1) / kWin;
+  const uint64_t nsup = (nwin + kCopyILP - 1) / kCopyILP;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  for (uint64_t sw = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); sw < nsup; sw += nwaves) {
+    BlockPlan b[kCopyILP];
+    uint64_t p0[kCopyILP];
+#pragma unroll
+    for (uint32_t q = 0; q < kCopyILP; ++q) {
+      const uint64_t w = sw * kCopyILP + q;
+      p0[q] = w * kWin + 16 * (uint64_t)lane;
+      if (w < nwin && p0[q] < c.total) b[q] = plan_block(c, w, p0[q]);
+      else { b[q].fast = false; b[q].h = ~0ull; }
+    }
+    uint4 v[kCopyILP];
+#pragma unroll
+    for (uint32_t q = 0; q < kCopyILP; ++q)
+      if (b[q].fast) v[q] = load16u(c.bt.hay + b[q].src);
+#pragma unroll
+    for (uint32_t q = 0; q < kCopyILP; ++q) {
+      if (b[q].fast) *(uint4 *)(out + p0[q]) = v[q];
+      else if (b[q].h != ~0ull) copy_block_slow(c, p0[q], b[q], out);
+    }
+  }
+}
+
+// replace_all over one haystack (the regex-dna strip and substitutions): the
+// window's matches (their replacement starts R and match ends E, one
+// coalesced load per wave) are staged in LDS and every lane searches and
+// reads them there, so a block's dependent global loads are the window
+// index, the staged records and its text; windows with more than 58 matches
+// take the generic path.
+constexpr uint32_t kStageSlots = 64;
+
+__global__ __launch_bounds__(256) void replace_copy1_kernel(CopyCtx c, uint8_t *out) {
+  __shared__ uint64_t sR[4][kStageSlots], sE[4][kStageSlots];
+  const uint64_t total = c.ooff[1] < c.cap ? c.ooff[1] : c.cap;
+  c.total = total;
+  const uint64_t nm = c.moff[1];
+  const uint64_t nwin = (total + kWin - 1) / kWin;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint64_t base, len;
+  hay_of(c.bt, 0, &base, &len);
+  const uint8_t *hay = c.bt.hay + base;
+  const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  for (uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv; w < nwin; w += nwaves) {
+    const uint64_t lo = c.widx[w], hi = c.widx[w + 1], cnt = hi - lo;
+    const uint64_t p0 = w * kWin + 16 * (uint64_t)lane;
+    if (cnt + 5 > kStageSlots) {  // dense window: the generic per-block path
+      if (p0 < total) {
+        const BlockPlan b = plan_block(c, w, p0);
+        if (b.fast) *(uint4 *)(out + p0) = load16u(c.bt.hay + b.src);
+        else copy_block_slow(c, p0, b, out);
+      }
+      continue;
+    }
+    {  // slot l = match lo - 1 + l (slot 0: the match before the window)
+      const int64_t g = (int64_t)lo - 1 + (int64_t)lane;
+      const bool ok = g >= 0 && (uint64_t)g < nm && (uint64_t)lane < cnt + 5;
+      sR[wv][lane] = ok ? c.G[g] : ~0ull;
+      sE[wv][lane] = ok ? c.m[2 * g + 1] : 0;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (p0 < total) {
+      uint32_t a = 0, bnd = (uint32_t)cnt;  // window matches with R <= p0: slots 1..a
+      while (a < bnd) {
+        const uint32_t mid = (a + bnd) >> 1;
+        if (sR[wv][1 + mid] <= p0) a = mid + 1;
+        else bnd = mid;
+      }
+      const uint64_t jj = lo + a;  // matches passed; the last one is slot a
+      const uint64_t nextR = sR[wv][a + 1];
+      const uint64_t r = jj ? sR[wv][a] : 0;
+      if (p0 + 16 <= total && p0 + 16 <= nextR && (jj == 0 || p0 - r >= c.rep_len)) {
+        const uint64_t src = jj ? sE[wv][a] + (p0 - r - c.rep_len) : p0;
+        *(uint4 *)(out + p0) = load16u(hay + src);
+      } else if (p0 + 16 <= total && sR[wv][a + 4] > p0 + 15) {
+        uint32_t x[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const uint64_t lc = p0 + i;
+          const uint32_t idx = (sR[wv][a + 1] <= lc) + (sR[wv][a + 2] <= lc) + (sR[wv][a + 3] <= lc);
+          uint8_t ch;
+          if (jj == 0 && idx == 0) {
+            ch = hay[lc];
+          } else {
+            const uint64_t rr = sR[wv][a + idx], off = lc - rr;
+            ch = off < c.rep_len ? c.rep[off] : hay[sE[wv][a + idx] + (off - c.rep_len)];
+          }
+          x[i >> 2] |= (uint32_t)ch << (8 * (i & 3));
+        }
+        *(uint4 *)(out + p0) = make_uint4(x[0], x[1], x[2], x[3]);
+      } else {
+        BlockPlan b;
+        b.h = 0;
+        b.jj = jj;
+        b.fast = false;
+        b.src = 0;
+        copy_block_slow(c, p0, b, out);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
 }
 
@@ -310,10 +572,48 @@ hipError_t launch_replace_plan(const BatchDev &b, const uint64_t *counts, const 
 hipError_t launch_replace_copy(const BatchDev &b, const uint64_t *ooff, const uint64_t *counts, const uint64_t *moff,
                                const uint64_t *m, const int64_t *shift, uint64_t limit, const uint8_t *rep,
                                uint64_t rep_len, uint8_t *out, uint64_t cap, uint64_t total_hint, hipStream_t st,
-                               int cus) {
-  hipLaunchKernelGGL(replace_copy_kernel, dim3(grid_for_items((total_hint + 15) / 16, 256, cus)), dim3(256), 0, st, b,
-                     ooff, counts, moff, m, shift, limit, rep, rep_len, out, cap);
-  return hipGetLastError();
+                               int cus, uint64_t nm) {
+  // total_hint bounds the bytes written (the output is at most the text
+  // plus the replacements, and at most cap)
+  const uint64_t nwin = (total_hint + kWin - 1) / kWin;
+  uint64_t *G = nullptr, *widx = nullptr;
+  hipError_t e = scratch_malloc((void **)&G, std::max<uint64_t>(nm, 1) * 8, st);
+  if (e == hipSuccess) e = scratch_malloc((void **)&widx, (nwin + 2) * 8, st);
+  if (e == hipSuccess && nm == 0) e = hipMemsetAsync(widx, 0, (nwin + 2) * 8, st);
+  if (e == hipSuccess && nm) {
+    hipLaunchKernelGGL(replace_g_kernel, dim3(grid_for_items(nm, 256, cus)), dim3(256), 0, st, b.count, ooff, moff, m,
+                       shift, G);
+    hipLaunchKernelGGL(replace_widx_kernel, dim3(grid_for_items(nwin + 1, 256, cus)), dim3(256), 0, st, b.count, moff,
+                       G, nwin + 1, widx);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) {
+    CopyCtx c;
+    c.bt = b;
+    c.ooff = ooff;
+    c.counts = counts;
+    c.moff = moff;
+    c.m = m;
+    c.G = G;
+    c.widx = widx;
+    c.shift = shift;
+    c.limit = limit;
+    c.rep_len = rep_len;
+    c.total = 0;
+    c.cap = cap;
+    c.rep = rep;
+    if (b.count == 1 && limit == ~0ull && !getenv("RURE_AMD_REPLACE_GENERIC"))
+      hipLaunchKernelGGL(replace_copy1_kernel, dim3(grid_for_items((total_hint + 15) / 16, 256, cus)), dim3(256), 0,
+                         st, c, out);
+    else
+      hipLaunchKernelGGL(replace_copy_kernel,
+                         dim3(grid_for_items((total_hint + 16 * kCopyILP - 1) / (16 * kCopyILP), 256, cus)),
+                         dim3(256), 0, st, c, out);
+    e = hipGetLastError();
+  }
+  for (uint64_t *q : {G, widx})
+    if (q) { hipError_t e2 = scratch_free(q, st); if (e == hipSuccess) e = e2; }
+  return e;
 }
 
 hipError_t launch_split(const BatchDev &b, const uint64_t *counts, const uint64_t *moff, const uint64_t *m,

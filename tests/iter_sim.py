@@ -8,10 +8,13 @@ NONE = None
 
 
 class UnitIter(object):
-    def __init__(self, fwd, rev, t, st, c1, fb=None):
+    def __init__(self, fwd, rev, t, st, c1, fb=None, scan_from=0):
         self.fwd, self.rev, self.t, self.fb = fwd, rev, t, fb
         self.p, self.lm = st
         self.c1 = c1
+        # the first search may scan from here (no match starts in [p, scan_from):
+        # the lexer's hand-over to the tail pass, iter_lex_tail_kernel)
+        self.scan_from = scan_from
         self.ended = False
         self.clean = False
         self.exit = None
@@ -43,9 +46,11 @@ class UnitIter(object):
             self.clean = self.p == self.c1 and self.lm != self.c1
             return None
         snap = (self.p, self.lm)
+        self.p = max(self.p, self.scan_from)
         m = self._iter_next()
         if m is not None and m[0] < self.c1:
             return m
+        self.p, self.lm = snap
         self.ended = True
         self.exit = snap
         self.clean = True

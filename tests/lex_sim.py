@@ -21,7 +21,7 @@ def lex_walk(lex, t, c0, end):
     for bp in range(c0, end, 16):
         kend = min(16, end - bp)
         if any(b >= 0x80 for b in t[bp:bp + kend]):
-            return out, p, lm, True
+            return out, p, lm, True, max(p, fc if fc is not None else c0)
         m = 0
         for k in range(kend):
             s = int(tab[76 * s + t[bp + k]])
@@ -42,7 +42,7 @@ def lex_walk(lex, t, c0, end):
         if A:
             fc = bp + (A.bit_length() - 1) // 2
         cz = zlast
-    return out, p, lm, False
+    return out, p, lm, False, max(p, fc if fc is not None else c0)
 
 
 def lex_unit(tab, fwd, rev, t, c0, c1):
@@ -51,8 +51,8 @@ def lex_unit(tab, fwd, rev, t, c0, c1):
     tail pass's generic cut-bounded iteration from the state it left.
     Returns (matches, exit, clean)."""
     from iter_sim import UnitIter
-    ms, p, lm, _ = lex_walk(tab, t, c0, max(c0, min(c1 - 1, len(t))))
-    it = UnitIter(fwd, rev, t, (p, lm), c1)
+    ms, p, lm, _, fc = lex_walk(tab, t, c0, max(c0, min(c1 - 1, len(t))))
+    it = UnitIter(fwd, rev, t, (p, lm), c1, scan_from=fc)
     while True:
         m = it.next()
         if m is None:
