@@ -631,6 +631,10 @@ __device__ __forceinline__ uint64_t core_scan_one(const SetCoreDev &f, const uin
   // per-lane streams are latency-bound: one round trip per block otherwise).
   // (Tried: 128-byte windows loaded at once, 8 unrolled chunk steps: 1.21 vs
   // 0.79 ms on C4.)
+  // (Tried, round 4: two blocks per round so the blocks alternate between
+  // two registers instead of being moved into place: 0.625 vs 0.590 ms on C4,
+  // VALU 249 M vs 254 M per launch; the kernel waits on its LDS chain, not
+  // on issue. profiles/r04_c4_ab.txt)
   while (!done && at + 16 <= len) {
     uint4 nxt = make_uint4(0, 0, 0, 0);
     if (at + 16 < len) nxt = *(const uint4 *)(base + at + 16);
