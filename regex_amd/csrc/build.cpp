@@ -551,6 +551,12 @@ DevTables *regex_device(rure *re, std::string *err) {
     t.m.suf = LitListDev{base + ls.bytes, (const uint32_t *)(base + ls.off), ls.n, re->xl.suffixes.matcher};
     t.m.lcs = base + o_lcs;
     t.m.lcs_len = (uint32_t)re->xl.suffixes.lcs.size();
+    // no proper prefix of the lcs is also its suffix: its occurrences never
+    // overlap, so the greedy walk of exec.rs:736-741 visits every occurrence
+    const std::string &l = re->xl.suffixes.lcs;
+    bool border = false;
+    for (size_t k = 1; k < l.size() && !border; ++k) border = l.compare(0, k, l, l.size() - k, k) == 0;
+    t.lcs_free = !l.empty() && !border;
   }
   if (re->dfa_ok) {
     const DenseDfa &fw = re->dfwd;

@@ -113,7 +113,57 @@ hipError_t run_dfa_step(int mode, const BatchDev &b, const DevTables &t, void *o
 // DFA would have quit too: the Pike VM answers).
 bool lane_search_ok(const DevTables &t) { return t.mt_lane && (t.m.mt != MT_DFA_SUFFIX || t.has_dfa); }
 
+// DfaSuffix over few long fixed-stride haystacks: the reverse suffix scans
+// cut into units (launch_suffix_long) instead of one lane per haystack; the
+// haystacks where the reference falls back to the forward DFA (None) then
+// take the chunked forward scan.  RURE_AMD_SUFFIX_LONG=0 keeps the lanes.
+bool suffix_long_ok(const BatchDev &b, const DevTables &t, uint64_t *chunk) {
+  if (t.m.mt != MT_DFA_SUFFIX || !t.lcs_free || !t.has_dfa || t.quit_possible || b.offs || b.count == 0 || !t.owner)
+    return false;
+  const char *v = getenv("RURE_AMD_SUFFIX_LONG");
+  if (v && v[0] == '0') return false;
+  const uint64_t span = b.length > b.start ? b.length - b.start : 0;
+  if (b.count >= (uint64_t)t.cus * 16 || (span < (256u << 10) && !(v && v[0] == '2'))) return false;
+  const uint64_t target = (uint64_t)t.cus * 1024;
+  const uint64_t per_h = (target + b.count - 1) / b.count;
+  *chunk = odd_lines(std::max<uint64_t>(v && v[0] == '2' ? 128 : 16u << 10, (span + per_h - 1) / per_h));
+  return true;
+}
+
+hipError_t run_suffix_long(int mode, const BatchDev &b, const DevTables &t, uint64_t chunk, void *out,
+                           hipStream_t st) {
+  uint8_t *status = nullptr;
+  hipError_t e = scratch_malloc((void **)&status, b.count, st);
+  if (e == hipSuccess) e = launch_suffix_long(mode, b, t.m, t.f, t.r, chunk, out, status, st, t.cus);
+  std::vector<uint8_t> hs(b.count);
+  if (e == hipSuccess) e = hipMemcpyAsync(hs.data(), status, b.count, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (status) { hipError_t e2 = scratch_free(status, st); if (e == hipSuccess) e = e2; }
+  if (e != hipSuccess) return e;
+  size_t nf = 0;
+  for (uint8_t x : hs) nf += x == 3;
+  if (!nf) return hipSuccess;
+  // exec.rs:764-769 / 700-709: None -> the forward DFA from the search start
+  std::string err;
+  const FwdDfaDev *iter = iter_device(t.owner, t, &err);
+  if (!iter) return hipErrorInvalidValue;
+  uint64_t fchunk = 0;
+  if (!long_batch(mode, b, t, &fchunk)) fchunk = chunk;
+  const size_t rec = mode == MODE_FIND ? 16 : mode == MODE_SHORTEST ? 8 : 1;
+  if (nf == b.count) return launch_long_scan(mode, b, *iter, t.r, fchunk, out, st, t.cus);
+  void *tmp = nullptr;
+  e = scratch_malloc(&tmp, b.count * rec, st);
+  if (e == hipSuccess) e = launch_long_scan(mode, b, *iter, t.r, fchunk, tmp, st, t.cus);
+  for (size_t h = 0; e == hipSuccess && h < b.count; ++h)
+    if (hs[h] == 3)
+      e = hipMemcpyAsync((uint8_t *)out + h * rec, (uint8_t *)tmp + h * rec, rec, hipMemcpyDeviceToDevice, st);
+  if (tmp) { hipError_t e2 = scratch_free(tmp, st); if (e == hipSuccess) e = e2; }
+  return e;
+}
+
 hipError_t run_lane_search(int mode, const BatchDev &b, const DevTables &t, void *out, hipStream_t st) {
+  uint64_t chunk = 0;
+  if (suffix_long_ok(b, t, &chunk)) return run_suffix_long(mode, b, t, chunk, out, st);
   if (!t.quit_possible || t.m.mt != MT_DFA_SUFFIX) return launch_lane_search(mode, b, t.m, t.f, t.r, out, st, t.cus);
   BatchDev bq = b;  // quit flag: see run_regex
   hipError_t e = scratch_malloc((void **)&bq.quit_flag, 4, st);

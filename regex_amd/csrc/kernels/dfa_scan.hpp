@@ -310,6 +310,13 @@ hipError_t launch_dfa_fwd(int mode, const BatchDev &b, const FwdDfaDev &f, const
 // last_fwd_path() = -5.
 hipError_t launch_lane_search(int mode, const BatchDev &b, const MatchDev &m, const FwdDfaDev &f,
                               const RevDfaDev &r, void *out, hipStream_t st, int cus);
+// DfaSuffix over few long fixed-stride haystacks (match_types.hip): answers
+// into out where the reverse suffix scans decide; status[h] = 3 where the
+// reference falls back to the forward DFA (the caller runs it).  Needs a
+// longest common suffix that cannot overlap itself.
+hipError_t launch_suffix_long(int mode, const BatchDev &b, const MatchDev &m, const FwdDfaDev &f,
+                              const RevDfaDev &r, uint64_t chunk, void *out, uint8_t *status, hipStream_t st,
+                              int cus);
 // MatchType::Literal (exec.rs:601-625, 1148-1166) for MODE_FIND / MODE_ISMATCH
 // batches of a regex that is a finite string set: f = the find_iter DFA
 // (lit_n > 0); same output layout as launch_dfa_fwd; last_fwd_path() = -3.

@@ -95,6 +95,7 @@ struct DevTables {
   // iteration with `m`.
   MatchDev m{-1, {}, {}, nullptr, 0};
   bool mt_lane = false;
+  bool lcs_free = false;    // DfaSuffix: the longest common suffix cannot overlap itself (launch_suffix_long)
   int cus = 256;
 };
 
@@ -344,6 +345,9 @@ bool long_batch(int mode, const BatchDev &b, const DevTables &t, uint64_t *chunk
 hipError_t run_dfa_step(int mode, const BatchDev &b, const DevTables &t, void *out, hipStream_t st, int dfa_grid,
                         const FwdDfaDev *iter);
 bool lane_search_ok(const DevTables &t);
+bool suffix_long_ok(const BatchDev &b, const DevTables &t, uint64_t *chunk);
+hipError_t run_suffix_long(int mode, const BatchDev &b, const DevTables &t, uint64_t chunk, void *out,
+                           hipStream_t st);
 hipError_t run_lane_search(int mode, const BatchDev &b, const DevTables &t, void *out, hipStream_t st);
 bool big_batch(const BatchDev &b, const DevTables &t);
 hipError_t run_regex(int mode, const BatchDev &b, const DevTables &t, void *out, hipStream_t st, int dfa_grid,
