@@ -319,6 +319,13 @@ int rure_amd_first_byte_export(rure *re, uint8_t *bytes);
  * that byte).  Returns the table's size in bytes (0: no lexer table), copies
  * at most `cap`. */
 int64_t rure_amd_lex_export(rure *re, uint8_t *table, size_t cap, uint32_t *s0);
+/* The same lexer four bytes per step (host only): kLex4Bytes = 5120 bytes,
+ * next row at [256 row + c] where c packs four byte classes (2 bits each,
+ * byte j at bits 2j; class 3 = no byte), the four bytes' codes (2 bits each)
+ * at [2048 + 256 row + c], byte -> class << 2j at [4096 + 256 j + b];
+ * *s0 = the start row.  Returns the size (0: the lexer does not fit: more
+ * than 8 rows or 3 ASCII byte classes, or no lexer table). */
+int64_t rure_amd_lex4_export(rure *re, uint8_t *table, size_t cap, uint32_t *s0);
 
 /* Export of the Pike VM closure tables the NFA kernel runs (host only):
  * leaves = 3 u32 per leaf (kind | lo << 8 | hi << 16, closure, slot),

@@ -612,6 +612,18 @@ class Regex(object):
         N.rure_amd_lex_export(self._re, t.ctypes.data, n, ctypes.byref(s0))
         return t, s0.value
 
+    def lex4_table(self):
+        """The four-bytes-per-step lexer table (rure_amd_lex4_export): (flat
+        uint8 table, start row), or None."""
+        import numpy as np
+        n = N.rure_amd_lex4_export(self._re, None, 0, None)
+        if n <= 0:
+            return None
+        t = np.zeros(n, dtype=np.uint8)
+        s0 = ctypes.c_uint32()
+        N.rure_amd_lex4_export(self._re, t.ctypes.data, n, ctypes.byref(s0))
+        return t, s0.value
+
     def program(self, which):
         """Compiled byte program (0 fwd DFA, 1 reverse DFA, 2 NFA): (info, insts)."""
         return _export(N.rure_amd_program_export, self._re, which)

@@ -838,6 +838,68 @@ bool build_lex(const DenseDfa &d, uint32_t ustart1, uint32_t fb_n, std::vector<u
   return true;
 }
 
+// The lexer four bytes per step (FwdDfaDev::lex4_image): the byte table's
+// entries reachable from S0 over ASCII become rows (at most kLex4Rows), the
+// ASCII bytes fall into at most 3 classes (bytes with equal columns in every
+// row), and a row's entry for four classes is the byte table walked over one
+// byte of each; class 3 walks nothing (flags 0), so a partial word's tail
+// leaves the state alone as lex16<false> does.  Bytes >= 0x80 never reach
+// the lexer (their blocks are the tail pass's).  Returns false when the
+// table does not fit.
+bool build_lex4(const std::vector<uint8_t> &img, uint32_t s0, std::vector<uint8_t> *out, uint32_t *s0_row) {
+  out->clear();
+  if (img.empty()) return false;
+  auto at = [&](uint32_t e, uint32_t c) -> uint32_t {
+    const size_t i = (size_t)e * kLexUnit + c;
+    return i < img.size() ? img[i] : 0;
+  };
+  std::vector<uint32_t> rows{s0};
+  std::vector<int> row_of(256, -1);
+  row_of[s0] = 0;
+  for (size_t i = 0; i < rows.size(); ++i)
+    for (uint32_t c = 0; c < 128; ++c) {
+      const uint32_t t = at(rows[i], c);
+      if (row_of[t] < 0) {
+        if (rows.size() == kLex4Rows) return false;
+        row_of[t] = (int)rows.size();
+        rows.push_back(t);
+      }
+    }
+  uint8_t cls[256] = {0};
+  std::vector<uint32_t> rep;  // a byte of each class
+  for (uint32_t c = 0; c < 128; ++c) {
+    int k = -1;
+    for (size_t j = 0; j < rep.size() && k < 0; ++j) {
+      bool same = true;
+      for (uint32_t e : rows) same = same && at(e, c) == at(e, rep[j]);
+      if (same) k = (int)j;
+    }
+    if (k < 0) {
+      if (rep.size() == 3) return false;
+      k = (int)rep.size();
+      rep.push_back(c);
+    }
+    cls[c] = (uint8_t)k;
+  }
+  out->assign(kLex4Bytes, 0);
+  for (size_t r = 0; r < rows.size(); ++r)
+    for (uint32_t c = 0; c < 256; ++c) {
+      uint32_t e = rows[r], fl = 0;
+      for (uint32_t k = 0; k < 4; ++k) {
+        const uint32_t ck = (c >> (2 * k)) & 3;
+        if (ck == 3 || ck >= rep.size()) continue;
+        e = at(e, rep[ck]);
+        fl |= (e & 3) << (2 * k);
+      }
+      (*out)[r * 256 + c] = (uint8_t)row_of[e];
+      (*out)[kLex4Flags + r * 256 + c] = (uint8_t)fl;
+    }
+  for (uint32_t j = 0; j < 4; ++j)
+    for (uint32_t c = 0; c < 256; ++c) (*out)[kLex4Cls + 256 * j + c] = (uint8_t)(cls[c] << (2 * j));
+  *s0_row = 0;
+  return true;
+}
+
 bool build_iter_dfa(rure *re) {
   if (!build_regex_dfas(re)) return false;
   std::lock_guard<std::mutex> g(re->mu);
@@ -851,7 +913,8 @@ bool build_iter_dfa(rure *re) {
     re->lits_done = true;
     if (re->iter_ok)
       re->fb_n = first_byte_rule(re->dfwd_iter, re->pf_iter.ustart1, !can_match_empty(re->nfa), re->fb_bytes);
-    if (re->iter_ok) build_lex(re->dfwd_iter, re->pf_iter.ustart1, re->fb_n, &re->lex, &re->lex_s0);
+    if (re->iter_ok && build_lex(re->dfwd_iter, re->pf_iter.ustart1, re->fb_n, &re->lex, &re->lex_s0))
+      build_lex4(re->lex, re->lex_s0, &re->lex4, &re->lex4_s0);
   }
   return re->iter_ok;
 }
@@ -957,6 +1020,7 @@ const FwdDfaDev *iter_device(rure *re, const DevTables &t, std::string *err) {
   if (re->lit_ok) build_shiftand(re->lits, &sa_img, &sa_init, &sa_final, &sa_len, &sa_bits);
   size_t o_sa = sa_img.empty() ? 0 : b.add(sa_img.data(), sa_img.size() * 8);
   size_t o_lex = re->lex.empty() ? 0 : b.add(re->lex.data(), re->lex.size());
+  size_t o_lex4 = re->lex4.empty() ? 0 : b.add(re->lex4.data(), re->lex4.size());
   DevTables tmp;
   if (!upload_blob(b, &tmp, err)) return nullptr;
   uint8_t *base = (uint8_t *)tmp.blob;
@@ -995,6 +1059,11 @@ const FwdDfaDev *iter_device(rure *re, const DevTables &t, std::string *err) {
     f.lex_image = base + o_lex;
     f.lex_bytes = (uint32_t)re->lex.size();
     f.lex_s0 = re->lex_s0;
+  }
+  // RURE_AMD_LEX4=0 keeps the byte-per-step lexer (A/B)
+  if (!re->lex4.empty() && !(getenv("RURE_AMD_LEX4") && getenv("RURE_AMD_LEX4")[0] == '0')) {
+    f.lex4_image = base + o_lex4;
+    f.lex4_s0 = re->lex4_s0;
   }
   if (!sa_img.empty()) {
     f.sa_image = (const uint64_t *)(base + o_sa);

@@ -813,6 +813,14 @@ int64_t rure_amd_lex_export(rure *re, uint8_t *table, size_t cap, uint32_t *s0) 
   return (int64_t)re->lex.size();
 }
 
+int64_t rure_amd_lex4_export(rure *re, uint8_t *table, size_t cap, uint32_t *s0) {
+  if (!re) return RURE_AMD_ERR_ARG;
+  if (!build_iter_dfa(re)) return RURE_AMD_ERR_DFA;
+  if (table) memcpy(table, re->lex4.data(), std::min(cap, re->lex4.size()));
+  if (s0) *s0 = re->lex4_s0;
+  return (int64_t)re->lex4.size();
+}
+
 int rure_amd_first_byte_export(rure *re, uint8_t *bytes) {
   if (!re) return RURE_AMD_ERR_ARG;
   if (!build_iter_dfa(re)) return RURE_AMD_ERR_DFA;

@@ -88,6 +88,14 @@ struct FwdDfaDev {
   // match ended at it (EMIT), 3 = EMIT only.
   const uint8_t *lex_image;
   uint32_t lex_bytes, lex_s0;
+  // The same lexer four bytes per step (host build_lex4; lex4_image null:
+  // none): at most kLex4Rows rows and 3 byte classes over ASCII, class 3 =
+  // "no byte" (a partial word's tail).  kLex4Bytes of LDS: next row at
+  // [row * 256 + c] (c = the four bytes' classes, 2 bits each), the four
+  // bytes' flags (2 bits each, codes as above) at kLex4Flags + the same
+  // index, and four byte -> class << 2j tables at kLex4Cls + 256 j.
+  const uint8_t *lex4_image;
+  uint32_t lex4_s0;
   // The start-state prefix skip (dfa.rs:700-711, 1504-1506 prefix_at): when
   // the regex has prefix literals (literal_sets.hpp, dfa.prefixes) whose
   // first bytes are at most 4 (pfx_rep[i] = byte * 0x01010101), every match
@@ -100,6 +108,8 @@ struct FwdDfaDev {
 constexpr uint32_t kLexMaxRows = 24;  // lexer table rows (iter_spec_lex_tile_kernel's static LDS)
 constexpr uint32_t kLexUnit = kRow / 4;  // lexer entry -> row address multiplier
 constexpr uint32_t kLexBytes = (kLexMaxRows * kRow + 3 * kLexUnit + 15) & ~15u;  // largest lexer image
+constexpr uint32_t kLex4Rows = 8, kLex4Flags = kLex4Rows * 256, kLex4Cls = 2 * kLex4Flags;
+constexpr uint32_t kLex4Bytes = kLex4Cls + 4 * 256;
 
 // Literal engine image layout (at most kLitMax literals of kLitLen bytes).
 constexpr uint32_t kLitMax = 64, kLitLen = 32;

@@ -51,7 +51,7 @@ enum : uint32_t {
   U_COPY = 16,        // fixed, and its matches are slots[skip, skip + count)
   U_LEX_TAIL = 32,    // iter_spec_lex_tile_kernel: exit = the lexer's iteration state, the tail pass finishes
   U_COMPACT = 64,     // the lexer's slots: its pad (= its count) records as u32 start - c0 | end - c0 << 16,
-                      // then the tail pass's as absolute ulonglong2 from the back of the slot area
+                      // then the tail pass's as absolute ulonglong2 from the back (lex_rec32 / lex_row16)
 };
 
 struct IterSt {
@@ -71,19 +71,33 @@ struct Geo {  // unit -> (haystack, chunk) for fixed-stride batches
   uint32_t slots;   // speculative matches stored per unit
 };
 
+// U_COMPACT slots are interleaved over the 64 units of a lexer wave (their
+// slot areas together, g.slots rows of 64 x 16 bytes): row k holds lexer
+// records 4k..4k+3 of every unit, lane by lane, so the lexer's per-tile row
+// stores write a few whole 1 KiB rows instead of 64 scattered partial lines
+// (the scattered layout left ~33 MB of partly written lines in flight,
+// more than L2).  The tail pass's records take rows from the back.
+// lex_rec32: u32 index of lexer record i of unit u; lex_row16: ulonglong2
+// index of unit u's 16 bytes in row k.
+__device__ __forceinline__ uint64_t lex_rec32(const Geo &g, uint64_t u, uint32_t i) {
+  return (u >> 6) * 256 * (uint64_t)g.slots + (uint64_t)(i >> 2) * 256 + (u & 63) * 4 + (i & 3);
+}
+__device__ __forceinline__ uint64_t lex_row16(const Geo &g, uint64_t u, uint32_t k) {
+  return (u >> 6) * 64 * (uint64_t)g.slots + (uint64_t)k * 64 + (u & 63);
+}
+
 // Speculative record i of unit u (U_COMPACT: the first nlex as u16 pairs
-// relative to c0, the rest absolute from the back of the unit's slots).
+// relative to c0, the rest absolute from the back rows).
 __device__ __forceinline__ ulonglong2 slot_rec(const uint64_t *slots, const Geo &g, uint64_t u, uint32_t i,
                                                bool compact, uint64_t c0, uint32_t nlex) {
-  const ulonglong2 *r16 = (const ulonglong2 *)(slots + u * g.slots * 2);
   if (compact) {
     if (i < nlex) {
-      const uint32_t v = ((const uint32_t *)r16)[i];
+      const uint32_t v = ((const uint32_t *)slots)[lex_rec32(g, u, i)];
       return make_ulonglong2(c0 + (v & 0xFFFFu), c0 + (v >> 16));
     }
-    return r16[g.slots - 1 - (i - nlex)];
+    return ((const ulonglong2 *)slots)[lex_row16(g, u, g.slots - 1 - (i - nlex))];
   }
-  return r16[i];
+  return ((const ulonglong2 *)(slots + u * g.slots * 2))[i];
 }
 
 __device__ __forceinline__ void unit_bounds(const BatchDev &b, const Geo &g, uint64_t u, uint64_t *h,
@@ -1226,32 +1240,72 @@ __device__ __forceinline__ uint32_t lex16(uint32_t &s, const uint32_t w[4], cons
   return m;
 }
 
-// The lexer's matches go to the unit's slots as u32 (start - c0 | end - c0 <<
-// 16) records (U_COMPACT) through a queue of four in registers, flushed once
-// per tile with one 16-byte store whatever it holds (LexQueue::flush): no store
-// in the block loop depends on the data, so the wait for the next tile's
-// loads counts a fixed number of younger stores.  A store whose count
-// depends on the data (one per match) made the compiler drain every store
-// before each tile's loads could be used (s_waitcnt vmcnt(0)): the kernel
-// ran 0.96 ms with them against 0.61 ms without (tools/lex_time.py A/B).
-// A fifth match in one tile flushes early, then waits for its stores.
-struct LexQueue {
-  uint32_t q0, q1, q2, q3;  // start | end << 16 (units of at most 64 KiB)
-  uint32_t qc, nf;          // queued; records flushed (written at [nf, nf + 4))
-  __device__ __forceinline__ void flush(uint32_t *dst, uint32_t cap4) {
-    *(uint4 *)(dst + min(nf, cap4 - 4)) = make_uint4(q0, q1, q2, q3);  // past the slots: a re-run unit, slots unread
-    nf += qc;
-    qc = 0;
+// lex16 four bytes per step (FwdDfaDev::lex4_image, host build_lex4): per
+// 4-byte word four independent class lookups (off the chain), then one
+// dependent LDS read for the next row and one for the four bytes' flags.
+// The chain is a quarter as long and the VALU per byte halves (the byte
+// lexer: byte extract, 24-bit multiply-add, flag shift and mask per byte).
+// s is a row number here.  FULL = false: bytes from kend on take class 3
+// (no byte: state kept, no flags).
+template <bool FULL>
+__device__ __forceinline__ uint32_t lex16x4(uint32_t &s, const uint32_t w[4], const uint8_t *tab, uint32_t kend) {
+  uint32_t c[4];
+#pragma unroll
+  for (uint32_t j = 0; j < 4; ++j) {
+    const uint32_t x = w[j];
+    c[j] = tab[kLex4Cls + (x & 0xFF)] | tab[kLex4Cls + 256 + ((x >> 8) & 0xFF)] |
+           tab[kLex4Cls + 512 + ((x >> 16) & 0xFF)] | tab[kLex4Cls + 768 + (x >> 24)];
+    if (!FULL) {
+      const uint32_t k0 = 4 * j;  // bytes [max(kend, k0), k0 + 4) of this word are absent
+      c[j] |= kend <= k0 ? 0xFFu : kend >= k0 + 4 ? 0u : (0xFFu << (2 * (kend - k0))) & 0xFFu;
+    }
   }
-  __device__ __forceinline__ void push(uint32_t r, uint32_t *dst, uint32_t cap4) {
-    if (qc == 4) {
-      flush(dst, cap4);
+  uint32_t m = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < 4; ++j) {
+    const uint32_t a = (s << 8) | c[j];
+    s = tab[a];
+    m |= (uint32_t)tab[kLex4Flags + a] << (8 * j);
+  }
+  return m;
+}
+
+// The lexer's matches go to the unit's slots as u32 (start - c0 | end - c0 <<
+// 16) records (U_COMPACT, interleaved rows: lex_rec32) through a queue of
+// eight in registers: q0..q3 = the row being filled, q4..q7 the next.  Once
+// per tile one 16-byte store writes the row whatever it holds
+// (LexQueue::flush) and a full row gives way to the next: no store in the
+// block loop depends on the data, so the wait for the next tile's loads
+// counts a fixed number of younger stores.  A store whose count depends on
+// the data (one per match) made the compiler drain every store before each
+// tile's loads could be used (s_waitcnt vmcnt(0)): the kernel ran 0.96 ms
+// with them against 0.61 ms without (tools/lex_time.py A/B).  A ninth
+// queued match flushes early, then waits for its stores.
+struct LexQueue {
+  uint32_t q0, q1, q2, q3, q4, q5, q6, q7;  // start | end << 16 (units of at most 64 KiB)
+  uint32_t qc, row;                         // queued; the row q0..q3 belong to
+  __device__ __forceinline__ void flush(uint32_t *dst, uint32_t rows) {
+    // past the slots: a re-run unit, slots unread
+    *(uint4 *)(dst + 256 * min(row, rows - 1)) = make_uint4(q0, q1, q2, q3);
+    if (qc >= 4) {
+      q0 = q4; q1 = q5; q2 = q6; q3 = q7;
+      qc -= 4;
+      ++row;
+    }
+  }
+  __device__ __forceinline__ void push(uint32_t r, uint32_t *dst, uint32_t rows) {
+    if (qc == 8) {
+      flush(dst, rows);
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the tile's store count stays fixed
     }
     q0 = qc == 0 ? r : q0;
     q1 = qc == 1 ? r : q1;
     q2 = qc == 2 ? r : q2;
     q3 = qc == 3 ? r : q3;
+    q4 = qc == 4 ? r : q4;
+    q5 = qc == 5 ? r : q5;
+    q6 = qc == 6 ? r : q6;
+    q7 = qc == 7 ? r : q7;
     ++qc;
   }
 };
@@ -1282,21 +1336,29 @@ __device__ __forceinline__ void lex_events(uint32_t m, uint32_t bp, uint32_t &cz
   cz = (Z >> 30) & 1u;
 }
 
-__global__ __launch_bounds__(256) void iter_spec_lex_tile_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f,
+// X4: the four-bytes-per-step table (lex16x4); else one byte per step.
+// SINGLE: one haystack (the tile's eight source lines are one base plus
+// multiples of 8 chunks: two registers instead of eight 64-bit pointers,
+// which keeps X4 within the 128 VGPRs of 4 waves per SIMD).
+template <bool X4, bool SINGLE>
+__global__ __launch_bounds__(256, 4) void iter_spec_lex_tile_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f,
                                                                  Unit *units, uint64_t *slots, uint32_t *counts) {
-  // the chain's address is one 24-bit multiply-add; 24 rows + the tile stage
-  // = 39.5 KB, 4 blocks (16 waves) per CU
-  __shared__ __attribute__((aligned(16))) uint8_t tab[kLexBytes];
+  // the byte chain's address is one 24-bit multiply-add; 24 rows + the tile
+  // stage = 39.5 KB (X4: 5 KB + the stage), 4 blocks (16 waves) per CU
+  __shared__ __attribute__((aligned(16))) uint8_t tab[X4 ? kLex4Bytes : kLexBytes];
   __shared__ __attribute__((aligned(16))) uint4 stage[4][64 * 8];
-  for (uint32_t i = threadIdx.x * 16; i < f.lex_bytes; i += blockDim.x * 16)
-    *(uint4 *)(tab + i) = *(const uint4 *)(f.lex_image + i);
+  {
+    const uint8_t *img = X4 ? f.lex4_image : f.lex_image;
+    const uint32_t nb = X4 ? kLex4Bytes : f.lex_bytes;
+    for (uint32_t i = threadIdx.x * 16; i < nb; i += blockDim.x * 16) *(uint4 *)(tab + i) = *(const uint4 *)(img + i);
+  }
   __syncthreads();
   const uint64_t C = g.chunk, nk = g.nk;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   uint4 *buf = stage[w];
   const int src_h = lane >> 3, src_seg = lane & 7, sw = (lane >> 1) & 7;
   const uint64_t ngroups = (nunits + 63) / 64, nwaves = (uint64_t)gridDim.x * 4;
-  const bool single = b.count == 1;
+  const bool single = SINGLE;
   // the last readable 16-byte block of the batch (ragged last units' tiles
   // are clamped to it; their bytes past the haystack are ignored)
   const uint8_t *last_blk = b.hay + (b.count - 1) * b.stride + ((b.length + 15) & ~(uint64_t)15) - 16;
@@ -1308,31 +1370,35 @@ __global__ __launch_bounds__(256) void iter_spec_lex_tile_kernel(BatchDev b, Geo
     uint64_t h, k;
     hk(u, h, k);
     const bool valid = u < nunits;
-    const uint8_t *src[8];
+    const uint8_t *src[SINGLE ? 1 : 8];
+    if (SINGLE) {
+      src[0] = b.hay + b.start + (gi * 64 + src_h) * C + 16 * src_seg;
+    } else {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      uint64_t us = gi * 64 + 8 * j + src_h, hs, ks;
-      hk(us, hs, ks);
-      if (us >= nunits) hs = ks = 0;  // absent units re-read unit 0
-      src[j] = b.hay + hs * b.stride + b.start + ks * C + 16 * src_seg;
+      for (int j = 0; j < 8; ++j) {
+        uint64_t us = gi * 64 + 8 * j + src_h, hs, ks;
+        hk(us, hs, ks);
+        if (us >= nunits) hs = ks = 0;  // absent units re-read unit 0
+        src[j] = b.hay + hs * b.stride + b.start + ks * C + 16 * src_seg;
+      }
     }
     const uint64_t len = b.length, c0 = b.start + k * C;
     const uint64_t c1 = k + 1 == nk ? g.end : c0 + C;
     // the lexer covers [c0, lim): the byte at c1 - 1 (where the search is cut)
     // and the end of the text are left to the tail pass
     const uint64_t lim = valid ? min(c1 - 1, len) : c0;
-    // compact records: four per slot of the unit's slot bytes (the queue's
-    // flush may write four past the last record)
-    uint32_t *const dst = (uint32_t *)(slots + u * g.slots * 2);
-    const uint32_t cap4 = 4 * g.slots;
+    // compact records: four per row (lex_rec32; the queue's row stores
+    // write whole rows)
+    uint32_t *const dst = (uint32_t *)slots + lex_rec32(g, u, 0);
+    const uint32_t cap4 = g.slots;  // rows
     LexQueue Q;
-    Q.q0 = Q.q1 = Q.q2 = Q.q3 = 0;
-    Q.qc = Q.nf = 0;
+    Q.q0 = Q.q1 = Q.q2 = Q.q3 = Q.q4 = Q.q5 = Q.q6 = Q.q7 = 0;
+    Q.qc = Q.row = 0;
     uint32_t fc = 0, last = 0;  // relative to c0 (lex_events)
-    uint32_t n = 0, s = f.lex_s0, cz = 1;
+    uint32_t n = 0, s = X4 ? f.lex4_s0 : f.lex_s0, cz = 1;
     bool frozen = false;  // a byte >= 0x80 was seen: the rest is the tail pass's
     uint4 n0, n1, n2, n3, n4, n5, n6, n7;
-#define RURE_LD(j, a) (*(const uint4 *)min(src[j] + (a), last_blk))
+#define RURE_LD(j, a) (*(const uint4 *)min((SINGLE ? src[0] + (j) * 8 * C : src[j]) + (a), last_blk))
 #define RURE_LOAD_TILE(a)                                                                                     \
   n0 = RURE_LD(0, a); n1 = RURE_LD(1, a); n2 = RURE_LD(2, a); n3 = RURE_LD(3, a);                            \
   n4 = RURE_LD(4, a); n5 = RURE_LD(5, a); n6 = RURE_LD(6, a); n7 = RURE_LD(7, a);
@@ -1366,7 +1432,7 @@ __global__ __launch_bounds__(256) void iter_spec_lex_tile_kernel(BatchDev b, Geo
           frozen = frozen || hi8;
           mw[m] = 0;
           if (!frozen) {
-            mw[m] = lex16<true>(s, wd, tab, 16);
+            mw[m] = X4 ? lex16x4<true>(s, wd, tab, 16) : lex16<true>(s, wd, tab, 16);
             act += 16;
           }
         }
@@ -1383,7 +1449,8 @@ __global__ __launch_bounds__(256) void iter_spec_lex_tile_kernel(BatchDev b, Geo
           frozen = frozen || (hi8 & 0x80808080u);
           mw[m] = 0;
           if (!frozen && kend) {
-            mw[m] = kend == 16 ? lex16<true>(s, wd, tab, 16) : lex16<false>(s, wd, tab, kend);
+            if (X4) mw[m] = kend == 16 ? lex16x4<true>(s, wd, tab, 16) : lex16x4<false>(s, wd, tab, kend);
+            else mw[m] = kend == 16 ? lex16<true>(s, wd, tab, 16) : lex16<false>(s, wd, tab, kend);
             act += kend;
           }
         }
@@ -1401,6 +1468,7 @@ __global__ __launch_bounds__(256) void iter_spec_lex_tile_kernel(BatchDev b, Geo
 #undef RURE_LD
 #undef RURE_LOAD_TILE
 #undef RURE_STAGE
+    if (Q.qc) Q.flush(dst, cap4);  // the next row's records (q4..q7 became q0..q3)
     if (!valid) continue;
     // (clean flags and counts only matter when the tail pass is skipped,
     // RURE_AMD_LEX_TAIL=0: a diagnostic that leaves the lexer's matches alone)
@@ -1444,9 +1512,9 @@ __global__ __launch_bounds__(256) void iter_lex_tail_kernel(BatchDev b, Geo g, u
     const bool compact = (U.flags & U_COMPACT) != 0;
     while (it.next(f, r, lds, rlds, base, len, &ms, &me)) {
       if (n < g.slots) {
-        // compact units: absolute records from the back (slot_rec)
-        const uint64_t k = compact ? g.slots - 1 - (n - U.pad) : n;
-        *(ulonglong2 *)&slots[(u * g.slots + k) * 2] = make_ulonglong2(ms, me);
+        // compact units: absolute records from the back rows (slot_rec)
+        const uint64_t k = compact ? lex_row16(g, u, g.slots - 1 - (n - U.pad)) : u * g.slots + n;
+        ((ulonglong2 *)slots)[k] = make_ulonglong2(ms, me);
       }
       ++n;
     }
@@ -1777,10 +1845,12 @@ __device__ __forceinline__ void emit_body(const BatchDev &b, const Geo &g, uint6
     // compact units: the record base (c0) rides along (~0 marks u64 records),
     // the lexer's records are u32 from the unit's slot start, the tail's u64
     // from its end
-    const uint64_t wcb = compact ? cbase : ~0ull, wsrc32 = u * g.slots * 4 + skip;
+    // (lex_rec32 / lex_row16 rows: the unit's u32 base and its last row)
+    const uint64_t wcb = compact ? cbase : ~0ull, wsrc32 = (u >> 6) * 256 * (uint64_t)g.slots + (u & 63) * 4;
     const uint64_t wlex = compact ? (nlex > skip ? nlex - skip : 0) : 0;
-    const uint64_t wend = (u * g.slots + g.slots - 1) * 2;  // u64 index of the unit's last slot
+    const uint64_t wend = compact ? 2 * lex_row16(g, u, g.slots - 1) : 0;  // u64 index of the unit's last row
     const uint64_t wtail0 = compact && skip > nlex ? skip - nlex : 0;
+    const uint64_t wskip = skip;
     const uint64_t busy = __ballot(wrec != 0);
     const bool a16 = ((uintptr_t)out & 15) == 0;
 #pragma unroll 1
@@ -1790,6 +1860,7 @@ __device__ __forceinline__ void emit_body(const BatchDev &b, const Geo &g, uint6
       const uint64_t cu = __shfl(wrec, ul), su = __shfl(wsrc, ul), du = __shfl(wdst, ul);
       const uint64_t cb = __shfl(wcb, ul), su32 = __shfl(wsrc32, ul);
       const uint64_t nl = __shfl(wlex, ul), se = __shfl(wend, ul), t0 = __shfl(wtail0, ul);
+      const uint64_t sk = __shfl(wskip, ul);
       uint64_t mx = cu;
       mx = max(mx, (uint64_t)__shfl_xor(mx, 8));
       mx = max(mx, (uint64_t)__shfl_xor(mx, 16));
@@ -1805,10 +1876,11 @@ __device__ __forceinline__ void emit_body(const BatchDev &b, const Geo &g, uint6
             const uint64_t j = i + 8 * t;
             if (j < cu) {
               if (j < nl) {
-                const uint32_t r = src32[j];
+                const uint64_t ii = sk + j;
+                const uint32_t r = src32[(ii >> 2) * 256 + (ii & 3)];
                 v[t] = make_ulonglong2(cb + (r & 0xFFFFu), cb + (r >> 16));
-              } else {  // the tail pass's records, backwards from the last slot
-                v[t] = *(const ulonglong2 *)(slots + se - 2 * (t0 + j - nl));
+              } else {  // the tail pass's records, backwards from the last row
+                v[t] = *(const ulonglong2 *)(slots + se - 128 * (t0 + j - nl));
               }
             }
           }
@@ -2587,8 +2659,20 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
                            g.chunk <= 65536;
       ktimer_begin(st);  // bench diagnostics: the speculative kernel's duration
       if (use_lex) {
-        hipLaunchKernelGGL(iter_spec_lex_tile_kernel, dim3(grid_cap((nunits + 63) / 64, 4, cus, 4)), dim3(256), 0,
-                           st, b, g, nunits, *f, units, slots, counts);
+        const dim3 lg(grid_cap((nunits + 63) / 64, 4, cus, 4));
+        const bool one = b.count == 1;
+        if (f->lex4_image && one)
+          hipLaunchKernelGGL((iter_spec_lex_tile_kernel<true, true>), lg, dim3(256), 0, st, b, g, nunits, *f, units,
+                             slots, counts);
+        else if (f->lex4_image)
+          hipLaunchKernelGGL((iter_spec_lex_tile_kernel<true, false>), lg, dim3(256), 0, st, b, g, nunits, *f, units,
+                             slots, counts);
+        else if (one)
+          hipLaunchKernelGGL((iter_spec_lex_tile_kernel<false, true>), lg, dim3(256), 0, st, b, g, nunits, *f, units,
+                             slots, counts);
+        else
+          hipLaunchKernelGGL((iter_spec_lex_tile_kernel<false, false>), lg, dim3(256), 0, st, b, g, nunits, *f, units,
+                             slots, counts);
         ktimer_end(st);
         if ((e = hipGetLastError()) != hipSuccess) break;
         if ((e = allow_lds(iter_lex_tail_kernel, lb)) != hipSuccess) break;

@@ -250,6 +250,8 @@ struct rure {
   uint8_t fb_bytes[4] = {0, 0, 0, 0};
   std::vector<uint8_t> lex;   // lexer table (build_lex), empty if none
   uint32_t lex_s0 = 0;
+  std::vector<uint8_t> lex4;  // four-byte lexer table (build_lex4), empty if none
+  uint32_t lex4_s0 = 0;
   LiteralSet lits;
   std::map<int, std::pair<void *, FwdDfaDev>> iter_dev;
 };
@@ -329,6 +331,7 @@ DevTables *regex_device(rure *re, std::string *err);
 bool big_device(const DevTables &tc);
 DevTables *set_device(rure_set *rs, std::string *err);
 uint32_t first_byte_rule(const DenseDfa &d, uint32_t ustart1, bool nonempty, uint8_t bytes[4]);
+bool build_lex4(const std::vector<uint8_t> &img, uint32_t s0, std::vector<uint8_t> *out, uint32_t *s0_row);
 bool build_lex(const DenseDfa &d, uint32_t ustart1, uint32_t fb_n, std::vector<uint8_t> *img,
                       uint32_t *s0_idx);
 bool build_iter_dfa(rure *re);

@@ -6,6 +6,36 @@ TEST INFRASTRUCTURE: validates the lexer algorithm on CPU."""
 NONE = None
 
 
+def lex16(lex, s, blk, kend):
+    """One 16-byte block on the byte table (iter_scan.hip lex16): returns the
+    flag word (2 bits per byte) and the entry after the block."""
+    tab, _ = lex
+    m = 0
+    for k in range(kend):
+        s = int(tab[76 * s + blk[k]])
+        m |= (s & 3) << (2 * k)
+    return m, s
+
+
+LEX4_FLAGS, LEX4_CLS = 2048, 4096  # dfa_scan.hpp kLex4Flags, kLex4Cls
+
+
+def lex16x4(lex4, s, blk, kend):
+    """The same block four bytes per step (iter_scan.hip lex16x4, host
+    build_lex4): s is a row; bytes from kend on take class 3 (no byte)."""
+    tab, _ = lex4
+    m = 0
+    for j in range(4):
+        c = 0
+        for k in range(4):
+            i = 4 * j + k
+            c |= 3 << (2 * k) if i >= kend else int(tab[LEX4_CLS + 256 * k + blk[i]])
+        a = (s << 8) | c
+        m |= int(tab[LEX4_FLAGS + a]) << (8 * j)
+        s = int(tab[a])
+    return m, s
+
+
 def lex_walk(lex, t, c0, end):
     """Walk text[c0, end) from the start state as the kernel does, block by
     block (16-byte blocks aligned to c0 here).  A block holding a byte >= 0x80
@@ -22,10 +52,7 @@ def lex_walk(lex, t, c0, end):
         kend = min(16, end - bp)
         if any(b >= 0x80 for b in t[bp:bp + kend]):
             return out, p, lm, True, max(p, fc if fc is not None else c0)
-        m = 0
-        for k in range(kend):
-            s = int(tab[76 * s + t[bp + k]])
-            m |= (s & 3) << (2 * k)
+        m, s = lex16(lex, s, t[bp:bp + kend], kend)
         E = (m >> 1) & 0x55555555
         Z = (m ^ (m >> 1)) & 0x55555555
         zlast = (Z >> 30) & 1

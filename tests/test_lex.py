@@ -11,7 +11,7 @@ import pytest
 
 import regex_amd as R
 from iter_sim import UnitIter, find_iter_chunked
-from lex_sim import lex_unit, lex_walk
+from lex_sim import lex16, lex16x4, lex_unit, lex_walk
 from oracle_py import OracleRegex
 
 LEX_PATTERNS = [r">[^\n]*\n|\n", r"\n", r"a[^b]*b", r"(?-u)>[^\n]*\n|\n", r'"[^"]*"', r"<[^>]*>"]
@@ -29,6 +29,34 @@ def test_lex_tables_exist():
         assert R.Regex(pat).lex_table() is not None, pat
     for pat in [r"a+", r">[^\n]*", r"\w+", r"\d{4}-\d{2}-\d{2}", r"x*", r"abc|ab"]:
         assert R.Regex(pat).lex_table() is None, pat
+
+
+@pytest.mark.parametrize("pat", LEX_PATTERNS + [r"B", r"Y"])
+def test_lex4_blocks_equal_bytes(pat):
+    """build_lex4: four bytes per step gives the byte lexer's flag words and
+    states on ASCII blocks, full and partial (the IUB codes' one-byte
+    regexes too)."""
+    re = R.Regex(pat)
+    lex, lex4 = re.lex_table(), re.lex4_table()
+    assert lex is not None and lex4 is not None, pat
+    tab4, r0 = lex4
+    # the row of each byte-table entry, followed along the walk
+    rng = random.Random(zlib.crc32(pat.encode()))
+    for i in range(40):
+        t = ascii_text(rng.randrange(1 << 30), 16 * 40)
+        if i % 3 == 2:
+            t = bytes(rng.randrange(128) for _ in range(16 * 40))
+        s, r = lex[1], r0
+        ent_of_row = {r0: s}
+        for bp in range(0, len(t), 16):
+            kend = 16 if bp + 16 < len(t) or i % 2 == 0 else 1 + rng.randrange(16)
+            blk = t[bp:bp + 16]
+            m1, s = lex16(lex, s, blk, kend)
+            m4, r = lex16x4(lex4, r, blk, kend)
+            assert m1 == m4, (pat, i, bp, kend)
+            assert ent_of_row.setdefault(r, s) == s, (pat, i, bp)
+            if kend < 16:
+                break
 
 
 @pytest.mark.parametrize("pat", LEX_PATTERNS)
