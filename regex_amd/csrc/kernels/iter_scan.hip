@@ -64,6 +64,8 @@ struct Unit {
   uint32_t skip, pad;  // U_COPY: speculative matches dropped at the front; pad: U_COMPACT's lexer count
 };
 
+static_assert(sizeof(Unit) == 64, "iter_copy_group_kernel reads a unit's last 16 bytes");
+
 struct Geo {  // unit -> (haystack, chunk) for fixed-stride batches
   uint64_t nk;      // units per haystack
   uint64_t chunk;   // bytes per unit
@@ -1420,7 +1422,8 @@ __global__ __launch_bounds__(256, 4) void iter_spec_lex_tile_kernel(BatchDev b, 
       // their matches: the event bookkeeping stays off the dependent chain.
       // Active bytes: [c0 + at, lim) up to the first block with a byte >= 0x80.
       const uint64_t t0 = c0 + at;
-      const uint32_t span = frozen || lim <= t0 ? 0u : (uint32_t)min<uint64_t>(lim - t0, 128);
+      const uint64_t rest = lim > t0 ? lim - t0 : 0;
+      const uint32_t span = frozen ? 0u : rest < 128 ? (uint32_t)rest : 128u;
       uint32_t mw[8];
       uint32_t act = 0;  // bytes of the tile the lexer took
       if (__builtin_expect(__all(span == 128), 1)) {
@@ -1941,11 +1944,126 @@ __global__ __launch_bounds__(1024) void iter_emit_kernel(BatchDev b, Geo g, uint
 // units' ranges at once (8 x 128 B per store instruction, scattered over
 // the whole output): 0.31 ms for the strip's 35 M records.  Units that are
 // re-run (no valid slots) are left to iter_emit_kernel.
+// The copies of a lexer pass by lexer group (U_COMPACT interleaved rows,
+// lex_rec32): one block per group of 64 units, whose output records are one
+// contiguous range.  Per window of kGrpWin output records the four waves
+// read the rows overlapping it (each row one coalesced 1 KiB load, four
+// records per unit) and scatter the records into LDS at their output
+// places, tagged with their unit; then the block writes the window out
+// front to back, 1 KiB per wave store.  Both HBM streams stay whole-line.
+// (A row-by-row copy straight from registers wrote 64 units' scattered
+// 64-byte pieces per store: 0.26 ms for the strip's 35 M records; an
+// output-ordered copy gathering 4-byte records: 0.20 ms.)  The tail pass's
+// few absolute records are written directly; positions of units that are
+// re-run stay untagged, for iter_emit_kernel.
+constexpr uint32_t kGrpWin = 4096;
+__global__ __launch_bounds__(256) void iter_copy_group_kernel(BatchDev b, Geo g, uint64_t nunits, const Unit *units,
+                                                              const uint64_t *slots, const uint64_t *off,
+                                                              uint64_t *out, uint64_t cap) {
+  __shared__ uint32_t wrec[kGrpWin];
+  __shared__ uint8_t wtag[kGrpWin];  // unit in the group, 0xFF: nothing to write here
+  __shared__ uint64_t sbase[64];
+  const uint64_t obase = off[0];
+  const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const uint64_t ngroups = (nunits + 63) / 64;
+  const uint4 *rows = (const uint4 *)slots;
+  for (uint64_t G = blockIdx.x; G < ngroups; G += gridDim.x) {
+    const uint64_t u = G * 64 + lane;
+    uint32_t skip = 0, nl = 0, i1 = 0;  // records [skip, i1) go to out[o0 + i - skip]
+    uint64_t o0 = 0, c0 = 0;
+    if (u < nunits) {
+      const uint64_t a = off[u] - obase, cnt = off[u + 1] - off[u];
+      const uint4 tl = ((const uint4 *)(units + u))[3];  // spec_count, flags, skip, pad
+      const bool rerun = ((tl.y & U_FIXED) && !(tl.y & U_COPY)) || cnt > g.slots;
+      if (cnt && a < cap && !rerun) {
+        o0 = a;
+        skip = (tl.y & U_COPY) ? tl.z : 0;
+        nl = tl.w;
+        i1 = skip + (uint32_t)min(cnt, cap - a);
+        uint64_t hh, ll, c1;
+        const uint8_t *bb;
+        unit_bounds(b, g, u, &hh, &bb, &ll, &c0, &c1);
+      }
+    }
+    if (wv == 0) {
+      sbase[lane] = c0;
+      for (uint32_t i = max(skip, nl); i < i1; ++i)  // the tail pass's records
+        ((ulonglong2 *)out)[o0 + i - skip] = ((const ulonglong2 *)slots)[lex_row16(g, u, g.slots - 1 - (i - nl))];
+    }
+    const uint32_t le = min(i1, nl);  // the lexer's records: [skip, le)
+    const uint64_t O0 = off[G * 64] - obase, O1 = min(off[min(G * 64 + 64, nunits)] - obase, cap);
+    const uint64_t rbase = G * 64 * (uint64_t)g.slots + lane;  // lex_row16(g, u, 0)
+    for (uint64_t w0 = O0; w0 < O1; w0 += kGrpWin) {
+      const uint64_t w1 = min(O1, w0 + kGrpWin);
+      for (uint32_t i = t; i < kGrpWin / 4; i += 256) ((uint32_t *)wtag)[i] = 0xFFFFFFFFu;
+      // this unit's records in the window: i in [ia, ib)
+      uint32_t ia = skip, ib = skip;
+      if (le > skip && o0 < w1 && o0 + (le - skip) > w0) {
+        ia = o0 >= w0 ? skip : skip + (uint32_t)(w0 - o0);
+        ib = min(le, skip + (uint32_t)(w1 - o0));
+      }
+      uint32_t k0 = ib > ia ? ia / 4 : 0xFFFFFFFFu, k1 = ib > ia ? (ib + 3) / 4 : 0;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        k0 = min(k0, (uint32_t)__shfl_xor((int)k0, d));
+        k1 = max(k1, (uint32_t)__shfl_xor((int)k1, d));
+      }
+      __syncthreads();
+      // eight rows per wave in flight (a loop of one load and its scatter
+      // waited out a load latency per row)
+      for (uint32_t k = k0 + wv; k < k1; k += 32) {
+        uint4 v[8];
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j)
+          if (k + 4 * j < k1) v[j] = rows[rbase + (uint64_t)(k + 4 * j) * 64];
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j) {
+          const uint32_t kk = k + 4 * j;
+          const uint32_t x[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+#pragma unroll
+          for (uint32_t q = 0; q < 4; ++q) {
+            const uint32_t i = 4 * kk + q;
+            if (kk < k1 && i >= ia && i < ib) {
+              const uint32_t pp = (uint32_t)(o0 + (i - skip) - w0);
+              wrec[pp] = x[q];
+              wtag[pp] = (uint8_t)lane;
+            }
+          }
+        }
+      }
+      __syncthreads();
+      ulonglong2 *dst = (ulonglong2 *)out + w0;
+      for (uint32_t pp = t; pp < (uint32_t)(w1 - w0); pp += 256) {
+        const uint32_t tg = wtag[pp];
+        if (tg != 0xFFu) {
+          const uint32_t r = wrec[pp];
+          const uint64_t cb = sbase[tg];
+          dst[pp] = make_ulonglong2(cb + (r & 0xFFFFu), cb + (r >> 16));
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
 constexpr uint32_t kCopyRecs = 4096;  // output records per block (256 threads x 16)
 constexpr uint32_t kCopyUnits = 64;   // units staged per round (the strip's 4096 records span ~31)
+
+// iter_copy_out_kernel's block index: bidx[k] = the unit holding output
+// record k * kCopyRecs (k < nb), so a block starts from one load instead of
+// a three-round search over the unit offsets.
+__global__ void copy_index_kernel(uint64_t nunits, const uint64_t *off, uint32_t *bidx, uint64_t nb) {
+  const uint64_t obase = off[0];
+  for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < nunits; u += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t lo = off[u] - obase, hi = off[u + 1] - obase;
+    for (uint64_t k = (lo + kCopyRecs - 1) / kCopyRecs; k * kCopyRecs < hi && k < nb; ++k) bidx[k] = (uint32_t)u;
+  }
+}
+
 __global__ __launch_bounds__(256) void iter_copy_out_kernel(BatchDev b, Geo g, uint64_t nunits, const Unit *units,
                                                             const uint64_t *slots, const uint64_t *off,
-                                                            uint64_t *out, uint64_t cap) {
+                                                            uint64_t *out, uint64_t cap, const uint32_t *bidx,
+                                                            uint64_t nb) {
   __shared__ uint64_t soff[kCopyUnits + 1];
   __shared__ uint64_t sbase[kCopyUnits];
   __shared__ uint32_t sskip[kCopyUnits], snlex[kCopyUnits], sok[kCopyUnits];
@@ -1955,6 +2073,7 @@ __global__ __launch_bounds__(256) void iter_copy_out_kernel(BatchDev b, Geo g, u
     // the unit holding record r0: last u with off[u] - obase <= r0 (a
     // 256-ary search, two or three rounds over the unit offsets)
     uint64_t lo = 0, hi = nunits;  // answer in [lo, hi)
+    if (r0 / kCopyRecs < nb) lo = bidx[r0 / kCopyRecs], hi = lo + 1;
     while (hi - lo > 1) {
       const uint64_t step = (hi - lo + 255) / 256;
       const uint64_t c = lo + threadIdx.x * step;
@@ -1985,7 +2104,7 @@ __global__ __launch_bounds__(256) void iter_copy_out_kernel(BatchDev b, Geo g, u
       }
       __syncthreads();
       const uint64_t lo_r = soff[0], hi_r = soff[kCopyUnits];
-#pragma unroll 4
+#pragma unroll 8
       for (uint32_t k = 0; k < kCopyRecs / 256; ++k) {
         const uint64_t rr = r0 + k * 256 + threadIdx.x;
         if (rr >= rend || rr < lo_r || rr >= hi_r) continue;
@@ -2370,9 +2489,21 @@ static hipError_t iter_post(const BatchDev &b, const Geo &g, uint64_t nunits, co
   // emit pass only re-runs units (needs a 16-byte aligned output)
   dense = dense && (((uintptr_t)o.matches) & 15) == 0;
   if (dense) {
-    hipLaunchKernelGGL(iter_copy_out_kernel, dim3((unsigned)std::min<uint64_t>((nunits * 16) / kCopyRecs + 1, (uint64_t)cus * 8)),
-                       dim3(256), 0, st, b, g, nunits, (const Unit *)sc.units, (const uint64_t *)sc.slots,
-                       (const uint64_t *)sc.off, o.matches, o.cap);
+    if (getenv("RURE_AMD_COPY_GROUP") && getenv("RURE_AMD_COPY_GROUP")[0] == '0') {
+      // (A/B) the output-ordered copy; its block index lives in the repair
+      // queue's space (the walk is done with it): 2 u32 per unit
+      const uint64_t nb = 2 * nunits;
+      hipLaunchKernelGGL(copy_index_kernel, dim3(grid_cap(nunits, 256, cus, 4)), dim3(256), 0, st, nunits,
+                         (const uint64_t *)sc.off, (uint32_t *)sc.queue, nb);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+      hipLaunchKernelGGL(iter_copy_out_kernel, dim3((unsigned)cus * 8), dim3(256), 0, st, b, g, nunits,
+                         (const Unit *)sc.units, (const uint64_t *)sc.slots, (const uint64_t *)sc.off, o.matches,
+                         o.cap, (const uint32_t *)sc.queue, nb);
+    } else {
+      hipLaunchKernelGGL(iter_copy_group_kernel, dim3(grid_cap((nunits + 63) / 64, 1, cus, 8)), dim3(256), 0, st, b,
+                         g, nunits, (const Unit *)sc.units, (const uint64_t *)sc.slots, (const uint64_t *)sc.off,
+                         o.matches, o.cap);
+    }
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   hipLaunchKernelGGL(iter_emit_kernel, dim3(grid), dim3(bs), lb, st, b, g, nunits, f, r, sc.units, sc.slots, sc.off,

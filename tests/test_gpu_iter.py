@@ -173,3 +173,29 @@ def test_find_iter_lexer(cuda, pat, nonascii):
         assert got[k:k + len(e)] == e, (pat, i)
         k += len(e)
     assert k == len(got)
+
+
+@pytest.mark.parametrize("pat", LEX_PATTERNS)
+@pytest.mark.parametrize("env", [("RURE_AMD_LEX4", "0"), ("RURE_AMD_COPY_GROUP", "0")])
+def test_find_iter_lexer_variants(cuda, pat, env):
+    """The byte-per-step lexer (RURE_AMD_LEX4=0) and the output-ordered copy
+    (RURE_AMD_COPY_GROUP=0) give the default path's matches; the default
+    (four bytes per step, group copy) is checked against the oracle, with a
+    capacity that cuts the output inside a unit."""
+    import os
+    re = R.Regex(pat)
+    o = OracleRegex(re)
+    text = _lex_text(zlib.crc32(pat.encode()) + 7, 300000, True)
+    d = to_dev(text + b"\0" * 16, cuda)
+    exp = o.find_iter(text)
+    _, m = re.find_iter_batch(d, stride=len(text), length=len(text), count=1)
+    assert as_pairs(m) == exp
+    if len(exp) > 10:
+        _, mc = re.find_iter_batch(d, stride=len(text), length=len(text), count=1, capacity=len(exp) // 2 + 3)
+        assert as_pairs(mc)[:len(exp) // 2 + 3] == exp[:len(exp) // 2 + 3]
+    os.environ[env[0]] = env[1]
+    try:
+        _, m1 = re.find_iter_batch(d, stride=len(text), length=len(text), count=1)
+    finally:
+        del os.environ[env[0]]
+    assert as_pairs(m1) == exp
