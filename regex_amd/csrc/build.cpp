@@ -356,6 +356,7 @@ bool build_regex(rure *re) {
   std::thread rt([&] { rev_ok = build_dense_dfa(re->rev, lim, &re->drev, &rerr); });
   const bool fwd_ok = build_dense_dfa(re->fwd, lim, &re->dfwd, &err);
   rt.join();
+  re->rev_ok = rev_ok;
   if (fwd_ok && !rev_ok) err = rerr;
   if (!fwd_ok || !rev_ok || !pack_forward(re->dfwd, &re->pf, &err) || !pack_forward(re->drev, &re->pr, &err, true)) {
     re->dfa_err = err.empty() ? "reverse DFA too large" : err;
@@ -655,6 +656,57 @@ bool big_device(const DevTables &tc) {
   }
   t.big_blob = tmp.blob;
   t.has_big = true;
+  return true;
+}
+
+// The on-demand forward DFA (host LazyDfa, big_dfa.hip lazy_dfa_kernel) for
+// automata past the eager budgets: built on the first batch that needs it.
+// Its reverse partner is the regular u16 reverse DFA (t.r, or drev packed
+// and uploaded here when the forward DFA did not materialise).  Programs
+// with a Unicode word boundary keep the Pike VM, as for the big automata.
+bool lazy_device(const DevTables &tc) {
+  DevTables &t = const_cast<DevTables &>(tc);
+  rure *re = t.owner;
+  if (!re) return false;
+  std::lock_guard<std::mutex> g(re->mu);
+  if (t.lazy_tried) return t.has_lazy;
+  t.lazy_tried = true;
+  if (!re->nfa_ok || re->fwd.has_unicode_word_boundary || re->rev.has_unicode_word_boundary) return false;
+  if (!re->nfa.anchored_start && re->nfa.anchored_end) return false;  // DfaAnchoredReverse
+  if (t.has_dfa) {
+    t.lr = t.r;
+  } else {
+    if (!re->rev_ok || re->drev.quit >= 0) return false;
+    std::string e;
+    if (re->pr.full.empty() && !pack_forward(re->drev, &re->pr, &e, true)) return false;
+    const DenseDfa &rv = re->drev;
+    std::vector<uint16_t> rfull(rv.trans.size()), rstart(128);
+    for (size_t i = 0; i < rv.trans.size(); ++i) rfull[i] = (uint16_t)rv.trans[i];
+    for (int i = 0; i < 128; ++i) rstart[i] = (uint16_t)rv.start[i];
+    Blob bl;
+    const size_t o_full = bl.add(rfull.data(), rfull.size() * 2), o_eof = bl.add(rv.eof_match.data(), rv.eof_match.size()),
+                 o_start = bl.add(rstart.data(), 256);
+    DevTables tmp;
+    if (!upload_blob(bl, &tmp, &e)) return false;
+    uint8_t *base = (uint8_t *)tmp.blob;
+    t.lazy_rblob = tmp.blob;
+    RevDfaDev &r = t.lr;
+    r = RevDfaDev{};
+    r.full = (const uint16_t *)(base + o_full);
+    r.eof = base + o_eof;
+    r.start = (const uint16_t *)(base + o_start);
+    r.n_normal = rv.n_normal;
+    r.n_match_end = rv.n_match_end;
+    r.dead = rv.dead;
+    r.quit = 0xFFFFFFFFu;
+    r.ustart1 = re->pr.ustart1;
+  }
+  if (!re->lazy) {
+    size_t budget = kBigDfaBytes;
+    if (const char *v = getenv("RURE_AMD_BIG_BYTES")) budget = (size_t)std::max(1ll, atoll(v));
+    re->lazy.reset(new LazyDfa(re->fwd, budget));
+  }
+  t.has_lazy = true;
   return true;
 }
 

@@ -191,6 +191,8 @@ void rure_free(rure *re) {
     (void)hipSetDevice(kv.first);
     (void)hipFree(kv.second.blob);
     if (kv.second.big_blob) (void)hipFree(kv.second.big_blob);
+    if (kv.second.lazy_buf) (void)hipFree(kv.second.lazy_buf);
+    if (kv.second.lazy_rblob) (void)hipFree(kv.second.lazy_rblob);
     (void)hipSetDevice(cur);
   }
   delete re;

@@ -188,10 +188,101 @@ bool big_batch(const BatchDev &b, const DevTables &t) {
   return b.count >= (uint64_t)t.cus * 64;
 }
 
+// find / is_match / shortest on the on-demand forward DFA (lazy_device):
+// rounds of lazy_dfa_kernel; between rounds the host builds the rows the
+// parked lanes need (and, ahead of them, more rows in discovery order) and
+// uploads the grown table.  Synchronous, as the reference's construction
+// happens inside its search.  The reference gives up on its lazy DFA when
+// the cache thrashes (dfa.rs:1282-1293) and runs the Pike VM; here a spent
+// memory budget or kLazyRounds rounds do the same for the batch.
+constexpr int kLazyRounds = 256;
+hipError_t run_lazy(int mode, const BatchDev &b, const DevTables &tc, void *out, hipStream_t st) {
+  DevTables &t = const_cast<DevTables &>(tc);
+  rure *re = t.owner;
+  std::lock_guard<std::mutex> g(re->mu);
+  LazyDfa &L = *re->lazy;
+  size_t ahead = 4096;  // rows built ahead per round (RURE_AMD_LAZY_ROWS: tests)
+  if (const char *v = getenv("RURE_AMD_LAZY_ROWS")) ahead = (size_t)std::max(1ll, atoll(v));
+  bool ok = L.nbuilt() > 0 || L.expand(ahead);
+  hipError_t e = hipSuccess;
+  LazyPark *pk[2] = {nullptr, nullptr};
+  unsigned long long *cnt = nullptr;
+  const size_t pbytes = std::max<uint64_t>(b.count, 1) * sizeof(LazyPark);
+  if ((e = scratch_malloc((void **)&pk[0], pbytes, st)) != hipSuccess) return e;
+  if ((e = scratch_malloc((void **)&pk[1], pbytes, st)) != hipSuccess) return e;
+  if ((e = scratch_malloc((void **)&cnt, 16, st)) != hipSuccess) return e;
+  const LazyPark *in = nullptr;
+  uint64_t nin = 0;
+  std::vector<LazyPark> host;
+  for (int round = 0; ok && e == hipSuccess; ++round) {
+    // the table: [colmap 256][start 512][eof cap][trans cap * ncol * 4]
+    const size_t ns = L.nstates(), need = 768 + ns + ns * (size_t)L.ncol * 4 + 16;
+    if (need > t.lazy_cap) {
+      if ((e = hipStreamSynchronize(st)) != hipSuccess) break;
+      if (t.lazy_buf) (void)hipFree(t.lazy_buf);
+      t.lazy_buf = nullptr;
+      t.lazy_cap = std::max(need * 3 / 2, (size_t)1 << 20);
+      if ((e = hipMalloc(&t.lazy_buf, t.lazy_cap)) != hipSuccess) { t.lazy_cap = 0; break; }
+    }
+    uint8_t *base = (uint8_t *)t.lazy_buf;
+    const size_t o_eof = 768, o_trans = (768 + ns + 15) & ~(size_t)15;
+    if ((e = hipMemcpyAsync(base, L.colmap, 256, hipMemcpyHostToDevice, st)) != hipSuccess) break;
+    if ((e = hipMemcpyAsync(base + 256, L.start, 512, hipMemcpyHostToDevice, st)) != hipSuccess) break;
+    if ((e = hipMemcpyAsync(base + o_eof, L.eof.data(), ns, hipMemcpyHostToDevice, st)) != hipSuccess) break;
+    if ((e = hipMemcpyAsync(base + o_trans, L.trans.data(), L.trans.size() * 4, hipMemcpyHostToDevice, st)) !=
+        hipSuccess)
+      break;
+    LazyDfaDev f{};
+    f.colmap = base;
+    f.start = (const uint32_t *)(base + 256);
+    f.eof = base + o_eof;
+    f.trans = (const uint32_t *)(base + o_trans);
+    f.ncol = L.ncol;
+    f.hot = std::min<uint32_t>((uint32_t)ns, lazy_dfa_hot_rows(L.ncol));
+    LazyPark *po = pk[round & 1];
+    if ((e = hipMemsetAsync(cnt, 0, 8, st)) != hipSuccess) break;
+    if ((e = launch_lazy_dfa(mode, b, f, t.lr, in, nin, po, cnt, out, st, t.cus)) != hipSuccess) break;
+    unsigned long long n = 0;
+    if ((e = hipMemcpyAsync(&n, cnt, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) break;
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) break;
+    if (n == 0) break;
+    if (round + 1 >= kLazyRounds) { ok = false; break; }
+    host.resize(n);
+    if ((e = hipMemcpy(host.data(), po, n * sizeof(LazyPark), hipMemcpyDeviceToHost)) != hipSuccess) break;
+    size_t built0 = L.nbuilt();
+    for (const LazyPark &x : host)
+      if (!(ok = L.build_row(x.s))) break;
+    // (a fixed number ahead: doubling the rows built ahead each round built
+    // states in discovery order the text never visits, seconds of host work
+    // for (?:a|b)*a(?:a|b){20})
+    (void)built0;
+    if (ok) ok = L.expand(ahead);
+    in = po;
+    nin = n;
+  }
+  for (int k = 0; k < 2; ++k) { hipError_t e2 = scratch_free(pk[k], st); if (e == hipSuccess) e = e2; }
+  { hipError_t e2 = scratch_free(cnt, st); if (e == hipSuccess) e = e2; }
+  if (e == hipSuccess && !ok) e = run_pike(mode, false, b, t, out, st);  // the whole batch again
+  return e;
+}
+
+// The on-demand DFA where the eager automata did not materialise (or
+// RURE_AMD_LAZY=1: tests, any regex), for batches that fill the device.
+static bool lazy_batch(const BatchDev &b, const DevTables &t) {
+  const char *env = getenv("RURE_AMD_LAZY");
+  if (env && env[0] == '0') return false;
+  const bool force = env && env[0] == '1';
+  if (!force && (t.has_dfa || !big_batch(b, t))) return false;
+  return lazy_device(t);
+}
+
 hipError_t run_regex(int mode, const BatchDev &b, const DevTables &t, void *out, hipStream_t st, int dfa_grid,
                      const FwdDfaDev *iter) {
   if (lane_search_ok(t)) return run_lane_search(mode, b, t, out, st);
+  if (getenv("RURE_AMD_LAZY") && getenv("RURE_AMD_LAZY")[0] == '1' && lazy_batch(b, t))
+    return run_lazy(mode, b, t, out, st);
   if (!t.has_dfa && big_batch(b, t) && big_device(t)) return launch_big_dfa(mode, b, t.bf, t.br, out, st, t.cus);
+  if (!t.has_dfa && lazy_batch(b, t)) return run_lazy(mode, b, t, out, st);
   if (!t.has_dfa) return run_pike(mode, false, b, t, out, st);
   uint64_t chunk = 0;
   if (iter && long_batch(mode, b, t, &chunk) && !(t.anchored_rev && b.start != 0))

@@ -44,6 +44,38 @@ class Builder {
     stamp_.assign(p.insts.size() + 1, 0);
   }
 
+  // On-demand construction (LazyDfa): the start states, then rows one state
+  // at a time in any order; states are raw (unminimised) ids, 0 = dead.
+  void lazy_init(uint8_t *colmap, uint32_t *ncol) {
+    keys_.push_back(std::string());
+    keys_.push_back(std::string());
+    compute_starts();
+    lazy_ncls_ = p_.num_byte_classes();
+    int seen = -1;
+    for (int b = 0; b < 256; ++b) {
+      if (p_.byte_classes[b] != seen) { seen = p_.byte_classes[b]; lazy_rep_[seen] = (uint8_t)b; }
+      colmap[b] = (uint8_t)p_.byte_classes[b];
+    }
+    *ncol = (uint32_t)lazy_ncls_;
+  }
+  uint32_t lazy_states() const { return (uint32_t)keys_.size(); }
+  size_t lazy_bytes() const { return key_bytes_; }
+  void lazy_row(uint32_t s, uint32_t *row) {
+    if (s < 2) {
+      for (int c = 0; c < lazy_ncls_; ++c) row[c] = s;
+      return;
+    }
+    const std::string key = keys_[s];  // copy: keys_ may grow
+    step_row(key, lazy_ncls_, lazy_rep_, row);
+  }
+  bool lazy_eof(uint32_t s) {
+    if (s < 2) return false;
+    uint64_t m = 0;
+    return step_eof(keys_[s], &m);
+  }
+  bool lazy_match(uint32_t s) const { return s >= 2 && (keys_[s][0] & SF_MATCH); }
+  uint32_t lazy_start(int fi) const { return start_used_[fi] ? start_raw_[fi] : 0; }
+
   bool build(DenseDfa *out, std::string *err) {
     const auto t_begin = std::chrono::steady_clock::now();
     // raw state 0 = DEAD, raw state 1 = QUIT (always allocated, maybe unused)
@@ -156,6 +188,8 @@ class Builder {
   std::vector<uint64_t> eof_mask_;
   uint32_t start_raw_[128];
   bool start_used_[128];
+  int lazy_ncls_ = 0;
+  uint8_t lazy_rep_[256] = {0};
 
   // dfa.rs:1073-1134
   void follow(uint32_t ip0, SparseSet &q, const EmptyFlags &f) {
@@ -654,6 +688,60 @@ class Builder {
 bool build_dense_dfa(const Program &prog, const DfaBuildLimits &lim, DenseDfa *out, std::string *err) {
   Builder b(prog, lim);
   return b.build(out, err);
+}
+
+struct LazyDfa::Impl {
+  Builder b;
+  Impl(const Program &p, const DfaBuildLimits &lim) : b(p, lim) {}
+};
+
+LazyDfa::LazyDfa(const Program &prog, size_t max_bytes) : max_bytes_(max_bytes) {
+  DfaBuildLimits lim;
+  lim.max_raw_states = 0x7FFFFFF0;
+  impl_ = new Impl(prog, lim);
+  impl_->b.lazy_init(colmap, &ncol);
+  for (int i = 0; i < 128; ++i) start[i] = impl_->b.lazy_start(i);
+  sync_new();
+  for (int i = 0; i < 128; ++i) start[i] = entry_of(start[i]);
+}
+
+LazyDfa::~LazyDfa() { delete impl_; }
+
+uint32_t LazyDfa::entry_of(uint32_t s) const {
+  return s | (impl_->b.lazy_match(s) ? kLazyMatch : 0u);
+}
+
+// rows (unknown) and EOF flags for the states interned since the last call
+void LazyDfa::sync_new() {
+  const uint32_t n = impl_->b.lazy_states();
+  for (uint32_t s = (uint32_t)eof.size(); s < n; ++s) {
+    eof.push_back(impl_->b.lazy_eof(s) ? 1 : 0);
+    built.push_back(s < 2 ? 1 : 0);
+    trans.resize((size_t)(s + 1) * ncol, s < 2 ? s : kLazyUnknown);
+    if (s >= 2) todo_.push_back(s);
+  }
+}
+
+bool LazyDfa::build_row(uint32_t s) {
+  if (s >= built.size() || built[s]) return true;
+  if (max_bytes_ && impl_->b.lazy_bytes() + trans.size() * 4 > max_bytes_) return false;
+  std::vector<uint32_t> row(ncol);
+  impl_->b.lazy_row(s, row.data());
+  sync_new();
+  for (uint32_t c = 0; c < ncol; ++c) trans[(size_t)s * ncol + c] = entry_of(row[c]);
+  built[s] = 1;
+  ++nbuilt_;
+  return true;
+}
+
+bool LazyDfa::expand(size_t rows) {
+  for (size_t k = 0; k < rows && todo_head_ < todo_.size(); ++todo_head_) {
+    const uint32_t s = todo_[todo_head_];
+    if (built[s]) continue;
+    if (!build_row(s)) return false;
+    ++k;
+  }
+  return true;
 }
 
 int start_flag_index_fwd(const uint8_t *text, size_t len, size_t at) {  // dfa.rs:1415-1434

@@ -59,8 +59,10 @@ struct DfaBuildLimits {
   bool minimise = true;   // false: raw states kept (same language, more states)
   size_t max_bytes = 0;   // construction memory budget (state keys + rows, estimated); 0 = none
 };
-// Raw-state budget of the u32 (column form) automata.
-constexpr int kBigDfaRawStates = 1 << 21;
+// Raw-state budget of the eager u32 (column form) automata; past it the
+// on-demand DFA (LazyDfa) builds only the states a batch visits.  (At 1 << 21
+// the failed eager attempt for (?:a|b)*a(?:a|b){20} cost ~5 s.)
+constexpr int kBigDfaRawStates = 1 << 18;
 // Construction memory budget of the u32 automata (RURE_AMD_BIG_BYTES overrides).
 constexpr size_t kBigDfaBytes = (size_t)1 << 30;
 
@@ -69,6 +71,44 @@ constexpr size_t kBigDfaBytes = (size_t)1 << 30;
 // exceeded.
 bool build_dense_dfa(const Program &prog, const DfaBuildLimits &lim, DenseDfa *out,
                      std::string *err);
+
+// On-demand construction past the eager budgets: the reference's lazy DFA
+// (dfa.rs:910-1048 exec_byte, 1282-1320 cache) restated for batched scans.
+// States are the subset construction's raw ids (0 = dead), numbered as they
+// are discovered; a row is built when a scan first needs it (or ahead, in
+// discovery order, by expand).  Table entries for the device: the next
+// state's id, | kLazyMatch when that state carries the (one-byte delayed)
+// match flag; kLazyUnknown for a row not built yet (the kernel parks the
+// lane there).  Columns are the program's byte classes (no quit states:
+// Unicode word boundaries keep the Pike VM).
+constexpr uint32_t kLazyMatch = 0x80000000u, kLazyUnknown = 0x7FFFFFFFu;
+class LazyDfa {
+ public:
+  LazyDfa(const Program &prog, size_t max_bytes);
+  ~LazyDfa();
+  LazyDfa(const LazyDfa &) = delete;
+  LazyDfa &operator=(const LazyDfa &) = delete;
+  // Builds state s's row (false: the memory budget is spent).
+  bool build_row(uint32_t s);
+  // Builds up to `rows` more rows in discovery order.
+  bool expand(size_t rows);
+  uint32_t nstates() const { return (uint32_t)eof.size(); }
+  size_t nbuilt() const { return nbuilt_; }
+  uint32_t ncol = 0;
+  uint8_t colmap[256] = {0};
+  uint32_t start[128];            // entries (id | kLazyMatch) per start-flag index
+  std::vector<uint32_t> trans;    // nstates * ncol entries
+  std::vector<uint8_t> eof;       // per state: the EOF step yields a match
+  std::vector<uint8_t> built;     // per state: its row is built
+ private:
+  struct Impl;
+  Impl *impl_ = nullptr;
+  size_t max_bytes_ = 0, nbuilt_ = 0;
+  std::vector<uint32_t> todo_;
+  size_t todo_head_ = 0;
+  uint32_t entry_of(uint32_t s) const;
+  void sync_new();
+};
 
 // Start-flag index for a forward search starting at `at` (dfa.rs:1415-1434).
 int start_flag_index_fwd(const uint8_t *text, size_t len, size_t at);

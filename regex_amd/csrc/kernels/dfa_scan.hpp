@@ -380,6 +380,31 @@ hipError_t launch_big_dfa(int mode, const BatchDev &b, const BigDfaDev &f, const
 // Rows of a big forward DFA the kernel holds in LDS.
 uint32_t big_dfa_hot_rows(uint32_t ncol, uint32_t nstates);
 
+// A forward DFA built on demand (host LazyDfa): entries are next-state ids,
+// | 0x80000000 when that state carries the match flag, 0x7FFFFFFF for a row
+// not built yet; id 0 is the dead state.  The first `hot` rows sit in LDS.
+struct LazyDfaDev {
+  const uint32_t *trans;
+  const uint8_t *colmap;      // 256 bytes
+  const uint8_t *eof;         // per state
+  const uint32_t *start;      // 128 start entries by flag index
+  uint32_t ncol, hot;
+};
+// A lane stopped at a row not built yet: haystack, position of the byte it
+// needs, the last match end so far (~0: none), the state.
+struct LazyPark {
+  uint64_t h, p, last;
+  uint32_t s, pad;
+};
+// One round of a batched forward scan on a LazyDfaDev (find: the reverse
+// DFA r gives the start, exec.rs:632-662): lanes are the haystacks (in =
+// nullptr) or the parked lanes of the previous round; lanes that need a
+// missing row are appended to park (*npark).
+hipError_t launch_lazy_dfa(int mode, const BatchDev &b, const LazyDfaDev &f, const RevDfaDev &r, const LazyPark *in,
+                           uint64_t nin, LazyPark *park, unsigned long long *npark, void *out, hipStream_t st,
+                           int cus);
+uint32_t lazy_dfa_hot_rows(uint32_t ncol);
+
 // Scratch device memory for the scans, cached by the library (scratch.cpp):
 // a freed block is kept with an event recorded on the freeing stream and
 // reused, after a wait on that event, by the next allocation of at most twice

@@ -86,6 +86,12 @@ struct DevTables {
   void *big_blob = nullptr; // their device copy
   struct rure *owner = nullptr;  // the regex (big_device builds its automata on first need)
   BigDfaDev bf{}, br{};
+  // the on-demand forward DFA (lazy_device / run_lazy): its device copy
+  // (grown as rows are built) and the reverse DFA it finds starts with
+  bool lazy_tried = false, has_lazy = false;
+  void *lazy_buf = nullptr, *lazy_rblob = nullptr;
+  size_t lazy_cap = 0;
+  RevDfaDev lr{};
   bool quit_possible = false;  // the DFA can quit (Unicode \b): Pike VM fallback pass
   bool anchored_rev = false;   // MatchType::DfaAnchoredReverse (exec.rs:1175-1177)
   // The reference's match type where its searches differ from a forward DFA
@@ -236,6 +242,9 @@ struct rure {
   // find / is_match / shortest_match only, when dfa_ok is false
   bool big_ok = false, big_built = false;
   DenseDfa bfwd, brev;
+  bool rev_ok = false;            // drev materialised (even when dfwd did not)
+  bool lazy_tried = false;        // the on-demand forward DFA (lazy_device)
+  std::unique_ptr<LazyDfa> lazy;
   NfaTables nt;
   bool nfa_ok = false;
   std::map<int, DevTables> dev;
@@ -329,6 +338,7 @@ bool needs_mt_lane(const ExecLiterals &x);
 void set_prefix_skip(const rure *re, FwdDfaDev *f);
 DevTables *regex_device(rure *re, std::string *err);
 bool big_device(const DevTables &tc);
+bool lazy_device(const DevTables &tc);
 DevTables *set_device(rure_set *rs, std::string *err);
 uint32_t first_byte_rule(const DenseDfa &d, uint32_t ustart1, bool nonempty, uint8_t bytes[4]);
 bool build_lex4(const std::vector<uint8_t> &img, uint32_t s0, std::vector<uint8_t> *out, uint32_t *s0_row);
