@@ -1273,42 +1273,59 @@ __device__ __forceinline__ uint32_t lex16x4(uint32_t &s, const uint32_t w[4], co
 }
 
 // The lexer's matches go to the unit's slots as u32 (start - c0 | end - c0 <<
-// 16) records (U_COMPACT, interleaved rows: lex_rec32) through a queue of
-// eight in registers: q0..q3 = the row being filled, q4..q7 the next.  Once
-// per tile one 16-byte store writes the row whatever it holds
-// (LexQueue::flush) and a full row gives way to the next: no store in the
-// block loop depends on the data, so the wait for the next tile's loads
-// counts a fixed number of younger stores.  A store whose count depends on
-// the data (one per match) made the compiler drain every store before each
-// tile's loads could be used (s_waitcnt vmcnt(0)): the kernel ran 0.96 ms
-// with them against 0.61 ms without (tools/lex_time.py A/B).  A ninth
-// queued match flushes early, then waits for its stores.
-struct LexQueue {
-  uint32_t q0, q1, q2, q3, q4, q5, q6, q7;  // start | end << 16 (units of at most 64 KiB)
-  uint32_t qc, row;                         // queued; the row q0..q3 belong to
-  __device__ __forceinline__ void flush(uint32_t *dst, uint32_t rows) {
-    // past the slots: a re-run unit, slots unread
-    *(uint4 *)(dst + 256 * min(row, rows - 1)) = make_uint4(q0, q1, q2, q3);
-    if (qc >= 4) {
-      q0 = q4; q1 = q5; q2 = q6; q3 = q7;
-      qc -= 4;
-      ++row;
-    }
+// 16) records (U_COMPACT, interleaved rows: lex_rec32) through a ring of
+// eight records per lane in LDS: the wave's stage buffer, free between the
+// tile's chain and the next tile's staging (ring position x of lane l at u32
+// 64 x + l: conflict-free), so a push is one LDS write (an eight-register
+// queue cost 16 VALU selects per match).  Once per tile one 16-byte store
+// writes the row being filled whatever it holds (LexRing::flush), carried in
+// four registers across the next staging: no store in the block loop
+// depends on the data, so the wait for the next tile's loads counts a fixed
+// number of younger stores.  A store whose count depends on the data (one
+// per match) made the compiler drain every store before each tile's loads
+// could be used (s_waitcnt vmcnt(0)): the kernel ran 0.96 ms with them
+// against 0.61 ms without (tools/lex_time.py A/B).  A ninth pending match
+// stores its full row early, then waits for its stores.
+struct LexRing {
+  uint32_t *ring;            // the wave's stage buffer as u32, + lane
+  uint32_t c0, c1, c2, c3;   // the row being filled (start | end << 16, units of at most 64 KiB)
+  uint32_t n, row;           // records pushed; the row being filled
+  __device__ __forceinline__ void restore() {
+    const uint32_t h = 256 * (row & 1);
+    ring[h] = c0;
+    ring[h + 64] = c1;
+    ring[h + 128] = c2;
+    ring[h + 192] = c3;
+  }
+  __device__ __forceinline__ void spill(uint32_t *dst, uint32_t rows) {  // the full row, out of turn
+    const uint32_t h = 256 * (row & 1);
+    *(uint4 *)(dst + 256 * min(row, rows - 1)) = make_uint4(ring[h], ring[h + 64], ring[h + 128], ring[h + 192]);
+    ++row;
   }
   __device__ __forceinline__ void push(uint32_t r, uint32_t *dst, uint32_t rows) {
-    if (qc == 8) {
-      flush(dst, rows);
+    if (n - 4 * row == 8) {
+      spill(dst, rows);
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the tile's store count stays fixed
     }
-    q0 = qc == 0 ? r : q0;
-    q1 = qc == 1 ? r : q1;
-    q2 = qc == 2 ? r : q2;
-    q3 = qc == 3 ? r : q3;
-    q4 = qc == 4 ? r : q4;
-    q5 = qc == 5 ? r : q5;
-    q6 = qc == 6 ? r : q6;
-    q7 = qc == 7 ? r : q7;
-    ++qc;
+    ring[64 * (n & 7)] = r;
+    ++n;
+  }
+  __device__ __forceinline__ void flush(uint32_t *dst, uint32_t rows) {
+    uint32_t h = 256 * (row & 1);
+    c0 = ring[h];
+    c1 = ring[h + 64];
+    c2 = ring[h + 128];
+    c3 = ring[h + 192];
+    // past the slots: a re-run unit, slots unread
+    *(uint4 *)(dst + 256 * min(row, rows - 1)) = make_uint4(c0, c1, c2, c3);
+    if (n >= 4 * (row + 1)) {
+      ++row;
+      h = 256 * (row & 1);
+      c0 = ring[h];
+      c1 = ring[h + 64];
+      c2 = ring[h + 128];
+      c3 = ring[h + 192];
+    }
   }
 };
 
@@ -1319,23 +1336,26 @@ struct LexQueue {
 // start c0 (fc: the last such position before the block; last: the end of
 // the last match).  For a partial block (kend < 16, the walk's last) the
 // candidate at bp + kend enters fc harmlessly.
-__device__ __forceinline__ void lex_events(uint32_t m, uint32_t bp, uint32_t &cz, uint32_t &fc, uint32_t &last,
-                                           uint32_t &n, LexQueue &Q, uint32_t *dst, uint32_t cap4) {
-  uint32_t E = (m >> 1) & 0x55555555u;
-  const uint32_t Z = (m ^ (m >> 1)) & 0x55555555u;
-  const uint32_t A = E | (Z << 2) | cz;
+// Over two blocks at once (bytes bp..bp+31, m1: the second block's flags,
+// 0 when it was not lexed).
+__device__ __forceinline__ void lex_events(uint32_t m0, uint32_t m1, uint32_t bp, uint32_t &cz, uint32_t &fc,
+                                            uint32_t &last, uint32_t &n, LexRing &Q, uint32_t *dst, uint32_t cap4) {
+  const uint64_t M = ((uint64_t)m1 << 32) | m0;
+  uint64_t E = (M >> 1) & 0x5555555555555555ull;
+  const uint64_t Z = (M ^ (M >> 1)) & 0x5555555555555555ull;
+  const uint64_t A = E | (Z << 2) | cz;
   while (E) {
-    const uint32_t j = __builtin_ctz(E);
+    const uint32_t j = (uint32_t)__builtin_ctzll(E);
     E &= E - 1;
-    const uint32_t below = A & ((1u << j) - 1u);
-    const uint32_t st = below ? bp + ((31 - __builtin_clz(below)) >> 1) : fc;
+    const uint64_t below = A & ((1ull << j) - 1ull);
+    const uint32_t st = below ? bp + ((63 - (uint32_t)__builtin_clzll(below)) >> 1) : fc;
     const uint32_t x = bp + (j >> 1);
     Q.push(st | (x << 16), dst, cap4);
     ++n;
     last = x;
   }
-  if (A) fc = bp + ((31 - __builtin_clz(A)) >> 1);
-  cz = (Z >> 30) & 1u;
+  if (A) fc = bp + ((63 - (uint32_t)__builtin_clzll(A)) >> 1);
+  cz = (uint32_t)(Z >> 62) & 1u;
 }
 
 // X4: the four-bytes-per-step table (lex16x4); else one byte per step.
@@ -1393,9 +1413,10 @@ __global__ __launch_bounds__(256, 4) void iter_spec_lex_tile_kernel(BatchDev b, 
     // write whole rows)
     uint32_t *const dst = (uint32_t *)slots + lex_rec32(g, u, 0);
     const uint32_t cap4 = g.slots;  // rows
-    LexQueue Q;
-    Q.q0 = Q.q1 = Q.q2 = Q.q3 = Q.q4 = Q.q5 = Q.q6 = Q.q7 = 0;
-    Q.qc = Q.row = 0;
+    LexRing Q;
+    Q.ring = (uint32_t *)buf + lane;
+    Q.c0 = Q.c1 = Q.c2 = Q.c3 = 0;
+    Q.n = Q.row = 0;
     uint32_t fc = 0, last = 0;  // relative to c0 (lex_events)
     uint32_t n = 0, s = X4 ? f.lex4_s0 : f.lex_s0, cz = 1;
     bool frozen = false;  // a byte >= 0x80 was seen: the rest is the tail pass's
@@ -1406,10 +1427,10 @@ __global__ __launch_bounds__(256, 4) void iter_spec_lex_tile_kernel(BatchDev b, 
   n4 = RURE_LD(4, a); n5 = RURE_LD(5, a); n6 = RURE_LD(6, a); n7 = RURE_LD(7, a);
 #define RURE_STAGE(kk, v) buf[(8 * (kk) + src_h) * 8 + (src_seg ^ (((8 * (kk) + src_h) >> 1) & 7))] = (v);
     RURE_LOAD_TILE(0)
-    // an empty flush: the loop is entered, as it loops back, with the two
-    // flush stores younger than the tile loads (the wait for the loads then
-    // leaves them in flight: vmcnt(2), not vmcnt(0))
-    Q.flush(dst, cap4);
+    // an empty row store: the loop is entered, as it loops back, with a
+    // store younger than the tile loads (the wait for the loads then leaves
+    // it in flight, not vmcnt(0))
+    *(uint4 *)dst = make_uint4(0, 0, 0, 0);
     for (uint64_t at = 0; at < C; at += 128) {
       RURE_STAGE(0, n0) RURE_STAGE(1, n1) RURE_STAGE(2, n2) RURE_STAGE(3, n3)
       RURE_STAGE(4, n4) RURE_STAGE(5, n5) RURE_STAGE(6, n6) RURE_STAGE(7, n7)
@@ -1460,9 +1481,14 @@ __global__ __launch_bounds__(256, 4) void iter_spec_lex_tile_kernel(BatchDev b, 
       }
       // unrolled: a loop over m indexes mw[] dynamically (a select chain
       // of 7 per block)
+      Q.restore();  // the chain has read the stage: the ring may use it
+      // two blocks per event loop: the loop runs whenever any lane of the
+      // wave has a match in its bytes, i.e. per block nearly always (one
+      // match per ~61 bytes per lane); per 32 bytes it runs half as often
+      // (0.633 -> 0.619 ms, tools/lex_time.py)
 #pragma unroll
-      for (int m = 0; m < 8; ++m)
-        if (16u * m < act) lex_events(mw[m], (uint32_t)at + 16 * m, cz, fc, last, n, Q, dst, cap4);
+      for (int m = 0; m < 8; m += 2)
+        if (16u * m < act) lex_events(mw[m], mw[m + 1], (uint32_t)at + 16 * m, cz, fc, last, n, Q, dst, cap4);
       Q.flush(dst, cap4);  // every lane, every tile (slots are padded to whole groups)
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -1471,7 +1497,7 @@ __global__ __launch_bounds__(256, 4) void iter_spec_lex_tile_kernel(BatchDev b, 
 #undef RURE_LD
 #undef RURE_LOAD_TILE
 #undef RURE_STAGE
-    if (Q.qc) Q.flush(dst, cap4);  // the next row's records (q4..q7 became q0..q3)
+    if (Q.n > 4 * Q.row) *(uint4 *)(dst + 256 * min(Q.row, cap4 - 1)) = make_uint4(Q.c0, Q.c1, Q.c2, Q.c3);
     if (!valid) continue;
     // (clean flags and counts only matter when the tail pass is skipped,
     // RURE_AMD_LEX_TAIL=0: a diagnostic that leaves the lexer's matches alone)

@@ -38,38 +38,54 @@ def lex16x4(lex4, s, blk, kend):
 
 def lex_walk(lex, t, c0, end):
     """Walk text[c0, end) from the start state as the kernel does, block by
-    block (16-byte blocks aligned to c0 here).  A block holding a byte >= 0x80
-    freezes the walk (the kernel leaves the rest to the tail pass).  Returns
-    (matches, p, lm, frozen): the matches whose search ended inside, the
-    iteration state after them, and whether the walk froze."""
+    block (16-byte blocks aligned to c0 here), the events of two blocks at a
+    time (lex_events).  A block holding a byte >= 0x80 freezes the walk (the
+    kernel leaves the rest to the tail pass).  Returns (matches, p, lm,
+    frozen, hint): the matches whose search ended inside, the iteration
+    state after them, whether the walk froze, and the tail pass's scan-from
+    hint."""
     tab, s0 = lex
     s = s0
     cz = 1                 # the state before c0 is the start state
     fc = None
     p, lm = c0, NONE
     out = []
-    for bp in range(c0, end, 16):
-        kend = min(16, end - bp)
-        if any(b >= 0x80 for b in t[bp:bp + kend]):
-            return out, p, lm, True, max(p, fc if fc is not None else c0)
-        m, s = lex16(lex, s, t[bp:bp + kend], kend)
-        E = (m >> 1) & 0x55555555
-        Z = (m ^ (m >> 1)) & 0x55555555
-        zlast = (Z >> 30) & 1
-        # (a partial block is the walk's last: its bit 2 kend only reaches fc)
-        A = (E | (Z << 2) | cz) & 0xFFFFFFFF
+    frozen = False
+    blocks = []            # (bp, m) of the pair being collected
+    bp = c0
+
+    def events(b0, m0, m1):
+        nonlocal cz, fc, p, lm
+        M = m0 | (m1 << 32)
+        E = (M >> 1) & 0x5555555555555555
+        Z = (M ^ (M >> 1)) & 0x5555555555555555
+        A = (E | (Z << 2) | cz) & 0xFFFFFFFFFFFFFFFF
         while E:
             j = (E & -E).bit_length() - 1
             E &= E - 1
             below = A & ((1 << j) - 1)
-            f = bp + (below.bit_length() - 1) // 2 if below else fc
-            x = bp + j // 2
+            f = b0 + (below.bit_length() - 1) // 2 if below else fc
+            x = b0 + j // 2
             out.append((f, x))
             p = lm = x
         if A:
-            fc = bp + (A.bit_length() - 1) // 2
-        cz = zlast
-    return out, p, lm, False, max(p, fc if fc is not None else c0)
+            fc = b0 + (A.bit_length() - 1) // 2
+        cz = (Z >> 62) & 1
+
+    while bp < end:
+        kend = min(16, end - bp)
+        if any(b >= 0x80 for b in t[bp:bp + kend]):
+            frozen = True
+            break
+        m, s = lex16(lex, s, t[bp:bp + kend], kend)
+        blocks.append((bp, m))
+        if len(blocks) == 2:
+            events(blocks[0][0], blocks[0][1], blocks[1][1])
+            blocks = []
+        bp += 16
+    if blocks:  # a pair's first block alone (its second was not lexed)
+        events(blocks[0][0], blocks[0][1], 0)
+    return out, p, lm, frozen, max(p, fc if fc is not None else c0)
 
 
 def lex_unit(tab, fwd, rev, t, c0, c1):
