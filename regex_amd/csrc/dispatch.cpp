@@ -248,7 +248,9 @@ hipError_t run_lazy(int mode, const BatchDev &b, const DevTables &tc, void *out,
     if (n == 0) break;
     if (round + 1 >= kLazyRounds) { ok = false; break; }
     host.resize(n);
-    if ((e = hipMemcpy(host.data(), po, n * sizeof(LazyPark), hipMemcpyDeviceToHost)) != hipSuccess) break;
+    if ((e = hipMemcpyAsync(host.data(), po, n * sizeof(LazyPark), hipMemcpyDeviceToHost, st)) != hipSuccess ||
+        (e = hipStreamSynchronize(st)) != hipSuccess)
+      break;
     size_t built0 = L.nbuilt();
     for (const LazyPark &x : host)
       if (!(ok = L.build_row(x.s))) break;
