@@ -99,3 +99,26 @@ def test_suffix_bordered_keeps_lanes(cuda, pat):
     """a self-overlapping lcs ("ingi", "abab"): the greedy occurrence walk is
     not every occurrence, so the lane search answers"""
     _check(cuda, pat, 2, 300_000, 21, expect_path=(-5,))
+
+
+def test_suffix_walk_differs_from_forward(cuda):
+    """The reference's suffix walk is not the forward DFA's leftmost-first
+    search: `xa*ingb*ing|a+ing` over `xaaingbing` gives (1, 6) (the first
+    "ing" decides: `a+ing` ends there), where a forward search gives (0, 10).
+    Short haystacks (lane path) and a long one (units path) both follow the
+    reference (the oracle restates its walk)."""
+    import torch
+    pat = r"xa*ingb*ing|a+ing"
+    re = R.Regex(pat)
+    o = OracleRegex(re)
+    assert o.find(b"xaaingbing") == (1, 6)
+    short = b"xaaingbing" + b" " * 22
+    d = torch.from_numpy(np.frombuffer(short * 4 + b"\0" * 16, dtype=np.uint8).copy()).to(cuda)
+    got = re.find_batch(d, stride=len(short), length=len(short), count=4).cpu().numpy()
+    assert got.tolist() == [[1, 6]] * 4
+    L = 400_000
+    text = b"z" * (L - 100) + b"xaaingbing" + b"q" * 90
+    d = torch.from_numpy(np.frombuffer(text + b"\0" * 16, dtype=np.uint8).copy()).to(cuda)
+    got = re.find_batch(d, stride=L, length=L, count=1).cpu().numpy()[0].tolist()
+    assert got == list(o.find(text)) == [L - 99, L - 94]
+    assert N.rure_amd_last_fwd_path() == -9

@@ -80,3 +80,15 @@ def test_long_literals_second_filter():
     """Literals of >= 8 bytes get the bytes-4..7 bitmap (C3 variants)."""
     lits = R.Regex(r"agggtaa[cgt]|[acg]ttaccct").literals()
     assert min(len(x) for x in lits) >= 8
+
+
+def test_suffix_walk_quirk_in_oracle():
+    """MatchType::DfaSuffix (exec.rs:725-794) restated in the oracle: the
+    walk over the longest common suffix's occurrences decides at the first
+    "ing" of `xaaingbing` (`a+ing`, start 1), where a leftmost-first search
+    finds the longer `xa*ingb*ing` from 0."""
+    re = R.Regex(r"xa*ingb*ing|a+ing")
+    assert re.match_info()["match_type"] == "DfaSuffix"
+    o = OracleRegex(re)
+    assert o.find(b"xaaingbing") == (1, 6)
+    assert o.find_iter(b"xaaingbing xaing") == [(1, 6), (12, 16)]
