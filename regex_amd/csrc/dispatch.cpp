@@ -799,6 +799,20 @@ hipError_t run_find_iter(rure *re, DevTables *t, const BatchDev &b, const IterOu
     hipError_t e2 = scratch_free(found, st);
     return e != hipSuccess ? e : e2;
   }
+  // DfaSuffix over few long haystacks: the iteration over suffix occurrences
+  // in parallel (launch_suffix_iter); RURE_AMD_SUFFIX_ITER=0 keeps the wave
+  // path, =2 takes it at any length with 128-byte units (tests).
+  if (lane_search_ok(*t) && !sp && t->m.mt == MT_DFA_SUFFIX && t->lcs_free && !t->quit_possible && !b.offs &&
+      b.count && b.count < (uint64_t)t->cus * 16 && b.length > b.start) {
+    const char *v = getenv("RURE_AMD_SUFFIX_ITER");
+    const uint64_t span = b.length - b.start;
+    if (!(v && v[0] == '0') && (span >= (256u << 10) || (v && v[0] == '2'))) {
+      const uint64_t per_h = ((uint64_t)t->cus * 1024 + b.count - 1) / b.count;
+      const uint64_t chunk = odd_lines(std::max<uint64_t>(v && v[0] == '2' ? 128 : 16u << 10, (span + per_h - 1) / per_h));
+      const hipError_t e = launch_suffix_iter(b, t->m, t->f, t->r, chunk, o, st, t->cus);
+      if (e != hipErrorNotSupported) return e;
+    }
+  }
   // The reference's Literal / DfaSuffix searches (DevTables::mt_lane): every
   // search of the iteration is one of those, on a wave per haystack (lane 0
   // searches, the wave runs the Pike VM where a DfaSuffix scan quits).

@@ -324,6 +324,13 @@ hipError_t launch_lane_search(int mode, const BatchDev &b, const MatchDev &m, co
 // into out where the reverse suffix scans decide; status[h] = 3 where the
 // reference falls back to the forward DFA (the caller runs it).  Needs a
 // longest common suffix that cannot overlap itself.
+// find_iter of a DfaSuffix regex over few long fixed-stride haystacks
+// (match_types.hip): every suffix occurrence's slice scanned once, each
+// search's match and successor per occurrence, the iteration's searches
+// marked by pointer doubling.  hipErrorNotSupported: nothing written (a
+// reverse scan quit), the caller runs the wave path.
+hipError_t launch_suffix_iter(const BatchDev &b, const MatchDev &m, const FwdDfaDev &f, const RevDfaDev &r,
+                              uint64_t chunk, const IterOut &o, hipStream_t st, int cus);
 hipError_t launch_suffix_long(int mode, const BatchDev &b, const MatchDev &m, const FwdDfaDev &f,
                               const RevDfaDev &r, uint64_t chunk, void *out, uint8_t *status, hipStream_t st,
                               int cus);
