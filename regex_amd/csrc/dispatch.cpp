@@ -802,7 +802,9 @@ hipError_t run_find_iter(rure *re, DevTables *t, const BatchDev &b, const IterOu
   // DfaSuffix over few long haystacks: the iteration over suffix occurrences
   // in parallel (launch_suffix_iter); RURE_AMD_SUFFIX_ITER=0 keeps the wave
   // path, =2 takes it at any length with 128-byte units (tests).
-  if (lane_search_ok(*t) && !sp && t->m.mt == MT_DFA_SUFFIX && t->lcs_free && !t->quit_possible && !b.offs &&
+  // (a DFA that can quit: the path gives up on the first quit, the wave path
+  // then runs with its Pike VM fallback)
+  if (lane_search_ok(*t) && !sp && t->m.mt == MT_DFA_SUFFIX && t->lcs_free && !b.offs &&
       b.count && b.count < (uint64_t)t->cus * 16 && b.length > b.start) {
     const char *v = getenv("RURE_AMD_SUFFIX_ITER");
     const uint64_t span = b.length - b.start;

@@ -29,12 +29,14 @@ class QuitError(Exception):
     pass
 
 
-def find(fwd, rev, t, start=0, mode="find", cut=None, fb=None):
+def find(fwd, rev, t, start=0, mode="find", cut=None, fb=None, out=None):
     """cut: the search may not start a match at or after `cut` (the kernel's
     dfa_find_cut: the state at cut - 1 is replaced by its stripped copy).
     fb: the first-byte start rule's bytes (iter_scan.hip, host
     first_byte_rule): when the scan ended in the dead state and every byte it
-    read was ASCII, the start is the first fb byte at or after `start`."""
+    read was ASCII, the start is the first fb byte at or after `start`.
+    out: a dict; out["reached"] says the reverse scan reached `start` alive
+    (its answer then depends on where the search began: the slice quirk)."""
     info, tr, eof, st = fwd
     s = int(st[fwd_flag(t, start)])
     last = None
@@ -74,6 +76,8 @@ def find(fwd, rev, t, start=0, mode="find", cut=None, fb=None):
     if last is None:
         return None
     if last == start:
+        if out is not None:
+            out["reached"] = True
         return (start, start)
     if fb and done and all(b < 0x80 for b in t[start:at + 1]):
         return (next(i for i in range(start, last) if t[i] in fb), last)
@@ -95,6 +99,10 @@ def find(fwd, rev, t, start=0, mode="find", cut=None, fb=None):
                 raise QuitError()
     if not dead and reof[s]:
         rs = start
+    if out is not None:
+        out["reached"] = not dead
+    if out is not None:
+        out["stop"] = rs is None  # a NoMatch that ends the reference's iteration
     if rs is None:  # exec.rs:656-660: the reverse DFA over text[start..] found no start -> NoMatch
         return None
     return (rs, last)

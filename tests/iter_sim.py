@@ -5,6 +5,7 @@ TEST INFRASTRUCTURE: validates the boundary-repair algorithm on CPU."""
 from dfa_sim import find
 
 NONE = None
+STOP = float("inf")  # the exit of an iteration that ended (a search's NoMatch)
 
 
 class UnitIter(object):
@@ -18,14 +19,28 @@ class UnitIter(object):
         self.ended = False
         self.clean = False
         self.exit = None
+        # the first search's reverse scan reached the entry alive: with
+        # look-around its answer depends on where the search began (the
+        # reverse slice starts there, dfa_sim.find), so a speculation entered
+        # fresh is not equivalent to the true iteration entering earlier
+        self.unsure = False
+        self.first = True
+        self.stop = False
 
     def _iter_next(self):
         t = self.t
         while True:
             if self.p > len(t):
                 return None
-            m = find(self.fwd, self.rev, t, self.p, cut=self.c1, fb=self.fb)
+            out = {}
+            m = find(self.fwd, self.rev, t, self.p, cut=self.c1, fb=self.fb, out=out)
+            if self.first:
+                self.unsure = out.get("reached", False)
+                self.first = False
             if m is None:
+                # the reverse scan found no start (look-around at the slice
+                # start): the reference's iteration ends here
+                self.stop = out.get("stop", False)
                 return None
             s, e = m
             if s == e:
@@ -39,6 +54,9 @@ class UnitIter(object):
 
     def next(self):
         if self.ended:
+            return None
+        if self.p == STOP:
+            self.ended, self.exit, self.clean = True, (STOP, None), False
             return None
         if self.p >= self.c1:
             self.ended = True
@@ -54,16 +72,23 @@ class UnitIter(object):
         self.ended = True
         self.exit = snap
         self.clean = True
+        if m is None and self.stop:
+            self.exit, self.clean = (STOP, None), False
         return None
 
 
-def equiv(ca, a, cb, b):
+def equiv(ca, a, cb, b, strict=False):
+    """two unit exits lead the next unit alike: both clean (a fresh start at
+    its c0) or the same state; strict (the next unit's speculation is unsure)
+    takes only the same state"""
+    if strict:
+        return a == b
     if ca or cb:
         return ca and cb
     return a == b
 
 
-def find_iter_chunked(fwd, rev, t, chunk, start=0, slots=1 << 30, fb=None):
+def find_iter_chunked(fwd, rev, t, chunk, start=0, slots=1 << 30, fb=None, looks=False):
     INF = float("inf")
     span = max(0, len(t) - start)
     nk = 1 if span <= chunk else (span + chunk - 1) // chunk
@@ -78,6 +103,7 @@ def find_iter_chunked(fwd, rev, t, chunk, start=0, slots=1 << 30, fb=None):
                 break
             ms.append(m)
         units.append({"entry": (c0, None), "spec": ms, "spec_exit": it.exit, "spec_clean": it.clean,
+                      "unsure": looks and k > 0 and it.unsure,
                       "exit": it.exit, "clean": it.clean, "fixed": False, "count": len(ms)})
 
     def sync_from_slots(j, E):
@@ -86,7 +112,7 @@ def find_iter_chunked(fwd, rev, t, chunk, start=0, slots=1 << 30, fb=None):
         c0, c1 = bounds[j]
         U = units[j]
         spec = U["spec"]
-        if len(spec) > slots or E[0] < c0:
+        if looks or len(spec) > slots or E[0] < c0:
             return None
         # p_i, lm_i: S's iteration state before it yielded match i
         ps, lms = [c0], [None]
@@ -107,6 +133,9 @@ def find_iter_chunked(fwd, rev, t, chunk, start=0, slots=1 << 30, fb=None):
             return i
         return i if U["spec_clean"] else None
 
+    def strict(j):
+        return j + 1 < nk and units[j + 1]["unsure"]
+
     def repair(j, E):
         c0, c1 = bounds[j]
         U = units[j]
@@ -114,7 +143,7 @@ def find_iter_chunked(fwd, rev, t, chunk, start=0, slots=1 << 30, fb=None):
         if E[0] >= c1:  # the true iteration skips the whole unit
             U["count"], U["exit"] = 0, E
             U["clean"] = E[0] == c1 and E[1] != c1
-            return not equiv(U["clean"], U["exit"], U["spec_clean"], U["spec_exit"])
+            return not equiv(U["clean"], U["exit"], U["spec_clean"], U["spec_exit"], strict(j))
         i = sync_from_slots(j, E)
         if i is not None:
             if i < len(U["spec"]):
@@ -122,7 +151,7 @@ def find_iter_chunked(fwd, rev, t, chunk, start=0, slots=1 << 30, fb=None):
                 U["exit"], U["clean"] = U["spec_exit"], U["spec_clean"]
                 return False
             U["count"], U["exit"], U["clean"] = 0, E, True
-            return not equiv(True, E, U["spec_clean"], U["spec_exit"])
+            return not equiv(True, E, U["spec_clean"], U["spec_exit"], strict(j))
         F = UnitIter(fwd, rev, t, E, c1)
         S = UnitIter(fwd, rev, t, (c0, None), c1)
         fm, sm = F.next(), S.next()
@@ -145,7 +174,7 @@ def find_iter_chunked(fwd, rev, t, chunk, start=0, slots=1 << 30, fb=None):
             U["exit"], U["clean"] = U["spec_exit"], U["spec_clean"]
             return False
         U["count"] = fcnt
-        changed = not equiv(F.clean, F.exit, U["spec_clean"], U["spec_exit"])
+        changed = not equiv(F.clean, F.exit, U["spec_clean"], U["spec_exit"], strict(j))
         U["exit"], U["clean"] = F.exit, F.clean
         return changed
 
@@ -154,7 +183,7 @@ def find_iter_chunked(fwd, rev, t, chunk, start=0, slots=1 << 30, fb=None):
 
     queue = []
     for u in range(nk - 1):  # pass 2: parallel repair
-        if not units[u]["spec_clean"]:
+        if not units[u]["spec_clean"] or units[u + 1]["unsure"]:
             if repair(u + 1, units[u]["spec_exit"]):
                 queue.append(u + 1)
     walked = 0  # pass 3: sequential walker
@@ -165,9 +194,9 @@ def find_iter_chunked(fwd, rev, t, chunk, start=0, slots=1 << 30, fb=None):
         X = units[j]
         while u < nk:
             P = units[u - 1]
-            if equiv(X["clean"], X["exit"], P["spec_clean"], P["spec_exit"]):
+            if equiv(X["clean"], X["exit"], P["spec_clean"], P["spec_exit"], strict(u - 1)):
                 break
-            if X["clean"]:
+            if X["clean"] and not units[u]["unsure"]:
                 W = units[u]
                 W["entry"], W["exit"], W["clean"], W["fixed"], W["count"], W["skip"] = \
                     (bounds[u][0], None), W["spec_exit"], W["spec_clean"], False, len(W["spec"]), None

@@ -78,6 +78,28 @@ def test_suffix_iter_small_units(cuda, pat, start):
         del os.environ["RURE_AMD_SUFFIX_ITER"]
 
 
+def test_suffix_iter_quit_falls_back(cuda):
+    r"""Unicode \b (a DFA that can quit): ASCII text stays on the parallel
+    path; a non-ASCII byte next to a slice makes it give up to the wave path
+    (its Pike VM answers), with the same results as the oracle"""
+    import torch
+    pat = r"\bx[a-z]*ing"
+    re = R.Regex(pat)
+    assert re.match_info()["match_type"] == "DfaSuffix"
+    o = OracleRegex(re)
+    L = 300_000
+    text = bytearray(_text(L, 77).replace(b"\xc3\xa9", b"ee"))
+    text = bytes(b if b < 0x80 else 0x20 for b in text)
+    for t in (text, text[:1000] + "é".encode() + b"xaing " + text[1008:]):
+        t = t[:L]
+        d = torch.from_numpy(np.frombuffer(t + b"\0" * 16, dtype=np.uint8).copy()).to(cuda)
+        counts, m = re.find_iter_batch(d, stride=L, length=L, count=1)
+        got = [tuple(x) for x in m.cpu().numpy().tolist()]
+        assert got == o.find_iter(t), pat
+        if t == text:
+            assert N.rure_amd_last_fwd_path() == -11, pat
+
+
 def test_suffix_iter_capacity_and_empty(cuda):
     import torch
     os.environ["RURE_AMD_SUFFIX_ITER"] = "2"

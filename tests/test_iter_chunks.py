@@ -84,3 +84,30 @@ def test_first_byte_rule(pat):
 def test_first_byte_rule_rejects():
     for pat in [r"abc|ab", r"\w+", r"\d{4}-\d{2}-\d{2}", r"x*", r"agggtaaa|tttaccct", r"a\b"]:
         assert R.Regex(pat).first_bytes() is None, pat
+
+
+LOOK_PATTERNS = [r"(?-u)\b[a-c]+\b", r"(?-u)\bx", r"(?m)^a+", r"(?m)a+$", r"(?-u)a\B", r"(?-u)\B[ab]+", r"(?m)^$",
+                 r"(?-u)\b", r"(?m)^", r"(?-u)[a-d]*\bd", r"a+\z", r"(?-u)\b\w+@\w+", r"(?-u)\B\w+",
+                 r"(?-u)[a-c]*\B[ab]", r"(?m)a*^b", r"(?-u)\B", r"(?-u)\B[a-d]*\b", r"(?m)(?-u)$|\b",
+                 r"(?-u)\b|\B[ab]", r"(?-u)[a-d]\B|x", r"(?m)[ab]*$", r"(?m)^[^\n]*$", r"(?m)^>.*$",
+                 r"(?-u)\bd\b|\Ba", r"(?m)(?-u)^\w*\b"]
+
+
+@pytest.mark.parametrize("pat", LOOK_PATTERNS)
+def test_chunked_iter_look_around(pat):
+    """Look-around: a search's reverse scan over [p, e) reads the slice start
+    p as the text's start (exec.rs:656-660 runs it over text[p..e]), so a
+    speculation entered fresh at a unit's c0 is exact only when its first
+    reverse scan died before c0 (else the unit is repaired from the true
+    entry), a NoMatch from the reverse scan ends the whole iteration, and
+    exits compare strictly ahead of such a unit."""
+    re = R.Regex(pat)
+    assert re.nfa_tables()[0]["looks"] != 0
+    fwd = re.dfa_tables(2)
+    rev = re.dfa_tables(1)
+    o = OracleRegex(re)
+    for i in range(12):
+        t = (text if i % 2 else mixed_text)(zlib.crc32(pat.encode()) + i, 40 + 23 * i)
+        exp = o.find_iter(t)
+        for chunk in (1, 2, 3, 7, 16):
+            assert find_iter_chunked(fwd, rev, t, chunk, looks=True) == exp, (pat, chunk, i)
