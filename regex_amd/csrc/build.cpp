@@ -1124,6 +1124,21 @@ const FwdDfaDev *iter_device(rure *re, const DevTables &t, std::string *err) {
     f.sa_len = sa_len;
     f.sa_bits = sa_bits;
   }
+  if (re->nt.looks_used || t.quit_possible) {
+    // look-around: the chunked iteration's slice rules (iter_scan.hip); the
+    // literal / Shift-And / lexer engines and the first-byte start rule read
+    // no assertions and skip the reverse scan, so they are off
+    f.looks = re->nt.looks_used ? 1 : 0;
+    f.can_quit = t.quit_possible ? 1 : 0;
+    f.fb_n = 0;
+    f.lit_image = nullptr;
+    f.lit_n = 0;
+    f.lex_image = nullptr;
+    f.lex_bytes = 0;
+    f.lex4_image = nullptr;
+    f.sa_image = nullptr;
+    f.sa_len = f.sa_bits = 0;
+  }
   re->iter_dev[d] = {tmp.blob, f};
   return &re->iter_dev[d].second;
 }

@@ -820,10 +820,17 @@ hipError_t run_find_iter(rure *re, DevTables *t, const BatchDev &b, const IterOu
   // searches, the wave runs the Pike VM where a DfaSuffix scan quits).
   if (lane_search_ok(*t) && re->nfa_ok)
     return launch_find_iter(b, t->has_dfa ? &t->f : nullptr, t->r, &t->n, false, 0, o, st, t->cus, sp, &t->m);
-  // Chunked speculative iteration needs a DFA that cannot quit and a pattern
-  // without assertions (see iter_scan.hip); otherwise one wave per haystack.
+  // Chunked speculative iteration (iter_scan.hip); otherwise one wave per
+  // haystack.  With look-around (or a DFA that can quit) it needs the
+  // stripped states (not an anchored regex) and a whole haystack (no span:
+  // a span's "fresh" exit is not enough to enter the next); a quit sends the
+  // batch to the wave path.  RURE_AMD_ITER_LOOKS=0 keeps those on the wave
+  // path (A/B).
   const FwdDfaDev *fi = nullptr;
-  if (t->has_dfa && !t->quit_possible && re->nfa_ok && re->nt.looks_used == 0) fi = iter_device(re, *t, err);
+  const bool looks = re->nt.looks_used != 0 || t->quit_possible;
+  const char *lv = getenv("RURE_AMD_ITER_LOOKS");
+  if (t->has_dfa && re->nfa_ok && (!looks || (!sp && !(lv && lv[0] == '0')))) fi = iter_device(re, *t, err);
+  if (fi && looks && re->dfwd_iter.strip.empty()) fi = nullptr;
   if (fi) {
     uint64_t chunk = ~0ull >> 2;
     const uint64_t lim = sp ? std::min<uint64_t>(b.length, sp->hi) : b.length;
@@ -836,8 +843,15 @@ hipError_t run_find_iter(rure *re, DevTables *t, const BatchDev &b, const IterOu
       const uint64_t target = (uint64_t)t->cus * per_cu;
       const uint64_t per_h = (target + b.count - 1) / b.count;
       chunk = odd_lines(std::max<uint64_t>(4096, (span + per_h - 1) / per_h));
+      // RURE_AMD_ITER_CHUNK: the unit size in bytes (tests: many boundaries)
+      if (const char *v = getenv("RURE_AMD_ITER_CHUNK")) chunk = std::max<uint64_t>(16, strtoull(v, nullptr, 10));
     }
-    return launch_find_iter(b, fi, t->r, &t->n, true, chunk, o, st, t->cus, sp);
+    bool quit = false;
+    const hipError_t e = launch_find_iter(b, fi, t->r, &t->n, true, chunk, o, st, t->cus, sp, nullptr, &quit);
+    // last_fwd_path: -12 = the chunked iteration of a look-around regex
+    // answered, -13 = it quit (the wave path answers)
+    if (looks && e == hipSuccess) note_fwd_path(quit ? -13 : -12);
+    if (e != hipSuccess || !quit) return e;
   }
   if (!re->nfa_ok) return hipErrorInvalidValue;
   return launch_find_iter(b, t->has_dfa ? &t->f : nullptr, t->r, &t->n, false, 0, o, st, t->cus, sp);

@@ -179,9 +179,12 @@ __device__ __forceinline__ void chunk16s(LaneState &L, const FwdDfaDev &f, const
 // forward one) ordinary steps stay in LDS.
 // QAM (quit_after_match, dfa.rs:805-812): return at the first match flag
 // (is_match / shortest_match of DfaAnchoredReverse; any match position).
+// reached (optional): set when the scan got to `lo` alive, i.e. its answer
+// may depend on where the slice starts (with look-around, the EOF step at lo
+// reads lo as the text's start).
 template <bool QAM = false>
 __device__ __forceinline__ uint64_t rev_scan(const RevDfaDev &r, const uint8_t *rlds, const uint8_t *base,
-                                             uint64_t len, uint64_t lo, uint64_t me) {
+                                             uint64_t len, uint64_t lo, uint64_t me, bool *reached = nullptr) {
   uint32_t s = r.ustart1 ? r.ustart1 - 1 : r.start[rev_flag_index(base, lo, len, me)];
   if (s == r.dead) return NONE;
   const uint32_t hot = rlds ? r.hot : 0;
@@ -217,6 +220,7 @@ __device__ __forceinline__ uint64_t rev_scan(const RevDfaDev &r, const uint8_t *
       }
     }
   }
+  if (reached) *reached = true;
   if (r.eof[s]) rs = lo;
   return rs;
 }
@@ -341,9 +345,14 @@ __device__ __forceinline__ int dfa_find(const FwdDfaDev &f, const RevDfaDev &r, 
 // the cut has been decided.  Used by the chunked find_iter: its result equals
 // the unrestricted search whenever that search's match starts before the cut,
 // and is "no match" otherwise.
+// With look-around (f.looks): returns 3 when the reverse scan finds no start
+// (exec.rs:656-660: the search's NoMatch, which ends the reference's
+// iteration), and *reached (optional) says whether the answer may depend on
+// the search start `at` (the reverse scan got to it alive, or the match is
+// empty at it).
 __device__ __forceinline__ int dfa_find_cut(const FwdDfaDev &f, const RevDfaDev &r, const uint8_t *lds,
                                             const uint8_t *rlds, const uint8_t *base, uint64_t len, uint64_t at,
-                                            uint64_t cut, uint64_t *ms, uint64_t *me) {
+                                            uint64_t cut, uint64_t *ms, uint64_t *me, bool *reached = nullptr) {
   LaneState L;
   lane_start(L, f, base, len, at);
   if (cut > at && cut - 1 <= len) {
@@ -360,10 +369,14 @@ __device__ __forceinline__ int dfa_find_cut(const FwdDfaDev &f, const RevDfaDev 
   if (L.quit) return 2;
   if (L.last == NONE) return 0;
   *me = L.last;
-  if (L.last == at) { *ms = at; return 1; }
-  const uint64_t rs = rev_scan(r, rlds, base, len, at, L.last);
+  if (L.last == at) {
+    if (reached) *reached = true;
+    *ms = at;
+    return 1;
+  }
+  const uint64_t rs = rev_scan(r, rlds, base, len, at, L.last, reached);
   if (rs == QUITMARK) return 2;
-  if (rs == NONE) return 0;
+  if (rs == NONE) return f.looks ? 3 : 0;
   *ms = rs;
   return 1;
 }

@@ -104,6 +104,12 @@ struct FwdDfaDev {
   // that hold none of those bytes (fwd_range); pfx_n = 0: off.
   uint32_t pfx_n;
   uint32_t pfx_rep[4];
+  // find_iter DFA only: the regex has look-around assertions (the chunked
+  // iteration then repairs units whose first reverse scan reached their
+  // start, and a reverse NoMatch ends the iteration; iter_scan.hip), and its
+  // DFA can quit (Unicode word boundary: a quit sends the batch to the wave
+  // path).  The literal, Shift-And, lexer and first-byte engines are off.
+  uint32_t looks, can_quit;
 };
 constexpr uint32_t kLexMaxRows = 24;  // lexer table rows (iter_spec_lex_tile_kernel's static LDS)
 constexpr uint32_t kLexUnit = kRow / 4;  // lexer entry -> row address multiplier
@@ -285,7 +291,10 @@ struct IterSpan {
 };
 hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaDev &r, const NfaDev *nf,
                             bool chunked, uint64_t chunk, const IterOut &o, hipStream_t st, int cus,
-                            const IterSpan *span = nullptr, const MatchDev *mt = nullptr);
+                            const IterSpan *span = nullptr, const MatchDev *mt = nullptr, bool *quit = nullptr);
+// (quit: chunked with a DFA that can quit, f->can_quit; set when a search
+// quit, the outputs then being void: the caller runs the wave path.  Reads
+// the flag back, so the call synchronises the stream.)
 // The k-mer probe engine of launch_find_iter_multi: the regexes' strings all
 // have one length len <= 8 over an alphabet of at most 4 bytes whose codes
 // (b >> shift) & 3 are distinct.  bitmap: 2048 u32, bit c set iff the L-mer

@@ -47,12 +47,29 @@ enum : uint32_t {
   U_SPEC_CLEAN = 1,   // speculative exit is equivalent to a fresh start at the next unit
   U_CLEAN = 2,        // final exit clean
   U_FIXED = 4,        // final entry differs from the speculative one
-  U_QUIT = 8,         // a search quit (cannot happen on the chunked path)
+  U_QUIT = 8,         // a search quit (sticky: the batch then goes to the wave path; f.can_quit only)
   U_COPY = 16,        // fixed, and its matches are slots[skip, skip + count)
   U_LEX_TAIL = 32,    // iter_spec_lex_tile_kernel: exit = the lexer's iteration state, the tail pass finishes
   U_COMPACT = 64,     // the lexer's slots: its pad (= its count) records as u32 start - c0 | end - c0 << 16,
                       // then the tail pass's as absolute ulonglong2 from the back (lex_rec32 / lex_row16)
+  U_UNSURE = 128,     // look-around: the speculation's first reverse scan reached c0, so the true
+                      // iteration entering earlier may differ even after a clean exit (repaired always)
 };
+
+// Look-around (FwdDfaDev::looks).  A search from p runs its reverse scan over
+// text[p..e] (exec.rs:651-661), whose EOF step reads p as the start of the
+// text: the start it reports may depend on p, not only on the match.  So
+//  - a unit's speculation (a fresh search at c0) equals the true iteration
+//    entering earlier only when its first reverse scan died before reaching
+//    c0 (U_UNSURE otherwise: repaired from the true entry like a dirty one);
+//  - two exits are interchangeable ahead of an U_UNSURE unit only when they
+//    are the same state (exit_equiv strict), and the join shortcut
+//    (join_speculation) is off;
+//  - a reverse NoMatch (dfa_find_cut 3) ends the reference's iteration: the
+//    exit is kIterStop and every later unit of the haystack yields nothing.
+// tests/iter_sim.py models this; tests/test_iter_chunks.py checks it against
+// the oracle with one-byte units.
+static constexpr uint64_t kIterStop = ~0ull - 1;
 
 struct IterSt {
   uint64_t p, lm;  // next search start; end of the last match (NONE if none)
@@ -120,11 +137,14 @@ __device__ __forceinline__ void unit_bounds(const BatchDev &b, const Geo &g, uin
 
 // One step of re_trait.rs:197-221 (empty-match rule: next search at e + 1,
 // an empty match at the previous match end is skipped).
+// reached: the first search's dfa_find_cut reach flag (look-around).
 __device__ int iter_next(const FwdDfaDev &f, const RevDfaDev &r, const uint8_t *lds, const uint8_t *rlds,
-                         const uint8_t *base, uint64_t len, uint64_t cut, IterSt &st, uint64_t *s, uint64_t *e) {
+                         const uint8_t *base, uint64_t len, uint64_t cut, IterSt &st, uint64_t *s, uint64_t *e,
+                         bool *reached = nullptr) {
   while (true) {
     if (st.p > len) return 0;
-    const int k = dfa_find_cut(f, r, lds, rlds, base, len, st.p, cut, s, e);
+    const int k = dfa_find_cut(f, r, lds, rlds, base, len, st.p, cut, s, e, reached);
+    reached = nullptr;
     if (k != 1) return k;
     if (*s == *e) {
       st.p = *e + 1;
@@ -143,18 +163,25 @@ struct UnitIter {
   uint64_t c1;
   uint64_t from;  // the first search may scan from here: no match starts in [st.p, from)
   bool ended, clean, quit;
+  bool first, unsure;  // look-around: the first search's reverse scan reached its start
   IterSt exit;
 
   __device__ void init(IterSt s0, uint64_t cut) {
     st = s0;
     c1 = cut;
     from = 0;
-    ended = clean = quit = false;
+    ended = clean = quit = unsure = false;
+    first = true;
   }
   // Returns true with the next owned match, false when the unit is finished.
   __device__ bool next(const FwdDfaDev &f, const RevDfaDev &r, const uint8_t *lds, const uint8_t *rlds,
                        const uint8_t *base, uint64_t len, uint64_t *s, uint64_t *e) {
     if (ended) return false;
+    if (st.p == kIterStop) {  // the iteration ended (look-around: a reverse NoMatch)
+      ended = true;
+      exit = st;
+      return false;
+    }
     if (st.p >= c1) {  // the previous match ran up to / past the cut
       ended = true;
       exit = st;
@@ -167,8 +194,16 @@ struct UnitIter {
     // look-around and never match empty); its state stays st's
     IterSt q = st;
     if (q.p < from) q.p = from;
-    const int k = iter_next(f, r, lds, rlds, base, len, c1, q, s, e);
+    bool reached = false;
+    const int k = iter_next(f, r, lds, rlds, base, len, c1, q, s, e, first ? &reached : nullptr);
+    if (first) unsure = reached;
+    first = false;
     if (k == 1 && *s < c1) { st = q; return true; }
+    if (k == 3) {  // look-around: this search's NoMatch ends the iteration
+      ended = true;
+      exit = {kIterStop, NONE};
+      return false;
+    }
     // no match starts before the cut (the search is cut-bounded, see
     // dfa_find_cut): a fresh search at the cut finds what the unrestricted
     // one would (no assertions on this path)
@@ -180,7 +215,9 @@ struct UnitIter {
   }
 };
 
-__device__ __forceinline__ bool exit_equiv(bool ca, const IterSt &a, bool cb, const IterSt &b) {
+// strict: the next unit is U_UNSURE (only the same state enters it alike)
+__device__ __forceinline__ bool exit_equiv(bool ca, const IterSt &a, bool cb, const IterSt &b, bool strict = false) {
+  if (strict) return a.p == b.p && a.lm == b.lm;
   if (ca || cb) return ca && cb;
   return a.p == b.p && a.lm == b.lm;
 }
@@ -222,11 +259,12 @@ __global__ __launch_bounds__(1024) void iter_spec_kernel(BatchDev b, Geo g, uint
     U.exit = it.exit;
     U.spec_exit = it.exit;
     U.spec_count = n;
-    U.flags = (it.clean ? (U_SPEC_CLEAN | U_CLEAN) : 0) | (it.quit ? U_QUIT : 0);
+    U.flags = (it.clean ? (U_SPEC_CLEAN | U_CLEAN) : 0) | (it.quit ? U_QUIT : 0) |
+              (f.looks && it.unsure && u % g.nk != 0 ? U_UNSURE : 0);
     U.skip = U.pad = 0;
     units[u] = U;
     counts[u] = n;
-    if (!(U.flags & U_SPEC_CLEAN)) atomicOr(dirty, 1u);  // the fix pass has work
+    if ((U.flags & (U_SPEC_CLEAN | U_UNSURE)) != U_SPEC_CLEAN) atomicOr(dirty, 1u);  // the fix pass has work
   }
 }
 
@@ -1615,20 +1653,22 @@ __device__ bool repair_unit(const BatchDev &b, const Geo &g, const FwdDfaDev &f,
   unit_bounds(b, g, j, &h, &base, &len, &c0, &c1);
   Unit U = units[j];
   const bool spec_clean = (U.flags & U_SPEC_CLEAN) != 0;
+  // the next unit's speculation is unsure: exits compare as states
+  const bool strict = f.looks && (j + 1) % g.nk != 0 && (units[j + 1].flags & U_UNSURE);
   U.entry = E;
-  U.flags = (U.flags & ~(U_COPY | U_CLEAN | U_QUIT)) | U_FIXED;
+  U.flags = (U.flags & ~(U_COPY | U_CLEAN)) | U_FIXED;
   U.skip = 0;
   bool changed;
   if (E.p >= c1) {  // the true iteration passes over the whole unit
     const bool cl = E.p == c1 && (E.lm != c1 || f.nonempty);
     counts[j] = 0;
-    changed = !exit_equiv(cl, E, spec_clean, U.spec_exit);
+    changed = !exit_equiv(cl, E, spec_clean, U.spec_exit, strict);
     U.exit = E;
     U.flags |= cl ? U_CLEAN : 0;
     units[j] = U;
     return changed;
   }
-  const int64_t i = join_speculation(U, c0, E, slots, g, j);
+  const int64_t i = f.looks ? -1 : join_speculation(U, c0, E, slots, g, j);
   if (i >= 0) {
     if (i < (int64_t)U.spec_count) {
       counts[j] = U.spec_count - (uint32_t)i;
@@ -1674,10 +1714,11 @@ __device__ bool repair_unit(const BatchDev &b, const Geo &g, const FwdDfaDev &f,
     changed = false;
   } else {
     counts[j] = fcnt;
-    changed = !exit_equiv(F.clean, F.exit, spec_clean, U.spec_exit);
+    changed = !exit_equiv(F.clean, F.exit, spec_clean, U.spec_exit, strict);
     U.exit = F.exit;
-    U.flags |= (F.clean ? U_CLEAN : 0) | (F.quit ? U_QUIT : 0);
+    U.flags |= (F.clean ? U_CLEAN : 0);
   }
+  U.flags |= (F.quit || S.quit) ? U_QUIT : 0;
   units[j] = U;
   return changed;
 }
@@ -1695,7 +1736,8 @@ __device__ __forceinline__ void fix_body(const BatchDev &b, const Geo &g, uint64
   bool staged = false;
   for (uint64_t u0 = (uint64_t)blockIdx.x * blockDim.x; u0 + 1 < nunits; u0 += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t u = u0 + threadIdx.x;
-    const bool need = u + 1 < nunits && (u + 1) % g.nk != 0 && !(units[u].flags & U_SPEC_CLEAN);
+    const bool need = u + 1 < nunits && (u + 1) % g.nk != 0 &&
+                      (!(units[u].flags & U_SPEC_CLEAN) || (units[u + 1].flags & U_UNSURE));
     if (!__syncthreads_or(need)) continue;
     if (!staged) {
       rlds = stage_tables(f, r, lds);
@@ -1738,15 +1780,16 @@ __device__ __forceinline__ void walk_body(const BatchDev &b, const Geo &g, uint6
       // entry the parallel passes assumed for unit u
       const Unit P = units[u - 1];
       const bool assumed_clean = (P.flags & U_SPEC_CLEAN) != 0;
-      if (exit_equiv((X.flags & U_CLEAN) != 0, X.exit, assumed_clean, P.spec_exit)) break;
+      const bool unsure = (V.flags & U_UNSURE) != 0;
+      if (exit_equiv((X.flags & U_CLEAN) != 0, X.exit, assumed_clean, P.spec_exit, unsure)) break;
       Unit W = V;
-      if (X.flags & U_CLEAN) {  // back to the speculative entry
+      if ((X.flags & U_CLEAN) && !unsure) {  // back to the speculative entry
         uint64_t h, len, c0, c1;
         const uint8_t *base;
         unit_bounds(b, g, u, &h, &base, &len, &c0, &c1);
         W.entry = {c0, NONE};
         W.exit = W.spec_exit;
-        W.flags = (W.flags & ~(U_FIXED | U_CLEAN | U_COPY | U_QUIT)) | ((W.flags & U_SPEC_CLEAN) ? U_CLEAN : 0);
+        W.flags = (W.flags & ~(U_FIXED | U_CLEAN | U_COPY)) | ((W.flags & U_SPEC_CLEAN) ? U_CLEAN : 0);
         W.skip = 0;
         units[u] = W;
         counts[u] = W.spec_count;
@@ -1758,6 +1801,14 @@ __device__ __forceinline__ void walk_body(const BatchDev &b, const Geo &g, uint6
     }
     walked = u;
   }
+}
+
+// Whether a search of the chunked iteration quit (U_QUIT is sticky).
+__global__ void iter_quit_kernel(const Unit *units, uint64_t nunits, uint32_t *quit) {
+  bool any = false;
+  for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < nunits; u += (uint64_t)gridDim.x * blockDim.x)
+    any |= (units[u].flags & U_QUIT) != 0;
+  if (any) atomicOr(quit, 1u);
 }
 
 __global__ void iter_walk_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r, Unit *units,
@@ -2770,7 +2821,7 @@ hipError_t launch_find_iter_multi(const BatchDev &b, int nre, const FwdDfaDev *c
 
 hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaDev &r, const NfaDev *nf,
                             bool chunked, uint64_t chunk, const IterOut &o, hipStream_t st, int cus,
-                            const IterSpan *spn, const MatchDev *mtd) {
+                            const IterSpan *spn, const MatchDev *mtd, bool *quit) {
   const uint64_t hi = spn ? spn->hi : ~0ull;
   hipError_t e = hipSuccess;
   if (b.count == 0) {
@@ -2863,7 +2914,7 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
         else
           hipLaunchKernelGGL((iter_spec_lit_kernel<false, false>), lg, dim3(bs), kLitImage, st, b, g, nunits, *f,
                              units, slots, counts, dirty);
-      } else if (!getenv("RURE_AMD_ITER_NESTED")) {
+      } else if (!getenv("RURE_AMD_ITER_NESTED") && !f->looks) {
         hipLaunchKernelGGL(iter_spec_burst_kernel, dim3(grid), dim3(bs), iter_lds_bytes(*f, r), st, b, g, nunits, *f,
                            r, units, slots, counts, dirty);
       } else {
@@ -2873,6 +2924,15 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
       if (!use_lex) ktimer_end(st);
       if ((e = hipGetLastError()) != hipSuccess) break;
       e = iter_post(b, g, nunits, *f, r, sc, o, spn, st, cus, use_lex);
+      if (e == hipSuccess && f->can_quit && quit) {  // did any search quit?
+        uint32_t q = 0;
+        if ((e = hipMemsetAsync(dirty, 0, 4, st)) != hipSuccess) break;
+        hipLaunchKernelGGL(iter_quit_kernel, dim3(grid_cap(nunits, 256, cus, 4)), dim3(256), 0, st, units, nunits,
+                           dirty);
+        if ((e = hipMemcpyAsync(&q, dirty, 4, hipMemcpyDeviceToHost, st)) != hipSuccess) break;
+        if ((e = hipStreamSynchronize(st)) != hipSuccess) break;
+        *quit = q != 0;
+      }
     } while (false);
     hipError_t e2 = scratch_free(sc.buf, st);
     return e != hipSuccess ? e : e2;

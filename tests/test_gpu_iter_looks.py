@@ -1,0 +1,106 @@
+"""GPU parity of the chunked find_iter for regexes with look-around
+assertions (iter_scan.hip, FwdDfaDev::looks) against the oracle's sequential
+find_iter (re_trait.rs:197-221 over exec.rs:632-662), bit-exact.
+
+The reverse scan of each search runs over text[p..e] and reads p as the
+text's start (exec.rs:651-661), so these cases stress what the chunked
+iteration must reproduce: units whose first reverse scan reaches their start
+(repaired from the true entry), reverse NoMatches that end the iteration
+(\\B at a unit start), and Unicode word boundaries whose DFA quits on
+non-ASCII bytes (the batch then goes to the wave path: last_fwd_path -13).
+RURE_AMD_ITER_CHUNK forces small units (many boundaries)."""
+import os
+import random
+import zlib
+
+import numpy as np
+import pytest
+
+import regex_amd as R
+from regex_amd import _native as N
+from golden_data import corpus
+from oracle_py import OracleRegex
+
+pytestmark = pytest.mark.gpu
+
+ASCII_PATTERNS = [r"(?-u)\b[a-c]+\b", r"(?m)^a+", r"(?m)a+$", r"(?-u)\B[ab]+", r"(?m)^$", r"(?-u)\b",
+                  r"(?-u)[a-d]*\bd", r"a+\z", r"(?-u)\B\w+", r"(?-u)\b|\B[ab]", r"(?m)^[^\n]*$",
+                  r"(?-u)\bd\b|\Ba", r"(?m)(?-u)^\w*\b", r"(?-u)\B"]
+UNICODE_PATTERNS = [r"\b\w+\b", r"[a-z]+ed\b", r"\bthe\b", r"\B[a-z]{2}", r"(?m)^\w+"]
+
+
+def _text(seed, n, nonascii):
+    rng = random.Random(seed)
+    alpha = [b"a", b"b", b"c", b"d", b" ", b"\n", b"x", b"@", b"e", b"d "]
+    w = [8, 6, 5, 3, 6, 3, 2, 1, 3, 2]
+    if nonascii:
+        alpha += ["é".encode(), b"\xff"]
+        w += [1, 1]
+    return b"".join(rng.choices(alpha, weights=w, k=n))[:n]
+
+
+def _dev(buf, cuda):
+    import torch
+    return torch.from_numpy(np.frombuffer(buf + b"\0" * 16, dtype=np.uint8).copy()).to(cuda)
+
+
+def _run(re, buf, L, count, cuda, chunk):
+    os.environ["RURE_AMD_ITER_CHUNK"] = str(chunk)
+    try:
+        counts, m = re.find_iter_batch(_dev(buf, cuda), stride=L, length=L, count=count)
+        return counts.cpu().numpy().tolist(), [tuple(x) for x in m.cpu().numpy().tolist()], N.rure_amd_last_fwd_path()
+    finally:
+        del os.environ["RURE_AMD_ITER_CHUNK"]
+
+
+def _check(re, buf, L, count, cuda, chunk):
+    o = OracleRegex(re)
+    counts, got, path = _run(re, buf, L, count, cuda, chunk)
+    k = 0
+    for i in range(count):
+        exp = o.find_iter(buf[i * L:(i + 1) * L])
+        assert counts[i] == len(exp), (i, chunk)
+        assert got[k:k + len(exp)] == exp, (i, chunk)
+        k += len(exp)
+    assert k == len(got)
+    return path
+
+
+@pytest.mark.parametrize("pat", ASCII_PATTERNS)
+@pytest.mark.parametrize("chunk", [16, 61, 4096])
+def test_find_iter_looks_chunked(cuda, pat, chunk):
+    re = R.Regex(pat)
+    L = 6000
+    for count, seed in ((1, 1), (3, 2)):
+        buf = _text(zlib.crc32(pat.encode()) + seed, L * count, False)
+        assert _check(re, buf, L, count, cuda, chunk) == -12, pat
+
+
+@pytest.mark.parametrize("pat", UNICODE_PATTERNS)
+@pytest.mark.parametrize("nonascii", [False, True])
+def test_find_iter_unicode_boundary(cuda, pat, nonascii):
+    """A DFA that can quit: ASCII text stays chunked (-12); a non-ASCII byte
+    next to a boundary makes a search quit and the wave path answer (-13)."""
+    re = R.Regex(pat)
+    L = 8000
+    buf = _text(zlib.crc32(pat.encode()), L, nonascii)
+    path = _check(re, buf, L, 1, cuda, 64)
+    if not nonascii:
+        assert path == -12, pat
+    elif "\\b" in pat or "\\B" in pat:
+        assert path == -13, pat
+
+
+@pytest.mark.parametrize("pat", [r"\b\w+\b", r"(?m)^\w+", r"\bthe\b", r"(?-u:\b)[A-Z]\w*", r"\w+ing\b"])
+def test_find_iter_looks_long_sherlock(cuda, pat):
+    """The default unit size over ~1 MB of English (ASCII)."""
+    text = corpus("sherlock")
+    text = bytes(b if b < 0x80 else 0x20 for b in text)
+    text = (text * 3)[:1 << 20]
+    re = R.Regex(pat)
+    import torch
+    counts, m = re.find_iter_batch(_dev(text, cuda), stride=len(text), length=len(text), count=1)
+    assert N.rure_amd_last_fwd_path() == -12, pat
+    exp = OracleRegex(re).find_iter(text)
+    assert [tuple(x) for x in m.cpu().numpy().tolist()] == exp
+    del torch

@@ -1,0 +1,57 @@
+"""find_iter of look-around regexes over 1 GiB of sherlock text (made ASCII,
+so Unicode \\b's DFA never quits): the chunked path (iter_scan.hip with
+FwdDfaDev::looks, last_fwd_path -12) against the wave path
+(RURE_AMD_ITER_LOOKS=0) on a 16 MiB prefix, outputs compared there.
+usage: python tools/looks_iter_bench.py"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import numpy as np
+import torch
+
+import regex_amd as R
+from regex_amd import _native as N
+from golden_data import corpus
+
+dev = torch.device("cuda", 0)
+raw = bytes(b if b < 0x80 else 0x20 for b in corpus("sherlock"))
+copies = (1 << 30) // len(raw)
+L = len(raw) * copies
+buf = torch.zeros(L + 16, dtype=torch.uint8, device=dev)
+one = torch.from_numpy(np.frombuffer(raw, dtype=np.uint8).copy()).to(dev)
+buf[:L].view(copies, len(raw)).copy_(one.expand(copies, len(raw)))
+SMALL = len(raw) * ((16 << 20) // len(raw))
+
+
+def timed(re, n, reps):
+    c, m = re.find_iter_batch(buf, stride=n, length=n, count=1, capacity=1)
+    cap = max(int(c[0].item()), 1)
+    re.find_iter_batch(buf, stride=n, length=n, count=1, capacity=cap)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        c, m = re.find_iter_batch(buf, stride=n, length=n, count=1, capacity=cap)
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / reps * 1e3, cap, m
+
+
+pats = [r"\b\w+\b", r"(?-u)\b\w+\b", r"\bthe\b", r"[a-z]+ed\b", r"(?m)^\w+", r"(?m)\w+$"]
+for pat in pats:
+    re = R.Regex(pat)
+    ms, cap, _ = timed(re, L, 5)
+    path = N.rure_amd_last_fwd_path()
+    _, _, m_small = timed(re, SMALL, 1)
+    os.environ["RURE_AMD_ITER_LOOKS"] = "0"
+    try:
+        wms, wcap, m_wave = timed(re, SMALL, 1)
+    finally:
+        del os.environ["RURE_AMD_ITER_LOOKS"]
+    same = bool(torch.equal(m_small, m_wave))
+    print(json.dumps({"pattern": pat, "path": path, "matches": cap, "ms": round(ms, 3),
+                      "GBps": round(L / ms / 1e6, 1), "wave_GBps_16MiB": round(SMALL / wms / 1e6, 3),
+                      "equal_16MiB": same}), flush=True)
