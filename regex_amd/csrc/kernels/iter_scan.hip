@@ -329,8 +329,9 @@ __device__ __forceinline__ void fwd_window_all(LaneState &L, const FwdDfaDev &f,
 
 // rev_scan (exec.rs:651-661, dfa.rs:768-866) for all-mode reverse tables:
 // blocks walked backwards, bytes reversed in registers, branch-free steps.
+// reached: as rev_scan's.
 __device__ __forceinline__ uint64_t rev_scan_all(const RevDfaDev &r, const uint8_t *rlds, const uint8_t *base,
-                                                 uint64_t len, uint64_t lo, uint64_t me) {
+                                                 uint64_t len, uint64_t lo, uint64_t me, bool *reached = nullptr) {
   uint32_t s = r.ustart1 ? r.ustart1 - 1 : r.start[rev_flag_index(base, lo, len, me)];
   if (s == r.dead) return NONE;
   uint64_t rs = NONE, a = me;
@@ -358,6 +359,7 @@ __device__ __forceinline__ uint64_t rev_scan_all(const RevDfaDev &r, const uint8
       if (s >= r.n_match_end) return s == r.dead ? rs : QUITMARK;
     }
   }
+  if (reached) *reached = true;
   if (r.eof[s]) rs = lo;
   return rs;
 }
@@ -385,6 +387,7 @@ __global__ __launch_bounds__(1024) void iter_spec_burst_kernel(BatchDev b, Geo g
     uint64_t at = 0, at0 = 0, cutpos = NONE;        // the current forward scan
     uint64_t ex_p = 0, ex_lm = NONE;
     bool clean = true, quit = false, searching = false;
+    bool first = true, unsure = false;  // look-around: UnitIter's
     uint32_t n = 0;
     LaneState L;
     L.done = true;
@@ -435,12 +438,22 @@ __global__ __launch_bounds__(1024) void iter_spec_burst_kernel(BatchDev b, Geo g
       if (L.last == NONE) { finish(sp, slm, true); continue; }
       const uint64_t me = L.last;
       uint64_t ms = at0;
+      bool reached = me == at0;
       if (me != at0) {  // exec.rs:647
-        const uint64_t rs = r.all ? rev_scan_all(r, rlds, base, len, at0, me) : rev_scan(r, rlds, base, len, at0, me);
+        const uint64_t rs = r.all ? rev_scan_all(r, rlds, base, len, at0, me, &reached)
+                                  : rev_scan(r, rlds, base, len, at0, me, &reached);
+        if (first) unsure = reached;
+        first = false;
         if (rs == QUITMARK) { quit = true; finish(sp, slm, false); continue; }
-        if (rs == NONE) { finish(sp, slm, true); continue; }
+        if (rs == NONE) {  // look-around: the search's NoMatch ends the iteration
+          if (f.looks) finish(kIterStop, NONE, false);
+          else finish(sp, slm, true);
+          continue;
+        }
         ms = rs;
       }
+      if (first) unsure = reached;
+      first = false;
       if (ms == me) {
         p = me + 1;
         if (lm == me) { begin_search(); continue; }  // empty match at the previous match end: skipped
@@ -459,11 +472,12 @@ __global__ __launch_bounds__(1024) void iter_spec_burst_kernel(BatchDev b, Geo g
       U.exit = {ex_p, ex_lm};
       U.spec_exit = U.exit;
       U.spec_count = n;
-      U.flags = (clean ? (U_SPEC_CLEAN | U_CLEAN) : 0) | (quit ? U_QUIT : 0);
+      U.flags = (clean ? (U_SPEC_CLEAN | U_CLEAN) : 0) | (quit ? U_QUIT : 0) |
+                (f.looks && unsure && u % g.nk != 0 ? U_UNSURE : 0);
       U.skip = U.pad = 0;
       units[u] = U;
       counts[u] = n;
-      if (!(U.flags & U_SPEC_CLEAN)) atomicOr(dirty, 1u);  // the fix pass has work
+      if ((U.flags & (U_SPEC_CLEAN | U_UNSURE)) != U_SPEC_CLEAN) atomicOr(dirty, 1u);  // the fix pass has work
     }
   }
 }
@@ -2830,6 +2844,15 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
   if (chunked) {
     Geo g;
     const uint64_t nunits = iter_geo(b, chunk, hi, &g);
+    // Dense matches: the caller's capacity tells how many to expect; slots
+    // that hold them spare the emit pass re-running every unit (\b\w+\b over
+    // English, ~750 matches per 4 KiB unit: 128 slots re-ran them all, 19 of
+    // 33 ms).  Not for the lexer (its compact rows), at most 4 GiB.
+    if (!f->lex_bytes && !b.offs && o.cap > (uint64_t)g.slots * nunits) {
+      const uint64_t per = (o.cap + nunits - 1) / nunits;
+      const uint64_t want = std::min<uint64_t>(per + per / 4 + 4, std::min<uint64_t>(g.chunk + 1, 8192));
+      if (want > g.slots && want * nunits * 16 <= (4ull << 30)) g.slots = (uint32_t)want;
+    }
     IterScratch sc;
     if ((e = iter_scratch(nunits, g.slots, st, &sc)) != hipSuccess) return e;
     // threads per block: the hot tables are staged once per block, so larger
@@ -2914,7 +2937,7 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
         else
           hipLaunchKernelGGL((iter_spec_lit_kernel<false, false>), lg, dim3(bs), kLitImage, st, b, g, nunits, *f,
                              units, slots, counts, dirty);
-      } else if (!getenv("RURE_AMD_ITER_NESTED") && !f->looks) {
+      } else if (!getenv("RURE_AMD_ITER_NESTED")) {
         hipLaunchKernelGGL(iter_spec_burst_kernel, dim3(grid), dim3(bs), iter_lds_bytes(*f, r), st, b, g, nunits, *f,
                            r, units, slots, counts, dirty);
       } else {

@@ -104,3 +104,17 @@ def test_find_iter_looks_long_sherlock(cuda, pat):
     exp = OracleRegex(re).find_iter(text)
     assert [tuple(x) for x in m.cpu().numpy().tolist()] == exp
     del torch
+
+
+@pytest.mark.parametrize("pat", ASCII_PATTERNS[:8])
+def test_find_iter_looks_nested_kernel(cuda, pat):
+    """The nested-loop speculative kernel (RURE_AMD_ITER_NESTED) follows the
+    same rules as the burst one."""
+    re = R.Regex(pat)
+    L = 6000
+    buf = _text(zlib.crc32(pat.encode()) + 9, L * 2, False)
+    os.environ["RURE_AMD_ITER_NESTED"] = "1"
+    try:
+        assert _check(re, buf, L, 2, cuda, 16) == -12, pat
+    finally:
+        del os.environ["RURE_AMD_ITER_NESTED"]

@@ -2,7 +2,7 @@
 so Unicode \\b's DFA never quits): the chunked path (iter_scan.hip with
 FwdDfaDev::looks, last_fwd_path -12) against the wave path
 (RURE_AMD_ITER_LOOKS=0) on a 16 MiB prefix, outputs compared there.
-usage: python tools/looks_iter_bench.py"""
+usage: python tools/looks_iter_bench.py [--no-wave] [pattern ...]"""
 import json
 import os
 import sys
@@ -41,10 +41,16 @@ def timed(re, n, reps):
 
 
 pats = [r"\b\w+\b", r"(?-u)\b\w+\b", r"\bthe\b", r"[a-z]+ed\b", r"(?m)^\w+", r"(?m)\w+$"]
-for pat in pats:
+args = [a for a in sys.argv[1:] if a != "--no-wave"]
+wave = "--no-wave" not in sys.argv
+for pat in args or pats:
     re = R.Regex(pat)
     ms, cap, _ = timed(re, L, 5)
     path = N.rure_amd_last_fwd_path()
+    if not wave:
+        print(json.dumps({"pattern": pat, "path": path, "matches": cap, "ms": round(ms, 3),
+                          "GBps": round(L / ms / 1e6, 1)}), flush=True)
+        continue
     _, _, m_small = timed(re, SMALL, 1)
     os.environ["RURE_AMD_ITER_LOOKS"] = "0"
     try:
