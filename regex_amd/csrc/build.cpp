@@ -499,6 +499,42 @@ void set_prefix_skip(const rure *re, FwdDfaDev *f) {
     f->pfx_rep[n++] = b * 0x01010101u;
   }
   f->pfx_n = n;
+  // byte sets of the prefixes' first three positions (case pairs folded)
+  // for the deeper filter, opt-in (RURE_AMD_PREFIX=3): on English text it
+  // lost to the first-byte filter (Sherlock\s+\w+ 1.47 -> 1.62 ms per GiB,
+  // (?i)watson\w* 1.46 -> 1.89) and won only where the prefix is absent
+  // ((?i)zqxj\w* 1.12 -> 0.65); profiles/r04_prefix_depth_ab.jsonl
+  f->pfx_depth = 0;
+  if (!(env && env[0] == '3')) return;
+  uint32_t depth = 0;
+  for (uint32_t j = 0; j < 3; ++j) {
+    bool in[256] = {false};
+    for (const Lit &l : p.lits.lits) {
+      if (l.v.size() <= j) goto done;
+      in[(uint8_t)l.v[j]] = true;
+    }
+    {
+      uint32_t c = 0;
+      for (int x = 0; x < 256; ++x) {
+        if (!in[x]) continue;
+        const bool letter = (x | 0x20) >= 'a' && (x | 0x20) <= 'z';
+        if (letter && (x & 0x20) == 0 && in[x | 0x20]) continue;  // folded with its lower case
+        if (c == 1) goto done;  // one entry per set (FwdDfaDev::pfx_depth)
+        const bool fold = letter && in[x ^ 0x20];
+        f->pfx_set[j][c] = (uint32_t)(fold ? (x | 0x20) : x) * 0x01010101u;
+        f->pfx_or[j][c] = fold ? 0x20202020u : 0;
+        ++c;
+      }
+      f->pfx_cnt[j] = c;
+      for (uint32_t i = c; i < 4; ++i) {  // unused entries repeat entry 0
+        f->pfx_set[j][i] = f->pfx_set[j][0];
+        f->pfx_or[j][i] = f->pfx_or[j][0];
+      }
+      depth = j + 1;
+    }
+  }
+done:
+  f->pfx_depth = depth >= 2 ? depth : 0;
 }
 
 // Upload (once per device) and return device descriptors.

@@ -104,6 +104,16 @@ struct FwdDfaDev {
   // that hold none of those bytes (fwd_range); pfx_n = 0: off.
   uint32_t pfx_n;
   uint32_t pfx_rep[4];
+  // The same skip over the first two or three bytes of the prefixes
+  // (pfx_depth >= 2; 0 or 1: pfx_rep alone): set j = the prefixes' bytes at
+  // position j, one entry (the filter runs one SWAR test per set and word;
+  // more entries cost more than the DFA chain saves); a byte x is in the set
+  // when (x | pfx_or[j][0]) == the byte of pfx_set[j][0] (pfx_or 0x20 folds
+  // an ASCII letter's two cases).  A burst is skipped when no position in it
+  // starts a byte sequence from set 0 x set 1 (x set 2).
+  uint32_t pfx_depth;
+  uint32_t pfx_cnt[3];
+  uint32_t pfx_set[3][4], pfx_or[3][4];
   // find_iter DFA only: the regex has look-around assertions (the chunked
   // iteration then repairs units whose first reverse scan reached their
   // start, and a reverse NoMatch ends the iteration; iter_scan.hip), and its
