@@ -26,3 +26,11 @@ def stdlib_fixtures():
     """Python-`re` answers for the BASELINE patterns (gen_stdlib_fixtures.py)."""
     with gzip.open(os.path.join(G, "stdlib_re_fixtures.json.gz"), "rt", encoding="ascii") as f:
         return json.load(f)
+
+
+def stdlib_looks_fixtures():
+    """Python-`re` finditer answers for look-around regexes over ASCII slices
+    of the sherlock corpus (gen_stdlib_looks.py); returns (fixtures, text)."""
+    with gzip.open(os.path.join(G, "stdlib_looks_fixtures.json.gz"), "rt", encoding="ascii") as f:
+        fx = json.load(f)
+    return fx, bytes(b if b < 0x80 else 0x20 for b in corpus("sherlock"))

@@ -18,7 +18,7 @@ import pytest
 
 import regex_amd as R
 from regex_amd import _native as N
-from golden_data import corpus
+from golden_data import corpus, stdlib_looks_fixtures
 from oracle_py import OracleRegex
 
 pytestmark = pytest.mark.gpu
@@ -118,3 +118,16 @@ def test_find_iter_looks_nested_kernel(cuda, pat):
         assert _check(re, buf, L, 2, cuda, 16) == -12, pat
     finally:
         del os.environ["RURE_AMD_ITER_NESTED"]
+
+
+@pytest.mark.parametrize("pat", stdlib_looks_fixtures()[0]["patterns"])
+@pytest.mark.parametrize("chunk", [64, 4096])
+def test_find_iter_looks_vs_stdlib(cuda, pat, chunk):
+    """The chunked path against Python's `re` (gen_stdlib_looks.py): an
+    anchor independent of the product's compiler."""
+    fx, text = stdlib_looks_fixtures()
+    re = R.Regex(pat)
+    for (off, n), exp in zip(fx["slices"], fx["find_iter"][pat]):
+        counts, got, path = _run(re, text[off:off + n], n, 1, cuda, chunk)
+        assert got == [tuple(x) for x in exp], (pat, off)
+        assert path == -12, pat
