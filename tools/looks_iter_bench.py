@@ -2,7 +2,9 @@
 so Unicode \\b's DFA never quits): the chunked path (iter_scan.hip with
 FwdDfaDev::looks, last_fwd_path -12) against the wave path
 (RURE_AMD_ITER_LOOKS=0) on a 16 MiB prefix, outputs compared there.
-usage: python tools/looks_iter_bench.py [--no-wave] [pattern ...]"""
+--ragged: the same text as a ragged batch of its lines (one unit per line)
+against the wave path, outputs compared.
+usage: python tools/looks_iter_bench.py [--no-wave] [--ragged] [pattern ...]"""
 import json
 import os
 import sys
@@ -41,8 +43,36 @@ def timed(re, n, reps):
 
 
 pats = [r"\b\w+\b", r"(?-u)\b\w+\b", r"\bthe\b", r"[a-z]+ed\b", r"(?m)^\w+", r"(?m)\w+$"]
-args = [a for a in sys.argv[1:] if a != "--no-wave"]
+args = [a for a in sys.argv[1:] if a not in ("--no-wave", "--ragged")]
 wave = "--no-wave" not in sys.argv
+if "--ragged" in sys.argv:
+    small = bytes(raw) * 8  # ~4.7 MB of lines (the wave path is slow)
+    ends = np.nonzero(np.frombuffer(small, dtype=np.uint8) == 10)[0] + 1
+    offs = torch.from_numpy(np.concatenate([[0], ends]).astype(np.int64)).to(dev)
+    hay = torch.from_numpy(np.frombuffer(small + b"\0" * 16, dtype=np.uint8).copy()).to(dev)
+
+    def run(re):
+        c, m = re.find_iter_batch(hay, offsets=offs)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(3):
+            c, m = re.find_iter_batch(hay, offsets=offs)
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / 3 * 1e3, m
+
+    for pat in args or [r"\bthe\b", r"\b\w+\b", r"(?m)^\w+", r"[a-z]+ed\b"]:
+        re = R.Regex(pat)
+        ms, m = run(re)
+        path = N.rure_amd_last_fwd_path()
+        os.environ["RURE_AMD_ITER_LOOKS"] = "0"
+        try:
+            wms, wm = run(re)
+        finally:
+            del os.environ["RURE_AMD_ITER_LOOKS"]
+        print(json.dumps({"pattern": pat, "ragged_lines": int(offs.numel() - 1), "bytes": len(small), "path": path,
+                          "matches": int(m.shape[0]), "ms": round(ms, 3), "wave_ms": round(wms, 3),
+                          "equal": bool(torch.equal(m, wm))}), flush=True)
+    sys.exit(0)
 for pat in args or pats:
     re = R.Regex(pat)
     ms, cap, _ = timed(re, L, 5)
