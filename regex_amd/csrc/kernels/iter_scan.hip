@@ -462,7 +462,10 @@ __global__ __launch_bounds__(1024) void iter_spec_burst_kernel(BatchDev b, Geo g
       }
       lm = me;
       if (ms >= c1) { finish(sp, slm, true); continue; }  // owned by the next unit
-      if (n < g.slots) *(ulonglong2 *)&slots[(u * g.slots + n) * 2] = make_ulonglong2(ms, me);
+      if (n < g.slots) {  // streaming stores: dense units write GBs of slots (5-7 % on \b\w+\b, [a-z]+)
+        __builtin_nontemporal_store(ms, &slots[(u * g.slots + n) * 2]);
+        __builtin_nontemporal_store(me, &slots[(u * g.slots + n) * 2 + 1]);
+      }
       ++n;
       unit_next();
     }
@@ -2484,6 +2487,17 @@ hipError_t launch_long_scan(int mode, const BatchDev &b, const FwdDfaDev &f, con
 
 // Unit geometry of a chunked find_iter: units of `chunk` bytes per haystack
 // (offset batches: one unit per haystack); returns the number of units.
+// Lexer engine (terminal matches + first-byte rule); RURE_AMD_LEX=0 disables.
+// (haystacks below 4 GiB: the lexer's records are u32 offsets from the unit
+// start, U_COMPACT; units of at most 64 KiB: its record queue packs two u16
+// per register)
+static bool lex_usable(const FwdDfaDev &f, const BatchDev &b, const Geo &g) {
+  const char *lex_env = getenv("RURE_AMD_LEX");
+  return f.lex_bytes && !(lex_env && lex_env[0] == '0') && !b.offs && g.nk >= 2 && (g.chunk % 128) == 0 &&
+         (b.count == 1 || (b.stride % 16) == 0) && (((uintptr_t)(b.hay + b.start)) & 15) == 0 &&
+         b.length < (1ull << 32) && g.chunk <= 65536;
+}
+
 static uint64_t iter_geo(const BatchDev &b, uint64_t chunk, uint64_t hi, Geo *g) {
   const uint64_t lim = std::min<uint64_t>(b.length, hi);
   const uint64_t span = (!b.offs && lim > b.start) ? lim - b.start : 0;
@@ -2850,7 +2864,7 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
     // that hold them spare the emit pass re-running every unit (\b\w+\b over
     // English, ~750 matches per 4 KiB unit: 128 slots re-ran them all, 19 of
     // 33 ms).  Not for the lexer (its compact rows), at most 4 GiB.
-    if (!f->lex_bytes && !b.offs && o.cap > (uint64_t)g.slots * nunits) {
+    if (!lex_usable(*f, b, g) && !b.offs && o.cap > (uint64_t)g.slots * nunits) {
       const uint64_t per = (o.cap + nunits - 1) / nunits;
       const uint64_t want = std::min<uint64_t>(per + per / 4 + 4, std::min<uint64_t>(g.chunk + 1, 8192));
       if (want > g.slots && want * nunits * 16 <= (4ull << 30)) g.slots = (uint32_t)want;
@@ -2882,14 +2896,7 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
       const bool use_sa = sa_usable(*f);
       const bool sa_tile = sa_tile_ok(b, g);
       // Lexer engine (terminal matches + first-byte rule); RURE_AMD_LEX=0 disables
-      const char *lex_env = getenv("RURE_AMD_LEX");
-      // (haystacks below 4 GiB: the lexer's records are u32 offsets from the
-      // unit start, U_COMPACT; units of at most 64 KiB: its record queue
-      // packs two u16 per register)
-      const bool use_lex = f->lex_bytes && !(lex_env && lex_env[0] == '0') && !b.offs && g.nk >= 2 &&
-                           (g.chunk % 128) == 0 && (b.count == 1 || (b.stride % 16) == 0) &&
-                           (((uintptr_t)(b.hay + b.start)) & 15) == 0 && b.length < (1ull << 32) &&
-                           g.chunk <= 65536;
+      const bool use_lex = lex_usable(*f, b, g);
       ktimer_begin(st);  // bench diagnostics: the speculative kernel's duration
       if (use_lex) {
         const dim3 lg(grid_cap((nunits + 63) / 64, 4, cus, 4));
