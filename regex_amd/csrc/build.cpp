@@ -1003,6 +1003,26 @@ bool build_iter_dfa(rure *re) {
       re->fb_n = first_byte_rule(re->dfwd_iter, re->pf_iter.ustart1, !can_match_empty(re->nfa), re->fb_bytes);
     if (re->iter_ok && build_lex(re->dfwd_iter, re->pf_iter.ustart1, re->fb_n, &re->lex, &re->lex_s0))
       build_lex4(re->lex, re->lex_s0, &re->lex4, &re->lex4_s0);
+    // ASCII shadow (iter_ascii_device): where the automaton is too big for
+    // the all-rows LDS table because of its UTF-8 states (Unicode classes),
+    // the same automaton with every byte >= 0x80 quitting and the states only
+    // those bytes reach dropped
+    if (re->iter_ok && !re->pf_iter.all && !re->fwd.has_unicode_word_boundary && !re->lit_ok &&
+        !(getenv("RURE_AMD_ASCII_SHADOW") && getenv("RURE_AMD_ASCII_SHADOW")[0] == '0')) {
+      DfaBuildLimits la;
+      la.strip = true;
+      la.ascii_only = true;
+      DenseDfa a;
+      PackedFwd pa;
+      if (build_dense_dfa(re->fwd, la, &a, &e)) {
+        prune_unreachable(&a);
+        if (a.nstates <= 255 && pack_forward(a, &pa, &e, true) && pa.all) {
+          re->dfwd_iter_a = std::move(a);
+          re->pf_iter_a = std::move(pa);
+          re->iter_a_ok = true;
+        }
+      }
+    }
   }
   return re->iter_ok;
 }
@@ -1056,6 +1076,51 @@ bool build_shiftand(const LiteralSet &ls, std::vector<uint64_t> *mask, uint64_t 
         if ((seqs[x][i][c >> 6] >> (c & 63)) & 1) (*mask)[c] |= 1ull << (x * L + i);
   }
   return true;
+}
+
+// The ASCII shadow of the find_iter DFA on this device (null if none): DFA
+// tables only (no string engines, no first-byte rule), can_quit set.
+const FwdDfaDev *iter_ascii_device(rure *re, const DevTables &t, std::string *err) {
+  if (!build_iter_dfa(re) || !re->iter_a_ok) return nullptr;
+  int d = 0;
+  if (!hip_ok(hipGetDevice(&d), err)) return nullptr;
+  std::lock_guard<std::mutex> g(re->mu);
+  auto it = re->iter_dev_a.find(d);
+  if (it != re->iter_dev_a.end()) return &it->second.second;
+  const PackedFwd &pf = re->pf_iter_a;
+  const DenseDfa &fw = re->dfwd_iter_a;
+  std::vector<uint16_t> strip(fw.strip.size());
+  for (size_t i = 0; i < strip.size(); ++i) strip[i] = (uint16_t)fw.strip[i];
+  Blob b;
+  size_t o_lds = b.add(pf.lds.data(), pf.lds.size());
+  size_t o_full = b.add(pf.full.data(), pf.full.size() * 2);
+  size_t o_eof = b.add(pf.eof.data(), pf.eof.size());
+  size_t o_start = b.add(pf.start.data(), 256);
+  size_t o_strip = b.add(strip.data(), strip.size() * 2);
+  DevTables tmp;
+  if (!upload_blob(b, &tmp, err)) return nullptr;
+  uint8_t *base = (uint8_t *)tmp.blob;
+  FwdDfaDev f{};
+  f.lds_image = base + o_lds;
+  f.lds_bytes = (uint32_t)pf.lds.size();
+  f.hot = pf.hot;
+  f.stride = 1;
+  f.cus = (uint32_t)t.cus;
+  f.full = (const uint16_t *)(base + o_full);
+  f.eof = base + o_eof;
+  f.start = (const uint16_t *)(base + o_start);
+  f.strip = (const uint16_t *)(base + o_strip);
+  f.n_normal = fw.n_normal;
+  f.n_match_end = fw.n_match_end;
+  f.dead = fw.dead;
+  f.quit = fw.quit < 0 ? 0xFFFFFFFFu : (uint32_t)fw.quit;
+  f.all = pf.all;
+  f.ustart1 = pf.ustart1;
+  f.nonempty = can_match_empty(re->nfa) ? 0 : 1;
+  f.looks = re->nt.looks_used ? 1 : 0;
+  f.can_quit = 1;
+  re->iter_dev_a[d] = {tmp.blob, f};
+  return &re->iter_dev_a[d].second;
 }
 
 const FwdDfaDev *iter_device(rure *re, const DevTables &t, std::string *err) {

@@ -178,6 +178,13 @@ rure *rure_compile_must(const char *pattern) {  // rure.rs:76-91
 void rure_free(rure *re) {
   if (!re) return;
   kmer_forget(re);
+  for (auto &kv : re->iter_dev_a) {
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(kv.first);
+    (void)hipFree(kv.second.first);
+    (void)hipSetDevice(cur);
+  }
   for (auto &kv : re->iter_dev) {
     int cur = 0;
     (void)hipGetDevice(&cur);

@@ -846,6 +846,20 @@ hipError_t run_find_iter(rure *re, DevTables *t, const BatchDev &b, const IterOu
       // RURE_AMD_ITER_CHUNK: the unit size in bytes (tests: many boundaries)
       if (const char *v = getenv("RURE_AMD_ITER_CHUNK")) chunk = std::max<uint64_t>(16, strtoull(v, nullptr, 10));
     }
+    // the ASCII shadow first (all-rows LDS tables; a non-ASCII byte quits
+    // and the full automaton re-runs the batch, still chunked); not for
+    // spans (the quit is read back)
+    if (!sp && !looks) {
+      if (const FwdDfaDev *fa = iter_ascii_device(re, *t, err)) {
+        bool q = false;
+        const hipError_t e = launch_find_iter(b, fa, t->r, &t->n, true, chunk, o, st, t->cus, sp, nullptr, &q);
+        if (e != hipSuccess || !q) {
+          if (e == hipSuccess) note_fwd_path(-14);
+          return e;
+        }
+        note_fwd_path(-15);  // a quit: the full automaton below answers
+      }
+    }
     bool quit = false;
     const hipError_t e = launch_find_iter(b, fi, t->r, &t->n, true, chunk, o, st, t->cus, sp, nullptr, &quit);
     // last_fwd_path: -12 = the chunked iteration of a look-around regex

@@ -39,7 +39,7 @@ class Builder {
     word_matters_ = false;
     for (const Inst &i : p.insts)
       if (i.op == OP_EMPTY && i.look >= LOOK_WORD_BOUNDARY) word_matters_ = true;
-    quit_ = p.has_unicode_word_boundary;
+    quit_ = p.has_unicode_word_boundary || lim.ascii_only;
     stack_.reserve(p.insts.size() + 1);
     stamp_.assign(p.insts.size() + 1, 0);
   }
@@ -762,6 +762,60 @@ int start_flag_index_rev(const uint8_t *text, size_t len, size_t at) {  // dfa.r
   bool wb = word_last != word;
   return (start ? 1 : 0) | (end ? 2 : 0) | (start_line ? 4 : 0) | (end ? 8 : 0) |
          (wb ? 16 : 32) | (word_last ? 64 : 0);
+}
+
+void prune_unreachable(DenseDfa *d) {
+  const int n = d->nstates;
+  if (n == 0 || d->trans.empty() || d->is_set) return;
+  std::vector<char> keep(n, 0);
+  std::vector<int> st;
+  auto mark = [&](uint32_t s) {
+    if (s < (uint32_t)n && !keep[s]) { keep[s] = 1; st.push_back((int)s); }
+  };
+  for (int i = 0; i < 128; ++i) mark(d->start[i]);
+  mark((uint32_t)d->dead);
+  if (d->quit >= 0) mark((uint32_t)d->quit);
+  while (!st.empty()) {
+    const int s = st.back();
+    st.pop_back();
+    for (int b = 0; b < 256; ++b) mark(d->trans[(size_t)s * 256 + b]);
+    if (!d->strip.empty()) mark(d->strip[s]);
+  }
+  std::vector<uint32_t> id(n, 0);
+  int next = 0, n_normal = 0, n_match_end = 0, n_ascii = 0;
+  for (int s = 0; s < n; ++s) {
+    if (!keep[s]) continue;
+    id[s] = (uint32_t)next++;
+    if (s < d->n_normal) ++n_normal;
+    if (s < d->n_match_end) ++n_match_end;
+    if (s < d->n_ascii) ++n_ascii;
+  }
+  if (next == n) return;
+  std::vector<uint32_t> trans((size_t)next * 256);
+  std::vector<uint8_t> eof_match(next);
+  std::vector<uint64_t> eof_mask(next), now_mask(next);
+  std::vector<uint32_t> strip(d->strip.empty() ? 0 : next);
+  for (int s = 0; s < n; ++s) {
+    if (!keep[s]) continue;
+    const uint32_t t = id[s];
+    for (int b = 0; b < 256; ++b) trans[(size_t)t * 256 + b] = id[d->trans[(size_t)s * 256 + b]];
+    eof_match[t] = d->eof_match[s];
+    eof_mask[t] = d->eof_mask[s];
+    now_mask[t] = d->now_mask[s];
+    if (!strip.empty()) strip[t] = id[d->strip[s]];
+  }
+  for (int i = 0; i < 128; ++i) d->start[i] = id[d->start[i]];
+  d->dead = (int)id[d->dead];
+  if (d->quit >= 0) d->quit = (int)id[d->quit];
+  d->n_normal = n_normal;
+  d->n_match_end = n_match_end;
+  d->n_ascii = n_ascii;
+  d->nstates = next;
+  d->trans.swap(trans);
+  d->eof_match.swap(eof_match);
+  d->eof_mask.swap(eof_mask);
+  d->now_mask.swap(now_mask);
+  d->strip.swap(strip);
 }
 
 }  // namespace rure_amd

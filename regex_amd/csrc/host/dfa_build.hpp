@@ -58,7 +58,12 @@ struct DfaBuildLimits {
   bool columns = false;   // emit ctrans / colmap instead of the 256-wide trans
   bool minimise = true;   // false: raw states kept (same language, more states)
   size_t max_bytes = 0;   // construction memory budget (state keys + rows, estimated); 0 = none
+  bool ascii_only = false;  // every byte >= 0x80 goes to QUIT (an ASCII shadow of the automaton)
 };
+// Drops the states no start state reaches (through transitions and strip
+// links), keeping the numbering's classes and order (normal with the ASCII-
+// reachable ones first, match-flag, dead, quit).  Row form, non-set only.
+void prune_unreachable(DenseDfa *d);
 // Raw-state budget of the eager u32 (column form) automata; past it the
 // on-demand DFA (LazyDfa) builds only the states a batch visits.  (At 1 << 21
 // the failed eager attempt for (?:a|b)*a(?:a|b){20} cost ~5 s.)

@@ -263,6 +263,11 @@ struct rure {
   uint32_t lex4_s0 = 0;
   LiteralSet lits;
   std::map<int, std::pair<void *, FwdDfaDev>> iter_dev;
+  // the find_iter DFA's ASCII shadow (build_iter_dfa, iter_ascii_device)
+  bool iter_a_ok = false;
+  DenseDfa dfwd_iter_a;
+  PackedFwd pf_iter_a;
+  std::map<int, std::pair<void *, FwdDfaDev>> iter_dev_a;
 };
 
 struct rure_set {
@@ -347,6 +352,7 @@ bool build_lex(const DenseDfa &d, uint32_t ustart1, uint32_t fb_n, std::vector<u
 bool build_iter_dfa(rure *re);
 bool build_shiftand(const LiteralSet &ls, std::vector<uint64_t> *mask, uint64_t *init, uint64_t *fin,
                            uint32_t *len, uint32_t *bits);
+const FwdDfaDev *iter_ascii_device(rure *re, const DevTables &t, std::string *err);
 const FwdDfaDev *iter_device(rure *re, const DevTables &t, std::string *err);
 bool adapt_cores(rure_set *rs, DevTables *t, const BatchDev &b, hipStream_t st, std::string *err);
 int device_cus(int dev);

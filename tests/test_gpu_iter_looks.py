@@ -131,3 +131,16 @@ def test_find_iter_looks_vs_stdlib(cuda, pat, chunk):
         counts, got, path = _run(re, text[off:off + n], n, 1, cuda, chunk)
         assert got == [tuple(x) for x in exp], (pat, off)
         assert path == -12, pat
+
+
+@pytest.mark.parametrize("pat", [r"\w+", r"\w+\s+\w+", r"[\w.]+@\w+", r"\pL+", r"\w{2,4}"])
+@pytest.mark.parametrize("nonascii", [False, True])
+def test_find_iter_ascii_shadow(cuda, pat, nonascii):
+    """Unicode classes: the find_iter automaton's ASCII shadow (all-rows LDS
+    tables, non-ASCII bytes quit) answers ASCII text (last_fwd_path -14); a
+    non-ASCII byte re-runs the batch on the full automaton (-15)."""
+    re = R.Regex(pat)
+    L = 20000
+    buf = _text(zlib.crc32(pat.encode()) + 5, L * 2, nonascii)
+    path = _check(re, buf, L, 2, cuda, 64)
+    assert path == (-15 if nonascii else -14), (pat, path)
