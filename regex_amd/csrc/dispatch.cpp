@@ -849,7 +849,7 @@ hipError_t run_find_iter(rure *re, DevTables *t, const BatchDev &b, const IterOu
     // the ASCII shadow first (all-rows LDS tables; a non-ASCII byte quits
     // and the full automaton re-runs the batch, still chunked); not for
     // spans (the quit is read back)
-    if (!sp && !looks) {
+    if (!sp) {
       if (const FwdDfaDev *fa = iter_ascii_device(re, *t, err)) {
         bool q = false;
         const hipError_t e = launch_find_iter(b, fa, t->r, &t->n, true, chunk, o, st, t->cus, sp, nullptr, &q);

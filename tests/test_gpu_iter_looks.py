@@ -73,7 +73,7 @@ def test_find_iter_looks_chunked(cuda, pat, chunk):
     L = 6000
     for count, seed in ((1, 1), (3, 2)):
         buf = _text(zlib.crc32(pat.encode()) + seed, L * count, False)
-        assert _check(re, buf, L, count, cuda, chunk) == -12, pat
+        assert _check(re, buf, L, count, cuda, chunk) in (-12, -14), pat
 
 
 @pytest.mark.parametrize("pat", UNICODE_PATTERNS)
@@ -86,7 +86,7 @@ def test_find_iter_unicode_boundary(cuda, pat, nonascii):
     buf = _text(zlib.crc32(pat.encode()), L, nonascii)
     path = _check(re, buf, L, 1, cuda, 64)
     if not nonascii:
-        assert path == -12, pat
+        assert path in (-12, -14), pat
     elif "\\b" in pat or "\\B" in pat:
         assert path == -13, pat
 
@@ -100,7 +100,7 @@ def test_find_iter_looks_long_sherlock(cuda, pat):
     re = R.Regex(pat)
     import torch
     counts, m = re.find_iter_batch(_dev(text, cuda), stride=len(text), length=len(text), count=1)
-    assert N.rure_amd_last_fwd_path() == -12, pat
+    assert N.rure_amd_last_fwd_path() in (-12, -14), pat
     exp = OracleRegex(re).find_iter(text)
     assert [tuple(x) for x in m.cpu().numpy().tolist()] == exp
     del torch
@@ -115,7 +115,7 @@ def test_find_iter_looks_nested_kernel(cuda, pat):
     buf = _text(zlib.crc32(pat.encode()) + 9, L * 2, False)
     os.environ["RURE_AMD_ITER_NESTED"] = "1"
     try:
-        assert _check(re, buf, L, 2, cuda, 16) == -12, pat
+        assert _check(re, buf, L, 2, cuda, 16) in (-12, -14), pat
     finally:
         del os.environ["RURE_AMD_ITER_NESTED"]
 
@@ -130,10 +130,11 @@ def test_find_iter_looks_vs_stdlib(cuda, pat, chunk):
     for (off, n), exp in zip(fx["slices"], fx["find_iter"][pat]):
         counts, got, path = _run(re, text[off:off + n], n, 1, cuda, chunk)
         assert got == [tuple(x) for x in exp], (pat, off)
-        assert path == -12, pat
+        assert path in (-12, -14), pat
 
 
-@pytest.mark.parametrize("pat", [r"\w+", r"\w+\s+\w+", r"[\w.]+@\w+", r"\pL+", r"\w{2,4}"])
+@pytest.mark.parametrize("pat", [r"\w+", r"\w+\s+\w+", r"[\w.]+@\w+", r"\pL+", r"\w{2,4}", r"(?m)^\w+",
+                                 r"(?m)\w+$", r"(?m)^\pL+\s"])
 @pytest.mark.parametrize("nonascii", [False, True])
 def test_find_iter_ascii_shadow(cuda, pat, nonascii):
     """Unicode classes: the find_iter automaton's ASCII shadow (all-rows LDS
@@ -143,4 +144,5 @@ def test_find_iter_ascii_shadow(cuda, pat, nonascii):
     L = 20000
     buf = _text(zlib.crc32(pat.encode()) + 5, L * 2, nonascii)
     path = _check(re, buf, L, 2, cuda, 64)
-    assert path == (-15 if nonascii else -14), (pat, path)
+    # (after a quit a look-around regex notes its own chunked path, -12)
+    assert path in ((-15, -12) if nonascii else (-14,)), (pat, path)
