@@ -262,7 +262,9 @@ typedef struct rure_amd_dfa_info {
 } rure_amd_dfa_info;
 /* which: 0 = forward DFA, 1 = reverse DFA, 2 = find_iter forward DFA,
  * 3 / 4 = the forward / reverse automata past the u16 tables (u32 column
- * form, built when 0 / 1 exceed 65535 states; byte_classes = columns). */
+ * form, built when 0 / 1 exceed 65535 states; byte_classes = columns),
+ * 5 = the find_iter forward DFA's ASCII shadow (bytes >= 0x80 quit; built
+ * where 2 is too big for the all-rows LDS table, else RURE_AMD_ERR_DFA). */
 int rure_amd_dfa_info_get(rure *re, int which, rure_amd_dfa_info *info);
 int rure_amd_set_dfa_info_get(rure_set *re, rure_amd_dfa_info *info);
 
@@ -286,7 +288,8 @@ int64_t rure_amd_set_program_export(rure_set *re, int which, rure_amd_prog_info 
                                     rure_amd_inst *insts, size_t cap);
 /* Export of a materialized DFA: trans = states*256 u32, eof_match = states
  * bytes, start = 128 u32.  which: 0 forward, 1 reverse, 2 the forward DFA
- * of the chunked find_iter (with stripped states, see _strip_export). */
+ * of the chunked find_iter (with stripped states, see _strip_export), 5 its
+ * ASCII shadow. */
 int rure_amd_dfa_export(rure *re, int which, uint32_t *trans, uint8_t *eof_match,
                         uint32_t *start);
 /* Export of a set's DFA (rure_amd_set_dfa_info_get gives the sizes): trans =

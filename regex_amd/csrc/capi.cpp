@@ -754,6 +754,11 @@ int rure_amd_dfa_info_get(rure *re, int which, rure_amd_dfa_info *info) {
     return RURE_AMD_OK;
   }
   if (!build_regex_dfas(re)) { info->ok = 0; return RURE_AMD_ERR_DFA; }
+  if (which == 5) {  // the find_iter automaton's ASCII shadow (build_iter_dfa)
+    if (!build_iter_dfa(re) || !re->iter_a_ok) { info->ok = 0; return RURE_AMD_ERR_DFA; }
+    fill_info(re->dfwd_iter_a, re->fwd, re->pf_iter_a.hot, info, &re->pf_iter_a);
+    return RURE_AMD_OK;
+  }
   if (which == 0) fill_info(re->dfwd, re->fwd, re->pf.hot, info, &re->pf);
   else if (which == 1) fill_info(re->drev, re->rev, re->pr.hot, info);
   else {
@@ -847,8 +852,9 @@ int rure_amd_dfa_strip_export(rure *re, uint32_t *strip) {
 int rure_amd_dfa_export(rure *re, int which, uint32_t *trans, uint8_t *eof_match, uint32_t *start) {
   if (!re) return RURE_AMD_ERR_ARG;
   if (!build_regex_dfas(re)) return RURE_AMD_ERR_DFA;
-  if (which == 2 && !build_iter_dfa(re)) return RURE_AMD_ERR_DFA;
-  const DenseDfa &d = which == 0 ? re->dfwd : which == 1 ? re->drev : re->dfwd_iter;
+  if ((which == 2 || which == 5) && !build_iter_dfa(re)) return RURE_AMD_ERR_DFA;
+  if (which == 5 && !re->iter_a_ok) return RURE_AMD_ERR_DFA;
+  const DenseDfa &d = which == 0 ? re->dfwd : which == 1 ? re->drev : which == 5 ? re->dfwd_iter_a : re->dfwd_iter;
   if (trans) memcpy(trans, d.trans.data(), d.trans.size() * 4);
   if (eof_match) memcpy(eof_match, d.eof_match.data(), d.eof_match.size());
   if (start) memcpy(start, d.start, sizeof(d.start));
