@@ -391,13 +391,20 @@ int rure_amd_match_info_get(rure *re, rure_amd_match_info *info);
  * Pike VM kernel (automaton too large), negative on error. */
 int rure_amd_uses_dfa(rure *re);
 int rure_amd_set_uses_dfa(rure_set *re);
-/* Diagnostics (host only): the forward-scan kernel the last batched
- * find / is_match / shortest_match launch of this process used — 0 = the
- * per-lane streaming kernel, 1 / 2 / 4 = the coalesced-tile kernel with that
- * many bytes per dependent table lookup, -2 = the reverse DFA from the end
- * (DfaAnchoredReverse), -3 = the literal engine (MatchType::Literal), -4 =
- * the chunked cut-bounded scan (long haystacks, small batches split into
- * units); -1 before the first launch. */
+/* Diagnostics (host only): the scan engine the last batched launch of this
+ * process used — 0 = the per-lane streaming kernel, 1 / 2 / 4 = the
+ * coalesced-tile kernel with that many bytes per dependent table lookup,
+ * -2 = the reverse DFA from the end (DfaAnchoredReverse), -3 = the literal
+ * engine (MatchType::Literal), -4 = the chunked cut-bounded scan (long
+ * haystacks, small batches split into units), -5 = the lane search of the
+ * Literal / DfaSuffix match types, -6 = the big (u32) DFA, -7 = the
+ * one-pass multi-group set kernel, -8 = the ragged line kernel, -9 = the
+ * chunked DfaSuffix scan, -10 = the on-demand DFA, -11 = the DfaSuffix
+ * find_iter, -12 / -13 = the chunked find_iter of a look-around regex (no
+ * quit / a quit sent it to the wave path), -14 / -15 = the ASCII-shadow
+ * find_iter (answered / quit), -16 = the Pike VM alone (no DFA), -17 / -18 =
+ * the set kernels over offset batches (one line per lane / line streams);
+ * -1 before the first launch. */
 int rure_amd_last_fwd_path(void);
 /* Diagnostics (bench): rure_amd_kernel_timer(1) resets and starts timing the
  * speculative kernel of every find_iter pass (the dominant kernel of a pass:

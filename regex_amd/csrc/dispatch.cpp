@@ -33,6 +33,7 @@ int pike_grid(size_t count, bool fallback, const NfaDev &n, int cus) {
 
 // Pike VM pass: all haystacks (no DFA) or only those the DFA quit on.
 hipError_t run_pike(int mode, bool fallback, const BatchDev &b, const DevTables &t, void *out, hipStream_t st) {
+  if (!fallback) note_fwd_path(-16);
   int grid = pike_grid(b.count, fallback, t.n, t.cus);
   size_t wb = nfa_wave_bytes(t.n.nleaves);
   if (wb <= kNfaLdsMax) return launch_pike(mode, fallback, b, t.n, out, nullptr, st, grid);

@@ -3,11 +3,13 @@
  * from the HIP runtime, rure_amd_find_batch / _find_iter_batch /
  * _find_iter_span, each checked against the single-haystack rure_find /
  * rure_iter_next of the same library (rure.h:197-330 semantics). */
+#define _POSIX_C_SOURCE 199309L
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "rure_amd.h"
 
@@ -93,6 +95,48 @@ int main(void) {
     got += cnt;
   }
   CHECK(got == total, "spans %zu vs %llu", got, (unsigned long long)total);
+
+  /* Stream order: with ~10 ms of finds queued ahead on a
+   * stream, find_iter of a regex that cannot quit returns while that work is
+   * still running (it only enqueues); find_iter of \w+ (Unicode classes: the
+   * ASCII shadow's quit flag is read back) is on the synchronising list and
+   * returns with the stream drained. */
+  {
+    const size_t BIGL = 4096, BIGN = 65536;
+    uint8_t *big = NULL;
+    rure_match *bm = NULL;
+    hipStream_t st;
+    HIP(hipStreamCreate(&st));
+    HIP(hipMalloc((void **)&big, BIGL * BIGN + 16));
+    HIP(hipMemset(big, 'a', BIGL * BIGN + 16));
+    HIP(hipMalloc((void **)&bm, BIGN * sizeof(rure_match)));
+    rure_amd_batch bb = {big, NULL, BIGL, BIGL, BIGN, 0};
+    rure *lower = rure_compile_must("[a-z]+");
+    rure *word = rure_compile_must("\\w+");
+    for (int pass = 0; pass < 2; ++pass) {
+      rure *r = pass == 0 ? lower : word;
+      /* warm: first calls build and upload tables */
+      CHECK(rure_amd_find_iter_batch(r, &one, dcount, di, cap, dtotal, st) == RURE_AMD_OK, "warm iter");
+      HIP(hipStreamSynchronize(st));
+      for (int i = 0; i < 200; ++i) CHECK(rure_amd_find_batch(re, &bb, bm, st) == RURE_AMD_OK, "queued find");
+      struct timespec t0, t1;
+      clock_gettime(CLOCK_MONOTONIC, &t0);
+      CHECK(rure_amd_find_iter_batch(r, &one, dcount, di, cap, dtotal, st) == RURE_AMD_OK, "iter after queue");
+      clock_gettime(CLOCK_MONOTONIC, &t1);
+      const hipError_t q = hipStreamQuery(st);
+      const double ms = (t1.tv_sec - t0.tv_sec) * 1e3 + (t1.tv_nsec - t0.tv_nsec) * 1e-6;
+      if (pass == 0)
+        CHECK(q == hipErrorNotReady, "find_iter of [a-z]+ waited for the stream (query %d, %.2f ms)", (int)q, ms);
+      else  /* it waited for the ~10 ms of finds queued ahead of it */
+        CHECK(ms > 3.0, "find_iter of \\w+ returned after %.2f ms, before the queued work", ms);
+      HIP(hipStreamSynchronize(st));
+    }
+    rure_free(lower);
+    rure_free(word);
+    hipFree(big);
+    hipFree(bm);
+    HIP(hipStreamDestroy(st));
+  }
 
   rure_free(re);
   hipFree(dev);

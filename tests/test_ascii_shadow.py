@@ -26,7 +26,12 @@ def test_ascii_shadow_equals_full_on_ascii(pat):
     full = re.dfa_tables(2)
     sh = re.dfa_tables(5)
     assert sh is not None, pat
-    assert sh[0]["states"] <= 255 < full[0]["states"] or sh[0]["states"] < full[0]["states"], pat
+    # the property the shadow exists for: it fits the all-rows LDS table
+    # (every state hot, <= 255 of them), the full automaton does not
+    i5, i2 = re.dfa_info(5), re.dfa_info(2)
+    assert i5["states"] <= 255 and i5["hot"] == i5["states"], (pat, i5)
+    assert i2["hot"] < i2["states"], (pat, i2)
+    assert i5["quit"] >= 0 and i2["quit"] < 0, pat  # non-ASCII bytes quit the shadow only
     rev = re.dfa_tables(1)
     quits = 0
     for i in range(6):
