@@ -10,7 +10,8 @@ RT_SRC = regex_amd/csrc/build.cpp regex_amd/csrc/dispatch.cpp regex_amd/csrc/scr
 RT_OBJ = $(patsubst regex_amd/csrc/%.cpp,$(OBJDIR)/rt_%.o,$(RT_SRC))
 KERNEL_SRC = regex_amd/csrc/kernels/dfa_scan.hip regex_amd/csrc/kernels/nfa_scan.hip regex_amd/csrc/kernels/iter_scan.hip \
              regex_amd/csrc/kernels/replace_scan.hip regex_amd/csrc/kernels/gather_scan.hip \
-             regex_amd/csrc/kernels/match_types.hip regex_amd/csrc/kernels/big_dfa.hip regex_amd/csrc/kernels/set_multi.hip
+             regex_amd/csrc/kernels/match_types.hip regex_amd/csrc/kernels/big_dfa.hip regex_amd/csrc/kernels/set_multi.hip \
+             regex_amd/csrc/kernels/run_iter.hip
 KERNEL_OBJ = $(patsubst regex_amd/csrc/kernels/%.hip,$(OBJDIR)/%.o,$(KERNEL_SRC))
 HDRS = $(wildcard regex_amd/csrc/host/*.hpp regex_amd/csrc/host/*.h regex_amd/csrc/kernels/*.hpp include/*.h)
 OBJDIR = regex_amd/build

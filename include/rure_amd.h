@@ -329,6 +329,16 @@ int64_t rure_amd_lex_export(rure *re, uint8_t *table, size_t cap, uint32_t *s0);
  * *s0 = the start row.  Returns the size (0: the lexer does not fit: more
  * than 8 rows or 3 ASCII byte classes, or no lexer table). */
 int64_t rure_amd_lex4_export(rure *re, uint8_t *table, size_t cap, uint32_t *s0);
+/* The lexer tables of the find_iter automaton's ASCII shadow (four = 0: the
+ * byte table, 1: four bytes per step), as rure_amd_lex_export; 0 if the
+ * shadow has none (its first-byte rule may have any number of first bytes:
+ * \w+, \S+, \pL+). */
+int64_t rure_amd_lex_ascii_export(rure *re, int four, uint8_t *table, size_t cap, uint32_t *s0);
+/* 1 if the regex is one byte class repeated (C+, the find_iter run engine:
+ * matches = the maximal runs of C bytes) on all bytes (ascii = 0) or on
+ * ASCII text (ascii = 1, the ASCII shadow: bytes >= 0x80 quit), with cls[b]
+ * bit 0 = b in C, bit 1 = b quits; 0 if not. */
+int rure_amd_run_class_export(rure *re, int ascii, uint8_t *cls);
 
 /* Export of the Pike VM closure tables the NFA kernel runs (host only):
  * leaves = 3 u32 per leaf (kind | lo << 8 | hi << 16, closure, slot),
@@ -402,8 +412,9 @@ int rure_amd_set_uses_dfa(rure_set *re);
  * chunked DfaSuffix scan, -10 = the on-demand DFA, -11 = the DfaSuffix
  * find_iter, -12 / -13 = the chunked find_iter of a look-around regex (no
  * quit / a quit sent it to the wave path), -14 / -15 = the ASCII-shadow
- * find_iter (answered / quit), -16 = the Pike VM alone (no DFA), -17 / -18 =
- * the set kernels over offset batches (one line per lane / line streams);
+ * find_iter (answered / quit), -16 = the Pike VM alone (no DFA), -17 = the
+ * core-form set kernel over an offset batch, -19 / -20 = the find_iter run
+ * engine of a C+ regex (its class over all bytes / the ASCII shadow's);
  * -1 before the first launch. */
 int rure_amd_last_fwd_path(void);
 /* Diagnostics (bench): rure_amd_kernel_timer(1) resets and starts timing the

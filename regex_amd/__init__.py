@@ -599,29 +599,46 @@ class Regex(object):
         n = N.rure_amd_first_byte_export(self._re, buf)
         return bytes(buf[:n]) if n > 0 else None
 
-    def lex_table(self):
+    def lex_table(self, ascii=False):
         """The find_iter lexer table: (flat uint8 table: the entry after byte
         b from entry e is table[76 e + b], start entry), or None (see
-        rure_amd.h rure_amd_lex_export)."""
+        rure_amd.h rure_amd_lex_export).  ascii=True: the ASCII shadow's
+        (rure_amd_lex_ascii_export)."""
         import numpy as np
-        n = N.rure_amd_lex_export(self._re, None, 0, None)
+        if ascii:
+            ex = lambda t, n, s: N.rure_amd_lex_ascii_export(self._re, 0, t, n, s)  # noqa: E731
+        else:
+            ex = lambda t, n, s: N.rure_amd_lex_export(self._re, t, n, s)  # noqa: E731
+        n = ex(None, 0, None)
         if n <= 0:
             return None
         t = np.zeros(n, dtype=np.uint8)
         s0 = ctypes.c_uint32()
-        N.rure_amd_lex_export(self._re, t.ctypes.data, n, ctypes.byref(s0))
+        ex(t.ctypes.data, n, ctypes.byref(s0))
         return t, s0.value
 
-    def lex4_table(self):
-        """The four-bytes-per-step lexer table (rure_amd_lex4_export): (flat
-        uint8 table, start row), or None."""
+    def run_class(self, ascii=False):
+        """The find_iter run engine's class (rure_amd_run_class_export): a
+        256-entry uint8 array (bit 0: the byte is in C, bit 1: it quits) if
+        the regex is C+ (on ASCII text when ascii=True), else None."""
         import numpy as np
-        n = N.rure_amd_lex4_export(self._re, None, 0, None)
+        c = np.zeros(256, dtype=np.uint8)
+        return c if N.rure_amd_run_class_export(self._re, 1 if ascii else 0, c.ctypes.data) == 1 else None
+
+    def lex4_table(self, ascii=False):
+        """The four-bytes-per-step lexer table (rure_amd_lex4_export): (flat
+        uint8 table, start row), or None.  ascii=True: the ASCII shadow's."""
+        import numpy as np
+        if ascii:
+            ex = lambda t, n, s: N.rure_amd_lex_ascii_export(self._re, 1, t, n, s)  # noqa: E731
+        else:
+            ex = lambda t, n, s: N.rure_amd_lex4_export(self._re, t, n, s)  # noqa: E731
+        n = ex(None, 0, None)
         if n <= 0:
             return None
         t = np.zeros(n, dtype=np.uint8)
         s0 = ctypes.c_uint32()
-        N.rure_amd_lex4_export(self._re, t.ctypes.data, n, ctypes.byref(s0))
+        ex(t.ctypes.data, n, ctypes.byref(s0))
         return t, s0.value
 
     def program(self, which):

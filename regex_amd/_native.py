@@ -155,6 +155,8 @@ rure_amd_last_fwd_path = _sig("rure_amd_last_fwd_path", ctypes.c_int)
 rure_amd_first_byte_export = _sig("rure_amd_first_byte_export", ctypes.c_int, VP, VP)
 rure_amd_lex_export = _sig("rure_amd_lex_export", ctypes.c_int64, VP, VP, c_size, VP)
 rure_amd_lex4_export = _sig("rure_amd_lex4_export", ctypes.c_int64, VP, VP, c_size, VP)
+rure_amd_run_class_export = _sig("rure_amd_run_class_export", ctypes.c_int, VP, ctypes.c_int, VP)
+rure_amd_lex_ascii_export = _sig("rure_amd_lex_ascii_export", ctypes.c_int64, VP, ctypes.c_int, VP, c_size, VP)
 rure_amd_set_matches_batch_words = _sig("rure_amd_set_matches_batch_words", ctypes.c_int, VP,
                                         ctypes.POINTER(RureBatch), VP, c_size, VP)
 class MatchInfo(ctypes.Structure):

@@ -835,18 +835,22 @@ DevTables *set_device(rure_set *rs, std::string *err) {
 // earlier starts have priority, dfa.rs:910-1048).  The kernel applies the
 // rule to a search only when every byte it loaded was ASCII (Unicode classes
 // such as `[^\n]` die on invalid UTF-8).  Returns |F| (1..4) or 0.
-uint32_t first_byte_rule(const DenseDfa &d, uint32_t ustart1, bool nonempty, uint8_t bytes[4]) {
-  if (!ustart1 || !nonempty || d.strip.empty() || d.quit >= 0) return 0;
+uint32_t first_byte_rule(const DenseDfa &d, uint32_t ustart1, bool nonempty, uint8_t bytes[4], bool *holds) {
+  *holds = false;
+  if (!ustart1 || !nonempty || d.strip.empty()) return 0;
   const uint32_t a0 = d.strip[ustart1 - 1];
   if ((int)a0 >= d.n_normal) return 0;
+  // (a quit state is allowed only on bytes >= 0x80: the ASCII shadow)
+  auto fails = [&](uint32_t t) { return (int)t == d.dead || (int)t == d.quit; };
   uint32_t nf = 0;
   std::vector<uint32_t> todo;
   std::vector<uint8_t> seen(d.nstates, 0);
   for (int c = 0; c < 128; ++c) {
     const uint32_t t = d.trans[(size_t)a0 * 256 + c];
     if ((int)t == d.dead) continue;
-    if (nf == 4) return 0;
-    bytes[nf++] = (uint8_t)c;
+    if ((int)t == d.quit) return 0;
+    if (nf < 4) bytes[nf] = (uint8_t)c;
+    ++nf;
     if ((int)t < d.n_normal && !seen[t]) { seen[t] = 1; todo.push_back(t); }
   }
   while (!todo.empty()) {  // pre-match states: normal states reached before a match flag
@@ -854,11 +858,69 @@ uint32_t first_byte_rule(const DenseDfa &d, uint32_t ustart1, bool nonempty, uin
     todo.pop_back();
     for (int c = 0; c < 128; ++c) {
       const uint32_t t = d.trans[(size_t)x * 256 + c];
-      if ((int)t == d.dead) return 0;
+      if (fails(t)) return 0;
       if ((int)t < d.n_normal && !seen[t]) { seen[t] = 1; todo.push_back(t); }
     }
   }
-  return nf;
+  *holds = nf > 0;
+  // the generic kernels' SWAR test holds at most four bytes (FwdDfaDev::fb_rep);
+  // the lexer needs only that the rule holds
+  return nf <= 4 && d.quit < 0 ? nf : 0;
+}
+
+// The run engine's class (FwdDfaDev::run_cls, run_iter.hip): true when the
+// find_iter DFA's anchored automaton (strip[start], flag-independent start)
+// is, over its byte columns (all 256, or ASCII: `ascii`, or an automaton
+// whose bytes >= 0x80 quit — the ASCII shadow; the bytes >= 0x80 then quit
+// the run engine too), the automaton of C+ for the byte class C on which it
+// survives its first byte — checked state by state against the ideal
+// automaton R0 -C-> R1, R1 / R2 -C-> R2 (match flag: a match ended one byte
+// before), R1 / R2 -not C-> T (flagged), T -> dead, R0 -not C-> dead, with
+// the one-byte-delayed match flags and dead states of dfa.rs:658-668 and
+// 728-731 agreeing in every reachable pair.  Then the leftmost-first match
+// of a search from p is the maximal run of C bytes starting at the first C
+// byte at or after p (the first-byte rule holds: a run never dies before it
+// has matched), and find_iter (re_trait.rs:197-221) yields exactly the
+// maximal runs.
+bool run_class(const DenseDfa &d, uint32_t ustart1, bool nonempty, uint8_t cls[256], bool ascii) {
+  if (!ustart1 || !nonempty || d.strip.empty()) return false;
+  const int NC = ascii || d.quit >= 0 ? 128 : 256;
+  const uint32_t a0 = d.strip[ustart1 - 1];
+  if ((int)a0 >= d.n_normal) return false;
+  bool in_c[256] = {false};
+  int nc = 0;
+  for (int c = 0; c < NC; ++c) {
+    const uint32_t t = d.trans[(size_t)a0 * 256 + c];
+    if ((int)t == d.quit) return false;
+    in_c[c] = (int)t != d.dead;
+    nc += in_c[c];
+  }
+  if (!nc) return false;
+  auto flagged = [&](uint32_t t) { return (int)t >= d.n_normal && (int)t < d.n_match_end; };
+  // ideal states: 0 = R0, 1 = R1, 2 = R2 (flagged), 3 = T (flagged), 4 = dead
+  auto ideal = [](int r, bool c) { return r == 0 ? (c ? 1 : 4) : (r == 1 || r == 2) ? (c ? 2 : 3) : 4; };
+  std::vector<uint8_t> seen((size_t)d.nstates * 5, 0);
+  std::vector<std::pair<uint32_t, int>> todo{{a0, 0}};
+  seen[(size_t)a0 * 5] = 1;
+  while (!todo.empty()) {
+    const auto [x, r] = todo.back();
+    todo.pop_back();
+    for (int c = 0; c < NC; ++c) {
+      const uint32_t t = d.trans[(size_t)x * 256 + c];
+      const int r2 = ideal(r, in_c[c]);
+      if ((int)t == d.quit) return false;
+      const bool dd = (int)t == d.dead;
+      if (dd != (r2 == 4)) return false;
+      if (dd) continue;
+      if (flagged(t) != (r2 == 2 || r2 == 3)) return false;
+      if (!seen[(size_t)t * 5 + r2]) {
+        seen[(size_t)t * 5 + r2] = 1;
+        todo.push_back({t, r2});
+      }
+    }
+  }
+  for (int c = 0; c < 256; ++c) cls[c] = c < NC ? (in_c[c] ? 1 : 0) : 2;
+  return true;
 }
 
 // The lexer table of FwdDfaDev::lex_image (iter_spec_lex_tile_kernel).
@@ -874,13 +936,17 @@ uint32_t first_byte_rule(const DenseDfa &d, uint32_t ustart1, bool nonempty, uin
 // S0, twin(S0), other twins] so that one clamp of the state number gives the
 // byte's flags (FwdDfaDev::lex_z).  Returns false if the rule does not hold
 // or the states do not fit u8.
-bool build_lex(const DenseDfa &d, uint32_t ustart1, uint32_t fb_n, std::vector<uint8_t> *img,
+bool build_lex(const DenseDfa &d, uint32_t ustart1, bool fb_holds, std::vector<uint8_t> *img,
                       uint32_t *s0_idx) {
   img->clear();
-  if (!fb_n || !ustart1 || d.quit >= 0) return false;
+  if (!fb_holds || !ustart1) return false;
+  // An automaton that quits (the ASCII shadow: bytes >= 0x80 quit) is read
+  // on ASCII columns only: the kernel leaves any block holding a byte >= 0x80
+  // to the tail pass, so its other columns are never stepped.
+  const int NC = d.quit >= 0 ? 128 : 256;
   const uint32_t s0 = ustart1 - 1;
   for (int m = d.n_normal; m < d.n_match_end; ++m)
-    for (int c = 0; c < 256; ++c)
+    for (int c = 0; c < NC; ++c)
       if ((int)d.trans[(size_t)m * 256 + c] != d.dead) return false;
   auto is_match = [&](uint32_t t) { return (int)t >= d.n_normal && (int)t < d.n_match_end; };
   // states reachable from S0 (match transitions replaced by restarts)
@@ -890,7 +956,7 @@ bool build_lex(const DenseDfa &d, uint32_t ustart1, uint32_t fb_n, std::vector<u
   while (!todo.empty()) {
     const uint32_t q = todo.back();
     todo.pop_back();
-    for (int c = 0; c < 256; ++c) {
+    for (int c = 0; c < NC; ++c) {
       uint32_t t = d.trans[(size_t)q * 256 + c];
       if (is_match(t)) t = d.trans[(size_t)s0 * 256 + c];
       if (is_match(t)) return false;  // S0 itself matching on one byte: an empty match
@@ -905,7 +971,7 @@ bool build_lex(const DenseDfa &d, uint32_t ustart1, uint32_t fb_n, std::vector<u
   rows.push_back(s0);
   twin[s0] = (int)rows.size();
   rows.push_back(s0);
-  for (int c = 0; c < 256; ++c) {
+  for (int c = 0; c < NC; ++c) {
     const uint32_t t = d.trans[(size_t)s0 * 256 + c];
     if (twin[t] < 0) { twin[t] = (int)rows.size(); rows.push_back(t); }
   }
@@ -918,6 +984,10 @@ bool build_lex(const DenseDfa &d, uint32_t ustart1, uint32_t fb_n, std::vector<u
   img->assign(((rows.size() - 1) * kRow + 3 * kLexUnit + 256 + 15) & ~(size_t)15, 0);
   for (size_t i = 0; i < rows.size(); ++i)
     for (int c = 0; c < 256; ++c) {
+      if (c >= NC) {  // never stepped: S0
+        (*img)[(size_t)entry((uint32_t)i) * kLexUnit + c] = entry(ps0);
+        continue;
+      }
       const uint32_t t = d.trans[(size_t)rows[i] * 256 + c];
       const int to = is_match(t) ? twin[d.trans[(size_t)s0 * 256 + c]] : plain[t];
       (*img)[(size_t)entry((uint32_t)i) * kLexUnit + c] = entry((uint32_t)to);
@@ -999,10 +1069,19 @@ bool build_iter_dfa(rure *re) {
     re->iter_ok = build_dense_dfa(re->fwd, lim, &re->dfwd_iter, &e) && pack_forward(re->dfwd_iter, &re->pf_iter, &e, true);
     if (!re->lits_done) re->lit_ok = extract_literals(re->nfa, kLitMax, kLitLen, &re->lits);
     re->lits_done = true;
+    bool fb_holds = false;
     if (re->iter_ok)
-      re->fb_n = first_byte_rule(re->dfwd_iter, re->pf_iter.ustart1, !can_match_empty(re->nfa), re->fb_bytes);
-    if (re->iter_ok && build_lex(re->dfwd_iter, re->pf_iter.ustart1, re->fb_n, &re->lex, &re->lex_s0))
+      re->fb_n = first_byte_rule(re->dfwd_iter, re->pf_iter.ustart1, !can_match_empty(re->nfa), re->fb_bytes,
+                                 &fb_holds);
+    // (the lexer of the full automaton keeps the rule's original bound of four
+    // first bytes: wider F are served by the ASCII shadow's lexer below)
+    if (re->iter_ok && fb_holds && build_lex(re->dfwd_iter, re->pf_iter.ustart1, fb_holds, &re->lex, &re->lex_s0))
       build_lex4(re->lex, re->lex_s0, &re->lex4, &re->lex4_s0);
+    // (over all bytes, else over ASCII text: Unicode \S+, \d+, [^\n]+)
+    const bool ne = !can_match_empty(re->nfa);
+    re->run_ok = re->iter_ok && !re->nt.looks_used && re->dfwd_iter.quit < 0 &&
+                 (run_class(re->dfwd_iter, re->pf_iter.ustart1, ne, re->run_cls, false) ||
+                  run_class(re->dfwd_iter, re->pf_iter.ustart1, ne, re->run_cls, true));
     // ASCII shadow (iter_ascii_device): where the automaton is too big for
     // the all-rows LDS table because of its UTF-8 states (Unicode classes),
     // the same automaton with every byte >= 0x80 quitting and the states only
@@ -1020,6 +1099,18 @@ bool build_iter_dfa(rure *re) {
           re->dfwd_iter_a = std::move(a);
           re->pf_iter_a = std::move(pa);
           re->iter_a_ok = true;
+          // its lexer (dense find_iter without reverse scans: \w+, \S+,
+          // \pL+ over ASCII text): the first-byte rule for any number of
+          // first bytes, terminal match states; not with look-around
+          bool holds = false;
+          uint8_t fbb[4];
+          (void)first_byte_rule(re->dfwd_iter_a, re->pf_iter_a.ustart1, !can_match_empty(re->nfa), fbb, &holds);
+          if (holds && !re->nt.looks_used &&
+              build_lex(re->dfwd_iter_a, re->pf_iter_a.ustart1, true, &re->lex_a, &re->lex_a_s0))
+            build_lex4(re->lex_a, re->lex_a_s0, &re->lex4_a, &re->lex4_a_s0);
+          re->run_a_ok = !re->nt.looks_used && !re->run_ok &&
+                         run_class(re->dfwd_iter_a, re->pf_iter_a.ustart1, !can_match_empty(re->nfa), re->run_cls_a,
+                                   true);
         }
       }
     }
@@ -1079,7 +1170,7 @@ bool build_shiftand(const LiteralSet &ls, std::vector<uint64_t> *mask, uint64_t 
 }
 
 // The ASCII shadow of the find_iter DFA on this device (null if none): DFA
-// tables only (no string engines, no first-byte rule), can_quit set.
+// tables and its lexer (no string engines), can_quit set.
 const FwdDfaDev *iter_ascii_device(rure *re, const DevTables &t, std::string *err) {
   if (!build_iter_dfa(re) || !re->iter_a_ok) return nullptr;
   int d = 0;
@@ -1097,6 +1188,9 @@ const FwdDfaDev *iter_ascii_device(rure *re, const DevTables &t, std::string *er
   size_t o_eof = b.add(pf.eof.data(), pf.eof.size());
   size_t o_start = b.add(pf.start.data(), 256);
   size_t o_strip = b.add(strip.data(), strip.size() * 2);
+  size_t o_run = re->run_a_ok ? b.add(re->run_cls_a, 256) : 0;
+  size_t o_lex = re->lex_a.empty() ? 0 : b.add(re->lex_a.data(), re->lex_a.size());
+  size_t o_lex4 = re->lex4_a.empty() ? 0 : b.add(re->lex4_a.data(), re->lex4_a.size());
   DevTables tmp;
   if (!upload_blob(b, &tmp, err)) return nullptr;
   uint8_t *base = (uint8_t *)tmp.blob;
@@ -1106,6 +1200,19 @@ const FwdDfaDev *iter_ascii_device(rure *re, const DevTables &t, std::string *er
   f.hot = pf.hot;
   f.stride = 1;
   f.cus = (uint32_t)t.cus;
+  if (re->run_a_ok) {
+    f.run_cls = base + o_run;
+    f.run_quit = 1;
+  }
+  if (!re->lex_a.empty()) {  // the lexer over ASCII blocks (build_iter_dfa)
+    f.lex_image = base + o_lex;
+    f.lex_bytes = (uint32_t)re->lex_a.size();
+    f.lex_s0 = re->lex_a_s0;
+  }
+  if (!re->lex4_a.empty() && !(getenv("RURE_AMD_LEX4") && getenv("RURE_AMD_LEX4")[0] == '0')) {
+    f.lex4_image = base + o_lex4;
+    f.lex4_s0 = re->lex4_a_s0;
+  }
   f.full = (const uint16_t *)(base + o_full);
   f.eof = base + o_eof;
   f.start = (const uint16_t *)(base + o_start);
@@ -1174,6 +1281,7 @@ const FwdDfaDev *iter_device(rure *re, const DevTables &t, std::string *err) {
   size_t o_sa = sa_img.empty() ? 0 : b.add(sa_img.data(), sa_img.size() * 8);
   size_t o_lex = re->lex.empty() ? 0 : b.add(re->lex.data(), re->lex.size());
   size_t o_lex4 = re->lex4.empty() ? 0 : b.add(re->lex4.data(), re->lex4.size());
+  size_t o_run = re->run_ok ? b.add(re->run_cls, 256) : 0;
   DevTables tmp;
   if (!upload_blob(b, &tmp, err)) return nullptr;
   uint8_t *base = (uint8_t *)tmp.blob;
@@ -1218,6 +1326,10 @@ const FwdDfaDev *iter_device(rure *re, const DevTables &t, std::string *err) {
     f.lex4_image = base + o_lex4;
     f.lex4_s0 = re->lex4_s0;
   }
+  if (re->run_ok) {
+    f.run_cls = base + o_run;
+    f.run_quit = re->run_cls[0x80] >> 1;  // (ASCII-only class: bytes >= 0x80 quit)
+  }
   if (!sa_img.empty()) {
     f.sa_image = (const uint64_t *)(base + o_sa);
     f.sa_init = sa_init;
@@ -1239,6 +1351,7 @@ const FwdDfaDev *iter_device(rure *re, const DevTables &t, std::string *err) {
     f.lex4_image = nullptr;
     f.sa_image = nullptr;
     f.sa_len = f.sa_bits = 0;
+    f.run_cls = nullptr;
   }
   re->iter_dev[d] = {tmp.blob, f};
   return &re->iter_dev[d].second;

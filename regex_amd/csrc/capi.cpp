@@ -835,6 +835,23 @@ int64_t rure_amd_lex4_export(rure *re, uint8_t *table, size_t cap, uint32_t *s0)
   return (int64_t)re->lex4.size();
 }
 
+int64_t rure_amd_lex_ascii_export(rure *re, int four, uint8_t *table, size_t cap, uint32_t *s0) {
+  if (!re) return RURE_AMD_ERR_ARG;
+  if (!build_iter_dfa(re)) return RURE_AMD_ERR_DFA;
+  const std::vector<uint8_t> &t = four ? re->lex4_a : re->lex_a;
+  if (table) memcpy(table, t.data(), std::min(cap, t.size()));
+  if (s0) *s0 = four ? re->lex4_a_s0 : re->lex_a_s0;
+  return (int64_t)t.size();
+}
+
+int rure_amd_run_class_export(rure *re, int ascii, uint8_t *cls) {
+  if (!re) return RURE_AMD_ERR_ARG;
+  if (!build_iter_dfa(re)) return RURE_AMD_ERR_DFA;
+  const bool ok = ascii ? re->run_a_ok : re->run_ok;
+  if (ok && cls) memcpy(cls, ascii ? re->run_cls_a : re->run_cls, 256);
+  return ok ? 1 : 0;
+}
+
 int rure_amd_first_byte_export(rure *re, uint8_t *bytes) {
   if (!re) return RURE_AMD_ERR_ARG;
   if (!build_iter_dfa(re)) return RURE_AMD_ERR_DFA;

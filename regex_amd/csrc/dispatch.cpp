@@ -847,11 +847,33 @@ hipError_t run_find_iter(rure *re, DevTables *t, const BatchDev &b, const IterOu
       // RURE_AMD_ITER_CHUNK: the unit size in bytes (tests: many boundaries)
       if (const char *v = getenv("RURE_AMD_ITER_CHUNK")) chunk = std::max<uint64_t>(16, strtoull(v, nullptr, 10));
     }
+    // A regex that is one byte class repeated (C+: [a-z]+, (?-u)\w+): its
+    // matches are the maximal runs (run_iter.hip), no DFA walk; its ASCII
+    // shadow's class (Unicode \w+, \S+, \pL+) answers ASCII text and quits
+    // on any other byte.  RURE_AMD_RUNS=0 keeps the DFA paths (A/B).
+    const char *rv = getenv("RURE_AMD_RUNS");
+    const bool runs = !sp && !(rv && rv[0] == '0');
+    if (runs && fi->run_cls) {
+      bool q = false;
+      const hipError_t e = launch_find_iter_runs(b, fi->run_cls, o, st, t->cus, fi->run_quit != 0, &q);
+      if (e != hipErrorNotSupported && (e != hipSuccess || !q)) {
+        if (e == hipSuccess) note_fwd_path(-19);
+        return e;
+      }
+    }
     // the ASCII shadow first (all-rows LDS tables; a non-ASCII byte quits
     // and the full automaton re-runs the batch, still chunked); not for
     // spans (the quit is read back)
     if (!sp) {
       if (const FwdDfaDev *fa = iter_ascii_device(re, *t, err)) {
+        if (runs && fa->run_cls) {
+          bool q = false;
+          const hipError_t e = launch_find_iter_runs(b, fa->run_cls, o, st, t->cus, true, &q);
+          if (e != hipErrorNotSupported && (e != hipSuccess || !q)) {
+            if (e == hipSuccess) note_fwd_path(-20);
+            return e;
+          }
+        }
         bool q = false;
         const hipError_t e = launch_find_iter(b, fa, t->r, &t->n, true, chunk, o, st, t->cus, sp, nullptr, &q);
         if (e != hipSuccess || !q) {

@@ -758,259 +758,6 @@ __global__ __launch_bounds__(1024) void set_core_kernel(BatchDev bt, SetCoreDev 
   }
 }
 
-// ------------------------------------------------------- sets, line streams
-// set_core_kernel runs one line per lane, so a wave's 64 lines take as long
-// as the longest (C4's uniform 40-160-byte lines: about 2/3 of the lane steps
-// are useful) and every line pays a masked head and tail chunk.  Here a lane
-// owns a contiguous run of lines instead — a wave's lines split into 64
-// equal byte ranges — and streams it as aligned 16-byte blocks, one block
-// per step of the wave loop, every lane busy until the wave's bytes are
-// done.  A line ends inside a block at byte jb: the dependent chain's row is
-// replaced by the next line's start core on that byte (one select on the
-// chain), the state before it is kept for the ending line's EOF mask, and
-// the output codes of the block split at jb into the ending line's bag and
-// the next line's (the masks of a line are the OR of its codes' masks,
-// dfa.rs:525-570 / exec.rs:998-1038 report the union).  A block holding a
-// second line end (lines shorter than 16 bytes, empty lines), a step that
-// leaves the hot cores and a code that needs the global mask table take the
-// careful path: the block again, byte by byte, from the state it was entered
-// with.  Blocks arrive through a ring of four loads in flight per lane (the
-// loop is unrolled over the ring, so no load result is moved or waited for
-// before its turn).  A wave whose lines are short on average (< kStreamMinLen
-// bytes: the careful path would dominate) runs them one line per lane.
-constexpr uint32_t kStreamMinLen = 48;
-
-struct StreamLine {        // one lane's position in its run of lines
-  uint64_t h;              // the next line to start (lines [h0, h1) are the lane's)
-  uint64_t e;              // where the current line ends (= offs[h])
-  uint64_t e2, e3;         // offs[h + 1], offs[h + 2] (clamped): loaded ahead
-  uint32_t t;              // the current core
-  uint32_t cur;            // a line of the lane is in progress (line h - 1)
-  uint64_t bag;            // its output codes so far
-  uint64_t dmask;          // masks its careful steps collected directly
-};
-
-// A line's result: the code bag through the LDS mask table (four lookups per
-// round), the masks collected directly, the EOF mask of the final core.
-__device__ __forceinline__ uint64_t stream_result(const SetCoreDev &f, const uint64_t *MT, const uint64_t *HE,
-                                                  uint64_t bag, uint64_t dmask, uint32_t t, uint32_t *qf) {
-  if (t == f.quit) { note_quit(qf); return QUITMARK; }
-  uint64_t mask = dmask;
-  uint64_t bb = bag & 0x7FFFFFFFFFFFFFFEull;
-  while (bb) {
-    uint32_t i[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      i[q] = bb ? (uint32_t)__builtin_ctzll(bb) : 0u;
-      bb &= bb - 1;
-    }
-    mask |= MT[i[0]] | MT[i[1]] | MT[i[2]] | MT[i[3]];
-  }
-  if (t != f.dead) mask |= t < f.hot ? HE[t] : f.eof[t];
-  return mask;
-}
-
-// The careful path: block [p, p + 16) byte by byte from the state the lane
-// entered it with, any number of line ends (empty lines included), LDS rows
-// for hot cores and the global tables otherwise.  Leaves e2 / e3 reloaded.
-__device__ __forceinline__ void stream_careful(StreamLine &L, const BatchDev &bt, const SetCoreDev &f, const uint8_t *cls,
-                                            const uint64_t *MT, const uint16_t *ST, const uint64_t *HE, uint4 v,
-                                            uint64_t p, uint64_t h1, uint64_t *out) {
-  const uint32_t K2 = 2 * (f.K + 1);
-  const uint64_t n = bt.count;
-  for (uint32_t j = 0; j < 16; ++j) {
-    const uint64_t pos = p + j;
-    while (pos == L.e) {  // the current line ends before byte pos
-      if (L.cur) out[L.h - 1] = stream_result(f, MT, HE, L.bag, L.dmask, L.t, bt.quit_flag);
-      if (L.h >= h1) { L.cur = 0; L.e = ~0ull; return; }
-      const uint64_t e_new = bt.offs[L.h + 1];
-      const uint32_t b = e_new > pos ? block_byte(v, j) : 0u;
-      L.t = ST[fwd_flag_index_bytes(e_new - pos, 0, 0, b)];
-      L.cur = 1;
-      L.bag = 0;
-      L.dmask = 0;
-      L.h += 1;
-      L.e = e_new;
-    }
-    if (L.t == f.dead || L.t == f.quit) continue;
-    const uint32_t k2 = cls[block_byte(v, j)];
-    if (L.t < f.hot) {  // an LDS row, unless the step leaves the hot cores
-      const uint32_t en = core_entry(L.t, K2, k2);
-      if ((en >> 6) != f.hot) {
-        if ((en & 63) == 63) L.dmask |= f.gout[(size_t)L.t * f.K + (k2 >> 1)];
-        else L.bag |= 1ull << (en & 63);
-        L.t = en >> 6;
-        continue;
-      }
-    }
-    const size_t i = (size_t)L.t * f.K + (k2 >> 1);
-    L.dmask |= f.gout[i];
-    L.t = f.gcore[i];
-  }
-  L.e2 = bt.offs[L.h + 1 < n ? L.h + 1 : n];
-  L.e3 = bt.offs[L.h + 2 < n ? L.h + 2 : n];
-}
-
-__global__ __launch_bounds__(1024) void set_stream_kernel(BatchDev bt, SetCoreDev f, uint64_t *out) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  for (uint32_t i = threadIdx.x * 16; i < f.lds_bytes; i += blockDim.x * 16)
-    *(uint4 *)(lds + i) = *(const uint4 *)(f.lds_image + i);
-  uint16_t *ST = (uint16_t *)(lds + core_start_off(f.lds_bytes));
-  uint64_t *HE = (uint64_t *)(lds + core_start_off(f.lds_bytes) + 256);
-  if (threadIdx.x < 128) ST[threadIdx.x] = f.start[threadIdx.x];
-  for (uint32_t i = threadIdx.x; i < f.hot; i += blockDim.x) HE[i] = f.eof[i];
-  __syncthreads();
-  if (threadIdx.x < 256) lds[threadIdx.x] = (uint8_t)(2 * lds[threadIdx.x]);  // class map, doubled (K < 128)
-  __syncthreads();
-  const uint8_t *cls = lds;
-  const uint64_t *MT = (const uint64_t *)(lds + f.mt_off);
-  const uint64_t n = bt.count;
-  const uint64_t *offs = bt.offs;
-  const uint32_t lane = threadIdx.x & 63;
-  const uint64_t gw = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-  const uint64_t H0 = gw * n / nw, H1 = (gw + 1) * n / nw;
-  if (H0 >= H1) return;  // (wave-uniform)
-  const uint64_t A = offs[H0], Bw = offs[H1];
-  if (Bw - A < (H1 - H0) * kStreamMinLen) {  // short lines: one line per lane
-    for (uint64_t h = H0 + lane; h < H1; h += 64) {
-      const uint64_t o0 = offs[h], o1 = offs[h + 1];
-      const uint8_t *p = bt.hay + o0;
-      const uint4 *a = (const uint4 *)(p - ((uintptr_t)p & 15));
-      const uint4 *q0 = o1 > o0 ? a : (const uint4 *)offs;  // (offs: 16 readable bytes)
-      const uint4 hb = *q0, b1 = *(o1 - o0 > 16 - ((uintptr_t)p & 15) ? a + 1 : q0);
-      out[h] = core_scan_one<false>(f, cls, MT, ST, HE, p, o1 - o0, 0, hb, b1, bt.quit_flag, nullptr, [] {});
-    }
-    return;
-  }
-  // this lane's lines: those starting in [T_lane, T_lane+1) of the wave's bytes
-  const uint64_t T = A + (Bw - A) * lane / 64;
-  uint64_t h0 = H0;
-  if (A < T) {  // first line h in (H0, H1] with offs[h] >= T: interpolation / bisection
-    uint64_t lo = H0, hi = H1, vlo = A, vhi = Bw;
-    for (uint32_t it = 0; hi - lo > 1; ++it) {
-      uint64_t g;
-      if (it >= 2 && (it & 1)) g = lo + (hi - lo) / 2;
-      else g = lo + (uint64_t)((double)(T - vlo) / (double)(vhi - vlo) * (double)(hi - lo));
-      g = g <= lo ? lo + 1 : g >= hi ? hi - 1 : g;
-      const uint64_t x = offs[g];
-      if (x < T) { lo = g; vlo = x; } else { hi = g; vhi = x; }
-    }
-    h0 = hi;
-  }
-  uint64_t h1 = ((uint64_t)__shfl_down((unsigned)(h0 >> 32), 1) << 32) | (uint64_t)__shfl_down((unsigned)h0, 1);
-  if (lane == 63) h1 = H1;
-  const uint32_t K2 = 2 * (f.K + 1), hot = f.hot;
-  const uint32_t S_w = min(ST[1 | 4 | 16], hot), S_nw = min(ST[1 | 4 | 32], hot);
-  StreamLine L;
-  L.h = h0;
-  L.e = offs[h0];
-  L.e2 = offs[h0 + 1 < n ? h0 + 1 : n];
-  L.e3 = offs[h0 + 2 < n ? h0 + 2 : n];
-  L.t = hot;  // (the bytes before the first line: nobody's)
-  L.cur = 0;
-  L.bag = 0;
-  L.dmask = 0;
-  const uint64_t B1 = offs[h1];
-  const uint64_t p0 = L.e & ~15ull;
-  const uint64_t plast = B1 > p0 ? (B1 - 1) & ~15ull : p0;
-  bool done = h0 >= h1;
-  const uint8_t *hay = bt.hay;
-  auto ld = [&](uint64_t q) { return *(const uint4 *)(hay + (q < plast ? q : plast)); };
-  uint4 r0 = ld(p0), r1 = ld(p0 + 16), r2 = ld(p0 + 32), r3 = ld(p0 + 48);
-  uint64_t p = p0;
-  // One block: the chain with the line end at jb (16 = none), then commit.
-  auto step = [&](uint4 &rr) {
-    const uint4 v = rr;
-    rr = ld(p + 64);
-#ifndef RURE_STREAM_SYNTH
-    const uint64_t d = L.e - p;  // >= 0: every line end before p has been taken
-    const bool bnd = d < 16;
-    const uint32_t jb = bnd ? (uint32_t)d : 16u;
-    const bool nxt = bnd && L.h < h1;
-    const bool multi = nxt && L.e2 - p < 16;
-#else  // diagnostic A/B: line ends from the block index (no offsets in the loop)
-    const uint32_t bi = (uint32_t)(p >> 4);
-    const bool bnd = (bi * 0x9E3779B1u >> 29) == 0 && p < plast;
-    const uint32_t jb = bnd ? (bi * 7u) & 15u : 16u;
-    const bool nxt = bnd;
-    const bool multi = false;
-#endif
-    const uint32_t b0 = block_byte(v, jb & 15);
-    const uint32_t S = word_byte(b0) ? S_w : S_nw;
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-    uint32_t kc[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) kc[j] = cls[(w[j >> 2] >> ((j & 3) * 8)) & 0xFF];
-    const uint32_t lom = (1u << jb) - 1u;   // bytes of the ending line
-    const uint32_t him = ~lom & 0xFFFFu;    // bytes of the next line
-    uint32_t t = L.t < hot ? L.t : hot, tb = t;
-    uint32_t lo0 = 0, lo1 = 0, hi0 = 0, hi1 = 0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const bool at = (uint32_t)j == jb;
-      tb = at ? t : tb;
-      const uint32_t tt = at ? S : t;
-      const uint32_t en = core_entry(tt, K2, kc[j]);
-      t = en >> 6;
-      const uint64_t vv = 1ull << (en & 63);
-      const uint32_t ml = (uint32_t)__builtin_amdgcn_sbfe((int)lom, j, 1);
-      const uint32_t mh = (uint32_t)__builtin_amdgcn_sbfe((int)him, j, 1);
-      lo0 |= (uint32_t)vv & ml;
-      lo1 |= (uint32_t)(vv >> 32) & ml;
-      hi0 |= (uint32_t)vv & mh;
-      hi1 |= (uint32_t)(vv >> 32) & mh;
-    }
-    const uint64_t lo = ((uint64_t)lo1 << 32) | lo0, hi = ((uint64_t)hi1 << 32) | hi0;
-    // (the bytes after the lane's last line end and before its first line
-    // are nobody's: their states and codes do not count)
-    const bool live = !bnd || nxt;
-    const bool careful = !done && (multi || (live && t == hot) || (bnd && L.cur && tb == hot) ||
-                                   (L.cur && (lo >> 63)) || (nxt && (hi >> 63)));
-    if (careful) {
-      stream_careful(L, bt, f, cls, MT, ST, HE, v, p, h1, out);
-      done = L.h >= h1 && !L.cur;
-    } else if (!done) {
-      if (bnd) {
-        if (L.cur) out[L.h - 1] = stream_result(f, MT, HE, L.bag | lo, L.dmask, tb, bt.quit_flag);
-        if (nxt) {
-          L.cur = 1;
-          L.h += 1;
-#ifndef RURE_STREAM_SYNTH
-          L.e = L.e2;
-          L.e2 = L.e3;
-          L.e3 = offs[L.h + 2 < n ? L.h + 2 : n];
-#else
-          if (L.h >= n) L.h = n - 1;
-#endif
-        } else {
-          L.cur = 0;
-          done = true;
-        }
-        L.bag = hi;
-        L.dmask = 0;
-      } else {
-        L.bag |= lo;
-      }
-      L.t = t;
-    }
-    p += 16;
-  };
-#ifdef RURE_STREAM_SYNTH
-  done = h0 >= h1;
-  auto fin = [&]() { if (p > plast + 64) done = true; };
-#else
-  auto fin = [&]() {};
-#endif
-  while (__any(!done)) {
-    fin();
-    step(r0);
-    step(r1);
-    step(r2);
-    step(r3);
-  }
-}
-
 // Visit counts per core over a sample of the batch (global tables only): the
 // host then re-ranks the cores so the LDS table holds the ones this data
 // visits — the adaptive counterpart of the reference's lazily filled cache
@@ -1083,18 +830,6 @@ hipError_t launch_set_cores(const BatchDev &b, const SetCoreDev &f, uint64_t *ou
       for (int k = 0; k < 5; ++k) sum[k] += (double)hp[w * 5 + k];
     fprintf(stderr, "core_prof per wave (memtime ticks): prologue+head %.0f body %.0f tail %.0f finish %.0f prefetch %.0f\n",
             sum[0] / nw, sum[1] / nw, sum[2] / nw, sum[3] / nw, sum[4] / nw);
-    return hipGetLastError();
-  }
-  // Offset batches of lines searched from 0: the line-stream kernel, opt-in
-  // (RURE_AMD_SET_STREAM=1) until it wins its A/B
-  const char *sv = getenv("RURE_AMD_SET_STREAM");
-  if (mode == 1 && b.start == 0 && bs == 1024 && sv && sv[0] == '1') {
-    if (lds > 64 * 1024 &&
-        (e = hipFuncSetAttribute((const void *)set_stream_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)lds)) != hipSuccess)
-      return e;
-    hipLaunchKernelGGL(set_stream_kernel, dim3(cus * per_cu), dim3(1024), lds, st, b, f, out);
-    note_fwd_path(-18);
     return hipGetLastError();
   }
   if (mode == 1) note_fwd_path(-17);

@@ -120,6 +120,11 @@ struct FwdDfaDev {
   // DFA can quit (Unicode word boundary: a quit sends the batch to the wave
   // path).  The literal, Shift-And, lexer and first-byte engines are off.
   uint32_t looks, can_quit;
+  // find_iter DFA only: the regex is one byte class repeated (C+, host
+  // run_class): run_cls[b] bit 0 = b is in C, bit 1 = b quits (the ASCII
+  // shadow: bytes >= 0x80); null: not such a regex (run_iter.hip)
+  const uint8_t *run_cls;
+  uint32_t run_quit;  // some byte quits (bit 1): the run engine's flag is read back
 };
 constexpr uint32_t kLexMaxRows = 24;  // lexer table rows (iter_spec_lex_tile_kernel's static LDS)
 constexpr uint32_t kLexUnit = kRow / 4;  // lexer entry -> row address multiplier
@@ -299,6 +304,12 @@ struct IterSpan {
   uint64_t *exit;
   uint64_t tail;  // the text length when the span runs to the end (hi = ~0), else ~0
 };
+// find_iter of a C+ regex (FwdDfaDev::run_cls, run_iter.hip): fixed-stride
+// batches whose searched bytes are 16-byte aligned (hipErrorNotSupported
+// otherwise); *quit = a byte of the quit class was read (can_quit: the
+// flag is read back) and the results are not the answer.
+hipError_t launch_find_iter_runs(const BatchDev &b, const uint8_t *cls, const IterOut &o, hipStream_t st, int cus,
+                                 bool can_quit, bool *quit);
 hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaDev &r, const NfaDev *nf,
                             bool chunked, uint64_t chunk, const IterOut &o, hipStream_t st, int cus,
                             const IterSpan *span = nullptr, const MatchDev *mt = nullptr, bool *quit = nullptr);

@@ -439,6 +439,186 @@ __global__ __launch_bounds__(256) void replace_copy1_kernel(CopyCtx c, uint8_t *
   }
 }
 
+// replace_copy1_kernel moves 1 KiB per wave per round, and every wave runs
+// the per-byte path of the blocks that hold a replacement edge: nearly every
+// 1 KiB window of the regex-dna strip (an edge every ~61 bytes) or of an IUB
+// substitution holds one, so the path ran for the whole wave with a few
+// lanes active — 3.7 G VALU instructions per strip pass, 4.9-5.6 ms
+// (profiles/r05_replace_pmc.txt).  Here a wave takes kGroupWin windows
+// (4 KiB of output) per round with one staging of the group's matches in
+// LDS, copies the blocks that lie in one text stretch (two aligned loads and
+// a funnel shift, all four windows' loads in flight together), and gathers
+// the group's edge blocks into an LDS list that the whole wave then works
+// through, every lane busy (no global atomics: a single edge list counter
+// for the grid serialised the waves, 25 ms).
+constexpr uint32_t kGroupWin = 4, kGroupSlots = 128;
+
+// 16 bytes from any address without a branch: both aligned blocks are always
+// loaded (the second is the first again when p is aligned, so nothing past
+// the block holding p[15] is read), then a funnel shift by 8 * (p & 15) bits.
+__device__ __forceinline__ uint4 load16u_nb(const uint8_t *p) {
+  const uint32_t off = (uint32_t)((uintptr_t)p & 15);
+  const uint8_t *a0 = p - off;  // (pointer arithmetic keeps the global address space)
+  const uint4 x = *(const uint4 *)a0;
+  const uint4 y = *(const uint4 *)(a0 + (off ? 16 : 0));
+  const uint64_t w0 = ((uint64_t)x.y << 32) | x.x, w1 = ((uint64_t)x.w << 32) | x.z;
+  const uint64_t w2 = ((uint64_t)y.y << 32) | y.x, w3 = ((uint64_t)y.w << 32) | y.z;
+  const bool hi = off >= 8;
+  const uint64_t u0 = hi ? w1 : w0, u1 = hi ? w2 : w1, u2 = hi ? w3 : w2;
+  const uint32_t sh = (off & 7) * 8;
+  const uint64_t r0 = sh ? (u0 >> sh) | (u1 << (64 - sh)) : u0;
+  const uint64_t r1 = sh ? (u1 >> sh) | (u2 << (64 - sh)) : u1;
+  return make_uint4((uint32_t)r0, (uint32_t)(r0 >> 32), (uint32_t)r1, (uint32_t)(r1 >> 32));
+}
+
+// matches of the group with R <= p0 (slots 1..a of the staged records)
+__device__ __forceinline__ uint32_t group_passed(const uint64_t *R, uint32_t cnt, uint64_t p0) {
+  uint32_t a = 0, bnd = cnt;
+  while (a < bnd) {
+    const uint32_t mid = (a + bnd) >> 1;
+    if (R[1 + mid] <= p0) a = mid + 1;
+    else bnd = mid;
+  }
+  return a;
+}
+
+// Blocks the group cannot do with its staged records (a dense group, a block
+// with more than three replacement starts: rare) go to a global list, done
+// by replace_rest_kernel through the generic per-block path (plan_block,
+// copy_block_slow: a function call would hold ~140 VGPRs in this kernel);
+// past the list's capacity replace_rest_kernel redoes the whole output.
+__device__ __forceinline__ void push_rest(uint32_t *rest, uint64_t rest_cap, unsigned long long *nrest, uint64_t p0) {
+  const unsigned long long k = atomicAdd(nrest, 1ull);
+  if (k < rest_cap) rest[k] = (uint32_t)(p0 >> 4);
+}
+
+__global__ __launch_bounds__(256) void replace_copy4_kernel(CopyCtx c, uint8_t *out, uint32_t *rest, uint64_t rest_cap,
+                                                            unsigned long long *nrest) {
+  __shared__ uint64_t sR[4][kGroupSlots], sE[4][kGroupSlots];
+  __shared__ uint16_t sEdge[4][kGroupWin * 64];
+  const uint64_t total = c.ooff[1] < c.cap ? c.ooff[1] : c.cap;
+  c.total = total;
+  const uint64_t nm = c.moff[1];
+  const uint64_t nwin = (total + kWin - 1) / kWin;
+  const uint64_t ngrp = (nwin + kGroupWin - 1) / kGroupWin;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint64_t base, len;
+  hay_of(c.bt, 0, &base, &len);
+  const uint8_t *hay = c.bt.hay + base;
+  const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  // widx has nwin + 2 entries: windows past the end clamp to the last one
+  auto wx = [&](uint64_t w) { return c.widx[w < nwin ? w : nwin]; };
+  uint64_t grp = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+  uint64_t lo = wx(grp * kGroupWin), hi = wx(grp * kGroupWin + kGroupWin);
+  for (; grp < ngrp; grp += nwaves) {
+    const uint64_t w0 = grp * kGroupWin;
+    const uint64_t cnt = hi - lo;
+    // the next group's window index, a round ahead
+    const uint64_t lo_n = wx((grp + nwaves) * kGroupWin), hi_n = wx((grp + nwaves) * kGroupWin + kGroupWin);
+    if (cnt + 5 > kGroupSlots) {  // dense group: the generic per-block path
+#pragma unroll 1
+      for (uint32_t q = 0; q < kGroupWin; ++q) {
+        const uint64_t p0 = (w0 + q) * kWin + 16 * (uint64_t)lane;
+        if (w0 + q < nwin && p0 < total) push_rest(rest, rest_cap, nrest, p0);
+      }
+      lo = lo_n;
+      hi = hi_n;
+      continue;
+    }
+    const uint64_t *R = sR[wv], *E = sE[wv];
+#pragma unroll
+    for (uint32_t s = lane; s < kGroupSlots; s += 64) {  // slot s = match lo - 1 + s
+      const int64_t g = (int64_t)lo - 1 + (int64_t)s;
+      const bool ok = g >= 0 && (uint64_t)g < nm && s < cnt + 5;
+      sR[wv][s] = ok ? c.G[g] : ~0ull;
+      sE[wv][s] = ok ? c.m[2 * g + 1] : 0;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    uint4 v[kGroupWin];
+    uint32_t fastm = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kGroupWin; ++q) {
+      const uint64_t p0 = (w0 + q) * kWin + 16 * (uint64_t)lane;
+      const uint32_t a = group_passed(R, (uint32_t)cnt, p0);
+      const uint64_t jj = lo + a;
+      const uint64_t nextR = R[a + 1];
+      const uint64_t r = jj ? R[a] : 0;
+      const bool fast = p0 + 16 <= total && p0 + 16 <= nextR && (jj == 0 || p0 - r >= c.rep_len);
+      const uint64_t src = fast ? (jj ? E[a] + (p0 - r - c.rep_len) : p0) : 0;
+      v[q] = load16u_nb(hay + src);
+      fastm |= fast ? 1u << q : 0u;
+    }
+    // the group's other blocks (inside the output) onto the wave's LDS list
+    uint32_t ne = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kGroupWin; ++q) {
+      const uint64_t p0 = (w0 + q) * kWin + 16 * (uint64_t)lane;
+      if (fastm >> q & 1) *(uint4 *)(out + p0) = v[q];
+      const bool edge = !(fastm >> q & 1) && p0 < total;
+      const uint64_t m = __ballot(edge);
+      if (edge) sEdge[wv][ne + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)(64 * q + lane);
+      ne += (uint32_t)__popcll(m);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll 1
+    for (uint32_t r0 = 0; r0 < ne; r0 += 64) {
+      if (r0 + lane >= ne) continue;
+      const uint32_t id = sEdge[wv][r0 + lane];
+      const uint64_t p0 = (w0 + (id >> 6)) * kWin + 16 * (uint64_t)(id & 63);
+      const uint32_t a = group_passed(R, (uint32_t)cnt, p0);
+      const uint64_t jj = lo + a;
+      if (p0 + 16 <= total && R[a + 4] > p0 + 15) {
+        // at most three replacement starts in the block: each byte's source
+        // from the staged records, the 16 byte loads independent
+        const uint64_t R0 = R[a], R1 = R[a + 1], R2 = R[a + 2], R3 = R[a + 3];
+        const uint64_t E0 = E[a], E1 = E[a + 1], E2 = E[a + 2], E3 = E[a + 3];
+        uint32_t x[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const uint64_t lc = p0 + i;
+          const uint32_t idx = (R1 <= lc) + (R2 <= lc) + (R3 <= lc);
+          uint8_t ch;
+          if (jj == 0 && idx == 0) {
+            ch = hay[lc];
+          } else {
+            const uint64_t rr = idx == 0 ? R0 : idx == 1 ? R1 : idx == 2 ? R2 : R3;
+            const uint64_t ee = idx == 0 ? E0 : idx == 1 ? E1 : idx == 2 ? E2 : E3;
+            const uint64_t off = lc - rr;
+            ch = off < c.rep_len ? c.rep[off] : hay[ee + (off - c.rep_len)];
+          }
+          x[i >> 2] |= (uint32_t)ch << (8 * (i & 3));
+        }
+        *(uint4 *)(out + p0) = make_uint4(x[0], x[1], x[2], x[3]);
+      } else {
+        push_rest(rest, rest_cap, nrest, p0);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    lo = lo_n;
+    hi = hi_n;
+  }
+}
+
+__global__ __launch_bounds__(256) void replace_rest_kernel(CopyCtx c, uint8_t *out, const uint32_t *rest,
+                                                           uint64_t rest_cap, const unsigned long long *nrest) {
+  c.total = c.ooff[1] < c.cap ? c.ooff[1] : c.cap;
+  const uint64_t n = *nrest;
+  const bool all = n > rest_cap;  // the list overflowed: every block
+  const uint64_t cnt = all ? (c.total + 15) / 16 : n;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t p0 = all ? i << 4 : (uint64_t)rest[i] << 4;
+    const BlockPlan b = plan_block(c, p0 / kWin, p0);
+    if (b.fast) *(uint4 *)(out + p0) = load16u(c.bt.hay + b.src);
+    else copy_block_slow(c, p0, b, out);
+  }
+}
+
 // SplitN (re_bytes.rs:699-749): with m = k matches + (tail non-empty), a limit
 // of `lim` fields gives all m fields when lim - 1 > m, else lim - 1 fields and
 // the remainder of the text after them.
@@ -602,14 +782,30 @@ hipError_t launch_replace_copy(const BatchDev &b, const uint64_t *ooff, const ui
     c.total = 0;
     c.cap = cap;
     c.rep = rep;
-    if (b.count == 1 && limit == ~0ull && !getenv("RURE_AMD_REPLACE_GENERIC"))
+    const char *cv = getenv("RURE_AMD_REPLACE_COPY");  // A/B: 1 = one window per round
+    if (b.count == 1 && limit == ~0ull && cv && cv[0] == '1')
       hipLaunchKernelGGL(replace_copy1_kernel, dim3(grid_for_items((total_hint + 15) / 16, 256, cus)), dim3(256), 0,
                          st, c, out);
+    else if (b.count == 1 && limit == ~0ull && !(cv && cv[0] == 'g') && total_hint < (1ull << 36)) {
+      const uint64_t nblk = (total_hint + 15) / 16, rcap = std::max<uint64_t>(4096, nblk / 16);
+      uint32_t *rest = nullptr;
+      e = scratch_malloc((void **)&rest, rcap * 4 + 256, st);  // (u32 block indices: outputs < 64 GiB)
+      unsigned long long *nrest = rest ? (unsigned long long *)(rest + ((rcap + 1) & ~(uint64_t)1)) : nullptr;
+      if (e == hipSuccess) e = hipMemsetAsync(nrest, 0, 8, st);
+      if (e == hipSuccess) {
+        hipLaunchKernelGGL(replace_copy4_kernel, dim3(grid_for_items((total_hint + 63) / 64, 256, cus)), dim3(256), 0,
+                           st, c, out, rest, rcap, nrest);
+        hipLaunchKernelGGL(replace_rest_kernel, dim3(grid_for_items(nblk / 64 + 1, 256, cus)), dim3(256), 0, st, c,
+                           out, rest, rcap, nrest);
+        e = hipGetLastError();
+      }
+      if (rest) { hipError_t e2 = scratch_free(rest, st); if (e == hipSuccess) e = e2; }
+    }
     else
       hipLaunchKernelGGL(replace_copy_kernel,
                          dim3(grid_for_items((total_hint + 16 * kCopyILP - 1) / (16 * kCopyILP), 256, cus)),
                          dim3(256), 0, st, c, out);
-    e = hipGetLastError();
+    if (e == hipSuccess) e = hipGetLastError();
   }
   for (uint64_t *q : {G, widx})
     if (q) { hipError_t e2 = scratch_free(q, st); if (e == hipSuccess) e = e2; }

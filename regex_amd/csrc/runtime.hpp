@@ -267,6 +267,12 @@ struct rure {
   bool iter_a_ok = false;
   DenseDfa dfwd_iter_a;
   PackedFwd pf_iter_a;
+  std::vector<uint8_t> lex_a, lex4_a;  // its lexer tables (build_lex / build_lex4), empty if none
+  uint32_t lex_a_s0 = 0, lex4_a_s0 = 0;
+  // the run engine's byte classes (run_class: the regex is C+), for the
+  // find_iter DFA over all bytes and for its ASCII shadow
+  bool run_ok = false, run_a_ok = false;
+  uint8_t run_cls[256] = {0}, run_cls_a[256] = {0};
   std::map<int, std::pair<void *, FwdDfaDev>> iter_dev_a;
 };
 
@@ -345,9 +351,10 @@ DevTables *regex_device(rure *re, std::string *err);
 bool big_device(const DevTables &tc);
 bool lazy_device(const DevTables &tc);
 DevTables *set_device(rure_set *rs, std::string *err);
-uint32_t first_byte_rule(const DenseDfa &d, uint32_t ustart1, bool nonempty, uint8_t bytes[4]);
+uint32_t first_byte_rule(const DenseDfa &d, uint32_t ustart1, bool nonempty, uint8_t bytes[4], bool *holds);
+bool run_class(const DenseDfa &d, uint32_t ustart1, bool nonempty, uint8_t cls[256], bool ascii);
 bool build_lex4(const std::vector<uint8_t> &img, uint32_t s0, std::vector<uint8_t> *out, uint32_t *s0_row);
-bool build_lex(const DenseDfa &d, uint32_t ustart1, uint32_t fb_n, std::vector<uint8_t> *img,
+bool build_lex(const DenseDfa &d, uint32_t ustart1, bool fb_holds, std::vector<uint8_t> *img,
                       uint32_t *s0_idx);
 bool build_iter_dfa(rure *re);
 bool build_shiftand(const LiteralSet &ls, std::vector<uint64_t> *mask, uint64_t *init, uint64_t *fin,
