@@ -5,12 +5,12 @@ CXXFLAGS = -O3 -std=c++17 -fPIC -Wall -Wno-unused-function
 LIB = regex_amd/lib/librure_amd.so
 HOST_SRC = regex_amd/csrc/host/syntax.cpp regex_amd/csrc/host/compile.cpp regex_amd/csrc/host/dfa_build.cpp \
            regex_amd/csrc/host/nfa_build.cpp regex_amd/csrc/host/literals.cpp \
-           regex_amd/csrc/host/literal_sets.cpp
+           regex_amd/csrc/host/literal_sets.cpp regex_amd/csrc/host/knobs.cpp
 RT_SRC = regex_amd/csrc/build.cpp regex_amd/csrc/dispatch.cpp regex_amd/csrc/scratch.cpp regex_amd/csrc/capi.cpp
 RT_OBJ = $(patsubst regex_amd/csrc/%.cpp,$(OBJDIR)/rt_%.o,$(RT_SRC))
 KERNEL_SRC = regex_amd/csrc/kernels/dfa_scan.hip regex_amd/csrc/kernels/nfa_scan.hip regex_amd/csrc/kernels/iter_scan.hip \
              regex_amd/csrc/kernels/replace_scan.hip regex_amd/csrc/kernels/gather_scan.hip \
-             regex_amd/csrc/kernels/match_types.hip regex_amd/csrc/kernels/big_dfa.hip regex_amd/csrc/kernels/set_multi.hip \
+             regex_amd/csrc/kernels/match_types.hip regex_amd/csrc/kernels/big_dfa.hip \
              regex_amd/csrc/kernels/run_iter.hip
 KERNEL_OBJ = $(patsubst regex_amd/csrc/kernels/%.hip,$(OBJDIR)/%.o,$(KERNEL_SRC))
 HDRS = $(wildcard regex_amd/csrc/host/*.hpp regex_amd/csrc/host/*.h regex_amd/csrc/kernels/*.hpp include/*.h)

@@ -575,8 +575,8 @@ def run_c3(ctx):
     # separate), and the match records written (16 B each)
     var_matches = sum(got) // W
     # the fused pass runs the k-mer probe engine when every variant is a set
-    # of 8-byte strings (all 9 are) unless RURE_AMD_KMER=0
-    kmer = os.environ.get("RURE_AMD_KMER", "1") != "0"
+    # of 8-byte strings (all 9 are) unless the debug knob kmer=0 is set
+    kmer = "kmer=0" not in os.environ.get("RURE_AMD_DEBUG", "")
     var_kernel = ("iter_spec_kmer_multi_tile" if kmer else "iter_spec_sa_multi_tile") if fused else "iter_spec_sa_tile"
     step_bytes = strip_bytes + var_bytes * (1 if fused else len(variants)) + 16 * (nsp_sharded // W + var_matches)
     config = {"workload": "C3: regex-dna x%d (%d B raw, %d B stripped): strip find_iter + 9 variant find_iter"
@@ -1027,15 +1027,14 @@ def run_big(ctx):
     sec = ctx.timed(scan)
     kms = ctx.kernel_ms(scan)
     res = out.cpu().numpy()
-    # Pike VM on the same batch (RURE_AMD_BIG=0 is read per call), untimed
-    os.environ["RURE_AMD_BIG"] = "0"
+    # Pike VM on the same batch (debug knob big=0, read per call), untimed
     pk = out.clone()
-    torch.cuda.synchronize()
-    tp = time.perf_counter()
-    re.find_batch(hay, stride=L, length=L, count=n, out=pk, stream=ctx.stream)
-    torch.cuda.synchronize()
-    pike_s = time.perf_counter() - tp
-    del os.environ["RURE_AMD_BIG"]
+    with R.debug(big=0):
+        torch.cuda.synchronize()
+        tp = time.perf_counter()
+        re.find_batch(hay, stride=L, length=L, count=n, out=pk, stream=ctx.stream)
+        torch.cuda.synchronize()
+        pike_s = time.perf_counter() - tp
     same = bool(torch.equal(pk, out))
     # oracle parity on a sample of haystacks
     o = OracleRegex(re)

@@ -235,12 +235,6 @@ size_t rure_amd_captures_len(rure *re);
  * Also done when the last rure / rure_set is freed.  Safe at any time: each
  * block is freed after the kernels that last used it. */
 void rure_amd_release_scratch(void);
-/* Sets searched as several automata in one pass (set_multi.hip: the
- * 64-pattern groups of a larger set): after the first batched call, the
- * number of groups run together (0: one pass per group), the LDS image size
- * and the smallest share of a profiled sample's visits that stayed in a
- * group's LDS-resident cores (the rule that picks one pass, >= 0.995). */
-int rure_amd_set_multi_info(rure_set *rs, uint32_t *groups, uint32_t *lds_bytes, double *coverage);
 // Scratch bookkeeping: bytes cached for reuse, bytes held by calls in
 // flight, and the number of rure / rure_set handles alive.
 void rure_amd_scratch_stats(size_t *cached, size_t *live, long *handles);
@@ -407,8 +401,8 @@ int rure_amd_set_uses_dfa(rure_set *re);
  * -2 = the reverse DFA from the end (DfaAnchoredReverse), -3 = the literal
  * engine (MatchType::Literal), -4 = the chunked cut-bounded scan (long
  * haystacks, small batches split into units), -5 = the lane search of the
- * Literal / DfaSuffix match types, -6 = the big (u32) DFA, -7 = the
- * one-pass multi-group set kernel, -8 = the ragged line kernel, -9 = the
+ * Literal / DfaSuffix match types, -6 = the big (u32) DFA, (-7: unused
+ * since round 5), -8 = the ragged line kernel, -9 = the
  * chunked DfaSuffix scan, -10 = the on-demand DFA, -11 = the DfaSuffix
  * find_iter, -12 / -13 = the chunked find_iter of a look-around regex (no
  * quit / a quit sent it to the wave path), -14 / -15 = the ASCII-shadow
@@ -417,6 +411,14 @@ int rure_amd_set_uses_dfa(rure_set *re);
  * engine of a C+ regex (its class over all bytes / the ASCII shadow's);
  * -1 before the first launch. */
 int rure_amd_last_fwd_path(void);
+/* Debug-only overrides of the engine dispatch and launch geometry
+ * (regex_amd/csrc/host/knobs.hpp lists them): replaces the whole override
+ * table, read once per process from RURE_AMD_DEBUG, by spec
+ * ("name=value,..."; NULL or "" clears it).  For tests and A/B tools; no
+ * production path needs an override.  Returns RURE_AMD_ERR_ARG (table
+ * unchanged) on an unknown name or a malformed value.  Tables a regex has
+ * already built for a device keep the overrides they were built under. */
+int rure_amd_debug_set(const char *spec);
 /* Diagnostics (bench): rure_amd_kernel_timer(1) resets and starts timing the
  * speculative kernel of every find_iter pass (the dominant kernel of a pass:
  * iter_spec_*; HIP events on the launch stream), (0) stops;

@@ -75,6 +75,39 @@ def release_scratch():
     N.rure_amd_release_scratch()
 
 
+_debug_spec = [None]
+
+
+class debug:
+    """Debug-only engine overrides for a block (rure_amd_debug_set; the knob
+    names are in regex_amd/csrc/host/knobs.hpp), restoring the previous
+    overrides after it:
+
+        with regex_amd.debug(lex4=0):      # the byte-per-step lexer
+            ...
+
+    For tests and A/B tools; the production dispatch never needs one.
+    Tables a regex already built keep the overrides they were built under."""
+
+    def __init__(self, **knobs):
+        self.spec = ",".join("%s=%d" % (k, int(v)) for k, v in knobs.items())
+
+    def __enter__(self):
+        self.prev = _debug_spec[0]
+        _debug_set(self.spec)
+        return self
+
+    def __exit__(self, *exc):
+        _debug_set(self.prev)
+        return False
+
+
+def _debug_set(spec):
+    if N.rure_amd_debug_set(spec.encode() if spec else None) != N.OK:
+        raise ValueError("unknown debug knob or bad value in %r" % spec)
+    _debug_spec[0] = spec
+
+
 def scratch_stats():
     """{"cached", "live", "handles"}: scratch bytes cached for reuse, bytes
     held by calls in flight, rure / rure_set handles alive."""
@@ -892,13 +925,6 @@ class RegexSet(object):
 
     def nfa_tables(self):
         return _nfa_export(N.rure_amd_set_nfa_export, self._set)
-
-    def multi_info(self):
-        """After a batched call: {"groups", "lds_bytes", "coverage"} of the
-        one-pass multi-group kernel (groups 0: one pass per group)."""
-        g, l, c = ctypes.c_uint32(0), ctypes.c_uint32(0), ctypes.c_double(0)
-        N.rure_amd_set_multi_info(self._set, ctypes.byref(g), ctypes.byref(l), ctypes.byref(c))
-        return {"groups": g.value, "lds_bytes": l.value, "coverage": c.value}
 
     def dfa_info(self):
         info = N.DfaInfo()

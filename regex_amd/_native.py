@@ -152,6 +152,7 @@ rure_amd_shiftand_export = _sig("rure_amd_shiftand_export", ctypes.c_int64, VP, 
 rure_amd_uses_dfa = _sig("rure_amd_uses_dfa", ctypes.c_int, VP)
 rure_amd_set_uses_dfa = _sig("rure_amd_set_uses_dfa", ctypes.c_int, VP)
 rure_amd_last_fwd_path = _sig("rure_amd_last_fwd_path", ctypes.c_int)
+rure_amd_debug_set = _sig("rure_amd_debug_set", ctypes.c_int, ctypes.c_char_p)
 rure_amd_first_byte_export = _sig("rure_amd_first_byte_export", ctypes.c_int, VP, VP)
 rure_amd_lex_export = _sig("rure_amd_lex_export", ctypes.c_int64, VP, VP, c_size, VP)
 rure_amd_lex4_export = _sig("rure_amd_lex4_export", ctypes.c_int64, VP, VP, c_size, VP)
@@ -174,8 +175,6 @@ rure_amd_literals_op = _sig("rure_amd_literals_op", ctypes.c_int64, ctypes.c_int
 rure_amd_exec_literals_export = _sig("rure_amd_exec_literals_export", ctypes.c_int64, VP, ctypes.c_int, VP, c_size)
 rure_amd_match_info_get = _sig("rure_amd_match_info_get", ctypes.c_int, VP, VP)
 rure_amd_release_scratch = _sig("rure_amd_release_scratch", None)
-rure_amd_set_multi_info = _sig("rure_amd_set_multi_info", ctypes.c_int, VP, ctypes.POINTER(ctypes.c_uint32),
-                               ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_double))
 rure_amd_scratch_stats = _sig("rure_amd_scratch_stats", None, ctypes.POINTER(c_size), ctypes.POINTER(c_size),
                               ctypes.POINTER(ctypes.c_long))
 rure_amd_kernel_timer = _sig("rure_amd_kernel_timer", ctypes.c_int, ctypes.c_int)

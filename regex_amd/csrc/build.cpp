@@ -147,7 +147,7 @@ bool pack_forward(const DenseDfa &d, PackedFwd *p, std::string *err, bool all) {
 // LDS budget of the core table (RURE_AMD_CORE_LDS overrides, tuning).
 size_t core_lds_budget() {
   size_t b = 150 * 1024;
-  if (const char *v = getenv("RURE_AMD_CORE_LDS")) b = std::max<size_t>(4096, std::min<size_t>(150 * 1024, atol(v)));
+  if (knob(Knob::CoreLds) > 0) b = std::max<size_t>(4096, std::min<size_t>(150 * 1024, knob(Knob::CoreLds)));
   return b;
 }
 
@@ -327,7 +327,7 @@ void build_big_dfas(rure *re) {
   DfaBuildLimits lim;
   lim.max_raw_states = kBigDfaRawStates;
   lim.max_bytes = kBigDfaBytes;
-  if (const char *v = getenv("RURE_AMD_BIG_BYTES")) lim.max_bytes = (size_t)std::max(1ll, atoll(v));
+  if (knob(Knob::BigBytes) > 0) lim.max_bytes = (size_t)knob(Knob::BigBytes);
   lim.columns = true;
   lim.minimise = false;   // construction already shares step targets; refinement doubled the build time
   std::string e1, e2;
@@ -481,11 +481,10 @@ bool needs_mt_lane(const ExecLiterals &x) {
 // DFA whose start does not depend on look-behind, from the regex's prefix
 // literals (dfa.prefixes, exec.rs:308-311; not for anchored starts,
 // dfa.rs:1516-1522 has_prefix) when they have at most 4 first bytes.
-// RURE_AMD_PREFIX=0 turns it off (A/B).
+// Knob prefix=0 turns it off (A/B).
 void set_prefix_skip(const rure *re, FwdDfaDev *f) {
   f->pfx_n = 0;
-  const char *env = getenv("RURE_AMD_PREFIX");
-  if ((env && env[0] == '0') || !f->ustart1 || re->nfa.anchored_start) return;
+  if (knob(Knob::Prefix) == 0 || !f->ustart1 || re->nfa.anchored_start) return;
   const LitSearcher &p = re->xl.prefixes;
   if (p.matcher == 0 || p.lits.lits.empty()) return;
   bool seen[256] = {false};
@@ -499,42 +498,10 @@ void set_prefix_skip(const rure *re, FwdDfaDev *f) {
     f->pfx_rep[n++] = b * 0x01010101u;
   }
   f->pfx_n = n;
-  // byte sets of the prefixes' first three positions (case pairs folded)
-  // for the deeper filter, opt-in (RURE_AMD_PREFIX=3): on English text it
-  // lost to the first-byte filter (Sherlock\s+\w+ 1.47 -> 1.62 ms per GiB,
-  // (?i)watson\w* 1.46 -> 1.89) and won only where the prefix is absent
-  // ((?i)zqxj\w* 1.12 -> 0.65); profiles/r04_prefix_depth_ab.jsonl
-  f->pfx_depth = 0;
-  if (!(env && env[0] == '3')) return;
-  uint32_t depth = 0;
-  for (uint32_t j = 0; j < 3; ++j) {
-    bool in[256] = {false};
-    for (const Lit &l : p.lits.lits) {
-      if (l.v.size() <= j) goto done;
-      in[(uint8_t)l.v[j]] = true;
-    }
-    {
-      uint32_t c = 0;
-      for (int x = 0; x < 256; ++x) {
-        if (!in[x]) continue;
-        const bool letter = (x | 0x20) >= 'a' && (x | 0x20) <= 'z';
-        if (letter && (x & 0x20) == 0 && in[x | 0x20]) continue;  // folded with its lower case
-        if (c == 1) goto done;  // one entry per set (FwdDfaDev::pfx_depth)
-        const bool fold = letter && in[x ^ 0x20];
-        f->pfx_set[j][c] = (uint32_t)(fold ? (x | 0x20) : x) * 0x01010101u;
-        f->pfx_or[j][c] = fold ? 0x20202020u : 0;
-        ++c;
-      }
-      f->pfx_cnt[j] = c;
-      for (uint32_t i = c; i < 4; ++i) {  // unused entries repeat entry 0
-        f->pfx_set[j][i] = f->pfx_set[j][0];
-        f->pfx_or[j][i] = f->pfx_or[j][0];
-      }
-      depth = j + 1;
-    }
-  }
-done:
-  f->pfx_depth = depth >= 2 ? depth : 0;
+  // (a filter over the prefixes' first two or three positions lost to this
+  // one on English text in round 4 — Sherlock\s+\w+ 1.47 -> 1.62 ms per GiB,
+  // (?i)watson\w* 1.46 -> 1.89, profiles/r04_prefix_depth_ab.jsonl — and
+  // was deleted in round 5)
 }
 
 // Upload (once per device) and return device descriptors.
@@ -739,7 +706,7 @@ bool lazy_device(const DevTables &tc) {
   }
   if (!re->lazy) {
     size_t budget = kBigDfaBytes;
-    if (const char *v = getenv("RURE_AMD_BIG_BYTES")) budget = (size_t)std::max(1ll, atoll(v));
+    if (knob(Knob::BigBytes) > 0) budget = (size_t)knob(Knob::BigBytes);
     re->lazy.reset(new LazyDfa(re->fwd, budget));
   }
   t.has_lazy = true;
@@ -1087,7 +1054,7 @@ bool build_iter_dfa(rure *re) {
     // the same automaton with every byte >= 0x80 quitting and the states only
     // those bytes reach dropped
     if (re->iter_ok && !re->pf_iter.all && !re->fwd.has_unicode_word_boundary && !re->lit_ok &&
-        !(getenv("RURE_AMD_ASCII_SHADOW") && getenv("RURE_AMD_ASCII_SHADOW")[0] == '0')) {
+        knob(Knob::AsciiShadow) != 0) {
       DfaBuildLimits la;
       la.strip = true;
       la.ascii_only = true;
@@ -1209,7 +1176,7 @@ const FwdDfaDev *iter_ascii_device(rure *re, const DevTables &t, std::string *er
     f.lex_bytes = (uint32_t)re->lex_a.size();
     f.lex_s0 = re->lex_a_s0;
   }
-  if (!re->lex4_a.empty() && !(getenv("RURE_AMD_LEX4") && getenv("RURE_AMD_LEX4")[0] == '0')) {
+  if (!re->lex4_a.empty() && knob(Knob::Lex4) != 0) {
     f.lex4_image = base + o_lex4;
     f.lex4_s0 = re->lex4_a_s0;
   }
@@ -1304,8 +1271,8 @@ const FwdDfaDev *iter_device(rure *re, const DevTables &t, std::string *err) {
   f.ustart1 = pf.ustart1;
   f.nonempty = can_match_empty(re->nfa) ? 0 : 1;
   set_prefix_skip(re, &f);
-  // RURE_AMD_FB=0 turns the first-byte start rule off (reverse scans)
-  f.fb_n = getenv("RURE_AMD_FB") && getenv("RURE_AMD_FB")[0] == '0' ? 0 : re->fb_n;
+  // knob fb=0 turns the first-byte start rule off (reverse scans)
+  f.fb_n = knob(Knob::Fb) == 0 ? 0 : re->fb_n;
   for (uint32_t i = 0; i < 4; ++i) f.fb_rep[i] = (i < re->fb_n ? re->fb_bytes[i] : re->fb_bytes[0]) * 0x01010101u;
   if (!lit_img.empty()) {
     f.lit_image = base + o_lit;
@@ -1321,8 +1288,8 @@ const FwdDfaDev *iter_device(rure *re, const DevTables &t, std::string *err) {
     f.lex_bytes = (uint32_t)re->lex.size();
     f.lex_s0 = re->lex_s0;
   }
-  // RURE_AMD_LEX4=0 keeps the byte-per-step lexer (A/B)
-  if (!re->lex4.empty() && !(getenv("RURE_AMD_LEX4") && getenv("RURE_AMD_LEX4")[0] == '0')) {
+  // knob lex4=0 keeps the byte-per-step lexer (A/B)
+  if (!re->lex4.empty() && knob(Knob::Lex4) != 0) {
     f.lex4_image = base + o_lex4;
     f.lex4_s0 = re->lex4_s0;
   }

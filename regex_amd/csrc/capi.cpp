@@ -372,7 +372,6 @@ rure_set *rure_compile_set(const uint8_t **patterns, const size_t *lens, size_t 
 
 void rure_set_free(rure_set *rs) {
   if (!rs) return;
-  free_multi(rs);
   if (rs->single) rure_free(rs->single);
   for (rure_set *g : rs->groups) rure_set_free(g);
   for (auto &kv : rs->dev) {
@@ -502,14 +501,6 @@ int rure_amd_set_matches_batch_words(rure_set *rs, const rure_amd_batch *batch, 
   if (words < std::max<size_t>(1, (n + 63) / 64)) return RURE_AMD_ERR_ARG;
   if (b.count == 0) return RURE_AMD_OK;
   hipStream_t st = (hipStream_t)stream;
-  if (words <= (size_t)kMultiMaxGroups && (!rs->groups.empty() || set_chains() > 1)) {
-    std::string err;
-    if (const MultiCoreDev *md = multi_device(rs, &err, b, st)) {
-      MultiCoreDev f = *md;
-      f.words = (uint32_t)words;
-      return run_set_multi(rs, b, f, mask, st);
-    }
-  }
   if (words == 1 && n >= 2) return set_batch_word(rs, b, mask, st);
   if (hipMemsetAsync(mask, 0, b.count * words * 8, st) != hipSuccess) return RURE_AMD_ERR_HIP;
   if (n == 0) return RURE_AMD_OK;  // MatchType::Nothing (exec.rs:276-286)
@@ -518,17 +509,6 @@ int rure_amd_set_matches_batch_words(rure_set *rs, const rure_amd_batch *batch, 
     int rc = set_batch_group(rs->groups[g], batch, b, mask, words, g, st);
     if (rc != RURE_AMD_OK) return rc;
   }
-  return RURE_AMD_OK;
-}
-
-int rure_amd_set_multi_info(rure_set *rs, uint32_t *groups, uint32_t *lds_bytes, double *coverage) {
-  if (!rs) return RURE_AMD_ERR_ARG;
-  std::lock_guard<std::mutex> g(rs->mu);
-  const MultiSet *m = rs->multi;
-  const bool ok = m && m->built && m->ok;
-  if (groups) *groups = ok ? m->proto.G : 0;
-  if (lds_bytes) *lds_bytes = ok ? m->proto.lds_bytes : 0;
-  if (coverage) *coverage = m && m->built ? m->coverage : 0.0;
   return RURE_AMD_OK;
 }
 
@@ -654,7 +634,7 @@ int rure_amd_find_iter_span_multi(rure *const *res, size_t n, const uint8_t *hay
     // the unit size of run_find_iter (one haystack: the span over the lanes in flight)
     const uint64_t span = std::min<uint64_t>(length, hcut) - lo;
     uint64_t per_cu = 1024;
-    if (const char *v = getenv("RURE_AMD_ITER_LANES")) per_cu = std::max(64, atoi(v));
+    if (knob(Knob::IterLanes) > 0) per_cu = std::max<uint64_t>(64, knob(Knob::IterLanes));
     const uint64_t chunk = odd_lines(std::max<uint64_t>(4096, (span + (uint64_t)cus * per_cu - 1) / ((uint64_t)cus * per_cu)));
     KmerDev kmv;
     const KmerDev *km = kmer_device(res, n, &kmv) ? &kmv : nullptr;
@@ -936,6 +916,7 @@ int rure_amd_uses_dfa(rure *re) {
 }
 
 int rure_amd_last_fwd_path(void) { return rure_amd::last_fwd_path(); }
+int rure_amd_debug_set(const char *spec) { return rure_amd::knob_set(spec) ? RURE_AMD_OK : RURE_AMD_ERR_ARG; }
 
 
 

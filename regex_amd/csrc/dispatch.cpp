@@ -74,8 +74,7 @@ bool long_batch(int mode, const BatchDev &b, const DevTables &t, uint64_t *chunk
     // shortest_match unit scans on until the DFA dies, so a pattern that never
     // dies ([^\n]* over text without newlines) would cost every unit the rest
     // of its haystack (about units / 2 times the unsplit work).
-    const char *sv = getenv("RURE_AMD_SPLIT");
-    if ((sv && sv[0] == '0') || mode != MODE_ISMATCH || t.anchored_rev || span < 512 || b.count < 64 ||
+    if (knob(Knob::Split) == 0 || mode != MODE_ISMATCH || t.anchored_rev || span < 512 || b.count < 64 ||
         b.count > (uint64_t)t.cus * 16)
       return false;
     const uint64_t per_h = ((uint64_t)t.cus * 64 + b.count - 1) / b.count;
@@ -87,7 +86,7 @@ bool long_batch(int mode, const BatchDev &b, const DevTables &t, uint64_t *chunk
   // 16 waves per CU: per-lane streams need latency hiding (RURE_AMD_LONG_LANES
   // per CU overrides, tuning)
   uint64_t per_cu = 1024;
-  if (const char *v = getenv("RURE_AMD_LONG_LANES")) per_cu = std::max(64, atoi(v));
+  if (knob(Knob::LongLanes) > 0) per_cu = std::max<uint64_t>(64, knob(Knob::LongLanes));
   const uint64_t target = (uint64_t)t.cus * per_cu;
   const uint64_t per_h = (target + b.count - 1) / b.count;
   uint64_t c = std::max<uint64_t>(16u << 10, (span + per_h - 1) / per_h);
@@ -121,13 +120,12 @@ bool lane_search_ok(const DevTables &t) { return t.mt_lane && (t.m.mt != MT_DFA_
 bool suffix_long_ok(const BatchDev &b, const DevTables &t, uint64_t *chunk) {
   if (t.m.mt != MT_DFA_SUFFIX || !t.lcs_free || !t.has_dfa || t.quit_possible || b.offs || b.count == 0 || !t.owner)
     return false;
-  const char *v = getenv("RURE_AMD_SUFFIX_LONG");
-  if (v && v[0] == '0') return false;
+  if (knob(Knob::SuffixLong) == 0) return false;
   const uint64_t span = b.length > b.start ? b.length - b.start : 0;
-  if (b.count >= (uint64_t)t.cus * 16 || (span < (256u << 10) && !(v && v[0] == '2'))) return false;
+  if (b.count >= (uint64_t)t.cus * 16 || (span < (256u << 10) && knob(Knob::SuffixLong) != 2)) return false;
   const uint64_t target = (uint64_t)t.cus * 1024;
   const uint64_t per_h = (target + b.count - 1) / b.count;
-  *chunk = odd_lines(std::max<uint64_t>(v && v[0] == '2' ? 128 : 16u << 10, (span + per_h - 1) / per_h));
+  *chunk = odd_lines(std::max<uint64_t>(knob(Knob::SuffixLong) == 2 ? 128 : 16u << 10, (span + per_h - 1) / per_h));
   return true;
 }
 
@@ -183,9 +181,8 @@ hipError_t run_lane_search(int mode, const BatchDev &b, const DevTables &t, void
 // haystack over a wave).  RURE_AMD_BIG=2 forces it (tests), =0 keeps the
 // Pike VM (A/B; read per call).
 bool big_batch(const BatchDev &b, const DevTables &t) {
-  const char *env = getenv("RURE_AMD_BIG");
-  if (env && env[0] == '2') return true;
-  if (env && env[0] == '0') return false;
+  if (knob(Knob::Big) == 2) return true;
+  if (knob(Knob::Big) == 0) return false;
   return b.count >= (uint64_t)t.cus * 64;
 }
 
@@ -202,8 +199,8 @@ hipError_t run_lazy(int mode, const BatchDev &b, const DevTables &tc, void *out,
   rure *re = t.owner;
   std::lock_guard<std::mutex> g(re->mu);
   LazyDfa &L = *re->lazy;
-  size_t ahead = 4096;  // rows built ahead per round (RURE_AMD_LAZY_ROWS: tests)
-  if (const char *v = getenv("RURE_AMD_LAZY_ROWS")) ahead = (size_t)std::max(1ll, atoll(v));
+  size_t ahead = 4096;  // rows built ahead per round (knob lazy_rows: tests)
+  if (knob(Knob::LazyRows) > 0) ahead = (size_t)knob(Knob::LazyRows);
   bool ok = L.nbuilt() > 0 || L.expand(ahead);
   hipError_t e = hipSuccess;
   LazyPark *pk[2] = {nullptr, nullptr};
@@ -272,9 +269,8 @@ hipError_t run_lazy(int mode, const BatchDev &b, const DevTables &tc, void *out,
 // The on-demand DFA where the eager automata did not materialise (or
 // RURE_AMD_LAZY=1: tests, any regex), for batches that fill the device.
 static bool lazy_batch(const BatchDev &b, const DevTables &t) {
-  const char *env = getenv("RURE_AMD_LAZY");
-  if (env && env[0] == '0') return false;
-  const bool force = env && env[0] == '1';
+  if (knob(Knob::Lazy) == 0) return false;
+  const bool force = knob(Knob::Lazy) == 1;
   if (!force && (t.has_dfa || !big_batch(b, t))) return false;
   return lazy_device(t);
 }
@@ -282,7 +278,7 @@ static bool lazy_batch(const BatchDev &b, const DevTables &t) {
 hipError_t run_regex(int mode, const BatchDev &b, const DevTables &t, void *out, hipStream_t st, int dfa_grid,
                      const FwdDfaDev *iter) {
   if (lane_search_ok(t)) return run_lane_search(mode, b, t, out, st);
-  if (getenv("RURE_AMD_LAZY") && getenv("RURE_AMD_LAZY")[0] == '1' && lazy_batch(b, t))
+  if (knob(Knob::Lazy) == 1 && lazy_batch(b, t))
     return run_lazy(mode, b, t, out, st);
   if (!t.has_dfa && big_batch(b, t) && big_device(t)) return launch_big_dfa(mode, b, t.bf, t.br, out, st, t.cus);
   if (!t.has_dfa && lazy_batch(b, t)) return run_lazy(mode, b, t, out, st);
@@ -436,16 +432,16 @@ uint64_t set_single_call(rure_set *rs, const uint8_t *hay, size_t len, size_t st
 static constexpr size_t kLitFindMax = 8;
 const FwdDfaDev *literal_engine(int mode, rure *re, DevTables &t, const BatchDev &b) {
   uint64_t chunk;
-  const char *env = getenv("RURE_AMD_LIT");
-  if (env && env[0] != '1') return nullptr;
+  const long long env = knob(Knob::Lit);
+  if (env >= 0 && env != 1) return nullptr;
   if (t.mt_lane) return nullptr;  // the reference's literal searcher differs from the regex's strings
-  if (!env && long_batch(mode, b, t, &chunk)) return nullptr;  // RURE_AMD_LIT=1 forces the literal engine
+  if (env < 0 && long_batch(mode, b, t, &chunk)) return nullptr;  // lit=1 forces the literal engine
   {
     // the literal set alone (cheap) before any find_iter DFA is built
     std::lock_guard<std::mutex> g(re->mu);
     if (!re->iter_built && !re->lits_done) re->lit_ok = extract_literals(re->nfa, kLitMax, kLitLen, &re->lits);
     re->lits_done = true;
-    if (!re->lit_ok || (!env && re->lits.lits.size() > kLitFindMax)) return nullptr;
+    if (!re->lit_ok || (env < 0 && re->lits.lits.size() > kLitFindMax)) return nullptr;
   }
   std::string err;
   const FwdDfaDev *fi = iter_device(re, t, &err);
@@ -465,25 +461,6 @@ int set_batch_word(rure_set *rs, const BatchDev &b, uint64_t *mask, hipStream_t 
 }
 
 // Group g (patterns [64 g, 64 g + len)) into word g of mask (words per haystack).
-// ------------------------------------------------- sets as one pass (groups)
-// A set of more than 64 patterns is searched as its 64-pattern groups
-// (rure_set::groups), one pass over the batch per group.  With
-// RURE_AMD_SET_MULTI=1, build_multi puts every group's core-form automaton
-// in one LDS image and set_multi.hip steps all of them over each haystack
-// read once; RURE_AMD_SET_CHAINS=G (2..4) splits a set of at most 64
-// patterns into G groups the same way.  Measured (tools/bigset_bench.py,
-// DESIGN.md §4.3): the chains share the VALU and LDS issue slots the single
-// chain already saturates, and the split LDS holds fewer hot cores, so one
-// pass is slower (C4 as 2 chains 1.50 vs 0.64 ms; 100 patterns 4.95 vs
-// 1.39 ms per-group) though it reads the text once; per-group passes stay
-// the default.
-
-
-int set_chains() {
-  const char *v = getenv("RURE_AMD_SET_CHAINS");
-  return v ? std::max(1, std::min(kMultiMaxGroups, atoi(v))) : 1;
-}
-
 int device_cus_cached() {
   int d = 0;
   (void)hipGetDevice(&d);
@@ -495,275 +472,6 @@ int device_cus_cached() {
   return cache[d] = device_cus(d);
 }
 
-void free_multi(rure_set *rs) {
-  MultiSet *m = rs->multi;
-  if (!m) return;
-  int cur = 0;
-  (void)hipGetDevice(&cur);
-  for (auto &kv : m->dev) {
-    (void)hipSetDevice(kv.first);
-    (void)hipFree(kv.second.first);
-  }
-  (void)hipSetDevice(cur);
-  for (rure_set *x : m->owned) rure_set_free(x);
-  delete m;
-  rs->multi = nullptr;
-}
-
-bool multi_fail(int why) {  // diagnostic (RURE_AMD_MULTI_DEBUG): which rule declined one pass
-  if (getenv("RURE_AMD_MULTI_DEBUG")) fprintf(stderr, "set_multi: not built (%d)\n", why);
-  return false;
-}
-
-bool build_multi_locked(rure_set *rs, MultiSet *m, std::string *err, const std::vector<std::string> *sample,
-                        size_t sample_start) {
-  const char *on = getenv("RURE_AMD_SET_MULTI");
-  if (!(on && on[0] == '1')) return multi_fail(1);
-  if (!rs->groups.empty()) {
-    for (size_t g = 0; g < rs->groups.size(); ++g) {
-      m->parts.push_back(rs->groups[g]);
-      m->word.push_back((uint32_t)g);
-      m->shift.push_back(0);
-    }
-  } else {
-    const int G = set_chains();
-    const size_t n = rs->exprs.size();
-    if (G < 2 || n < (size_t)G) return multi_fail(2);
-    const size_t per = (n + G - 1) / G;
-    for (size_t lo = 0; lo < n; lo += per) {
-      const size_t cnt = std::min(per, n - lo);
-      std::vector<const uint8_t *> ps;
-      std::vector<size_t> ls;
-      for (size_t i = lo; i < lo + cnt; ++i) {
-        ps.push_back((const uint8_t *)rs->patterns[i].data());
-        ls.push_back(rs->patterns[i].size());
-      }
-      rure_error e;
-      rure_set *x = rure_compile_set(ps.data(), ls.data(), cnt, rs->flags, &rs->opts, &e);
-      if (!x) { if (err) *err = e.msg; return multi_fail(3); }
-      m->owned.push_back(x);
-      m->parts.push_back(x);
-      m->word.push_back(0);
-      m->shift.push_back((uint32_t)lo);
-    }
-  }
-  const int G = (int)m->parts.size();
-  if (G < 2 || G > kMultiMaxGroups) return multi_fail(4);
-  for (rure_set *x : m->parts)
-    if (x->single || !build_set_dfa(x)) return multi_fail(5);
-  // quit states (Unicode \b): the Pike VM redoes the words a lane quit in,
-  // with each group's NFA (one word each) or the whole set's (split sets)
-  if (rs->groups.empty() && !rs->nfa_ok) return multi_fail(6);  // (built by multi_device before the lock)
-  // which cores the batch visits (the hot LDS rows) and which masks it
-  // reports (the 62 LDS codes): each group's DFA run on the host over a
-  // sample of the first batch (one copy + sync, once per set, like
-  // adapt_cores)
-  std::vector<std::vector<uint64_t>> sw(G);
-  std::vector<std::unordered_map<uint64_t, uint64_t>> mw(G);
-  if (sample && !sample->empty()) {
-    for (int g = 0; g < G; ++g) {
-      const DenseDfa &d = m->parts[g]->dfa;
-      sw[g].assign(d.nstates, 0);
-      for (const std::string &line : *sample) {
-        const uint8_t *tx = (const uint8_t *)line.data();
-        const size_t len = line.size();
-        if (sample_start > len) continue;
-        uint32_t c = d.start[start_flag_index_fwd(tx, len, sample_start)];
-        for (size_t i = sample_start; i < len && (int)c != d.dead && (int)c != d.quit; ++i) {
-          c = d.trans[(size_t)c * 256 + tx[i]];
-          ++sw[g][c];
-          if (d.now_mask[c]) ++mw[g][d.now_mask[c]];
-        }
-      }
-    }
-  }
-  // one LDS image for all groups: each group's share of 159 KiB, shrunk
-  // until the image fits (class map 512 B, rows, code masks 512 B, start
-  // cores 256 B, hot EOF masks 8 B per hot core)
-  const size_t L = 159 * 1024;
-  size_t bud = L / G;
-  m->cores.assign(G, CoreSet());
-  auto al16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
-  for (int tries = 0;; ++tries) {
-    size_t total = 0;
-    for (int g = 0; g < G; ++g) {
-      m->cores[g] = CoreSet();
-      const bool prof = sample && !sample->empty();
-      if (!build_set_cores(m->parts[g]->dfa, bud, &m->cores[g], nullptr, prof ? &mw[g] : nullptr,
-                           prof ? &sw[g] : nullptr))
-        return multi_fail(7);
-      const CoreSet &cs = m->cores[g];
-      total += 512 + al16((size_t)(cs.hot + 1) * (cs.K + 1) * 2) + 512 + 256 + al16(8 * (size_t)cs.hot);
-    }
-    if (total <= L) break;
-    if (tries > 16 || bud < 16 * 1024) return multi_fail(8);
-    bud -= 4 * 1024;
-  }
-  // The share of the sample's visits that stays in every group's LDS cores
-  // (the LDS is split between the groups), for rure_amd_set_multi_info.
-  m->coverage = 1.0;
-  if (sample && !sample->empty()) {
-    for (int g = 0; g < G; ++g) {
-      uint64_t tot = 0;
-      for (uint64_t v : sw[g]) tot += v;
-      const double cov = tot ? (double)m->cores[g].hot_visits / (double)tot : 1.0;
-      m->coverage = std::min(m->coverage, cov);
-    }
-  }
-  MultiCoreDev &P = m->proto;
-  P = MultiCoreDev{};
-  P.G = (uint32_t)G;
-  P.split = rs->groups.empty() ? 1u : 0u;
-  size_t cur = 0;
-  for (int g = 0; g < G; ++g) {
-    const CoreSet &cs = m->cores[g];
-    MultiGroupDev &d = P.g[g];
-    const size_t rows = (size_t)(cs.hot + 1) * (cs.K + 1) * 2;
-    d.K = cs.K;
-    d.hot = cs.hot;
-    d.dead = cs.dead;
-    d.quit = cs.quit;
-    if (cs.quit != 0xFFFFFFFFu) m->quit = true;
-    d.cls_off = (uint32_t)cur;
-    d.rows_off = (uint32_t)(cur + 512);
-    d.mt_off = (uint32_t)(d.rows_off + al16(rows));
-    d.st_off = d.mt_off + 512;
-    d.he_off = d.st_off + 256;
-    d.word = m->word[g];
-    d.shift = m->shift[g];
-    const size_t np = m->parts[g]->exprs.size();
-    d.all = np >= 64 ? ~0ull : ((1ull << np) - 1);
-    cur = d.he_off + al16(8 * (size_t)cs.hot);
-    m->lds.resize(cur, 0);
-    uint16_t *cm = (uint16_t *)(m->lds.data() + d.cls_off);
-    for (int b = 0; b < 256; ++b) cm[b] = (uint16_t)(2 * cs.lds[b]);
-    memcpy(m->lds.data() + d.rows_off, cs.lds.data() + 256, rows);
-    memcpy(m->lds.data() + d.mt_off, cs.codemask, 512);
-    memcpy(m->lds.data() + d.st_off, cs.start, 256);
-    memcpy(m->lds.data() + d.he_off, cs.eof.data(), 8 * (size_t)cs.hot);
-  }
-  m->lds.resize(al16(m->lds.size()), 0);
-  P.lds_bytes = (uint32_t)m->lds.size();
-  uint32_t words = 0;
-  for (int g = 0; g < G; ++g) words = std::max(words, P.g[g].word + 1);
-  P.words = words;
-  return true;
-}
-
-// Host copy of the first haystacks of the batch (the profile sample): at most
-// 4096 of them, each cut to its first 4 KiB, at most 4 MiB in all (so a few
-// huge haystacks cost a bounded copy).
-std::vector<std::string> batch_sample(const BatchDev &b, hipStream_t st) {
-  std::vector<std::string> out;
-  const uint64_t n = std::min<uint64_t>(b.count, 4096);
-  if (!n) return out;
-  constexpr uint64_t kPerHay = 4096, kTotal = 4u << 20;
-  std::vector<uint64_t> offs(n + 1);
-  if (b.offs) {
-    if (hipMemcpyAsync(offs.data(), b.offs, (n + 1) * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess)
-      return out;
-  } else {
-    for (uint64_t i = 0; i <= n; ++i) offs[i] = i * b.stride;
-  }
-  std::vector<uint8_t> buf;
-  uint64_t total = 0;
-  for (uint64_t i = 0; i < n && total < kTotal; ++i) {
-    const uint64_t len = b.offs ? offs[i + 1] - offs[i] : b.length;
-    const uint64_t take = std::min<uint64_t>({len, kPerHay, kTotal - total});
-    buf.resize(take);
-    if (take && (hipMemcpyAsync(buf.data(), b.hay + offs[i], take, hipMemcpyDeviceToHost, st) != hipSuccess ||
-                 hipStreamSynchronize(st) != hipSuccess))
-      return out;
-    out.emplace_back((const char *)buf.data(), take);
-    total += take;
-  }
-  return out;
-}
-
-const MultiCoreDev *multi_device(rure_set *rs, std::string *err, const BatchDev &b, hipStream_t st) {
-  if (rs->groups.empty()) build_set(rs);  // split sets: the whole set's NFA (quit fallback); takes rs->mu
-  std::lock_guard<std::mutex> g(rs->mu);
-  if (!rs->multi) rs->multi = new MultiSet();
-  MultiSet *m = rs->multi;
-  if (!m->built) {
-    m->built = true;
-    // opt-in (RURE_AMD_SET_MULTI=1): the default path never samples
-    const char *on = getenv("RURE_AMD_SET_MULTI");
-    if (!(on && on[0] == '1')) {
-      m->ok = false;
-      return nullptr;
-    }
-    const std::vector<std::string> sample = batch_sample(b, st);
-    m->ok = build_multi_locked(rs, m, err, &sample, b.start);
-  }
-  if (!m->ok) return nullptr;
-  int d = 0;
-  if (!hip_ok(hipGetDevice(&d), err)) return nullptr;
-  auto it = m->dev.find(d);
-  if (it != m->dev.end()) return &it->second.second;
-  Blob bl;
-  const int G = (int)m->parts.size();
-  size_t o_core[kMultiMaxGroups], o_out[kMultiMaxGroups], o_eof[kMultiMaxGroups];
-  for (int k = 0; k < G; ++k) {
-    const CoreSet &cs = m->cores[k];
-    o_core[k] = bl.add(cs.gcore.data(), cs.gcore.size() * 2);
-    o_out[k] = bl.add(cs.gout.data(), cs.gout.size() * 8);
-    o_eof[k] = bl.add(cs.eof.data(), cs.eof.size() * 8);
-  }
-  const size_t o_lds = bl.add(m->lds.data(), m->lds.size());
-  DevTables tmp;
-  if (!upload_blob(bl, &tmp, err)) return nullptr;
-  uint8_t *base = (uint8_t *)tmp.blob;
-  MultiCoreDev f = m->proto;
-  f.lds_image = base + o_lds;
-  for (int k = 0; k < G; ++k) {
-    f.g[k].gcore = (const uint16_t *)(base + o_core[k]);
-    f.g[k].gout = (const uint64_t *)(base + o_out[k]);
-    f.g[k].eof = (const uint64_t *)(base + o_eof[k]);
-  }
-  auto &slot = m->dev[d];
-  slot = std::make_pair(tmp.blob, f);
-  return &slot.second;
-}
-
-// The one-pass kernel, then (only where a lane quit: the Pike kernels read
-// the flag first) the Pike VM over the words marked QUITMARK.
-int run_set_multi(rure_set *rs, const BatchDev &b, const MultiCoreDev &f, uint64_t *mask, hipStream_t st) {
-  MultiSet *m = rs->multi;
-  const int cus = device_cus_cached();
-  if (getenv("RURE_AMD_MULTI_DEBUG")) {  // diagnostic: the combined image's layout
-    fprintf(stderr, "set_multi: G %u words %u split %u lds %u quit %d\n", f.G, f.words, f.split, f.lds_bytes,
-            (int)m->quit);
-    for (uint32_t g = 0; g < f.G; ++g)
-      fprintf(stderr, "  group %u: K %u hot %u dead %u quit %u cls %u rows %u mt %u st %u he %u word %u shift %u\n", g,
-              f.g[g].K, f.g[g].hot, f.g[g].dead, f.g[g].quit, f.g[g].cls_off, f.g[g].rows_off, f.g[g].mt_off,
-              f.g[g].st_off, f.g[g].he_off, f.g[g].word, f.g[g].shift);
-  }
-  if (!m->quit) return launch_set_multi(b, f, mask, st, cus) == hipSuccess ? RURE_AMD_OK : RURE_AMD_ERR_HIP;
-  std::string err;
-  BatchDev bq = b;
-  hipError_t e = scratch_malloc((void **)&bq.quit_flag, 4, st);
-  if (e == hipSuccess) e = hipMemsetAsync(bq.quit_flag, 0, 4, st);
-  if (e == hipSuccess) e = launch_set_multi(bq, f, mask, st, cus);
-  if (e == hipSuccess && f.split) {
-    const DevTables *t = set_device(rs, &err);
-    e = t ? run_pike(MODE_SET, true, bq, *t, mask, st) : hipErrorInvalidValue;
-  } else {
-    for (size_t g = 0; e == hipSuccess && g < m->parts.size(); ++g) {
-      const DevTables *t = set_device(m->parts[g], &err);
-      if (!t) { e = hipErrorInvalidValue; break; }
-      BatchDev bg = bq;
-      bg.out_stride = f.words;
-      e = run_pike(MODE_SET, true, bg, *t, mask + f.g[g].word, st);
-    }
-  }
-  if (bq.quit_flag) {
-    hipError_t e2 = scratch_free(bq.quit_flag, st);
-    if (e == hipSuccess) e = e2;
-  }
-  return e == hipSuccess ? RURE_AMD_OK : RURE_AMD_ERR_HIP;
-}
 
 int set_batch_group(rure_set *g, const rure_amd_batch *batch, const BatchDev &b, uint64_t *mask, size_t words,
                     size_t w, hipStream_t st) {
@@ -807,11 +515,11 @@ hipError_t run_find_iter(rure *re, DevTables *t, const BatchDev &b, const IterOu
   // then runs with its Pike VM fallback)
   if (lane_search_ok(*t) && !sp && t->m.mt == MT_DFA_SUFFIX && t->lcs_free && !b.offs &&
       b.count && b.count < (uint64_t)t->cus * 16 && b.length > b.start) {
-    const char *v = getenv("RURE_AMD_SUFFIX_ITER");
     const uint64_t span = b.length - b.start;
-    if (!(v && v[0] == '0') && (span >= (256u << 10) || (v && v[0] == '2'))) {
+    if (knob(Knob::SuffixIter) != 0 && (span >= (256u << 10) || knob(Knob::SuffixIter) == 2)) {
       const uint64_t per_h = ((uint64_t)t->cus * 1024 + b.count - 1) / b.count;
-      const uint64_t chunk = odd_lines(std::max<uint64_t>(v && v[0] == '2' ? 128 : 16u << 10, (span + per_h - 1) / per_h));
+      const uint64_t chunk =
+          odd_lines(std::max<uint64_t>(knob(Knob::SuffixIter) == 2 ? 128 : 16u << 10, (span + per_h - 1) / per_h));
       const hipError_t e = launch_suffix_iter(b, t->m, t->f, t->r, chunk, o, st, t->cus);
       if (e != hipErrorNotSupported) return e;
     }
@@ -829,8 +537,7 @@ hipError_t run_find_iter(rure *re, DevTables *t, const BatchDev &b, const IterOu
   // path (A/B).
   const FwdDfaDev *fi = nullptr;
   const bool looks = re->nt.looks_used != 0 || t->quit_possible;
-  const char *lv = getenv("RURE_AMD_ITER_LOOKS");
-  if (t->has_dfa && re->nfa_ok && (!looks || (!sp && !(lv && lv[0] == '0')))) fi = iter_device(re, *t, err);
+  if (t->has_dfa && re->nfa_ok && (!looks || (!sp && knob(Knob::IterLooks) != 0))) fi = iter_device(re, *t, err);
   if (fi && looks && re->dfwd_iter.strip.empty()) fi = nullptr;
   if (fi) {
     uint64_t chunk = ~0ull >> 2;
@@ -840,19 +547,18 @@ hipError_t run_find_iter(rure *re, DevTables *t, const BatchDev &b, const IterOu
       // lanes in flight: 16 waves per CU (tools/iter_sweep.py);
       // RURE_AMD_ITER_LANES (per CU) overrides (tuning)
       uint64_t per_cu = 1024;
-      if (const char *v = getenv("RURE_AMD_ITER_LANES")) per_cu = std::max(64, atoi(v));
+      if (knob(Knob::IterLanes) > 0) per_cu = std::max<uint64_t>(64, knob(Knob::IterLanes));
       const uint64_t target = (uint64_t)t->cus * per_cu;
       const uint64_t per_h = (target + b.count - 1) / b.count;
       chunk = odd_lines(std::max<uint64_t>(4096, (span + per_h - 1) / per_h));
-      // RURE_AMD_ITER_CHUNK: the unit size in bytes (tests: many boundaries)
-      if (const char *v = getenv("RURE_AMD_ITER_CHUNK")) chunk = std::max<uint64_t>(16, strtoull(v, nullptr, 10));
+      // knob iter_chunk: the unit size in bytes (tests: many boundaries)
+      if (knob(Knob::IterChunk) > 0) chunk = std::max<uint64_t>(16, knob(Knob::IterChunk));
     }
     // A regex that is one byte class repeated (C+: [a-z]+, (?-u)\w+): its
     // matches are the maximal runs (run_iter.hip), no DFA walk; its ASCII
     // shadow's class (Unicode \w+, \S+, \pL+) answers ASCII text and quits
     // on any other byte.  RURE_AMD_RUNS=0 keeps the DFA paths (A/B).
-    const char *rv = getenv("RURE_AMD_RUNS");
-    const bool runs = !sp && !(rv && rv[0] == '0');
+    const bool runs = !sp && knob(Knob::Runs) != 0;
     if (runs && fi->run_cls) {
       bool q = false;
       const hipError_t e = launch_find_iter_runs(b, fi->run_cls, o, st, t->cus, fi->run_quit != 0, &q);
@@ -934,7 +640,8 @@ struct KmerCacheEntry {
 std::mutex g_kmer_mu;
 std::vector<KmerCacheEntry> g_kmer;
 
-bool build_kmer(rure *const *res, size_t n, std::vector<uint32_t> *bitmap, std::vector<uint16_t> *mask, KmerDev *km) {
+bool build_kmer(rure *const *res, size_t n, std::vector<uint32_t> *bitmap, std::vector<uint16_t> *mask,
+                std::vector<uint16_t> *hmask, KmerDev *km) {
   if (n == 0 || n > 16) return false;
   size_t L = 0;
   bool seen[256] = {false};
@@ -972,6 +679,11 @@ bool build_kmer(rure *const *res, size_t n, std::vector<uint32_t> *bitmap, std::
     km->lut |= (uint32_t)c << (8 * code);
     km->present |= 1u << code;
   }
+  km->vlut = 0;
+  for (uint32_t c = 0; c < 4; ++c) {
+    const uint32_t v = (km->present >> c) & 1u ? (km->lut >> (8 * c)) & 0xFFu : ((c ^ 1u) << shift);
+    km->vlut |= v << (8 * c);
+  }
   km->len = L;
   km->cmask = (uint32_t)((1ull << (2 * L)) - 1);
   bitmap->assign(2048, 0);
@@ -983,7 +695,33 @@ bool build_kmer(rure *const *res, size_t n, std::vector<uint32_t> *bitmap, std::
       (*bitmap)[code >> 5] |= 1u << (code & 31);
       (*mask)[code] |= (uint16_t)(1u << i);
     }
-  return true;
+  // the masks' perfect hash for the tile kernel's LDS (kmer_hit_lds): an odd
+  // multiplier whose top 10 product bits are distinct over the string codes
+  std::vector<uint32_t> codes;
+  for (uint32_t c = 0; c < (uint32_t)mask->size(); ++c)
+    if ((*mask)[c]) codes.push_back(c);
+  if (codes.size() > 512) return false;
+  uint64_t rng = 0x9E3779B97F4A7C15ull;
+  std::vector<uint16_t> slot(1024);
+  for (int t = 0; t < 100000; ++t) {
+    rng ^= rng << 13, rng ^= rng >> 7, rng ^= rng << 17;
+    const uint32_t K = (uint32_t)rng | 1u;
+    std::fill(slot.begin(), slot.end(), 0);
+    std::vector<bool> used(1024, false);
+    bool ok = true;
+    for (uint32_t c : codes) {
+      const uint32_t h = (c * K) >> 22;
+      if (used[h]) { ok = false; break; }
+      used[h] = true;
+      slot[h] = (*mask)[c];
+    }
+    if (ok) {
+      km->hmul = K;
+      *hmask = slot;
+      return true;
+    }
+  }
+  return false;
 }
 
 // The cached device tables for this regex list, copied into *out while the
@@ -1004,15 +742,18 @@ bool kmer_device(rure *const *res, size_t n, KmerDev *out) {
   ent.blob = nullptr;
   std::vector<uint32_t> bm;
   std::vector<uint16_t> mk;
-  if (build_kmer(res, n, &bm, &mk, &ent.km)) {
+  std::vector<uint16_t> hm;
+  if (build_kmer(res, n, &bm, &mk, &hm, &ent.km)) {
     Blob b;
     const size_t ob = b.add(bm.data(), bm.size() * 4), om = b.add(mk.data(), mk.size() * 2);
+    const size_t oh = b.add(hm.data(), hm.size() * 2);
     DevTables tmp;
     std::string err;
     if (upload_blob(b, &tmp, &err)) {
       ent.blob = tmp.blob;
       ent.km.bitmap = (const uint32_t *)((uint8_t *)tmp.blob + ob);
       ent.km.mask = (const uint16_t *)((uint8_t *)tmp.blob + om);
+      ent.km.hmask = (const uint16_t *)((uint8_t *)tmp.blob + oh);
     }
   }
   g_kmer.push_back(ent);

@@ -1,5 +1,6 @@
 // Eager DFA materialization + minimisation.  See dfa_build.hpp.
 #include "dfa_build.hpp"
+#include "knobs.hpp"
 
 #include <algorithm>
 #include <chrono>
@@ -154,7 +155,7 @@ class Builder {
     std::vector<uint32_t>().swap(trans_cls_);
     minimise(nraw, tc, ncol, out);
     out->raw_states = nraw;
-    if (getenv("RURE_AMD_TIMING")) {  // diagnostic: construction and minimisation times
+    if (knob(Knob::Timing) == 1) {  // diagnostic: construction and minimisation times
       const auto t_end = std::chrono::steady_clock::now();
       fprintf(stderr, "dfa_build: %d raw states, %d classes, %d states: construct %.3f s, minimise %.3f s\n", nraw,
               ncls, out->nstates, std::chrono::duration<double>(t_built - t_begin).count(),

@@ -232,34 +232,11 @@ __device__ __forceinline__ uint32_t has_byte(uint32_t w, uint32_t rep) {
 }
 __device__ __forceinline__ bool prefix_hit(const FwdDfaDev &f, const uint4 *v) {
   uint32_t acc = 0;
-  if (f.pfx_depth < 2) {
-    for (uint32_t i = 0; i < f.pfx_n; ++i) {
-      const uint32_t rep = f.pfx_rep[i];
+  for (uint32_t i = 0; i < f.pfx_n; ++i) {
+    const uint32_t rep = f.pfx_rep[i];
 #pragma unroll
-      for (int k = 0; k < 8; ++k)
-        acc |= has_byte(v[k].x, rep) | has_byte(v[k].y, rep) | has_byte(v[k].z, rep) | has_byte(v[k].w, rep);
-    }
-    return acc != 0;
-  }
-  // a position can start a match only if its byte is in set 0, the next in
-  // set 1 and (depth 3) the one after in set 2 (one entry per set); bytes
-  // past the burst count as hits (the filter stays a superset)
-  const uint32_t r0 = f.pfx_set[0][0], o0 = f.pfx_or[0][0], r1 = f.pfx_set[1][0], o1 = f.pfx_or[1][0];
-  const uint32_t r2 = f.pfx_set[2][0], o2 = f.pfx_or[2][0];
-  const bool d3 = f.pfx_depth > 2;
-  uint32_t n1 = 0x80808080u, n2 = 0x80808080u;  // the next word's set-1 / set-2 bytes
-#pragma unroll
-  for (int k = 7; k >= 0; --k) {
-    const uint32_t w4[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
-#pragma unroll
-    for (int q = 3; q >= 0; --q) {
-      const uint32_t w = w4[q];
-      const uint32_t m0 = has_byte(w | o0, r0), m1 = has_byte(w | o1, r1);
-      const uint32_t m2 = d3 ? has_byte(w | o2, r2) : 0x80808080u;
-      acc |= m0 & ((m1 >> 8) | (n1 << 24)) & ((m2 >> 16) | (n2 << 16));
-      n1 = m1;
-      n2 = m2;
-    }
+    for (int k = 0; k < 8; ++k)
+      acc |= has_byte(v[k].x, rep) | has_byte(v[k].y, rep) | has_byte(v[k].z, rep) | has_byte(v[k].w, rep);
   }
   return acc != 0;
 }

@@ -795,7 +795,7 @@ hipError_t launch_set_cores(const BatchDev &b, const SetCoreDev &f, uint64_t *ou
   // threads per block (RURE_AMD_CORE_BS overrides, tuning); blocks per CU
   // as the LDS table allows
   int bs = 1024;
-  if (const char *v = getenv("RURE_AMD_CORE_BS")) bs = std::max(64, std::min(1024, atoi(v)));
+  if (knob(Knob::CoreBs) > 0) bs = std::max(64, std::min<int>(1024, (int)knob(Knob::CoreBs)));
   const int per_cu =
       std::max<int>(1, std::min<int>(2048 / bs, (int)((160u * 1024u) / core_lds_total(f.lds_bytes, f.hot))));
   const int mode = b.offs ? 1 : 0;
@@ -812,7 +812,7 @@ hipError_t launch_set_cores(const BatchDev &b, const SetCoreDev &f, uint64_t *ou
     hipLaunchKernelGGL(kern, dim3(grid), dim3(bs), lds, st, b, f, out, (uint64_t *)nullptr);
     return hipGetLastError();
   };
-  if (mode == 1 && getenv("RURE_AMD_CORE_PROF")) {  // diagnostic: per-phase clock stamps
+  if (mode == 1 && knob(Knob::CoreProf) == 1) {  // diagnostic: per-phase clock stamps
     const uint64_t nw = (uint64_t)grid * bs / 64;
     uint64_t *prof = nullptr;
     if ((e = hipMalloc(&prof, nw * 5 * 8)) != hipSuccess) return e;
@@ -970,8 +970,7 @@ __global__ __launch_bounds__(1024) void dfa_line_kernel(BatchDev bt, FwdDfaDev f
 // one-lane-per-haystack dfa_fwd_kernel, A/B)
 static bool line_path_ok(const BatchDev &b, const FwdDfaDev &f) {
   if (b.offs == nullptr || f.all || b.count == 0) return false;
-  const char *v = getenv("RURE_AMD_LINES");
-  return !(v && v[0] == '0');
+  return knob(Knob::Lines) != 0;
 }
 
 template <int MODE>

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../host/knobs.hpp"
+
 namespace rure_amd {
 
 // Row pitch of the LDS hot tables (bytes).  256 columns + 48 bytes: row s
@@ -25,7 +27,7 @@ struct BatchDev {
   // fallback pass then runs, else it returns at once (nullptr: always runs)
   uint32_t *quit_flag = nullptr;
   // set masks (the Pike VM's MODE_SET): words between consecutive haystacks'
-  // masks (the set groups of set_multi.hip write word g of `words`)
+  // masks (a set of more than 64 patterns: group g writes word g)
   uint32_t out_stride = 1;
 };
 
@@ -104,16 +106,6 @@ struct FwdDfaDev {
   // that hold none of those bytes (fwd_range); pfx_n = 0: off.
   uint32_t pfx_n;
   uint32_t pfx_rep[4];
-  // The same skip over the first two or three bytes of the prefixes
-  // (pfx_depth >= 2; 0 or 1: pfx_rep alone): set j = the prefixes' bytes at
-  // position j, one entry (the filter runs one SWAR test per set and word;
-  // more entries cost more than the DFA chain saves); a byte x is in the set
-  // when (x | pfx_or[j][0]) == the byte of pfx_set[j][0] (pfx_or 0x20 folds
-  // an ASCII letter's two cases).  A burst is skipped when no position in it
-  // starts a byte sequence from set 0 x set 1 (x set 2).
-  uint32_t pfx_depth;
-  uint32_t pfx_cnt[3];
-  uint32_t pfx_set[3][4], pfx_or[3][4];
   // find_iter DFA only: the regex has look-around assertions (the chunked
   // iteration then repairs units whose first reverse scan reached their
   // start, and a reverse NoMatch ends the iteration; iter_scan.hip), and its
@@ -207,31 +199,6 @@ struct SetCoreDev {
 };
 hipError_t launch_set_cores(const BatchDev &b, const SetCoreDev &f, uint64_t *out, hipStream_t st, int cus);
 
-// Several core-form set automata run side by side over each haystack in one
-// pass (set_multi.hip): the groups of a set of more than 64 patterns (group
-// g = patterns 64 g .. 64 g + 63, mask word g), or a set split into smaller
-// groups (A/B, RURE_AMD_SET_CHAINS).  Each lane steps every group's chain
-// over the same bytes.  Per group, in the combined LDS image: a 256-entry u16
-// class map holding 2k (k = the byte's class), its hot
-// rows ((hot + 1) x (K + 1) u16, SetCoreDev layout), its 64 code masks, its
-// 128 start cores and its hot cores' EOF masks.
-constexpr int kMultiMaxGroups = 4;
-struct MultiGroupDev {
-  const uint16_t *gcore;
-  const uint64_t *gout;
-  const uint64_t *eof;
-  uint64_t all;
-  uint32_t K, hot, dead, quit;                          // quit = 0xFFFFFFFF if none
-  uint32_t cls_off, rows_off, mt_off, st_off, he_off;   // LDS byte offsets
-  uint32_t word, shift;                                 // where its mask goes
-};
-struct MultiCoreDev {
-  const uint8_t *lds_image;
-  uint32_t lds_bytes, G, words;
-  uint32_t split;   // groups share word 0 (a split set): a quit marks the whole word
-  MultiGroupDev g[kMultiMaxGroups];
-};
-hipError_t launch_set_multi(const BatchDev &b, const MultiCoreDev &f, uint64_t *out, hipStream_t st, int cus);
 hipError_t launch_core_profile(const BatchDev &b, const SetCoreDev &f, uint64_t count, unsigned int *visits,
                                unsigned int *mask_counts, hipStream_t st, int cus);
 
@@ -325,6 +292,9 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
 struct KmerDev {
   const uint32_t *bitmap;
   const uint16_t *mask;
+  const uint16_t *hmask;  // 1024: mask[c] at (c * hmul) >> 22, injective on the string codes
+  uint32_t hmul;
+  uint32_t vlut;  // byte k: the alphabet byte of code k (absent code: a byte of another code)
   uint32_t shift, lut, present, cmask;
   uint64_t len;
 };

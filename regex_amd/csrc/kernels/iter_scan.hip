@@ -237,37 +237,6 @@ __device__ __forceinline__ const uint8_t *stage_tables(const FwdDfaDev &f, const
   return r.lds_bytes ? rl : nullptr;
 }
 
-// Pass 1: speculative iteration of every unit.
-__global__ __launch_bounds__(1024) void iter_spec_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
-                                                        Unit *units, uint64_t *slots, uint32_t *counts, uint32_t *dirty) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const uint8_t *rlds = stage_tables(f, r, lds);
-  for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < nunits; u += (uint64_t)gridDim.x * blockDim.x) {
-    uint64_t h, len, c0, c1;
-    const uint8_t *base;
-    unit_bounds(b, g, u, &h, &base, &len, &c0, &c1);
-    UnitIter it;
-    it.init({c0, NONE}, c1);
-    uint32_t n = 0;
-    uint64_t s, e;
-    while (it.next(f, r, lds, rlds, base, len, &s, &e)) {
-      if (n < g.slots) *(ulonglong2 *)&slots[(u * g.slots + n) * 2] = make_ulonglong2(s, e);
-      ++n;
-    }
-    Unit U;
-    U.entry = {c0, NONE};
-    U.exit = it.exit;
-    U.spec_exit = it.exit;
-    U.spec_count = n;
-    U.flags = (it.clean ? (U_SPEC_CLEAN | U_CLEAN) : 0) | (it.quit ? U_QUIT : 0) |
-              (f.looks && it.unsure && u % g.nk != 0 ? U_UNSURE : 0);
-    U.skip = U.pad = 0;
-    units[u] = U;
-    counts[u] = n;
-    if ((U.flags & (U_SPEC_CLEAN | U_UNSURE)) != U_SPEC_CLEAN) atomicOr(dirty, 1u);  // the fix pass has work
-  }
-}
-
 // Branch-free exact steps for small automata (FwdDfaDev::all /
 // RevDfaDev::all: every state's row in LDS; dead and quit absorb).  Bytes
 // k in [k0, kend) of the 16 in `w` are stepped from `s`; lastk = the last k
@@ -364,16 +333,17 @@ __device__ __forceinline__ uint64_t rev_scan_all(const RevDfaDev &r, const uint8
   return rs;
 }
 
-// Pass 1, burst-interleaved.  In iter_spec_kernel every search is a nest of
-// loops (forward scan to the dead state, reverse scan, restart), so a lane
-// whose search ends early waits, masked off, until every other lane of its
-// wave has finished its own forward loop — usually its whole unit — and then
-// scans the rest of its unit alone.  Here the wave loop is over bursts: in
+// Pass 1, burst-interleaved.  Written as a nest of loops per lane (forward
+// scan to the dead state, reverse scan, restart; the round-1 kernel, deleted
+// in round 5 after losing every A/B), a lane whose search ends early waits,
+// masked off, until every other lane of its wave has finished its own
+// forward loop — usually its whole unit — and then scans the rest of its
+// unit alone.  Here the wave loop is over bursts: in
 // each iteration every searching lane advances its current forward scan by
 // at most one aligned 128-byte burst (the same LDS fast path, fwd_range); a
 // lane whose scan ended does its reverse scan, applies the iteration rule
 // (re_trait.rs:197-221) and sets up its next search (exec.rs:632-662) in
-// the same iteration.  Same unit records as iter_spec_kernel.
+// the same iteration.
 __global__ __launch_bounds__(1024) void iter_spec_burst_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f,
                                                               RevDfaDev r, Unit *units, uint64_t *slots,
                                                               uint32_t *counts, uint32_t *dirty) {
@@ -496,7 +466,7 @@ __global__ __launch_bounds__(1024) void iter_spec_burst_kernel(BatchDev b, Geo g
 // first literal that matches is the leftmost-first match) and the greedy
 // iteration of re_trait.rs:197-221 keeps those starting at or after the
 // previous match end (literals are non-empty).  The unit records are the
-// same as iter_spec_kernel's; repairs and the walker use the DFA.
+// same as iter_spec_burst_kernel's; repairs and the walker use the DFA.
 // (lit_verify: dfa_device.hpp)
 template <bool K4, bool K8>
 __global__ __launch_bounds__(1024) void iter_spec_lit_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f,
@@ -1009,7 +979,13 @@ __device__ __forceinline__ void sam_block(uint32_t (&D)[NW], const uint32_t *B, 
 // (code(b) = (b >> shift) & 3, four bytes per VALU op) join the previous
 // block's in a 64-bit window register; the L-mer ending at each byte is one
 // independent probe of the LDS bitmap of the strings' codes (no dependent
-// chain).  Returns the probe hits (bit j: the L-mer ending at byte j).  Rp:
+// chain).  The probes' random dwords cost ~4.6 bank-conflict cycles per LDS
+// read (C3: 171M conflict cycles, 37.5M LDS instructions); a conflict-free
+// 32-dword prefilter (1.4% of the 10-bit prefixes hit on regex-dna) with
+// the exact bitmap read for its hits cut them to 15M but added a dependent
+// LDS round trip and ~45 VALU per block: 0.78-0.86 ms against 0.69
+// (round 5, profiles/r05_c3_ab.txt), so the direct probe stays.
+// Returns the probe hits (bit j: the L-mer ending at byte j).  Rp:
 // the previous block's codes (garbage before a unit's first block: the
 // windows reaching into it start before the unit and are dropped by
 // kmer_hit).
@@ -1071,6 +1047,45 @@ __device__ __forceinline__ void kmer_hit(const SaMulti &m, uint64_t e, uint64_t 
   }
 }
 
+// kmer_hit for the tile loop, from LDS only: the 8-mer ending at byte p of
+// the staged line (bytes before the line: the previous line's last 8, pz:pw)
+// is read back from the wave's stage buffer, checked against the alphabet
+// (four bytes per v_perm: the byte each code stands for, KmerDev::vlut) and
+// its regex mask read from the LDS perfect hash HT (KmerDev::hmul).  kmer_hit
+// takes two dependent global round trips (the bytes, then mask[code]), which
+// the wave waited for once per line.
+template <int MQ>
+__device__ __forceinline__ void kmer_hit_lds(const SaMulti &m, const uint16_t *HT, const uint4 *buf, int lane, int sw,
+                                             uint32_t p, uint32_t pz, uint32_t pw, uint64_t ls, uint64_t c0,
+                                             uint64_t c1, uint32_t (&pn)[MQ], uint64_t u, uint32_t nslots) {
+  const KmerDev &km = m.km;
+  const uint64_t e = ls + p + 1;
+  if (e < 8 || e - 8 < c0) return;  // starts before the unit: not its match
+  // virtual dwords: 0, 1 = pz, pw; 2 + 4 b + r = dword r of the line's block b
+  const uint32_t v0 = p + 1, d0 = v0 >> 2, sh = 8 * (v0 & 3);
+  const uint32_t *bw = (const uint32_t *)(buf + lane * 8);
+  uint32_t dw[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const uint32_t d = d0 + i, ld = d >= 2 ? min(d - 2, 31u) : 0u;
+    const uint32_t x = bw[(((ld >> 2) ^ (uint32_t)sw) << 2) | (ld & 3)];
+    dw[i] = d == 0 ? pz : d == 1 ? pw : x;
+  }
+  const uint32_t lo = __builtin_amdgcn_alignbit(dw[1], dw[0], sh), hi = __builtin_amdgcn_alignbit(dw[2], dw[1], sh);
+  const uint32_t M = 0x03030303u << km.shift;
+  const uint32_t cl = (lo & M) >> km.shift, ch = (hi & M) >> km.shift;  // one code per byte
+  if ((__builtin_amdgcn_perm(0u, km.vlut, cl) ^ lo) | (__builtin_amdgcn_perm(0u, km.vlut, ch) ^ hi)) return;
+  const uint32_t code =
+      __builtin_amdgcn_udot4(cl, 0x40100401u, 0u, false) | (__builtin_amdgcn_udot4(ch, 0x40100401u, 0u, false) << 8);
+  const uint32_t mask = HT[(code * km.hmul) >> 22];
+  const uint64_t st = e - 8;
+#pragma unroll
+  for (int q = 0; q < MQ; ++q) {
+    if ((uint32_t)q >= m.nre) break;
+    if ((mask >> q) & 1u) multi_record<MQ>(m, pn, q, st, e, c0, c1, u, nslots);
+  }
+}
+
 // The k-mer engine's step of one block with its hits settled at once (the
 // tail paths; the tile loop defers a line's hits to its end, see
 // multi_tile_body): bytes k0..kend of the block at bp.
@@ -1104,12 +1119,23 @@ __device__ __forceinline__ void multi_block(uint32_t (&D)[NW], const uint32_t *B
 // consecutive units; each load covers 8 units x one 128-byte line, staged
 // through a swizzled LDS buffer), each lane running every regex of the pass
 // over its unit.  MQ >= m.nre bounds the per-regex state arrays.
-template <int NW, bool KMER, int MQ>
+template <int NW, bool KMER, int MQ, int WPB = 4>
 __device__ __forceinline__ void multi_tile_body(const BatchDev &b, const Geo &g, uint64_t nunits, const SaMulti &m) {
-  __shared__ __attribute__((aligned(16))) uint32_t B[KMER ? 2048 : 256 * SamPitch<NW>::v];
-  __shared__ __attribute__((aligned(16))) uint4 stage[4][64 * 8];
+  // one LDS object, the table first: its probes' addresses need no base
+  // (the compiler placed a separate stage array first and added its size to
+  // every probe address: one VALU per byte); k-mer: the bitmap, then the
+  // regex masks' perfect hash of kmer_hit_lds
+  struct __attribute__((aligned(16))) Lds {
+    uint32_t B[KMER ? 2048 : 256 * SamPitch<NW>::v];
+    uint16_t HT[KMER ? 1024 : 2];
+    uint4 stage[WPB][64 * 8];
+  };
+  __shared__ Lds lds_;
+  uint32_t *const B = lds_.B;
+  uint4 (*const stage)[64 * 8] = lds_.stage;
   if (KMER) {
     for (uint32_t i = threadIdx.x; i < 2048; i += blockDim.x) B[i] = m.km.bitmap[i];
+    for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) lds_.HT[i] = m.km.hmask[i];
   } else {
     for (uint32_t i = threadIdx.x; i < 256 * SamPitch<NW>::v; i += blockDim.x) B[i] = m.image[i];
   }
@@ -1118,10 +1144,10 @@ __device__ __forceinline__ void multi_tile_body(const BatchDev &b, const Geo &g,
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   uint4 *buf = stage[w];
   const int src_h = lane >> 3, src_seg = lane & 7, sw = (lane >> 1) & 7;
-  const uint64_t ngroups = (nunits + 63) / 64, nwaves = (uint64_t)gridDim.x * 4;
+  const uint64_t ngroups = (nunits + 63) / 64, nwaves = (uint64_t)gridDim.x * WPB;
   const uint8_t *const base = b.hay;  // one haystack
   const uint64_t len = b.length;
-  for (uint64_t gi = (uint64_t)blockIdx.x * 4 + w; gi < ngroups; gi += nwaves) {
+  for (uint64_t gi = (uint64_t)blockIdx.x * WPB + w; gi < ngroups; gi += nwaves) {
     const uint64_t u = gi * 64 + lane, k = u;
     const bool valid = u < nunits;
     const bool full = valid && k + 1 < nk;
@@ -1137,8 +1163,8 @@ __device__ __forceinline__ void multi_tile_body(const BatchDev &b, const Geo &g,
     uint32_t D[NW];
 #pragma unroll
     for (int x = 0; x < NW; ++x) D[x] = 0;
-    uint4 first = make_uint4(0, 0, 0, 0);
     uint4 n0, n1, n2, n3, n4, n5, n6, n7;
+    uint32_t pz = 0, pw = 0;  // k-mer: the previous line's last 8 bytes (kmer_hit_lds)
 #define RURE_SRC(j, a) (src0 + ((us0 + 8 * (j) + 1 < nk) ? (us0 + 8 * (j)) * C : 0) + (a))
 #define RURE_LOAD_TILE(a)                                                                                     \
   n0 = *(const uint4 *)RURE_SRC(0, a); n1 = *(const uint4 *)RURE_SRC(1, a);                                  \
@@ -1155,46 +1181,61 @@ __device__ __forceinline__ void multi_tile_body(const BatchDev &b, const Geo &g,
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       const uint64_t an = at + 128 < C ? at + 128 : at;
       RURE_LOAD_TILE(an)
-      if (full) {
+      if constexpr (KMER) {
+        // The line's probe hits collect in a 128-bit shift register (block
+        // mm at bits 16 mm) and are settled after the line: the block loop
+        // issues no global load, so nothing in it waits on the next line's
+        // tile loads in flight (one vmcnt counter, in order).  Every lane
+        // runs the block loop (a lane without a full unit probes staged
+        // bytes of unit 0 and drops its hits): the probes' exec mask stays
+        // whole.
         uint4 cur = buf[lane * 8 + sw];
-        if (at == 0) first = cur;
-        if (KMER) {
-          // The line's probe hits collect in a 128-bit shift register (block
-          // mm at bits 16 mm) and are settled after the line: the block loop
-          // issues no global load, so nothing in it waits on the next
-          // line's tile loads in flight (one vmcnt counter, in order).
-          uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+        // (two blocks per iteration: a pair's hits are one word of the
+        // register, shifted in by moves; after the loop cur is block 7)
+        uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
 #pragma unroll 1
-          for (int mm = 0; mm < 8; ++mm) {
-            const uint4 nx = buf[lane * 8 + ((mm + 1 < 8 ? mm + 1 : 7) ^ sw)];
+        for (int mm = 0; mm < 8; mm += 2) {
+          uint32_t pair = 0;
+#pragma unroll
+          for (int x = 0; x < 2; ++x) {
+            const uint4 nx = buf[lane * 8 + ((mm + x + 1 < 8 ? mm + x + 1 : 7) ^ sw)];
             const uint32_t wd[4] = {cur.x, cur.y, cur.z, cur.w};
             const uint32_t cm = kmer_probe<8>(D[0], B, m.km, wd);
-            h0 = __builtin_amdgcn_alignbit(h1, h0, 16);
-            h1 = __builtin_amdgcn_alignbit(h2, h1, 16);
-            h2 = __builtin_amdgcn_alignbit(h3, h2, 16);
-            h3 = __builtin_amdgcn_alignbit(cm, h3, 16);
+            pair |= cm << (16 * x);
             cur = nx;
           }
-          const uint32_t hw[4] = {h0, h1, h2, h3};
-#pragma unroll
-          for (int x = 0; x < 4; ++x) {
-            uint32_t hm = hw[x];
+          h0 = h1;
+          h1 = h2;
+          h2 = h3;
+          h3 = pair;
+        }
+        if (full) {
+          // one loop over the line's 128 hit bits: the wave iterates as
+          // often as its lane with the most hits (mostly once), not once per
+          // word holding a hit in some lane
 #pragma unroll 1
-            while (hm) {
-              const uint32_t j = __builtin_ctz(hm);
-              hm &= hm - 1;
-              kmer_hit<MQ, 8>(m, c0 + at + 32 * x + j + 1, c0, c1, pn, u, g.slots, base);
-            }
+          while (h0 | h1 | h2 | h3) {
+            const uint32_t x = h0 ? 0u : h1 ? 1u : h2 ? 2u : 3u;
+            const uint32_t hm = x == 0 ? h0 : x == 1 ? h1 : x == 2 ? h2 : h3;
+            const uint32_t j = __builtin_ctz(hm), rest = hm & (hm - 1);
+            h0 = x == 0 ? rest : h0;
+            h1 = x == 1 ? rest : h1;
+            h2 = x == 2 ? rest : h2;
+            h3 = x == 3 ? rest : h3;
+            kmer_hit_lds<MQ>(m, lds_.HT, buf, lane, sw, 32 * x + j, pz, pw, c0 + at, c0, c1, pn, u, g.slots);
           }
-        } else {
+        }
+        pz = cur.z;
+        pw = cur.w;
+      } else if (full) {
+        uint4 cur = buf[lane * 8 + sw];
 #pragma unroll 1
-          for (int mm = 0; mm < 8; ++mm) {
-            const uint4 nx = buf[lane * 8 + ((mm + 1 < 8 ? mm + 1 : 7) ^ sw)];
-            const uint32_t wd[4] = {cur.x, cur.y, cur.z, cur.w};
-            multi_block<NW, KMER, MQ>(D, B, m, wd, 0, 16, (int64_t)(c0 + at + 16 * mm), c0, c1, pn, u, g.slots,
-                                      base);
-            cur = nx;
-          }
+        for (int mm = 0; mm < 8; ++mm) {
+          const uint4 nx = buf[lane * 8 + ((mm + 1 < 8 ? mm + 1 : 7) ^ sw)];
+          const uint32_t wd[4] = {cur.x, cur.y, cur.z, cur.w};
+          multi_block<NW, KMER, MQ>(D, B, m, wd, 0, 16, (int64_t)(c0 + at + 16 * mm), c0, c1, pn, u, g.slots,
+                                    base);
+          cur = nx;
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1204,23 +1245,13 @@ __device__ __forceinline__ void multi_tile_body(const BatchDev &b, const Geo &g,
 #undef RURE_LOAD_TILE
 #undef RURE_STAGE
 #undef RURE_SRC
-    uint4 nxt;
-    nxt.x = __shfl_down(first.x, 1);
-    nxt.y = __shfl_down(first.y, 1);
-    nxt.z = __shfl_down(first.z, 1);
-    nxt.w = __shfl_down(first.w, 1);
     if (!valid) continue;
     if (full) {
-      // strings starting before the cut end in [c1, c1 + L - 1)
+      // strings starting before the cut end in [c1, c1 + L - 1): the next
+      // unit's first bytes, from memory (aligned: c1 is; keeping the tile's
+      // first block for a shuffle held 4 more VGPRs over the whole loop)
       const uint64_t qend = min(len, c1 + L - 1);
-      uint64_t q = c1;
-      if (q < qend && lane < 63 && k + 2 < nk) {  // the next unit is full: lane + 1 holds its first block
-        const uint32_t wd[4] = {nxt.x, nxt.y, nxt.z, nxt.w};
-        const uint32_t kend = qend - q < 16 ? (uint32_t)(qend - q) : 16;
-        multi_block<NW, KMER, MQ>(D, B, m, wd, 0, kend, (int64_t)q, c0, c1, pn, u, g.slots, base);
-        q += 16;
-      }
-      for (; q < qend; q += 16) {  // from memory (aligned: c1 is)
+      for (uint64_t q = c1; q < qend; q += 16) {
         const uint4 v = *(const uint4 *)(base + q);
         const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
         const uint32_t kend = qend - q < 16 ? (uint32_t)(qend - q) : 16;
@@ -1896,7 +1927,7 @@ __device__ __forceinline__ void emit_body(const BatchDev &b, const Geo &g, uint6
       if (cnt && o0 < cap) {
         const uint32_t fl = units[u].flags;
         rerun = ((fl & U_FIXED) && !(fl & U_COPY)) || cnt > g.slots;
-        copy = !rerun && copies;  // copies = false: iter_copy_out_kernel wrote them
+        copy = !rerun && copies;  // copies = false: iter_copy_group_kernel wrote them
         skip = (fl & U_COPY) ? units[u].skip : 0;  // loaded by every lane at once, not per copied unit
         compact = LEX && (fl & U_COMPACT) != 0;
         if (compact) {
@@ -2030,14 +2061,6 @@ __global__ __launch_bounds__(1024) void iter_emit_kernel(BatchDev b, Geo g, uint
   emit_body<true>(b, g, nunits, f, r, units, slots, off, out, cap, lds, copies != 0);
 }
 
-// The copies of a lexer pass in output order: block k writes output records
-// [k R, (k + 1) R) — one contiguous range, 16 B per lane per store — reading
-// them from the few units that hold them (their slots: u16 pairs, the tail
-// pass's records from the back), kCopyUnits units staged at a time.
-// emit_body's unit-ordered copy writes 64
-// units' ranges at once (8 x 128 B per store instruction, scattered over
-// the whole output): 0.31 ms for the strip's 35 M records.  Units that are
-// re-run (no valid slots) are left to iter_emit_kernel.
 // The copies of a lexer pass by lexer group (U_COMPACT interleaved rows,
 // lex_rec32): one block per group of 64 units, whose output records are one
 // contiguous range.  Per window of kGrpWin output records the four waves
@@ -2139,90 +2162,6 @@ __global__ __launch_bounds__(256) void iter_copy_group_kernel(BatchDev b, Geo g,
     }
   }
 }
-
-constexpr uint32_t kCopyRecs = 4096;  // output records per block (256 threads x 16)
-constexpr uint32_t kCopyUnits = 64;   // units staged per round (the strip's 4096 records span ~31)
-
-// iter_copy_out_kernel's block index: bidx[k] = the unit holding output
-// record k * kCopyRecs (k < nb), so a block starts from one load instead of
-// a three-round search over the unit offsets.
-__global__ void copy_index_kernel(uint64_t nunits, const uint64_t *off, uint32_t *bidx, uint64_t nb) {
-  const uint64_t obase = off[0];
-  for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < nunits; u += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t lo = off[u] - obase, hi = off[u + 1] - obase;
-    for (uint64_t k = (lo + kCopyRecs - 1) / kCopyRecs; k * kCopyRecs < hi && k < nb; ++k) bidx[k] = (uint32_t)u;
-  }
-}
-
-__global__ __launch_bounds__(256) void iter_copy_out_kernel(BatchDev b, Geo g, uint64_t nunits, const Unit *units,
-                                                            const uint64_t *slots, const uint64_t *off,
-                                                            uint64_t *out, uint64_t cap, const uint32_t *bidx,
-                                                            uint64_t nb) {
-  __shared__ uint64_t soff[kCopyUnits + 1];
-  __shared__ uint64_t sbase[kCopyUnits];
-  __shared__ uint32_t sskip[kCopyUnits], snlex[kCopyUnits], sok[kCopyUnits];
-  const uint64_t obase = off[0];
-  const uint64_t total = min(off[nunits] - obase, cap);
-  for (uint64_t r0 = (uint64_t)blockIdx.x * kCopyRecs; r0 < total; r0 += (uint64_t)gridDim.x * kCopyRecs) {
-    // the unit holding record r0: last u with off[u] - obase <= r0 (a
-    // 256-ary search, two or three rounds over the unit offsets)
-    uint64_t lo = 0, hi = nunits;  // answer in [lo, hi)
-    if (r0 / kCopyRecs < nb) lo = bidx[r0 / kCopyRecs], hi = lo + 1;
-    while (hi - lo > 1) {
-      const uint64_t step = (hi - lo + 255) / 256;
-      const uint64_t c = lo + threadIdx.x * step;
-      const bool le = c < hi && off[c] - obase <= r0;
-      // the largest probe with off <= r0
-      const uint64_t best = __syncthreads_count(le);  // probes are monotone: the first `best` hold
-      const uint64_t nlo = lo + (best ? best - 1 : 0) * step;
-      hi = min(hi, nlo + step);
-      lo = nlo;
-      __syncthreads();
-    }
-    // the units from u0 on, kCopyUnits at a time, into LDS; each round
-    // writes the block's records that fall into them (offsets are sorted)
-    const uint64_t rend = min(total, r0 + kCopyRecs);
-    for (uint64_t u0 = lo;; u0 += kCopyUnits) {
-      const uint64_t uu = u0 + threadIdx.x;
-      if (threadIdx.x <= kCopyUnits) soff[threadIdx.x] = uu <= nunits ? off[uu] - obase : ~0ull;
-      if (threadIdx.x < kCopyUnits && uu < nunits) {
-        const Unit U = units[uu];
-        const uint64_t cnt = off[uu + 1] - off[uu];
-        sok[threadIdx.x] = !(((U.flags & U_FIXED) && !(U.flags & U_COPY)) || cnt > g.slots);
-        sskip[threadIdx.x] = (U.flags & U_COPY) ? U.skip : 0;
-        snlex[threadIdx.x] = (U.flags & U_COMPACT) ? U.pad : 0xFFFFFFFFu;  // ~0: u64 slots
-        uint64_t hh, ll, c0, c1;
-        const uint8_t *bb;
-        unit_bounds(b, g, uu, &hh, &bb, &ll, &c0, &c1);
-        sbase[threadIdx.x] = c0;
-      }
-      __syncthreads();
-      const uint64_t lo_r = soff[0], hi_r = soff[kCopyUnits];
-#pragma unroll 8
-      for (uint32_t k = 0; k < kCopyRecs / 256; ++k) {
-        const uint64_t rr = r0 + k * 256 + threadIdx.x;
-        if (rr >= rend || rr < lo_r || rr >= hi_r) continue;
-        uint32_t a = 0, z = kCopyUnits;  // last j with soff[j] <= rr
-        while (z - a > 1) {
-          const uint32_t m = (a + z) >> 1;
-          if (soff[m] <= rr) a = m;
-          else z = m;
-        }
-        if (!sok[a]) continue;  // re-run by iter_emit_kernel
-        const uint64_t u = u0 + a;
-        const uint32_t i = sskip[a] + (uint32_t)(rr - soff[a]);
-        const uint32_t nl = snlex[a];
-        const ulonglong2 v = nl != 0xFFFFFFFFu ? slot_rec(slots, g, u, i, true, sbase[a], nl)
-                                               : slot_rec(slots, g, u, i, false, 0, 0);
-        *(ulonglong2 *)(out + 2 * rr) = v;
-      }
-      __syncthreads();
-      if (hi_r >= rend) break;
-    }
-    __syncthreads();
-  }
-}
-
 
 // ---------------------------------------------------- one wave per haystack
 // exec.rs:473-514 per search: the DFA on lane 0; the Pike VM on the whole
@@ -2451,9 +2390,7 @@ hipError_t long_scan_m(const BatchDev &b, const FwdDfaDev &f, const RevDfaDev &r
     // first byte: measured faster there (Sherlock\s+\w+ 1.76 -> 1.54 ms per
     // GiB, >[^\n]*\n 1.10 -> 0.31) and slower with two ((?i)holmes\w*:
     // 1.46 -> 1.73 ms; profiles/r03_prefix_ab.jsonl)
-    // (two or three prefix positions, pfx_depth: a burst is skipped unless a
-    // position starts one of the prefixes' byte sequences)
-    if (f.pfx_n == 1 || f.pfx_depth >= 2) {
+    if (f.pfx_n == 1) {
       if ((e = allow_lds(long_scan_kernel<MODE, true>, iter_lds_bytes(f, r))) != hipSuccess) break;
       hipLaunchKernelGGL((long_scan_kernel<MODE, true>), lg, dim3(256), iter_lds_bytes(f, r), st, b, g, nunits, f, r,
                          ures, best);
@@ -2492,8 +2429,7 @@ hipError_t launch_long_scan(int mode, const BatchDev &b, const FwdDfaDev &f, con
 // start, U_COMPACT; units of at most 64 KiB: its record queue packs two u16
 // per register)
 static bool lex_usable(const FwdDfaDev &f, const BatchDev &b, const Geo &g) {
-  const char *lex_env = getenv("RURE_AMD_LEX");
-  return f.lex_bytes && !(lex_env && lex_env[0] == '0') && !b.offs && g.nk >= 2 && (g.chunk % 128) == 0 &&
+  return f.lex_bytes && knob(Knob::Lex) != 0 && !b.offs && g.nk >= 2 && (g.chunk % 128) == 0 &&
          (b.count == 1 || (b.stride % 16) == 0) && (((uintptr_t)(b.hay + b.start)) & 15) == 0 &&
          b.length < (1ull << 32) && g.chunk <= 65536;
 }
@@ -2542,19 +2478,17 @@ static hipError_t iter_scratch(uint64_t nunits, uint32_t nslots, hipStream_t st,
 
 static int iter_bs() {
   int bs = 256;
-  if (const char *v = getenv("RURE_AMD_ITER_BS")) bs = std::max(64, std::min(1024, atoi(v)));
+  if (knob(Knob::IterBs) > 0) bs = std::max(64, std::min<int>(1024, (int)knob(Knob::IterBs)));
   return bs;
 }
 
 static bool sa_usable(const FwdDfaDev &f) {
-  const char *sa_env = getenv("RURE_AMD_SA"), *lit_env = getenv("RURE_AMD_LIT");
-  return f.sa_len && !(sa_env && sa_env[0] == '0') && !(lit_env && lit_env[0] == '1');
+  return f.sa_len && knob(Knob::Sa) != 0 && knob(Knob::Lit) != 1;
 }
 
 static bool sa_tile_ok(const BatchDev &b, const Geo &g) {
-  const char *sa_env = getenv("RURE_AMD_SA");
   return !b.offs && g.nk >= 2 && (g.chunk % 128) == 0 && (b.count == 1 || (b.stride % 16) == 0) &&
-         (((uintptr_t)(b.hay + b.start)) & 15) == 0 && !(sa_env && sa_env[0] == '2');
+         (((uintptr_t)(b.hay + b.start)) & 15) == 0 && knob(Knob::Sa) != 2;
 }
 
 // The passes after the speculative one (same for every engine): a span's
@@ -2596,21 +2530,9 @@ static hipError_t iter_post(const BatchDev &b, const Geo &g, uint64_t nunits, co
   // emit pass only re-runs units (needs a 16-byte aligned output)
   dense = dense && (((uintptr_t)o.matches) & 15) == 0;
   if (dense) {
-    if (getenv("RURE_AMD_COPY_GROUP") && getenv("RURE_AMD_COPY_GROUP")[0] == '0') {
-      // (A/B) the output-ordered copy; its block index lives in the repair
-      // queue's space (the walk is done with it): 2 u32 per unit
-      const uint64_t nb = 2 * nunits;
-      hipLaunchKernelGGL(copy_index_kernel, dim3(grid_cap(nunits, 256, cus, 4)), dim3(256), 0, st, nunits,
-                         (const uint64_t *)sc.off, (uint32_t *)sc.queue, nb);
-      if ((e = hipGetLastError()) != hipSuccess) return e;
-      hipLaunchKernelGGL(iter_copy_out_kernel, dim3((unsigned)cus * 8), dim3(256), 0, st, b, g, nunits,
-                         (const Unit *)sc.units, (const uint64_t *)sc.slots, (const uint64_t *)sc.off, o.matches,
-                         o.cap, (const uint32_t *)sc.queue, nb);
-    } else {
-      hipLaunchKernelGGL(iter_copy_group_kernel, dim3(grid_cap((nunits + 63) / 64, 1, cus, 8)), dim3(256), 0, st, b,
-                         g, nunits, (const Unit *)sc.units, (const uint64_t *)sc.slots, (const uint64_t *)sc.off,
-                         o.matches, o.cap);
-    }
+    hipLaunchKernelGGL(iter_copy_group_kernel, dim3(grid_cap((nunits + 63) / 64, 1, cus, 8)), dim3(256), 0, st, b, g,
+                       nunits, (const Unit *)sc.units, (const uint64_t *)sc.slots, (const uint64_t *)sc.off, o.matches,
+                       o.cap);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   hipLaunchKernelGGL(iter_emit_kernel, dim3(grid), dim3(bs), lb, st, b, g, nunits, f, r, sc.units, sc.slots, sc.off,
@@ -2632,11 +2554,13 @@ __global__ __launch_bounds__(256) void iter_spec_sa_multi_tile_kernel(BatchDev b
   multi_tile_body<NW, false, MQ>(b, g, nunits, m);
 }
 // The k-mer engine holds no Shift-And words: capped at 128 VGPRs for 4 waves
-// per SIMD (16 per CU; 146 VGPRs uncapped = 3 waves)
+// per SIMD (16 per CU; HIP's second bound is waves per SIMD).  Blocks of 8
+// waves share one bitmap: two blocks of 72.1 KB LDS per CU (four of 4 waves
+// held 4 x 40 KB, all 160 KB).
 template <int MQ>
-__global__ __launch_bounds__(256, 4) void iter_spec_kmer_multi_tile_kernel(BatchDev b, Geo g, uint64_t nunits,
+__global__ __launch_bounds__(512, 4) void iter_spec_kmer_multi_tile_kernel(BatchDev b, Geo g, uint64_t nunits,
                                                                            SaMulti m) {
-  multi_tile_body<1, true, MQ>(b, g, nunits, m);
+  multi_tile_body<1, true, MQ, 8>(b, g, nunits, m);
 }
 
 // The passes after a fused speculative pass for all its regexes at once:
@@ -2722,9 +2646,8 @@ hipError_t launch_find_iter_multi(const BatchDev &b, int nre, const FwdDfaDev *c
   SaMulti m{};
   m.nre = (uint32_t)nre;
   m.len = f[0]->sa_len;
-  // RURE_AMD_KMER=0 keeps the Shift-And words (A/B)
-  const char *kenv = getenv("RURE_AMD_KMER");
-  const bool kmer = km && km->bitmap && km->len == m.len && m.len == 8 && !(kenv && kenv[0] == '0');
+  // knob kmer=0 keeps the Shift-And words (A/B)
+  const bool kmer = km && km->bitmap && km->len == m.len && m.len == 8 && knob(Knob::Kmer) != 0;
   if (kmer) m.km = *km;
   // packed per-regex state (multi_record): positions up to chunk + L, and at
   // most one match per L bytes of a unit
@@ -2810,13 +2733,13 @@ hipError_t launch_find_iter_multi(const BatchDev &b, int nre, const FwdDfaDev *c
     break;
     if (kmer) {
       ktimer_begin(st);
+      const dim3 kg(grid_cap((nunits + 63) / 64, 8, cus, 2));
       if (nre <= 4)
-        hipLaunchKernelGGL((iter_spec_kmer_multi_tile_kernel<4>), sg, dim3(256), 0, st, b, g, nunits, m);
+        hipLaunchKernelGGL((iter_spec_kmer_multi_tile_kernel<4>), kg, dim3(512), 0, st, b, g, nunits, m);
       else if (nre <= 9)
-        hipLaunchKernelGGL((iter_spec_kmer_multi_tile_kernel<9>), sg, dim3(256), 0, st, b, g, nunits, m);
+        hipLaunchKernelGGL((iter_spec_kmer_multi_tile_kernel<9>), kg, dim3(512), 0, st, b, g, nunits, m);
       else
-        hipLaunchKernelGGL((iter_spec_kmer_multi_tile_kernel<kSaMultiMax>), sg, dim3(256), 0, st, b, g,
-                           nunits, m);
+        hipLaunchKernelGGL((iter_spec_kmer_multi_tile_kernel<kSaMultiMax>), kg, dim3(512), 0, st, b, g, nunits, m);
       ktimer_end(st);
     } else {
       switch (nw) {
@@ -2882,16 +2805,15 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
     uint32_t *counts = sc.counts, *dirty = sc.dirty;
     do {
       const size_t lb = iter_lds_bytes(*f, r);
-      if ((e = allow_lds(iter_spec_kernel, lb)) != hipSuccess || (e = allow_lds(iter_spec_burst_kernel, lb)) != hipSuccess || (e = allow_lds(iter_fix_kernel, lb)) != hipSuccess ||
+      if ((e = allow_lds(iter_spec_burst_kernel, lb)) != hipSuccess || (e = allow_lds(iter_fix_kernel, lb)) != hipSuccess ||
           (e = allow_lds(iter_emit_kernel, lb)) != hipSuccess)
         break;
       // Literal engine: where the DFA does not fit LDS exactly (> 255 states,
       // e.g. alternations of many words) it wins clearly (tools/lit_vs_dfa.py:
       // 16 words 2.29 -> 0.72 ms, 64 words 5.43 -> 2.29 ms per GiB); with a
       // small DFA it depends on the text (English -25 %, DNA +25 %), so the
-      // DFA stays.  RURE_AMD_LIT=1 / 0 forces it on / off.
-      const char *lit_env = getenv("RURE_AMD_LIT");
-      const bool use_lit = f->lit_n && (lit_env ? lit_env[0] == '1' : !f->all);
+      // DFA stays.  Knob lit=1 / 0 forces it on / off.
+      const bool use_lit = f->lit_n && (knob(Knob::Lit) >= 0 ? knob(Knob::Lit) == 1 : !f->all);
       // Shift-And engine for equal-length string sets; RURE_AMD_SA=0 disables
       const bool use_sa = sa_usable(*f);
       const bool sa_tile = sa_tile_ok(b, g);
@@ -2916,7 +2838,7 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
         ktimer_end(st);
         if ((e = hipGetLastError()) != hipSuccess) break;
         if ((e = allow_lds(iter_lex_tail_kernel, lb)) != hipSuccess) break;
-        if (!(getenv("RURE_AMD_LEX_TAIL") && getenv("RURE_AMD_LEX_TAIL")[0] == '0'))
+        if (knob(Knob::LexTail) != 0)
           hipLaunchKernelGGL(iter_lex_tail_kernel, dim3(grid_cap(nunits, 256, cus, 8)), dim3(256), lb, st, b, g, nunits,
                            *f, r, units, slots, counts, dirty);
       } else if (use_sa && sa_tile) {
@@ -2946,12 +2868,9 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
         else
           hipLaunchKernelGGL((iter_spec_lit_kernel<false, false>), lg, dim3(bs), kLitImage, st, b, g, nunits, *f,
                              units, slots, counts, dirty);
-      } else if (!getenv("RURE_AMD_ITER_NESTED")) {
+      } else {
         hipLaunchKernelGGL(iter_spec_burst_kernel, dim3(grid), dim3(bs), iter_lds_bytes(*f, r), st, b, g, nunits, *f,
                            r, units, slots, counts, dirty);
-      } else {
-        hipLaunchKernelGGL(iter_spec_kernel, dim3(grid), dim3(bs), iter_lds_bytes(*f, r), st, b, g, nunits, *f, r,
-                           units, slots, counts, dirty);
       }
       if (!use_lex) ktimer_end(st);
       if ((e = hipGetLastError()) != hipSuccess) break;

@@ -92,37 +92,6 @@ __global__ __launch_bounds__(256) void replace_shift_kernel(BatchDev bt, const u
   }
 }
 
-// One wave per haystack: shift_j for its first k matches and the output length.
-// (Replaced by replace_vals / replace_shift: a haystack's matches were one
-// wave's sequential loop, 0.4 s for the regex-dna strip's 35 M matches.)
-__global__ __launch_bounds__(256) void replace_plan_kernel(BatchDev bt, const uint64_t *counts, const uint64_t *moff,
-                                                           const uint64_t *m, uint64_t limit, uint64_t rep_len,
-                                                           int64_t *shift, uint64_t *out_len) {
-  const uint32_t lane = threadIdx.x & 63;
-  const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
-  for (uint64_t h = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); h < bt.count; h += nw) {
-    uint64_t base, len;
-    hay_of(bt, h, &base, &len);
-    const uint64_t k = counts[h] < limit ? counts[h] : limit;
-    const uint64_t m0 = moff[h];
-    uint64_t carry = 0;  // bytes removed by the matches before this chunk of 64
-    for (uint64_t j0 = 0; j0 < k; j0 += 64) {
-      const uint64_t j = j0 + lane;
-      uint64_t d = 0;
-      if (j < k) d = m[2 * (m0 + j) + 1] - m[2 * (m0 + j)];
-      uint64_t incl = d;  // inclusive wave scan
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint64_t v = __shfl_up(incl, o, 64);
-        if (lane >= (uint32_t)o) incl += v;
-      }
-      if (j < k) shift[m0 + j] = (int64_t)(carry + incl - d) - (int64_t)(j * rep_len);
-      carry += __shfl(incl, 63, 64);
-    }
-    if (lane == 0) out_len[h] = len - carry + k * rep_len;
-  }
-}
-
 // 16 bytes from an arbitrary address, as two aligned 16-byte loads and a
 // funnel shift (the second load is the aligned block holding p[15], so it
 // stays inside the buffer's 16-byte-rounded end whenever p[0..16) does).
@@ -356,91 +325,9 @@ __global__ __launch_bounds__(256) void replace_copy_kernel(CopyCtx c, uint8_t *o
   }
 }
 
-// replace_all over one haystack (the regex-dna strip and substitutions): the
-// window's matches (their replacement starts R and match ends E, one
-// coalesced load per wave) are staged in LDS and every lane searches and
-// reads them there, so a block's dependent global loads are the window
-// index, the staged records and its text; windows with more than 58 matches
-// take the generic path.
-constexpr uint32_t kStageSlots = 64;
-
-__global__ __launch_bounds__(256) void replace_copy1_kernel(CopyCtx c, uint8_t *out) {
-  __shared__ uint64_t sR[4][kStageSlots], sE[4][kStageSlots];
-  const uint64_t total = c.ooff[1] < c.cap ? c.ooff[1] : c.cap;
-  c.total = total;
-  const uint64_t nm = c.moff[1];
-  const uint64_t nwin = (total + kWin - 1) / kWin;
-  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint64_t base, len;
-  hay_of(c.bt, 0, &base, &len);
-  const uint8_t *hay = c.bt.hay + base;
-  const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-  for (uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv; w < nwin; w += nwaves) {
-    const uint64_t lo = c.widx[w], hi = c.widx[w + 1], cnt = hi - lo;
-    const uint64_t p0 = w * kWin + 16 * (uint64_t)lane;
-    if (cnt + 5 > kStageSlots) {  // dense window: the generic per-block path
-      if (p0 < total) {
-        const BlockPlan b = plan_block(c, w, p0);
-        if (b.fast) *(uint4 *)(out + p0) = load16u(c.bt.hay + b.src);
-        else copy_block_slow(c, p0, b, out);
-      }
-      continue;
-    }
-    {  // slot l = match lo - 1 + l (slot 0: the match before the window)
-      const int64_t g = (int64_t)lo - 1 + (int64_t)lane;
-      const bool ok = g >= 0 && (uint64_t)g < nm && (uint64_t)lane < cnt + 5;
-      sR[wv][lane] = ok ? c.G[g] : ~0ull;
-      sE[wv][lane] = ok ? c.m[2 * g + 1] : 0;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (p0 < total) {
-      uint32_t a = 0, bnd = (uint32_t)cnt;  // window matches with R <= p0: slots 1..a
-      while (a < bnd) {
-        const uint32_t mid = (a + bnd) >> 1;
-        if (sR[wv][1 + mid] <= p0) a = mid + 1;
-        else bnd = mid;
-      }
-      const uint64_t jj = lo + a;  // matches passed; the last one is slot a
-      const uint64_t nextR = sR[wv][a + 1];
-      const uint64_t r = jj ? sR[wv][a] : 0;
-      if (p0 + 16 <= total && p0 + 16 <= nextR && (jj == 0 || p0 - r >= c.rep_len)) {
-        const uint64_t src = jj ? sE[wv][a] + (p0 - r - c.rep_len) : p0;
-        *(uint4 *)(out + p0) = load16u(hay + src);
-      } else if (p0 + 16 <= total && sR[wv][a + 4] > p0 + 15) {
-        uint32_t x[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const uint64_t lc = p0 + i;
-          const uint32_t idx = (sR[wv][a + 1] <= lc) + (sR[wv][a + 2] <= lc) + (sR[wv][a + 3] <= lc);
-          uint8_t ch;
-          if (jj == 0 && idx == 0) {
-            ch = hay[lc];
-          } else {
-            const uint64_t rr = sR[wv][a + idx], off = lc - rr;
-            ch = off < c.rep_len ? c.rep[off] : hay[sE[wv][a + idx] + (off - c.rep_len)];
-          }
-          x[i >> 2] |= (uint32_t)ch << (8 * (i & 3));
-        }
-        *(uint4 *)(out + p0) = make_uint4(x[0], x[1], x[2], x[3]);
-      } else {
-        BlockPlan b;
-        b.h = 0;
-        b.jj = jj;
-        b.fast = false;
-        b.src = 0;
-        copy_block_slow(c, p0, b, out);
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  }
-}
-
-// replace_copy1_kernel moves 1 KiB per wave per round, and every wave runs
-// the per-byte path of the blocks that hold a replacement edge: nearly every
+// A copy moving 1 KiB per wave per round (round 4's replace_copy1_kernel,
+// deleted in round 5) ran the per-byte path of the blocks that hold a
+// replacement edge for the whole wave: nearly every
 // 1 KiB window of the regex-dna strip (an edge every ~61 bytes) or of an IUB
 // substitution holds one, so the path ran for the whole wave with a few
 // lanes active — 3.7 G VALU instructions per strip pass, 4.9-5.6 ms
@@ -717,11 +604,6 @@ hipError_t exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, hip
 hipError_t launch_replace_plan(const BatchDev &b, const uint64_t *counts, const uint64_t *moff, const uint64_t *m,
                                uint64_t limit, uint64_t rep_len, int64_t *shift, uint64_t *out_len, hipStream_t st,
                                int cus, uint64_t nm) {
-  if (getenv("RURE_AMD_REPLACE_WAVE")) {  // the previous wave-per-haystack plan (A/B)
-    hipLaunchKernelGGL(replace_plan_kernel, dim3(grid_for_items(b.count, 4, cus)), dim3(256), 0, st, b, counts, moff,
-                       m, limit, rep_len, shift, out_len);
-    return hipGetLastError();
-  }
   int64_t *val = nullptr, *S = nullptr;
   hipError_t e = scratch_malloc((void **)&val, (nm + 1) * 8, st);
   if (e == hipSuccess) e = scratch_malloc((void **)&S, (nm + 1) * 8, st);
@@ -782,11 +664,7 @@ hipError_t launch_replace_copy(const BatchDev &b, const uint64_t *ooff, const ui
     c.total = 0;
     c.cap = cap;
     c.rep = rep;
-    const char *cv = getenv("RURE_AMD_REPLACE_COPY");  // A/B: 1 = one window per round
-    if (b.count == 1 && limit == ~0ull && cv && cv[0] == '1')
-      hipLaunchKernelGGL(replace_copy1_kernel, dim3(grid_for_items((total_hint + 15) / 16, 256, cus)), dim3(256), 0,
-                         st, c, out);
-    else if (b.count == 1 && limit == ~0ull && !(cv && cv[0] == 'g') && total_hint < (1ull << 36)) {
+    if (b.count == 1 && limit == ~0ull && knob(Knob::ReplaceGeneric) != 1 && total_hint < (1ull << 36)) {
       const uint64_t nblk = (total_hint + 15) / 16, rcap = std::max<uint64_t>(4096, nblk / 16);
       uint32_t *rest = nullptr;
       e = scratch_malloc((void **)&rest, rcap * 4 + 256, st);  // (u32 block indices: outputs < 64 GiB)

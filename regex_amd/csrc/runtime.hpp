@@ -192,19 +192,6 @@ struct Staging {
 };
 
 
-struct MultiSet {
-  bool built = false, ok = false;
-  std::vector<rure_set *> owned;   // split groups (RURE_AMD_SET_CHAINS), freed with the set
-  std::vector<rure_set *> parts;
-  std::vector<uint32_t> word, shift;
-  std::vector<CoreSet> cores;
-  std::vector<uint8_t> lds;
-  MultiCoreDev proto{};            // offsets and scalars; pointers filled per device
-  bool quit = false;               // some group can quit: Pike VM fallback passes
-  double coverage = 1.0;           // smallest share of sampled visits in a group's hot cores
-  std::map<int, std::pair<void *, MultiCoreDev>> dev;
-};
-
 // find_iter into internal device buffers: counts (n + 1, last 0), their
 // exclusive sums moff (n + 1) and the match records; reads the total on the
 // host (one sync) and reruns once with an exact buffer if the guess was short.
@@ -301,7 +288,6 @@ struct rure_set {
   // groups' answers concatenated are the set's.  The combined programs are
   // still compiled (size limit, program export).
   std::vector<rure_set *> groups;
-  struct MultiSet *multi = nullptr;   // the groups as one pass (build_multi)
 };
 
 
@@ -386,21 +372,14 @@ bool single_call(rure *re, int mode, const uint8_t *hay, size_t len, size_t star
 uint64_t set_single_call(rure_set *rs, const uint8_t *hay, size_t len, size_t start);
 const FwdDfaDev *literal_engine(int mode, rure *re, DevTables &t, const BatchDev &b);
 int set_batch_word(rure_set *rs, const BatchDev &b, uint64_t *mask, hipStream_t stream);
-int set_chains();
 int device_cus_cached();
-void free_multi(rure_set *rs);
-bool multi_fail(int why);
-bool build_multi_locked(rure_set *rs, MultiSet *m, std::string *err, const std::vector<std::string> *sample,
-                        size_t sample_start);
-std::vector<std::string> batch_sample(const BatchDev &b, hipStream_t st);
-const MultiCoreDev *multi_device(rure_set *rs, std::string *err, const BatchDev &b, hipStream_t st);
-int run_set_multi(rure_set *rs, const BatchDev &b, const MultiCoreDev &f, uint64_t *mask, hipStream_t st);
 int set_batch_group(rure_set *g, const rure_amd_batch *batch, const BatchDev &b, uint64_t *mask, size_t words,
                     size_t w, hipStream_t st);
 hipError_t run_find_iter(rure *re, DevTables *t, const BatchDev &b, const IterOut &o, hipStream_t st,
                          std::string *err, const IterSpan *sp = nullptr);
 hipError_t iter_to_device(rure *re, DevTables *t, const BatchDev &b, hipStream_t st, IterBufs *ib, std::string *err);
-bool build_kmer(rure *const *res, size_t n, std::vector<uint32_t> *bitmap, std::vector<uint16_t> *mask, KmerDev *km);
+bool build_kmer(rure *const *res, size_t n, std::vector<uint32_t> *bitmap, std::vector<uint16_t> *mask,
+                std::vector<uint16_t> *hmask, KmerDev *km);
 bool kmer_device(rure *const *res, size_t n, KmerDev *out);
 void kmer_forget(const rure *re);
 void scratch_release();

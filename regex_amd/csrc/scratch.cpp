@@ -37,7 +37,7 @@ ScratchCache &scratch_cache() {
 }
 size_t scratch_round(size_t n) { return n <= 4096 ? 4096 : (n + 65535) & ~(size_t)65535; }
 size_t scratch_cap(const ScratchCache &c) {
-  if (const char *v = getenv("RURE_AMD_SCRATCH_CAP")) return (size_t)strtoull(v, nullptr, 10);
+  if (knob(Knob::ScratchCap) >= 0) return (size_t)knob(Knob::ScratchCap);
   return std::min(kScratchMaxCap, std::max(kScratchMinCap, 2 * c.peak_live));
 }
 // Returns a block to the driver after its last use.

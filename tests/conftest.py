@@ -20,3 +20,17 @@ def cuda():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch.device("cuda:0")
+
+
+@pytest.fixture
+def knobs():
+    """Debug-only engine overrides for one test (regex_amd.debug's table;
+    names in regex_amd/csrc/host/knobs.hpp): knobs(lit=1) replaces the
+    table, knobs() clears it; cleared again after the test."""
+    import regex_amd as R
+
+    def set_(**kw):
+        R._debug_set(",".join("%s=%d" % (k, int(v)) for k, v in kw.items()) or None)
+
+    yield set_
+    R._debug_set(None)

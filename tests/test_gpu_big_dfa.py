@@ -25,13 +25,8 @@ def _hay(n, L, seed, alphabet):
 
 @pytest.fixture
 def force_big():
-    old = os.environ.get("RURE_AMD_BIG")
-    os.environ["RURE_AMD_BIG"] = "2"
-    yield
-    if old is None:
-        del os.environ["RURE_AMD_BIG"]
-    else:
-        os.environ["RURE_AMD_BIG"] = old
+    with R.debug(big=2):
+        yield
 
 
 @pytest.mark.parametrize("pat", BIG)

@@ -76,54 +76,3 @@ def test_small_sets_words_api(cuda):
         for i, t in enumerate(texts):
             assert _bits(got[i].view(np.uint64), len(pats)) == rs.matches(t), (pats, t)
             assert got[i, 1] == 0
-
-
-@pytest.mark.parametrize("k", [100, 130])
-def test_big_set_one_pass(cuda, k):
-    """RURE_AMD_SET_MULTI=1: the 64-pattern groups run as one pass
-    (set_multi.hip: every group's chain over each haystack read once) and
-    agree with the pass per group (130: one group has no DFA, so the set
-    stays on the per-group passes)."""
-    import os
-    import torch
-    from regex_amd import _native as N
-    buf, offs = log_lines_host(4000, seed=0x0E + k)
-    d = torch.from_numpy(np.concatenate([buf, np.zeros(16, dtype=np.uint8)])).to(cuda)
-    od = torch.from_numpy(offs).to(cuda)
-    os.environ["RURE_AMD_SET_MULTI"] = "1"  # one pass whatever the hot-core coverage
-    try:
-        rs = R.RegexSet(SETS[k])
-        one = rs.matches_batch(d, offsets=od).cpu().numpy()
-        info = rs.multi_info()
-    finally:
-        del os.environ["RURE_AMD_SET_MULTI"]
-    assert info["groups"] == ((k + 63) // 64 if k == 100 else 0), info
-    rs2 = R.RegexSet(SETS[k])
-    per = rs2.matches_batch(d, offsets=od).cpu().numpy()
-    assert rs2.multi_info()["groups"] == 0
-    assert (one == per).all()
-
-
-@pytest.mark.parametrize("chains", [2])
-def test_split_set_chains(cuda, chains):
-    """RURE_AMD_SET_CHAINS: a set of at most 64 patterns split into groups run
-    side by side (the multi-chain A/B on C4's 64 patterns) against the oracle."""
-    import os
-    import torch
-    from regex_amd import _native as N
-    from regex_amd.workloads import C4_PATTERNS
-    os.environ["RURE_AMD_SET_CHAINS"] = str(chains)
-    os.environ["RURE_AMD_SET_MULTI"] = "1"
-    try:
-        rs = R.RegexSet(C4_PATTERNS)
-        o = OracleRegex(rs)
-        buf, offs = log_lines_host(3000, seed=0x5C + chains)
-        d = torch.from_numpy(np.concatenate([buf, np.zeros(16, dtype=np.uint8)])).to(cuda)
-        got = rs.matches_batch(d, offsets=torch.from_numpy(offs).to(cuda)).cpu().numpy().reshape(3000, -1)
-        assert rs.multi_info()["groups"] == chains
-    finally:
-        del os.environ["RURE_AMD_SET_CHAINS"]
-        del os.environ["RURE_AMD_SET_MULTI"]
-    for i in range(3000):
-        t = bytes(buf[offs[i]:offs[i + 1]])
-        assert _bits(got[i].view(np.uint64), len(C4_PATTERNS)) == o.matches(t), i

@@ -148,7 +148,7 @@ def _lex_text(seed, n, nonascii):
 @pytest.mark.parametrize("nonascii", [False, True])
 def test_find_iter_lexer(cuda, pat, nonascii):
     """The lexer engine (iter_spec_lex_tile_kernel + tail pass) against the
-    oracle and against the burst kernel (RURE_AMD_LEX=0): one long haystack
+    oracle and against the burst kernel (debug knob lex=0): one long haystack
     (many units) and a fixed-stride batch of several haystacks."""
     import os
     re = R.Regex(pat)
@@ -159,11 +159,8 @@ def test_find_iter_lexer(cuda, pat, nonascii):
     exp = o.find_iter(text)
     counts, m = re.find_iter_batch(d, stride=len(text), length=len(text), count=1)
     assert as_pairs(m) == exp
-    os.environ["RURE_AMD_LEX"] = "0"
-    try:
+    with R.debug(lex=0):
         _, m0 = re.find_iter_batch(d, stride=len(text), length=len(text), count=1)
-    finally:
-        del os.environ["RURE_AMD_LEX"]
     assert as_pairs(m0) == exp
     n, L = 6, 60000
     counts, m = re.find_iter_batch(d, stride=L, length=L - 5, count=n)
@@ -176,11 +173,10 @@ def test_find_iter_lexer(cuda, pat, nonascii):
 
 
 @pytest.mark.parametrize("pat", LEX_PATTERNS)
-@pytest.mark.parametrize("env", [("RURE_AMD_LEX4", "0"), ("RURE_AMD_COPY_GROUP", "0")])
-def test_find_iter_lexer_variants(cuda, pat, env):
-    """The byte-per-step lexer (RURE_AMD_LEX4=0) and the output-ordered copy
-    (RURE_AMD_COPY_GROUP=0) give the default path's matches; the default
-    (four bytes per step, group copy) is checked against the oracle, with a
+def test_find_iter_lexer_variants(cuda, pat):
+    """The byte-per-step lexer (debug knob lex4=0: the fallback when the
+    four-byte table does not build) gives the default path's matches; the
+    default (four bytes per step) is checked against the oracle, with a
     capacity that cuts the output inside a unit."""
     import os
     re = R.Regex(pat)
@@ -193,9 +189,7 @@ def test_find_iter_lexer_variants(cuda, pat, env):
     if len(exp) > 10:
         _, mc = re.find_iter_batch(d, stride=len(text), length=len(text), count=1, capacity=len(exp) // 2 + 3)
         assert as_pairs(mc)[:len(exp) // 2 + 3] == exp[:len(exp) // 2 + 3]
-    os.environ[env[0]] = env[1]
-    try:
-        _, m1 = re.find_iter_batch(d, stride=len(text), length=len(text), count=1)
-    finally:
-        del os.environ[env[0]]
+    with R.debug(lex4=0):
+        re1 = R.Regex(pat)  # (a fresh regex: device tables keep the knobs of their first use)
+        _, m1 = re1.find_iter_batch(d, stride=len(text), length=len(text), count=1)
     assert as_pairs(m1) == exp

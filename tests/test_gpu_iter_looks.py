@@ -8,7 +8,7 @@ iteration must reproduce: units whose first reverse scan reaches their start
 (repaired from the true entry), reverse NoMatches that end the iteration
 (\\B at a unit start), and Unicode word boundaries whose DFA quits on
 non-ASCII bytes (the batch then goes to the wave path: last_fwd_path -13).
-RURE_AMD_ITER_CHUNK forces small units (many boundaries)."""
+The debug knob iter_chunk forces small units (many boundaries)."""
 import os
 import random
 import zlib
@@ -45,12 +45,9 @@ def _dev(buf, cuda):
 
 
 def _run(re, buf, L, count, cuda, chunk):
-    os.environ["RURE_AMD_ITER_CHUNK"] = str(chunk)
-    try:
+    with R.debug(iter_chunk=chunk):
         counts, m = re.find_iter_batch(_dev(buf, cuda), stride=L, length=L, count=count)
         return counts.cpu().numpy().tolist(), [tuple(x) for x in m.cpu().numpy().tolist()], N.rure_amd_last_fwd_path()
-    finally:
-        del os.environ["RURE_AMD_ITER_CHUNK"]
 
 
 def _check(re, buf, L, count, cuda, chunk):
@@ -104,20 +101,6 @@ def test_find_iter_looks_long_sherlock(cuda, pat):
     exp = OracleRegex(re).find_iter(text)
     assert [tuple(x) for x in m.cpu().numpy().tolist()] == exp
     del torch
-
-
-@pytest.mark.parametrize("pat", ASCII_PATTERNS[:8])
-def test_find_iter_looks_nested_kernel(cuda, pat):
-    """The nested-loop speculative kernel (RURE_AMD_ITER_NESTED) follows the
-    same rules as the burst one."""
-    re = R.Regex(pat)
-    L = 6000
-    buf = _text(zlib.crc32(pat.encode()) + 9, L * 2, False)
-    os.environ["RURE_AMD_ITER_NESTED"] = "1"
-    try:
-        assert _check(re, buf, L, 2, cuda, 16) in (-12, -14), pat
-    finally:
-        del os.environ["RURE_AMD_ITER_NESTED"]
 
 
 @pytest.mark.parametrize("pat", stdlib_looks_fixtures()[0]["patterns"])

@@ -3,8 +3,8 @@ rows are built when a scan first needs them, as the reference's lazy DFA
 builds a state when a search first steps into it (dfa.rs:910-1048); lanes
 that meet a missing row park, the host builds the rows and the next round
 resumes them.  `(?:a|b)*a(?:a|b){20}` has ~2^21 states, past the eager
-budgets (kBigDfaRawStates), so it used to run on the Pike VM; RURE_AMD_LAZY=1
-with RURE_AMD_LAZY_ROWS=1 (one row built ahead per round) forces ordinary
+budgets (kBigDfaRawStates), so it used to run on the Pike VM; debug knobs
+lazy=1, lazy_rows=1 (one row built ahead per round) force ordinary
 regexes through many parking rounds.  find / is_match / shortest_match
 against the oracle; rure_amd_last_fwd_path() == -10 asserts the lazy kernel
 answered."""
@@ -21,22 +21,6 @@ from golden_data import corpus
 pytestmark = pytest.mark.gpu
 
 HUGE = r"(?:a|b)*a(?:a|b){20}"
-
-
-class _Env:
-    def __init__(self, **kv):
-        self.kv = kv
-
-    def __enter__(self):
-        self.old = {k: os.environ.get(k) for k in self.kv}
-        os.environ.update({k: str(v) for k, v in self.kv.items()})
-
-    def __exit__(self, *a):
-        for k, v in self.old.items():
-            if v is None:
-                del os.environ[k]
-            else:
-                os.environ[k] = v
 
 
 def _mixed(n, L, seed):
@@ -80,7 +64,7 @@ def _check(cuda, pat, raw, n, L, start=0):
 def test_lazy_huge(cuda, start):
     """past the eager budgets: the lazy kernel, not the Pike VM"""
     n, L = 400, 200
-    with _Env(RURE_AMD_BIG="2"):
+    with R.debug(big=2):
         hits = _check(cuda, HUGE, _mixed(n, L, 5 + start), n, L, start)
     assert 0 < hits < n
 
@@ -91,7 +75,7 @@ def test_lazy_forced_rounds(cuda, pat):
     """one row built ahead per round: every lane parks many times"""
     n, L = 300, 150
     raw = _mixed(n, L, len(pat))
-    with _Env(RURE_AMD_LAZY="1", RURE_AMD_LAZY_ROWS="1"):
+    with R.debug(lazy=1, lazy_rows=1):
         _check(cuda, pat, raw, n, L, 0)
 
 
@@ -104,7 +88,7 @@ def test_lazy_offsets(cuda):
     cuts = np.sort(rng.choice(len(text), size=500, replace=False))
     offs = np.concatenate([[0], cuts, [len(text)]]).astype(np.int64)
     d = torch.from_numpy(np.frombuffer(text + b"\0" * 16, dtype=np.uint8).copy()).to(cuda)
-    with _Env(RURE_AMD_BIG="2"):
+    with R.debug(big=2):
         got = re.find_batch(d, offsets=torch.from_numpy(offs).to(cuda)).cpu().numpy()
         assert N.rure_amd_last_fwd_path() == -10
     for i in range(len(offs) - 1):

@@ -8,7 +8,7 @@ one-line-ahead prefetch meet: empty lines, 1-byte lines, lines inside one
 at the end of the batch, lines carrying Unicode digits / word characters and
 invalid UTF-8 (the sentinel redo on the global table), and searches from
 start > 0 (look-behind from the byte before start).  rure_amd_last_fwd_path()
-== -8 asserts the line kernel ran; RURE_AMD_LINES=0 gives the previous
+== -8 asserts the line kernel ran; debug knob lines=0 gives the previous
 one-lane-per-haystack kernel, checked for the same answers.
 """
 import os
@@ -91,12 +91,9 @@ def test_lines_parity(cuda, pat):
     buf, offs = _lines(30_000, 0x11 + len(pat))
     path, got = _check(cuda, re, o, buf, offs, 0)
     # the previous per-lane kernel gives the same answers (A/B switch)
-    os.environ["RURE_AMD_LINES"] = "0"
-    try:
-        import torch
+    import torch
+    with R.debug(lines=0):
         got0 = re.find_batch(torch.from_numpy(buf).to(cuda), offsets=torch.from_numpy(offs).to(cuda)).cpu().numpy()
-    finally:
-        del os.environ["RURE_AMD_LINES"]
     assert np.array_equal(got, got0)
 
 

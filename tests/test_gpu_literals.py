@@ -19,10 +19,10 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(autouse=True)
-def literal_engine(monkeypatch):
+def literal_engine(knobs):
     # force the literal engine (by default it runs only where the DFA does not
     # fit LDS exactly)
-    monkeypatch.setenv("RURE_AMD_LIT", "1")
+    knobs(lit=1)
 
 PATTERNS = [r"agggtaaa|tttaccct", r"[cgt]gggtaaa|tttaccc[acg]", r"a|ab", r"ab|a", r"aa", r"e", r"(?i)holm",
             r"Sherlock|Holmes|Watson", r"foo(bar)?", r"x(a|ab)(c|bcd)", r"[0-3]{2}", r"abc|abd|ab", r"é"]
@@ -97,10 +97,10 @@ def test_regexdna_variants_literal_engine(cuda):
         assert pairs(m) == OracleRegex(re).find_iter(big), v["re"]
 
 
-def test_default_dispatch_large_word_set(cuda, monkeypatch):
+def test_default_dispatch_large_word_set(cuda, knobs):
     """A 40-word alternation (DFA > 255 states): the literal engine is the
     default engine here; same matches as the oracle and as the DFA."""
-    monkeypatch.delenv("RURE_AMD_LIT", raising=False)
+    knobs()
     text = corpus("sherlock")
     words = sorted(set(w for w in text.decode("latin-1").split() if w.isalpha() and 6 <= len(w) <= 10))[:40]
     re = R.Regex("|".join(words))
@@ -108,7 +108,7 @@ def test_default_dispatch_large_word_set(cuda, monkeypatch):
     exp = OracleRegex(re).find_iter(text)
     c, m = re.find_iter_batch(dev(text, cuda), stride=len(text), length=len(text), count=1)
     assert pairs(m) == exp
-    monkeypatch.setenv("RURE_AMD_LIT", "0")
+    knobs(lit=0)
     c, m = re.find_iter_batch(dev(text, cuda), stride=len(text), length=len(text), count=1)
     assert pairs(m) == exp
 
@@ -220,12 +220,12 @@ def test_literal_find_batch_strided(cuda, pat):
 
 
 @pytest.mark.parametrize("nwords", [3, 64])
-def test_literal_find_default_dispatch(cuda, monkeypatch, nwords):
-    """Without RURE_AMD_LIT a set of at most 8 literals takes the literal
-    engine and a larger one the DFA (measured faster there); RURE_AMD_LIT=0
+def test_literal_find_default_dispatch(cuda, knobs, nwords):
+    """Without the lit knob a set of at most 8 literals takes the literal
+    engine and a larger one the DFA (measured faster there); lit=0
     (the DFA) gives the same answers, and both equal the oracle."""
     from regex_amd import _native as NN
-    monkeypatch.delenv("RURE_AMD_LIT", raising=False)
+    knobs()
     text = corpus("sherlock")
     if nwords == 3:
         pat = r"Sherlock|Holmes|Watson"
@@ -244,7 +244,7 @@ def test_literal_find_default_dispatch(cuda, monkeypatch, nwords):
     assert (path == -3) == (nwords <= 8), path
     assert NN.rure_amd_last_fwd_path() == path
     assert len(re.literals()) == nwords
-    monkeypatch.setenv("RURE_AMD_LIT", "0")
+    knobs(lit=0)
     ref = re.find_batch(d, stride=L, length=L, count=n).cpu().numpy()
     assert NN.rure_amd_last_fwd_path() != -3
     assert np.array_equal(got, ref)

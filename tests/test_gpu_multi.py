@@ -99,13 +99,13 @@ def test_multi_counts_known_answers(cuda, k):
 
 
 @pytest.mark.parametrize("engine", ["kmer", "shiftand"])
-def test_multi_engines_mixed_bytes(cuda, monkeypatch, engine):
+def test_multi_engines_mixed_bytes(cuda, knobs, engine):
     """The fused pass with the k-mer probe engine (default for the regex-dna
-    variants) and with the Shift-And words (RURE_AMD_KMER=0): text with
+    variants) and with the Shift-And words (knob kmer=0): text with
     uppercase ACGT, IUB codes, 'n', bytes >= 0x80 and newlines between the
     motifs — every regex's output equals its own single pass and the oracle."""
     if engine == "shiftand":
-        monkeypatch.setenv("RURE_AMD_KMER", "0")
+        knobs(kmer=0)
     rng = np.random.default_rng(11)
     motifs = [b"agggtaaa", b"tttaccct", b"cgggtaaa", b"tttacccg", b"aggggtaa", b"ggtaaaTT", b"AGGGTAAA"]
     noise = np.frombuffer(b"acgtacgtACGTnNBDHKMRSVWY\n\x80\xff\xc3\xa9", dtype=np.uint8)

@@ -1,11 +1,9 @@
-"""GPU parity of the start-state prefix skip with the 2-3 byte filter
-(FwdDfaDev::pfx_depth; dfa.rs:700-711 prefix_at restated as a burst filter)
-on the chunked long scan (last_fwd_path -4): find / is_match / shortest
-over long haystacks against the oracle, with the only occurrence planted
-across 128-byte burst edges (a prefix whose first byte ends a burst must not
-be skipped), case-folded prefix sets and sets that stop the filter at depth
-1 or 2.  The deeper filter is opt-in (RURE_AMD_PREFIX=3); both filters
-run here."""
+"""GPU parity of the start-state prefix skip (FwdDfaDev::pfx_*; dfa.rs:700-711
+prefix_at restated as a burst filter) on the chunked long scan
+(last_fwd_path -4): find / is_match / shortest over long haystacks against
+the oracle, with the only occurrence planted across 128-byte burst edges (a
+prefix whose first byte ends a burst must not be skipped) and case-folded
+prefix sets; with the skip and without it (debug knob prefix=0)."""
 import numpy as np
 import pytest
 
@@ -28,16 +26,11 @@ def _filler(n):
     return base[:n]
 
 
-@pytest.fixture(params=["3", None])
-def prefix_mode(request):
-    import os
-    old = os.environ.pop("RURE_AMD_PREFIX", None)
-    if request.param:
-        os.environ["RURE_AMD_PREFIX"] = request.param
+@pytest.fixture(params=[0, None])
+def prefix_mode(request, knobs):
+    if request.param is not None:
+        knobs(prefix=request.param)
     yield request.param
-    os.environ.pop("RURE_AMD_PREFIX", None)
-    if old is not None:
-        os.environ["RURE_AMD_PREFIX"] = old
 
 
 @pytest.mark.parametrize("pat,occ", CASES)

@@ -7,8 +7,8 @@ self-overlapping strings (`aa` in runs of `a`, `agggtaaa` after `agg`),
 strings merged into class sequences (`(?i)holm`, `[0-3]{2}`), multi-byte
 UTF-8 strings, and matches across unit cuts.  Each case runs through the
 coalesced tile kernel (the default for fixed-stride batches of whole
-128-byte-line units), the per-lane kernel (RURE_AMD_SA=2) and the DFA burst
-kernel (RURE_AMD_SA=0)."""
+128-byte-line units), the per-lane kernel (knob sa=2) and the DFA burst
+kernel (sa=0)."""
 import random
 import zlib
 
@@ -48,19 +48,19 @@ def texts(pat):
     yield b"".join(rng.choice(alpha) for _ in range(60000))
 
 
-def both_engines(monkeypatch):
+def both_engines(knobs):
     # default (coalesced tile kernel where the batch allows it), the per-lane
-    # Shift-And kernel (RURE_AMD_SA=2), the DFA burst kernel (RURE_AMD_SA=0)
-    for v in (None, "2", "0"):
+    # Shift-And kernel (knob sa=2), the DFA burst kernel (sa=0)
+    for v in (None, 2, 0):
         if v is None:
-            monkeypatch.delenv("RURE_AMD_SA", raising=False)
+            knobs()
         else:
-            monkeypatch.setenv("RURE_AMD_SA", v)
+            knobs(sa=v)
         yield v
 
 
 @pytest.mark.parametrize("pat", PATTERNS)
-def test_shiftand_find_iter(cuda, pat, monkeypatch):
+def test_shiftand_find_iter(cuda, pat, knobs):
     re = R.Regex(pat)
     lits = re.literals()
     assert lits and len(set(len(x) for x in lits)) == 1, pat
@@ -68,7 +68,7 @@ def test_shiftand_find_iter(cuda, pat, monkeypatch):
     for t in texts(pat):
         exp = o.find_iter(t)
         d = dev(t, cuda)
-        for _ in both_engines(monkeypatch):
+        for _ in both_engines(knobs):
             c, m = re.find_iter_batch(d, stride=len(t), length=len(t), count=1)
             assert int(c[0]) == len(exp) and pairs(m) == exp, (pat, len(t))
 
@@ -140,7 +140,7 @@ def test_regexdna_variants_shiftand(cuda):
 
 
 @pytest.mark.parametrize("L", [70001, 70003, 4099])
-def test_shiftand_haystack_end(cuda, L, monkeypatch):
+def test_shiftand_haystack_end(cuda, L, knobs):
     """Odd-length haystacks followed, inside their stride, by bytes that would
     complete a match straddling the end: the kernels read whole aligned
     16-byte blocks (include/rure_amd.h: the buffer must be readable to its
@@ -155,7 +155,7 @@ def test_shiftand_haystack_end(cuda, L, monkeypatch):
     d = torch.from_numpy(np.frombuffer(bytes(buf), dtype=np.uint8).copy()).to(cuda)
     re = R.Regex(r"agggtaaa|tttaccct")
     o = OracleRegex(re)
-    for _ in both_engines(monkeypatch):
+    for _ in both_engines(knobs):
         c, m = re.find_iter_batch(d, stride=S, length=L, count=n)
         got, k = pairs(m), 0
         for i in range(n):

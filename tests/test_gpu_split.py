@@ -4,7 +4,7 @@ split into units of >= 128 B scanned with the cut-bounded search
 is_match takes it (find / shortest_match units would scan on until the DFA
 dies: a never-dying pattern costs every unit the rest of its haystack);
 is_match / find / shortest_match must equal the oracle and the unsplit
-kernels (RURE_AMD_SPLIT=0) bit for bit, with matches crossing every unit cut,
+kernels (debug knob split=0) bit for bit, with matches crossing every unit cut,
 Unicode and invalid UTF-8 bytes, start > 0 and ragged strides."""
 import numpy as np
 import pytest
@@ -31,7 +31,7 @@ def _buf(n, L, S, seed):
 
 @pytest.mark.parametrize("pat", PATS)
 @pytest.mark.parametrize("shape", [(1024, 1024, 1024), (300, 1000, 1008), (64, 5000, 5008)])
-def test_split_small_batch(cuda, monkeypatch, pat, shape):
+def test_split_small_batch(cuda, knobs, pat, shape):
     import torch
     n, L, S = shape
     buf = _buf(n, L, S, 0x5151 + n)
@@ -44,11 +44,11 @@ def test_split_small_batch(cuda, monkeypatch, pat, shape):
         got_m = re.is_match_batch(d, stride=S, length=L, count=n, start=start).cpu().numpy()
         if pat in SPLIT_PATS:  # only is_match takes the split (a find unit scans until the DFA dies)
             assert N.rure_amd_last_fwd_path() == -4, (pat, shape)
-        monkeypatch.setenv("RURE_AMD_SPLIT", "0")
+        knobs(split=0)
         ref_f = re.find_batch(d, stride=S, length=L, count=n, start=start).cpu().numpy()
         ref_m = re.is_match_batch(d, stride=S, length=L, count=n, start=start).cpu().numpy()
         ref_s = re.shortest_match_batch(d, stride=S, length=L, count=n, start=start).cpu().numpy()
-        monkeypatch.delenv("RURE_AMD_SPLIT")
+        knobs()
         assert np.array_equal(got_f, ref_f), (pat, shape, start)
         assert np.array_equal(got_m, ref_m), (pat, shape, start)
         assert np.array_equal(got_s, ref_s), (pat, shape, start)

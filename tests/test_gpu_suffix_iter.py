@@ -70,12 +70,9 @@ def test_suffix_iter_long(cuda, pat):
 @pytest.mark.parametrize("start", [0, 7])
 def test_suffix_iter_small_units(cuda, pat, start):
     """units of 128 bytes: occurrences and slices cross many unit edges"""
-    os.environ["RURE_AMD_SUFFIX_ITER"] = "2"
-    try:
+    with R.debug(suffix_iter=2):
         for seed in range(3):
             _check(cuda, pat, 3, 9_000 + 177 * seed, 50 + seed, start)
-    finally:
-        del os.environ["RURE_AMD_SUFFIX_ITER"]
 
 
 def test_suffix_iter_quit_falls_back(cuda):
@@ -102,8 +99,7 @@ def test_suffix_iter_quit_falls_back(cuda):
 
 def test_suffix_iter_capacity_and_empty(cuda):
     import torch
-    os.environ["RURE_AMD_SUFFIX_ITER"] = "2"
-    try:
+    with R.debug(suffix_iter=2):
         n = _check(cuda, PATS[0], 2, 20_000, 9)
         _check(cuda, PATS[0], 2, 20_000, 9, capacity=n // 3)
         # no occurrence at all
@@ -112,5 +108,3 @@ def test_suffix_iter_capacity_and_empty(cuda):
         d = torch.from_numpy(np.frombuffer(text + b"\0" * 16, dtype=np.uint8).copy()).to(cuda)
         counts, m = re.find_iter_batch(d, stride=5000, length=5000, count=1)
         assert counts.cpu().numpy().tolist() == [0] and m.shape[0] == 0
-    finally:
-        del os.environ["RURE_AMD_SUFFIX_ITER"]

@@ -70,14 +70,11 @@ def test_suffix_long(cuda, pat):
 
 @pytest.mark.parametrize("pat", [r"[a-z]+ing", r"\w+@gmail\.com"])
 def test_suffix_long_small_units(cuda, pat):
-    """units of 128 B (RURE_AMD_SUFFIX_LONG=2): occurrences and slices cross
-    many unit edges"""
-    os.environ["RURE_AMD_SUFFIX_LONG"] = "2"
-    try:
+    """units of 128 B (debug knob suffix_long=2): occurrences and slices
+    cross many unit edges"""
+    with R.debug(suffix_long=2):
         for seed in range(4):
             _check(cuda, pat, 3, 20_000 + 333 * seed, 40 + seed)
-    finally:
-        del os.environ["RURE_AMD_SUFFIX_LONG"]
 
 
 def test_suffix_long_no_occurrence(cuda):

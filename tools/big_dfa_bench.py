@@ -1,5 +1,5 @@
 """Batched find over a >65535-state automaton: the big-DFA kernel
-(big_dfa.hip) against the Pike VM (RURE_AMD_BIG=0), GB/s.
+(big_dfa.hip) against the Pike VM (knob big=0), GB/s.
 python tools/big_dfa_bench.py [pattern] [count] [length]"""
 import os
 import sys
@@ -26,7 +26,7 @@ print("compile+build %.2f s" % (time.time() - t0), info, flush=True)
 out = torch.empty((n, 2), dtype=torch.int64, device=dev)
 res = {}
 for mode in ("2", "0"):
-    os.environ["RURE_AMD_BIG"] = mode
+    R._debug_set("big=%s" % (mode))
     re.find_batch(buf, stride=L, length=L, count=n, out=out)
     torch.cuda.synchronize()
     reps = 3 if mode == "2" else 1

@@ -1,6 +1,6 @@
 """Tuning sweep for the chunked find_iter (C3 passes): times the strip pass
 and the 9 variant passes (HIP events on the launch stream) under each
-RURE_AMD_ITER_BS / RURE_AMD_ITER_LANES setting given on the command line,
+iter_bs / iter_lanes debug-knob setting given on the command line,
 e.g.  python tools/iter_sweep.py 256:1024 1024:2048 256:1024:NESTED"""
 import ctypes
 import json
@@ -47,13 +47,7 @@ def run(re_, buf, L):
 for cfg in sys.argv[1:] or ["1024:2048"]:
     parts = cfg.split(":")
     bs, lanes = parts[0], parts[1]
-    os.environ["RURE_AMD_ITER_BS"] = bs
-    os.environ["RURE_AMD_ITER_LANES"] = lanes
-    for flag in parts[2:]:  # e.g. PREFETCH -> RURE_AMD_ITER_PREFETCH=1
-        os.environ["RURE_AMD_ITER_" + flag] = "1"
-    for k in ("PREFETCH", "NESTED"):
-        if k not in parts[2:]:
-            os.environ.pop("RURE_AMD_ITER_" + k, None)
+    R._debug_set("iter_bs=%s,iter_lanes=%s" % (bs, lanes))
     res = {}
     for name, re_, buf, L in passes:
         for _ in range(2):

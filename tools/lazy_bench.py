@@ -1,9 +1,9 @@
-"""The on-demand DFA (RURE_AMD_LAZY, host LazyDfa + lazy_dfa_kernel) on a
+"""The on-demand DFA (debug knob lazy, host LazyDfa + lazy_dfa_kernel) on a
 regex past the eager budgets, `(?:a|b)*a(?:a|b){20}`, over a batch of
 sherlock lines mixed with a/b runs: first call (the eager attempt that
 fails, then the rounds that build the rows the text needs) and steady state
 (every row the text visits built: one round), against the Pike VM
-(RURE_AMD_LAZY=0).  Prints one JSON line per mode.
+(lazy=0; its path is -16, the Pike VM alone).  Prints one JSON line per mode.
 usage: python tools/lazy_bench.py [haystacks] [length] [sparse|dense]"""
 import json
 import os
@@ -57,8 +57,7 @@ def timed(fn, reps):
 
 # the default dispatch's first call: the eager big automaton is attempted
 # first (kBigDfaRawStates) and fails, then the on-demand DFA runs
-for k in ("RURE_AMD_LAZY", "RURE_AMD_BIG"):
-    os.environ.pop(k, None)
+R._debug_set(None)
 re0 = R.Regex(pat)
 t0 = time.perf_counter()
 re0.is_match_batch(d, stride=L, length=L, count=n)
@@ -69,9 +68,8 @@ for mode in ("find", "is_match"):
     res = {}
     for lazy in ("1", "0"):
         # "1": forced on-demand DFA (no eager attempt first); "0": Pike VM
-        # (the eager big automaton does not build: RURE_AMD_BIG=0 skips it)
-        os.environ["RURE_AMD_LAZY"] = lazy
-        os.environ["RURE_AMD_BIG"] = "0"
+        # (the eager big automaton does not build: big=0 skips it)
+        R._debug_set("lazy=%s,big=0" % lazy)
         re = R.Regex(pat)
         f = (lambda: re.find_batch(d, stride=L, length=L, count=n)) if mode == "find" else \
             (lambda: re.is_match_batch(d, stride=L, length=L, count=n))

@@ -1,7 +1,7 @@
 """Literal engine vs DFA for batched find / is_match (lit_find_kernel vs the
 DFA kernels): sherlock text cut into 262144 haystacks of 2000 B (~0.5 GB),
 kernel times (HIP events on the launch stream) per pattern with
-RURE_AMD_LIT=0 / 1, and whether the answers agree."""
+knob lit=0 / 1, and whether the answers agree."""
 import json
 import os
 import sys
@@ -42,7 +42,7 @@ for name, pat in pats.items():
     res = {"pattern": name, "literals": len(re.literals() or []), "dfa_states": info and info["states"]}
     outs = {}
     for mode in ("0", "1"):
-        os.environ["RURE_AMD_LIT"] = mode
+        R._debug_set("lit=%s" % (mode))
         for op in ("find", "is_match"):
             fn = re.find_batch if op == "find" else re.is_match_batch
             o = fn(buf, stride=L, length=L, count=n)

@@ -1,6 +1,6 @@
 """Literal engine vs DFA for find_iter over one long haystack (sherlock
 replicated to ~1 GiB): prints per-pattern kernel times (HIP events) for the
-default dispatch and with RURE_AMD_LIT=1, plus DFA sizes."""
+default dispatch and with knob lit=1, plus DFA sizes."""
 import ctypes
 import json
 import os
@@ -42,9 +42,9 @@ for name, pat in pats.items():
            "hot": info and info["hot"]}
     for mode in ("dfa", "lit"):
         if mode == "lit":
-            os.environ["RURE_AMD_LIT"] = "1"
+            R._debug_set("lit=%s" % ("1"))
         else:
-            os.environ.pop("RURE_AMD_LIT", None)
+            R._debug_set(None)
 
         def run():
             rc = NN.rure_amd_find_iter_span(re._re, ctypes.c_void_p(buf.data_ptr()), L, 0, L, None,

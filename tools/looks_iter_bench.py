@@ -1,7 +1,7 @@
 """find_iter of look-around regexes over 1 GiB of sherlock text (made ASCII,
 so Unicode \\b's DFA never quits): the chunked path (iter_scan.hip with
 FwdDfaDev::looks, last_fwd_path -12) against the wave path
-(RURE_AMD_ITER_LOOKS=0) on a 16 MiB prefix, outputs compared there.
+(knob iter_looks=0) on a 16 MiB prefix, outputs compared there.
 --ragged: the same text as a ragged batch of its lines (one unit per line)
 against the wave path, outputs compared.
 usage: python tools/looks_iter_bench.py [--no-wave] [--ragged] [pattern ...]"""
@@ -64,11 +64,11 @@ if "--ragged" in sys.argv:
         re = R.Regex(pat)
         ms, m = run(re)
         path = N.rure_amd_last_fwd_path()
-        os.environ["RURE_AMD_ITER_LOOKS"] = "0"
+        R._debug_set("iter_looks=%s" % ("0"))
         try:
             wms, wm = run(re)
         finally:
-            del os.environ["RURE_AMD_ITER_LOOKS"]
+            R._debug_set(None)
         print(json.dumps({"pattern": pat, "ragged_lines": int(offs.numel() - 1), "bytes": len(small), "path": path,
                           "matches": int(m.shape[0]), "ms": round(ms, 3), "wave_ms": round(wms, 3),
                           "equal": bool(torch.equal(m, wm))}), flush=True)
@@ -82,11 +82,11 @@ for pat in args or pats:
                           "GBps": round(L / ms / 1e6, 1)}), flush=True)
         continue
     _, _, m_small = timed(re, SMALL, 1)
-    os.environ["RURE_AMD_ITER_LOOKS"] = "0"
+    R._debug_set("iter_looks=%s" % ("0"))
     try:
         wms, wcap, m_wave = timed(re, SMALL, 1)
     finally:
-        del os.environ["RURE_AMD_ITER_LOOKS"]
+        R._debug_set(None)
     same = bool(torch.equal(m_small, m_wave))
     print(json.dumps({"pattern": pat, "path": path, "matches": cap, "ms": round(ms, 3),
                       "GBps": round(L / ms / 1e6, 1), "wave_GBps_16MiB": round(SMALL / wms / 1e6, 3),

@@ -1,5 +1,5 @@
 """A/B of the start-state prefix skip (dfa.rs:700-711; FwdDfaDev::pfx_*,
-RURE_AMD_PREFIX=0 turns it off, unset: the first-byte filter, =3: the
+knob prefix=0 turns it off, unset: the first-byte filter, =3: the
 2-3 byte filter, pfx_depth) on sherlock text: kernel time of batched
 find with and without the skip (HIP events on the launch stream), outputs
 compared.  Shapes: ragged line batches (dfa_fwd_kernel, one lane per line),
@@ -51,9 +51,9 @@ def main():
         out = {}
         for mode in ("0", "1", "2"):
             if mode == "1":
-                os.environ.pop("RURE_AMD_PREFIX", None)
+                R._debug_set(None)
             else:
-                os.environ["RURE_AMD_PREFIX"] = "3" if mode == "2" else mode
+                R._debug_set("prefix=%s" % ("3" if mode == "2" else mode))
             re = R.Regex(pat)
             r_lines = re.find_batch(hay, offsets=offs)
             t_lines = timed(lambda: re.find_batch(hay, offsets=offs, out=r_lines))

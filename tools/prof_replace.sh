@@ -1,7 +1,7 @@
 #!/bin/bash
 # Kernel trace of tools/replace_bench.py (strip + one IUB substitution on the
 # 2 GiB regex-dna stream): per-kernel times under gpurun_out/<tag>/.
-# usage: tools/prof_replace.sh <tag>   (env passes through: RURE_AMD_REPLACE_COPY=1 ...)
+# usage: tools/prof_replace.sh <tag>   (env passes through: RURE_AMD_DEBUG=replace_generic=1 ...)
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 TAG=${1:-repprof}
 OUT=$R/gpurun_out/$TAG

@@ -2,7 +2,7 @@
 replicated to ~1 GiB and cut at its newlines (23.5 M lines), batched find /
 is_match per line through the offsets API.  Kernel time by HIP events on the
 launch stream for the line kernel (dfa_line_kernel, default) and the previous
-one-lane-per-haystack kernel (RURE_AMD_LINES=0); outputs compared.  One JSON
+one-lane-per-haystack kernel (knob lines=0); outputs compared.  One JSON
 line per (pattern, mode)."""
 import json
 import os
@@ -48,14 +48,14 @@ def main():
         re = R.Regex(pat)
         res = {}
         for lines in ("1", "0"):
-            os.environ["RURE_AMD_LINES"] = lines
+            R._debug_set("lines=%s" % (lines))
             for mode in ("find", "is_match"):
                 fn = re.find_batch if mode == "find" else re.is_match_batch
                 r = fn(hay, offsets=offs)
                 path = N.rure_amd_last_fwd_path()
                 t = timed(lambda: fn(hay, offsets=offs, out=r))
                 res[(lines, mode)] = (t, r.cpu().numpy(), path)
-        os.environ.pop("RURE_AMD_LINES", None)
+        R._debug_set(None)
         for mode in ("find", "is_match"):
             t1, r1, p1 = res[("1", mode)]
             t0, r0, p0 = res[("0", mode)]

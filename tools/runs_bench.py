@@ -1,6 +1,6 @@
 """find_iter of C+ regexes (the run engine, run_iter.hip, last_fwd_path
 -19) over 1 GiB of sherlock text made ASCII, against the DFA paths
-(RURE_AMD_RUNS=0: the ASCII shadow / chunked iteration); outputs of the two
+(knob runs=0: the ASCII shadow / chunked iteration); outputs of the two
 compared in full (count and every record).  One JSON line per pattern.
 usage: python tools/runs_bench.py [pattern ...]"""
 import json
@@ -42,11 +42,11 @@ def run(re, reps):
 
 pats = sys.argv[1:] or [r"\w+", r"[a-z]+", r"\S+", r"\pL+", r"\d+", r"[^\n]+"]
 for pat in pats:
-    os.environ.pop("RURE_AMD_RUNS", None)
+    R._debug_set(None)
     ms, n, m, path = run(R.Regex(pat), 5)
-    os.environ["RURE_AMD_RUNS"] = "0"
+    R._debug_set("runs=%s" % ("0"))
     ms0, n0, m0, path0 = run(R.Regex(pat), 2)
-    os.environ.pop("RURE_AMD_RUNS", None)
+    R._debug_set(None)
     same = n == n0 and bool(torch.equal(m, m0))
     alg = L + 16 * n
     print(json.dumps({"pattern": pat, "bytes": L, "matches": n, "runs_ms": round(ms, 3), "runs_path": path,

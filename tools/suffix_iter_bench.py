@@ -1,6 +1,6 @@
 """find_iter of DfaSuffix regexes over one long haystack (~1 GiB of sherlock
 text): the parallel suffix iteration (launch_suffix_iter) against the wave
-path it replaces (RURE_AMD_SUFFIX_ITER=0: lane 0 of one wave walks the
+path it replaces (knob suffix_iter=0: lane 0 of one wave walks the
 haystack), the latter on a 16 MiB prefix; outputs compared on the prefix.
 usage: python tools/suffix_iter_bench.py"""
 import json
@@ -48,13 +48,13 @@ for pat in (r"[a-z]+ing", r"\w+@gmail\.com", r"\w+\s+Holmes"):
     path = N.rure_amd_last_fwd_path()
     cp, mp = run(re, P, cap)
     fast = mp.cpu().numpy()
-    os.environ["RURE_AMD_SUFFIX_ITER"] = "0"
+    R._debug_set("suffix_iter=%s" % ("0"))
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     cw, mw = run(re, P, cap)
     torch.cuda.synchronize()
     wave_ms = (time.perf_counter() - t0) * 1e3
-    del os.environ["RURE_AMD_SUFFIX_ITER"]
+    R._debug_set(None)
     print(json.dumps({"pattern": pat, "match_type": re.match_info()["match_type"], "bytes": L, "matches": total,
                       "iter_ms": round(ms, 3), "iter_GBps": round(L / ms / 1e6, 1), "path": path,
                       "wave_ms_16MiB": round(wave_ms, 1), "wave_GBps": round(P / wave_ms / 1e6, 3),

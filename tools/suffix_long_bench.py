@@ -2,7 +2,7 @@
 walked the whole haystack): `[a-z]+ing` and `\\w+@gmail\\.com` find /
 is_match over sherlock text replicated to 1 GiB on the unit path
 (launch_suffix_long) and, on a 16 MiB prefix, the one-lane path
-(RURE_AMD_SUFFIX_LONG=0), with outputs compared on the prefix.  One JSON
+(knob suffix_long=0), with outputs compared on the prefix.  One JSON
 line per (pattern, mode)."""
 import json
 import os
@@ -45,10 +45,10 @@ def main():
             path = N.rure_amd_last_fwd_path()
             t_units = timed(lambda: fn(hay, stride=n, length=n, count=1, out=r))
             rs = fn(hay, stride=small, length=small, count=1)
-            os.environ["RURE_AMD_SUFFIX_LONG"] = "0"
+            R._debug_set("suffix_long=%s" % ("0"))
             r0 = fn(hay, stride=small, length=small, count=1)
             t_lane = timed(lambda: fn(hay, stride=small, length=small, count=1, out=r0), reps=1)
-            del os.environ["RURE_AMD_SUFFIX_LONG"]
+            R._debug_set(None)
             print(json.dumps({"pattern": pat, "mode": mode, "bytes": n, "units_ms": round(t_units, 3),
                               "units_GBps": round(n / t_units / 1e6, 1), "path": path,
                               "one_lane_ms_16MiB": round(t_lane, 3),
