@@ -331,8 +331,14 @@ int64_t rure_amd_lex_ascii_export(rure *re, int four, uint8_t *table, size_t cap
 /* 1 if the regex is one byte class repeated (C+, the find_iter run engine:
  * matches = the maximal runs of C bytes) on all bytes (ascii = 0) or on
  * ASCII text (ascii = 1, the ASCII shadow: bytes >= 0x80 quit), with cls[b]
- * bit 0 = b in C, bit 1 = b quits; 0 if not. */
+ * bit 0 = b in C, bit 1 = b quits, bit 2 = b (>= 0x80) is read as UTF-8
+ * (a Unicode class: rure_amd_run_cp_export); 0 if not. */
 int rure_amd_run_class_export(rure *re, int ascii, uint8_t *cls);
+/* The run engine's code point bitmap of a Unicode class C+ (\w+, \pL+,
+ * \S+ in Unicode mode: bit c of bits[c / 32]), at most n words copied;
+ * returns its size in words (0x110000 / 32) or 0 if the engine reads no
+ * UTF-8 for this regex. */
+int rure_amd_run_cp_export(rure *re, uint32_t *bits, size_t n);
 
 /* Export of the Pike VM closure tables the NFA kernel runs (host only):
  * leaves = 3 u32 per leaf (kind | lo << 8 | hi << 16, closure, slot),

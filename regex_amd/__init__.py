@@ -658,6 +658,18 @@ class Regex(object):
         c = np.zeros(256, dtype=np.uint8)
         return c if N.rure_amd_run_class_export(self._re, 1 if ascii else 0, c.ctypes.data) == 1 else None
 
+    def run_code_points(self):
+        """The run engine's code point bitmap for a Unicode class C+
+        (rure_amd_run_cp_export): a uint32 array of 0x110000 bits, or None
+        when the engine reads no UTF-8 for this regex."""
+        import numpy as np
+        n = N.rure_amd_run_cp_export(self._re, None, 0)
+        if n <= 0:
+            return None
+        b = np.zeros(n, dtype=np.uint32)
+        N.rure_amd_run_cp_export(self._re, b.ctypes.data, n)
+        return b
+
     def lex4_table(self, ascii=False):
         """The four-bytes-per-step lexer table (rure_amd_lex4_export): (flat
         uint8 table, start row), or None.  ascii=True: the ASCII shadow's."""

@@ -890,6 +890,28 @@ bool run_class(const DenseDfa &d, uint32_t ustart1, bool nonempty, uint8_t cls[2
   return true;
 }
 
+// The code points of a regex that is one Unicode class repeated, greedy and
+// unbounded (C+: \w+, \pL+, \S+, [^\n]+ in Unicode mode), read off the
+// syntax tree (groups around the class or the repetition only bound
+// captures, which find_iter does not report).  Its program matches exactly
+// the valid UTF-8 encodings of C's code points one or more times
+// (compile.rs:386-396 c_class over utf8 ranges), so its leftmost-first
+// matches are the maximal runs of such encodings: run_iter.hip decodes the
+// bytes >= 0x80 against the bitmap.
+static bool unicode_run_set(const Expr &e0, std::vector<CRange> *out) {
+  const Expr *e = &e0;
+  while (e->kind == EK::Group && e->subs.size() == 1) e = &e->subs[0];
+  if (e->kind != EK::Repeat || !e->greedy || e->subs.size() != 1) return false;
+  if (!(e->rep == Rep::OneOrMore || (e->rep == Rep::Range && e->rmin == 1 && !e->has_max))) return false;
+  const Expr *c = &e->subs[0];
+  while (c->kind == EK::Group && c->subs.size() == 1) c = &c->subs[0];
+  if (c->kind == EK::AnyChar) *out = {{0, 0x10FFFF}};
+  else if (c->kind == EK::AnyCharNoNL) *out = {{0, 9}, {11, 0x10FFFF}};
+  else if (c->kind == EK::Class && !c->cls.empty()) *out = c->cls;
+  else return false;
+  return true;
+}
+
 // The lexer table of FwdDfaDev::lex_image (iter_spec_lex_tile_kernel).
 // Needs the first-byte start rule (a match's start is the first F byte of its
 // search on ASCII text) and terminal match states: every state carrying the
@@ -1046,9 +1068,21 @@ bool build_iter_dfa(rure *re) {
       build_lex4(re->lex, re->lex_s0, &re->lex4, &re->lex4_s0);
     // (over all bytes, else over ASCII text: Unicode \S+, \d+, [^\n]+)
     const bool ne = !can_match_empty(re->nfa);
-    re->run_ok = re->iter_ok && !re->nt.looks_used && re->dfwd_iter.quit < 0 &&
-                 (run_class(re->dfwd_iter, re->pf_iter.ustart1, ne, re->run_cls, false) ||
-                  run_class(re->dfwd_iter, re->pf_iter.ustart1, ne, re->run_cls, true));
+    // (a Unicode class: its code point bitmap, preferred to the ASCII-only
+    // table whose bytes >= 0x80 quit)
+    std::vector<CRange> ucls;
+    re->run_cp.clear();
+    const bool run_base = re->iter_ok && !re->nt.looks_used && re->dfwd_iter.quit < 0;
+    re->run_ok = run_base && run_class(re->dfwd_iter, re->pf_iter.ustart1, ne, re->run_cls, false);
+    if (run_base && !re->run_ok && unicode_run_set(re->expr, &ucls)) {
+      re->run_cp.assign(0x110000 / 32, 0);
+      for (const CRange &r : ucls)
+        for (uint32_t c = r.lo; c <= r.hi && c < 0x110000; ++c) re->run_cp[c >> 5] |= 1u << (c & 31);
+      for (int c = 0; c < 256; ++c) re->run_cls[c] = c < 0x80 ? (re->run_cp[c >> 5] >> (c & 31)) & 1u : 4;
+      re->run_ok = true;
+    }
+    if (run_base && !re->run_ok)
+      re->run_ok = run_class(re->dfwd_iter, re->pf_iter.ustart1, ne, re->run_cls, true);
     // ASCII shadow (iter_ascii_device): where the automaton is too big for
     // the all-rows LDS table because of its UTF-8 states (Unicode classes),
     // the same automaton with every byte >= 0x80 quitting and the states only
@@ -1249,6 +1283,7 @@ const FwdDfaDev *iter_device(rure *re, const DevTables &t, std::string *err) {
   size_t o_lex = re->lex.empty() ? 0 : b.add(re->lex.data(), re->lex.size());
   size_t o_lex4 = re->lex4.empty() ? 0 : b.add(re->lex4.data(), re->lex4.size());
   size_t o_run = re->run_ok ? b.add(re->run_cls, 256) : 0;
+  size_t o_cp = re->run_cp.empty() ? 0 : b.add(re->run_cp.data(), re->run_cp.size() * 4);
   DevTables tmp;
   if (!upload_blob(b, &tmp, err)) return nullptr;
   uint8_t *base = (uint8_t *)tmp.blob;
@@ -1295,7 +1330,8 @@ const FwdDfaDev *iter_device(rure *re, const DevTables &t, std::string *err) {
   }
   if (re->run_ok) {
     f.run_cls = base + o_run;
-    f.run_quit = re->run_cls[0x80] >> 1;  // (ASCII-only class: bytes >= 0x80 quit)
+    f.run_cp = re->run_cp.empty() ? nullptr : (const uint32_t *)(base + o_cp);
+    f.run_quit = (re->run_cls[0x80] >> 1) & 1u;  // (ASCII-only class: bytes >= 0x80 quit)
   }
   if (!sa_img.empty()) {
     f.sa_image = (const uint64_t *)(base + o_sa);

@@ -832,6 +832,14 @@ int rure_amd_run_class_export(rure *re, int ascii, uint8_t *cls) {
   return ok ? 1 : 0;
 }
 
+int rure_amd_run_cp_export(rure *re, uint32_t *bits, size_t n) {
+  if (!re) return RURE_AMD_ERR_ARG;
+  if (!build_iter_dfa(re)) return RURE_AMD_ERR_DFA;
+  if (!re->run_ok || re->run_cp.empty()) return 0;
+  if (bits) memcpy(bits, re->run_cp.data(), std::min(n, re->run_cp.size()) * 4);
+  return (int)re->run_cp.size();
+}
+
 int rure_amd_first_byte_export(rure *re, uint8_t *bytes) {
   if (!re) return RURE_AMD_ERR_ARG;
   if (!build_iter_dfa(re)) return RURE_AMD_ERR_DFA;

@@ -554,14 +554,15 @@ hipError_t run_find_iter(rure *re, DevTables *t, const BatchDev &b, const IterOu
       // knob iter_chunk: the unit size in bytes (tests: many boundaries)
       if (knob(Knob::IterChunk) > 0) chunk = std::max<uint64_t>(16, knob(Knob::IterChunk));
     }
-    // A regex that is one byte class repeated (C+: [a-z]+, (?-u)\w+): its
-    // matches are the maximal runs (run_iter.hip), no DFA walk; its ASCII
-    // shadow's class (Unicode \w+, \S+, \pL+) answers ASCII text and quits
-    // on any other byte.  RURE_AMD_RUNS=0 keeps the DFA paths (A/B).
+    // A regex that is one class repeated (C+: [a-z]+, (?-u)\w+, and Unicode
+    // classes \w+, \S+, \pL+ over UTF-8): its matches are the maximal runs
+    // (run_iter.hip), no DFA walk; the ASCII shadow's class (an ASCII-only
+    // class in Unicode mode) answers ASCII text and quits on any other
+    // byte.  Knob runs=0 keeps the DFA paths (A/B).
     const bool runs = !sp && knob(Knob::Runs) != 0;
     if (runs && fi->run_cls) {
       bool q = false;
-      const hipError_t e = launch_find_iter_runs(b, fi->run_cls, o, st, t->cus, fi->run_quit != 0, &q);
+      const hipError_t e = launch_find_iter_runs(b, fi->run_cls, fi->run_cp, o, st, t->cus, fi->run_quit != 0, &q);
       if (e != hipErrorNotSupported && (e != hipSuccess || !q)) {
         if (e == hipSuccess) note_fwd_path(-19);
         return e;
@@ -574,7 +575,7 @@ hipError_t run_find_iter(rure *re, DevTables *t, const BatchDev &b, const IterOu
       if (const FwdDfaDev *fa = iter_ascii_device(re, *t, err)) {
         if (runs && fa->run_cls) {
           bool q = false;
-          const hipError_t e = launch_find_iter_runs(b, fa->run_cls, o, st, t->cus, true, &q);
+          const hipError_t e = launch_find_iter_runs(b, fa->run_cls, nullptr, o, st, t->cus, true, &q);
           if (e != hipErrorNotSupported && (e != hipSuccess || !q)) {
             if (e == hipSuccess) note_fwd_path(-20);
             return e;

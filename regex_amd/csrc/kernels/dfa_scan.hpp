@@ -114,8 +114,11 @@ struct FwdDfaDev {
   uint32_t looks, can_quit;
   // find_iter DFA only: the regex is one byte class repeated (C+, host
   // run_class): run_cls[b] bit 0 = b is in C, bit 1 = b quits (the ASCII
-  // shadow: bytes >= 0x80); null: not such a regex (run_iter.hip)
+  // shadow: bytes >= 0x80), bit 2 = decode (a Unicode class C+, host
+  // unicode_run_set: bytes >= 0x80 are read as UTF-8 against run_cp, its
+  // code point bitmap); null: not such a regex (run_iter.hip)
   const uint8_t *run_cls;
+  const uint32_t *run_cp;
   uint32_t run_quit;  // some byte quits (bit 1): the run engine's flag is read back
 };
 constexpr uint32_t kLexMaxRows = 24;  // lexer table rows (iter_spec_lex_tile_kernel's static LDS)
@@ -275,8 +278,10 @@ struct IterSpan {
 // batches whose searched bytes are 16-byte aligned (hipErrorNotSupported
 // otherwise); *quit = a byte of the quit class was read (can_quit: the
 // flag is read back) and the results are not the answer.
-hipError_t launch_find_iter_runs(const BatchDev &b, const uint8_t *cls, const IterOut &o, hipStream_t st, int cus,
-                                 bool can_quit, bool *quit);
+// cp: a Unicode class's code point bitmap (class bit 2 on bytes >= 0x80),
+// else null.
+hipError_t launch_find_iter_runs(const BatchDev &b, const uint8_t *cls, const uint32_t *cp, const IterOut &o,
+                                 hipStream_t st, int cus, bool can_quit, bool *quit);
 hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaDev &r, const NfaDev *nf,
                             bool chunked, uint64_t chunk, const IterOut &o, hipStream_t st, int cus,
                             const IterSpan *span = nullptr, const MatchDev *mt = nullptr, bool *quit = nullptr);

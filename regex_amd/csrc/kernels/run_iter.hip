@@ -21,6 +21,17 @@
 // Unicode class: a byte >= 0x80 may belong to a multi-byte match): any such
 // byte in a unit raises the quit flag, and the caller answers the batch with
 // the full automaton.
+//
+// A Unicode class (cp: its code point bitmap, 0x110000 bits; the table
+// marks every byte >= 0x80 with bit 2) needs no quit: the Unicode-mode
+// program matches only valid UTF-8 encodings of C's code points, so a byte
+// is "in C" when it belongs to such an encoding, and the maximal runs of
+// those bytes are again the matches (no two valid encodings overlap, and a
+// run's first byte is a lead byte).  A lane holding a byte >= 0x80 (rare on
+// mostly-ASCII text) decodes around each such byte: back over at most three
+// continuation bytes to the lead (never before the search start: the search
+// does not see earlier bytes), then the sequence's validity (no overlong
+// form, no surrogate, at most U+10FFFF) and its code point's bit.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -36,8 +47,35 @@ namespace {
 
 constexpr uint32_t kRunUnit = 4096;  // bytes per wave unit: 64 lanes x 64 bytes
 
+// Whether byte q of the haystack at base (bytes [lo, len) visible) belongs
+// to a valid UTF-8 encoding of a code point in the bitmap cp.
+__device__ __noinline__ bool utf8_in_class(const uint8_t *base, uint64_t lo, uint64_t len, uint64_t q,
+                                           const uint32_t *cp) {
+  uint64_t p = q;
+  for (int k = 0; k < 3 && p > lo && (base[p] & 0xC0) == 0x80; ++k) --p;
+  const uint32_t b0 = base[p];
+  uint32_t n, c;
+  if (b0 >= 0xC2 && b0 <= 0xDF) n = 2, c = b0 & 0x1F;
+  else if (b0 >= 0xE0 && b0 <= 0xEF) n = 3, c = b0 & 0x0F;
+  else if (b0 >= 0xF0 && b0 <= 0xF4) n = 4, c = b0 & 0x07;
+  else return false;  // ASCII, a continuation byte or an invalid lead
+  if (p + n <= q || p + n > len) return false;
+  for (uint32_t i = 1; i < n; ++i) {
+    const uint32_t bi = base[p + i];
+    if ((bi & 0xC0) != 0x80) return false;
+    if (i == 1) {  // the second byte's range excludes overlong forms, surrogates and > U+10FFFF
+      if ((b0 == 0xE0 && bi < 0xA0) || (b0 == 0xED && bi > 0x9F) || (b0 == 0xF0 && bi < 0x90) ||
+          (b0 == 0xF4 && bi > 0x8F))
+        return false;
+    }
+    c = (c << 6) | (bi & 0x3F);
+  }
+  return (cp[c >> 5] >> (c & 31)) & 1u;
+}
+
 // The 64 bytes of a lane at p (16-byte aligned): class bits (bit 0: in C)
-// of the bytes before `len` into a 64-bit mask; *q = any byte's bit 1.
+// of the bytes before `len` into a 64-bit mask; *q = any byte's bits 1
+// (quit) and 2 (decode: a byte >= 0x80 of a Unicode class).
 __device__ __forceinline__ uint64_t run_mask(const uint8_t *cls, const uint8_t *p, uint64_t avail, uint32_t *q) {
   uint64_t m = 0;
   uint32_t qq = 0;
@@ -57,7 +95,15 @@ __device__ __forceinline__ uint64_t run_mask(const uint8_t *cls, const uint8_t *
       qq |= ok;
     }
   }
-  *q = qq & 2u;
+  *q = qq & 6u;
+  return m;
+}
+
+// The decode bits of a lane whose bytes include some >= 0x80 (Unicode class).
+__device__ __noinline__ uint64_t run_mask_utf8(uint64_t m, const uint8_t *base, uint64_t s0, uint64_t lo,
+                                               uint64_t len, const uint32_t *cp) {
+  for (uint32_t i = 0; i < 64 && s0 + i < len; ++i)
+    if (base[s0 + i] >= 0x80 && utf8_in_class(base, lo, len, s0 + i, cp)) m |= 1ull << i;
   return m;
 }
 
@@ -67,10 +113,10 @@ __device__ __forceinline__ uint64_t run_mask(const uint8_t *cls, const uint8_t *
 // EMIT = true: the records, a run that continues past its unit ending at the
 // first byte not in C after the unit (ufz suffix minima: uzs).
 template <bool EMIT>
-__global__ __launch_bounds__(256) void run_iter_kernel(BatchDev b, const uint8_t *cls_g, uint64_t nk, uint64_t nunits,
-                                                       uint64_t *ucount, uint64_t *ufz, const uint64_t *uoff,
-                                                       const uint64_t *uzs, uint64_t *matches, uint64_t cap,
-                                                       uint32_t *quit) {
+__global__ __launch_bounds__(256) void run_iter_kernel(BatchDev b, const uint8_t *cls_g, const uint32_t *cp,
+                                                       uint64_t nk, uint64_t nunits, uint64_t *ucount, uint64_t *ufz,
+                                                       const uint64_t *uoff, const uint64_t *uzs, uint64_t *matches,
+                                                       uint64_t cap, uint32_t *quit) {
   __shared__ uint8_t cls[256];
   if (threadIdx.x < 256) cls[threadIdx.x] = cls_g[threadIdx.x];
   __syncthreads();
@@ -84,17 +130,24 @@ __global__ __launch_bounds__(256) void run_iter_kernel(BatchDev b, const uint8_t
     const uint64_t s0 = c0 + 64 * (uint64_t)lane;
     const uint64_t avail = s0 < len ? len - s0 : 0;
     uint32_t q = 0;
-    const uint64_t m = run_mask(cls, base + s0, avail, &q);
+    uint64_t m = run_mask(cls, base + s0, avail, &q);
+    if (q & 4u) m = run_mask_utf8(m, base, s0, b.start, len, cp);
     // the byte before the lane's first: lane l - 1's bit 63; lane 0 reads it
     // (not in C at the search start: the search begins there)
     uint64_t pm = (uint64_t)__shfl_up((unsigned)(m >> 63), 1);
-    if (lane == 0) pm = (c0 > b.start && c0 - 1 < len) ? (cls[base[c0 - 1]] & 1u) : 0u;
+    if (lane == 0) {
+      pm = 0;
+      if (c0 > b.start && c0 - 1 < len) {
+        const uint32_t x = cls[base[c0 - 1]];
+        pm = (x & 4u) ? (utf8_in_class(base, b.start, len, c0 - 1, cp) ? 1u : 0u) : (x & 1u);
+      }
+    }
     const uint64_t starts = m & ~((m << 1) | pm);
     const uint32_t n = (uint32_t)__popcll(starts);
     const uint64_t nz = ~m;  // (bytes past the haystack are not in C)
     const uint64_t fz = nz ? s0 + (uint64_t)__builtin_ctzll(nz) : (1ull << 63);
     if (!EMIT) {
-      if (__any(q != 0)) {
+      if (__any((q & 2u) != 0)) {
         if (lane == 0) atomicOr(quit, 1u);
       }
       uint32_t tot = n;
@@ -168,8 +221,8 @@ hipError_t exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, hip
 // Fixed-stride batches whose searched bytes start 16-byte aligned (single
 // haystacks from start 0).  quit (host) = a byte with the quit class was
 // read: the results are then not the answer (one read-back of a flag).
-hipError_t launch_find_iter_runs(const BatchDev &b, const uint8_t *cls, const IterOut &o, hipStream_t st, int cus,
-                                 bool can_quit, bool *quit) {
+hipError_t launch_find_iter_runs(const BatchDev &b, const uint8_t *cls, const uint32_t *cp, const IterOut &o,
+                                 hipStream_t st, int cus, bool can_quit, bool *quit) {
   if (quit) *quit = false;
   if (b.offs || (((uintptr_t)(b.hay + b.start)) & 15) || (b.count > 1 && (b.stride & 15)))
     return hipErrorNotSupported;
@@ -188,7 +241,7 @@ hipError_t launch_find_iter_runs(const BatchDev &b, const uint8_t *cls, const It
   do {
     if ((e = hipMemsetAsync(ucount + nunits, 0, 8, st)) != hipSuccess) break;
     if ((e = hipMemsetAsync(qf, 0, 4, st)) != hipSuccess) break;
-    hipLaunchKernelGGL(run_iter_kernel<false>, dim3(grid), dim3(256), 0, st, b, cls, nk, nunits, ucount, ufz,
+    hipLaunchKernelGGL(run_iter_kernel<false>, dim3(grid), dim3(256), 0, st, b, cls, cp, nk, nunits, ucount, ufz,
                        (const uint64_t *)nullptr, (const uint64_t *)nullptr, (uint64_t *)nullptr, (uint64_t)0, qf);
     if ((e = hipGetLastError()) != hipSuccess) break;
     if (can_quit && quit) {
@@ -210,7 +263,7 @@ hipError_t launch_find_iter_runs(const BatchDev &b, const uint8_t *cls, const It
           hipSuccess)
         break;
     }
-    hipLaunchKernelGGL(run_iter_kernel<true>, dim3(grid), dim3(256), 0, st, b, cls, nk, nunits, ucount, ufz, uoff,
+    hipLaunchKernelGGL(run_iter_kernel<true>, dim3(grid), dim3(256), 0, st, b, cls, cp, nk, nunits, ucount, ufz, uoff,
                        uzs, o.matches, o.cap, qf);
     if ((e = hipGetLastError()) != hipSuccess) break;
     const int g2 = (int)std::max<uint64_t>(1, std::min<uint64_t>((b.count + 256) / 256, (uint64_t)cus * 4));

@@ -259,6 +259,7 @@ struct rure {
   // the run engine's byte classes (run_class: the regex is C+), for the
   // find_iter DFA over all bytes and for its ASCII shadow
   bool run_ok = false, run_a_ok = false;
+  std::vector<uint32_t> run_cp;  // Unicode C+: C's code point bitmap (0x110000 bits), else empty
   uint8_t run_cls[256] = {0}, run_cls_a[256] = {0};
   std::map<int, std::pair<void *, FwdDfaDev>> iter_dev_a;
 };

@@ -2,11 +2,12 @@
 C+ regexes' matches = maximal runs, against the oracle's find_iter
 (re_trait.rs:197-221) — single long haystacks (runs crossing lanes and 4 KiB
 units, a run longer than many units, all-C text), fixed-stride batches,
-searches from start > 0, and text with bytes >= 0x80 (an ASCII-only class
-quits and the DFA path answers, still exact)."""
+searches from start > 0, and text with bytes >= 0x80 (a Unicode class reads
+them as UTF-8, valid or not, and still answers)."""
 import gzip
 import os
 import random
+import zlib
 
 import numpy as np
 import pytest
@@ -88,16 +89,40 @@ def test_runs_stride_batch(cuda, pat):
         assert got == exp, (pat, start)
 
 
-@pytest.mark.parametrize("pat", [r"\w+", r"\S+", r"\pL+", r"[a-z]+"])
+@pytest.mark.parametrize("pat", [r"\w+", r"\S+", r"\pL+", r"[a-z]+", r"\d+", r"(?i)[a-z]+", r"[^\n]+", r".+"])
 def test_runs_non_ascii(cuda, pat):
-    """Bytes >= 0x80: a Unicode class's ASCII run engine quits (the DFA path
-    answers); [a-z]+'s class is exact on every byte (no quit)."""
+    """Bytes >= 0x80: a Unicode class's engine decodes them as UTF-8 (valid
+    letters, marks, digits, symbols, astral code points; stray
+    continuations, truncated leads, overlong forms, surrogates, bytes past
+    U+10FFFF) and still answers (-19), with runs crossing lanes and units;
+    [a-z]+'s class is exact on every byte."""
+    from test_run_engine import utf8_text
     re = R.Regex(pat)
     rng = random.Random(3)
     alpha = [b"ab", b"Z9", b" ", b"\n", "é".encode(), "✓".encode(), b"\xff", "٣".encode(), b"x_y"]
     t = b"".join(rng.choices(alpha, k=30000))
-    check_one(re, t, cuda)
-    if pat == r"[a-z]+":
-        assert N.rure_amd_last_fwd_path() == -19
-    else:
-        assert N.rure_amd_last_fwd_path() != -19
+    check_one(re, t, cuda, expect_path=-19)
+    check_one(re, t, cuda, start=4097)
+    u = utf8_text(zlib.crc32(pat.encode()), 40000)
+    check_one(re, u, cuda, expect_path=-19)
+    for st in (1, 2, 63, 4095, 4097):
+        check_one(re, u, cuda, start=st)
+    # a multi-byte encoding straddling every lane and unit edge: é at 62-63,
+    # 中 at 4094-4096, an astral letter at 8190-8193
+    edge = bytearray(b"a" * 12288)
+    edge[62:64] = "é".encode()
+    edge[4094:4097] = "中".encode()
+    edge[8190:8194] = "\U0001d400".encode()
+    edge[200:201] = b" "
+    check_one(re, bytes(edge), cuda, expect_path=-19)
+
+
+def test_runs_sherlock_unicode(cuda):
+    """The sherlock corpus as it is (with its non-ASCII bytes): \w+ = the
+    reference's count 109214 (bench/src/sherlock.rs:116) on the run engine."""
+    re = R.Regex(r"\w+")
+    t = sherlock()
+    assert any(b >= 0x80 for b in t)
+    check_one(re, t, cuda, expect_path=-19)
+    counts, _ = re.find_iter_batch(dev(t, cuda), stride=len(t), length=len(t), count=1)
+    assert int(counts[0]) == 109214
