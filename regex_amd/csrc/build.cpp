@@ -2,6 +2,7 @@
 // automata restated from the reference (host/*.cpp) are materialised, packed
 // into the kernels' table images and uploaded once per device.
 #include "runtime.hpp"
+#include "host/byte_freq.h"
 
 namespace rt {
 
@@ -481,27 +482,79 @@ bool needs_mt_lane(const ExecLiterals &x) {
 // DFA whose start does not depend on look-behind, from the regex's prefix
 // literals (dfa.prefixes, exec.rs:308-311; not for anchored starts,
 // dfa.rs:1516-1522 has_prefix) when they have at most 4 first bytes.
-// Knob prefix=0 turns it off (A/B).
+// FwdDfaDev::rare_*: the same skip on the prefixes' rarest byte or pair of
+// bytes at most 3 apart (host/byte_freq.h), when it is rarer than the first
+// byte.  Knob prefix: 0 off, 1 first byte only, 2 rare bytes only.
+// (A filter over the prefixes' first two or three positions lost to the
+// first-byte one on English text in round 4 — Sherlock\s+\w+ 1.47 -> 1.62
+// ms per GiB, (?i)watson\w* 1.46 -> 1.89, profiles/r04_prefix_depth_ab.jsonl
+// — and was deleted in round 5.)
 void set_prefix_skip(const rure *re, FwdDfaDev *f) {
   f->pfx_n = 0;
-  if (knob(Knob::Prefix) == 0 || !f->ustart1 || re->nfa.anchored_start) return;
+  f->rare_on = 0;
+  const long long mode = knob(Knob::Prefix);
+  if (mode == 0 || !f->ustart1 || re->nfa.anchored_start) return;
   const LitSearcher &p = re->xl.prefixes;
   if (p.matcher == 0 || p.lits.lits.empty()) return;
   bool seen[256] = {false};
   uint32_t n = 0;
+  bool first_ok = true;
   for (const Lit &l : p.lits.lits) {
     if (l.v.empty()) return;
     const uint8_t b = (uint8_t)l.v[0];
     if (seen[b]) continue;
-    if (n == 4) return;
+    if (n == 4) { first_ok = false; break; }
     seen[b] = true;
     f->pfx_rep[n++] = b * 0x01010101u;
   }
-  f->pfx_n = n;
-  // (a filter over the prefixes' first two or three positions lost to this
-  // one on English text in round 4 — Sherlock\s+\w+ 1.47 -> 1.62 ms per GiB,
-  // (?i)watson\w* 1.46 -> 1.89, profiles/r04_prefix_depth_ab.jsonl — and
-  // was deleted in round 5)
+  uint64_t first_freq = 0;
+  for (int b = 0; b < 256; ++b) first_freq += seen[b] ? kByteFreq[b] : 0;
+  if (!first_ok) n = 0;
+  // the byte class of every prefix at position j, as one entry (x | or ==
+  // rep: one byte, or an ASCII letter's two cases), and its frequency
+  size_t minlen = ~(size_t)0;
+  for (const Lit &l : p.lits.lits) minlen = std::min(minlen, l.v.size());
+  const size_t J = std::min<size_t>(minlen, 16);
+  std::vector<int> rep(J, -1), orm(J, 0);
+  std::vector<uint64_t> fr(J, 0);
+  for (size_t j = 0; j < J; ++j) {
+    bool in[256] = {false};
+    for (const Lit &l : p.lits.lits) in[(uint8_t)l.v[j]] = true;
+    int c = 0, x0 = -1;
+    for (int x = 0; x < 256; ++x)
+      if (in[x]) ++c, x0 = x0 < 0 ? x : x0;
+    const bool letter = (x0 | 0x20) >= 'a' && (x0 | 0x20) <= 'z';
+    if (c == 1) {
+      rep[j] = x0, orm[j] = 0, fr[j] = kByteFreq[x0];
+    } else if (c == 2 && letter && in[x0 ^ 0x20]) {
+      rep[j] = x0 | 0x20, orm[j] = 0x20, fr[j] = kByteFreq[x0] + kByteFreq[x0 ^ 0x20];
+    }
+  }
+  // the rarest single byte class or pair (i1, i1 + d), d <= 3, i1 + d <= 15
+  // (a pair's frequency: the product, as if independent)
+  double best = 1e30;
+  int bi = -1, bd = 0;
+  for (size_t i = 0; i < J; ++i) {
+    if (rep[i] < 0) continue;
+    if ((double)fr[i] < best) best = (double)fr[i], bi = (int)i, bd = 0;
+    for (int d = 1; d <= 3 && i + d < J && i + d <= 15; ++d) {
+      if (rep[i + d] < 0) continue;
+      const double pf = (double)fr[i] * (double)fr[i + d] / (double)(1u << 20);
+      if (pf < best) best = pf, bi = (int)i, bd = d;
+    }
+  }
+  const bool rare_ok = bi >= 0 && mode != 1;
+  const bool first_use = n > 0 && mode != 2;
+  if (rare_ok && (!first_use || best < (double)first_freq)) {
+    f->rare_on = 1;
+    f->rare_d = (uint32_t)bd;
+    f->rare_rep[0] = (uint32_t)rep[bi] * 0x01010101u;
+    f->rare_or[0] = (uint32_t)orm[bi] * 0x01010101u;
+    f->rare_rep[1] = (uint32_t)rep[bi + bd] * 0x01010101u;
+    f->rare_or[1] = (uint32_t)orm[bi + bd] * 0x01010101u;
+    return;
+  }
+  f->pfx_n = first_use ? n : 0;
 }
 
 // Upload (once per device) and return device descriptors.

@@ -241,6 +241,28 @@ __device__ __forceinline__ bool prefix_hit(const FwdDfaDev &f, const uint4 *v) {
   return acc != 0;
 }
 
+// FwdDfaDev::rare_*: whether the 144 bytes of v (the burst and the next 16)
+// hold a candidate start of the burst.
+__device__ __forceinline__ bool rare_hit(const FwdDfaDev &f, const uint4 *v) {
+  const uint32_t r1 = f.rare_rep[0], o1 = f.rare_or[0], r2 = f.rare_rep[1], o2 = f.rare_or[1];
+  const uint32_t sh = 8 * f.rare_d;
+  uint32_t acc = 0, a_prev = 0, b_prev = 0;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const uint32_t w4[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t a = has_byte(w4[q] | o1, r1), b = has_byte(w4[q] | o2, r2);
+      if (k + q > 0) acc |= a_prev & __builtin_amdgcn_alignbit(b, b_prev, sh);
+      a_prev = a;
+      b_prev = b;
+    }
+  }
+  // the last word's class-2 bytes past the window count as hits
+  acc |= a_prev & __builtin_amdgcn_alignbit(0x80808080u, b_prev, sh);
+  return acc != 0;
+}
+
 // One lane's forward scan of text[at..end) (dfa.rs:576-764): 16-byte
 // chunks through the LDS fast table, 128-byte bursts per lane.  No EOF step.
 // PFX: with the start-state prefix skip (FwdDfaDev::pfx_*).  A separate
@@ -262,15 +284,22 @@ __device__ __forceinline__ void fwd_range(LaneState &L, const FwdDfaDev &f, cons
     for (; j < 16 && at < end && !L.done; ++j, ++at) step1<MODE>(L, f, lds, (w[j >> 2] >> ((j & 3) * 8)) & 0xFF, at);
   }
   while (!L.done && at + 128 <= end) {
-    if (PFX && f.pfx_n && L.s + 1 == f.ustart1) {
+    if (PFX && (f.pfx_n || f.rare_on) && L.s + 1 == f.ustart1) {
       // start-state prefix skip (dfa.rs:700-711): bursts without a prefix
       // first byte cannot start a match, and the state stays the start state
       while (true) {
-        uint4 t[8];
+        uint4 t[9];
         const uint4 *q = (const uint4 *)(base + at);
+        if (f.rare_on) {
+          if (at + 144 > end) break;  // (the window's 16 bytes past the burst)
 #pragma unroll
-        for (int k = 0; k < 8; ++k) t[k] = q[k];
-        if (prefix_hit(f, t)) break;
+          for (int k = 0; k < 9; ++k) t[k] = q[k];
+          if (rare_hit(f, t)) break;
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) t[k] = q[k];
+          if (prefix_hit(f, t)) break;
+        }
         at += 128;
         if (at + 128 > end) break;
       }

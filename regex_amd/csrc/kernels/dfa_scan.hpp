@@ -106,6 +106,18 @@ struct FwdDfaDev {
   // that hold none of those bytes (fwd_range); pfx_n = 0: off.
   uint32_t pfx_n;
   uint32_t pfx_rep[4];
+  // The same skip on the prefixes' rarest bytes (literals.rs:390-510
+  // FreqyPacked picks the rarest byte by a frequency table; here the table
+  // is host/byte_freq.h, and on 128-byte bursts a pair is needed, a single
+  // common-word letter being in nearly every burst): every prefix has byte
+  // class 1 at offset i1 and class 2 at i1 + rare_d (d <= 3; d = 0: one
+  // byte), each one byte or an ASCII letter's two cases (x | rare_or ==
+  // rare_rep).  A burst [a, a + 128) is skipped when no q in [a, a + 140)
+  // has class 1 at q and class 2 at q + d (i1 + d <= 15, so every start in
+  // the burst is covered; positions past it only add candidates).  rare_on =
+  // 0: the first-byte skip above.
+  uint32_t rare_on, rare_d;
+  uint32_t rare_rep[2], rare_or[2];
   // find_iter DFA only: the regex has look-around assertions (the chunked
   // iteration then repairs units whose first reverse scan reached their
   // start, and a reverse NoMatch ends the iteration; iter_scan.hip), and its

@@ -2390,7 +2390,7 @@ hipError_t long_scan_m(const BatchDev &b, const FwdDfaDev &f, const RevDfaDev &r
     // first byte: measured faster there (Sherlock\s+\w+ 1.76 -> 1.54 ms per
     // GiB, >[^\n]*\n 1.10 -> 0.31) and slower with two ((?i)holmes\w*:
     // 1.46 -> 1.73 ms; profiles/r03_prefix_ab.jsonl)
-    if (f.pfx_n == 1) {
+    if (f.pfx_n == 1 || f.rare_on) {
       if ((e = allow_lds(long_scan_kernel<MODE, true>, iter_lds_bytes(f, r))) != hipSuccess) break;
       hipLaunchKernelGGL((long_scan_kernel<MODE, true>), lg, dim3(256), iter_lds_bytes(f, r), st, b, g, nunits, f, r,
                          ures, best);

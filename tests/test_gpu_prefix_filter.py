@@ -3,7 +3,9 @@ prefix_at restated as a burst filter) on the chunked long scan
 (last_fwd_path -4): find / is_match / shortest over long haystacks against
 the oracle, with the only occurrence planted across 128-byte burst edges (a
 prefix whose first byte ends a burst must not be skipped) and case-folded
-prefix sets; with the skip and without it (debug knob prefix=0)."""
+prefix sets; without the skip (debug knob prefix=0), on the first byte
+(prefix=1), on the rarest byte or pair of bytes (prefix=2, FwdDfaDev::rare_*)
+and the default choice."""
 import numpy as np
 import pytest
 
@@ -26,7 +28,7 @@ def _filler(n):
     return base[:n]
 
 
-@pytest.fixture(params=[0, None])
+@pytest.fixture(params=[0, 1, 2, None])
 def prefix_mode(request, knobs):
     if request.param is not None:
         knobs(prefix=request.param)

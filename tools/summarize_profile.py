@@ -66,6 +66,37 @@ def main(tag, kernel_substr="rure_amd::"):
     }
     if out["hbm_read_bytes_per_launch"] and alg:
         out["traffic_over_alg"] = out["hbm_read_bytes_per_launch"] / alg
+    # every roofline of the bench line (C3: the variant kernel and the strip
+    # lexer) from the launches of its workload alone: the kernel trace's
+    # dispatches of that kernel with the largest grid (the shootout pipeline
+    # and the warm-up ramp launch the same kernels over smaller inputs), and
+    # the FETCH_SIZE rows of the same grid
+    trace = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv"))))
+    out["rooflines"] = {}
+    for key, v in bench.items():
+        if not (key.startswith("roofline") and isinstance(v, dict) and v.get("alg_bytes_per_launch")):
+            continue
+        kid = str(v.get("kernel", "")).split("(")[-1].split(":")[0].split("_kernel")[0].strip()
+        rows = [r for r in trace if "rure_amd::" in r["Kernel_Name"] and kid and kid + "_kernel" in r["Kernel_Name"]]
+        if not rows:
+            continue
+        grid = lambda r: int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
+        g = max(grid(r) for r in rows)
+        main = [r for r in rows if grid(r) == g]
+        durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in main]
+        avg = sum(durs) / len(durs)
+        fk = [float(r["Counter_Value"]) for r in pmc
+              if kid + "_kernel" in r["Kernel_Name"] and r["Counter_Name"] == "FETCH_SIZE" and int(r["Grid_Size"]) == g]
+        a = v["alg_bytes_per_launch"]
+        ent = {"kernel": short(main[0]["Kernel_Name"]), "grid": g, "launches": len(main),
+               "avg_ns": round(avg, 1), "alg_bytes_per_launch": a,
+               "achieved_GBps": round(a / avg, 1), "peak_GBps": v.get("peak"),
+               "frac": round(a / avg / float(v.get("peak") or 8000.0), 4),
+               "bench_kernel_ms_events": v.get("kernel_ms")}
+        if fk:
+            ent["hbm_read_bytes_per_launch"] = sum(fk) / len(fk) * 1024 * 2
+            ent["traffic_over_alg"] = round(ent["hbm_read_bytes_per_launch"] / a, 4)
+        out["rooflines"][key] = ent
     os.makedirs(os.path.join(root, "profiles"), exist_ok=True)
     with open(os.path.join(root, "profiles", tag + "_summary.json"), "w") as f:
         json.dump(out, f, indent=1)
