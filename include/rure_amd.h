@@ -414,8 +414,9 @@ int rure_amd_set_uses_dfa(rure_set *re);
  * quit / a quit sent it to the wave path), -14 / -15 = the ASCII-shadow
  * find_iter (answered / quit), -16 = the Pike VM alone (no DFA), -17 = the
  * core-form set kernel over an offset batch, -19 / -20 = the find_iter run
- * engine of a C+ regex (its class over all bytes / the ASCII shadow's);
- * -1 before the first launch. */
+ * engine of a C+ regex (its class over all bytes / the ASCII shadow's),
+ * -21 = the chunked find_iter of the full automaton (no look-around), -22 =
+ * find_iter with one haystack per wavefront; -1 before the first launch. */
 int rure_amd_last_fwd_path(void);
 /* Debug-only overrides of the engine dispatch and launch geometry
  * (regex_amd/csrc/host/knobs.hpp lists them): replaces the whole override

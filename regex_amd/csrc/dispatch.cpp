@@ -594,11 +594,14 @@ hipError_t run_find_iter(rure *re, DevTables *t, const BatchDev &b, const IterOu
     const hipError_t e = launch_find_iter(b, fi, t->r, &t->n, true, chunk, o, st, t->cus, sp, nullptr, &quit);
     // last_fwd_path: -12 = the chunked iteration of a look-around regex
     // answered, -13 = it quit (the wave path answers)
-    if (looks && e == hipSuccess) note_fwd_path(quit ? -13 : -12);
+    // (-21: the chunked iteration of the full automaton answered)
+    if (e == hipSuccess) note_fwd_path(looks ? (quit ? -13 : -12) : -21);
     if (e != hipSuccess || !quit) return e;
   }
   if (!re->nfa_ok) return hipErrorInvalidValue;
-  return launch_find_iter(b, t->has_dfa ? &t->f : nullptr, t->r, &t->n, false, 0, o, st, t->cus, sp);
+  const hipError_t e = launch_find_iter(b, t->has_dfa ? &t->f : nullptr, t->r, &t->n, false, 0, o, st, t->cus, sp);
+  if (e == hipSuccess && last_fwd_path() != -13) note_fwd_path(-22);  // one haystack per wavefront
+  return e;
 }
 
 

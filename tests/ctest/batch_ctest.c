@@ -98,8 +98,9 @@ int main(void) {
 
   /* Stream order: with ~10 ms of finds queued ahead on a
    * stream, find_iter of a regex that cannot quit returns while that work is
-   * still running (it only enqueues); find_iter of \w+ (Unicode classes: the
-   * ASCII shadow's quit flag is read back) is on the synchronising list and
+   * still running (it only enqueues): [a-z]+, and \w+ (the run engine reads
+   * UTF-8 itself); find_iter of \w+@\w+\.\w+ (Unicode classes: the ASCII
+   * shadow's quit flag is read back) is on the synchronising list and
    * returns with the stream drained. */
   {
     const size_t BIGL = 4096, BIGN = 65536;
@@ -113,8 +114,9 @@ int main(void) {
     rure_amd_batch bb = {big, NULL, BIGL, BIGL, BIGN, 0};
     rure *lower = rure_compile_must("[a-z]+");
     rure *word = rure_compile_must("\\w+");
-    for (int pass = 0; pass < 2; ++pass) {
-      rure *r = pass == 0 ? lower : word;
+    rure *mail = rure_compile_must("\\w+@\\w+\\.\\w+");
+    for (int pass = 0; pass < 3; ++pass) {
+      rure *r = pass == 0 ? lower : pass == 1 ? word : mail;
       /* warm: first calls build and upload tables */
       CHECK(rure_amd_find_iter_batch(r, &one, dcount, di, cap, dtotal, st) == RURE_AMD_OK, "warm iter");
       HIP(hipStreamSynchronize(st));
@@ -125,14 +127,15 @@ int main(void) {
       clock_gettime(CLOCK_MONOTONIC, &t1);
       const hipError_t q = hipStreamQuery(st);
       const double ms = (t1.tv_sec - t0.tv_sec) * 1e3 + (t1.tv_nsec - t0.tv_nsec) * 1e-6;
-      if (pass == 0)
-        CHECK(q == hipErrorNotReady, "find_iter of [a-z]+ waited for the stream (query %d, %.2f ms)", (int)q, ms);
+      if (pass < 2)
+        CHECK(q == hipErrorNotReady, "find_iter (pass %d) waited for the stream (query %d, %.2f ms)", pass, (int)q, ms);
       else  /* it waited for the ~10 ms of finds queued ahead of it */
-        CHECK(ms > 3.0, "find_iter of \\w+ returned after %.2f ms, before the queued work", ms);
+        CHECK(ms > 3.0, "find_iter of \\w+@\\w+\\.\\w+ returned after %.2f ms, before the queued work", ms);
       HIP(hipStreamSynchronize(st));
     }
     rure_free(lower);
     rure_free(word);
+    rure_free(mail);
     hipFree(big);
     hipFree(bm);
     HIP(hipStreamDestroy(st));
