@@ -483,8 +483,8 @@ bool needs_mt_lane(const ExecLiterals &x) {
 // literals (dfa.prefixes, exec.rs:308-311; not for anchored starts,
 // dfa.rs:1516-1522 has_prefix) when they have at most 4 first bytes.
 // FwdDfaDev::rare_*: the same skip on the prefixes' rarest byte or pair of
-// bytes at most 3 apart (host/byte_freq.h), when it is rarer than the first
-// byte.  Knob prefix: 0 off, 1 first byte only, 2 rare bytes only.
+// bytes at most 3 apart (host/byte_freq.h), where they have more than one
+// first byte.  Knob prefix: 0 off, 1 first byte only, 2 rare bytes only.
 // (A filter over the prefixes' first two or three positions lost to the
 // first-byte one on English text in round 4 — Sherlock\s+\w+ 1.47 -> 1.62
 // ms per GiB, (?i)watson\w* 1.46 -> 1.89, profiles/r04_prefix_depth_ab.jsonl
@@ -507,8 +507,6 @@ void set_prefix_skip(const rure *re, FwdDfaDev *f) {
     seen[b] = true;
     f->pfx_rep[n++] = b * 0x01010101u;
   }
-  uint64_t first_freq = 0;
-  for (int b = 0; b < 256; ++b) first_freq += seen[b] ? kByteFreq[b] : 0;
   if (!first_ok) n = 0;
   // the byte class of every prefix at position j, as one entry (x | or ==
   // rep: one byte, or an ASCII letter's two cases), and its frequency
@@ -543,9 +541,17 @@ void set_prefix_skip(const rure *re, FwdDfaDev *f) {
       if (pf < best) best = pf, bi = (int)i, bd = d;
     }
   }
+  // Which, by measurement (tools/prefix_ab.py, profiles/r05_prefix_ab.jsonl,
+  // 1 GiB of sherlock, long scan): one first byte wins where there is one
+  // (Sherlock\s+\w+ 1.55 ms against 1.73 for the rare pair, >[^\n]*\n 0.31
+  // against 0.39: a single-byte SWAR test per word is cheaper, and English
+  // pairs are not independent: "l..k" of Sherlock is in "look"); the rare
+  // skip where the first bytes are several ((?i)holmes\w* 1.41 -> 1.14 ms,
+  // (?i)watson\w* 1.68 -> 1.61, (?i)zqxj\w* 1.11 -> 0.54; (?i)baker\s+street
+  // loses, 1.48 -> 1.56: "b.k" of "back", "book").
   const bool rare_ok = bi >= 0 && mode != 1;
   const bool first_use = n > 0 && mode != 2;
-  if (rare_ok && (!first_use || best < (double)first_freq)) {
+  if (rare_ok && (mode == 2 || !(first_use && n == 1))) {
     f->rare_on = 1;
     f->rare_d = (uint32_t)bd;
     f->rare_rep[0] = (uint32_t)rep[bi] * 0x01010101u;

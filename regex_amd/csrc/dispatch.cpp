@@ -571,6 +571,7 @@ hipError_t run_find_iter(rure *re, DevTables *t, const BatchDev &b, const IterOu
     // the ASCII shadow first (all-rows LDS tables; a non-ASCII byte quits
     // and the full automaton re-runs the batch, still chunked); not for
     // spans (the quit is read back)
+    bool shadow_quit = false;
     if (!sp) {
       if (const FwdDfaDev *fa = iter_ascii_device(re, *t, err)) {
         if (runs && fa->run_cls) {
@@ -587,15 +588,16 @@ hipError_t run_find_iter(rure *re, DevTables *t, const BatchDev &b, const IterOu
           if (e == hipSuccess) note_fwd_path(-14);
           return e;
         }
-        note_fwd_path(-15);  // a quit: the full automaton below answers
+        shadow_quit = true;  // a quit: the full automaton below answers (-15)
       }
     }
     bool quit = false;
     const hipError_t e = launch_find_iter(b, fi, t->r, &t->n, true, chunk, o, st, t->cus, sp, nullptr, &quit);
     // last_fwd_path: -12 = the chunked iteration of a look-around regex
     // answered, -13 = it quit (the wave path answers)
-    // (-21: the chunked iteration of the full automaton answered)
-    if (e == hipSuccess) note_fwd_path(looks ? (quit ? -13 : -12) : -21);
+    // (-21: the chunked iteration of the full automaton answered; -15: so,
+    // after the ASCII shadow quit)
+    if (e == hipSuccess) note_fwd_path(looks ? (quit ? -13 : -12) : shadow_quit ? -15 : -21);
     if (e != hipSuccess || !quit) return e;
   }
   if (!re->nfa_ok) return hipErrorInvalidValue;

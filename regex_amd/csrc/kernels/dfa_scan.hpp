@@ -112,10 +112,11 @@ struct FwdDfaDev {
   // common-word letter being in nearly every burst): every prefix has byte
   // class 1 at offset i1 and class 2 at i1 + rare_d (d <= 3; d = 0: one
   // byte), each one byte or an ASCII letter's two cases (x | rare_or ==
-  // rare_rep).  A burst [a, a + 128) is skipped when no q in [a, a + 140)
+  // rare_rep).  A burst [a, a + 128) is skipped when no q in [a, a + 144)
   // has class 1 at q and class 2 at q + d (i1 + d <= 15, so every start in
-  // the burst is covered; positions past it only add candidates).  rare_on =
-  // 0: the first-byte skip above.
+  // the burst is covered; positions past it only add candidates).  Used
+  // where the prefixes have several first bytes ((?i)holmes); rare_on = 0:
+  // the first-byte skip above.
   uint32_t rare_on, rare_d;
   uint32_t rare_rep[2], rare_or[2];
   // find_iter DFA only: the regex has look-around assertions (the chunked

@@ -118,7 +118,7 @@ def test_runs_non_ascii(cuda, pat):
 
 
 def test_runs_sherlock_unicode(cuda):
-    """The sherlock corpus as it is (with its non-ASCII bytes): \w+ = the
+    r"""The sherlock corpus as it is (with its non-ASCII bytes): \w+ = the
     reference's count 109214 (bench/src/sherlock.rs:116) on the run engine."""
     re = R.Regex(r"\w+")
     t = sherlock()
