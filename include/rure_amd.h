@@ -339,6 +339,10 @@ int rure_amd_run_class_export(rure *re, int ascii, uint8_t *cls);
  * returns its size in words (0x110000 / 32) or 0 if the engine reads no
  * UTF-8 for this regex. */
 int rure_amd_run_cp_export(rure *re, uint32_t *bits, size_t n);
+/* 1 if every match of the regex is exactly one byte of a class (cls[b] = 1
+ * for its bytes): its replace_all over one haystack then runs without a
+ * match list (rure_amd_replace_batch, last_fwd_path -23); 0 if not. */
+int rure_amd_class_one_export(rure *re, uint8_t *cls);
 
 /* Export of the Pike VM closure tables the NFA kernel runs (host only):
  * leaves = 3 u32 per leaf (kind | lo << 8 | hi << 16, closure, slot),
@@ -416,7 +420,8 @@ int rure_amd_set_uses_dfa(rure_set *re);
  * core-form set kernel over an offset batch, -19 / -20 = the find_iter run
  * engine of a C+ regex (its class over all bytes / the ASCII shadow's),
  * -21 = the chunked find_iter of the full automaton (no look-around), -22 =
- * find_iter with one haystack per wavefront; -1 before the first launch. */
+ * find_iter with one haystack per wavefront, -23 = replace_all of a
+ * one-byte-class regex without a match list; -1 before the first launch. */
 int rure_amd_last_fwd_path(void);
 /* Debug-only overrides of the engine dispatch and launch geometry
  * (regex_amd/csrc/host/knobs.hpp lists them): replaces the whole override

@@ -158,6 +158,7 @@ rure_amd_lex_export = _sig("rure_amd_lex_export", ctypes.c_int64, VP, VP, c_size
 rure_amd_lex4_export = _sig("rure_amd_lex4_export", ctypes.c_int64, VP, VP, c_size, VP)
 rure_amd_run_class_export = _sig("rure_amd_run_class_export", ctypes.c_int, VP, ctypes.c_int, VP)
 rure_amd_run_cp_export = _sig("rure_amd_run_cp_export", ctypes.c_int, VP, VP, c_size)
+rure_amd_class_one_export = _sig("rure_amd_class_one_export", ctypes.c_int, VP, VP)
 rure_amd_lex_ascii_export = _sig("rure_amd_lex_ascii_export", ctypes.c_int64, VP, ctypes.c_int, VP, c_size, VP)
 rure_amd_set_matches_batch_words = _sig("rure_amd_set_matches_batch_words", ctypes.c_int, VP,
                                         ctypes.POINTER(RureBatch), VP, c_size, VP)

@@ -957,18 +957,63 @@ bool run_class(const DenseDfa &d, uint32_t ustart1, bool nonempty, uint8_t cls[2
 // (compile.rs:386-396 c_class over utf8 ranges), so its leftmost-first
 // matches are the maximal runs of such encodings: run_iter.hip decodes the
 // bytes >= 0x80 against the bitmap.
+static const Expr *unwrap(const Expr *e) {  // groups, one-element sequences
+  while ((e->kind == EK::Group || e->kind == EK::Concat || e->kind == EK::Alternate) && e->subs.size() == 1)
+    e = &e->subs[0];
+  return e;
+}
+
 static bool unicode_run_set(const Expr &e0, std::vector<CRange> *out) {
-  const Expr *e = &e0;
-  while (e->kind == EK::Group && e->subs.size() == 1) e = &e->subs[0];
+  const Expr *e = unwrap(&e0);
   if (e->kind != EK::Repeat || !e->greedy || e->subs.size() != 1) return false;
   if (!(e->rep == Rep::OneOrMore || (e->rep == Rep::Range && e->rmin == 1 && !e->has_max))) return false;
-  const Expr *c = &e->subs[0];
-  while (c->kind == EK::Group && c->subs.size() == 1) c = &c->subs[0];
+  const Expr *c = unwrap(&e->subs[0]);
   if (c->kind == EK::AnyChar) *out = {{0, 0x10FFFF}};
   else if (c->kind == EK::AnyCharNoNL) *out = {{0, 9}, {11, 0x10FFFF}};
   else if (c->kind == EK::Class && !c->cls.empty()) *out = c->cls;
   else return false;
   return true;
+}
+
+// Whether every match of the regex is exactly one byte of a class (read off
+// the syntax tree: one byte literal, a byte class, or a Unicode class of
+// ASCII code points; a case-insensitive literal is left out, its Unicode
+// folds can be multi-byte): then its find_iter is the positions of those
+// bytes and replace_all needs no match list (launch_replace_class).
+bool class_one_set(const Expr &e0, uint8_t cls[256]) {
+  const Expr *e = unwrap(&e0);
+  std::memset(cls, 0, 256);
+  switch (e->kind) {
+    case EK::LiteralBytes:
+      if (e->bytes.size() != 1 || e->casei) return false;
+      cls[e->bytes[0]] = 1;
+      return true;
+    case EK::Literal:
+      if (e->chars.size() != 1 || e->casei || e->chars[0] >= 0x80) return false;
+      cls[e->chars[0]] = 1;
+      return true;
+    case EK::ClassBytes:
+      if (e->bcls.empty()) return false;
+      for (const BRange &r : e->bcls)
+        for (uint32_t b = r.lo; b <= r.hi; ++b) cls[b] = 1;
+      return true;
+    case EK::Class:
+      if (e->cls.empty()) return false;
+      for (const CRange &r : e->cls)
+        if (r.hi >= 0x80) return false;
+      for (const CRange &r : e->cls)
+        for (uint32_t b = r.lo; b <= r.hi; ++b) cls[b] = 1;
+      return true;
+    case EK::AnyByte:
+      std::memset(cls, 1, 256);
+      return true;
+    case EK::AnyByteNoNL:
+      std::memset(cls, 1, 256);
+      cls['\n'] = 0;
+      return true;
+    default:
+      return false;
+  }
 }
 
 // The lexer table of FwdDfaDev::lex_image (iter_spec_lex_tile_kernel).

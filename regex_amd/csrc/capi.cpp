@@ -161,6 +161,7 @@ rure *rure_compile(const uint8_t *pattern, size_t length, uint32_t flags, rure_o
   if (!compile_program(es, o, &re->rev, &err)) { if (error) error->msg = err; return nullptr; }
   re->fwd.dfa_size_limit = re->rev.dfa_size_limit = re->opts.dfa_size_limit;
   re->xl = exec_literals(re->expr);
+  re->cls_one_ok = class_one_set(re->expr, re->cls_one);
   handle_created();
   return re.release();
 }
@@ -662,11 +663,28 @@ int rure_amd_replace_batch(rure *re, const rure_amd_batch *batch, const uint8_t 
   DevTables *t = regex_device(re, &err);
   if (!t) return err.rfind("HIP", 0) == 0 ? RURE_AMD_ERR_HIP : RURE_AMD_ERR_DFA;
   if (!t->has_dfa && !re->nfa_ok) return RURE_AMD_ERR_DFA;
+  const uint64_t lim = limit == 0 ? ~0ull : (uint64_t)limit;  // replacen: 0 = all
+  // a regex whose matches are single bytes of one class, replace_all over
+  // one haystack: no match list (launch_replace_class); no synchronisation
+  if (re->cls_one_ok && b.count == 1 && !b.offs && b.start == 0 && lim == ~0ull && rep_len >= 1 && rep_len <= 64 &&
+      knob(Knob::ReplaceGeneric) != 1) {
+    uint8_t *dt = nullptr;
+    hipError_t e = scratch_malloc((void **)&dt, 256 + 64, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(dt, re->cls_one, 256, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(dt + 256, rep, rep_len, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess)
+      e = launch_replace_class(b.hay, b.length, dt, dt + 256, (uint32_t)rep_len, out, out_capacity, out_offsets, total,
+                               st, t->cus);
+    if (dt) { const hipError_t e2 = scratch_free(dt, st); if (e == hipSuccess) e = e2; }
+    if (e != hipErrorNotSupported) {
+      if (e == hipSuccess) note_fwd_path(-23);
+      return e == hipSuccess ? RURE_AMD_OK : RURE_AMD_ERR_HIP;
+    }
+  }
   IterBufs ib;
   int64_t *shift = nullptr;
   uint64_t *olen = nullptr;
   uint8_t *drep = nullptr;
-  const uint64_t lim = limit == 0 ? ~0ull : (uint64_t)limit;  // replacen: 0 = all
   hipError_t e = iter_to_device(re, t, b, st, &ib, &err);
   if (e == hipSuccess) e = scratch_malloc((void **)&shift, std::max<uint64_t>(ib.nm, 1) * 8, st);
   if (e == hipSuccess) e = scratch_malloc((void **)&olen, (b.count + 1) * 8, st);
@@ -830,6 +848,12 @@ int rure_amd_run_class_export(rure *re, int ascii, uint8_t *cls) {
   const bool ok = ascii ? re->run_a_ok : re->run_ok;
   if (ok && cls) memcpy(cls, ascii ? re->run_cls_a : re->run_cls, 256);
   return ok ? 1 : 0;
+}
+
+int rure_amd_class_one_export(rure *re, uint8_t *cls) {
+  if (!re) return RURE_AMD_ERR_ARG;
+  if (re->cls_one_ok && cls) memcpy(cls, re->cls_one, 256);
+  return re->cls_one_ok ? 1 : 0;
 }
 
 int rure_amd_run_cp_export(rure *re, uint32_t *bits, size_t n) {

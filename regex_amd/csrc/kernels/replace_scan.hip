@@ -588,6 +588,178 @@ int grid_for_items(uint64_t items, int threads, int cus) {
   return (int)(g < 1 ? 1 : g);
 }
 
+
+// ---------------------------------------------- one byte class, replace_all
+// A regex whose every match is one byte of a class C (`B`, `[KM]`; host
+// class_replace_set) has as find_iter the positions of the C bytes, so its
+// replace_all needs no match list: the output of input unit u (kClsUnit bytes)
+// starts at u kClsUnit + (L - 1) (C bytes before the unit), a prefix sum of
+// per-unit counts.  Pass 1 counts; pass 2 (a wave per unit) stages the unit's
+// bytes and per-lane layout in LDS and writes the unit's output range: the
+// 16-byte blocks inside it from LDS (a block in a stretch without a
+// replacement is one unaligned 16-byte read of the staged text), the partial
+// blocks at its two edges byte by byte (they share an aligned block with the
+// neighbouring units' edges: byte stores do not race).
+constexpr uint32_t kClsUnit = 4096;  // bytes per unit: 64 lanes x 64
+
+__device__ __forceinline__ uint64_t cls_mask(const uint8_t *cls, const uint4 *v, uint32_t avail) {
+  uint64_t m = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t w[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const uint32_t pos = 16 * j + i;
+      const uint32_t c = cls[(w[i >> 2] >> (8 * (i & 3))) & 0xFF];
+      m |= (uint64_t)(pos < avail ? c : 0u) << pos;
+    }
+  }
+  return m;
+}
+
+__device__ __forceinline__ void cls_load(const uint8_t *hay, uint64_t n, uint64_t s0, uint4 *v, uint32_t *avail) {
+  const uint64_t a = s0 < n ? n - s0 : 0;
+  *avail = a > 64 ? 64u : (uint32_t)a;
+  const uint4 *q = (const uint4 *)(hay + s0);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = 16u * j < *avail ? q[j] : make_uint4(0, 0, 0, 0);
+}
+
+__global__ __launch_bounds__(256) void replace_cls_count_kernel(const uint8_t *hay, uint64_t n, const uint8_t *cls_g,
+                                                                uint64_t nunits, uint64_t *ucount) {
+  __shared__ uint8_t cls[256];
+  cls[threadIdx.x] = cls_g[threadIdx.x];
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t nw = (uint64_t)gridDim.x * 4;
+  for (uint64_t u = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); u < nunits; u += nw) {
+    uint4 v[4];
+    uint32_t avail;
+    cls_load(hay, n, u * kClsUnit + 64 * (uint64_t)lane, v, &avail);
+    uint32_t k = (uint32_t)__popcll(cls_mask(cls, v, avail));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) k += __shfl_xor(k, o);
+    if (lane == 0) ucount[u] = k;
+  }
+}
+
+// total (device) = the output length; out_offsets = {0, total}
+__global__ void replace_cls_total_kernel(uint64_t n, uint64_t rep_len, const uint64_t *uoff, uint64_t nunits,
+                                         uint64_t *ooff, uint64_t *total) {
+  const uint64_t t = n + uoff[nunits] * rep_len - uoff[nunits];
+  ooff[0] = 0;
+  ooff[1] = t;
+  *total = t;
+}
+
+// The output byte at unit-relative output position r (< the unit's output
+// length): lane x = the lane whose output chunk holds it (rel[x] <= r), then
+// within its 64 input bytes the replacement or text byte (its C bytes in
+// ascending order: at most a few).
+__device__ __forceinline__ uint8_t cls_out_byte(uint32_t r, const uint32_t *rel, const uint64_t *msk,
+                                                const uint8_t *txt, const uint8_t *rep, uint32_t L) {
+  uint32_t x = min(r >> 6, 63u);
+  while (x > 0 && rel[x] > r) --x;
+  uint32_t p = r - rel[x];
+  uint64_t m = msk[x];
+  uint32_t cnt = 0;
+  while (m) {
+    const uint32_t c = (uint32_t)__builtin_ctzll(m);
+    m &= m - 1;
+    const uint32_t oc = c + (L - 1) * cnt;  // the output offset of C byte c in the chunk
+    if (oc > p) break;
+    if (p < oc + L) return rep[p - oc];
+    ++cnt;
+  }
+  return txt[64 * x + p - (L - 1) * cnt];
+}
+
+// 16 bytes of the staged text from byte offset o (o + 16 <= kClsUnit + 16:
+// the stage has 16 spare bytes).
+__device__ __forceinline__ uint4 lds16u(const uint8_t *txt, uint32_t o) {
+  const uint32_t *w = (const uint32_t *)(txt + (o & ~3u));
+  const uint32_t sh = 8 * (o & 3);
+  const uint32_t a = w[0], b = w[1], c = w[2], d = w[3], e = w[4];
+  return make_uint4(__builtin_amdgcn_alignbit(b, a, sh), __builtin_amdgcn_alignbit(c, b, sh),
+                    __builtin_amdgcn_alignbit(d, c, sh), __builtin_amdgcn_alignbit(e, d, sh));
+}
+
+__global__ __launch_bounds__(256) void replace_cls_write_kernel(const uint8_t *hay, uint64_t n, const uint8_t *cls_g,
+                                                                uint64_t nunits, const uint64_t *uoff,
+                                                                const uint8_t *rep_g, uint32_t L, uint8_t *out,
+                                                                uint64_t cap) {
+  __shared__ uint8_t cls[256];
+  __shared__ uint8_t rep[64];
+  __shared__ __attribute__((aligned(16))) uint8_t stage[4][kClsUnit + 32];
+  __shared__ uint32_t srel[4][65];
+  __shared__ uint64_t smsk[4][64];
+  cls[threadIdx.x] = cls_g[threadIdx.x];
+  if (threadIdx.x < 64) rep[threadIdx.x] = threadIdx.x < L ? rep_g[threadIdx.x] : 0;
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint8_t *txt = stage[w];
+  uint32_t *rel = srel[w];
+  uint64_t *msk = smsk[w];
+  const uint64_t nw = (uint64_t)gridDim.x * 4;
+  for (uint64_t u = (uint64_t)blockIdx.x * 4 + w; u < nunits; u += nw) {
+    uint4 v[4];
+    uint32_t avail;
+    cls_load(hay, n, u * kClsUnit + 64 * (uint64_t)lane, v, &avail);
+    const uint64_t m = cls_mask(cls, v, avail);
+    const uint32_t k = (uint32_t)__popcll(m);
+    const uint32_t len = avail + (L - 1) * k;  // this lane's output bytes
+    uint32_t incl = len;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t x = __shfl_up(incl, o);
+      if (lane >= (uint32_t)o) incl += x;
+    }
+    const uint32_t T = __shfl(incl, 63);  // the unit's output bytes
+#pragma unroll
+    for (int j = 0; j < 4; ++j) *(uint4 *)(txt + 64 * lane + 16 * j) = v[j];
+    if (lane == 0) *(uint4 *)(txt + kClsUnit) = make_uint4(0, 0, 0, 0);
+    rel[lane] = incl - len;
+    msk[lane] = m;
+    if (lane == 63) rel[64] = T;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint64_t ob = u * kClsUnit + uoff[u] * (L - 1);  // the unit's output start
+    const uint64_t A = (ob + 15) & ~(uint64_t)15, E = ob + T, B = E & ~(uint64_t)15;
+    // whole aligned blocks
+    if (B > A) {
+      for (uint64_t q = A + 16 * (uint64_t)lane; q < B; q += 1024) {
+        const uint32_t r = (uint32_t)(q - ob);
+        if (q + 16 > cap) {  // the output buffer ends inside this block
+          for (uint32_t j = 0; q + j < cap; ++j) out[q + j] = cls_out_byte(r + j, rel, msk, txt, rep, L);
+          break;
+        }
+        uint32_t x = min(r >> 6, 63u);
+        while (x > 0 && rel[x] > r) --x;
+        uint4 o;
+        if (msk[x] == 0 && r + 16 <= rel[x + 1]) {  // inside one lane's text stretch
+          o = lds16u(txt, 64 * x + (r - rel[x]));
+        } else {
+          uint32_t b[4] = {0, 0, 0, 0};
+#pragma unroll 1
+          for (uint32_t j = 0; j < 16; ++j)
+            b[j >> 2] |= (uint32_t)cls_out_byte(r + j, rel, msk, txt, rep, L) << (8 * (j & 3));
+          o = make_uint4(b[0], b[1], b[2], b[3]);
+        }
+        *(uint4 *)(out + q) = o;
+      }
+    }
+    // the edges: [ob, min(A, E)) and [max(B, A), E), byte by byte
+    const uint64_t h1 = min(A, E), t0 = max(B, A);
+    const uint64_t pos = lane < 16 ? ob + lane : t0 + (lane - 16);
+    const bool mine = lane < 16 ? pos < h1 : (lane < 32 && pos < E);
+    if (mine && pos < cap) out[pos] = cls_out_byte((uint32_t)(pos - ob), rel, msk, txt, rep, L);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
 }  // namespace
 
 hipError_t exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, hipStream_t st) {
@@ -701,6 +873,38 @@ hipError_t launch_split(const BatchDev &b, const uint64_t *counts, const uint64_
   hipLaunchKernelGGL(split_emit_kernel, dim3(grid_for_items(nmatches + b.count, 256, cus)), dim3(256), 0, st, b,
                      counts, moff, m, lim, foff, pieces, cap);
   return hipGetLastError();
+}
+
+
+// replace_all of a one-byte-class regex over one haystack (16-byte aligned,
+// search from 0): cls[256] (device) = the class, rep (device) at most 64
+// bytes.  Writes out (at most cap bytes), out_offsets {0, total}, *total.
+hipError_t launch_replace_class(const uint8_t *hay, uint64_t n, const uint8_t *cls, const uint8_t *rep,
+                                uint32_t rep_len, uint8_t *out, uint64_t cap, uint64_t *ooff, uint64_t *total,
+                                hipStream_t st, int cus) {
+  if (((uintptr_t)hay & 15) || rep_len > 64 || rep_len == 0) return hipErrorNotSupported;
+  const uint64_t nunits = std::max<uint64_t>(1, (n + kClsUnit - 1) / kClsUnit);
+  uint64_t *buf = nullptr;
+  hipError_t e = scratch_malloc((void **)&buf, (2 * nunits + 2) * 8, st);
+  if (e != hipSuccess) return e;
+  uint64_t *ucount = buf, *uoff = buf + nunits + 1;
+  const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((nunits + 3) / 4, (uint64_t)cus * 8));
+  do {
+    if ((e = hipMemsetAsync(ucount + nunits, 0, 8, st)) != hipSuccess) break;
+    hipLaunchKernelGGL(replace_cls_count_kernel, dim3(grid), dim3(256), 0, st, hay, n, cls, nunits, ucount);
+    if ((e = hipGetLastError()) != hipSuccess) break;
+    if ((e = exclusive_scan_u64(ucount, uoff, nunits + 1, st)) != hipSuccess) break;
+    hipLaunchKernelGGL(replace_cls_total_kernel, dim3(1), dim3(1), 0, st, n, (uint64_t)rep_len, uoff, nunits, ooff,
+                       total);
+    if ((e = hipGetLastError()) != hipSuccess) break;
+    if (cap) {
+      hipLaunchKernelGGL(replace_cls_write_kernel, dim3(grid), dim3(256), 0, st, hay, n, cls, nunits, uoff, rep,
+                         rep_len, out, cap);
+      e = hipGetLastError();
+    }
+  } while (false);
+  hipError_t e2 = scratch_free(buf, st);
+  return e != hipSuccess ? e : e2;
 }
 
 }  // namespace rure_amd

@@ -260,6 +260,9 @@ struct rure {
   // find_iter DFA over all bytes and for its ASCII shadow
   bool run_ok = false, run_a_ok = false;
   std::vector<uint32_t> run_cp;  // Unicode C+: C's code point bitmap (0x110000 bits), else empty
+  // every match is one byte of a class (class_replace_set): cls_one[b] = b in it
+  bool cls_one_ok = false;
+  uint8_t cls_one[256] = {0};
   uint8_t run_cls[256] = {0}, run_cls_a[256] = {0};
   std::map<int, std::pair<void *, FwdDfaDev>> iter_dev_a;
 };
@@ -379,6 +382,7 @@ int set_batch_group(rure_set *g, const rure_amd_batch *batch, const BatchDev &b,
 hipError_t run_find_iter(rure *re, DevTables *t, const BatchDev &b, const IterOut &o, hipStream_t st,
                          std::string *err, const IterSpan *sp = nullptr);
 hipError_t iter_to_device(rure *re, DevTables *t, const BatchDev &b, hipStream_t st, IterBufs *ib, std::string *err);
+bool class_one_set(const Expr &e, uint8_t cls[256]);
 bool build_kmer(rure *const *res, size_t n, std::vector<uint32_t> *bitmap, std::vector<uint16_t> *mask,
                 std::vector<uint16_t> *hmask, KmerDev *km);
 bool kmer_device(rure *const *res, size_t n, KmerDev *out);
