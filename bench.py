@@ -236,13 +236,20 @@ def profiled_traffic(config, b_alg, kernel=None):
         except (OSError, ValueError):
             continue
         strip = lambda c: {k: v for k, v in (c or {}).items() if k != "parallelism"}
-        if strip(d.get("bench_config")) != strip(config) or not d.get("hbm_read_bytes_per_launch"):
+        if strip(d.get("bench_config")) != strip(config):
             continue
-        if kernel is not None and kernel not in (d.get("kernel") or ""):
-            continue
-        key = (d.get("generated_utc", ""), os.path.basename(p))
-        if best is None or key >= best[0]:
-            best = (key, p, d)
+        # the summary's dominant kernel, or one of its per-roofline entries
+        # (launches of the workload's grid only: C3's strip lexer)
+        cands = [d] + list((d.get("rooflines") or {}).values())
+        for e in cands:
+            if not e.get("hbm_read_bytes_per_launch"):
+                continue
+            if kernel is not None and kernel not in (e.get("kernel") or ""):
+                continue
+            key = (d.get("generated_utc", ""), os.path.basename(p))
+            if best is None or key >= best[0]:
+                best = (key, p, e)
+            break
     if best is None:
         return None
     d = best[2]

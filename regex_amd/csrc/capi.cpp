@@ -672,9 +672,16 @@ int rure_amd_replace_batch(rure *re, const rure_amd_batch *batch, const uint8_t 
     hipError_t e = scratch_malloc((void **)&dt, 256 + 64, st);
     if (e == hipSuccess) e = hipMemcpyAsync(dt, re->cls_one, 256, hipMemcpyHostToDevice, st);
     if (e == hipSuccess) e = hipMemcpyAsync(dt + 256, rep, rep_len, hipMemcpyHostToDevice, st);
+    // (a class of one or two bytes: SWAR compares instead of the table; byte
+    // 0 can not be a repeated compare value, it would read as "no class")
+    uint32_t sw[2] = {0, 0}, nb = 0;
+    for (int c = 1; c < 256 && nb <= 2; ++c)
+      if (re->cls_one[c]) { if (nb < 2) sw[nb] = (uint32_t)c * 0x01010101u; ++nb; }
+    if (re->cls_one[0] || nb > 2) sw[0] = sw[1] = 0;
+    else if (nb == 1) sw[1] = sw[0];
     if (e == hipSuccess)
       e = launch_replace_class(b.hay, b.length, dt, dt + 256, (uint32_t)rep_len, out, out_capacity, out_offsets, total,
-                               st, t->cus);
+                               st, t->cus, sw[0], sw[1]);
     if (dt) { const hipError_t e2 = scratch_free(dt, st); if (e == hipSuccess) e = e2; }
     if (e != hipErrorNotSupported) {
       if (e == hipSuccess) note_fwd_path(-23);

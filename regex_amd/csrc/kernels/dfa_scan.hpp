@@ -267,9 +267,11 @@ hipError_t launch_replace_copy(const BatchDev &b, const uint64_t *ooff, const ui
 // replace_all of a regex whose matches are single bytes of one class over
 // one 16-byte aligned haystack (replace_scan.hip); hipErrorNotSupported if
 // the replacement is empty or longer than 64 bytes.
+// sw1 / sw2: a class of at most two bytes (byte * 0x01010101; sw2 = sw1 for
+// one byte), else 0 (the cls table).
 hipError_t launch_replace_class(const uint8_t *hay, uint64_t n, const uint8_t *cls, const uint8_t *rep,
                                 uint32_t rep_len, uint8_t *out, uint64_t cap, uint64_t *ooff, uint64_t *total,
-                                hipStream_t st, int cus);
+                                hipStream_t st, int cus, uint32_t sw1, uint32_t sw2);
 hipError_t launch_split(const BatchDev &b, const uint64_t *counts, const uint64_t *moff, const uint64_t *m,
                         uint64_t lim, uint64_t *fields, uint64_t *foff, uint64_t *pieces, uint64_t cap,
                         uint64_t nmatches, hipStream_t st, int cus);

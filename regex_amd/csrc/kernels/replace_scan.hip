@@ -458,6 +458,43 @@ __global__ __launch_bounds__(256) void replace_copy4_kernel(CopyCtx c, uint8_t *
       const uint64_t p0 = (w0 + (id >> 6)) * kWin + 16 * (uint64_t)(id & 63);
       const uint32_t a = group_passed(R, (uint32_t)cnt, p0);
       const uint64_t jj = lo + a;
+      // deletions (rep_len 0, the regex-dna strip: an edge every ~61 bytes):
+      // the block is at most four text stretches, each one unaligned 16-byte
+      // load at the source of the block's byte 0 had the stretch covered it,
+      // merged by byte masks — 8 aligned loads and ~30 VALU instead of 16
+      // dependent-free byte loads and their selects
+      if (c.rep_len == 0 && p0 + 16 <= total && R[a + 4] > p0 + 15) {
+        int64_t bs[4];
+        uint32_t k[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint64_t Rq = R[a + q];
+          const bool in = q == 0 || Rq <= p0 + 15;  // the stretch after match a + q starts in the block
+          k[q] = q == 0 ? 0u : in ? (uint32_t)(Rq - p0) : 16u;
+          bs[q] = q == 0 && jj == 0 ? (int64_t)p0 : in ? (int64_t)(E[a + q] - Rq + p0) : (int64_t)p0;
+        }
+        if (bs[0] >= 0 && bs[1] >= 0 && bs[2] >= 0 && bs[3] >= 0) {
+          uint4 t[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) t[q] = load16u_nb(hay + bs[q]);
+          uint32_t x[4];
+#pragma unroll
+          for (int d = 0; d < 4; ++d) {
+            uint32_t r = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const uint32_t word = d == 0 ? t[q].x : d == 1 ? t[q].y : d == 2 ? t[q].z : t[q].w;
+              // bytes of dword d at or after k[q] (the later stretches overwrite)
+              const int lo = (int)k[q] - 4 * d;
+              const uint32_t ge = lo <= 0 ? 0xFFFFFFFFu : lo >= 4 ? 0u : 0xFFFFFFFFu << (8 * lo);
+              r = (r & ~ge) | (word & ge);
+            }
+            x[d] = r;
+          }
+          *(uint4 *)(out + p0) = make_uint4(x[0], x[1], x[2], x[3]);
+          continue;
+        }
+      }
       if (p0 + 16 <= total && R[a + 4] > p0 + 15) {
         // at most three replacement starts in the block: each byte's source
         // from the staged records, the 16 byte loads independent
@@ -601,8 +638,32 @@ int grid_for_items(uint64_t items, int threads, int cus) {
 // blocks at its two edges byte by byte (they share an aligned block with the
 // neighbouring units' edges: byte stores do not race).
 constexpr uint32_t kClsUnit = 4096;  // bytes per unit: 64 lanes x 64
+constexpr uint32_t kClsSlow = 512;   // a wave's list of blocks that meet a replacement
 
-__device__ __forceinline__ uint64_t cls_mask(const uint8_t *cls, const uint4 *v, uint32_t avail) {
+// bit 7 of each byte of w equal to the byte of rep (rep = byte * 0x01010101;
+// exact: no borrow between bytes)
+__device__ __forceinline__ uint32_t eq_bytes(uint32_t w, uint32_t rep) {
+  const uint32_t x = w ^ rep;
+  return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+}
+
+// sw1 / sw2: a class of at most two bytes as repeated bytes (sw1 = 0: use the
+// table): four bytes' bits per SWAR compare instead of a table read per byte
+__device__ __forceinline__ uint64_t cls_mask(const uint8_t *cls, const uint4 *v, uint32_t avail, uint32_t sw1,
+                                             uint32_t sw2) {
+  if (sw1) {
+    uint64_t m = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t w[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const uint32_t z = (eq_bytes(w[d], sw1) | eq_bytes(w[d], sw2)) >> 7;  // bits 0, 8, 16, 24
+        m |= (uint64_t)((z * 0x01020408u) >> 24 & 0xFu) << (16 * j + 4 * d);
+      }
+    }
+    return avail >= 64 ? m : m & ((1ull << avail) - 1ull);
+  }
   uint64_t m = 0;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -617,16 +678,19 @@ __device__ __forceinline__ uint64_t cls_mask(const uint8_t *cls, const uint4 *v,
   return m;
 }
 
+// (loads without a branch: absent blocks re-read the haystack's first block
+// and are masked off by avail in cls_mask, so a prefetch's loads stay in
+// flight past this call)
 __device__ __forceinline__ void cls_load(const uint8_t *hay, uint64_t n, uint64_t s0, uint4 *v, uint32_t *avail) {
   const uint64_t a = s0 < n ? n - s0 : 0;
   *avail = a > 64 ? 64u : (uint32_t)a;
-  const uint4 *q = (const uint4 *)(hay + s0);
 #pragma unroll
-  for (int j = 0; j < 4; ++j) v[j] = 16u * j < *avail ? q[j] : make_uint4(0, 0, 0, 0);
+  for (int j = 0; j < 4; ++j) v[j] = *(const uint4 *)(16u * j < *avail ? hay + s0 + 16 * j : hay);
 }
 
 __global__ __launch_bounds__(256) void replace_cls_count_kernel(const uint8_t *hay, uint64_t n, const uint8_t *cls_g,
-                                                                uint64_t nunits, uint64_t *ucount) {
+                                                                uint64_t nunits, uint64_t *ucount, uint32_t sw1,
+                                                                uint32_t sw2) {
   __shared__ uint8_t cls[256];
   cls[threadIdx.x] = cls_g[threadIdx.x];
   __syncthreads();
@@ -636,7 +700,7 @@ __global__ __launch_bounds__(256) void replace_cls_count_kernel(const uint8_t *h
     uint4 v[4];
     uint32_t avail;
     cls_load(hay, n, u * kClsUnit + 64 * (uint64_t)lane, v, &avail);
-    uint32_t k = (uint32_t)__popcll(cls_mask(cls, v, avail));
+    uint32_t k = (uint32_t)__popcll(cls_mask(cls, v, avail, sw1, sw2));
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) k += __shfl_xor(k, o);
     if (lane == 0) ucount[u] = k;
@@ -684,15 +748,52 @@ __device__ __forceinline__ uint4 lds16u(const uint8_t *txt, uint32_t o) {
                     __builtin_amdgcn_alignbit(d, c, sh), __builtin_amdgcn_alignbit(e, d, sh));
 }
 
+// The 16 output bytes from unit-relative output position r with a running
+// state (the lane chunk, its C bytes passed), for blocks that meet a
+// replacement: ~10 VALU per byte instead of a search per byte.
+__device__ __forceinline__ uint4 cls_block_slow(uint32_t r, uint32_t T, const uint32_t *rel, const uint64_t *msk,
+                                                const uint8_t *txt, const uint8_t *rep, uint32_t L) {
+  uint32_t x = min(r >> 6, 63u);
+  while (x > 0 && rel[x] > r) --x;
+  uint32_t p = r - rel[x], lenx = rel[x + 1] - rel[x], cnt = 0;
+  uint64_t m = msk[x];
+  // next C byte of the chunk and its output offset (none: past the chunk)
+  uint32_t cn = m ? (uint32_t)__builtin_ctzll(m) : 64u, ocn = cn;
+  uint32_t b[4] = {0, 0, 0, 0};
+#pragma unroll 1
+  for (uint32_t j = 0; j < 16 && r + j < T; ++j) {
+    while (p >= lenx) {  // into the next lane's chunk
+      p -= lenx;
+      ++x;
+      lenx = rel[x + 1] - rel[x];
+      m = msk[x];
+      cnt = 0;
+      cn = m ? (uint32_t)__builtin_ctzll(m) : 64u;
+      ocn = cn;
+    }
+    while (m && p >= ocn + L) {  // past C byte cn's replacement
+      m &= m - 1;
+      ++cnt;
+      cn = m ? (uint32_t)__builtin_ctzll(m) : 64u;
+      ocn = cn + (L - 1) * cnt;
+    }
+    const uint32_t ch = (m && p >= ocn) ? rep[p - ocn] : txt[64 * x + p - (L - 1) * cnt];
+    b[j >> 2] |= ch << (8 * (j & 3));
+    ++p;
+  }
+  return make_uint4(b[0], b[1], b[2], b[3]);
+}
+
 __global__ __launch_bounds__(256) void replace_cls_write_kernel(const uint8_t *hay, uint64_t n, const uint8_t *cls_g,
                                                                 uint64_t nunits, const uint64_t *uoff,
                                                                 const uint8_t *rep_g, uint32_t L, uint8_t *out,
-                                                                uint64_t cap) {
+                                                                uint64_t cap, uint32_t sw1, uint32_t sw2) {
   __shared__ uint8_t cls[256];
   __shared__ uint8_t rep[64];
   __shared__ __attribute__((aligned(16))) uint8_t stage[4][kClsUnit + 32];
-  __shared__ uint32_t srel[4][65];
-  __shared__ uint64_t smsk[4][64];
+  __shared__ uint32_t srel[4][66];
+  __shared__ uint64_t smsk[4][65];
+  __shared__ uint16_t sslow[4][kClsSlow];
   cls[threadIdx.x] = cls_g[threadIdx.x];
   if (threadIdx.x < 64) rep[threadIdx.x] = threadIdx.x < L ? rep_g[threadIdx.x] : 0;
   __syncthreads();
@@ -700,12 +801,13 @@ __global__ __launch_bounds__(256) void replace_cls_write_kernel(const uint8_t *h
   uint8_t *txt = stage[w];
   uint32_t *rel = srel[w];
   uint64_t *msk = smsk[w];
+  uint16_t *slow = sslow[w];
   const uint64_t nw = (uint64_t)gridDim.x * 4;
   for (uint64_t u = (uint64_t)blockIdx.x * 4 + w; u < nunits; u += nw) {
     uint4 v[4];
     uint32_t avail;
     cls_load(hay, n, u * kClsUnit + 64 * (uint64_t)lane, v, &avail);
-    const uint64_t m = cls_mask(cls, v, avail);
+    const uint64_t m = cls_mask(cls, v, avail, sw1, sw2);
     const uint32_t k = (uint32_t)__popcll(m);
     const uint32_t len = avail + (L - 1) * k;  // this lane's output bytes
     uint32_t incl = len;
@@ -720,33 +822,69 @@ __global__ __launch_bounds__(256) void replace_cls_write_kernel(const uint8_t *h
     if (lane == 0) *(uint4 *)(txt + kClsUnit) = make_uint4(0, 0, 0, 0);
     rel[lane] = incl - len;
     msk[lane] = m;
-    if (lane == 63) rel[64] = T;
+    if (lane == 63) { rel[64] = T; rel[65] = T; msk[64] = 0; }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const uint64_t ob = u * kClsUnit + uoff[u] * (L - 1);  // the unit's output start
     const uint64_t A = (ob + 15) & ~(uint64_t)15, E = ob + T, B = E & ~(uint64_t)15;
-    // whole aligned blocks
-    if (B > A) {
-      for (uint64_t q = A + 16 * (uint64_t)lane; q < B; q += 1024) {
+    // whole aligned blocks: a block in one text stretch (no replacement
+    // byte, the input behind it contiguous) is one unaligned 16-byte read
+    // of the staged text; the others go to the wave's slow list
+    uint32_t ns = 0;
+    for (uint64_t q0 = A; q0 < B; q0 += 1024) {
+      const uint64_t q = q0 + 16 * (uint64_t)lane;
+      bool fast = false, sl = false;
+      if (q < B) {
         const uint32_t r = (uint32_t)(q - ob);
-        if (q + 16 > cap) {  // the output buffer ends inside this block
-          for (uint32_t j = 0; q + j < cap; ++j) out[q + j] = cls_out_byte(r + j, rel, msk, txt, rep, L);
-          break;
-        }
         uint32_t x = min(r >> 6, 63u);
         while (x > 0 && rel[x] > r) --x;
-        uint4 o;
-        if (msk[x] == 0 && r + 16 <= rel[x + 1]) {  // inside one lane's text stretch
-          o = lds16u(txt, 64 * x + (r - rel[x]));
-        } else {
-          uint32_t b[4] = {0, 0, 0, 0};
-#pragma unroll 1
-          for (uint32_t j = 0; j < 16; ++j)
-            b[j >> 2] |= (uint32_t)cls_out_byte(r + j, rel, msk, txt, rep, L) << (8 * (j & 3));
-          o = make_uint4(b[0], b[1], b[2], b[3]);
+        const uint32_t p = r - rel[x];
+        uint64_t mm = msk[x];
+        uint32_t cnt = 0, cn = 64;
+        bool inrep = false;
+        while (mm) {
+          const uint32_t c = (uint32_t)__builtin_ctzll(mm);
+          const uint32_t oc = c + (L - 1) * cnt;
+          if (oc > p) { cn = c; break; }
+          if (p < oc + L) { inrep = true; break; }
+          mm &= mm - 1;
+          ++cnt;
         }
-        *(uint4 *)(out + q) = o;
+        const uint32_t t = p - (L - 1) * cnt;  // input offset of the block's first byte in lane x
+        // the next C byte after it in unit input coordinates
+        uint32_t nxt = 64 * x + cn;
+        if (cn == 64 && x < 63) nxt = msk[x + 1] ? 64 * (x + 1) + (uint32_t)__builtin_ctzll(msk[x + 1]) : 64 * (x + 2);
+        fast = !inrep && 64 * x + t + 16 <= nxt && q + 16 <= cap;
+        if (fast) *(uint4 *)(out + q) = lds16u(txt, 64 * x + t);
+        sl = !fast;
+      }
+      const uint64_t bm = __ballot(sl);
+      if (sl) slow[ns + __popcll(bm & ((1ull << lane) - 1ull))] = (uint16_t)((q - A) >> 4);
+      ns += (uint32_t)__popcll(bm);
+      // the list is worked off when full (a unit dense in replacements of a
+      // long string has up to 256 L blocks) and after the unit's last round
+      if (ns + 64 > kClsSlow || q0 + 1024 >= B) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll 1
+        for (uint32_t i0 = 0; i0 < ns; i0 += 64) {
+          if (i0 + lane < ns) {
+            const uint64_t qs = A + 16 * (uint64_t)slow[i0 + lane];
+            const uint4 o = cls_block_slow((uint32_t)(qs - ob), T, rel, msk, txt, rep, L);
+            if (qs + 16 <= cap) {
+              *(uint4 *)(out + qs) = o;
+            } else {  // the output buffer ends inside this block
+              const uint32_t bb[4] = {o.x, o.y, o.z, o.w};
+              for (uint32_t j = 0; qs + j < cap; ++j) out[qs + j] = (uint8_t)(bb[j >> 2] >> (8 * (j & 3)));
+            }
+          }
+        }
+        ns = 0;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       }
     }
     // the edges: [ob, min(A, E)) and [max(B, A), E), byte by byte
@@ -881,7 +1019,7 @@ hipError_t launch_split(const BatchDev &b, const uint64_t *counts, const uint64_
 // bytes.  Writes out (at most cap bytes), out_offsets {0, total}, *total.
 hipError_t launch_replace_class(const uint8_t *hay, uint64_t n, const uint8_t *cls, const uint8_t *rep,
                                 uint32_t rep_len, uint8_t *out, uint64_t cap, uint64_t *ooff, uint64_t *total,
-                                hipStream_t st, int cus) {
+                                hipStream_t st, int cus, uint32_t sw1, uint32_t sw2) {
   if (((uintptr_t)hay & 15) || rep_len > 64 || rep_len == 0) return hipErrorNotSupported;
   const uint64_t nunits = std::max<uint64_t>(1, (n + kClsUnit - 1) / kClsUnit);
   uint64_t *buf = nullptr;
@@ -891,7 +1029,7 @@ hipError_t launch_replace_class(const uint8_t *hay, uint64_t n, const uint8_t *c
   const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((nunits + 3) / 4, (uint64_t)cus * 8));
   do {
     if ((e = hipMemsetAsync(ucount + nunits, 0, 8, st)) != hipSuccess) break;
-    hipLaunchKernelGGL(replace_cls_count_kernel, dim3(grid), dim3(256), 0, st, hay, n, cls, nunits, ucount);
+    hipLaunchKernelGGL(replace_cls_count_kernel, dim3(grid), dim3(256), 0, st, hay, n, cls, nunits, ucount, sw1, sw2);
     if ((e = hipGetLastError()) != hipSuccess) break;
     if ((e = exclusive_scan_u64(ucount, uoff, nunits + 1, st)) != hipSuccess) break;
     hipLaunchKernelGGL(replace_cls_total_kernel, dim3(1), dim3(1), 0, st, n, (uint64_t)rep_len, uoff, nunits, ooff,
@@ -899,7 +1037,7 @@ hipError_t launch_replace_class(const uint8_t *hay, uint64_t n, const uint8_t *c
     if ((e = hipGetLastError()) != hipSuccess) break;
     if (cap) {
       hipLaunchKernelGGL(replace_cls_write_kernel, dim3(grid), dim3(256), 0, st, hay, n, cls, nunits, uoff, rep,
-                         rep_len, out, cap);
+                         rep_len, out, cap, sw1, sw2);
       e = hipGetLastError();
     }
   } while (false);
