@@ -638,7 +638,7 @@ int grid_for_items(uint64_t items, int threads, int cus) {
 // blocks at its two edges byte by byte (they share an aligned block with the
 // neighbouring units' edges: byte stores do not race).
 constexpr uint32_t kClsUnit = 4096;  // bytes per unit: 64 lanes x 64
-constexpr uint32_t kClsSlow = 512;   // a wave's list of blocks that meet a replacement
+constexpr uint32_t kClsSlow = 256;   // a wave's list of blocks that meet a replacement
 
 // bit 7 of each byte of w equal to the byte of rep (rep = byte * 0x01010101;
 // exact: no borrow between bytes)
@@ -716,6 +716,13 @@ __global__ void replace_cls_total_kernel(uint64_t n, uint64_t rep_len, const uin
   *total = t;
 }
 
+// The staged text is swizzled: the 16-byte piece j of lane c's 64 bytes sits
+// in slot (j + c / 4) % 4, so that a quarter wave's 16-byte stores (and the
+// fast path's reads) fall on distinct banks.  tx: logical -> LDS offset.
+__device__ __forceinline__ uint32_t tx(uint32_t o) {
+  return (o & ~63u) | ((((o >> 4) + (o >> 8)) & 3u) << 4) | (o & 15u);
+}
+
 // The output byte at unit-relative output position r (< the unit's output
 // length): lane x = the lane whose output chunk holds it (rel[x] <= r), then
 // within its 64 input bytes the replacement or text byte (its C bytes in
@@ -735,17 +742,18 @@ __device__ __forceinline__ uint8_t cls_out_byte(uint32_t r, const uint32_t *rel,
     if (p < oc + L) return rep[p - oc];
     ++cnt;
   }
-  return txt[64 * x + p - (L - 1) * cnt];
+  return txt[tx(64 * x + p - (L - 1) * cnt)];
 }
 
-// 16 bytes of the staged text from byte offset o (o + 16 <= kClsUnit + 16:
-// the stage has 16 spare bytes).
+// 16 bytes of the staged text from logical offset o (o + 16 <= kClsUnit +
+// 16: the stage has 16 spare bytes, in no swizzled piece)
 __device__ __forceinline__ uint4 lds16u(const uint8_t *txt, uint32_t o) {
-  const uint32_t *w = (const uint32_t *)(txt + (o & ~3u));
-  const uint32_t sh = 8 * (o & 3);
-  const uint32_t a = w[0], b = w[1], c = w[2], d = w[3], e = w[4];
+  const uint32_t d = o & ~3u, sh = 8 * (o & 3);
+  const uint32_t a = *(const uint32_t *)(txt + tx(d)), b = *(const uint32_t *)(txt + tx(d + 4)),
+                 c = *(const uint32_t *)(txt + tx(d + 8)), e = *(const uint32_t *)(txt + tx(d + 12)),
+                 f = *(const uint32_t *)(txt + tx(d + 16));
   return make_uint4(__builtin_amdgcn_alignbit(b, a, sh), __builtin_amdgcn_alignbit(c, b, sh),
-                    __builtin_amdgcn_alignbit(d, c, sh), __builtin_amdgcn_alignbit(e, d, sh));
+                    __builtin_amdgcn_alignbit(e, c, sh), __builtin_amdgcn_alignbit(f, e, sh));
 }
 
 // The 16 output bytes from unit-relative output position r with a running
@@ -777,33 +785,54 @@ __device__ __forceinline__ uint4 cls_block_slow(uint32_t r, uint32_t T, const ui
       cn = m ? (uint32_t)__builtin_ctzll(m) : 64u;
       ocn = cn + (L - 1) * cnt;
     }
-    const uint32_t ch = (m && p >= ocn) ? rep[p - ocn] : txt[64 * x + p - (L - 1) * cnt];
+    const uint32_t ch = (m && p >= ocn) ? rep[p - ocn] : txt[tx(64 * x + p - (L - 1) * cnt)];
     b[j >> 2] |= ch << (8 * (j & 3));
     ++p;
   }
   return make_uint4(b[0], b[1], b[2], b[3]);
 }
 
-__global__ __launch_bounds__(256) void replace_cls_write_kernel(const uint8_t *hay, uint64_t n, const uint8_t *cls_g,
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// A unit whose output spans at most kClsMap bytes from the aligned block
+// before it gets a block map: per 16-byte output block the C bytes whose
+// replacement starts in an earlier block (prefix of counts) and whether a
+// replacement meets it.  A block no replacement meets is text only, read
+// from staged offset (block start - (L - 1) * C bytes before it).
+constexpr uint32_t kClsMap = 6144;
+constexpr uint32_t kClsCW = kClsMap / 32 / 64;  // a lane's words of the count map
+static_assert(kClsMap % 2048 == 0, "the map is worked by whole lanes");
+
+struct ClsWave {
+  uint8_t txt[kClsUnit + 32];
+  uint32_t cnt[kClsMap / 32];   // per block pair: C bytes starting in the block (low, high half)
+  uint8_t slowb[kClsMap / 16];  // per block: a replacement meets it
+  uint32_t rel[66];
+  uint64_t msk[65];
+  uint16_t slow[kClsSlow];
+};
+
+__global__ __launch_bounds__(256, 6) void replace_cls_write_kernel(const uint8_t *hay, uint64_t n, const uint8_t *cls_g,
                                                                 uint64_t nunits, const uint64_t *uoff,
                                                                 const uint8_t *rep_g, uint32_t L, uint8_t *out,
                                                                 uint64_t cap, uint32_t sw1, uint32_t sw2) {
   __shared__ uint8_t cls[256];
   __shared__ uint8_t rep[64];
-  __shared__ __attribute__((aligned(16))) uint8_t stage[4][kClsUnit + 32];
-  __shared__ uint32_t srel[4][66];
-  __shared__ uint64_t smsk[4][65];
-  __shared__ uint16_t sslow[4][kClsSlow];
+  __shared__ __attribute__((aligned(16))) ClsWave sw[4];
   cls[threadIdx.x] = cls_g[threadIdx.x];
   if (threadIdx.x < 64) rep[threadIdx.x] = threadIdx.x < L ? rep_g[threadIdx.x] : 0;
   __syncthreads();
-  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  uint8_t *txt = stage[w];
-  uint32_t *rel = srel[w];
-  uint64_t *msk = smsk[w];
-  uint16_t *slow = sslow[w];
+  const uint32_t lane = threadIdx.x & 63;
+  ClsWave &W = sw[threadIdx.x >> 6];
   const uint64_t nw = (uint64_t)gridDim.x * 4;
-  for (uint64_t u = (uint64_t)blockIdx.x * 4 + w; u < nunits; u += nw) {
+  for (uint64_t u = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); u < nunits; u += nw) {
+    // stage: the lane's 64 bytes, class mask, output offset in the unit
+    // (loading the next unit here, behind this one's output, was slower:
+    // profiles/r05_replace_class.txt)
     uint4 v[4];
     uint32_t avail;
     cls_load(hay, n, u * kClsUnit + 64 * (uint64_t)lane, v, &avail);
@@ -817,62 +846,110 @@ __global__ __launch_bounds__(256) void replace_cls_write_kernel(const uint8_t *h
       if (lane >= (uint32_t)o) incl += x;
     }
     const uint32_t T = __shfl(incl, 63);  // the unit's output bytes
+    const uint32_t r0 = incl - len;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) *(uint4 *)(txt + 64 * lane + 16 * j) = v[j];
-    if (lane == 0) *(uint4 *)(txt + kClsUnit) = make_uint4(0, 0, 0, 0);
-    rel[lane] = incl - len;
-    msk[lane] = m;
-    if (lane == 63) { rel[64] = T; rel[65] = T; msk[64] = 0; }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int j = 0; j < 4; ++j) *(uint4 *)(W.txt + tx(64 * lane + 16 * j)) = v[j];
+    if (lane == 0) *(uint4 *)(W.txt + kClsUnit) = make_uint4(0, 0, 0, 0);
+    W.rel[lane] = r0;
+    W.msk[lane] = m;
+    if (lane == 63) { W.rel[64] = T; W.rel[65] = T; W.msk[64] = 0; }
     const uint64_t ob = u * kClsUnit + uoff[u] * (L - 1);  // the unit's output start
-    const uint64_t A = (ob + 15) & ~(uint64_t)15, E = ob + T, B = E & ~(uint64_t)15;
-    // whole aligned blocks: a block in one text stretch (no replacement
-    // byte, the input behind it contiguous) is one unaligned 16-byte read
-    // of the staged text; the others go to the wave's slow list
+    const uint32_t o15 = (uint32_t)(ob & 15);
+    const bool map = o15 + T + 16 <= kClsMap;
+    if (map) {
+#pragma unroll
+      for (uint32_t i = 0; i < kClsCW; ++i) W.cnt[kClsCW * lane + i] = 0;
+#pragma unroll
+      for (uint32_t i = 0; i < kClsCW; ++i) *(uint16_t *)(W.slowb + 2 * (kClsCW * lane + i)) = 0;
+      wave_sync();
+      uint64_t mm = m;
+      uint32_t P = o15 + r0;  // output offset of the next C byte from the aligned base, less c
+      while (mm) {
+        const uint32_t c = (uint32_t)__builtin_ctzll(mm);
+        mm &= mm - 1;
+        const uint32_t q = P + c;
+        atomicAdd(&W.cnt[q >> 5], (q & 16) ? 0x10000u : 1u);
+        for (uint32_t bb = q >> 4; bb <= (q + L - 1) >> 4; ++bb) W.slowb[bb] = 1;
+        P += L - 1;
+      }
+      wave_sync();
+      // exclusive prefix over the blocks (lane: words kClsCW lane ..)
+      uint32_t cw[kClsCW];
+#pragma unroll
+      for (uint32_t i = 0; i < kClsCW; ++i) cw[i] = W.cnt[kClsCW * lane + i];
+      uint32_t tot = 0;
+#pragma unroll
+      for (uint32_t i = 0; i < kClsCW; ++i) tot += (cw[i] & 0xFFFF) + (cw[i] >> 16);
+      uint32_t ex = tot;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t x = __shfl_up(ex, o);
+        if (lane >= (uint32_t)o) ex += x;
+      }
+      ex -= tot;
+#pragma unroll
+      for (uint32_t i = 0; i < kClsCW; ++i) {
+        const uint32_t lo = ex;
+        ex += cw[i] & 0xFFFF;
+        W.cnt[kClsCW * lane + i] = lo | ex << 16;
+        ex += cw[i] >> 16;
+      }
+    }
+    wave_sync();
+    const uint64_t base = ob - o15, A = (ob + 15) & ~(uint64_t)15, E = ob + T, B = E & ~(uint64_t)15;
+    // whole aligned blocks: text-only blocks from the staged text, the
+    // others to the wave's slow list
     uint32_t ns = 0;
     for (uint64_t q0 = A; q0 < B; q0 += 1024) {
       const uint64_t q = q0 + 16 * (uint64_t)lane;
-      bool fast = false, sl = false;
+      bool sl = false;
       if (q < B) {
         const uint32_t r = (uint32_t)(q - ob);
-        uint32_t x = min(r >> 6, 63u);
-        while (x > 0 && rel[x] > r) --x;
-        const uint32_t p = r - rel[x];
-        uint64_t mm = msk[x];
-        uint32_t cnt = 0, cn = 64;
-        bool inrep = false;
-        while (mm) {
-          const uint32_t c = (uint32_t)__builtin_ctzll(mm);
-          const uint32_t oc = c + (L - 1) * cnt;
-          if (oc > p) { cn = c; break; }
-          if (p < oc + L) { inrep = true; break; }
-          mm &= mm - 1;
-          ++cnt;
+        bool fast;
+        uint32_t src;
+        if (map) {
+          const uint32_t bl = (uint32_t)(q - base) >> 4;
+          fast = !W.slowb[bl];
+          src = r - (L - 1) * ((W.cnt[bl >> 1] >> (16 * (bl & 1))) & 0xFFFF);
+        } else {
+          uint32_t x = min(r >> 6, 63u);
+          while (x > 0 && W.rel[x] > r) --x;
+          const uint32_t p = r - W.rel[x];
+          uint64_t mm = W.msk[x];
+          uint32_t cnt = 0, cn = 64;
+          bool inrep = false;
+          while (mm) {
+            const uint32_t c = (uint32_t)__builtin_ctzll(mm);
+            const uint32_t oc = c + (L - 1) * cnt;
+            if (oc > p) { cn = c; break; }
+            if (p < oc + L) { inrep = true; break; }
+            mm &= mm - 1;
+            ++cnt;
+          }
+          const uint32_t t = p - (L - 1) * cnt;  // input offset of the block's first byte in lane x
+          // the next C byte after it in unit input coordinates
+          uint32_t nxt = 64 * x + cn;
+          if (cn == 64 && x < 63)
+            nxt = W.msk[x + 1] ? 64 * (x + 1) + (uint32_t)__builtin_ctzll(W.msk[x + 1]) : 64 * (x + 2);
+          fast = !inrep && 64 * x + t + 16 <= nxt;
+          src = 64 * x + t;
         }
-        const uint32_t t = p - (L - 1) * cnt;  // input offset of the block's first byte in lane x
-        // the next C byte after it in unit input coordinates
-        uint32_t nxt = 64 * x + cn;
-        if (cn == 64 && x < 63) nxt = msk[x + 1] ? 64 * (x + 1) + (uint32_t)__builtin_ctzll(msk[x + 1]) : 64 * (x + 2);
-        fast = !inrep && 64 * x + t + 16 <= nxt && q + 16 <= cap;
-        if (fast) *(uint4 *)(out + q) = lds16u(txt, 64 * x + t);
+        fast = fast && q + 16 <= cap;
+        if (fast) *(uint4 *)(out + q) = lds16u(W.txt, src);
         sl = !fast;
       }
       const uint64_t bm = __ballot(sl);
-      if (sl) slow[ns + __popcll(bm & ((1ull << lane) - 1ull))] = (uint16_t)((q - A) >> 4);
+      if (sl) W.slow[ns + __popcll(bm & ((1ull << lane) - 1ull))] = (uint16_t)((q - A) >> 4);
       ns += (uint32_t)__popcll(bm);
       // the list is worked off when full (a unit dense in replacements of a
       // long string has up to 256 L blocks) and after the unit's last round
       if (ns + 64 > kClsSlow || q0 + 1024 >= B) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        wave_sync();
 #pragma unroll 1
         for (uint32_t i0 = 0; i0 < ns; i0 += 64) {
           if (i0 + lane < ns) {
-            const uint64_t qs = A + 16 * (uint64_t)slow[i0 + lane];
-            const uint4 o = cls_block_slow((uint32_t)(qs - ob), T, rel, msk, txt, rep, L);
+            const uint64_t qs = A + 16 * (uint64_t)W.slow[i0 + lane];
+            const uint4 o = cls_block_slow((uint32_t)(qs - ob), T, W.rel, W.msk, W.txt, rep, L);
             if (qs + 16 <= cap) {
               *(uint4 *)(out + qs) = o;
             } else {  // the output buffer ends inside this block
@@ -882,19 +959,15 @@ __global__ __launch_bounds__(256) void replace_cls_write_kernel(const uint8_t *h
           }
         }
         ns = 0;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        wave_sync();
       }
     }
     // the edges: [ob, min(A, E)) and [max(B, A), E), byte by byte
     const uint64_t h1 = min(A, E), t0 = max(B, A);
     const uint64_t pos = lane < 16 ? ob + lane : t0 + (lane - 16);
     const bool mine = lane < 16 ? pos < h1 : (lane < 32 && pos < E);
-    if (mine && pos < cap) out[pos] = cls_out_byte((uint32_t)(pos - ob), rel, msk, txt, rep, L);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (mine && pos < cap) out[pos] = cls_out_byte((uint32_t)(pos - ob), W.rel, W.msk, W.txt, rep, L);
+    wave_sync();
   }
 }
 
@@ -1022,11 +1095,18 @@ hipError_t launch_replace_class(const uint8_t *hay, uint64_t n, const uint8_t *c
                                 hipStream_t st, int cus, uint32_t sw1, uint32_t sw2) {
   if (((uintptr_t)hay & 15) || rep_len > 64 || rep_len == 0) return hipErrorNotSupported;
   const uint64_t nunits = std::max<uint64_t>(1, (n + kClsUnit - 1) / kClsUnit);
+  // resident blocks only (a grid-stride loop over more blocks than the
+  // CUs hold runs the rest as a tail at low occupancy)
+  static int occ_w = 0;
+  if (!occ_w &&
+      (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_w, replace_cls_write_kernel, 256, 0) != hipSuccess || occ_w < 1))
+    occ_w = 1;
   uint64_t *buf = nullptr;
   hipError_t e = scratch_malloc((void **)&buf, (2 * nunits + 2) * 8, st);
   if (e != hipSuccess) return e;
   uint64_t *ucount = buf, *uoff = buf + nunits + 1;
   const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((nunits + 3) / 4, (uint64_t)cus * 8));
+  const int gridw = (int)std::max<uint64_t>(1, std::min<uint64_t>((nunits + 3) / 4, (uint64_t)cus * occ_w));
   do {
     if ((e = hipMemsetAsync(ucount + nunits, 0, 8, st)) != hipSuccess) break;
     hipLaunchKernelGGL(replace_cls_count_kernel, dim3(grid), dim3(256), 0, st, hay, n, cls, nunits, ucount, sw1, sw2);
@@ -1036,7 +1116,7 @@ hipError_t launch_replace_class(const uint8_t *hay, uint64_t n, const uint8_t *c
                        total);
     if ((e = hipGetLastError()) != hipSuccess) break;
     if (cap) {
-      hipLaunchKernelGGL(replace_cls_write_kernel, dim3(grid), dim3(256), 0, st, hay, n, cls, nunits, uoff, rep,
+      hipLaunchKernelGGL(replace_cls_write_kernel, dim3(gridw), dim3(256), 0, st, hay, n, cls, nunits, uoff, rep,
                          rep_len, out, cap, sw1, sw2);
       e = hipGetLastError();
     }
