@@ -688,6 +688,21 @@ __device__ __forceinline__ void cls_load(const uint8_t *hay, uint64_t n, uint64_
   for (int j = 0; j < 4; ++j) v[j] = *(const uint4 *)(16u * j < *avail ? hay + s0 + 16 * j : hay);
 }
 
+// Coalesced: lane l loads the unit's 16-byte pieces l, l + 64, l + 128,
+// l + 192 (each load instruction one contiguous KiB of the wave).  *avail =
+// the unit's bytes (<= kClsUnit).
+__device__ __forceinline__ void cls_load_co(const uint8_t *hay, uint64_t n, uint64_t u, uint32_t lane, uint4 *v,
+                                            uint32_t *avail) {
+  const uint64_t s0 = u * kClsUnit;
+  const uint64_t a = s0 < n ? n - s0 : 0;
+  *avail = a > kClsUnit ? kClsUnit : (uint32_t)a;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t o = 16 * lane + 1024 * j;
+    v[j] = *(const uint4 *)(o < *avail ? hay + s0 + o : hay);
+  }
+}
+
 __global__ __launch_bounds__(256) void replace_cls_count_kernel(const uint8_t *hay, uint64_t n, const uint8_t *cls_g,
                                                                 uint64_t nunits, uint64_t *ucount, uint32_t sw1,
                                                                 uint32_t sw2) {
@@ -696,11 +711,22 @@ __global__ __launch_bounds__(256) void replace_cls_count_kernel(const uint8_t *h
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t nw = (uint64_t)gridDim.x * 4;
-  for (uint64_t u = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); u < nunits; u += nw) {
+  // last unit first: the tail of the text is what the previous pass wrote
+  // last (still in the last-level cache), and the head this pass reads last
+  // is what the write pass reads first
+  for (uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < nunits; i += nw) {
+    const uint64_t u = nunits - 1 - i;
     uint4 v[4];
-    uint32_t avail;
-    cls_load(hay, n, u * kClsUnit + 64 * (uint64_t)lane, v, &avail);
-    uint32_t k = (uint32_t)__popcll(cls_mask(cls, v, avail, sw1, sw2));
+    uint32_t ua;
+    cls_load_co(hay, n, u, lane, v, &ua);
+    uint64_t m = cls_mask(cls, v, 64, sw1, sw2);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // the pieces' bytes past the haystack
+      const uint32_t o = 16 * lane + 1024 * j;
+      const uint32_t a = o < ua ? min(ua - o, 16u) : 0u;
+      m &= ~(((0xFFFFull << a) & 0xFFFFull) << (16 * j));
+    }
+    uint32_t k = (uint32_t)__popcll(m);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) k += __shfl_xor(k, o);
     if (lane == 0) ucount[u] = k;
@@ -799,24 +825,60 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 // A unit whose output spans at most kClsMap bytes from the aligned block
-// before it gets a block map: per 16-byte output block the C bytes whose
-// replacement starts in an earlier block (prefix of counts) and whether a
-// replacement meets it.  A block no replacement meets is text only, read
-// from staged offset (block start - (L - 1) * C bytes before it).
+// before it and holds at most kClsRank C bytes gets a block map: the output
+// offset of every replacement (P, by rank) and per 16-byte output block the
+// replacements starting before it (prefix of counts).  A block with no
+// replacement starting in it and the one before it ended is text only, read
+// from staged offset (block start - (L - 1) * replacements before it); a
+// block a replacement meets walks P from there byte by byte.
 constexpr uint32_t kClsMap = 6144;
+constexpr uint32_t kClsRank = 256;
+#ifndef CLS_WAVES
+#define CLS_WAVES 5
+#endif
 constexpr uint32_t kClsCW = kClsMap / 32 / 64;  // a lane's words of the count map
 static_assert(kClsMap % 2048 == 0, "the map is worked by whole lanes");
 
+// The 16 output bytes of block x0 (offset from the unit's aligned output
+// base) with c0 replacements starting before it.
+__device__ __forceinline__ uint4 cls_block_map(uint32_t x0, uint32_t c0, uint32_t K, const uint16_t *P, uint32_t o15,
+                                               const uint8_t *txt, const uint8_t *rep, uint32_t L) {
+  int idx = (int)c0 - 1;  // the last replacement starting at or before the byte
+  uint32_t cur = idx >= 0 ? P[idx] : 0u, nxt = c0 < K ? P[c0] : ~0u;
+  uint32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0;
+#pragma unroll 1
+  for (uint32_t j0 = 0; j0 < 16; j0 += 4) {  // a word per round, shifted in from the top
+    uint32_t w = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+      const uint32_t x = x0 + j0 + j;
+      if (x >= nxt) {
+        ++idx;
+        cur = nxt;
+        nxt = (uint32_t)(idx + 1) < K ? P[idx + 1] : ~0u;
+      }
+      const uint32_t ch =
+          (idx >= 0 && x - cur < L) ? rep[x - cur] : txt[tx(x - o15 - (L - 1) * (uint32_t)(idx + 1))];
+      w |= ch << (8 * j);
+    }
+    b0 = b1;
+    b1 = b2;
+    b2 = b3;
+    b3 = w;
+  }
+  return make_uint4(b0, b1, b2, b3);
+}
+
 struct ClsWave {
   uint8_t txt[kClsUnit + 32];
-  uint32_t cnt[kClsMap / 32];   // per block pair: C bytes starting in the block (low, high half)
-  uint8_t slowb[kClsMap / 16];  // per block: a replacement meets it
+  uint32_t cnt[kClsMap / 32];  // per block pair: C bytes starting in the block (low, high half)
+  uint16_t P[kClsRank];        // output offset of each replacement from the aligned base
   uint32_t rel[66];
   uint64_t msk[65];
   uint16_t slow[kClsSlow];
 };
 
-__global__ __launch_bounds__(256, 6) void replace_cls_write_kernel(const uint8_t *hay, uint64_t n, const uint8_t *cls_g,
+__global__ __launch_bounds__(256, CLS_WAVES) void replace_cls_write_kernel(const uint8_t *hay, uint64_t n, const uint8_t *cls_g,
                                                                 uint64_t nunits, const uint64_t *uoff,
                                                                 const uint8_t *rep_g, uint32_t L, uint8_t *out,
                                                                 uint64_t cap, uint32_t sw1, uint32_t sw2) {
@@ -834,42 +896,46 @@ __global__ __launch_bounds__(256, 6) void replace_cls_write_kernel(const uint8_t
     // (loading the next unit here, behind this one's output, was slower:
     // profiles/r05_replace_class.txt)
     uint4 v[4];
-    uint32_t avail;
-    cls_load(hay, n, u * kClsUnit + 64 * (uint64_t)lane, v, &avail);
+    uint32_t ua;
+    cls_load_co(hay, n, u, lane, v, &ua);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) *(uint4 *)(W.txt + tx(16 * lane + 1024 * j)) = v[j];
+    wave_sync();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = *(const uint4 *)(W.txt + tx(64 * lane + 16 * j));
+    const uint32_t avail = ua > 64 * lane ? min(ua - 64 * lane, 64u) : 0u;
     const uint64_t m = cls_mask(cls, v, avail, sw1, sw2);
     const uint32_t k = (uint32_t)__popcll(m);
     const uint32_t len = avail + (L - 1) * k;  // this lane's output bytes
-    uint32_t incl = len;
+    // (output bytes: < 2^19; C bytes, <= 4096, above them)
+    uint32_t incl = len | k << 19;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t x = __shfl_up(incl, o);
       if (lane >= (uint32_t)o) incl += x;
     }
-    const uint32_t T = __shfl(incl, 63);  // the unit's output bytes
-    const uint32_t r0 = incl - len;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) *(uint4 *)(W.txt + tx(64 * lane + 16 * j)) = v[j];
+    const uint32_t tot = __shfl(incl, 63);
+    const uint32_t T = tot & 0x7FFFF, K = tot >> 19;  // the unit's output bytes, C bytes
+    const uint32_t r0 = (incl & 0x7FFFF) - len, kex = (incl >> 19) - k;
     if (lane == 0) *(uint4 *)(W.txt + kClsUnit) = make_uint4(0, 0, 0, 0);
     W.rel[lane] = r0;
     W.msk[lane] = m;
     if (lane == 63) { W.rel[64] = T; W.rel[65] = T; W.msk[64] = 0; }
     const uint64_t ob = u * kClsUnit + uoff[u] * (L - 1);  // the unit's output start
     const uint32_t o15 = (uint32_t)(ob & 15);
-    const bool map = o15 + T + 16 <= kClsMap;
+    const bool map = o15 + T + 16 <= kClsMap && K <= kClsRank;
     if (map) {
 #pragma unroll
       for (uint32_t i = 0; i < kClsCW; ++i) W.cnt[kClsCW * lane + i] = 0;
-#pragma unroll
-      for (uint32_t i = 0; i < kClsCW; ++i) *(uint16_t *)(W.slowb + 2 * (kClsCW * lane + i)) = 0;
       wave_sync();
       uint64_t mm = m;
-      uint32_t P = o15 + r0;  // output offset of the next C byte from the aligned base, less c
+      uint32_t P = o15 + r0, rk = kex;  // output offset of the next C byte from the aligned base, less c; its rank
       while (mm) {
         const uint32_t c = (uint32_t)__builtin_ctzll(mm);
         mm &= mm - 1;
         const uint32_t q = P + c;
         atomicAdd(&W.cnt[q >> 5], (q & 16) ? 0x10000u : 1u);
-        for (uint32_t bb = q >> 4; bb <= (q + L - 1) >> 4; ++bb) W.slowb[bb] = 1;
+        W.P[rk++] = (uint16_t)q;
         P += L - 1;
       }
       wave_sync();
@@ -909,8 +975,10 @@ __global__ __launch_bounds__(256, 6) void replace_cls_write_kernel(const uint8_t
         uint32_t src;
         if (map) {
           const uint32_t bl = (uint32_t)(q - base) >> 4;
-          fast = !W.slowb[bl];
-          src = r - (L - 1) * ((W.cnt[bl >> 1] >> (16 * (bl & 1))) & 0xFFFF);
+          const uint32_t c0 = (W.cnt[bl >> 1] >> (16 * (bl & 1))) & 0xFFFF,
+                         c1 = (W.cnt[(bl + 1) >> 1] >> (16 * ((bl + 1) & 1))) & 0xFFFF;
+          fast = c1 == c0 && (c0 == 0 || W.P[c0 - 1] + L <= 16 * bl);
+          src = r - (L - 1) * c0;
         } else {
           uint32_t x = min(r >> 6, 63u);
           while (x > 0 && W.rel[x] > r) --x;
@@ -949,7 +1017,13 @@ __global__ __launch_bounds__(256, 6) void replace_cls_write_kernel(const uint8_t
         for (uint32_t i0 = 0; i0 < ns; i0 += 64) {
           if (i0 + lane < ns) {
             const uint64_t qs = A + 16 * (uint64_t)W.slow[i0 + lane];
-            const uint4 o = cls_block_slow((uint32_t)(qs - ob), T, W.rel, W.msk, W.txt, rep, L);
+            uint4 o;
+            if (map) {
+              const uint32_t bl = (uint32_t)(qs - base) >> 4;
+              o = cls_block_map(16 * bl, (W.cnt[bl >> 1] >> (16 * (bl & 1))) & 0xFFFF, K, W.P, o15, W.txt, rep, L);
+            } else {
+              o = cls_block_slow((uint32_t)(qs - ob), T, W.rel, W.msk, W.txt, rep, L);
+            }
             if (qs + 16 <= cap) {
               *(uint4 *)(out + qs) = o;
             } else {  // the output buffer ends inside this block
