@@ -693,7 +693,7 @@ int rure_amd_replace_batch(rure *re, const rure_amd_batch *batch, const uint8_t 
   uint64_t *olen = nullptr;
   uint8_t *drep = nullptr;
   hipError_t e = iter_to_device(re, t, b, st, &ib, &err);
-  if (e == hipSuccess) e = scratch_malloc((void **)&shift, std::max<uint64_t>(ib.nm, 1) * 8, st);
+  if (e == hipSuccess) e = scratch_malloc((void **)&shift, (ib.nm + 1) * 8, st);
   if (e == hipSuccess) e = scratch_malloc((void **)&olen, (b.count + 1) * 8, st);
   if (e == hipSuccess) e = scratch_malloc((void **)&drep, std::max<size_t>(rep_len, 1), st);
   if (e == hipSuccess && rep_len) e = hipMemcpyAsync(drep, rep, rep_len, hipMemcpyHostToDevice, st);

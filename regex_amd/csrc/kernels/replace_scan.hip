@@ -92,6 +92,23 @@ __global__ __launch_bounds__(256) void replace_shift_kernel(BatchDev bt, const u
   }
 }
 
+// One haystack, every match replaced: shift = S itself (the scan of the
+// match lengths less rep_len, read through ValOne), out_len = len - S[nm].
+struct ValOne {
+  const uint64_t *m;
+  uint64_t nm;
+  int64_t rep_len;
+  __device__ int64_t operator()(uint64_t g) const {
+    return g < nm ? (int64_t)(m[2 * g + 1] - m[2 * g]) - rep_len : 0;
+  }
+};
+
+__global__ void replace_len1_kernel(BatchDev bt, const int64_t *S, uint64_t nm, uint64_t *out_len) {
+  uint64_t base, len;
+  hay_of(bt, 0, &base, &len);
+  out_len[0] = (uint64_t)((int64_t)len - S[nm]);
+}
+
 // 16 bytes from an arbitrary address, as two aligned 16-byte loads and a
 // funnel shift (the second load is the aligned block holding p[15], so it
 // stays inside the buffer's 16-byte-rounded end whenever p[0..16) does).
@@ -1061,6 +1078,23 @@ hipError_t exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, hip
 hipError_t launch_replace_plan(const BatchDev &b, const uint64_t *counts, const uint64_t *moff, const uint64_t *m,
                                uint64_t limit, uint64_t rep_len, int64_t *shift, uint64_t *out_len, hipStream_t st,
                                int cus, uint64_t nm) {
+  if (b.count == 1 && limit == ~0ull) {  // one scan, no per-match passes (shift: nm + 1 entries)
+    auto in = rocprim::make_transform_iterator(rocprim::make_counting_iterator<uint64_t>(0),
+                                               ValOne{m, nm, (int64_t)rep_len});
+    size_t tmp = 0;
+    hipError_t e = rocprim::exclusive_scan(nullptr, tmp, in, shift, (int64_t)0, (size_t)(nm + 1),
+                                           rocprim::plus<int64_t>(), st);
+    void *buf = nullptr;
+    if (e == hipSuccess) e = scratch_malloc(&buf, tmp, st);
+    if (e == hipSuccess)
+      e = rocprim::exclusive_scan(buf, tmp, in, shift, (int64_t)0, (size_t)(nm + 1), rocprim::plus<int64_t>(), st);
+    if (buf) { hipError_t e2 = scratch_free(buf, st); if (e == hipSuccess) e = e2; }
+    if (e == hipSuccess) {
+      hipLaunchKernelGGL(replace_len1_kernel, dim3(1), dim3(1), 0, st, b, shift, nm, out_len);
+      e = hipGetLastError();
+    }
+    return e;
+  }
   int64_t *val = nullptr, *S = nullptr;
   hipError_t e = scratch_malloc((void **)&val, (nm + 1) * 8, st);
   if (e == hipSuccess) e = scratch_malloc((void **)&S, (nm + 1) * 8, st);
