@@ -255,6 +255,8 @@ hipError_t launch_captures(const BatchDev &b, const NfaDev &n, const uint64_t *f
 // replacen / split over find_iter output (replace_scan.hip).  counts / moff:
 // matches per haystack and their exclusive sums; m: the records.
 hipError_t exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, hipStream_t st);
+// shift: nm + 1 entries; one haystack with every match replaced holds the
+// replacement starts there instead (the plan's output, the copy's input).
 hipError_t launch_replace_plan(const BatchDev &b, const uint64_t *counts, const uint64_t *moff, const uint64_t *m,
                                uint64_t limit, uint64_t rep_len, int64_t *shift, uint64_t *out_len, hipStream_t st,
                                int cus,

@@ -92,21 +92,23 @@ __global__ __launch_bounds__(256) void replace_shift_kernel(BatchDev bt, const u
   }
 }
 
-// One haystack, every match replaced: shift = S itself (the scan of the
-// match lengths less rep_len, read through ValOne), out_len = len - S[nm].
-struct ValOne {
-  const uint64_t *m;
-  uint64_t nm;
+// One haystack, every match replaced: the replacement starts G come
+// straight out of one inclusive scan, G_0 = s_0 and G_j = G_(j-1) + s_j -
+// e_(j-1) + rep_len (the text between two matches, then a replacement), read
+// through GOne; with s_nm = the haystack length, G_nm is the output length.
+// No shift array: the copy reads G as the replacement starts (CopyCtx::one).
+struct GOne {
+  const uint64_t *m, *offs;
+  uint64_t nm, length;
   int64_t rep_len;
-  __device__ int64_t operator()(uint64_t g) const {
-    return g < nm ? (int64_t)(m[2 * g + 1] - m[2 * g]) - rep_len : 0;
+  __device__ int64_t operator()(uint64_t j) const {
+    const int64_t s = j < nm ? (int64_t)m[2 * j] : (int64_t)(offs ? offs[1] - offs[0] : length);
+    return j ? s - (int64_t)m[2 * j - 1] + rep_len : s;
   }
 };
 
-__global__ void replace_len1_kernel(BatchDev bt, const int64_t *S, uint64_t nm, uint64_t *out_len) {
-  uint64_t base, len;
-  hay_of(bt, 0, &base, &len);
-  out_len[0] = (uint64_t)((int64_t)len - S[nm]);
+__global__ void replace_len1_kernel(const int64_t *G, uint64_t nm, uint64_t *out_len) {
+  out_len[0] = (uint64_t)G[nm];
 }
 
 // 16 bytes from an arbitrary address, as two aligned 16-byte loads and a
@@ -183,7 +185,10 @@ struct CopyCtx {
   const int64_t *shift;
   uint64_t limit, rep_len, total, cap;
   const uint8_t *rep;
-  __device__ __forceinline__ uint64_t R(uint64_t j) const { return (uint64_t)((int64_t)m[2 * j] - shift[j]); }
+  bool one;  // one haystack, every match replaced: G holds the replacement starts, no shift
+  __device__ __forceinline__ uint64_t R(uint64_t j) const {
+    return one ? G[j] : (uint64_t)((int64_t)m[2 * j] - shift[j]);
+  }
 };
 
 struct BlockPlan {
@@ -375,17 +380,6 @@ __device__ __forceinline__ uint4 load16u_nb(const uint8_t *p) {
   return make_uint4((uint32_t)r0, (uint32_t)(r0 >> 32), (uint32_t)r1, (uint32_t)(r1 >> 32));
 }
 
-// matches of the group with R <= p0 (slots 1..a of the staged records)
-__device__ __forceinline__ uint32_t group_passed(const uint64_t *R, uint32_t cnt, uint64_t p0) {
-  uint32_t a = 0, bnd = cnt;
-  while (a < bnd) {
-    const uint32_t mid = (a + bnd) >> 1;
-    if (R[1 + mid] <= p0) a = mid + 1;
-    else bnd = mid;
-  }
-  return a;
-}
-
 // Blocks the group cannot do with its staged records (a dense group, a block
 // with more than three replacement starts: rare) go to a global list, done
 // by replace_rest_kernel through the generic per-block path (plan_block,
@@ -396,10 +390,11 @@ __device__ __forceinline__ void push_rest(uint32_t *rest, uint64_t rest_cap, uns
   if (k < rest_cap) rest[k] = (uint32_t)(p0 >> 4);
 }
 
-__global__ __launch_bounds__(256) void replace_copy4_kernel(CopyCtx c, uint8_t *out, uint32_t *rest, uint64_t rest_cap,
+__global__ __launch_bounds__(256, 5) void replace_copy4_kernel(CopyCtx c, uint8_t *out, uint32_t *rest, uint64_t rest_cap,
                                                             unsigned long long *nrest) {
   __shared__ uint64_t sR[4][kGroupSlots], sE[4][kGroupSlots];
   __shared__ uint16_t sEdge[4][kGroupWin * 64];
+  __shared__ uint32_t sA[4][kGroupWin * 64];  // per block of the group: its matches with R <= the block start
   const uint64_t total = c.ooff[1] < c.cap ? c.ooff[1] : c.cap;
   c.total = total;
   const uint64_t nm = c.moff[1];
@@ -430,12 +425,41 @@ __global__ __launch_bounds__(256) void replace_copy4_kernel(CopyCtx c, uint8_t *
       continue;
     }
     const uint64_t *R = sR[wv], *E = sE[wv];
+    uint32_t *A = sA[wv];
+    const uint64_t gs = w0 * kWin;
+#pragma unroll
+    for (uint32_t q = 0; q < kGroupWin; ++q) A[64 * q + lane] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
     for (uint32_t s = lane; s < kGroupSlots; s += 64) {  // slot s = match lo - 1 + s
       const int64_t g = (int64_t)lo - 1 + (int64_t)s;
       const bool ok = g >= 0 && (uint64_t)g < nm && s < cnt + 5;
-      sR[wv][s] = ok ? c.G[g] : ~0ull;
+      const uint64_t Rg = ok ? c.G[g] : ~0ull;
+      sR[wv][s] = Rg;
       sE[wv][s] = ok ? c.m[2 * g + 1] : 0;
+      // the group's matches by the first block whose start is >= R
+      // (R >= gs; the last bucket, past the group, is not counted)
+      if (s >= 1 && s <= cnt) {
+        const uint64_t bk = (Rg - gs + 15) >> 4;
+        if (bk < kGroupWin * 64) atomicAdd(&A[bk], 1u);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    {  // inclusive prefix over the group's blocks (lane: blocks 4 lane .. 4 lane + 3)
+      const uint4 a4 = *(const uint4 *)(A + 4 * lane);
+      const uint32_t t = a4.x + a4.y + a4.z + a4.w;
+      uint32_t ex = t;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t x = __shfl_up(ex, o);
+        if (lane >= (uint32_t)o) ex += x;
+      }
+      ex -= t;
+      *(uint4 *)(A + 4 * lane) = make_uint4(ex + a4.x, ex + a4.x + a4.y, ex + a4.x + a4.y + a4.z, ex + t);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -445,7 +469,7 @@ __global__ __launch_bounds__(256) void replace_copy4_kernel(CopyCtx c, uint8_t *
 #pragma unroll
     for (uint32_t q = 0; q < kGroupWin; ++q) {
       const uint64_t p0 = (w0 + q) * kWin + 16 * (uint64_t)lane;
-      const uint32_t a = group_passed(R, (uint32_t)cnt, p0);
+      const uint32_t a = A[64 * q + lane];
       const uint64_t jj = lo + a;
       const uint64_t nextR = R[a + 1];
       const uint64_t r = jj ? R[a] : 0;
@@ -473,7 +497,7 @@ __global__ __launch_bounds__(256) void replace_copy4_kernel(CopyCtx c, uint8_t *
       if (r0 + lane >= ne) continue;
       const uint32_t id = sEdge[wv][r0 + lane];
       const uint64_t p0 = (w0 + (id >> 6)) * kWin + 16 * (uint64_t)(id & 63);
-      const uint32_t a = group_passed(R, (uint32_t)cnt, p0);
+      const uint32_t a = A[id];
       const uint64_t jj = lo + a;
       // deletions (rep_len 0, the regex-dna strip: an edge every ~61 bytes):
       // the block is at most four text stretches, each one unaligned 16-byte
@@ -720,6 +744,22 @@ __device__ __forceinline__ void cls_load_co(const uint8_t *hay, uint64_t n, uint
   }
 }
 
+// The class bytes of a unit loaded by cls_load_co (wave total).
+__device__ __forceinline__ uint32_t cls_count_co(const uint8_t *cls, const uint4 *v, uint32_t ua, uint32_t lane,
+                                                 uint32_t sw1, uint32_t sw2) {
+  uint64_t m = cls_mask(cls, v, 64, sw1, sw2);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {  // the pieces' bytes past the haystack
+    const uint32_t o = 16 * lane + 1024 * j;
+    const uint32_t a = o < ua ? min(ua - o, 16u) : 0u;
+    m &= ~(((0xFFFFull << a) & 0xFFFFull) << (16 * j));
+  }
+  uint32_t k = (uint32_t)__popcll(m);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) k += __shfl_xor(k, o);
+  return k;
+}
+
 __global__ __launch_bounds__(256) void replace_cls_count_kernel(const uint8_t *hay, uint64_t n, const uint8_t *cls_g,
                                                                 uint64_t nunits, uint64_t *ucount, uint32_t sw1,
                                                                 uint32_t sw2) {
@@ -731,22 +771,18 @@ __global__ __launch_bounds__(256) void replace_cls_count_kernel(const uint8_t *h
   // last unit first: the tail of the text is what the previous pass wrote
   // last (still in the last-level cache), and the head this pass reads last
   // is what the write pass reads first
-  for (uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < nunits; i += nw) {
-    const uint64_t u = nunits - 1 - i;
-    uint4 v[4];
-    uint32_t ua;
-    cls_load_co(hay, n, u, lane, v, &ua);
-    uint64_t m = cls_mask(cls, v, 64, sw1, sw2);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {  // the pieces' bytes past the haystack
-      const uint32_t o = 16 * lane + 1024 * j;
-      const uint32_t a = o < ua ? min(ua - o, 16u) : 0u;
-      m &= ~(((0xFFFFull << a) & 0xFFFFull) << (16 * j));
+  // (two units per round: both units' loads in flight together)
+  for (uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < nunits; i += 2 * nw) {
+    const uint64_t u0 = nunits - 1 - i, u1 = i + nw < nunits ? nunits - 1 - (i + nw) : nunits;
+    uint4 v0[4], v1[4];
+    uint32_t a0, a1;
+    cls_load_co(hay, n, u0, lane, v0, &a0);
+    cls_load_co(hay, n, u1, lane, v1, &a1);
+    const uint32_t k0 = cls_count_co(cls, v0, a0, lane, sw1, sw2), k1 = cls_count_co(cls, v1, a1, lane, sw1, sw2);
+    if (lane == 0) {
+      ucount[u0] = k0;
+      if (u1 < nunits) ucount[u1] = k1;
     }
-    uint32_t k = (uint32_t)__popcll(m);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) k += __shfl_xor(k, o);
-    if (lane == 0) ucount[u] = k;
   }
 }
 
@@ -1078,19 +1114,18 @@ hipError_t exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, hip
 hipError_t launch_replace_plan(const BatchDev &b, const uint64_t *counts, const uint64_t *moff, const uint64_t *m,
                                uint64_t limit, uint64_t rep_len, int64_t *shift, uint64_t *out_len, hipStream_t st,
                                int cus, uint64_t nm) {
-  if (b.count == 1 && limit == ~0ull) {  // one scan, no per-match passes (shift: nm + 1 entries)
+  if (b.count == 1 && limit == ~0ull) {  // one scan into shift's nm + 1 entries: G (GOne)
     auto in = rocprim::make_transform_iterator(rocprim::make_counting_iterator<uint64_t>(0),
-                                               ValOne{m, nm, (int64_t)rep_len});
+                                               GOne{m, b.offs, nm, b.length, (int64_t)rep_len});
     size_t tmp = 0;
-    hipError_t e = rocprim::exclusive_scan(nullptr, tmp, in, shift, (int64_t)0, (size_t)(nm + 1),
-                                           rocprim::plus<int64_t>(), st);
+    hipError_t e = rocprim::inclusive_scan(nullptr, tmp, in, shift, (size_t)(nm + 1), rocprim::plus<int64_t>(), st);
     void *buf = nullptr;
     if (e == hipSuccess) e = scratch_malloc(&buf, tmp, st);
     if (e == hipSuccess)
-      e = rocprim::exclusive_scan(buf, tmp, in, shift, (int64_t)0, (size_t)(nm + 1), rocprim::plus<int64_t>(), st);
+      e = rocprim::inclusive_scan(buf, tmp, in, shift, (size_t)(nm + 1), rocprim::plus<int64_t>(), st);
     if (buf) { hipError_t e2 = scratch_free(buf, st); if (e == hipSuccess) e = e2; }
     if (e == hipSuccess) {
-      hipLaunchKernelGGL(replace_len1_kernel, dim3(1), dim3(1), 0, st, b, shift, nm, out_len);
+      hipLaunchKernelGGL(replace_len1_kernel, dim3(1), dim3(1), 0, st, shift, nm, out_len);
       e = hipGetLastError();
     }
     return e;
@@ -1129,13 +1164,17 @@ hipError_t launch_replace_copy(const BatchDev &b, const uint64_t *ooff, const ui
   // total_hint bounds the bytes written (the output is at most the text
   // plus the replacements, and at most cap)
   const uint64_t nwin = (total_hint + kWin - 1) / kWin;
-  uint64_t *G = nullptr, *widx = nullptr;
-  hipError_t e = scratch_malloc((void **)&G, std::max<uint64_t>(nm, 1) * 8, st);
+  // one haystack, every match replaced: launch_replace_plan left G in shift
+  const bool one = b.count == 1 && limit == ~0ull;
+  uint64_t *G = one ? (uint64_t *)shift : nullptr, *gbuf = nullptr, *widx = nullptr;
+  hipError_t e = one ? hipSuccess : scratch_malloc((void **)&gbuf, std::max<uint64_t>(nm, 1) * 8, st);
+  if (!one) G = gbuf;
   if (e == hipSuccess) e = scratch_malloc((void **)&widx, (nwin + 2) * 8, st);
   if (e == hipSuccess && nm == 0) e = hipMemsetAsync(widx, 0, (nwin + 2) * 8, st);
   if (e == hipSuccess && nm) {
-    hipLaunchKernelGGL(replace_g_kernel, dim3(grid_for_items(nm, 256, cus)), dim3(256), 0, st, b.count, ooff, moff, m,
-                       shift, G);
+    if (!one)
+      hipLaunchKernelGGL(replace_g_kernel, dim3(grid_for_items(nm, 256, cus)), dim3(256), 0, st, b.count, ooff, moff,
+                         m, shift, G);
     hipLaunchKernelGGL(replace_widx_kernel, dim3(grid_for_items(nwin + 1, 256, cus)), dim3(256), 0, st, b.count, moff,
                        G, nwin + 1, widx);
     e = hipGetLastError();
@@ -1155,6 +1194,7 @@ hipError_t launch_replace_copy(const BatchDev &b, const uint64_t *ooff, const ui
     c.total = 0;
     c.cap = cap;
     c.rep = rep;
+    c.one = one;
     if (b.count == 1 && limit == ~0ull && knob(Knob::ReplaceGeneric) != 1 && total_hint < (1ull << 36)) {
       const uint64_t nblk = (total_hint + 15) / 16, rcap = std::max<uint64_t>(4096, nblk / 16);
       uint32_t *rest = nullptr;
@@ -1176,7 +1216,7 @@ hipError_t launch_replace_copy(const BatchDev &b, const uint64_t *ooff, const ui
                          dim3(256), 0, st, c, out);
     if (e == hipSuccess) e = hipGetLastError();
   }
-  for (uint64_t *q : {G, widx})
+  for (uint64_t *q : {gbuf, widx})
     if (q) { hipError_t e2 = scratch_free(q, st); if (e == hipSuccess) e = e2; }
   return e;
 }
@@ -1205,15 +1245,20 @@ hipError_t launch_replace_class(const uint8_t *hay, uint64_t n, const uint8_t *c
   const uint64_t nunits = std::max<uint64_t>(1, (n + kClsUnit - 1) / kClsUnit);
   // resident blocks only (a grid-stride loop over more blocks than the
   // CUs hold runs the rest as a tail at low occupancy)
-  static int occ_w = 0;
-  if (!occ_w &&
-      (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_w, replace_cls_write_kernel, 256, 0) != hipSuccess || occ_w < 1))
-    occ_w = 1;
+  static int occ_w = 0, occ_c = 0;
+  if (!occ_w) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_c, replace_cls_count_kernel, 256, 0) != hipSuccess ||
+        occ_c < 1)
+      occ_c = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_w, replace_cls_write_kernel, 256, 0) != hipSuccess ||
+        occ_w < 1)
+      occ_w = 1;
+  }
   uint64_t *buf = nullptr;
   hipError_t e = scratch_malloc((void **)&buf, (2 * nunits + 2) * 8, st);
   if (e != hipSuccess) return e;
   uint64_t *ucount = buf, *uoff = buf + nunits + 1;
-  const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((nunits + 3) / 4, (uint64_t)cus * 8));
+  const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((nunits + 7) / 8, (uint64_t)cus * occ_c));
   const int gridw = (int)std::max<uint64_t>(1, std::min<uint64_t>((nunits + 3) / 4, (uint64_t)cus * occ_w));
   do {
     if ((e = hipMemsetAsync(ucount + nunits, 0, 8, st)) != hipSuccess) break;
