@@ -344,9 +344,12 @@ __device__ __forceinline__ uint64_t rev_scan_all(const RevDfaDev &r, const uint8
 // lane whose scan ended does its reverse scan, applies the iteration rule
 // (re_trait.rs:197-221) and sets up its next search (exec.rs:632-662) in
 // the same iteration.
+// abortf (a caller that re-runs the batch when a search quits): the first
+// quit sets it, and every wave polls it every 16 bursts and stops (its unit
+// records are then meaningless; the call reports the quit).
 __global__ __launch_bounds__(1024) void iter_spec_burst_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f,
                                                               RevDfaDev r, Unit *units, uint64_t *slots,
-                                                              uint32_t *counts, uint32_t *dirty) {
+                                                              uint32_t *counts, uint32_t *dirty, uint32_t *abortf) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const uint8_t *rlds = stage_tables(f, r, lds);
   for (uint64_t u0 = (uint64_t)blockIdx.x * blockDim.x; u0 < nunits; u0 += (uint64_t)gridDim.x * blockDim.x) {
@@ -386,7 +389,11 @@ __global__ __launch_bounds__(1024) void iter_spec_burst_kernel(BatchDev b, Geo g
       p = c0;
       unit_next();
     }
+    uint32_t polls = 0;
     while (__ballot(searching)) {
+      if (abortf && (++polls & 15) == 0 &&
+          __ballot(__hip_atomic_load(abortf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0))
+        break;
       if (!searching) continue;
       if (at == cutpos) {  // dfa_find_cut: no new match may start at or after the cut
         L.s = f.strip[L.s];
@@ -404,7 +411,12 @@ __global__ __launch_bounds__(1024) void iter_spec_burst_kernel(BatchDev b, Geo g
       if (!L.done && (at < len || cutpos == len)) continue;  // the scan goes on next burst
       // the forward scan ended: EOF step, reverse scan, iteration rule
       if (!L.done && f.eof[L.s]) L.last = len;
-      if (L.quit) { quit = true; finish(sp, slm, false); continue; }
+      if (L.quit) {
+        quit = true;
+        if (abortf) atomicOr(abortf, 1u);
+        finish(sp, slm, false);
+        continue;
+      }
       if (L.last == NONE) { finish(sp, slm, true); continue; }
       const uint64_t me = L.last;
       uint64_t ms = at0;
@@ -414,7 +426,12 @@ __global__ __launch_bounds__(1024) void iter_spec_burst_kernel(BatchDev b, Geo g
                                   : rev_scan(r, rlds, base, len, at0, me, &reached);
         if (first) unsure = reached;
         first = false;
-        if (rs == QUITMARK) { quit = true; finish(sp, slm, false); continue; }
+        if (rs == QUITMARK) {
+          quit = true;
+          if (abortf) atomicOr(abortf, 1u);
+          finish(sp, slm, false);
+          continue;
+        }
         if (rs == NONE) {  // look-around: the search's NoMatch ends the iteration
           if (f.looks) finish(kIterStop, NONE, false);
           else finish(sp, slm, true);
@@ -2819,6 +2836,13 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
       const bool sa_tile = sa_tile_ok(b, g);
       // Lexer engine (terminal matches + first-byte rule); RURE_AMD_LEX=0 disables
       const bool use_lex = lex_usable(*f, b, g);
+      // the quit flag (a caller that re-runs on a quit): zeroed here, set by
+      // the burst kernel's first quit (the others stop) and by iter_quit_kernel
+      uint32_t *qd = nullptr;
+      if (f->can_quit && quit) {
+        if ((e = scratch_malloc((void **)&qd, 8, st)) != hipSuccess) break;
+        if ((e = hipMemsetAsync(qd, 0, 4, st)) != hipSuccess) { (void)scratch_free(qd, st); break; }
+      }
       ktimer_begin(st);  // bench diagnostics: the speculative kernel's duration
       if (use_lex) {
         const dim3 lg(grid_cap((nunits + 63) / 64, 4, cus, 4));
@@ -2870,10 +2894,36 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
                              units, slots, counts, dirty);
       } else {
         hipLaunchKernelGGL(iter_spec_burst_kernel, dim3(grid), dim3(bs), iter_lds_bytes(*f, r), st, b, g, nunits, *f,
-                           r, units, slots, counts, dirty);
+                           r, units, slots, counts, dirty, qd);
       }
       if (!use_lex) ktimer_end(st);
-      if ((e = hipGetLastError()) != hipSuccess) break;
+      if ((e = hipGetLastError()) != hipSuccess) {
+        if (qd) (void)scratch_free(qd, st);
+        break;
+      }
+      // a quit in the speculative pass ends the call here: the caller re-runs
+      // the batch on the full automaton or the wave path, and the fix walk
+      // over quit units is serial (the ASCII shadow over sherlock as it is,
+      // a non-ASCII byte every few KiB: 17 s; then 47.6 ms with the whole
+      // speculative pass run, against 38.4 ms on the full automaton alone;
+      // profiles/r05_shadow_bench.jsonl)
+      if (qd) {
+        uint32_t q = 0;
+        if (e == hipSuccess) {
+          hipLaunchKernelGGL(iter_quit_kernel, dim3(grid_cap(nunits, 256, cus, 4)), dim3(256), 0, st, units, nunits,
+                             qd);
+          e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipMemcpyAsync(&q, qd, 4, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        const hipError_t e2 = scratch_free(qd, st);
+        if (e == hipSuccess) e = e2;
+        if (e != hipSuccess) break;
+        if (q) {
+          *quit = true;
+          break;
+        }
+      }
       e = iter_post(b, g, nunits, *f, r, sc, o, spn, st, cus, use_lex);
       if (e == hipSuccess && f->can_quit && quit) {  // did any search quit?
         uint32_t q = 0;
