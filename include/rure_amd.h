@@ -200,7 +200,9 @@ int rure_amd_find_iter_span_multi(rure *const *res, size_t n, const uint8_t *hay
  * output lengths); out (device) receives the concatenated outputs, at most
  * out_capacity bytes; *total (device) = the bytes needed (call again with a
  * larger buffer if it exceeds out_capacity).  Synchronises the stream once
- * (to size the match buffer). */
+ * to size the match buffer (twice if the first guess was short), except for
+ * replace_all (limit 0) of a regex whose matches are single bytes of one
+ * class over one fixed-stride haystack, which only enqueues. */
 int rure_amd_replace_batch(rure *re, const rure_amd_batch *batch, const uint8_t *rep, size_t rep_len,
                            size_t limit, uint8_t *out, uint64_t *out_offsets, size_t out_capacity,
                            uint64_t *total, void *stream);
@@ -208,7 +210,9 @@ int rure_amd_replace_batch(rure *re, const rure_amd_batch *batch, const uint8_t 
  * as (start, end) records relative to each haystack, concatenated;
  * counts[i] (device) = fields of haystack i; at most `limit` fields per
  * haystack with SplitN's rule (the last is the rest of the haystack);
- * limit = SIZE_MAX for split.  *total (device) = number of fields. */
+ * limit = SIZE_MAX for split.  *total (device) = number of fields.
+ * Synchronises the stream once (twice if the first guess of the match
+ * buffer was short) to size the match buffer. */
 int rure_amd_split_batch(rure *re, const rure_amd_batch *batch, size_t limit, uint64_t *counts,
                          rure_match *pieces, size_t capacity, uint64_t *total, void *stream);
 

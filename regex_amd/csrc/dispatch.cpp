@@ -560,6 +560,7 @@ hipError_t run_find_iter(rure *re, DevTables *t, const BatchDev &b, const IterOu
     // class in Unicode mode) answers ASCII text and quits on any other
     // byte.  Knob runs=0 keeps the DFA paths (A/B).
     const bool runs = !sp && knob(Knob::Runs) != 0;
+    bool run_quit = false;
     if (runs && fi->run_cls) {
       bool q = false;
       const hipError_t e = launch_find_iter_runs(b, fi->run_cls, fi->run_cp, o, st, t->cus, fi->run_quit != 0, &q);
@@ -567,12 +568,14 @@ hipError_t run_find_iter(rure *re, DevTables *t, const BatchDev &b, const IterOu
         if (e == hipSuccess) note_fwd_path(-19);
         return e;
       }
+      run_quit = q;
     }
     // the ASCII shadow first (all-rows LDS tables; a non-ASCII byte quits
     // and the full automaton re-runs the batch, still chunked); not for
-    // spans (the quit is read back)
+    // spans (the quit is read back), and not after the run engine quit (it
+    // quits on a byte >= 0x80, where the shadow would quit too)
     bool shadow_quit = false;
-    if (!sp) {
+    if (!sp && !run_quit) {
       if (const FwdDfaDev *fa = iter_ascii_device(re, *t, err)) {
         if (runs && fa->run_cls) {
           bool q = false;
@@ -616,10 +619,13 @@ hipError_t iter_to_device(rure *re, DevTables *t, const BatchDev &b, hipStream_t
   if ((e = scratch_malloc((void **)&ib->total, 8, st)) != hipSuccess) return e;
   if ((e = hipMemsetAsync(ib->counts, 0, (n + 1) * 8, st)) != hipSuccess) return e;
   const uint64_t bytes = b.offs ? 0 : (uint64_t)b.count * b.length;
-  // first guess: a match per 32 bytes (scratch is cached; a guess of one per
-  // 64 bytes overflowed on the regex-dna strip, a match per 61 bytes, and
-  // re-ran the whole search: 0.95 ms of its 5 ms)
-  uint64_t cap = std::max<uint64_t>(1024, bytes / 32 + 2 * n);
+  // first guess: the regex's density on its previous call plus an eighth,
+  // else a match per 64 bytes (an overflow re-runs the search once with the
+  // exact size: the regex-dna strip, a match per 61 bytes, paid that once)
+  const int64_t per_mib = re->iter_per_mib.load(std::memory_order_relaxed);
+  uint64_t cap = per_mib >= 0 ? (uint64_t)((double)bytes / (1 << 20) * (double)per_mib * 1.125) + 2 * n
+                              : bytes / 64 + 2 * n;
+  cap = std::max<uint64_t>(1024, cap);
   for (int pass = 0; pass < 2; ++pass) {
     if ((e = scratch_malloc((void **)&ib->m, cap * 16, st)) != hipSuccess) return e;
     IterOut o{ib->counts, ib->m, cap, ib->total};
@@ -628,6 +634,8 @@ hipError_t iter_to_device(rure *re, DevTables *t, const BatchDev &b, hipStream_t
     if ((e = hipMemcpyAsync(&tot, ib->total, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
     if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
     ib->nm = tot;
+    if (bytes >= (1u << 20)) re->iter_per_mib.store((int64_t)((double)tot / ((double)bytes / (1 << 20)) + 1),
+                                                    std::memory_order_relaxed);
     if (tot <= cap) break;
     (void)scratch_free(ib->m, st);
     ib->m = nullptr;
@@ -705,32 +713,41 @@ bool build_kmer(rure *const *res, size_t n, std::vector<uint32_t> *bitmap, std::
       (*mask)[code] |= (uint16_t)(1u << i);
     }
   // the masks' perfect hash for the tile kernel's LDS (kmer_hit_lds): an odd
-  // multiplier whose top 10 product bits are distinct over the string codes
+  // multiplier whose top 10 product bits are distinct over the string codes.
+  // Random multipliers find one with probability ~exp(-c^2 / 2048) per try
+  // for c codes, so past 160 codes (< 4e-6 per try) none is searched for;
+  // without one the hits read mask[code] from global memory (hglobal).
   std::vector<uint32_t> codes;
   for (uint32_t c = 0; c < (uint32_t)mask->size(); ++c)
     if ((*mask)[c]) codes.push_back(c);
   if (codes.size() > 512) return false;
+  km->hmul = 0;
+  km->hglobal = 1;
+  hmask->assign(1024, 0);
+  if (codes.size() > 160) return true;
   uint64_t rng = 0x9E3779B97F4A7C15ull;
   std::vector<uint16_t> slot(1024);
+  std::vector<uint8_t> used(1024);
   for (int t = 0; t < 100000; ++t) {
     rng ^= rng << 13, rng ^= rng >> 7, rng ^= rng << 17;
     const uint32_t K = (uint32_t)rng | 1u;
     std::fill(slot.begin(), slot.end(), 0);
-    std::vector<bool> used(1024, false);
+    std::fill(used.begin(), used.end(), 0);
     bool ok = true;
     for (uint32_t c : codes) {
       const uint32_t h = (c * K) >> 22;
       if (used[h]) { ok = false; break; }
-      used[h] = true;
+      used[h] = 1;
       slot[h] = (*mask)[c];
     }
     if (ok) {
       km->hmul = K;
+      km->hglobal = 0;
       *hmask = slot;
       return true;
     }
   }
-  return false;
+  return true;
 }
 
 // The cached device tables for this regex list, copied into *out while the

@@ -712,11 +712,12 @@ __global__ __launch_bounds__(1024) void set_core_kernel(BatchDev bt, SetCoreDev 
   // addresses and no branches (a load under a branch is waited for at the
   // branch's end).  The start cores are read from LDS.
   // (past the batch: the last line's offsets, never scanned)
-  auto line = [&](uint64_t h, uint64_t &o0, uint64_t &o1) {
-    const uint64_t hc = h < bt.count ? h : bt.count - 1;
-    if (MODE == 0) { o0 = hc * bt.stride; o1 = o0 + bt.length; return; }
-    o0 = bt.offs[hc];
-    o1 = bt.offs[hc + 1];
+  // offsets of line l (MODE 0: stride; l clamped into the batch)
+  auto line = [&](uint64_t l, uint64_t &o0, uint64_t &o1) {
+    const uint64_t lc = l < bt.count ? l : bt.count - 1;
+    if (MODE == 0) { o0 = lc * bt.stride; o1 = o0 + bt.length; return; }
+    o0 = bt.offs[lc];
+    o1 = bt.offs[lc + 1];
   };
   // the block holding text[at] and the one after it (if the line continues)
   auto blocks = [&](uint64_t o0, uint64_t o1, uint4 &b0, uint4 &b1) {
@@ -816,21 +817,29 @@ hipError_t launch_set_cores(const BatchDev &b, const SetCoreDev &f, uint64_t *ou
     const uint64_t nw = (uint64_t)grid * bs / 64;
     uint64_t *prof = nullptr;
     if ((e = hipMalloc(&prof, nw * 5 * 8)) != hipSuccess) return e;
-    (void)hipMemsetAsync(prof, 0, nw * 5 * 8, st);
-    auto kern = set_core_kernel<1, true>;
-    if ((e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess)
-      return e;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(bs), lds, st, b, f, out, prof);
     std::vector<uint64_t> hp(nw * 5);
-    (void)hipMemcpyAsync(hp.data(), prof, nw * 5 * 8, hipMemcpyDeviceToHost, st);
-    (void)hipStreamSynchronize(st);
-    (void)hipFree(prof);
+    auto kern = set_core_kernel<1, true>;
+    auto run = [&]() -> hipError_t {
+      hipError_t r;
+      if ((r = hipMemsetAsync(prof, 0, nw * 5 * 8, st)) != hipSuccess) return r;
+      if ((r = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) !=
+          hipSuccess)
+        return r;
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(bs), lds, st, b, f, out, prof);
+      if ((r = hipGetLastError()) != hipSuccess) return r;
+      if ((r = hipMemcpyAsync(hp.data(), prof, nw * 5 * 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return r;
+      return hipStreamSynchronize(st);
+    };
+    e = run();
+    const hipError_t ef = hipFree(prof);
+    if (e != hipSuccess) return e;
+    if (ef != hipSuccess) return ef;
     double sum[5] = {0, 0, 0, 0, 0};
     for (uint64_t w = 0; w < nw; ++w)
       for (int k = 0; k < 5; ++k) sum[k] += (double)hp[w * 5 + k];
     fprintf(stderr, "core_prof per wave (memtime ticks): prologue+head %.0f body %.0f tail %.0f finish %.0f prefetch %.0f\n",
             sum[0] / nw, sum[1] / nw, sum[2] / nw, sum[3] / nw, sum[4] / nw);
-    return hipGetLastError();
+    return hipSuccess;
   }
   if (mode == 1) note_fwd_path(-17);
   if (mode == 1) return go(set_core_kernel<1>);

@@ -322,6 +322,7 @@ struct KmerDev {
   const uint16_t *mask;
   const uint16_t *hmask;  // 1024: mask[c] at (c * hmul) >> 22, injective on the string codes
   uint32_t hmul;
+  uint32_t hglobal;       // 1: no injective hash was found; hits read mask[code] from global memory
   uint32_t vlut;  // byte k: the alphabet byte of code k (absent code: a byte of another code)
   uint32_t shift, lut, present, cmask;
   uint64_t len;

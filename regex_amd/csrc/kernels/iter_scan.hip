@@ -1094,7 +1094,8 @@ __device__ __forceinline__ void kmer_hit_lds(const SaMulti &m, const uint16_t *H
   if ((__builtin_amdgcn_perm(0u, km.vlut, cl) ^ lo) | (__builtin_amdgcn_perm(0u, km.vlut, ch) ^ hi)) return;
   const uint32_t code =
       __builtin_amdgcn_udot4(cl, 0x40100401u, 0u, false) | (__builtin_amdgcn_udot4(ch, 0x40100401u, 0u, false) << 8);
-  const uint32_t mask = HT[(code * km.hmul) >> 22];
+  // (a set with no injective 10-bit hash: the global table, one round trip)
+  const uint32_t mask = km.hglobal ? km.mask[code] : HT[(code * km.hmul) >> 22];
   const uint64_t st = e - 8;
 #pragma unroll
   for (int q = 0; q < MQ; ++q) {

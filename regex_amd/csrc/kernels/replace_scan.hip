@@ -22,6 +22,8 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
+#include <vector>
 #include <rocprim/rocprim.hpp>
 #include <stdint.h>
 
@@ -1238,6 +1240,26 @@ hipError_t launch_split(const BatchDev &b, const uint64_t *counts, const uint64_
 // replace_all of a one-byte-class regex over one haystack (16-byte aligned,
 // search from 0): cls[256] (device) = the class, rep (device) at most 64
 // bytes.  Writes out (at most cap bytes), out_offsets {0, total}, *total.
+// The class replace kernels' resident blocks per CU, per device (computed
+// once per device under a lock: the launch may come from several threads
+// and devices)
+static hipError_t cls_occupancy(int dev, int *occ_c, int *occ_w) {
+  static std::mutex mu;
+  static std::vector<std::pair<int, int>> cache;
+  std::lock_guard<std::mutex> g(mu);
+  if ((int)cache.size() <= dev) cache.resize(dev + 1, {0, 0});
+  if (!cache[dev].first) {
+    int c = 0, w = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&c, replace_cls_count_kernel, 256, 0);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&w, replace_cls_write_kernel, 256, 0);
+    if (e != hipSuccess) return e;
+    cache[dev] = {std::max(1, c), std::max(1, w)};
+  }
+  *occ_c = cache[dev].first;
+  *occ_w = cache[dev].second;
+  return hipSuccess;
+}
+
 hipError_t launch_replace_class(const uint8_t *hay, uint64_t n, const uint8_t *cls, const uint8_t *rep,
                                 uint32_t rep_len, uint8_t *out, uint64_t cap, uint64_t *ooff, uint64_t *total,
                                 hipStream_t st, int cus, uint32_t sw1, uint32_t sw2) {
@@ -1245,18 +1267,12 @@ hipError_t launch_replace_class(const uint8_t *hay, uint64_t n, const uint8_t *c
   const uint64_t nunits = std::max<uint64_t>(1, (n + kClsUnit - 1) / kClsUnit);
   // resident blocks only (a grid-stride loop over more blocks than the
   // CUs hold runs the rest as a tail at low occupancy)
-  static int occ_w = 0, occ_c = 0;
-  if (!occ_w) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_c, replace_cls_count_kernel, 256, 0) != hipSuccess ||
-        occ_c < 1)
-      occ_c = 1;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_w, replace_cls_write_kernel, 256, 0) != hipSuccess ||
-        occ_w < 1)
-      occ_w = 1;
-  }
-  uint64_t *buf = nullptr;
-  hipError_t e = scratch_malloc((void **)&buf, (2 * nunits + 2) * 8, st);
+  int dev = 0, occ_c = 0, occ_w = 0;
+  hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
+  if ((e = cls_occupancy(dev, &occ_c, &occ_w)) != hipSuccess) return e;
+  uint64_t *buf = nullptr;
+  if ((e = scratch_malloc((void **)&buf, (2 * nunits + 2) * 8, st)) != hipSuccess) return e;
   uint64_t *ucount = buf, *uoff = buf + nunits + 1;
   const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((nunits + 7) / 8, (uint64_t)cus * occ_c));
   const int gridw = (int)std::max<uint64_t>(1, std::min<uint64_t>((nunits + 3) / 4, (uint64_t)cus * occ_w));

@@ -265,6 +265,10 @@ struct rure {
   uint8_t cls_one[256] = {0};
   uint8_t run_cls[256] = {0}, run_cls_a[256] = {0};
   std::map<int, std::pair<void *, FwdDfaDev>> iter_dev_a;
+  // matches per MiB of text seen by the last replace / split over a
+  // fixed-stride batch (iter_to_device's first guess of the match buffer;
+  // -1: none yet)
+  std::atomic<int64_t> iter_per_mib{-1};
 };
 
 struct rure_set {

@@ -131,3 +131,21 @@ def test_multi_kmer_known_answers(cuda):
     for v, re, g in zip(kc["variants"], res, got):
         seam = len(OracleRegex(re).find_iter(one * 2)) - 2 * v["count"]
         assert int(g[0].item()) == v["count"] * 40 + seam * 39, v["re"]
+
+
+@pytest.mark.parametrize("extra", [0, 1])
+def test_multi_kmer_many_codes(cuda, extra):
+    """String sets whose codes admit no injective 10-bit hash (192 and 256
+    8-byte strings over acgt, above the 160 the search is tried for): the
+    k-mer engine settles its hits through the global mask table instead of
+    the LDS hash, with outputs equal to each regex's own pass and the oracle."""
+    pats = [r"[acgt]{3}ggtaa", r"tt[acgt]{3}acc", r"cc[acgt]{3}tgg"] + ([r"a[acgt]{3}tgca"] if extra else [])
+    res = [R.Regex(p) for p in pats]
+    rng = np.random.default_rng(21 + extra)
+    text = bytes(rng.choice(np.frombuffer(b"acgt", dtype=np.uint8), size=400000))
+    h = dev(text, cuda)
+    got = check_same(res, h, len(text), 0, len(text))
+    for i, re in enumerate(res):
+        exp = OracleRegex(re).find_iter(text)
+        assert len(exp) > 100
+        assert pairs(got[i][1]) == exp, i
