@@ -206,6 +206,27 @@ int rure_amd_find_iter_span_multi(rure *const *res, size_t n, const uint8_t *hay
 int rure_amd_replace_batch(rure *re, const rure_amd_batch *batch, const uint8_t *rep, size_t rep_len,
                            size_t limit, uint8_t *out, uint64_t *out_offsets, size_t out_capacity,
                            uint64_t *total, void *stream);
+/* A chain of replace_all calls over one haystack, step i on step i - 1's
+ * output: the regex-dna shootout's IUB substitutions
+ * (examples/shootout-regex-dna-bytes.rs:44-60, each a bytes::Regex::
+ * replace_all with NoExpand, re_bytes.rs:489-512).  Step i replaces every
+ * match of res[i] by reps[i][0..rep_lens[i]) (host memory, no `$`
+ * expansion).  Every res[i] must be a regex whose matches are single bytes of
+ * one class (a literal byte, a byte class: rure_amd_class_one_export) and
+ * 1 <= rep_lens[i] <= 64, else RURE_AMD_ERR_ARG.  haystack (device, 16-byte
+ * aligned) holds `length` bytes; step i writes out0 if i is even, else out1
+ * (device, 16-byte aligned, `capacity` bytes each; readable 16 bytes past
+ * capacity); the result is in out0 if n is odd, else out1.  lengths (device,
+ * n + 1 uint64) = length, then each step's output length.  An output longer
+ * than capacity is cut; that step's length is exact, the steps after it read
+ * their input cut and their lengths are lower bounds (a step never shortens
+ * its text, so lengths[n] > capacity): retry with capacity = lengths[n]
+ * until lengths[n] <= capacity.  Only enqueues:
+ * each step's match count per 4 KiB is counted by the previous step's kernel
+ * as it writes the text, and nothing is read back. */
+int rure_amd_replace_all_chain(rure *const *res, const uint8_t *const *reps, const size_t *rep_lens, size_t n,
+                               const uint8_t *haystack, size_t length, uint8_t *out0, uint8_t *out1,
+                               size_t capacity, uint64_t *lengths, void *stream);
 /* Batched split / splitn (re_bytes.rs:699-749): the fields between matches
  * as (start, end) records relative to each haystack, concatenated;
  * counts[i] (device) = fields of haystack i; at most `limit` fields per

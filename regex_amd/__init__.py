@@ -753,6 +753,37 @@ class Regex(object):
         return info, trans.reshape(n, 256), eof, start
 
 
+def replace_all_chain(regexes, reps, haystack, length=None, capacity=None, stream=None):
+    """replace_all of each regex in turn over one haystack, every step on the
+    previous step's output (rure_amd_replace_all_chain: regexes whose matches
+    are single bytes of one class, replacements of 1-64 bytes, e.g. the
+    regex-dna IUB substitutions).  Only enqueues.  Returns (out, lengths):
+    the final text in out[:lengths[-1]] (a device tensor of capacity + 16
+    bytes) and the n + 1 lengths (device int64).  If lengths[-1] exceeds
+    capacity the output was cut: call again with capacity >= lengths[-1]."""
+    import torch
+    n = len(regexes)
+    length = haystack.numel() - 16 if length is None else length
+    capacity = length + length // 2 + 4096 if capacity is None else capacity
+    dev = haystack.device
+    bufs = [torch.empty((capacity + 16,), dtype=torch.uint8, device=dev) for _ in range(min(n, 2) or 1)]
+    for b in bufs:
+        b[capacity:].zero_()
+    lengths = torch.empty((n + 1,), dtype=torch.int64, device=dev)
+    reps = [bytes(r.rep if isinstance(r, NoExpand) else r) for r in reps]
+    res_arr = (ctypes.c_void_p * max(n, 1))(*[r._re for r in regexes])
+    rep_bufs = [ctypes.create_string_buffer(r, max(len(r), 1)) for r in reps]
+    rep_arr = (ctypes.c_void_p * max(n, 1))(*[ctypes.addressof(b) for b in rep_bufs])
+    len_arr = (ctypes.c_size_t * max(n, 1))(*[len(r) for r in reps])
+    _check(N.rure_amd_replace_all_chain(res_arr, rep_arr, len_arr, n, ctypes.c_void_p(haystack.data_ptr()), length,
+                                        ctypes.c_void_p(bufs[0].data_ptr()),
+                                        ctypes.c_void_p(bufs[-1].data_ptr()), capacity,
+                                        ctypes.c_void_p(lengths.data_ptr()), _stream_ptr(stream)),
+           "replace_all_chain")
+    out = haystack if n == 0 else bufs[0] if n % 2 else bufs[1]
+    return out, lengths
+
+
 def find_iter_span_multi(regexes, haystack, lo, hi, length=None, entries=None, capacities=None, stream=None):
     """Regex.find_iter_span for several regexes over the same span [lo, hi)
     (rure_amd_find_iter_span_multi: finite string sets of one common length,

@@ -123,6 +123,8 @@ rure_amd_set_matches_batch = _sig("rure_amd_set_matches_batch", ctypes.c_int, VP
                                   VP, VP)
 rure_amd_replace_batch = _sig("rure_amd_replace_batch", ctypes.c_int, VP, ctypes.POINTER(RureBatch), ctypes.c_char_p,
                               c_size, c_size, VP, VP, c_size, VP, VP)
+rure_amd_replace_all_chain = _sig("rure_amd_replace_all_chain", ctypes.c_int, VP, VP, VP, c_size, VP, c_size, VP, VP,
+                                  c_size, VP, VP)
 rure_amd_split_batch = _sig("rure_amd_split_batch", ctypes.c_int, VP, ctypes.POINTER(RureBatch), c_size, VP, VP,
                             c_size, VP, VP)
 rure_amd_captures_batch = _sig("rure_amd_captures_batch", ctypes.c_int, VP, ctypes.POINTER(RureBatch), VP, VP)

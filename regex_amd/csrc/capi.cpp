@@ -651,6 +651,107 @@ int rure_amd_find_iter_span_multi(rure *const *res, size_t n, const uint8_t *hay
   return RURE_AMD_OK;
 }
 
+int rure_amd_replace_all_chain(rure *const *res, const uint8_t *const *reps, const size_t *rep_lens, size_t n,
+                               const uint8_t *haystack, size_t length, uint8_t *out0, uint8_t *out1,
+                               size_t capacity, uint64_t *lengths, void *stream) {
+  if (!res || (n && (!reps || !rep_lens)) || !lengths || !haystack || !out0 || (n > 1 && !out1) ||
+      ((uintptr_t)haystack & 15) || ((uintptr_t)out0 & 15) || (out1 && ((uintptr_t)out1 & 15)))
+    return RURE_AMD_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  if (n == 0) return hipMemcpyAsync(lengths, &length, 8, hipMemcpyHostToDevice, st) == hipSuccess ? RURE_AMD_OK
+                                                                                              : RURE_AMD_ERR_HIP;
+  std::vector<uint32_t> rl(n);
+  std::vector<std::array<uint32_t, 2>> sw(n);
+  std::vector<uint8_t> host(n * 320, 0);  // per step: the class (256), the replacement (64)
+  int cus = 0;
+  for (size_t i = 0; i < n; ++i) {
+    rure *re = res[i];
+    if (!re || rep_lens[i] < 1 || rep_lens[i] > 64 || !reps[i]) return RURE_AMD_ERR_ARG;
+    std::string err;
+    DevTables *t = regex_device(re, &err);
+    if (!t) return err.rfind("HIP", 0) == 0 ? RURE_AMD_ERR_HIP : RURE_AMD_ERR_DFA;
+    if (!re->cls_one_ok) return RURE_AMD_ERR_ARG;
+    cus = t->cus;
+    rl[i] = (uint32_t)rep_lens[i];
+    memcpy(&host[i * 320], re->cls_one, 256);
+    memcpy(&host[i * 320 + 256], reps[i], rep_lens[i]);
+    // a class of one or two bytes as SWAR compares (as rure_amd_replace_batch)
+    uint32_t w[2] = {0, 0}, nb = 0;
+    for (int c = 1; c < 256 && nb <= 2; ++c)
+      if (re->cls_one[c]) { if (nb < 2) w[nb] = (uint32_t)c * 0x01010101u; ++nb; }
+    if (re->cls_one[0] || nb > 2) w[0] = w[1] = 0;
+    else if (nb == 1) w[1] = w[0];
+    sw[i] = {w[0], w[1]};
+  }
+  // The chain is a string homomorphism: compose each byte's image F(x) and
+  // its length after every step, and run it as one map (launch_replace_hmap)
+  // when the images are at most 64 bytes and fit the 4 KiB pool.
+  if (knob(Knob::ChainSeq) != 1) {
+    std::vector<std::string> img(256);
+    std::vector<uint32_t> dl(n * 256, 0);
+    bool ok = true;
+    for (int x = 0; x < 256 && ok; ++x) {
+      std::string cur(1, (char)x);
+      for (size_t i = 0; i < n && ok; ++i) {
+        std::string nx;
+        for (unsigned char c : cur) {
+          if (res[i]->cls_one[c]) nx.append((const char *)reps[i], rep_lens[i]);
+          else nx.push_back((char)c);
+        }
+        cur.swap(nx);
+        if (cur.size() > 64) ok = false;
+        dl[i * 256 + x] = (uint32_t)cur.size() - 1;
+      }
+      img[x] = cur;
+    }
+    size_t pool = 0;
+    for (int x = 0; x < 256; ++x) pool += img[x].size();
+    if (ok && pool <= kHMapPoolMax) {
+      std::vector<uint8_t> blob(1024 + kHMapPoolMax + n * 256 * 4, 0);
+      uint16_t *so = (uint16_t *)(blob.data() + 256);
+      size_t at = 0;
+      for (int x = 0; x < 256; ++x) {
+        blob[x] = (uint8_t)img[x].size();
+        so[x] = (uint16_t)at;
+        blob[768 + x] = !(img[x].size() == 1 && (uint8_t)img[x][0] == x);
+        memcpy(blob.data() + 1024 + at, img[x].data(), img[x].size());
+        at += img[x].size();
+      }
+      memcpy(blob.data() + 1024 + kHMapPoolMax, dl.data(), dl.size() * 4);
+      uint8_t *db = nullptr;
+      hipError_t e = scratch_malloc((void **)&db, blob.size(), st);
+      if (e == hipSuccess) e = hipMemcpyAsync(db, blob.data(), blob.size(), hipMemcpyHostToDevice, st);
+      uint8_t *out = (n & 1) ? out0 : out1;
+      if (e == hipSuccess)
+        e = launch_replace_hmap(haystack, length, (int)n, db, (uint32_t)pool, out, capacity, lengths, st, cus);
+      if (db) { const hipError_t e2 = scratch_free(db, st); if (e == hipSuccess) e = e2; }
+      if (e == hipSuccess) note_fwd_path(-24);
+      if (e != hipErrorNotSupported) return e == hipSuccess ? RURE_AMD_OK : RURE_AMD_ERR_HIP;
+    }
+  }
+  uint8_t *dt = nullptr;
+  hipError_t e = scratch_malloc((void **)&dt, host.size(), st);
+  if (e == hipSuccess) e = hipMemcpyAsync(dt, host.data(), host.size(), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) {
+    std::vector<const uint8_t *> cls(n), rep(n);
+    for (size_t i = 0; i < n; ++i) {
+      cls[i] = dt + i * 320;
+      rep[i] = dt + i * 320 + 256;
+    }
+    // the bytes of each replacement in the next step's class
+    std::vector<uint32_t> nrep(n, 0);
+    for (size_t i = 0; i + 1 < n; ++i)
+      for (size_t t = 0; t < rep_lens[i]; ++t) nrep[i] += res[i + 1]->cls_one[reps[i][t]] ? 1u : 0u;
+    e = launch_replace_class_chain(haystack, length, (int)n, cls.data(), rep.data(), rl.data(),
+                                   (const uint32_t(*)[2])sw.data(), nrep.data(), out0, out1, capacity, lengths, st,
+                                   cus);
+  }
+  if (dt) { const hipError_t e2 = scratch_free(dt, st); if (e == hipSuccess) e = e2; }
+  if (e == hipErrorNotSupported) return RURE_AMD_ERR_ARG;
+  if (e == hipSuccess) note_fwd_path(-23);
+  return e == hipSuccess ? RURE_AMD_OK : RURE_AMD_ERR_HIP;
+}
+
 int rure_amd_replace_batch(rure *re, const rure_amd_batch *batch, const uint8_t *rep, size_t rep_len, size_t limit,
                            uint8_t *out, uint64_t *out_offsets, size_t out_capacity, uint64_t *total, void *stream) {
   BatchDev b;

@@ -38,6 +38,7 @@ enum class Knob : int {
   ScratchCap,      // bytes of cached scratch kept for reuse
   Timing,          // 1: DFA construction times on stderr
   ReplaceGeneric,  // 1: replace's generic per-block copy, not the grouped copy
+  ChainSeq,        // 1: a replace_all chain step by step, not as one composed byte map
   kCount
 };
 

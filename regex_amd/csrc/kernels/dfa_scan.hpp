@@ -274,6 +274,21 @@ hipError_t launch_replace_copy(const BatchDev &b, const uint64_t *ooff, const ui
 hipError_t launch_replace_class(const uint8_t *hay, uint64_t n, const uint8_t *cls, const uint8_t *rep,
                                 uint32_t rep_len, uint8_t *out, uint64_t cap, uint64_t *ooff, uint64_t *total,
                                 hipStream_t st, int cus, uint32_t sw1, uint32_t sw2);
+// A chain of one-byte-class replace_all calls (replace_scan.hip): step i
+// reads step i - 1's output, buffers alternate out0 / out1, lengths (device,
+// steps + 1) = the input length, then each step's output length; sw[i] = step
+// i's class as up to two SWAR bytes ({0, 0}: wider, counted from cls[i]).
+// The same chain as one byte -> string map composed on the host (blob:
+// |F(x)| 256 u8, offsets 256 u16, changed 256 u8, the strings (<= 4096
+// bytes), per step |F_i(x)| - 1 as 256 u32); the final text to out.
+constexpr uint32_t kHMapPoolMax = 4096;
+hipError_t launch_replace_hmap(const uint8_t *in, uint64_t n, int steps, const uint8_t *blob, uint32_t pool_len,
+                               uint8_t *out, uint64_t cap, uint64_t *lengths, hipStream_t st, int cus);
+// nrep[i] = the bytes of step i's replacement in step i + 1's class.
+hipError_t launch_replace_class_chain(const uint8_t *hay, uint64_t n0, int steps, const uint8_t *const *cls,
+                                      const uint8_t *const *rep, const uint32_t *rep_len, const uint32_t (*sw)[2],
+                                      const uint32_t *nrep, uint8_t *out0, uint8_t *out1, uint64_t cap,
+                                      uint64_t *lengths, hipStream_t st, int cus);
 hipError_t launch_split(const BatchDev &b, const uint64_t *counts, const uint64_t *moff, const uint64_t *m,
                         uint64_t lim, uint64_t *fields, uint64_t *foff, uint64_t *pieces, uint64_t cap,
                         uint64_t nmatches, hipStream_t st, int cus);

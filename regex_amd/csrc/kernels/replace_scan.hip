@@ -764,10 +764,14 @@ __device__ __forceinline__ uint32_t cls_count_co(const uint8_t *cls, const uint4
 
 __global__ __launch_bounds__(256) void replace_cls_count_kernel(const uint8_t *hay, uint64_t n, const uint8_t *cls_g,
                                                                 uint64_t nunits, uint64_t *ucount, uint32_t sw1,
-                                                                uint32_t sw2) {
+                                                                uint32_t sw2, const uint64_t *n_dev) {
   __shared__ uint8_t cls[256];
   cls[threadIdx.x] = cls_g[threadIdx.x];
   __syncthreads();
+  if (n_dev) {  // chained calls: the length on the device (n, nunits: upper bounds; units past it count 0)
+    n = *n_dev;
+    nunits = min(nunits, max<uint64_t>(1, (n + kClsUnit - 1) / kClsUnit));
+  }
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t nw = (uint64_t)gridDim.x * 4;
   // last unit first: the tail of the text is what the previous pass wrote
@@ -788,10 +792,16 @@ __global__ __launch_bounds__(256) void replace_cls_count_kernel(const uint8_t *h
   }
 }
 
-// total (device) = the output length; out_offsets = {0, total}
+// total (device) = the output length; out_offsets = {0, total} (either may
+// be null); n_dev (chained calls): the input length on the device
 __global__ void replace_cls_total_kernel(uint64_t n, uint64_t rep_len, const uint64_t *uoff, uint64_t nunits,
-                                         uint64_t *ooff, uint64_t *total) {
+                                         uint64_t *ooff, uint64_t *total, const uint64_t *n_dev) {
+  if (n_dev) n = *n_dev;
   const uint64_t t = n + uoff[nunits] * rep_len - uoff[nunits];
+  if (!ooff) {
+    *total = t;
+    return;
+  }
   ooff[0] = 0;
   ooff[1] = t;
   *total = t;
@@ -924,6 +934,23 @@ __device__ __forceinline__ uint4 cls_block_map(uint32_t x0, uint32_t c0, uint32_
   return make_uint4(b0, b1, b2, b3);
 }
 
+// The next substitution's class bytes (at most two byte values as SWAR
+// compares, s1 != 0) among a lane's staged bytes, as a 64-bit mask (bytes
+// past avail: none).
+__device__ __forceinline__ uint64_t next_mask(const uint4 *v, uint32_t avail, uint32_t s1, uint32_t s2) {
+  uint64_t m = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t w[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const uint32_t z = (eq_bytes(w[d], s1) | eq_bytes(w[d], s2)) >> 7;  // bits 0, 8, 16, 24
+      m |= (uint64_t)((z * 0x01020408u) >> 24 & 0xFu) << (16 * j + 4 * d);
+    }
+  }
+  return avail >= 64 ? m : m & ((1ull << avail) - 1ull);
+}
+
 struct ClsWave {
   uint8_t txt[kClsUnit + 32];
   uint32_t cnt[kClsMap / 32];  // per block pair: C bytes starting in the block (low, high half)
@@ -933,10 +960,15 @@ struct ClsWave {
   uint16_t slow[kClsSlow];
 };
 
+// n_dev (chained calls): the input length on the device (n, nunits: upper
+// bounds); ncnt (chained calls): the next substitution's class bytes
+// (nsw1 / nsw2) per 4 KiB unit of this output, added up here.
 __global__ __launch_bounds__(256, CLS_WAVES) void replace_cls_write_kernel(const uint8_t *hay, uint64_t n, const uint8_t *cls_g,
                                                                 uint64_t nunits, const uint64_t *uoff,
                                                                 const uint8_t *rep_g, uint32_t L, uint8_t *out,
-                                                                uint64_t cap, uint32_t sw1, uint32_t sw2) {
+                                                                uint64_t cap, uint32_t sw1, uint32_t sw2,
+                                                                const uint64_t *n_dev, uint32_t nsw1, uint32_t nsw2,
+                                                                uint32_t nrep, unsigned long long *ncnt) {
   __shared__ uint8_t cls[256];
   __shared__ uint8_t rep[64];
   __shared__ __attribute__((aligned(16))) ClsWave sw[4];
@@ -946,6 +978,11 @@ __global__ __launch_bounds__(256, CLS_WAVES) void replace_cls_write_kernel(const
   const uint32_t lane = threadIdx.x & 63;
   ClsWave &W = sw[threadIdx.x >> 6];
   const uint64_t nw = (uint64_t)gridDim.x * 4;
+  const uint64_t ulim = nunits;  // the count arrays' units (ncnt: this output's)
+  if (n_dev) {
+    n = *n_dev;
+    nunits = min(nunits, max<uint64_t>(1, (n + kClsUnit - 1) / kClsUnit));
+  }
   for (uint64_t u = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); u < nunits; u += nw) {
     // stage: the lane's 64 bytes, class mask, output offset in the unit
     // (loading the next unit here, behind this one's output, was slower:
@@ -978,6 +1015,63 @@ __global__ __launch_bounds__(256, CLS_WAVES) void replace_cls_write_kernel(const
     if (lane == 63) { W.rel[64] = T; W.rel[65] = T; W.msk[64] = 0; }
     const uint64_t ob = u * kClsUnit + uoff[u] * (L - 1);  // the unit's output start
     const uint32_t o15 = (uint32_t)(ob & 15);
+    if (nsw1) {
+      // the next substitution's class bytes in this lane's output, by 4 KiB
+      // output unit (the next call's units): its text bytes outside this
+      // class, plus the copies in each replacement (nrep of them); a lane
+      // whose output crosses a unit edge places them byte by byte
+      const uint64_t nm = next_mask(v, avail, nsw1, nsw2) & ~m;
+      const uint64_t os = ob + r0, oe = os + len;
+      uint32_t lo = 0, hi = 0;  // counts in unit os >> 12 and the one after
+      if (len == 0 || (os >> 12) == ((oe - 1) >> 12)) {
+        lo = (uint32_t)__popcll(nm) + k * nrep;
+      } else {
+        // bytes before e1 count in the lane's first unit, before e1 + 4096 in
+        // the next; later ones (a lane's output is at most 64 * 64 bytes:
+        // only long replacements reach that far) take an atomic each
+        const uint64_t e1 = (os | 4095) + 1;
+        auto put = [&](uint64_t q) {
+          if (q < e1) ++lo;
+          else if (q < e1 + 4096) ++hi;
+          else if ((q >> 12) < ulim) atomicAdd(&ncnt[q >> 12], 1ull);
+        };
+        uint64_t pos = os;
+        for (uint32_t i = 0; i < avail; ++i) {
+          if ((m >> i) & 1) {
+#pragma unroll 1
+            for (uint32_t t = 0; t < L; ++t) {
+              const uint32_t rb = rep[t] * 0x01010101u;
+              if (rb == nsw1 || rb == nsw2) put(pos + t);
+            }
+            pos += L;
+          } else {
+            if ((nm >> i) & 1) put(pos);
+            ++pos;
+          }
+        }
+      }
+      // lanes' first units are U0 or U0 + 1 (U0 + 2 for a few): two packed sums
+      const uint64_t U0 = ob >> 12;
+      const uint32_t d = (uint32_t)((os >> 12) - U0);
+      uint32_t p01 = 0, p12 = 0;
+      if (d == 0) p01 = lo | hi << 16;
+      else if (d == 1) p12 = lo | hi << 16;
+      else {
+        if (lo) atomicAdd(&ncnt[min(os >> 12, ulim - 1)], (unsigned long long)lo);
+        if (hi) atomicAdd(&ncnt[min((os >> 12) + 1, ulim - 1)], (unsigned long long)hi);
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        p01 += __shfl_xor(p01, o);
+        p12 += __shfl_xor(p12, o);
+      }
+      if (lane == 0) {  // (each half: at most 4096 + 64 * 63 per unit... fits 16 bits)
+        const uint32_t c0 = p01 & 0xFFFF, c1 = (p01 >> 16) + (p12 & 0xFFFF), c2 = p12 >> 16;
+        if (c0 && U0 < ulim) atomicAdd(&ncnt[U0], (unsigned long long)c0);
+        if (c1 && U0 + 1 < ulim) atomicAdd(&ncnt[U0 + 1], (unsigned long long)c1);
+        if (c2 && U0 + 2 < ulim) atomicAdd(&ncnt[U0 + 2], (unsigned long long)c2);
+      }
+    }
     const bool map = o15 + T + 16 <= kClsMap && K <= kClsRank;
     if (map) {
 #pragma unroll
@@ -1098,6 +1192,163 @@ __global__ __launch_bounds__(256, CLS_WAVES) void replace_cls_write_kernel(const
     if (mine && pos < cap) out[pos] = cls_out_byte((uint32_t)(pos - ob), W.rel, W.msk, W.txt, rep, L);
     wave_sync();
   }
+}
+
+// ------------------------------------------------------------------
+// A chain of one-byte-class replace_all steps is a string homomorphism: step
+// i maps each byte of its class to rep_i and every other byte to itself, so
+// the chain maps each byte x to F(x) = h_n(...h_1(x)), a string the host
+// composes (HMap).  The whole chain is then one count pass and one write
+// pass (the sequential chain: a count and a write pass per step), and every
+// intermediate length follows from the input's histogram of the bytes F
+// changes: length_i = n + sum_x hist[x] (|F_i(x)| - 1).
+struct HMapDev {
+  const uint8_t *flen;    // 256: |F(x)| (1..64)
+  const uint16_t *soff;   // 256: offset of F(x) in pool
+  const uint8_t *pool;    // the strings (at most kHMapPool bytes)
+  const uint8_t *active;  // 256: F(x) != x
+  uint32_t pool_len;
+};
+constexpr uint32_t kHMapPool = kHMapPoolMax;
+constexpr uint32_t kHMapOut = 8192;  // a wave's staged output per 4 KiB unit (beyond: direct byte stores)
+
+// The lane's 64 input bytes of unit u (4 loads at a 64-byte stride: the
+// wave's loads cover the unit's 4 KiB, every fetched byte used); avail =
+// bytes before n.
+__device__ __forceinline__ void hmap_load(const uint8_t *in, uint64_t n, uint64_t u, uint32_t lane, uint4 *v,
+                                          uint32_t *avail) {
+  const uint64_t s0 = u * 4096 + 64 * (uint64_t)lane;
+  const uint64_t a = s0 < n ? n - s0 : 0;
+  *avail = a > 64 ? 64u : (uint32_t)a;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = 16u * j < *avail ? *(const uint4 *)(in + s0 + 16 * j) : make_uint4(0, 0, 0, 0);
+}
+
+__device__ __forceinline__ uint32_t byte_at(const uint4 *v, uint32_t i) {
+  const uint4 q = v[i >> 4];
+  const uint32_t k = (i >> 2) & 3, w = k == 0 ? q.x : k == 1 ? q.y : k == 2 ? q.z : q.w;
+  return (w >> (8 * (i & 3))) & 0xFF;
+}
+
+// Per unit: the output bytes it adds (sum of |F(x)| - 1); per block, the
+// histogram of the changed bytes, added to hist once at the end.
+__global__ __launch_bounds__(256) void hmap_count_kernel(const uint8_t *in, uint64_t n, uint64_t nunits, HMapDev h,
+                                                         uint64_t *ucount, unsigned long long *hist) {
+  __shared__ uint8_t fl[256], act[256];
+  __shared__ uint32_t lh[256];
+  fl[threadIdx.x] = h.flen[threadIdx.x];
+  act[threadIdx.x] = h.active[threadIdx.x];
+  lh[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t nw = (uint64_t)gridDim.x * 4;
+  for (uint64_t u = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); u < nunits; u += nw) {
+    uint4 v[4];
+    uint32_t avail;
+    hmap_load(in, n, u, lane, v, &avail);
+    uint32_t extra = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 64; ++i) {
+      const uint32_t x = byte_at(v, i);
+      const bool in_ = i < avail;
+      extra += in_ ? fl[x] - 1u : 0u;
+      if (in_ && act[x]) atomicAdd(&lh[x], 1u);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) extra += __shfl_xor(extra, o);
+    if (lane == 0) ucount[u] = extra;
+  }
+  __syncthreads();
+  if (lh[threadIdx.x]) atomicAdd(&hist[threadIdx.x], (unsigned long long)lh[threadIdx.x]);
+}
+
+// Per unit: the lane's output (its bytes' images) staged in LDS at the
+// unit's output alignment, then whole aligned 16-byte blocks stored by
+// consecutive lanes, the two edge blocks byte by byte (they share an aligned
+// block with the neighbouring units: byte stores do not race).  uoff =
+// exclusive sums of the units' added bytes.
+__global__ __launch_bounds__(256) void hmap_write_kernel(const uint8_t *in, uint64_t n, uint64_t nunits, HMapDev h,
+                                                         const uint64_t *uoff, uint8_t *out, uint64_t cap) {
+  __shared__ uint8_t fl[256];
+  __shared__ uint16_t so[256];
+  __shared__ __attribute__((aligned(16))) uint8_t pool[kHMapPool];
+  __shared__ __attribute__((aligned(16))) uint8_t obuf[4][kHMapOut + 32];
+  fl[threadIdx.x] = h.flen[threadIdx.x];
+  so[threadIdx.x] = h.soff[threadIdx.x];
+  for (uint32_t i = threadIdx.x; i < h.pool_len; i += blockDim.x) pool[i] = h.pool[i];
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63;
+  uint8_t *ob_ = obuf[threadIdx.x >> 6];
+  const uint64_t nw = (uint64_t)gridDim.x * 4;
+  for (uint64_t u = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); u < nunits; u += nw) {
+    uint4 v[4];
+    uint32_t avail;
+    hmap_load(in, n, u, lane, v, &avail);
+    uint32_t len = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 64; ++i) len += i < avail ? fl[byte_at(v, i)] : 0u;
+    uint32_t incl = len;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t x = __shfl_up(incl, o);
+      if (lane >= (uint32_t)o) incl += x;
+    }
+    const uint32_t T = __shfl(incl, 63), r0 = incl - len;
+    const uint64_t ob = u * 4096 + uoff[u];  // the unit's output start
+    const uint32_t o15 = (uint32_t)(ob & 15);
+    if (o15 + T + 16 > kHMapOut) {  // a unit that grows past the stage: byte stores
+      uint64_t p = ob + r0;
+      for (uint32_t i = 0; i < avail; ++i) {
+        const uint32_t x = byte_at(v, i), l = fl[x], o = so[x];
+        for (uint32_t t = 0; t < l; ++t, ++p)
+          if (p < cap) out[p] = pool[o + t];
+      }
+      continue;
+    }
+    {  // stage: the lane's images at o15 + r0 ..
+      uint32_t p = o15 + r0;
+#pragma unroll 4
+      for (uint32_t i = 0; i < avail; ++i) {
+        const uint32_t x = byte_at(v, i), l = fl[x];
+        if (l == 1) {
+          ob_[p++] = pool[so[x]];
+        } else {
+          const uint32_t o = so[x];
+          for (uint32_t t = 0; t < l; ++t) ob_[p++] = pool[o + t];
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint64_t base = ob - o15, E = ob + T;
+    const uint64_t A = (ob + 15) & ~(uint64_t)15, B = E & ~(uint64_t)15;
+    for (uint64_t q = A + 16 * (uint64_t)lane; q < B; q += 1024) {
+      const uint4 x = *(const uint4 *)(ob_ + (q - base));
+      if (q + 16 <= cap) *(uint4 *)(out + q) = x;
+      else for (uint32_t j = 0; q + j < cap; ++j) out[q + j] = ob_[q - base + j];
+    }
+    // the edges: [ob, min(A, E)) and [max(B, A), E)
+    const uint64_t h1 = min(A, E), t0 = max(B, A);
+    const uint64_t pos = lane < 16 ? ob + lane : t0 + (lane - 16);
+    const bool mine = lane < 16 ? pos < h1 : (lane < 32 && pos < E);
+    if (mine && pos < cap) out[pos] = ob_[pos - base];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
+// lengths[i + 1] = n + sum_x hist[x] * dlen[i * 256 + x] (dlen = |F_i(x)| - 1
+// for the bytes F changes), one thread per step
+__global__ void hmap_lengths_kernel(uint64_t n, int steps, const unsigned long long *hist, const uint32_t *dlen,
+                                    uint64_t *lengths) {
+  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (i == 0) lengths[0] = n;
+  if (i >= steps) return;
+  uint64_t t = n;
+  for (int x = 0; x < 256; ++x) t += (uint64_t)hist[x] * dlen[(size_t)i * 256 + x];
+  lengths[i + 1] = t;
 }
 
 }  // namespace
@@ -1278,16 +1529,119 @@ hipError_t launch_replace_class(const uint8_t *hay, uint64_t n, const uint8_t *c
   const int gridw = (int)std::max<uint64_t>(1, std::min<uint64_t>((nunits + 3) / 4, (uint64_t)cus * occ_w));
   do {
     if ((e = hipMemsetAsync(ucount + nunits, 0, 8, st)) != hipSuccess) break;
-    hipLaunchKernelGGL(replace_cls_count_kernel, dim3(grid), dim3(256), 0, st, hay, n, cls, nunits, ucount, sw1, sw2);
+    hipLaunchKernelGGL(replace_cls_count_kernel, dim3(grid), dim3(256), 0, st, hay, n, cls, nunits, ucount, sw1, sw2,
+                       (const uint64_t *)nullptr);
     if ((e = hipGetLastError()) != hipSuccess) break;
     if ((e = exclusive_scan_u64(ucount, uoff, nunits + 1, st)) != hipSuccess) break;
     hipLaunchKernelGGL(replace_cls_total_kernel, dim3(1), dim3(1), 0, st, n, (uint64_t)rep_len, uoff, nunits, ooff,
-                       total);
+                       total, (const uint64_t *)nullptr);
     if ((e = hipGetLastError()) != hipSuccess) break;
     if (cap) {
       hipLaunchKernelGGL(replace_cls_write_kernel, dim3(gridw), dim3(256), 0, st, hay, n, cls, nunits, uoff, rep,
-                         rep_len, out, cap, sw1, sw2);
+                         rep_len, out, cap, sw1, sw2, (const uint64_t *)nullptr, 0u, 0u, 0u,
+                         (unsigned long long *)nullptr);
       e = hipGetLastError();
+    }
+  } while (false);
+  hipError_t e2 = scratch_free(buf, st);
+  return e != hipSuccess ? e : e2;
+}
+
+// The chain as one byte -> string map (see HMapDev): tab = per byte |F(x)|
+// (256 u8), soff (256 u16), active (256 u8), the pool, then per step i
+// |F_i(x)| - 1 as 256 u32 (device, one blob); the final text goes to out.
+hipError_t launch_replace_hmap(const uint8_t *in, uint64_t n, int steps, const uint8_t *blob, uint32_t pool_len,
+                               uint8_t *out, uint64_t cap, uint64_t *lengths, hipStream_t st, int cus) {
+  HMapDev h;
+  h.flen = blob;
+  h.soff = (const uint16_t *)(blob + 256);
+  h.active = blob + 768;
+  h.pool = blob + 1024;
+  h.pool_len = pool_len;
+  const uint32_t *dlen = (const uint32_t *)(blob + 1024 + kHMapPool);
+  if (pool_len > kHMapPool) return hipErrorNotSupported;
+  const uint64_t nunits = std::max<uint64_t>(1, (n + 4095) / 4096);
+  uint64_t *buf = nullptr;
+  hipError_t e = scratch_malloc((void **)&buf, (2 * (nunits + 1) + 256) * 8, st);
+  if (e != hipSuccess) return e;
+  uint64_t *ucount = buf, *uoff = buf + nunits + 1;
+  unsigned long long *hist = (unsigned long long *)(uoff + nunits + 1);
+  do {
+    if ((e = hipMemsetAsync(ucount + nunits, 0, 8, st)) != hipSuccess) break;
+    if ((e = hipMemsetAsync(hist, 0, 256 * 8, st)) != hipSuccess) break;
+    const int g = grid_for_items((nunits + 3) / 4 * 256, 256, cus);
+    const int gw = std::min(g, cus * 4);  // (the write kernel's LDS stage: 4 blocks per CU)
+    hipLaunchKernelGGL(hmap_count_kernel, dim3(g), dim3(256), 0, st, in, n, nunits, h, ucount, hist);
+    if ((e = hipGetLastError()) != hipSuccess) break;
+    if ((e = exclusive_scan_u64(ucount, uoff, nunits + 1, st)) != hipSuccess) break;
+    hipLaunchKernelGGL(hmap_write_kernel, dim3(gw), dim3(256), 0, st, in, n, nunits, h, uoff, out, cap);
+    if ((e = hipGetLastError()) != hipSuccess) break;
+    hipLaunchKernelGGL(hmap_lengths_kernel, dim3(1), dim3(std::max(64, (steps + 63) / 64 * 64)), 0, st, n, steps,
+                       (const unsigned long long *)hist, dlen, lengths);
+    e = hipGetLastError();
+  } while (false);
+  hipError_t e2 = scratch_free(buf, st);
+  return e != hipSuccess ? e : e2;
+}
+
+// A chain of replace_all calls of one-byte-class regexes over one haystack
+// (the IUB substitutions), step i reading step i - 1's output: buffers
+// alternate out0, out1, out0, ...  The input of step i > 0 is counted by step
+// i - 1's write kernel as it writes it (the next class as SWAR bytes,
+// nxt[i][0..1], when the class has at most two bytes), so only step 0 and
+// steps after a wider class run the count pass; the lengths stay on the
+// device (lengths[i + 1] = the output length of step i) and nothing is read
+// back.  Outputs past cap are cut (the lengths still count them; a step whose
+// input was cut reads garbage past cap, so the caller checks lengths[steps]
+// <= cap: replacements are never shorter than the byte they replace, so the
+// lengths only grow).
+hipError_t launch_replace_class_chain(const uint8_t *hay, uint64_t n0, int steps, const uint8_t *const *cls,
+                                      const uint8_t *const *rep, const uint32_t *rep_len, const uint32_t (*sw)[2],
+                                      const uint32_t *nrep, uint8_t *out0, uint8_t *out1, uint64_t cap,
+                                      uint64_t *lengths, hipStream_t st, int cus) {
+  if (steps <= 0) return hipSuccess;
+  if (((uintptr_t)hay & 15) || ((uintptr_t)out0 & 15) || ((uintptr_t)out1 & 15)) return hipErrorNotSupported;
+  for (int i = 0; i < steps; ++i)
+    if (rep_len[i] > 64 || rep_len[i] == 0) return hipErrorNotSupported;
+  int dev = 0, occ_c = 0, occ_w = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if ((e = cls_occupancy(dev, &occ_c, &occ_w)) != hipSuccess) return e;
+  // units: enough for the largest input (n0 or cap)
+  const uint64_t nmax = std::max<uint64_t>(n0, cap);
+  const uint64_t nunits = std::max<uint64_t>(1, (nmax + kClsUnit - 1) / kClsUnit);
+  uint64_t *buf = nullptr;
+  if ((e = scratch_malloc((void **)&buf, (3 * (nunits + 1) + 1) * 8, st)) != hipSuccess) return e;
+  uint64_t *cnt[2] = {buf, buf + nunits + 1}, *uoff = buf + 2 * (nunits + 1);
+  const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((nunits + 7) / 8, (uint64_t)cus * occ_c));
+  const int gridw = (int)std::max<uint64_t>(1, std::min<uint64_t>((nunits + 3) / 4, (uint64_t)cus * occ_w));
+  do {
+    if ((e = hipMemcpyAsync(lengths, &n0, 8, hipMemcpyHostToDevice, st)) != hipSuccess) break;
+    bool counted = false;  // cnt[i & 1] holds step i's unit counts
+    for (int i = 0; i < steps && e == hipSuccess; ++i) {
+      const uint8_t *in = i == 0 ? hay : (i & 1) ? out0 : out1;
+      uint8_t *out = (i & 1) ? out1 : out0;
+      const uint64_t n = i == 0 ? n0 : nmax;  // (an upper bound past step 0: the kernels read lengths[i])
+      const uint64_t *n_dev = i == 0 ? nullptr : lengths + i;
+      uint64_t *c = cnt[i & 1], *cn = cnt[(i + 1) & 1];
+      if (!counted) {
+        if ((e = hipMemsetAsync(c, 0, (nunits + 1) * 8, st)) != hipSuccess) break;
+        hipLaunchKernelGGL(replace_cls_count_kernel, dim3(grid), dim3(256), 0, st, in, n, cls[i], nunits, c,
+                           sw[i][0], sw[i][1], n_dev);
+        if ((e = hipGetLastError()) != hipSuccess) break;
+      }
+      if ((e = exclusive_scan_u64(c, uoff, nunits + 1, st)) != hipSuccess) break;
+      const bool chain = i + 1 < steps && sw[i + 1][0] != 0;
+      if (chain && (e = hipMemsetAsync(cn, 0, (nunits + 1) * 8, st)) != hipSuccess) break;
+      hipLaunchKernelGGL(replace_cls_write_kernel, dim3(gridw), dim3(256), 0, st, in, n, cls[i], nunits, uoff, rep[i],
+                         rep_len[i], out, cap, sw[i][0], sw[i][1], n_dev, chain ? sw[i + 1][0] : 0u,
+                         chain ? sw[i + 1][1] : 0u, chain ? nrep[i] : 0u,
+                         chain ? (unsigned long long *)cn : (unsigned long long *)nullptr);
+      if ((e = hipGetLastError()) != hipSuccess) break;
+      hipLaunchKernelGGL(replace_cls_total_kernel, dim3(1), dim3(1), 0, st, n, (uint64_t)rep_len[i], uoff, nunits,
+                         (uint64_t *)nullptr, lengths + i + 1, n_dev);
+      e = hipGetLastError();
+      counted = chain;
     }
   } while (false);
   hipError_t e2 = scratch_free(buf, st);

@@ -46,6 +46,7 @@ namespace rure_amd {
 namespace {
 
 constexpr uint32_t kRunUnit = 4096;  // bytes per wave unit: 64 lanes x 64 bytes
+constexpr uint32_t kRunWin = 256;    // records per wave staged in LDS by the emit pass (4 KiB)
 
 // Whether byte q of the haystack at base (bytes [lo, len) visible) belongs
 // to a valid UTF-8 encoding of a code point in the bitmap cp.
@@ -118,9 +119,14 @@ __global__ __launch_bounds__(256) void run_iter_kernel(BatchDev b, const uint8_t
                                                        const uint64_t *uoff, const uint64_t *uzs, uint64_t *matches,
                                                        uint64_t cap, uint32_t *quit) {
   __shared__ uint8_t cls[256];
+  // EMIT: a window of kRunWin records per wave, written to LDS by the lanes
+  // that own them and copied out as whole 1 KiB stores (lanes write their
+  // runs' records at scattered indices, 16 B at a time otherwise)
+  __shared__ uint4 recs[EMIT ? 4 * kRunWin : 1];
   if (threadIdx.x < 256) cls[threadIdx.x] = cls_g[threadIdx.x];
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63;
+  uint4 *wrec = recs + (EMIT ? (threadIdx.x >> 6) * kRunWin : 0);
   const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
   for (uint64_t u = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); u < nunits; u += nwaves) {
     const uint64_t h = u / nk, k = u - h * nk;
@@ -164,15 +170,18 @@ __global__ __launch_bounds__(256) void run_iter_kernel(BatchDev b, const uint8_t
       }
       continue;
     }
-    // the record index of this lane's first run: the unit's offset plus the
-    // runs of the lanes before it
+    // the record index of this lane's first run in the unit: the runs of the
+    // lanes before it
     uint32_t incl = n;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t x = __shfl_up(incl, o);
       if (lane >= (uint32_t)o) incl += x;
     }
-    uint64_t at = uoff[u] + (incl - n);
+    const uint32_t T = __shfl(incl, 63);  // the unit's runs
+    const uint64_t at0 = uoff[u];
+    const bool a16 = ((uintptr_t)matches & 15) == 0;
+    uint32_t r = incl - n;
     // the first byte not in C in the lanes after this one (suffix minimum)
     uint64_t after = __shfl_down(fz, 1);
     if (lane == 63) after = 1ull << 63;
@@ -182,26 +191,45 @@ __global__ __launch_bounds__(256) void run_iter_kernel(BatchDev b, const uint8_t
       if (lane + o < 64) after = min(after, x);
     }
     uint64_t st = starts;
-    while (st) {
-      const uint32_t i = (uint32_t)__builtin_ctzll(st);
-      st &= st - 1;
-      const uint64_t rest = nz >> i;  // bit 0 = byte i itself (in C)
-      uint64_t e;
-      if (rest) {
-        e = s0 + i + (uint64_t)__builtin_ctzll(rest);
-      } else if (after != (1ull << 63)) {
-        e = after;
-      } else if (k + 1 == nk) {  // the haystack's last unit: its end
-        e = len;
-      } else {  // the run continues past the unit
-        e = uzs[u + 1] - h * b.stride;
+    for (uint32_t w0 = 0; w0 < T; w0 += kRunWin) {
+      while (st && r < w0 + kRunWin) {  // this lane's records in the window
+        const uint32_t i = (uint32_t)__builtin_ctzll(st);
+        st &= st - 1;
+        const uint64_t rest = nz >> i;  // bit 0 = byte i itself (in C)
+        uint64_t e;
+        if (rest) {
+          e = s0 + i + (uint64_t)__builtin_ctzll(rest);
+        } else if (after != (1ull << 63)) {
+          e = after;
+        } else if (k + 1 == nk) {  // the haystack's last unit: its end
+          e = len;
+        } else {  // the run continues past the unit
+          e = uzs[u + 1] - h * b.stride;
+        }
+        if (e > len) e = len;
+        const uint64_t sp = s0 + i;
+        wrec[r - w0] = make_uint4((uint32_t)sp, (uint32_t)(sp >> 32), (uint32_t)e, (uint32_t)(e >> 32));
+        ++r;
       }
-      if (e > len) e = len;
-      if (at < cap) {
-        matches[2 * at] = s0 + i;
-        matches[2 * at + 1] = e;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const uint32_t nrec = min(kRunWin, T - w0);
+      for (uint32_t j = lane; j < nrec; j += 64) {
+        const uint64_t g = at0 + w0 + j;
+        if (g < cap) {
+          const uint4 v = wrec[j];
+          if (a16) {
+            *(uint4 *)(matches + 2 * g) = v;
+          } else {  // records only 8-byte aligned
+            matches[2 * g] = (uint64_t)v.x | (uint64_t)v.y << 32;
+            matches[2 * g + 1] = (uint64_t)v.z | (uint64_t)v.w << 32;
+          }
+        }
       }
-      ++at;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
   }
 }

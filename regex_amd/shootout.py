@@ -5,7 +5,8 @@ on the device, through the C ABI only:
   2. the 9 variant find_iter counts (:24-42) — rure_amd_find_iter_span_multi
      (one fused pass over the stripped stream)
   3. the 11 IUB substitutions (:44-60), each a replace_all of one byte by its
-     alternation text — rure_amd_replace_batch, chained
+     alternation text — rure_amd_replace_all_chain: the 11 steps enqueued
+     at once, each step's kernel counting the next step's byte as it writes
   4. the three lengths the program prints (:65): input, stripped, substituted
 
 The sequence stays in HBM from the input to the last substitution; only the
@@ -14,7 +15,7 @@ counts and lengths are read back.
 import ctypes
 
 from . import _native as N
-from . import Regex, _check, _stream_ptr, find_iter_span_multi
+from . import Regex, _check, _stream_ptr, find_iter_span_multi, replace_all_chain
 
 STRIP = b">[^\n]*\n|\n"
 VARIANTS = [
@@ -75,8 +76,14 @@ class RegexDna(object):
         res = find_iter_span_multi(self.variants, stripped, 0, clen, length=clen, capacities=[1 << 16] * 9,
                                    stream=stream)
         counts = [int(c.item()) for c, _, _ in res]
-        cur, cl = stripped, clen
-        for re_, rep in self.substs:
-            # each IUB code byte grows to len(rep): size the output generously
-            cur, cl = self._replace(re_, cur, cl, rep, stream, cl + cl // 4 + 1024)
-        return {"counts": counts, "ilen": n, "clen": clen, "slen": cl}
+        # the 11 substitutions in one enqueue; the final length is the one
+        # read-back (a cut output, lengths[-1] > capacity, reruns sized exactly)
+        cap = clen + clen // 4 + 4096
+        while True:
+            _, lengths = replace_all_chain([r for r, _ in self.substs], [t for _, t in self.substs], stripped,
+                                           length=clen, capacity=cap, stream=stream)
+            sl = int(lengths[-1].item())
+            if sl <= cap:
+                break
+            cap = sl
+        return {"counts": counts, "ilen": n, "clen": clen, "slen": sl}

@@ -96,3 +96,92 @@ def test_iub_chain_known_length(cuda):
         import torch
         cur = torch.cat([out[:n], torch.zeros(16, dtype=torch.uint8, device=cuda)])
     assert n == kc["substituted_len"], (n, kc["substituted_len"])
+
+
+def chain_expect(steps, t):
+    for re, rep in steps:
+        t = expect(re, t, rep)
+    return t
+
+
+CHAINS = [
+    # the IUB substitutions' shape: one byte each, the next step's byte counted as written
+    [(r"B", b"(c|g|t)"), (r"D", b"(a|g|t)"), (r"N", b"(a|c|g|t)")],
+    # two-byte classes (SWAR), a wide class (the count pass), a 64-byte replacement
+    [(r"[KM]", b"<km>"), (r"[a-c]", b"Q"), (r"Q", b"<" + b"q" * 62 + b">"), (r"[<>]", b"D")],
+    # replacements that create the next step's bytes, and a one-step chain
+    [(r"x", b"yxy"), (r"y", b"xx")],
+    [(r"(?-u)\xff", b"\xff\xfe\xff")],
+]
+
+
+@pytest.mark.parametrize("seq", [0, 1])
+@pytest.mark.parametrize("ci", range(len(CHAINS)))
+@pytest.mark.parametrize("n", [0, 1, 63, 4096, 4097, 70001, 300007])
+def test_replace_chain(cuda, knobs, seq, ci, n):
+    """rure_amd_replace_all_chain against the host rule applied step by step:
+    the same bytes and every intermediate length — as one composed byte map
+    (default, last_fwd_path -24) and step by step (knob chain_seq=1, -23)."""
+    if seq:
+        knobs(chain_seq=1)
+    steps = [(R.Regex(p), rep) for p, rep in CHAINS[ci]]
+    alpha = b"acgtBDNKMxy\xff\xfe<>Q\n"
+    t = text(ci * 1000 + n, n, alpha)
+    out, lengths = R.replace_all_chain([r for r, _ in steps], [rep for _, rep in steps], dev(t, cuda), length=n,
+                                       capacity=16 * n + 4096)
+    exp, lens = t, [n]
+    for re, rep in steps:
+        exp = expect(re, exp, rep)
+        lens.append(len(exp))
+    assert lengths.cpu().numpy().tolist() == lens
+    assert bytes(out[:lens[-1]].cpu().numpy()) == exp
+    if n:
+        assert N.rure_amd_last_fwd_path() == (-23 if seq else -24)
+
+
+@pytest.mark.parametrize("seq", [0, 1])
+def test_replace_chain_cut(cuda, knobs, seq):
+    """A capacity below an intermediate length: that step's length is exact,
+    the later ones are at least as large (step by step they are lower bounds:
+    a step reads its input cut), so lengths[-1] > capacity and the caller
+    retries with it until the chain fits."""
+    if seq:
+        knobs(chain_seq=1)
+    steps = [(R.Regex(r"x"), b"x" * 40), (R.Regex(r"y"), b"yy"), (R.Regex(r"z"), b"zzz")]
+    t = text(5, 20000, b"xyz ")
+    exps = [t]
+    for re, rep in steps:
+        exps.append(expect(re, exps[-1], rep))
+    cap, tries = len(t) + 100, 0
+    while True:
+        out, lengths = R.replace_all_chain([r for r, _ in steps], [rep for _, rep in steps], dev(t, cuda),
+                                           length=len(t), capacity=cap)
+        ln = lengths.cpu().numpy().tolist()
+        tries += 1
+        assert ln[0] == len(t) and ln[1] == len(exps[1]) and ln[1] <= ln[2] <= ln[3]
+        if ln[3] <= cap:
+            break
+        assert ln[3] > cap
+        cap = ln[3]
+    assert tries >= 2
+    assert ln == [len(x) for x in exps]
+    assert bytes(out[:ln[3]].cpu().numpy()) == exps[3]
+
+
+def test_replace_chain_rejects(cuda):
+    """A regex whose matches are not single class bytes is refused."""
+    with pytest.raises(Exception):
+        R.replace_all_chain([R.Regex(r"ab")], [b"x"], dev(b"abab", cuda), length=4)
+
+
+def test_replace_chain_long_images(cuda):
+    """Images longer than 64 bytes after composition (x -> 40 x, then each x
+    -> 2 x): the call runs the chain step by step (-23), same bytes."""
+    steps = [(R.Regex(r"x"), b"x" * 40), (R.Regex(r"x"), b"xx")]
+    t = text(9, 5000, b"xab")
+    out, lengths = R.replace_all_chain([r for r, _ in steps], [rep for _, rep in steps], dev(t, cuda), length=len(t),
+                                       capacity=100 * len(t))
+    assert N.rure_amd_last_fwd_path() == -23
+    exp = chain_expect(steps, t)
+    assert int(lengths[-1]) == len(exp)
+    assert bytes(out[:len(exp)].cpu().numpy()) == exp

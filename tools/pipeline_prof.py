@@ -17,6 +17,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 from regex_amd import shootout  # noqa: E402
 from regex_amd import find_iter_span_multi  # noqa: E402
+import regex_amd as R  # noqa: E402
 from golden_data import corpus  # noqa: E402
 
 reps = int(sys.argv[sys.argv.index("--reps") + 1]) if "--reps" in sys.argv else 5
@@ -45,13 +46,13 @@ for rep in range(reps + 1):
     (stripped, clen), row["strip"] = stage(lambda: dna._replace(dna.strip, big, N, b"", None, N))
     _, row["variants"] = stage(lambda: find_iter_span_multi(dna.variants, stripped, 0, clen, length=clen,
                                                             capacities=[1 << 16] * 9))
-    cur, cl = stripped, clen
-    for re_, r in dna.substs:
-        prev = cl
-        name = "iub_" + (re_.pattern.decode() if isinstance(re_.pattern, bytes) else str(re_.pattern))
-        (cur, cl), row[name] = stage(
-            lambda: dna._replace(re_, cur, cl, r, None, cl + cl // 4 + 1024))
-        row.setdefault("_grow", []).append(cl - prev)
+    cap = clen + clen // 4 + 4096
+    (_, lengths), row["iub_chain"] = stage(lambda: R.replace_all_chain([r for r, _ in dna.substs],
+                                                                       [t for _, t in dna.substs], stripped,
+                                                                       length=clen, capacity=cap))
+    lens = lengths.cpu().numpy().tolist()
+    cl = lens[-1]
+    row["_grow"] = [b - a for a, b in zip(lens[:-1], lens[1:])]
     if rep:
         rows.append(row)
 keys = [k for k in rows[0] if not k.startswith("_")]

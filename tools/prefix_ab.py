@@ -22,7 +22,9 @@ from regex_amd import _native as N  # noqa: E402
 from golden_data import corpus  # noqa: E402
 
 PATS = [r"(?i)holmes\w*", r"Sherlock\s+\w+", r"(?i)watson\w*", r"Holmes\s+\w+", r"(?i)baker\s+street",
-        r"(?i)the\s+\w+", r"(?i)zqxj\w*", r">[^\n]*\n"]
+        r"(?i)the\s+\w+", r"(?i)zqxj\w*", r">[^\n]*\n",
+        # held out (round 6): not looked at when the dispatch was chosen
+        r"(?i)moriarty", r"Lestrade\s+\w+", r"(?i)lady\s+\w+", r"(?i)inspector"]
 MODES = [("off", "prefix=0"), ("first", "prefix=1"), ("rare", "prefix=2"), ("default", None)]
 
 
