@@ -549,7 +549,18 @@ void set_prefix_skip(const rure *re, FwdDfaDev *f) {
   // skip where the first bytes are several ((?i)holmes\w* 1.41 -> 1.14 ms,
   // (?i)watson\w* 1.68 -> 1.61, (?i)zqxj\w* 1.11 -> 0.54; (?i)baker\s+street
   // loses, 1.48 -> 1.56: "b.k" of "back", "book").
-  const bool rare_ok = bi >= 0 && mode != 1;
+  // ... and the rare skip only where the byte it keys on is rare by the
+  // reference's own ranking (freqs.rs: rank <= 150 — q, j, z, most capitals,
+  // control and high bytes), the way FreqyPacked picks a byte for memchr
+  // (literals.rs:390-510): on English text a pair of common letters is in
+  // most 128-byte bursts whatever the product of their frequencies says
+  // (r06 A/B: (?i)moriarty's "mo" cost 58 %, (?i)baker's "ba" 15 %), and a
+  // burst that holds a candidate is tested and then stepped anyway
+  auto cls_rank = [&](int j) {
+    return orm[j] ? std::max(kByteRank[rep[j]], kByteRank[rep[j] ^ 0x20]) : kByteRank[rep[j]];
+  };
+  const bool rare_byte = bi >= 0 && std::min(cls_rank(bi), cls_rank(bi + bd)) <= 150;
+  const bool rare_ok = bi >= 0 && mode != 1 && (mode == 2 || rare_byte);
   const bool first_use = n > 0 && mode != 2;
   if (rare_ok && (mode == 2 || !(first_use && n == 1))) {
     f->rare_on = 1;

@@ -710,10 +710,13 @@ int rure_amd_replace_all_chain(rure *const *res, const uint8_t *const *reps, con
       std::vector<uint8_t> blob(1024 + kHMapPoolMax + n * 256 * 4, 0);
       uint16_t *so = (uint16_t *)(blob.data() + 256);
       size_t at = 0;
+      uint32_t nact = 0;
       for (int x = 0; x < 256; ++x) {
         blob[x] = (uint8_t)img[x].size();
         so[x] = (uint16_t)at;
-        blob[768 + x] = !(img[x].size() == 1 && (uint8_t)img[x][0] == x);
+        const bool same = img[x].size() == 1 && (uint8_t)img[x][0] == x;
+        blob[768 + x] = same ? 0xFF : (uint8_t)nact;
+        nact += same ? 0 : 1;
         memcpy(blob.data() + 1024 + at, img[x].data(), img[x].size());
         at += img[x].size();
       }
@@ -723,7 +726,8 @@ int rure_amd_replace_all_chain(rure *const *res, const uint8_t *const *reps, con
       if (e == hipSuccess) e = hipMemcpyAsync(db, blob.data(), blob.size(), hipMemcpyHostToDevice, st);
       uint8_t *out = (n & 1) ? out0 : out1;
       if (e == hipSuccess)
-        e = launch_replace_hmap(haystack, length, (int)n, db, (uint32_t)pool, out, capacity, lengths, st, cus);
+        e = launch_replace_hmap(haystack, length, (int)n, db, (uint32_t)pool, nact, out, capacity, lengths, st,
+                                cus);
       if (db) { const hipError_t e2 = scratch_free(db, st); if (e == hipSuccess) e = e2; }
       if (e == hipSuccess) note_fwd_path(-24);
       if (e != hipErrorNotSupported) return e == hipSuccess ? RURE_AMD_OK : RURE_AMD_ERR_HIP;

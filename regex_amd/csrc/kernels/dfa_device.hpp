@@ -283,17 +283,15 @@ __device__ __forceinline__ void fwd_range(LaneState &L, const FwdDfaDev &f, cons
 #pragma unroll 1
     for (; j < 16 && at < end && !L.done; ++j, ++at) step1<MODE>(L, f, lds, (w[j >> 2] >> ((j & 3) * 8)) & 0xFF, at);
   }
-  // the skip's own effectiveness: bursts it tested and bursts that held a
-  // candidate; once at least half of 32 or more held one, testing costs more
-  // than it saves (each such burst is tested, then stepped anyway) and this
-  // lane steps the rest of its range without it (results never depend on it)
-  uint32_t sk_n = 0, sk_hit = 0;
-  bool sk_on = PFX && (f.pfx_n || f.rare_on);
+  // (Tried, round 6: a lane switching its skip off once half of 8 or 32
+  // tested bursts held a candidate.  Worse: a lane that stops skipping still
+  // runs this instantiation, with half the waves of the one without the skip
+  // loop, so the first-byte skip lost 19-42 % where a few early bursts held
+  // its byte; profiles/r06_prefix_ab.jsonl.)
   while (!L.done && at + 128 <= end) {
-    if (PFX && sk_on && L.s + 1 == f.ustart1) {
+    if (PFX && (f.pfx_n || f.rare_on) && L.s + 1 == f.ustart1) {
       // start-state prefix skip (dfa.rs:700-711): bursts without a prefix
       // first byte cannot start a match, and the state stays the start state
-      bool hit = false;
       while (true) {
         uint4 t[9];
         const uint4 *q = (const uint4 *)(base + at);
@@ -301,18 +299,15 @@ __device__ __forceinline__ void fwd_range(LaneState &L, const FwdDfaDev &f, cons
           if (at + 144 > end) break;  // (the window's 16 bytes past the burst)
 #pragma unroll
           for (int k = 0; k < 9; ++k) t[k] = q[k];
-          hit = rare_hit(f, t);
+          if (rare_hit(f, t)) break;
         } else {
 #pragma unroll
           for (int k = 0; k < 8; ++k) t[k] = q[k];
-          hit = prefix_hit(f, t);
+          if (prefix_hit(f, t)) break;
         }
-        ++sk_n;
-        if (hit) break;
         at += 128;
         if (at + 128 > end) break;
       }
-      if (hit && ++sk_hit * 2 >= sk_n && sk_n >= 32) sk_on = false;
       if (at + 128 > end) break;
     }
     const uint4 *p = (const uint4 *)(base + at);

@@ -279,11 +279,13 @@ hipError_t launch_replace_class(const uint8_t *hay, uint64_t n, const uint8_t *c
 // steps + 1) = the input length, then each step's output length; sw[i] = step
 // i's class as up to two SWAR bytes ({0, 0}: wider, counted from cls[i]).
 // The same chain as one byte -> string map composed on the host (blob:
-// |F(x)| 256 u8, offsets 256 u16, changed 256 u8, the strings (<= 4096
-// bytes), per step |F_i(x)| - 1 as 256 u32); the final text to out.
+// |F(x)| 256 u8, offsets 256 u16, changed-byte indices 256 u8 (0xFF: F(x) =
+// x; nact changed), the strings (<= 4096 bytes), per step |F_i(x)| - 1 as
+// 256 u32); the final text to out.
 constexpr uint32_t kHMapPoolMax = 4096;
 hipError_t launch_replace_hmap(const uint8_t *in, uint64_t n, int steps, const uint8_t *blob, uint32_t pool_len,
-                               uint8_t *out, uint64_t cap, uint64_t *lengths, hipStream_t st, int cus);
+                               uint32_t nact, uint8_t *out, uint64_t cap, uint64_t *lengths, hipStream_t st,
+                               int cus);
 // nrep[i] = the bytes of step i's replacement in step i + 1's class.
 hipError_t launch_replace_class_chain(const uint8_t *hay, uint64_t n0, int steps, const uint8_t *const *cls,
                                       const uint8_t *const *rep, const uint32_t *rep_len, const uint32_t (*sw)[2],

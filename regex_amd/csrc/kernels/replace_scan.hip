@@ -1205,88 +1205,168 @@ __global__ __launch_bounds__(256, CLS_WAVES) void replace_cls_write_kernel(const
 struct HMapDev {
   const uint8_t *flen;    // 256: |F(x)| (1..64)
   const uint16_t *soff;   // 256: offset of F(x) in pool
+  const uint8_t *aidx;    // 256: index of x among the bytes F changes, 0xFF if F(x) = x
   const uint8_t *pool;    // the strings (at most kHMapPool bytes)
-  const uint8_t *active;  // 256: F(x) != x
   uint32_t pool_len;
+  uint32_t nact;          // bytes F changes
 };
 constexpr uint32_t kHMapPool = kHMapPoolMax;
 constexpr uint32_t kHMapOut = 8192;  // a wave's staged output per 4 KiB unit (beyond: direct byte stores)
+constexpr uint32_t kHMapReg = 16;    // changed bytes counted in lane registers (more: LDS atomics)
 
-// The lane's 64 input bytes of unit u (4 loads at a 64-byte stride: the
-// wave's loads cover the unit's 4 KiB, every fetched byte used); avail =
-// bytes before n.
-__device__ __forceinline__ void hmap_load(const uint8_t *in, uint64_t n, uint64_t u, uint32_t lane, uint4 *v,
-                                          uint32_t *avail) {
-  const uint64_t s0 = u * 4096 + 64 * (uint64_t)lane;
-  const uint64_t a = s0 < n ? n - s0 : 0;
-  *avail = a > 64 ? 64u : (uint32_t)a;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) v[j] = 16u * j < *avail ? *(const uint4 *)(in + s0 + 16 * j) : make_uint4(0, 0, 0, 0);
-}
-
-__device__ __forceinline__ uint32_t byte_at(const uint4 *v, uint32_t i) {
-  const uint4 q = v[i >> 4];
-  const uint32_t k = (i >> 2) & 3, w = k == 0 ? q.x : k == 1 ? q.y : k == 2 ? q.z : q.w;
-  return (w >> (8 * (i & 3))) & 0xFF;
-}
-
-// Per unit: the output bytes it adds (sum of |F(x)| - 1); per block, the
-// histogram of the changed bytes, added to hist once at the end.
+// Per unit: the output bytes it adds (sum of |F(x)| - 1); the histogram of
+// the changed bytes.  Coalesced loads (lane l: the unit's 16-byte pieces l,
+// l + 64, l + 128, l + 192); one LDS read per byte (info: |F(x)| - 1 and the
+// changed-byte index); a changed byte (rare) bumps one of kHMapReg 16-bit
+// lane counters (packed two per register, the index selecting the register
+// by compares: no register array indexed at run time), summed over the wave
+// and added to hist at the end — atomics per byte serialised on the few
+// counters (0.94 ms per 2 GiB).  Past kHMapReg changed bytes: LDS atomics.
 __global__ __launch_bounds__(256) void hmap_count_kernel(const uint8_t *in, uint64_t n, uint64_t nunits, HMapDev h,
                                                          uint64_t *ucount, unsigned long long *hist) {
-  __shared__ uint8_t fl[256], act[256];
+  __shared__ uint32_t info[256];
+  __shared__ uint8_t alist[256];
   __shared__ uint32_t lh[256];
-  fl[threadIdx.x] = h.flen[threadIdx.x];
-  act[threadIdx.x] = h.active[threadIdx.x];
-  lh[threadIdx.x] = 0;
+  __shared__ __attribute__((aligned(16))) uint8_t txt[4][4096];
+  {
+    const uint32_t x = threadIdx.x, a = h.aidx[x];
+    info[x] = (uint32_t)(h.flen[x] - 1) | a << 16;
+    if (a != 0xFF) alist[a] = (uint8_t)x;
+    lh[x] = 0;
+  }
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63;
-  const uint64_t nw = (uint64_t)gridDim.x * 4;
-  for (uint64_t u = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); u < nunits; u += nw) {
-    uint4 v[4];
-    uint32_t avail;
-    hmap_load(in, n, u, lane, v, &avail);
-    uint32_t extra = 0;
+  uint8_t *T = txt[threadIdx.x >> 6];
+  const bool reg = h.nact <= kHMapReg;
+  uint32_t c[kHMapReg / 2];
 #pragma unroll
-    for (uint32_t i = 0; i < 64; ++i) {
-      const uint32_t x = byte_at(v, i);
-      const bool in_ = i < avail;
-      extra += in_ ? fl[x] - 1u : 0u;
-      if (in_ && act[x]) atomicAdd(&lh[x], 1u);
+  for (uint32_t k = 0; k < kHMapReg / 2; ++k) c[k] = 0;
+  const uint64_t nw = (uint64_t)gridDim.x * 4;
+  uint32_t rounds = 0;
+  for (uint64_t u = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); u < nunits; u += nw) {
+    const uint64_t s0 = u * 4096;
+    const uint64_t av = s0 < n ? n - s0 : 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // coalesced: lane l the pieces l, l + 64, ...
+      const uint64_t o = 16 * (uint64_t)lane + 1024 * j;
+      *(uint4 *)(T + o) = o < av ? *(const uint4 *)(in + s0 + o) : make_uint4(0, 0, 0, 0);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // lane l counts dwords l, l + 64, ... (conflict-free reads); the changed
+    // bytes (rare, but in nearly every step of some lane) are marked and
+    // counted after the loop, so the loop has no branch
+    uint32_t extra = 0;
+    uint64_t chg = 0;
+#pragma unroll 4
+    for (uint32_t i = 0; i < 16; ++i) {
+      const uint32_t d = lane + 64 * i, w = ((const uint32_t *)T)[d];
+#pragma unroll
+      for (uint32_t b = 0; b < 4; ++b) {
+        const uint32_t inf = 4 * d + b < av ? info[(w >> (8 * b)) & 0xFF] : 0xFF0000u;
+        extra += inf & 0xFFFF;
+        chg |= (uint64_t)((inf >> 16) != 0xFF) << (4 * i + b);
+      }
+    }
+    while (chg) {
+      const uint32_t t = (uint32_t)__builtin_ctzll(chg);
+      chg &= chg - 1;
+      const uint32_t a = info[T[4 * (lane + 64 * (t >> 2)) + (t & 3)]] >> 16;
+      if (reg) {
+#pragma unroll
+        for (uint32_t k = 0; k < kHMapReg / 2; ++k) c[k] += (a >> 1) == k ? 1u << (16 * (a & 1)) : 0u;
+      } else {
+        atomicAdd(&lh[alist[a]], 1u);
+      }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) extra += __shfl_xor(extra, o);
     if (lane == 0) ucount[u] = extra;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // (16-bit lane counters: at most 64 per unit; emptied every 512 units)
+    if (reg && ++rounds == 512) {
+      rounds = 0;
+#pragma unroll
+      for (uint32_t a = 0; a < kHMapReg; ++a) {
+        uint32_t t = (c[a >> 1] >> (16 * (a & 1))) & 0xFFFF;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+        if (lane == 0 && t && a < h.nact) atomicAdd(&lh[alist[a]], t);
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < kHMapReg / 2; ++k) c[k] = 0;
+    }
+  }
+  if (reg) {
+#pragma unroll
+    for (uint32_t a = 0; a < kHMapReg; ++a) {
+      uint32_t t = (c[a >> 1] >> (16 * (a & 1))) & 0xFFFF;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+      if (lane == 0 && t && a < h.nact) atomicAdd(&lh[alist[a]], t);
+    }
   }
   __syncthreads();
   if (lh[threadIdx.x]) atomicAdd(&hist[threadIdx.x], (unsigned long long)lh[threadIdx.x]);
 }
 
-// Per unit: the lane's output (its bytes' images) staged in LDS at the
-// unit's output alignment, then whole aligned 16-byte blocks stored by
-// consecutive lanes, the two edge blocks byte by byte (they share an aligned
-// block with the neighbouring units: byte stores do not race).  uoff =
-// exclusive sums of the units' added bytes.
+// Per unit: each lane holds its 64 bytes in registers (the next unit's
+// already in flight: the kernel waits on memory otherwise, 3-4 waves per SIMD
+// with one HBM round trip per unit) and writes their images into the wave's
+// output stage at the unit's output alignment — every byte's first image
+// byte in one branch-free pass, the longer images' other bytes from a wave
+// list (ballot slots) by one lane each — then whole aligned 16-byte blocks
+// are stored by consecutive lanes and the two edge blocks byte by byte (they
+// share an aligned block with the neighbouring units: byte stores do not
+// race).  uoff = exclusive sums of the units' added bytes.
+struct HMapWave {
+  uint8_t out[kHMapOut + 32];
+  uint32_t rest[128];  // images longer than one byte: output offset << 8 | byte
+};
+
+__device__ __forceinline__ void hmap_lane_load(const uint8_t *in, uint64_t n, uint64_t u, uint32_t lane, uint4 *g) {
+  const uint64_t s0 = u * 4096 + 64 * (uint64_t)lane;
+  const uint64_t av = s0 < n ? n - s0 : 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) g[j] = 16u * j < av ? *(const uint4 *)(in + s0 + 16 * j) : make_uint4(0, 0, 0, 0);
+}
+
 __global__ __launch_bounds__(256) void hmap_write_kernel(const uint8_t *in, uint64_t n, uint64_t nunits, HMapDev h,
                                                          const uint64_t *uoff, uint8_t *out, uint64_t cap) {
-  __shared__ uint8_t fl[256];
-  __shared__ uint16_t so[256];
-  __shared__ __attribute__((aligned(16))) uint8_t pool[kHMapPool];
-  __shared__ __attribute__((aligned(16))) uint8_t obuf[4][kHMapOut + 32];
-  fl[threadIdx.x] = h.flen[threadIdx.x];
-  so[threadIdx.x] = h.soff[threadIdx.x];
+  __shared__ uint32_t info[256];  // |F(x)| | (F(x) = x) << 7 | offset << 8
+  __shared__ __attribute__((aligned(16))) HMapWave sw[4];
+  extern __shared__ __attribute__((aligned(16))) uint8_t pool[];  // (dynamic: pool_len)
+  {
+    const uint32_t x = threadIdx.x;
+    info[x] = (uint32_t)h.flen[x] | (h.aidx[x] == 0xFF ? 0x80u : 0u) | (uint32_t)h.soff[x] << 8;
+  }
   for (uint32_t i = threadIdx.x; i < h.pool_len; i += blockDim.x) pool[i] = h.pool[i];
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63;
-  uint8_t *ob_ = obuf[threadIdx.x >> 6];
+  HMapWave &W = sw[threadIdx.x >> 6];
   const uint64_t nw = (uint64_t)gridDim.x * 4;
-  for (uint64_t u = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); u < nunits; u += nw) {
-    uint4 v[4];
-    uint32_t avail;
-    hmap_load(in, n, u, lane, v, &avail);
+  uint64_t u = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  uint4 gn[4];
+  hmap_lane_load(in, n, u, lane, gn);
+  for (; u < nunits; u += nw) {
+    uint4 g[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) g[j] = gn[j];
+    hmap_lane_load(in, n, u + nw < nunits ? u + nw : u, lane, gn);  // the next unit, in flight
+    const uint64_t s0 = u * 4096;
+    const uint64_t lb = s0 + 64 * (uint64_t)lane;
+    const uint32_t avail = n > lb ? (uint32_t)min<uint64_t>(n - lb, 64) : 0u;
     uint32_t len = 0;
 #pragma unroll
-    for (uint32_t i = 0; i < 64; ++i) len += i < avail ? fl[byte_at(v, i)] : 0u;
+    for (uint32_t k = 0; k < 16; ++k) {
+      const uint4 q = g[k >> 2];
+      const uint32_t w = (k & 3) == 0 ? q.x : (k & 3) == 1 ? q.y : (k & 3) == 2 ? q.z : q.w;
+#pragma unroll 1
+      for (uint32_t b = 0; b < 4; ++b) len += 4 * k + b < avail ? info[(w >> (8 * b)) & 0xFF] & 0x7F : 0u;
+    }
     uint32_t incl = len;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -1294,45 +1374,71 @@ __global__ __launch_bounds__(256) void hmap_write_kernel(const uint8_t *in, uint
       if (lane >= (uint32_t)o) incl += x;
     }
     const uint32_t T = __shfl(incl, 63), r0 = incl - len;
-    const uint64_t ob = u * 4096 + uoff[u];  // the unit's output start
+    const uint64_t ob = s0 + uoff[u];  // the unit's output start
     const uint32_t o15 = (uint32_t)(ob & 15);
-    if (o15 + T + 16 > kHMapOut) {  // a unit that grows past the stage: byte stores
+    if (o15 + T + 16 > kHMapOut) {  // a unit that grows past the stage: byte stores, in order
       uint64_t p = ob + r0;
-      for (uint32_t i = 0; i < avail; ++i) {
-        const uint32_t x = byte_at(v, i), l = fl[x], o = so[x];
-        for (uint32_t t = 0; t < l; ++t, ++p)
-          if (p < cap) out[p] = pool[o + t];
+#pragma unroll
+      for (uint32_t k = 0; k < 16; ++k) {
+        const uint4 q = g[k >> 2];
+        const uint32_t w = (k & 3) == 0 ? q.x : (k & 3) == 1 ? q.y : (k & 3) == 2 ? q.z : q.w;
+#pragma unroll 1
+        for (uint32_t b = 0; b < 4 && 4 * k + b < avail; ++b) {
+          const uint32_t inf = info[(w >> (8 * b)) & 0xFF], l = inf & 0x7F, off = inf >> 8;
+          for (uint32_t t = 0; t < l; ++t, ++p)
+            if (p < cap) out[p] = pool[off + t];
+        }
       }
       continue;
     }
-    {  // stage: the lane's images at o15 + r0 ..
-      uint32_t p = o15 + r0;
-#pragma unroll 4
-      for (uint32_t i = 0; i < avail; ++i) {
-        const uint32_t x = byte_at(v, i), l = fl[x];
-        if (l == 1) {
-          ob_[p++] = pool[so[x]];
-        } else {
-          const uint32_t o = so[x];
-          for (uint32_t t = 0; t < l; ++t) ob_[p++] = pool[o + t];
+    {
+      uint32_t pos = o15 + r0, nrest = 0;
+      auto flush = [&]() {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t e = lane; e < nrest; e += 64) {
+          const uint32_t r = W.rest[e], inf = info[r & 0xFF], l = inf & 0x7F, off = inf >> 8;
+          uint8_t *d = W.out + (r >> 8);
+          for (uint32_t j = 1; j < l; ++j) d[j] = pool[off + j];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        nrest = 0;
+      };
+#pragma unroll
+      for (uint32_t k = 0; k < 16; ++k) {
+        const uint4 q = g[k >> 2];
+        const uint32_t w = (k & 3) == 0 ? q.x : (k & 3) == 1 ? q.y : (k & 3) == 2 ? q.z : q.w;
+#pragma unroll 1
+        for (uint32_t b = 0; b < 4; ++b) {
+          const bool in_ = 4 * k + b < avail;
+          const uint32_t x = (w >> (8 * b)) & 0xFF, inf = info[x];
+          const uint32_t l = in_ ? inf & 0x7F : 0u;
+          if (in_) W.out[pos] = (inf & 0x80) ? (uint8_t)x : pool[inf >> 8];
+          const bool lg = l > 1;
+          const uint64_t m = __ballot(lg);
+          if (lg) W.rest[nrest + __popcll(m & ((1ull << lane) - 1ull))] = pos << 8 | x;
+          nrest += (uint32_t)__popcll(m);
+          pos += l;
+          if (nrest > 64) flush();  // (at most 64 join per byte step: the list holds 128)
         }
       }
+      if (nrest) flush();
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const uint64_t base = ob - o15, E = ob + T;
     const uint64_t A = (ob + 15) & ~(uint64_t)15, B = E & ~(uint64_t)15;
     for (uint64_t q = A + 16 * (uint64_t)lane; q < B; q += 1024) {
-      const uint4 x = *(const uint4 *)(ob_ + (q - base));
+      const uint4 x = *(const uint4 *)(W.out + (q - base));
       if (q + 16 <= cap) *(uint4 *)(out + q) = x;
-      else for (uint32_t j = 0; q + j < cap; ++j) out[q + j] = ob_[q - base + j];
+      else for (uint32_t j = 0; q + j < cap; ++j) out[q + j] = W.out[q - base + j];
     }
     // the edges: [ob, min(A, E)) and [max(B, A), E)
     const uint64_t h1 = min(A, E), t0 = max(B, A);
     const uint64_t pos = lane < 16 ? ob + lane : t0 + (lane - 16);
     const bool mine = lane < 16 ? pos < h1 : (lane < 32 && pos < E);
-    if (mine && pos < cap) out[pos] = ob_[pos - base];
+    if (mine && pos < cap) out[pos] = W.out[pos - base];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1547,17 +1653,20 @@ hipError_t launch_replace_class(const uint8_t *hay, uint64_t n, const uint8_t *c
   return e != hipSuccess ? e : e2;
 }
 
-// The chain as one byte -> string map (see HMapDev): tab = per byte |F(x)|
-// (256 u8), soff (256 u16), active (256 u8), the pool, then per step i
-// |F_i(x)| - 1 as 256 u32 (device, one blob); the final text goes to out.
+// The chain as one byte -> string map (see HMapDev): per byte |F(x)| (256
+// u8), offsets (256 u16), changed-byte indices (256 u8, 0xFF: unchanged;
+// nact of them), the pool, then per step i |F_i(x)| - 1 as 256 u32 (device,
+// one blob); the final text goes to out.
 hipError_t launch_replace_hmap(const uint8_t *in, uint64_t n, int steps, const uint8_t *blob, uint32_t pool_len,
-                               uint8_t *out, uint64_t cap, uint64_t *lengths, hipStream_t st, int cus) {
+                               uint32_t nact, uint8_t *out, uint64_t cap, uint64_t *lengths, hipStream_t st,
+                               int cus) {
   HMapDev h;
   h.flen = blob;
   h.soff = (const uint16_t *)(blob + 256);
-  h.active = blob + 768;
+  h.aidx = blob + 768;
   h.pool = blob + 1024;
   h.pool_len = pool_len;
+  h.nact = nact;
   const uint32_t *dlen = (const uint32_t *)(blob + 1024 + kHMapPool);
   if (pool_len > kHMapPool) return hipErrorNotSupported;
   const uint64_t nunits = std::max<uint64_t>(1, (n + 4095) / 4096);
@@ -1570,11 +1679,12 @@ hipError_t launch_replace_hmap(const uint8_t *in, uint64_t n, int steps, const u
     if ((e = hipMemsetAsync(ucount + nunits, 0, 8, st)) != hipSuccess) break;
     if ((e = hipMemsetAsync(hist, 0, 256 * 8, st)) != hipSuccess) break;
     const int g = grid_for_items((nunits + 3) / 4 * 256, 256, cus);
-    const int gw = std::min(g, cus * 4);  // (the write kernel's LDS stage: 4 blocks per CU)
+    const int gw = std::min(g, cus * 4);  // (the write kernel's LDS stages: 4 blocks per CU)
     hipLaunchKernelGGL(hmap_count_kernel, dim3(g), dim3(256), 0, st, in, n, nunits, h, ucount, hist);
     if ((e = hipGetLastError()) != hipSuccess) break;
     if ((e = exclusive_scan_u64(ucount, uoff, nunits + 1, st)) != hipSuccess) break;
-    hipLaunchKernelGGL(hmap_write_kernel, dim3(gw), dim3(256), 0, st, in, n, nunits, h, uoff, out, cap);
+    hipLaunchKernelGGL(hmap_write_kernel, dim3(gw), dim3(256), (pool_len + 15) & ~15u, st, in, n, nunits, h, uoff,
+                       out, cap);
     if ((e = hipGetLastError()) != hipSuccess) break;
     hipLaunchKernelGGL(hmap_lengths_kernel, dim3(1), dim3(std::max(64, (steps + 63) / 64 * 64)), 0, st, n, steps,
                        (const unsigned long long *)hist, dlen, lengths);
