@@ -77,8 +77,10 @@ class RegexDna(object):
                                    stream=stream)
         counts = [int(c.item()) for c, _, _ in res]
         # the 11 substitutions in one enqueue; the final length is the one
-        # read-back (a cut output, lengths[-1] > capacity, reruns sized exactly)
-        cap = clen + clen // 4 + 4096
+        # read-back (a cut output, lengths[-1] > capacity, reruns sized
+        # exactly; the IUB codes grow the stream by a third, so twice its
+        # length is never cut)
+        cap = 2 * clen + 4096
         while True:
             _, lengths = replace_all_chain([r for r, _ in self.substs], [t for _, t in self.substs], stripped,
                                            length=clen, capacity=cap, stream=stream)
