@@ -1342,6 +1342,8 @@ const FwdDfaDev *iter_ascii_device(rure *re, const DevTables &t, std::string *er
   f.nonempty = can_match_empty(re->nfa) ? 0 : 1;
   f.looks = re->nt.looks_used ? 1 : 0;
   f.can_quit = 1;
+  // (no set_prefix_skip: the skip is read by the long find / is_match scan
+  // only, and the shadow serves find_iter, whose burst kernel has none)
   re->iter_dev_a[d] = {tmp.blob, f};
   return &re->iter_dev_a[d].second;
 }

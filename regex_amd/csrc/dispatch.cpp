@@ -585,6 +585,30 @@ hipError_t run_find_iter(rure *re, DevTables *t, const BatchDev &b, const IterOu
             return e;
           }
         }
+        // The full automaton cannot quit: both passes are enqueued, the
+        // shadow's quit staying a device word -- its passes after the quit
+        // check run while the word is 0, the full automaton's while it is set
+        // (-25; nothing read back, the call only enqueues).  Knob
+        // shadow_sync=1 reads the quit back (-14 / -15).
+        if (!fi->can_quit && knob(Knob::ShadowSync) != 1) {
+          uint32_t *qf = nullptr;
+          hipError_t e = scratch_malloc((void **)&qf, 8, st);
+          if (e == hipSuccess) e = hipMemsetAsync(qf, 0, 4, st);
+          if (e == hipSuccess)
+            e = launch_find_iter(b, fa, t->r, &t->n, true, chunk, o, st, t->cus, nullptr, nullptr, nullptr, qf);
+          if (e == hipSuccess) {
+            BatchDev bf = b;
+            bf.gate = qf;
+            bf.gate_set = 1;
+            e = launch_find_iter(bf, fi, t->r, &t->n, true, chunk, o, st, t->cus, nullptr);
+          }
+          if (qf) {
+            const hipError_t e2 = scratch_free(qf, st);
+            if (e == hipSuccess) e = e2;
+          }
+          if (e == hipSuccess) note_fwd_path(-25);
+          return e;
+        }
         bool q = false;
         const hipError_t e = launch_find_iter(b, fa, t->r, &t->n, true, chunk, o, st, t->cus, sp, nullptr, &q);
         if (e != hipSuccess || !q) {

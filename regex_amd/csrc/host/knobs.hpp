@@ -39,6 +39,7 @@ enum class Knob : int {
   Timing,          // 1: DFA construction times on stderr
   ReplaceGeneric,  // 1: replace's generic per-block copy, not the grouped copy
   ChainSeq,        // 1: a replace_all chain step by step, not as one composed byte map
+  ShadowSync,      // 1: the ASCII shadow's find_iter quit read back, not gated on the device
   kCount
 };
 

@@ -26,6 +26,12 @@ struct BatchDev {
   // set (atomic OR) by the DFA kernels when a haystack's DFA quit; the Pike VM
   // fallback pass then runs, else it returns at once (nullptr: always runs)
   uint32_t *quit_flag = nullptr;
+  // a deferred fallback's gate (nullptr: always runs): the find_iter kernels
+  // return at once unless (*gate != 0) == gate_set, so the ASCII shadow's
+  // passes after its quit check and the full automaton's re-run are both
+  // enqueued and one of them works (dispatch.cpp run_find_iter)
+  const uint32_t *gate = nullptr;
+  uint32_t gate_set = 0;
   // set masks (the Pike VM's MODE_SET): words between consecutive haystacks'
   // masks (a set of more than 64 patterns: group g writes word g)
   uint32_t out_stride = 1;
@@ -324,10 +330,14 @@ hipError_t launch_find_iter_runs(const BatchDev &b, const uint8_t *cls, const ui
                                  hipStream_t st, int cus, bool can_quit, bool *quit);
 hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaDev &r, const NfaDev *nf,
                             bool chunked, uint64_t chunk, const IterOut &o, hipStream_t st, int cus,
-                            const IterSpan *span = nullptr, const MatchDev *mt = nullptr, bool *quit = nullptr);
+                            const IterSpan *span = nullptr, const MatchDev *mt = nullptr, bool *quit = nullptr,
+                            uint32_t *quit_dev = nullptr);
 // (quit: chunked with a DFA that can quit, f->can_quit; set when a search
 // quit, the outputs then being void: the caller runs the wave path.  Reads
-// the flag back, so the call synchronises the stream.)
+// the flag back, so the call synchronises the stream.  quit_dev instead (a
+// zeroed device word, chunked, no span): a quit ORs 1 into it and the passes
+// after the speculative one run gated on it staying 0 -- nothing is read
+// back, and the caller enqueues its fallback gated on the word being set.)
 // The k-mer probe engine of launch_find_iter_multi: the regexes' strings all
 // have one length len <= 8 over an alphabet of at most 4 bytes whose codes
 // (b >> shift) & 3 are distinct.  bitmap: 2048 u32, bit c set iff the L-mer

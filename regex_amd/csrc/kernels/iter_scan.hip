@@ -36,6 +36,12 @@ namespace rure_amd {
 
 namespace {
 
+// A launch gated on a device word (BatchDev::gate): it returns at once
+// unless (*gate != 0) == gate_set (every block alike).
+__device__ __forceinline__ bool gated_off(const BatchDev &b) {
+  return b.gate && ((__atomic_load_n(b.gate, __ATOMIC_RELAXED) != 0) != (b.gate_set != 0));
+}
+
 // Speculative matches kept per unit: enough for one match per 32 bytes of
 // the unit (the emit pass copies them instead of re-running the unit).
 __host__ __device__ inline uint32_t unit_slots(uint64_t chunk) {
@@ -350,6 +356,7 @@ __device__ __forceinline__ uint64_t rev_scan_all(const RevDfaDev &r, const uint8
 __global__ __launch_bounds__(1024) void iter_spec_burst_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f,
                                                               RevDfaDev r, Unit *units, uint64_t *slots,
                                                               uint32_t *counts, uint32_t *dirty, uint32_t *abortf) {
+  if (gated_off(b)) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const uint8_t *rlds = stage_tables(f, r, lds);
   for (uint64_t u0 = (uint64_t)blockIdx.x * blockDim.x; u0 < nunits; u0 += (uint64_t)gridDim.x * blockDim.x) {
@@ -488,6 +495,7 @@ __global__ __launch_bounds__(1024) void iter_spec_burst_kernel(BatchDev b, Geo g
 template <bool K4, bool K8>
 __global__ __launch_bounds__(1024) void iter_spec_lit_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f,
                                                             Unit *units, uint64_t *slots, uint32_t *counts, uint32_t *dirty) {
+  if (gated_off(b)) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   for (uint32_t i = threadIdx.x * 16; i < f.lit_bytes; i += blockDim.x * 16)
     *(uint4 *)(lds + i) = *(const uint4 *)(f.lit_image + i);
@@ -555,6 +563,7 @@ template <typename W>
 __global__ __launch_bounds__(256) void iter_spec_sa_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f,
                                                            Unit *units, uint64_t *slots, uint32_t *counts,
                                                            uint32_t *dirty) {
+  if (gated_off(b)) return;
   __shared__ W B[256];
   for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) B[i] = (W)f.sa_image[i];
   __syncthreads();
@@ -711,6 +720,7 @@ template <typename W>
 __global__ __launch_bounds__(256) void iter_spec_sa_tile_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f,
                                                                 Unit *units, uint64_t *slots, uint32_t *counts,
                                                                 uint32_t *dirty) {
+  if (gated_off(b)) return;
   __shared__ W B[256];
   __shared__ __attribute__((aligned(16))) uint4 stage[4][64 * 8];
   for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) B[i] = (W)f.sa_image[i];
@@ -1469,6 +1479,7 @@ __device__ __forceinline__ void lex_events(uint32_t m0, uint32_t m1, uint32_t bp
 template <bool X4, bool SINGLE>
 __global__ __launch_bounds__(256, 4) void iter_spec_lex_tile_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f,
                                                                  Unit *units, uint64_t *slots, uint32_t *counts) {
+  if (gated_off(b)) return;
   // the byte chain's address is one 24-bit multiply-add; 24 rows + the tile
   // stage = 39.5 KB (X4: 5 KB + the stage), 4 blocks (16 waves) per CU
   __shared__ __attribute__((aligned(16))) uint8_t tab[X4 ? kLex4Bytes : kLexBytes];
@@ -1630,6 +1641,7 @@ __global__ __launch_bounds__(256, 4) void iter_spec_lex_tile_kernel(BatchDev b, 
 __global__ __launch_bounds__(256) void iter_lex_tail_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f,
                                                             RevDfaDev r, Unit *units, uint64_t *slots,
                                                             uint32_t *counts, uint32_t *dirty) {
+  if (gated_off(b)) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const uint8_t *rlds = stage_tables(f, r, lds);
   for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < nunits; u += (uint64_t)gridDim.x * blockDim.x) {
@@ -1820,6 +1832,7 @@ __global__ __launch_bounds__(1024) void iter_fix_kernel(BatchDev b, Geo g, uint6
                                                        Unit *units, uint32_t *counts, const uint64_t *slots,
                                                        uint64_t *queue, unsigned long long *qlen,
                                                        const uint32_t *dirty) {
+  if (gated_off(b)) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   fix_body(b, g, nunits, f, r, units, counts, slots, queue, qlen, dirty, lds);
 }
@@ -1879,6 +1892,7 @@ __global__ void iter_quit_kernel(const Unit *units, uint64_t nunits, uint32_t *q
 
 __global__ void iter_walk_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r, Unit *units,
                                  uint32_t *counts, const uint64_t *slots, uint64_t *queue, unsigned long long *qlen) {
+  if (gated_off(b)) return;
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   walk_body(b, g, nunits, f, r, units, counts, slots, queue, qlen);
 }
@@ -1890,6 +1904,7 @@ __global__ void iter_walk_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f
 __global__ void iter_entry_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r, Unit *units,
                                   uint32_t *counts, const uint64_t *slots, const uint64_t *entry, uint64_t *queue,
                                   unsigned long long *qlen) {
+  if (gated_off(b)) return;
   if (threadIdx.x != 0 || blockIdx.x != 0 || entry[2]) return;
   if (repair_unit(b, g, f, r, f.lds_image /* unused: hot = 0 */, nullptr, 0, IterSt{entry[0], entry[1]}, units,
                   counts, slots) &&
@@ -2075,6 +2090,7 @@ __device__ __forceinline__ void emit_body(const BatchDev &b, const Geo &g, uint6
 __global__ __launch_bounds__(1024) void iter_emit_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
                                                         const Unit *units, const uint64_t *slots, const uint64_t *off,
                                                         uint64_t *out, uint64_t cap, int copies) {
+  if (gated_off(b)) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   emit_body<true>(b, g, nunits, f, r, units, slots, off, out, cap, lds, copies != 0);
 }
@@ -2095,6 +2111,7 @@ constexpr uint32_t kGrpWin = 4096;
 __global__ __launch_bounds__(256) void iter_copy_group_kernel(BatchDev b, Geo g, uint64_t nunits, const Unit *units,
                                                               const uint64_t *slots, const uint64_t *off,
                                                               uint64_t *out, uint64_t cap) {
+  if (gated_off(b)) return;
   __shared__ uint32_t wrec[kGrpWin];
   __shared__ uint8_t wtag[kGrpWin];  // unit in the group, 0xFF: nothing to write here
   __shared__ uint64_t sbase[64];
@@ -2189,6 +2206,7 @@ __global__ __launch_bounds__(64) void iter_wave_kernel(BatchDev b, FwdDfaDev f, 
                                                        uint32_t *counts, const uint64_t *off, uint64_t *out,
                                                        uint64_t cap, uint8_t *scratch, const uint64_t *entry,
                                                        uint64_t hi, uint64_t *exit, MatchDev m) {
+  if (gated_off(b)) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_mem[];
   uint8_t *mem = scratch ? scratch + (size_t)blockIdx.x * nfa_wave_bytes(nf.nleaves) : lds_mem;
   pike::Lists W;
@@ -2278,7 +2296,8 @@ __device__ __forceinline__ void counts_body(uint64_t nh, uint64_t nk, const uint
   if (blockIdx.x == 0 && threadIdx.x == 0) *total = off[nh * nk] - off[0];
 }
 __global__ void iter_counts_kernel(uint64_t nh, uint64_t nk, const uint64_t *off, uint64_t *hcounts,
-                                   uint64_t *total) {
+                                   uint64_t *total, BatchDev b) {
+  if (gated_off(b)) return;
   counts_body(nh, nk, off, hcounts, total);
 }
 
@@ -2557,7 +2576,7 @@ static hipError_t iter_post(const BatchDev &b, const Geo &g, uint64_t nunits, co
                      o.matches, o.cap, dense ? 0 : 1);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(iter_counts_kernel, dim3(grid_cap(b.count, 256, cus, 4)), dim3(256), 0, st, b.count, g.nk,
-                     sc.off, o.counts, o.total);
+                     sc.off, o.counts, o.total, b);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if (spn && spn->exit) {
     hipLaunchKernelGGL(iter_exit_kernel, dim3(1), dim3(64), 0, st, (const Unit *)sc.units, nunits, spn->exit,
@@ -2792,8 +2811,9 @@ hipError_t launch_find_iter_multi(const BatchDev &b, int nre, const FwdDfaDev *c
 
 hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaDev &r, const NfaDev *nf,
                             bool chunked, uint64_t chunk, const IterOut &o, hipStream_t st, int cus,
-                            const IterSpan *spn, const MatchDev *mtd, bool *quit) {
+                            const IterSpan *spn, const MatchDev *mtd, bool *quit, uint32_t *quit_dev) {
   const uint64_t hi = spn ? spn->hi : ~0ull;
+  if (quit_dev && (!chunked || spn || b.gate || !f || !f->can_quit)) return hipErrorInvalidValue;
   hipError_t e = hipSuccess;
   if (b.count == 0) {
     return hipMemsetAsync(o.total, 0, 8, st);
@@ -2839,8 +2859,8 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
       const bool use_lex = lex_usable(*f, b, g);
       // the quit flag (a caller that re-runs on a quit): zeroed here, set by
       // the burst kernel's first quit (the others stop) and by iter_quit_kernel
-      uint32_t *qd = nullptr;
-      if (f->can_quit && quit) {
+      uint32_t *qd = quit_dev;
+      if (!qd && f->can_quit && quit) {
         if ((e = scratch_malloc((void **)&qd, 8, st)) != hipSuccess) break;
         if ((e = hipMemsetAsync(qd, 0, 4, st)) != hipSuccess) { (void)scratch_free(qd, st); break; }
       }
@@ -2899,7 +2919,18 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
       }
       if (!use_lex) ktimer_end(st);
       if ((e = hipGetLastError()) != hipSuccess) {
-        if (qd) (void)scratch_free(qd, st);
+        if (qd && !quit_dev) (void)scratch_free(qd, st);
+        break;
+      }
+      // deferred: the quit check stays on the device and gates the rest
+      if (quit_dev) {
+        hipLaunchKernelGGL(iter_quit_kernel, dim3(grid_cap(nunits, 256, cus, 4)), dim3(256), 0, st, units, nunits,
+                           quit_dev);
+        if ((e = hipGetLastError()) != hipSuccess) break;
+        BatchDev bg = b;
+        bg.gate = quit_dev;
+        bg.gate_set = 0;
+        e = iter_post(bg, g, nunits, *f, r, sc, o, spn, st, cus, use_lex);
         break;
       }
       // a quit in the speculative pass ends the call here: the caller re-runs
@@ -2975,7 +3006,7 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
                        spn ? spn->entry : (const uint64_t *)nullptr, hi, (uint64_t *)nullptr, md);
     if ((e = hipGetLastError()) != hipSuccess) break;
     hipLaunchKernelGGL(iter_counts_kernel, dim3(grid_cap(b.count, 256, cus, 4)), dim3(256), 0, st, b.count,
-                       (uint64_t)1, off, o.counts, o.total);
+                       (uint64_t)1, off, o.counts, o.total, b);
     e = hipGetLastError();
   } while (false);
   hipError_t e2 = scratch_free(buf, st);

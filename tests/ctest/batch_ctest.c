@@ -97,11 +97,10 @@ int main(void) {
   CHECK(got == total, "spans %zu vs %llu", got, (unsigned long long)total);
 
   /* Stream order: with ~10 ms of finds queued ahead on a
-   * stream, find_iter of a regex that cannot quit returns while that work is
-   * still running (it only enqueues): [a-z]+, and \w+ (the run engine reads
-   * UTF-8 itself); find_iter of \w+@\w+\.\w+ (Unicode classes: the ASCII
-   * shadow's quit flag is read back) is on the synchronising list and
-   * returns with the stream drained. */
+   * stream, find_iter returns while that work is still running (it only
+   * enqueues): [a-z]+, \w+ (the run engine reads UTF-8 itself) and
+   * \w+@\w+\.\w+ (Unicode classes: the ASCII shadow's quit stays a device
+   * flag that gates the full automaton's pass, enqueued behind it). */
   {
     const size_t BIGL = 4096, BIGN = 65536;
     uint8_t *big = NULL;
@@ -127,10 +126,7 @@ int main(void) {
       clock_gettime(CLOCK_MONOTONIC, &t1);
       const hipError_t q = hipStreamQuery(st);
       const double ms = (t1.tv_sec - t0.tv_sec) * 1e3 + (t1.tv_nsec - t0.tv_nsec) * 1e-6;
-      if (pass < 2)
-        CHECK(q == hipErrorNotReady, "find_iter (pass %d) waited for the stream (query %d, %.2f ms)", pass, (int)q, ms);
-      else  /* it waited for the ~10 ms of finds queued ahead of it */
-        CHECK(ms > 3.0, "find_iter of \\w+@\\w+\\.\\w+ returned after %.2f ms, before the queued work", ms);
+      CHECK(q == hipErrorNotReady, "find_iter (pass %d) waited for the stream (query %d, %.2f ms)", pass, (int)q, ms);
       HIP(hipStreamSynchronize(st));
     }
     rure_free(lower);

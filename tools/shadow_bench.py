@@ -1,7 +1,8 @@
 """find_iter of regexes that take the ASCII shadow automaton (DESIGN §4.3:
-last_fwd_path -14 = the shadow answered, -15 = a unit quit on a non-ASCII
-byte and the batch re-ran on the full automaton) against the full automaton
-alone (knob ascii_shadow=0), over 1 GiB of sherlock text three ways: made
+by default the shadow's quit is a device flag gating both passes, path -25;
+with knob shadow_sync=1 it is read back, -14 = the shadow answered, -15 = a
+unit quit on a non-ASCII byte and the batch re-ran on the full automaton)
+against the full automaton alone (knob ascii_shadow=0), over 1 GiB of sherlock text three ways: made
 ASCII, as it is (sparse non-ASCII bytes), and dense (every 64th byte's word
 turned into a two-byte UTF-8 letter).  Outputs of the two compared in full.
 One JSON line per pattern and text.  (Not a Unicode-\b regex by default: on
@@ -66,11 +67,15 @@ for name, raw in texts():
     for pat in pats:
         R._debug_set(None)
         ms, n, m, path = run(R.Regex(pat), buf, L, 3)
+        R._debug_set("shadow_sync=1")
+        ms1, n1, m1, path1 = run(R.Regex(pat), buf, L, 3)
         R._debug_set("ascii_shadow=0")
         ms0, n0, m0, path0 = run(R.Regex(pat), buf, L, 3)
         R._debug_set(None)
         print(json.dumps({"pattern": pat, "text": name, "bytes": L, "matches": n, "shadow_ms": round(ms, 3),
-                          "shadow_path": path, "full_ms": round(ms0, 3), "full_path": path0,
+                          "shadow_path": path, "sync_ms": round(ms1, 3), "sync_path": path1,
+                          "sync_equal": n == n1 and bool(torch.equal(m, m1)),
+                          "full_ms": round(ms0, 3), "full_path": path0,
                           "shadow_speedup": round(ms0 / ms, 2), "outputs_equal": n == n0 and bool(torch.equal(m, m0))}),
               flush=True)
     del buf
