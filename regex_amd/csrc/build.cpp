@@ -1462,7 +1462,9 @@ const FwdDfaDev *iter_device(rure *re, const DevTables &t, std::string *err) {
     // literal / Shift-And / lexer engines and the first-byte start rule read
     // no assertions and skip the reverse scan, so they are off
     f.looks = re->nt.looks_used ? 1 : 0;
-    f.can_quit = t.quit_possible ? 1 : 0;
+    // (2: the quit is a Unicode word boundary's, dfa.rs:1487-1496 -- the
+    // chunked find_iter then also hands over starts after a byte >= 0x80)
+    f.can_quit = t.quit_possible ? (re->fwd.has_unicode_word_boundary ? 2 : 1) : 0;
     f.fb_n = 0;
     f.lit_image = nullptr;
     f.lit_n = 0;

@@ -618,6 +618,16 @@ hipError_t run_find_iter(rure *re, DevTables *t, const BatchDev &b, const IterOu
         shadow_quit = true;  // a quit: the full automaton below answers (-15)
       }
     }
+    // A DFA that can quit (Unicode \b over non-ASCII bytes): the units whose
+    // searches quit are served by the wave's Pike VM inside the chunked
+    // iteration (iter_scan.hip iter_wspec_kernel .. iter_wemit_kernel; -27,
+    // nothing read back).  Spans, and knob iter_wave=0, keep the read-back of
+    // the quit and the one-wave-per-haystack fallback (-13).
+    if (fi->can_quit && !sp && re->nfa_ok && knob(Knob::IterWave) != 0) {
+      const hipError_t e = launch_find_iter(b, fi, t->r, &t->n, true, chunk, o, st, t->cus, nullptr);
+      if (e == hipSuccess) note_fwd_path(-27);
+      return e;
+    }
     bool quit = false;
     const hipError_t e = launch_find_iter(b, fi, t->r, &t->n, true, chunk, o, st, t->cus, sp, nullptr, &quit);
     // last_fwd_path: -12 = the chunked iteration of a look-around regex

@@ -128,8 +128,9 @@ struct FwdDfaDev {
   // find_iter DFA only: the regex has look-around assertions (the chunked
   // iteration then repairs units whose first reverse scan reached their
   // start, and a reverse NoMatch ends the iteration; iter_scan.hip), and its
-  // DFA can quit (Unicode word boundary: a quit sends the batch to the wave
-  // path).  The literal, Shift-And, lexer and first-byte engines are off.
+  // DFA can quit (1; 2: a Unicode word boundary's quit, whose units the wave
+  // serves, iter_scan.hip).  The literal, Shift-And, lexer and first-byte
+  // engines are off.
   uint32_t looks, can_quit;
   // find_iter DFA only: the regex is one byte class repeated (C+, host
   // run_class): run_cls[b] bit 0 = b is in C, bit 1 = b quits (the ASCII

@@ -141,15 +141,49 @@ __device__ __forceinline__ void unit_bounds(const BatchDev &b, const Geo &g, uin
   *c1 = (k + 1 == g.nk) ? g.end : b.start + (k + 1) * g.chunk;
 }
 
+// The wave's Pike VM for searches whose DFA quits (the wave-served chunked
+// iteration: every lane of the wave runs the same search, wave-uniform).
+struct WaveCtx {
+  const NfaDev *nf;
+  pike::Lists *W;
+  pike::TagGen *tg;
+};
+
 // One step of re_trait.rs:197-221 (empty-match rule: next search at e + 1,
 // an empty match at the previous match end is skipped).
 // reached: the first search's dfa_find_cut reach flag (look-around).
+// wc: a search whose DFA quits runs on the Pike VM instead (exec.rs:485-487:
+// the reference's fallback for that one search), bounded by the cut the same
+// way (pike_one's cut); its answer does not depend on the search start.
 __device__ int iter_next(const FwdDfaDev &f, const RevDfaDev &r, const uint8_t *lds, const uint8_t *rlds,
                          const uint8_t *base, uint64_t len, uint64_t cut, IterSt &st, uint64_t *s, uint64_t *e,
-                         bool *reached = nullptr) {
+                         bool *reached = nullptr, const WaveCtx *wc = nullptr, bool *piked = nullptr) {
   while (true) {
     if (st.p > len) return 0;
-    const int k = dfa_find_cut(f, r, lds, rlds, base, len, st.p, cut, s, e, reached);
+    int k = dfa_find_cut(f, r, lds, rlds, base, len, st.p, cut, s, e, reached);
+    if (k == 0 && f.can_quit == 2 && st.p > 0 && st.p < cut && base[st.p - 1] >= 0x80) {
+      // No match before the cut, from a start whose previous byte is >= 0x80:
+      // the DFA's start flags read it as a non-word byte (dfa.rs:1423), and
+      // the reference's unbounded scan goes on past the cut -- if it quits
+      // on a byte >= 0x80 its NFA answers for this search, which may start
+      // before the cut.  The lanes hand such a search over as a quit; the
+      // wave runs the unbounded scan to see.
+      if (!wc) {
+        k = 2;
+      } else {
+        uint64_t s2, e2;
+        if (dfa_find(f, r, lds, rlds, base, len, st.p, &s2, &e2) == 2) k = 2;
+      }
+    }
+    if (k == 2 && wc) {
+      if (piked) *piked = true;
+      uint64_t r0, r1;
+      pike::pike_one<MODE_FIND>(*wc->nf, *wc->W, *wc->tg, base, len, st.p, &r0, &r1, st.p < cut ? cut : ~0ull);
+      if (reached) *reached = false;
+      k = r1 == NONE ? 0 : 1;
+      *s = r0;
+      *e = r1;
+    }
     reached = nullptr;
     if (k != 1) return k;
     if (*s == *e) {
@@ -170,18 +204,19 @@ struct UnitIter {
   uint64_t from;  // the first search may scan from here: no match starts in [st.p, from)
   bool ended, clean, quit;
   bool first, unsure;  // look-around: the first search's reverse scan reached its start
+  bool waved;          // a search ran on the wave's Pike VM (wc)
   IterSt exit;
 
   __device__ void init(IterSt s0, uint64_t cut) {
     st = s0;
     c1 = cut;
     from = 0;
-    ended = clean = quit = unsure = false;
+    ended = clean = quit = unsure = waved = false;
     first = true;
   }
   // Returns true with the next owned match, false when the unit is finished.
   __device__ bool next(const FwdDfaDev &f, const RevDfaDev &r, const uint8_t *lds, const uint8_t *rlds,
-                       const uint8_t *base, uint64_t len, uint64_t *s, uint64_t *e) {
+                       const uint8_t *base, uint64_t len, uint64_t *s, uint64_t *e, const WaveCtx *wc = nullptr) {
     if (ended) return false;
     if (st.p == kIterStop) {  // the iteration ended (look-around: a reverse NoMatch)
       ended = true;
@@ -201,7 +236,9 @@ struct UnitIter {
     IterSt q = st;
     if (q.p < from) q.p = from;
     bool reached = false;
-    const int k = iter_next(f, r, lds, rlds, base, len, c1, q, s, e, first ? &reached : nullptr);
+    bool pk = false;
+    const int k = iter_next(f, r, lds, rlds, base, len, c1, q, s, e, first ? &reached : nullptr, wc, &pk);
+    waved |= pk;
     if (first) unsure = reached;
     first = false;
     if (k == 1 && *s < c1) { st = q; return true; }
@@ -368,6 +405,7 @@ __global__ __launch_bounds__(1024) void iter_spec_burst_kernel(BatchDev b, Geo g
     uint64_t ex_p = 0, ex_lm = NONE;
     bool clean = true, quit = false, searching = false;
     bool first = true, unsure = false;  // look-around: UnitIter's
+    bool qfirst = false;                // the search that quit was the unit's first
     uint32_t n = 0;
     LaneState L;
     L.done = true;
@@ -420,21 +458,36 @@ __global__ __launch_bounds__(1024) void iter_spec_burst_kernel(BatchDev b, Geo g
       if (!L.done && f.eof[L.s]) L.last = len;
       if (L.quit) {
         quit = true;
+        qfirst = first;
         if (abortf) atomicOr(abortf, 1u);
         finish(sp, slm, false);
         continue;
       }
-      if (L.last == NONE) { finish(sp, slm, true); continue; }
+      if (L.last == NONE) {
+        // (iter_next: a start after a byte >= 0x80 with no match before the
+        // cut is handed over as a quit)
+        if (f.can_quit == 2 && at0 > 0 && at0 < c1 && base[at0 - 1] >= 0x80) {
+          quit = true;
+          qfirst = first;
+          if (abortf) atomicOr(abortf, 1u);
+          finish(sp, slm, false);
+        } else {
+          finish(sp, slm, true);
+        }
+        continue;
+      }
       const uint64_t me = L.last;
       uint64_t ms = at0;
       bool reached = me == at0;
       if (me != at0) {  // exec.rs:647
         const uint64_t rs = r.all ? rev_scan_all(r, rlds, base, len, at0, me, &reached)
                                   : rev_scan(r, rlds, base, len, at0, me, &reached);
+        const bool was_first = first;
         if (first) unsure = reached;
         first = false;
         if (rs == QUITMARK) {
           quit = true;
+          qfirst = was_first;
           if (abortf) atomicOr(abortf, 1u);
           finish(sp, slm, false);
           continue;
@@ -469,9 +522,14 @@ __global__ __launch_bounds__(1024) void iter_spec_burst_kernel(BatchDev b, Geo g
       U.exit = {ex_p, ex_lm};
       U.spec_exit = U.exit;
       U.spec_count = n;
+      // (a unit after a byte >= 0x80 is unsure too when the DFA can quit: a
+      // search from before its start reads that byte and quits, the fresh
+      // one at c0 reads it as a non-word byte, dfa.rs:1423)
+      const bool pre = f.can_quit == 2 && c0 > 0 && base[c0 - 1] >= 0x80;
       U.flags = (clean ? (U_SPEC_CLEAN | U_CLEAN) : 0) | (quit ? U_QUIT : 0) |
-                (f.looks && unsure && u % g.nk != 0 ? U_UNSURE : 0);
-      U.skip = U.pad = 0;
+                (((f.looks && unsure) || pre) && u % g.nk != 0 ? U_UNSURE : 0);
+      U.skip = 0;
+      U.pad = quit && qfirst ? 1 : 0;  // (a quit unit: its exit is the state before the search that quit)
       units[u] = U;
       counts[u] = n;
       if ((U.flags & (U_SPEC_CLEAN | U_UNSURE)) != U_SPEC_CLEAN) atomicOr(dirty, 1u);  // the fix pass has work
@@ -1725,7 +1783,7 @@ __device__ int64_t join_speculation(const Unit &U, uint64_t c0, IterSt E, const 
 // Updates the unit's record and count; returns true if its exit changed.
 __device__ bool repair_unit(const BatchDev &b, const Geo &g, const FwdDfaDev &f, const RevDfaDev &r,
                             const uint8_t *lds, const uint8_t *rlds, uint64_t j, IterSt E, Unit *units,
-                            uint32_t *counts, const uint64_t *slots) {
+                            uint32_t *counts, const uint64_t *slots, const WaveCtx *wc = nullptr) {
   uint64_t h, len, c0, c1;
   const uint8_t *base;
   unit_bounds(b, g, j, &h, &base, &len, &c0, &c1);
@@ -1767,18 +1825,18 @@ __device__ bool repair_unit(const BatchDev &b, const Geo &g, const FwdDfaDev &f,
   F.init(E, c1);
   S.init({c0, NONE}, c1);
   uint64_t fs, fe, ss, se;
-  bool fm = F.next(f, r, lds, rlds, base, len, &fs, &fe);
-  bool sm = S.next(f, r, lds, rlds, base, len, &ss, &se);
+  bool fm = F.next(f, r, lds, rlds, base, len, &fs, &fe, wc);
+  bool sm = S.next(f, r, lds, rlds, base, len, &ss, &se, wc);
   uint32_t fcnt = 0, scnt = 0;
   bool synced = false;
   while (fm) {
     if (sm && fs == ss && fe == se) { synced = true; break; }
     if (!sm || fs < ss || (fs == ss && fe < se)) {
       ++fcnt;
-      fm = F.next(f, r, lds, rlds, base, len, &fs, &fe);
+      fm = F.next(f, r, lds, rlds, base, len, &fs, &fe, wc);
     } else {
       ++scnt;
-      sm = S.next(f, r, lds, rlds, base, len, &ss, &se);
+      sm = S.next(f, r, lds, rlds, base, len, &ss, &se, wc);
     }
   }
   if (synced) {
@@ -1796,7 +1854,9 @@ __device__ bool repair_unit(const BatchDev &b, const Geo &g, const FwdDfaDev &f,
     U.exit = F.exit;
     U.flags |= (F.clean ? U_CLEAN : 0);
   }
-  U.flags |= (F.quit || S.quit) ? U_QUIT : 0;
+  // (U_QUIT: a search quit -- or, served by the wave, ran on the Pike VM:
+  // the unit stays the wave kernels' to re-run)
+  U.flags |= (F.quit || S.quit || F.waved || S.waved) ? U_QUIT : 0;
   units[j] = U;
   return changed;
 }
@@ -1821,7 +1881,11 @@ __device__ __forceinline__ void fix_body(const BatchDev &b, const Geo &g, uint64
       rlds = stage_tables(f, r, lds);
       staged = true;
     }
-    if (need && repair_unit(b, g, f, r, lds, rlds, u + 1, units[u].spec_exit, units, counts, slots)) {
+    // (a unit with U_QUIT is the wave pass's, iter_wfix_kernel: also one
+    // whose lane repair quits here)
+    const bool lane_ok = need && !(units[u + 1].flags & U_QUIT);
+    if (lane_ok && repair_unit(b, g, f, r, lds, rlds, u + 1, units[u].spec_exit, units, counts, slots) &&
+        !(units[u + 1].flags & U_QUIT)) {
       const unsigned long long q = atomicAdd(qlen, 1ull);
       queue[q] = u + 1;
     }
@@ -1838,16 +1902,21 @@ __global__ __launch_bounds__(1024) void iter_fix_kernel(BatchDev b, Geo g, uint6
 }
 
 // Pass 3 (one thread): propagate exits that changed, in unit order.
+// wc: the whole wave runs it (wave-uniform; every lane stores the same
+// values) and a search whose DFA quits runs on the Pike VM.
 __device__ __forceinline__ void walk_body(const BatchDev &b, const Geo &g, uint64_t nunits, const FwdDfaDev &f,
                                           const RevDfaDev &r, Unit *units, uint32_t *counts, const uint64_t *slots,
-                                          uint64_t *queue, unsigned long long *qlen) {
+                                          uint64_t *queue, unsigned long long *qlen, const WaveCtx *wc = nullptr) {
   const uint64_t n = *qlen;
   if (n == 0) return;
-  for (uint64_t i = 1; i < n; ++i) {  // insertion sort (the queue is short)
-    uint64_t v = queue[i], k = i;
-    while (k > 0 && queue[k - 1] > v) { queue[k] = queue[k - 1]; --k; }
-    queue[k] = v;
+  if (threadIdx.x == 0) {
+    for (uint64_t i = 1; i < n; ++i) {  // insertion sort (the queue is short)
+      uint64_t v = queue[i], k = i;
+      while (k > 0 && queue[k - 1] > v) { queue[k] = queue[k - 1]; --k; }
+      queue[k] = v;
+    }
   }
+  if (wc) __syncthreads();
   uint64_t walked = 0;
   for (uint64_t i = 0; i < n; ++i) {
     const uint64_t j = queue[i];
@@ -1873,8 +1942,9 @@ __device__ __forceinline__ void walk_body(const BatchDev &b, const Geo &g, uint6
         units[u] = W;
         counts[u] = W.spec_count;
       } else {
-        repair_unit(b, g, f, r, f.lds_image /* unused: hot = 0 */, nullptr, u, X.exit, units, counts, slots);
+        repair_unit(b, g, f, r, f.lds_image /* unused: hot = 0 */, nullptr, u, X.exit, units, counts, slots, wc);
       }
+      if (wc) __syncthreads();
       X = units[u];
       ++u;
     }
@@ -1895,6 +1965,148 @@ __global__ void iter_walk_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f
   if (gated_off(b)) return;
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   walk_body(b, g, nunits, f, r, units, counts, slots, queue, qlen);
+}
+
+// ------------------------------------- the wave-served chunked iteration
+// A regex whose DFA can quit (a Unicode \b over non-ASCII bytes,
+// dfa.rs:1491-1496) keeps the chunked iteration: the lane passes above run
+// as usual, and a unit where a search quit (U_QUIT) is taken over by one
+// wave, which runs that search -- and any later one whose DFA quits -- on
+// the Pike VM (exec.rs:485-487: the reference's NFA fallback for that
+// search), bounded by the unit's cut like the DFA's.  U_QUIT then marks the
+// unit as the wave kernels': its speculation (iter_wspec_kernel), its repair
+// (iter_wfix_kernel), the walker (iter_wwalk_kernel, wave-uniform) and its
+// re-emission (iter_wemit_kernel).  Tables: global (the LDS holds the Pike
+// VM's lists, pike::Lists, nfa_wave_bytes per wave): f.hot = r.hot = 0, and
+// an all-rows table is read from its global image (as the walker does).
+
+__device__ __forceinline__ void wave_lists(const NfaDev &nf, uint8_t *mem, pike::Lists &W) {
+  const uint32_t N = nf.nleaves;
+  W.st[0] = (uint64_t *)mem;
+  W.st[1] = W.st[0] + N;
+  W.stamp = (uint32_t *)(W.st[1] + N);
+  W.leaf[0] = W.stamp + N;
+  W.leaf[1] = W.leaf[0] + N;
+  for (uint32_t i = pike::lane_id(); i < N; i += 64) W.stamp[i] = 0xFFFFFFFFu;
+  pike::wave_sync();
+}
+
+// The speculation of every U_QUIT unit, resumed at the search that quit
+// (the lane pass left the state before it as the unit's exit, its matches so
+// far in the slots, U.pad = that search was the unit's first).
+__global__ __launch_bounds__(64) void iter_wspec_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f,
+                                                        RevDfaDev r, NfaDev nf, Unit *units, uint64_t *slots,
+                                                        uint32_t *counts, uint32_t *dirty, uint8_t *scratch) {
+  if (gated_off(b)) return;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds_mem[];
+  pike::Lists W;
+  wave_lists(nf, scratch ? scratch + (size_t)blockIdx.x * nfa_wave_bytes(nf.nleaves) : lds_mem, W);
+  pike::TagGen tg;
+  const WaveCtx wc{&nf, &W, &tg};
+  const uint32_t lane = pike::lane_id();
+  for (uint64_t u = blockIdx.x; u < nunits; u += gridDim.x) {
+    const Unit U = units[u];
+    if (!(U.flags & U_QUIT)) continue;
+    uint64_t h, len, c0, c1;
+    const uint8_t *base;
+    unit_bounds(b, g, u, &h, &base, &len, &c0, &c1);
+    UnitIter it;
+    it.init(U.exit, c1);
+    it.first = U.pad != 0;
+    uint32_t n = U.spec_count;
+    uint64_t s, e;
+    while (it.next(f, r, f.lds_image, nullptr, base, len, &s, &e, &wc)) {
+      if (n < g.slots && lane == 0) {
+        slots[(u * g.slots + n) * 2] = s;
+        slots[(u * g.slots + n) * 2 + 1] = e;
+      }
+      ++n;
+    }
+    const bool pre = f.can_quit == 2 && c0 > 0 && base[c0 - 1] >= 0x80;  // (as iter_spec_burst_kernel)
+    const bool unsure = (U.pad != 0 ? f.looks && it.unsure : (U.flags & U_UNSURE) != 0) || pre;
+    Unit V;
+    V.entry = {c0, NONE};
+    V.exit = it.exit;
+    V.spec_exit = it.exit;
+    V.spec_count = n;
+    V.flags = (it.clean ? (U_SPEC_CLEAN | U_CLEAN) : 0) | U_QUIT | (unsure && u % g.nk != 0 ? U_UNSURE : 0);
+    V.skip = V.pad = 0;
+    if (lane == 0) {
+      units[u] = V;
+      counts[u] = n;
+      if ((V.flags & (U_SPEC_CLEAN | U_UNSURE)) != U_SPEC_CLEAN) atomicOr(dirty, 1u);
+    }
+  }
+}
+
+// fix_body's repairs of the units the lane pass left (U_QUIT: a quit in the
+// speculation or in the lane repair); a changed exit is queued for the walker.
+__global__ __launch_bounds__(64) void iter_wfix_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
+                                                       NfaDev nf, Unit *units, uint32_t *counts, const uint64_t *slots,
+                                                       uint64_t *queue, unsigned long long *qlen, const uint32_t *dirty,
+                                                       uint8_t *scratch) {
+  if (gated_off(b) || *dirty == 0) return;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds_mem[];
+  pike::Lists W;
+  wave_lists(nf, scratch ? scratch + (size_t)blockIdx.x * nfa_wave_bytes(nf.nleaves) : lds_mem, W);
+  pike::TagGen tg;
+  const WaveCtx wc{&nf, &W, &tg};
+  for (uint64_t u = blockIdx.x; u + 1 < nunits; u += gridDim.x) {
+    const uint32_t fn = units[u + 1].flags;
+    const bool need = (u + 1) % g.nk != 0 && (fn & U_QUIT) &&
+                      (!(units[u].flags & U_SPEC_CLEAN) || (fn & U_UNSURE));
+    if (!need) continue;
+    const bool ch = repair_unit(b, g, f, r, f.lds_image, nullptr, u + 1, units[u].spec_exit, units, counts, slots, &wc);
+    if (ch && pike::lane_id() == 0) {
+      const unsigned long long q = atomicAdd(qlen, 1ull);
+      queue[q] = u + 1;
+    }
+  }
+}
+
+// The walker with the whole wave (one block of 64).
+__global__ __launch_bounds__(64) void iter_wwalk_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
+                                                        NfaDev nf, Unit *units, uint32_t *counts, const uint64_t *slots,
+                                                        uint64_t *queue, unsigned long long *qlen, uint8_t *scratch) {
+  if (gated_off(b) || blockIdx.x != 0) return;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds_mem[];
+  pike::Lists W;
+  wave_lists(nf, scratch ? scratch : lds_mem, W);
+  pike::TagGen tg;
+  const WaveCtx wc{&nf, &W, &tg};
+  walk_body(b, g, nunits, f, r, units, counts, slots, queue, qlen, &wc);
+}
+
+// emit_body's re-runs of U_QUIT units (from the unit's entry, cnt matches).
+__global__ __launch_bounds__(64) void iter_wemit_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
+                                                        NfaDev nf, const Unit *units, const uint64_t *off,
+                                                        uint64_t *out, uint64_t cap, uint8_t *scratch) {
+  if (gated_off(b)) return;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds_mem[];
+  pike::Lists W;
+  wave_lists(nf, scratch ? scratch + (size_t)blockIdx.x * nfa_wave_bytes(nf.nleaves) : lds_mem, W);
+  pike::TagGen tg;
+  const WaveCtx wc{&nf, &W, &tg};
+  const uint64_t obase = off[0];
+  for (uint64_t u = blockIdx.x; u < nunits; u += gridDim.x) {
+    const uint32_t fl = units[u].flags;
+    if (!(fl & U_QUIT)) continue;
+    const uint64_t o0 = off[u] - obase, cnt = off[u + 1] - off[u];
+    if (!cnt || o0 >= cap || !(((fl & U_FIXED) && !(fl & U_COPY)) || cnt > g.slots)) continue;
+    uint64_t h, len, c0, c1;
+    const uint8_t *base;
+    unit_bounds(b, g, u, &h, &base, &len, &c0, &c1);
+    UnitIter it;
+    it.init(units[u].entry, c1);
+    uint64_t s, e, i = 0;
+    while (i < cnt && it.next(f, r, f.lds_image, nullptr, base, len, &s, &e, &wc)) {
+      if (o0 + i < cap && pike::lane_id() == 0) {
+        out[2 * (o0 + i)] = s;
+        out[2 * (o0 + i) + 1] = e;
+      }
+      ++i;
+    }
+  }
 }
 
 // Span entry (sharded / streamed find_iter): the first unit is entered with
@@ -1961,6 +2173,7 @@ __device__ __forceinline__ void emit_body(const BatchDev &b, const Geo &g, uint6
         const uint32_t fl = units[u].flags;
         rerun = ((fl & U_FIXED) && !(fl & U_COPY)) || cnt > g.slots;
         copy = !rerun && copies;  // copies = false: iter_copy_group_kernel wrote them
+        if (fl & U_QUIT) rerun = false;  // the wave's (iter_wemit_kernel)
         skip = (fl & U_COPY) ? units[u].skip : 0;  // loaded by every lane at once, not per copied unit
         compact = LEX && (fl & U_COMPACT) != 0;
         if (compact) {
@@ -2531,9 +2744,39 @@ static bool sa_tile_ok(const BatchDev &b, const Geo &g) {
 // The passes after the speculative one (same for every engine): a span's
 // entry, the repairs (fix, walk), the output offsets, emission, per-haystack
 // counts and a span's exit.
+// wnf: the wave-served iteration (U_QUIT units on the Pike VM, above).
+static hipError_t iter_post_body(const BatchDev &b, const Geo &g, uint64_t nunits, const FwdDfaDev &f,
+                                 const RevDfaDev &r, const IterScratch &sc, const IterOut &o, const IterSpan *spn,
+                                 hipStream_t st, int cus, bool dense, const NfaDev *wnf, uint8_t *wscr, size_t wlds,
+                                 int wgrid);
+
 static hipError_t iter_post(const BatchDev &b, const Geo &g, uint64_t nunits, const FwdDfaDev &f, const RevDfaDev &r,
                             const IterScratch &sc, const IterOut &o, const IterSpan *spn, hipStream_t st, int cus,
-                            bool dense = false) {
+                            bool dense = false, const NfaDev *wnf = nullptr) {
+  if (!wnf) return iter_post_body(b, g, nunits, f, r, sc, o, spn, st, cus, dense, nullptr, nullptr, 0, 0);
+  // one wave per block, the Pike VM's lists in LDS (else global scratch)
+  const size_t wb = nfa_wave_bytes(wnf->nleaves);
+  const bool use_lds = wb <= kNfaLdsMax;
+  const int wgrid = grid_cap(nunits, 1, cus, use_lds ? std::max<int>(1, std::min<int>(32, (int)((160u * 1024u) / wb))) : 4);
+  uint8_t *wscr = nullptr;
+  hipError_t e = hipSuccess;
+  if (!use_lds && (e = scratch_malloc((void **)&wscr, wb * (size_t)wgrid, st)) != hipSuccess) return e;
+  const size_t wlds = use_lds ? wb : 0;
+  if (wlds > 64 * 1024 &&
+      ((e = allow_lds(iter_wspec_kernel, wlds)) != hipSuccess || (e = allow_lds(iter_wfix_kernel, wlds)) != hipSuccess ||
+       (e = allow_lds(iter_wwalk_kernel, wlds)) != hipSuccess || (e = allow_lds(iter_wemit_kernel, wlds)) != hipSuccess)) {
+    (void)scratch_free(wscr, st);
+    return e;
+  }
+  e = iter_post_body(b, g, nunits, f, r, sc, o, spn, st, cus, dense, wnf, wscr, wlds, wgrid);
+  const hipError_t e2 = scratch_free(wscr, st);
+  return e != hipSuccess ? e : e2;
+}
+
+static hipError_t iter_post_body(const BatchDev &b, const Geo &g, uint64_t nunits, const FwdDfaDev &f,
+                                 const RevDfaDev &r, const IterScratch &sc, const IterOut &o, const IterSpan *spn,
+                                 hipStream_t st, int cus, bool dense, const NfaDev *wnf, uint8_t *wscr, size_t wlds,
+                                 int wgrid) {
   hipError_t e;
   const int bs = iter_bs();
   const size_t lb = iter_lds_bytes(f, r);
@@ -2541,6 +2784,15 @@ static hipError_t iter_post(const BatchDev &b, const Geo &g, uint64_t nunits, co
   const int grid = grid_cap(nunits, bs, cus, per_cu);
   if ((e = allow_lds(iter_fix_kernel, lb)) != hipSuccess || (e = allow_lds(iter_emit_kernel, lb)) != hipSuccess)
     return e;
+  FwdDfaDev fw0 = f;  // the wave kernels: global tables
+  fw0.hot = 0;
+  RevDfaDev rw0 = r;
+  rw0.hot = 0;
+  if (wnf) {  // the quit units' speculation, resumed on the wave
+    hipLaunchKernelGGL(iter_wspec_kernel, dim3(wgrid), dim3(64), wlds, st, b, g, nunits, fw0, rw0, *wnf, sc.units,
+                       sc.slots, sc.counts, sc.dirty, wscr);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
   if (spn && spn->entry) {
     FwdDfaDev fw = f;
     fw.hot = 0;
@@ -2554,12 +2806,16 @@ static hipError_t iter_post(const BatchDev &b, const Geo &g, uint64_t nunits, co
     hipLaunchKernelGGL(iter_fix_kernel, dim3(grid), dim3(bs), lb, st, b, g, nunits, f, r, sc.units, sc.counts,
                        (const uint64_t *)sc.slots, sc.queue, sc.qlen, (const uint32_t *)sc.dirty);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    FwdDfaDev fw = f;
-    fw.hot = 0;
-    RevDfaDev rw = r;
-    rw.hot = 0;
-    hipLaunchKernelGGL(iter_walk_kernel, dim3(1), dim3(64), 0, st, b, g, nunits, fw, rw, sc.units, sc.counts,
-                       (const uint64_t *)sc.slots, sc.queue, sc.qlen);
+    if (wnf) {
+      hipLaunchKernelGGL(iter_wfix_kernel, dim3(wgrid), dim3(64), wlds, st, b, g, nunits, fw0, rw0, *wnf, sc.units,
+                         sc.counts, (const uint64_t *)sc.slots, sc.queue, sc.qlen, (const uint32_t *)sc.dirty, wscr);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+      hipLaunchKernelGGL(iter_wwalk_kernel, dim3(1), dim3(64), wlds, st, b, g, nunits, fw0, rw0, *wnf, sc.units,
+                         sc.counts, (const uint64_t *)sc.slots, sc.queue, sc.qlen, wscr);
+    } else {
+      hipLaunchKernelGGL(iter_walk_kernel, dim3(1), dim3(64), 0, st, b, g, nunits, fw0, rw0, sc.units, sc.counts,
+                         (const uint64_t *)sc.slots, sc.queue, sc.qlen);
+    }
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   if ((e = scan_counts(sc.counts, sc.off, nunits, st)) != hipSuccess) return e;
@@ -2575,6 +2831,11 @@ static hipError_t iter_post(const BatchDev &b, const Geo &g, uint64_t nunits, co
   hipLaunchKernelGGL(iter_emit_kernel, dim3(grid), dim3(bs), lb, st, b, g, nunits, f, r, sc.units, sc.slots, sc.off,
                      o.matches, o.cap, dense ? 0 : 1);
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  if (wnf) {
+    hipLaunchKernelGGL(iter_wemit_kernel, dim3(wgrid), dim3(64), wlds, st, b, g, nunits, fw0, rw0, *wnf,
+                       (const Unit *)sc.units, (const uint64_t *)sc.off, o.matches, o.cap, wscr);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(iter_counts_kernel, dim3(grid_cap(b.count, 256, cus, 4)), dim3(256), 0, st, b.count, g.nk,
                      sc.off, o.counts, o.total, b);
   if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -2814,6 +3075,10 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
                             const IterSpan *spn, const MatchDev *mtd, bool *quit, uint32_t *quit_dev) {
   const uint64_t hi = spn ? spn->hi : ~0ull;
   if (quit_dev && (!chunked || spn || b.gate || !f || !f->can_quit)) return hipErrorInvalidValue;
+  // chunked, a DFA that can quit, no quit flag asked for: the wave-served
+  // iteration (the quit units' searches on the Pike VM; no span)
+  const bool wq = chunked && f && f->can_quit && !quit && !quit_dev && nf;
+  if (wq && spn) return hipErrorInvalidValue;
   hipError_t e = hipSuccess;
   if (b.count == 0) {
     return hipMemsetAsync(o.total, 0, 8, st);
@@ -2851,12 +3116,14 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
       // 16 words 2.29 -> 0.72 ms, 64 words 5.43 -> 2.29 ms per GiB); with a
       // small DFA it depends on the text (English -25 %, DNA +25 %), so the
       // DFA stays.  Knob lit=1 / 0 forces it on / off.
-      const bool use_lit = f->lit_n && (knob(Knob::Lit) >= 0 ? knob(Knob::Lit) == 1 : !f->all);
+      // (a DFA that can quit takes the burst kernel: it alone hands quits
+      // and starts after a byte >= 0x80 over, iter_next)
+      const bool use_lit = !f->can_quit && f->lit_n && (knob(Knob::Lit) >= 0 ? knob(Knob::Lit) == 1 : !f->all);
       // Shift-And engine for equal-length string sets; RURE_AMD_SA=0 disables
-      const bool use_sa = sa_usable(*f);
+      const bool use_sa = !f->can_quit && sa_usable(*f);
       const bool sa_tile = sa_tile_ok(b, g);
       // Lexer engine (terminal matches + first-byte rule); RURE_AMD_LEX=0 disables
-      const bool use_lex = lex_usable(*f, b, g);
+      const bool use_lex = !f->can_quit && lex_usable(*f, b, g);
       // the quit flag (a caller that re-runs on a quit): zeroed here, set by
       // the burst kernel's first quit (the others stop) and by iter_quit_kernel
       uint32_t *qd = quit_dev;
@@ -2956,7 +3223,7 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
           break;
         }
       }
-      e = iter_post(b, g, nunits, *f, r, sc, o, spn, st, cus, use_lex);
+      e = iter_post(b, g, nunits, *f, r, sc, o, spn, st, cus, use_lex, wq ? nf : nullptr);
       if (e == hipSuccess && f->can_quit && quit) {  // did any search quit?
         uint32_t q = 0;
         if ((e = hipMemsetAsync(dirty, 0, 4, st)) != hipSuccess) break;

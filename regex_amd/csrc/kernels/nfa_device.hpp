@@ -169,9 +169,13 @@ struct TagGen {
 };
 
 // pikevm.rs:130-223 for one haystack (wave-uniform control flow).
+// cut (the chunked find_iter's unit end, > start): no thread starts at or
+// after it, so the search ends once every thread that started before it has
+// died or matched -- the unrestricted search's answer when that starts
+// before the cut (an earlier start outranks every later one), else none.
 template <int MODE>
 __device__ void pike_one(const NfaDev &nf, Lists &W, TagGen &tg, const uint8_t *text, uint64_t len, uint64_t start,
-                         uint64_t *r0, uint64_t *r1) {
+                         uint64_t *r0, uint64_t *r1, uint64_t cut = ~0ull) {
   const uint32_t lane = lane_id();
   uint64_t ms = NONE, me = NONE, mask = 0;
   bool matched = false, all_matched = false;
@@ -186,8 +190,8 @@ __device__ void pike_one(const NfaDev &nf, Lists &W, TagGen &tg, const uint8_t *
   uint32_t nc = 0, ctag = tg.next(W.stamp, nf.nleaves);
   uint64_t at = start;
   while (true) {
-    if (nc == 0 && ((matched && nf.single) || all_matched || (at != 0 && nf.anchored))) break;
-    if (nc == 0 || (!nf.anchored && !all_matched))
+    if (nc == 0 && ((matched && nf.single) || all_matched || (at != 0 && nf.anchored) || at >= cut)) break;
+    if (at < cut && (nc == 0 || (!nf.anchored && !all_matched)))
       nc = append_closure(nf, nf.root, look_holds(text, len, at, nf), at, W.stamp, ctag, W.leaf[c], W.st[c], nc);
     const uint32_t b = at < len ? text[at] : 0x100u;
     const uint32_t ntag = tg.next(W.stamp, nf.nleaves);

@@ -2,15 +2,45 @@
 regex_amd/csrc/kernels/iter_scan.hip (speculative units, lockstep repair,
 sequential walker, emit), over the exported find_iter DFA tables.
 TEST INFRASTRUCTURE: validates the boundary-repair algorithm on CPU."""
-from dfa_sim import find
+from dfa_sim import QuitError, find
 
 NONE = None
 STOP = float("inf")  # the exit of an iteration that ended (a search's NoMatch)
 
 
+def wave_search(nfa):
+    """iter_scan.hip iter_next with a WaveCtx (the wave-served units of a
+    regex with a Unicode word boundary): a search whose DFA quits runs on the
+    NFA (nfa(t, start): the reference's NFA search, exec.rs:485-487) bounded
+    by the cut; a search from just after a byte >= 0x80 that finds no match
+    before the cut runs the DFA unbounded, as the reference does, and takes
+    the NFA's answer if that scan quits (its start flags read the byte as a
+    non-word byte, dfa.rs:1423)."""
+    def search(fwd, rev, t, start=0, mode="find", cut=None, fb=None, out=None):
+        def by_nfa():
+            if out is not None:
+                out["reached"] = False
+            m = nfa(t, start)
+            if m is None or (cut is not None and start < cut and m[0] >= cut):
+                return None
+            return tuple(m)
+        try:
+            m = find(fwd, rev, t, start, mode, cut, fb, out)
+        except QuitError:
+            return by_nfa()
+        if m is None and start > 0 and t[start - 1] >= 0x80 and cut is not None and start < cut:
+            try:
+                find(fwd, rev, t, start, mode, None, fb, {})
+            except QuitError:
+                return by_nfa()
+        return m
+    return search
+
+
 class UnitIter(object):
-    def __init__(self, fwd, rev, t, st, c1, fb=None, scan_from=0):
+    def __init__(self, fwd, rev, t, st, c1, fb=None, scan_from=0, search=find):
         self.fwd, self.rev, self.t, self.fb = fwd, rev, t, fb
+        self.search = search
         self.p, self.lm = st
         self.c1 = c1
         # the first search may scan from here (no match starts in [p, scan_from):
@@ -33,7 +63,7 @@ class UnitIter(object):
             if self.p > len(t):
                 return None
             out = {}
-            m = find(self.fwd, self.rev, t, self.p, cut=self.c1, fb=self.fb, out=out)
+            m = self.search(self.fwd, self.rev, t, self.p, cut=self.c1, fb=self.fb, out=out)
             if self.first:
                 self.unsure = out.get("reached", False)
                 self.first = False
@@ -88,14 +118,17 @@ def equiv(ca, a, cb, b, strict=False):
     return a == b
 
 
-def find_iter_chunked(fwd, rev, t, chunk, start=0, slots=1 << 30, fb=None, looks=False):
+def find_iter_chunked(fwd, rev, t, chunk, start=0, slots=1 << 30, fb=None, looks=False, nfa=None):
+    """nfa: the wave-served iteration of a regex with a Unicode word
+    boundary (wave_search; a unit after a byte >= 0x80 is unsure)."""
     INF = float("inf")
+    search = wave_search(nfa) if nfa else find
     span = max(0, len(t) - start)
     nk = 1 if span <= chunk else (span + chunk - 1) // chunk
     bounds = [(start + k * chunk, INF if k + 1 == nk else start + (k + 1) * chunk) for k in range(nk)]
     units = []
     for k, (c0, c1) in enumerate(bounds):  # pass 1: speculation
-        it = UnitIter(fwd, rev, t, (c0, None), c1, fb)
+        it = UnitIter(fwd, rev, t, (c0, None), c1, fb, search=search)
         ms = []
         while True:
             m = it.next()
@@ -103,7 +136,7 @@ def find_iter_chunked(fwd, rev, t, chunk, start=0, slots=1 << 30, fb=None, looks
                 break
             ms.append(m)
         units.append({"entry": (c0, None), "spec": ms, "spec_exit": it.exit, "spec_clean": it.clean,
-                      "unsure": looks and k > 0 and it.unsure,
+                      "unsure": k > 0 and ((looks and it.unsure) or (nfa is not None and t[c0 - 1] >= 0x80)),
                       "exit": it.exit, "clean": it.clean, "fixed": False, "count": len(ms)})
 
     def sync_from_slots(j, E):
@@ -152,8 +185,8 @@ def find_iter_chunked(fwd, rev, t, chunk, start=0, slots=1 << 30, fb=None, looks
                 return False
             U["count"], U["exit"], U["clean"] = 0, E, True
             return not equiv(True, E, U["spec_clean"], U["spec_exit"], strict(j))
-        F = UnitIter(fwd, rev, t, E, c1)
-        S = UnitIter(fwd, rev, t, (c0, None), c1)
+        F = UnitIter(fwd, rev, t, E, c1, search=search)
+        S = UnitIter(fwd, rev, t, (c0, None), c1, search=search)
         fm, sm = F.next(), S.next()
         fcnt = scnt = 0
         synced = False
@@ -216,7 +249,7 @@ def find_iter_chunked(fwd, rev, t, chunk, start=0, slots=1 << 30, fb=None, looks
         if U.get("skip") is not None:  # repaired by joining the speculation: copy
             out.extend(U["spec"][U["skip"]:U["skip"] + U["count"]])
             continue
-        it = UnitIter(fwd, rev, t, U["entry"], bounds[u][1])
+        it = UnitIter(fwd, rev, t, U["entry"], bounds[u][1], search=search)
         got = []
         while len(got) < U["count"]:
             m = it.next()

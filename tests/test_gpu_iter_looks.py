@@ -7,7 +7,8 @@ text's start (exec.rs:651-661), so these cases stress what the chunked
 iteration must reproduce: units whose first reverse scan reaches their start
 (repaired from the true entry), reverse NoMatches that end the iteration
 (\\B at a unit start), and Unicode word boundaries whose DFA quits on
-non-ASCII bytes (the batch then goes to the wave path: last_fwd_path -13).
+non-ASCII bytes (the quitting units are served by the wave's Pike VM:
+last_fwd_path -27; tests/test_gpu_iter_wave.py).
 The debug knob iter_chunk forces small units (many boundaries)."""
 import os
 import random
@@ -70,22 +71,25 @@ def test_find_iter_looks_chunked(cuda, pat, chunk):
     L = 6000
     for count, seed in ((1, 1), (3, 2)):
         buf = _text(zlib.crc32(pat.encode()) + seed, L * count, False)
-        assert _check(re, buf, L, count, cuda, chunk) in (-12, -14, -25), pat
+        assert _check(re, buf, L, count, cuda, chunk) in (-12, -14, -25, -27), pat
 
 
 @pytest.mark.parametrize("pat", UNICODE_PATTERNS)
 @pytest.mark.parametrize("nonascii", [False, True])
-def test_find_iter_unicode_boundary(cuda, pat, nonascii):
-    """A DFA that can quit: ASCII text stays chunked (-12); a non-ASCII byte
-    next to a boundary makes a search quit and the wave path answer (-13)."""
+@pytest.mark.parametrize("wave", [1, 0])
+def test_find_iter_unicode_boundary(cuda, pat, nonascii, wave):
+    """A DFA that can quit (Unicode \\b): ASCII text stays chunked; with
+    non-ASCII bytes the units whose searches quit are served by the wave's
+    Pike VM inside the chunked iteration (-27); knob iter_wave=0 reads the
+    quit back and sends the batch to the wave path (-13)."""
     re = R.Regex(pat)
     L = 8000
     buf = _text(zlib.crc32(pat.encode()), L, nonascii)
-    path = _check(re, buf, L, 1, cuda, 64)
+    path = _check(re, buf, L, 1, cuda, 64, iter_wave=wave)
     if not nonascii:
-        assert path in (-12, -14, -25), pat
+        assert path in (-12, -14, -25, -27), pat
     elif "\\b" in pat or "\\B" in pat:
-        assert path == -13, pat
+        assert path == (-27 if wave else -13), pat
 
 
 @pytest.mark.parametrize("pat", [r"\b\w+\b", r"(?m)^\w+", r"\bthe\b", r"(?-u:\b)[A-Z]\w*", r"\w+ing\b"])
@@ -97,7 +101,7 @@ def test_find_iter_looks_long_sherlock(cuda, pat):
     re = R.Regex(pat)
     import torch
     counts, m = re.find_iter_batch(_dev(text, cuda), stride=len(text), length=len(text), count=1)
-    assert N.rure_amd_last_fwd_path() in (-12, -14, -25), pat
+    assert N.rure_amd_last_fwd_path() in (-12, -14, -25, -27), pat
     exp = OracleRegex(re).find_iter(text)
     assert [tuple(x) for x in m.cpu().numpy().tolist()] == exp
     del torch
@@ -113,7 +117,7 @@ def test_find_iter_looks_vs_stdlib(cuda, pat, chunk):
     for (off, n), exp in zip(fx["slices"], fx["find_iter"][pat]):
         counts, got, path = _run(re, text[off:off + n], n, 1, cuda, chunk)
         assert got == [tuple(x) for x in exp], (pat, off)
-        assert path in (-12, -14, -25), pat
+        assert path in (-12, -14, -25, -27), pat
 
 
 @pytest.mark.parametrize("pat", [r"\w+", r"\w+\s+\w+", r"[\w.]+@\w+", r"\pL+", r"\w{2,4}", r"(?m)^\w+",

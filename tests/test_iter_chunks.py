@@ -111,3 +111,46 @@ def test_chunked_iter_look_around(pat):
         exp = o.find_iter(t)
         for chunk in (1, 2, 3, 7, 16):
             assert find_iter_chunked(fwd, rev, t, chunk, looks=True) == exp, (pat, chunk, i)
+
+
+UWB_PATTERNS = [r"\b", r"\B", r"\b\w", r"\w\b", r"\B[a-z]{2}", r"[a-z]+ed\b", r"\b\w+\b", r"\w+\B", r"\b\w+n\b",
+                r"(?m)^\w+\b", r"\b|\B"]
+
+
+def uwb_text(seed, n, every):
+    """words with non-ASCII letters, marks, CJK, punctuation and invalid
+    bytes about every `every` bytes"""
+    rng = random.Random(seed)
+    words = [b"the", b"then", b"seen", b"added", b"ran", b"a", b"in", b"x1", b"_n"]
+    seps = [b" ", b", ", b".\n", b"-"]
+    odd = ["é".encode(), "ñ".encode(), b"\xff", "中".encode(), "’".encode(), "ёn".encode(), "́".encode()]
+    out = []
+    k = 0
+    while k < n:
+        w = rng.choice(words)
+        if rng.random() < 6.0 / every:
+            w = w[: rng.randint(0, len(w))] + rng.choice(odd) + w[rng.randint(0, len(w)):]
+        s = rng.choice(seps)
+        out += [w, s]
+        k += len(w) + len(s)
+    return b"".join(out)[:n]
+
+
+@pytest.mark.parametrize("pat", UWB_PATTERNS)
+def test_chunked_iter_unicode_boundary_wave(pat):
+    """The wave-served iteration of a Unicode word boundary (iter_scan.hip
+    iter_wspec_kernel .. iter_wemit_kernel; the reference's DFA quits on any
+    byte >= 0x80, dfa.rs:1487-1496, and that search runs on its NFA,
+    exec.rs:485-487): quitting searches on the NFA bounded by the cut, a
+    start after a byte >= 0x80 with no match before the cut decided by the
+    unbounded DFA scan, units after such a byte unsure.  Against the
+    oracle's sequential find_iter, tiny units, sparse and dense non-ASCII."""
+    re = R.Regex(pat)
+    fwd = re.dfa_tables(2)
+    rev = re.dfa_tables(1)
+    o = OracleRegex(re)
+    for i, every in enumerate((8, 30, 300, 8, 30, 300)):
+        t = uwb_text(zlib.crc32(pat.encode()) + i, 700 + 97 * i, every)
+        exp = o.find_iter(t)
+        for chunk in (3, 7, 16, 61):
+            assert find_iter_chunked(fwd, rev, t, chunk, looks=True, nfa=o.find_nfa) == exp, (pat, chunk, i)
