@@ -41,6 +41,7 @@ enum class Knob : int {
   ChainSeq,        // 1: a replace_all chain step by step, not as one composed byte map
   ShadowSync,      // 1: the ASCII shadow's find_iter quit read back, not gated on the device
   IterWave,        // 0: a find_iter DFA quit sends the batch to the wave path, not to the wave-served units
+  WaveCu,          // the wave-served units' waves per CU, their Pike VM lists in global scratch
   kCount
 };
 

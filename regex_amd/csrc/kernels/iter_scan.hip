@@ -2756,8 +2756,16 @@ static hipError_t iter_post(const BatchDev &b, const Geo &g, uint64_t nunits, co
   if (!wnf) return iter_post_body(b, g, nunits, f, r, sc, o, spn, st, cus, dense, nullptr, nullptr, 0, 0);
   // one wave per block, the Pike VM's lists in LDS (else global scratch)
   const size_t wb = nfa_wave_bytes(wnf->nleaves);
-  const bool use_lds = wb <= kNfaLdsMax;
-  const int wgrid = grid_cap(nunits, 1, cus, use_lds ? std::max<int>(1, std::min<int>(32, (int)((160u * 1024u) / wb))) : 4);
+  // Lists in LDS where 16 waves per CU fit, else in global scratch with 16
+  // waves per CU: the waves' work is latency-bound chains (global-table DFA
+  // steps, the Pike VM's list walks), and more waves in flight beat LDS
+  // lists (\b\w+n\b over 1 GiB of sherlock as it is, 2460 NFA leaves:
+  // 2 waves per CU in LDS 186 ms, 4 / 8 / 16 in scratch 134 / 112 / 102 ms,
+  // profiles/r06_wave_iter_bench.jsonl).  Knob wave_cu: waves per CU (A/B).
+  const long long kw = knob(Knob::WaveCu);
+  const int lds_cu = (int)std::min<size_t>(32, (160u * 1024u) / wb);
+  const bool use_lds = wb <= kNfaLdsMax && kw <= 0 && lds_cu >= 16;
+  const int wgrid = grid_cap(nunits, 1, cus, use_lds ? lds_cu : kw > 0 ? (int)std::min<long long>(kw, 32) : 16);
   uint8_t *wscr = nullptr;
   hipError_t e = hipSuccess;
   if (!use_lds && (e = scratch_malloc((void **)&wscr, wb * (size_t)wgrid, st)) != hipSuccess) return e;

@@ -46,13 +46,18 @@ def run(re, buf, L, reps):
 
 
 pats = sys.argv[1:] or [r"\b\w+n\b", r"\b\w+\b"]
+KN = os.environ.get("WAVE_KNOBS") or None  # a debug spec for the default runs (A/B of unit sizes)
+TEXTS = os.environ.get("WAVE_TEXTS", "as_is,ascii").split(",")
 for name, raw in (("as_is", raw0), ("ascii", bytes(b if b < 0x80 else 0x20 for b in raw0))):
+    if name not in TEXTS:
+        continue
     buf, L = device_text(raw)
     for pat in pats:
-        R._debug_set(None)
+        R._debug_set(KN)
         ms, n, m, path = run(R.Regex(pat), buf, L, 3)
+        R._debug_set(None)
         line = {"pattern": pat, "text": name, "bytes": L, "matches": n, "ms": round(ms, 3), "path": path,
-                "GBps": round(L / ms / 1e6, 2)}
+                "GBps": round(L / ms / 1e6, 2), "knobs": KN}
         if name == "ascii":
             R._debug_set("iter_wave=0")
             ms0, n0, m0, path0 = run(R.Regex(pat), buf, L, 3)
