@@ -60,6 +60,9 @@ enum : uint32_t {
                       // then the tail pass's as absolute ulonglong2 from the back (lex_rec32 / lex_row16)
   U_UNSURE = 128,     // look-around: the speculation's first reverse scan reached c0, so the true
                       // iteration entering earlier may differ even after a clean exit (repaired always)
+  U_PEND = 256,       // the wave-served iteration: the lane stopped at a search that quit (exit = the
+                      // state before it, U.pad = it is the unit's first); a wave answers it
+  U_RESUME = 512,     // ... answered: the lanes go on from the exit (iter_spec_burst_kernel mode 2)
 };
 
 // Look-around (FwdDfaDev::looks).  A search from p runs its reverse scan over
@@ -392,8 +395,12 @@ __device__ __forceinline__ uint64_t rev_scan_all(const RevDfaDev &r, const uint8
 // records are then meaningless; the call reports the quit).
 __global__ __launch_bounds__(1024) void iter_spec_burst_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f,
                                                               RevDfaDev r, Unit *units, uint64_t *slots,
-                                                              uint32_t *counts, uint32_t *dirty, uint32_t *abortf) {
-  if (gated_off(b)) return;
+                                                              uint32_t *counts, uint32_t *dirty, uint32_t *abortf,
+                                                              uint32_t mode) {
+  // mode bit 0: the wave-served iteration (a quit leaves the unit U_PEND);
+  // bit 1: resume the U_RESUME units from their records, skip the others
+  // (none when no unit was left pending: dirty bit 1)
+  if (gated_off(b) || ((mode & 2) && !(__atomic_load_n(dirty, __ATOMIC_RELAXED) & 2u))) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const uint8_t *rlds = stage_tables(f, r, lds);
   for (uint64_t u0 = (uint64_t)blockIdx.x * blockDim.x; u0 < nunits; u0 += (uint64_t)gridDim.x * blockDim.x) {
@@ -429,9 +436,21 @@ __global__ __launch_bounds__(1024) void iter_spec_burst_kernel(BatchDev b, Geo g
       slm = lm;
       begin_search();
     };
-    if (u < nunits) {
+    bool active = u < nunits;
+    if (active && (mode & 2)) {
+      const Unit R0 = units[u];
+      active = (R0.flags & U_RESUME) != 0;
+      if (active) {
+        p = R0.exit.p;
+        lm = R0.exit.lm;
+        n = R0.spec_count;
+        first = R0.pad != 0;
+        unsure = (R0.flags & U_UNSURE) != 0;
+      }
+    }
+    if (active) {
       unit_bounds(b, g, u, &h, &base, &len, &c0, &c1);
-      p = c0;
+      if (!(mode & 2)) p = c0;
       unit_next();
     }
     uint32_t polls = 0;
@@ -516,7 +535,7 @@ __global__ __launch_bounds__(1024) void iter_spec_burst_kernel(BatchDev b, Geo g
       ++n;
       unit_next();
     }
-    if (u < nunits) {
+    if (active) {
       Unit U;
       U.entry = {c0, NONE};
       U.exit = {ex_p, ex_lm};
@@ -526,13 +545,15 @@ __global__ __launch_bounds__(1024) void iter_spec_burst_kernel(BatchDev b, Geo g
       // search from before its start reads that byte and quits, the fresh
       // one at c0 reads it as a non-word byte, dfa.rs:1423)
       const bool pre = f.can_quit == 2 && c0 > 0 && base[c0 - 1] >= 0x80;
-      U.flags = (clean ? (U_SPEC_CLEAN | U_CLEAN) : 0) | (quit ? U_QUIT : 0) |
-                (((f.looks && unsure) || pre) && u % g.nk != 0 ? U_UNSURE : 0);
+      // (a resumed unit stays U_QUIT: one of its searches ran on the Pike VM)
+      U.flags = (clean ? (U_SPEC_CLEAN | U_CLEAN) : 0) | (quit ? U_QUIT : 0) | (quit && (mode & 1) ? U_PEND : 0) |
+                ((mode & 2) ? U_QUIT : 0) | (((f.looks && unsure) || pre) && u % g.nk != 0 ? U_UNSURE : 0);
       U.skip = 0;
       U.pad = quit && qfirst ? 1 : 0;  // (a quit unit: its exit is the state before the search that quit)
       units[u] = U;
       counts[u] = n;
-      if ((U.flags & (U_SPEC_CLEAN | U_UNSURE)) != U_SPEC_CLEAN) atomicOr(dirty, 1u);  // the fix pass has work
+      // (the fix pass has work; bit 1: some unit is pending, the wave rounds have work)
+      if ((U.flags & (U_SPEC_CLEAN | U_UNSURE)) != U_SPEC_CLEAN) atomicOr(dirty, (U.flags & U_PEND) ? 3u : 1u);
     }
   }
 }
@@ -1980,6 +2001,10 @@ __global__ void iter_walk_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f
 // VM's lists, pike::Lists, nfa_wave_bytes per wave): f.hot = r.hot = 0, and
 // an all-rows table is read from its global image (as the walker does).
 
+// Rounds of (a wave answers each pending unit's quitting search, the lanes
+// resume) before the waves finish the rest of the pending units themselves.
+constexpr int kWaveRounds = 3;
+
 __device__ __forceinline__ void wave_lists(const NfaDev &nf, uint8_t *mem, pike::Lists &W) {
   const uint32_t N = nf.nleaves;
   W.st[0] = (uint64_t *)mem;
@@ -1991,13 +2016,16 @@ __device__ __forceinline__ void wave_lists(const NfaDev &nf, uint8_t *mem, pike:
   pike::wave_sync();
 }
 
-// The speculation of every U_QUIT unit, resumed at the search that quit
+// The speculation of every U_PEND unit, resumed at the search that quit
 // (the lane pass left the state before it as the unit's exit, its matches so
-// far in the slots, U.pad = that search was the unit's first).
+// far in the slots, U.pad = that search was the unit's first).  STEP: only
+// that search, then the unit goes back to the lanes (U_RESUME) unless it
+// ended; else the rest of the unit on the wave.
+template <bool STEP>
 __global__ __launch_bounds__(64) void iter_wspec_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f,
                                                         RevDfaDev r, NfaDev nf, Unit *units, uint64_t *slots,
                                                         uint32_t *counts, uint32_t *dirty, uint8_t *scratch) {
-  if (gated_off(b)) return;
+  if (gated_off(b) || !(__atomic_load_n(dirty, __ATOMIC_RELAXED) & 2u)) return;  // nothing pending
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_mem[];
   pike::Lists W;
   wave_lists(nf, scratch ? scratch + (size_t)blockIdx.x * nfa_wave_bytes(nf.nleaves) : lds_mem, W);
@@ -2006,7 +2034,7 @@ __global__ __launch_bounds__(64) void iter_wspec_kernel(BatchDev b, Geo g, uint6
   const uint32_t lane = pike::lane_id();
   for (uint64_t u = blockIdx.x; u < nunits; u += gridDim.x) {
     const Unit U = units[u];
-    if (!(U.flags & U_QUIT)) continue;
+    if (!(U.flags & U_PEND)) continue;
     uint64_t h, len, c0, c1;
     const uint8_t *base;
     unit_bounds(b, g, u, &h, &base, &len, &c0, &c1);
@@ -2015,12 +2043,24 @@ __global__ __launch_bounds__(64) void iter_wspec_kernel(BatchDev b, Geo g, uint6
     it.first = U.pad != 0;
     uint32_t n = U.spec_count;
     uint64_t s, e;
-    while (it.next(f, r, f.lds_image, nullptr, base, len, &s, &e, &wc)) {
+    bool more = true;
+    while ((more = it.next(f, r, f.lds_image, nullptr, base, len, &s, &e, &wc))) {
       if (n < g.slots && lane == 0) {
         slots[(u * g.slots + n) * 2] = s;
         slots[(u * g.slots + n) * 2 + 1] = e;
       }
       ++n;
+      if (STEP) break;  // the search that quit is answered: the lanes go on
+    }
+    if (STEP && more) {
+      Unit V = U;
+      V.exit = it.st;
+      V.spec_count = n;
+      V.pad = 0;
+      V.flags = (U.flags & ~(U_PEND | U_UNSURE)) | U_RESUME | U_QUIT |
+                ((U.pad != 0 ? f.looks && it.unsure : (U.flags & U_UNSURE) != 0) ? U_UNSURE : 0);
+      if (lane == 0) units[u] = V;
+      continue;
     }
     const bool pre = f.can_quit == 2 && c0 > 0 && base[c0 - 1] >= 0x80;  // (as iter_spec_burst_kernel)
     const bool unsure = (U.pad != 0 ? f.looks && it.unsure : (U.flags & U_UNSURE) != 0) || pre;
@@ -2771,7 +2811,8 @@ static hipError_t iter_post(const BatchDev &b, const Geo &g, uint64_t nunits, co
   if (!use_lds && (e = scratch_malloc((void **)&wscr, wb * (size_t)wgrid, st)) != hipSuccess) return e;
   const size_t wlds = use_lds ? wb : 0;
   if (wlds > 64 * 1024 &&
-      ((e = allow_lds(iter_wspec_kernel, wlds)) != hipSuccess || (e = allow_lds(iter_wfix_kernel, wlds)) != hipSuccess ||
+      ((e = allow_lds(iter_wspec_kernel<false>, wlds)) != hipSuccess ||
+       (e = allow_lds(iter_wspec_kernel<true>, wlds)) != hipSuccess || (e = allow_lds(iter_wfix_kernel, wlds)) != hipSuccess ||
        (e = allow_lds(iter_wwalk_kernel, wlds)) != hipSuccess || (e = allow_lds(iter_wemit_kernel, wlds)) != hipSuccess)) {
     (void)scratch_free(wscr, st);
     return e;
@@ -2796,9 +2837,22 @@ static hipError_t iter_post_body(const BatchDev &b, const Geo &g, uint64_t nunit
   fw0.hot = 0;
   RevDfaDev rw0 = r;
   rw0.hot = 0;
-  if (wnf) {  // the quit units' speculation, resumed on the wave
-    hipLaunchKernelGGL(iter_wspec_kernel, dim3(wgrid), dim3(64), wlds, st, b, g, nunits, fw0, rw0, *wnf, sc.units,
-                       sc.slots, sc.counts, sc.dirty, wscr);
+  if (wnf) {
+    // The quit units' speculation: a wave answers the search that quit and
+    // hands the unit back to the lanes (kWaveRounds times: most units quit
+    // once or twice, at a cluster of non-ASCII bytes), then the waves finish
+    // what is still pending.
+    if ((e = allow_lds(iter_spec_burst_kernel, lb)) != hipSuccess) return e;
+    for (int k = 0; k < kWaveRounds; ++k) {
+      hipLaunchKernelGGL(iter_wspec_kernel<true>, dim3(wgrid), dim3(64), wlds, st, b, g, nunits, fw0, rw0, *wnf,
+                         sc.units, sc.slots, sc.counts, sc.dirty, wscr);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+      hipLaunchKernelGGL(iter_spec_burst_kernel, dim3(grid), dim3(bs), lb, st, b, g, nunits, f, r, sc.units, sc.slots,
+                         sc.counts, sc.dirty, (uint32_t *)nullptr, 3u);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(iter_wspec_kernel<false>, dim3(wgrid), dim3(64), wlds, st, b, g, nunits, fw0, rw0, *wnf,
+                       sc.units, sc.slots, sc.counts, sc.dirty, wscr);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   if (spn && spn->entry) {
@@ -3190,7 +3244,7 @@ hipError_t launch_find_iter(const BatchDev &b, const FwdDfaDev *f, const RevDfaD
                              units, slots, counts, dirty);
       } else {
         hipLaunchKernelGGL(iter_spec_burst_kernel, dim3(grid), dim3(bs), iter_lds_bytes(*f, r), st, b, g, nunits, *f,
-                           r, units, slots, counts, dirty, qd);
+                           r, units, slots, counts, dirty, qd, wq ? 1u : 0u);
       }
       if (!use_lex) ktimer_end(st);
       if ((e = hipGetLastError()) != hipSuccess) {
