@@ -42,6 +42,7 @@ enum class Knob : int {
   ShadowSync,      // 1: the ASCII shadow's find_iter quit read back, not gated on the device
   IterWave,        // 0: a find_iter DFA quit sends the batch to the wave path, not to the wave-served units
   WaveCu,          // the wave-served units' waves per CU, their Pike VM lists in global scratch
+  WaveSplit,       // 0: those waves' stamps in scratch too, not in the LDS
   kCount
 };
 

@@ -2005,12 +2005,17 @@ __global__ void iter_walk_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f
 // resume) before the waves finish the rest of the pending units themselves.
 constexpr int kWaveRounds = 3;
 
-__device__ __forceinline__ void wave_lists(const NfaDev &nf, uint8_t *mem, pike::Lists &W) {
+// The lists: all in the LDS (no scratch), all in the block's scratch, or
+// (split) the stamps -- read and written at random by append_closure -- in
+// the LDS and the thread lists, written and read in order, in scratch.
+__device__ __forceinline__ void wave_lists(const NfaDev &nf, uint8_t *lds_mem, uint8_t *scratch, uint32_t split,
+                                           pike::Lists &W) {
   const uint32_t N = nf.nleaves;
+  uint8_t *mem = scratch ? scratch + (size_t)blockIdx.x * nfa_wave_bytes(N) : lds_mem;
   W.st[0] = (uint64_t *)mem;
   W.st[1] = W.st[0] + N;
-  W.stamp = (uint32_t *)(W.st[1] + N);
-  W.leaf[0] = W.stamp + N;
+  W.stamp = split ? (uint32_t *)lds_mem : (uint32_t *)(W.st[1] + N);
+  W.leaf[0] = (uint32_t *)(W.st[1] + N) + N;
   W.leaf[1] = W.leaf[0] + N;
   for (uint32_t i = pike::lane_id(); i < N; i += 64) W.stamp[i] = 0xFFFFFFFFu;
   pike::wave_sync();
@@ -2024,11 +2029,11 @@ __device__ __forceinline__ void wave_lists(const NfaDev &nf, uint8_t *mem, pike:
 template <bool STEP>
 __global__ __launch_bounds__(64) void iter_wspec_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f,
                                                         RevDfaDev r, NfaDev nf, Unit *units, uint64_t *slots,
-                                                        uint32_t *counts, uint32_t *dirty, uint8_t *scratch) {
+                                                        uint32_t *counts, uint32_t *dirty, uint8_t *scratch, uint32_t split) {
   if (gated_off(b) || !(__atomic_load_n(dirty, __ATOMIC_RELAXED) & 2u)) return;  // nothing pending
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_mem[];
   pike::Lists W;
-  wave_lists(nf, scratch ? scratch + (size_t)blockIdx.x * nfa_wave_bytes(nf.nleaves) : lds_mem, W);
+  wave_lists(nf, lds_mem, scratch, split, W);
   pike::TagGen tg;
   const WaveCtx wc{&nf, &W, &tg};
   const uint32_t lane = pike::lane_id();
@@ -2084,11 +2089,11 @@ __global__ __launch_bounds__(64) void iter_wspec_kernel(BatchDev b, Geo g, uint6
 __global__ __launch_bounds__(64) void iter_wfix_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
                                                        NfaDev nf, Unit *units, uint32_t *counts, const uint64_t *slots,
                                                        uint64_t *queue, unsigned long long *qlen, const uint32_t *dirty,
-                                                       uint8_t *scratch) {
+                                                       uint8_t *scratch, uint32_t split) {
   if (gated_off(b) || *dirty == 0) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_mem[];
   pike::Lists W;
-  wave_lists(nf, scratch ? scratch + (size_t)blockIdx.x * nfa_wave_bytes(nf.nleaves) : lds_mem, W);
+  wave_lists(nf, lds_mem, scratch, split, W);
   pike::TagGen tg;
   const WaveCtx wc{&nf, &W, &tg};
   for (uint64_t u = blockIdx.x; u + 1 < nunits; u += gridDim.x) {
@@ -2107,11 +2112,11 @@ __global__ __launch_bounds__(64) void iter_wfix_kernel(BatchDev b, Geo g, uint64
 // The walker with the whole wave (one block of 64).
 __global__ __launch_bounds__(64) void iter_wwalk_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
                                                         NfaDev nf, Unit *units, uint32_t *counts, const uint64_t *slots,
-                                                        uint64_t *queue, unsigned long long *qlen, uint8_t *scratch) {
+                                                        uint64_t *queue, unsigned long long *qlen, uint8_t *scratch, uint32_t split) {
   if (gated_off(b) || blockIdx.x != 0) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_mem[];
   pike::Lists W;
-  wave_lists(nf, scratch ? scratch : lds_mem, W);
+  wave_lists(nf, lds_mem, scratch, split, W);
   pike::TagGen tg;
   const WaveCtx wc{&nf, &W, &tg};
   walk_body(b, g, nunits, f, r, units, counts, slots, queue, qlen, &wc);
@@ -2120,11 +2125,11 @@ __global__ __launch_bounds__(64) void iter_wwalk_kernel(BatchDev b, Geo g, uint6
 // emit_body's re-runs of U_QUIT units (from the unit's entry, cnt matches).
 __global__ __launch_bounds__(64) void iter_wemit_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
                                                         NfaDev nf, const Unit *units, const uint64_t *off,
-                                                        uint64_t *out, uint64_t cap, uint8_t *scratch) {
+                                                        uint64_t *out, uint64_t cap, uint8_t *scratch, uint32_t split) {
   if (gated_off(b)) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_mem[];
   pike::Lists W;
-  wave_lists(nf, scratch ? scratch + (size_t)blockIdx.x * nfa_wave_bytes(nf.nleaves) : lds_mem, W);
+  wave_lists(nf, lds_mem, scratch, split, W);
   pike::TagGen tg;
   const WaveCtx wc{&nf, &W, &tg};
   const uint64_t obase = off[0];
@@ -2788,12 +2793,12 @@ static bool sa_tile_ok(const BatchDev &b, const Geo &g) {
 static hipError_t iter_post_body(const BatchDev &b, const Geo &g, uint64_t nunits, const FwdDfaDev &f,
                                  const RevDfaDev &r, const IterScratch &sc, const IterOut &o, const IterSpan *spn,
                                  hipStream_t st, int cus, bool dense, const NfaDev *wnf, uint8_t *wscr, size_t wlds,
-                                 int wgrid);
+                                 int wgrid, uint32_t wsplit);
 
 static hipError_t iter_post(const BatchDev &b, const Geo &g, uint64_t nunits, const FwdDfaDev &f, const RevDfaDev &r,
                             const IterScratch &sc, const IterOut &o, const IterSpan *spn, hipStream_t st, int cus,
                             bool dense = false, const NfaDev *wnf = nullptr) {
-  if (!wnf) return iter_post_body(b, g, nunits, f, r, sc, o, spn, st, cus, dense, nullptr, nullptr, 0, 0);
+  if (!wnf) return iter_post_body(b, g, nunits, f, r, sc, o, spn, st, cus, dense, nullptr, nullptr, 0, 0, 0);
   // one wave per block, the Pike VM's lists in LDS (else global scratch)
   const size_t wb = nfa_wave_bytes(wnf->nleaves);
   // Lists in LDS where 16 waves per CU fit, else in global scratch with 16
@@ -2802,14 +2807,19 @@ static hipError_t iter_post(const BatchDev &b, const Geo &g, uint64_t nunits, co
   // lists (\b\w+n\b over 1 GiB of sherlock as it is, 2460 NFA leaves:
   // 2 waves per CU in LDS 186 ms, 4 / 8 / 16 in scratch 134 / 112 / 102 ms,
   // profiles/r06_wave_iter_bench.jsonl).  Knob wave_cu: waves per CU (A/B).
+  // ... and the stamps alone in the LDS where 16 waves' stamps fit (split;
+  // knob wave_split=0: all in scratch)
   const long long kw = knob(Knob::WaveCu);
   const int lds_cu = (int)std::min<size_t>(32, (160u * 1024u) / wb);
   const bool use_lds = wb <= kNfaLdsMax && kw <= 0 && lds_cu >= 16;
-  const int wgrid = grid_cap(nunits, 1, cus, use_lds ? lds_cu : kw > 0 ? (int)std::min<long long>(kw, 32) : 16);
+  const int wcu = use_lds ? lds_cu : kw > 0 ? (int)std::min<long long>(kw, 32) : 16;
+  const size_t sb = ((size_t)wnf->nleaves * 4 + 255) & ~(size_t)255;
+  const uint32_t wsplit = !use_lds && knob(Knob::WaveSplit) != 0 && sb * (size_t)wcu <= 160u * 1024u ? 1u : 0u;
+  const int wgrid = grid_cap(nunits, 1, cus, wcu);
   uint8_t *wscr = nullptr;
   hipError_t e = hipSuccess;
   if (!use_lds && (e = scratch_malloc((void **)&wscr, wb * (size_t)wgrid, st)) != hipSuccess) return e;
-  const size_t wlds = use_lds ? wb : 0;
+  const size_t wlds = use_lds ? wb : wsplit ? sb : 0;
   if (wlds > 64 * 1024 &&
       ((e = allow_lds(iter_wspec_kernel<false>, wlds)) != hipSuccess ||
        (e = allow_lds(iter_wspec_kernel<true>, wlds)) != hipSuccess || (e = allow_lds(iter_wfix_kernel, wlds)) != hipSuccess ||
@@ -2817,7 +2827,7 @@ static hipError_t iter_post(const BatchDev &b, const Geo &g, uint64_t nunits, co
     (void)scratch_free(wscr, st);
     return e;
   }
-  e = iter_post_body(b, g, nunits, f, r, sc, o, spn, st, cus, dense, wnf, wscr, wlds, wgrid);
+  e = iter_post_body(b, g, nunits, f, r, sc, o, spn, st, cus, dense, wnf, wscr, wlds, wgrid, wsplit);
   const hipError_t e2 = scratch_free(wscr, st);
   return e != hipSuccess ? e : e2;
 }
@@ -2825,7 +2835,7 @@ static hipError_t iter_post(const BatchDev &b, const Geo &g, uint64_t nunits, co
 static hipError_t iter_post_body(const BatchDev &b, const Geo &g, uint64_t nunits, const FwdDfaDev &f,
                                  const RevDfaDev &r, const IterScratch &sc, const IterOut &o, const IterSpan *spn,
                                  hipStream_t st, int cus, bool dense, const NfaDev *wnf, uint8_t *wscr, size_t wlds,
-                                 int wgrid) {
+                                 int wgrid, uint32_t wsplit) {
   hipError_t e;
   const int bs = iter_bs();
   const size_t lb = iter_lds_bytes(f, r);
@@ -2845,14 +2855,14 @@ static hipError_t iter_post_body(const BatchDev &b, const Geo &g, uint64_t nunit
     if ((e = allow_lds(iter_spec_burst_kernel, lb)) != hipSuccess) return e;
     for (int k = 0; k < kWaveRounds; ++k) {
       hipLaunchKernelGGL(iter_wspec_kernel<true>, dim3(wgrid), dim3(64), wlds, st, b, g, nunits, fw0, rw0, *wnf,
-                         sc.units, sc.slots, sc.counts, sc.dirty, wscr);
+                         sc.units, sc.slots, sc.counts, sc.dirty, wscr, wsplit);
       if ((e = hipGetLastError()) != hipSuccess) return e;
       hipLaunchKernelGGL(iter_spec_burst_kernel, dim3(grid), dim3(bs), lb, st, b, g, nunits, f, r, sc.units, sc.slots,
                          sc.counts, sc.dirty, (uint32_t *)nullptr, 3u);
       if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     hipLaunchKernelGGL(iter_wspec_kernel<false>, dim3(wgrid), dim3(64), wlds, st, b, g, nunits, fw0, rw0, *wnf,
-                       sc.units, sc.slots, sc.counts, sc.dirty, wscr);
+                       sc.units, sc.slots, sc.counts, sc.dirty, wscr, wsplit);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   if (spn && spn->entry) {
@@ -2870,10 +2880,10 @@ static hipError_t iter_post_body(const BatchDev &b, const Geo &g, uint64_t nunit
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (wnf) {
       hipLaunchKernelGGL(iter_wfix_kernel, dim3(wgrid), dim3(64), wlds, st, b, g, nunits, fw0, rw0, *wnf, sc.units,
-                         sc.counts, (const uint64_t *)sc.slots, sc.queue, sc.qlen, (const uint32_t *)sc.dirty, wscr);
+                         sc.counts, (const uint64_t *)sc.slots, sc.queue, sc.qlen, (const uint32_t *)sc.dirty, wscr, wsplit);
       if ((e = hipGetLastError()) != hipSuccess) return e;
       hipLaunchKernelGGL(iter_wwalk_kernel, dim3(1), dim3(64), wlds, st, b, g, nunits, fw0, rw0, *wnf, sc.units,
-                         sc.counts, (const uint64_t *)sc.slots, sc.queue, sc.qlen, wscr);
+                         sc.counts, (const uint64_t *)sc.slots, sc.queue, sc.qlen, wscr, wsplit);
     } else {
       hipLaunchKernelGGL(iter_walk_kernel, dim3(1), dim3(64), 0, st, b, g, nunits, fw0, rw0, sc.units, sc.counts,
                          (const uint64_t *)sc.slots, sc.queue, sc.qlen);
@@ -2895,7 +2905,7 @@ static hipError_t iter_post_body(const BatchDev &b, const Geo &g, uint64_t nunit
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if (wnf) {
     hipLaunchKernelGGL(iter_wemit_kernel, dim3(wgrid), dim3(64), wlds, st, b, g, nunits, fw0, rw0, *wnf,
-                       (const Unit *)sc.units, (const uint64_t *)sc.off, o.matches, o.cap, wscr);
+                       (const Unit *)sc.units, (const uint64_t *)sc.off, o.matches, o.cap, wscr, wsplit);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   hipLaunchKernelGGL(iter_counts_kernel, dim3(grid_cap(b.count, 256, cus, 4)), dim3(256), 0, st, b.count, g.nk,
