@@ -443,6 +443,8 @@ void fix_nfa(NfaDev *n, uint8_t *base, const NfaOffsets &o, const NfaTables &nt,
   n->single = single ? 1 : 0;
   n->looks = nt.looks_used;
   n->unicode_wb = nt.unicode_wb ? 1 : 0;
+  n->ncl_off = (uint32_t)nt.cl_off.size();
+  n->nentries = (uint32_t)nt.entries.size();
 }
 
 bool upload_blob(const Blob &b, DevTables *t, std::string *err) {

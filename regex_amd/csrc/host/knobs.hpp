@@ -43,6 +43,7 @@ enum class Knob : int {
   IterWave,        // 0: a find_iter DFA quit sends the batch to the wave path, not to the wave-served units
   WaveCu,          // the wave-served units' waves per CU, their Pike VM lists in global scratch
   WaveSplit,       // 0: those waves' stamps in scratch too, not in the LDS
+  WaveTables,      // 0: no NFA tables staged in the LDS for those waves
   kCount
 };
 

@@ -234,6 +234,7 @@ struct NfaDev {
   uint32_t perlw_n;
   uint32_t nleaves, root, nmatch;
   uint32_t anchored, single, looks, unicode_wb;
+  uint32_t ncl_off, nentries;  // cl_off's and entries' lengths (the wave kernels stage them in LDS)
   const uint32_t *save_off;   // per entry: CSR offsets into save_slot (Saves on its path)
   const uint16_t *save_slot;
 };

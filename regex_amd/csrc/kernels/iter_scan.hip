@@ -2005,19 +2005,60 @@ __global__ void iter_walk_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f
 // resume) before the waves finish the rest of the pending units themselves.
 constexpr int kWaveRounds = 3;
 
-// The lists: all in the LDS (no scratch), all in the block's scratch, or
-// (split) the stamps -- read and written at random by append_closure -- in
-// the LDS and the thread lists, written and read in order, in scratch.
-__device__ __forceinline__ void wave_lists(const NfaDev &nf, uint8_t *lds_mem, uint8_t *scratch, uint32_t split,
-                                           pike::Lists &W) {
-  const uint32_t N = nf.nleaves;
-  uint8_t *mem = scratch ? scratch + (size_t)blockIdx.x * nfa_wave_bytes(N) : lds_mem;
-  W.st[0] = (uint64_t *)mem;
-  W.st[1] = W.st[0] + N;
-  W.stamp = split ? (uint32_t *)lds_mem : (uint32_t *)(W.st[1] + N);
-  W.leaf[0] = (uint32_t *)(W.st[1] + N) + N;
-  W.leaf[1] = W.leaf[0] + N;
-  for (uint32_t i = pike::lane_id(); i < N; i += 64) W.stamp[i] = 0xFFFFFFFFu;
+// Where a wave keeps the Pike VM's working set (iter_post picks):
+//  kWaveLds    one wave per block, stamps and thread lists in the LDS;
+//  kWaveSplit  one wave per block, the stamps -- read and written at random
+//              by append_closure -- in the LDS, the thread lists (written and
+//              read in order) in the wave's scratch;
+//  kWaveTables several waves per block sharing the NFA's tables (leaves,
+//              closure offsets and entries, the Unicode word ranges) staged
+//              in the LDS, each with its stamps there and its lists in
+//              scratch: every step of the Pike VM reads those tables.
+enum : uint32_t { kWaveLds = 0, kWaveSplit = 1, kWaveScratch = 2, kWaveTables = 3 };
+
+__host__ __device__ inline size_t wave_table_bytes(const NfaDev &nf) {
+  return (((size_t)nf.nentries * 8 + (size_t)nf.nleaves * 12 + (size_t)nf.ncl_off * 4 + (size_t)nf.perlw_n * 8) + 255) &
+         ~(size_t)255;
+}
+__host__ __device__ inline size_t wave_stamp_bytes(const NfaDev &nf) { return ((size_t)nf.nleaves * 4 + 255) & ~(size_t)255; }
+
+struct WaveSetup {
+  NfaDev nf;  // kWaveTables: its table pointers into the LDS
+  pike::Lists W;
+  uint64_t wave, nwaves;
+};
+
+__device__ __forceinline__ void wave_setup(const NfaDev &nf0, uint8_t *lds_mem, uint8_t *scratch, uint32_t mode,
+                                           WaveSetup &S) {
+  const uint32_t wpb = blockDim.x >> 6, wib = threadIdx.x >> 6;
+  S.wave = (uint64_t)blockIdx.x * wpb + wib;
+  S.nwaves = (uint64_t)gridDim.x * wpb;
+  S.nf = nf0;
+  const uint32_t N = nf0.nleaves;
+  uint8_t *stamps = lds_mem;
+  if (mode == kWaveTables) {
+    uint32_t *d = (uint32_t *)lds_mem;
+    auto stage = [&](const void *src, uint32_t words) {
+      const uint32_t *q = (const uint32_t *)src;
+      for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) d[i] = q[i];
+      uint32_t *at = d;
+      d += words;
+      return (const void *)at;
+    };
+    S.nf.entries = (const uint2 *)stage(nf0.entries, 2 * nf0.nentries);
+    S.nf.leaves = (const uint32_t *)stage(nf0.leaves, 3 * N);
+    S.nf.cl_off = (const uint32_t *)stage(nf0.cl_off, nf0.ncl_off);
+    S.nf.perlw = (const uint32_t *)stage(nf0.perlw, 2 * nf0.perlw_n);
+    __syncthreads();
+    stamps = lds_mem + wave_table_bytes(nf0) + (size_t)wib * wave_stamp_bytes(nf0);
+  }
+  uint8_t *mem = scratch ? scratch + (size_t)S.wave * nfa_wave_bytes(N) : lds_mem;
+  S.W.st[0] = (uint64_t *)mem;
+  S.W.st[1] = S.W.st[0] + N;
+  S.W.stamp = mode == kWaveLds || mode == kWaveScratch ? (uint32_t *)(S.W.st[1] + N) : (uint32_t *)stamps;
+  S.W.leaf[0] = (uint32_t *)(S.W.st[1] + N) + N;
+  S.W.leaf[1] = S.W.leaf[0] + N;
+  for (uint32_t i = pike::lane_id(); i < N; i += 64) S.W.stamp[i] = 0xFFFFFFFFu;
   pike::wave_sync();
 }
 
@@ -2027,17 +2068,17 @@ __device__ __forceinline__ void wave_lists(const NfaDev &nf, uint8_t *lds_mem, u
 // that search, then the unit goes back to the lanes (U_RESUME) unless it
 // ended; else the rest of the unit on the wave.
 template <bool STEP>
-__global__ __launch_bounds__(64) void iter_wspec_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f,
+__global__ __launch_bounds__(512) void iter_wspec_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f,
                                                         RevDfaDev r, NfaDev nf, Unit *units, uint64_t *slots,
-                                                        uint32_t *counts, uint32_t *dirty, uint8_t *scratch, uint32_t split) {
+                                                        uint32_t *counts, uint32_t *dirty, uint8_t *scratch, uint32_t split) {  // split: kWave*
   if (gated_off(b) || !(__atomic_load_n(dirty, __ATOMIC_RELAXED) & 2u)) return;  // nothing pending
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_mem[];
-  pike::Lists W;
-  wave_lists(nf, lds_mem, scratch, split, W);
+  WaveSetup S;
+  wave_setup(nf, lds_mem, scratch, split, S);
   pike::TagGen tg;
-  const WaveCtx wc{&nf, &W, &tg};
+  const WaveCtx wc{&S.nf, &S.W, &tg};
   const uint32_t lane = pike::lane_id();
-  for (uint64_t u = blockIdx.x; u < nunits; u += gridDim.x) {
+  for (uint64_t u = S.wave; u < nunits; u += S.nwaves) {
     const Unit U = units[u];
     if (!(U.flags & U_PEND)) continue;
     uint64_t h, len, c0, c1;
@@ -2086,17 +2127,17 @@ __global__ __launch_bounds__(64) void iter_wspec_kernel(BatchDev b, Geo g, uint6
 
 // fix_body's repairs of the units the lane pass left (U_QUIT: a quit in the
 // speculation or in the lane repair); a changed exit is queued for the walker.
-__global__ __launch_bounds__(64) void iter_wfix_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
+__global__ __launch_bounds__(512) void iter_wfix_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
                                                        NfaDev nf, Unit *units, uint32_t *counts, const uint64_t *slots,
                                                        uint64_t *queue, unsigned long long *qlen, const uint32_t *dirty,
-                                                       uint8_t *scratch, uint32_t split) {
+                                                       uint8_t *scratch, uint32_t split) {  // split: kWave*
   if (gated_off(b) || *dirty == 0) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_mem[];
-  pike::Lists W;
-  wave_lists(nf, lds_mem, scratch, split, W);
+  WaveSetup S;
+  wave_setup(nf, lds_mem, scratch, split, S);
   pike::TagGen tg;
-  const WaveCtx wc{&nf, &W, &tg};
-  for (uint64_t u = blockIdx.x; u + 1 < nunits; u += gridDim.x) {
+  const WaveCtx wc{&S.nf, &S.W, &tg};
+  for (uint64_t u = S.wave; u + 1 < nunits; u += S.nwaves) {
     const uint32_t fn = units[u + 1].flags;
     const bool need = (u + 1) % g.nk != 0 && (fn & U_QUIT) &&
                       (!(units[u].flags & U_SPEC_CLEAN) || (fn & U_UNSURE));
@@ -2112,28 +2153,28 @@ __global__ __launch_bounds__(64) void iter_wfix_kernel(BatchDev b, Geo g, uint64
 // The walker with the whole wave (one block of 64).
 __global__ __launch_bounds__(64) void iter_wwalk_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
                                                         NfaDev nf, Unit *units, uint32_t *counts, const uint64_t *slots,
-                                                        uint64_t *queue, unsigned long long *qlen, uint8_t *scratch, uint32_t split) {
+                                                        uint64_t *queue, unsigned long long *qlen, uint8_t *scratch, uint32_t split) {  // split: kWave*
   if (gated_off(b) || blockIdx.x != 0) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_mem[];
-  pike::Lists W;
-  wave_lists(nf, lds_mem, scratch, split, W);
+  WaveSetup S;
+  wave_setup(nf, lds_mem, scratch, split, S);
   pike::TagGen tg;
-  const WaveCtx wc{&nf, &W, &tg};
+  const WaveCtx wc{&S.nf, &S.W, &tg};
   walk_body(b, g, nunits, f, r, units, counts, slots, queue, qlen, &wc);
 }
 
 // emit_body's re-runs of U_QUIT units (from the unit's entry, cnt matches).
-__global__ __launch_bounds__(64) void iter_wemit_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
+__global__ __launch_bounds__(512) void iter_wemit_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
                                                         NfaDev nf, const Unit *units, const uint64_t *off,
-                                                        uint64_t *out, uint64_t cap, uint8_t *scratch, uint32_t split) {
+                                                        uint64_t *out, uint64_t cap, uint8_t *scratch, uint32_t split) {  // split: kWave*
   if (gated_off(b)) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_mem[];
-  pike::Lists W;
-  wave_lists(nf, lds_mem, scratch, split, W);
+  WaveSetup S;
+  wave_setup(nf, lds_mem, scratch, split, S);
   pike::TagGen tg;
-  const WaveCtx wc{&nf, &W, &tg};
+  const WaveCtx wc{&S.nf, &S.W, &tg};
   const uint64_t obase = off[0];
-  for (uint64_t u = blockIdx.x; u < nunits; u += gridDim.x) {
+  for (uint64_t u = S.wave; u < nunits; u += S.nwaves) {
     const uint32_t fl = units[u].flags;
     if (!(fl & U_QUIT)) continue;
     const uint64_t o0 = off[u] - obase, cnt = off[u + 1] - off[u];
@@ -2789,37 +2830,54 @@ static bool sa_tile_ok(const BatchDev &b, const Geo &g) {
 // The passes after the speculative one (same for every engine): a span's
 // entry, the repairs (fix, walk), the output offsets, emission, per-haystack
 // counts and a span's exit.
-// wnf: the wave-served iteration (U_QUIT units on the Pike VM, above).
+// wnf: the wave-served iteration (U_QUIT units on the Pike VM, above):
+// its blocks, threads per block, LDS bytes (and the walker's), kWave* mode.
+struct WaveGeo {
+  int grid = 0, threads = 64;
+  size_t lds = 0, lds1 = 0;
+  uint32_t mode = 0;
+};
 static hipError_t iter_post_body(const BatchDev &b, const Geo &g, uint64_t nunits, const FwdDfaDev &f,
                                  const RevDfaDev &r, const IterScratch &sc, const IterOut &o, const IterSpan *spn,
-                                 hipStream_t st, int cus, bool dense, const NfaDev *wnf, uint8_t *wscr, size_t wlds,
-                                 int wgrid, uint32_t wsplit);
+                                 hipStream_t st, int cus, bool dense, const NfaDev *wnf, uint8_t *wscr,
+                                 const WaveGeo &wg);
 
 static hipError_t iter_post(const BatchDev &b, const Geo &g, uint64_t nunits, const FwdDfaDev &f, const RevDfaDev &r,
                             const IterScratch &sc, const IterOut &o, const IterSpan *spn, hipStream_t st, int cus,
                             bool dense = false, const NfaDev *wnf = nullptr) {
-  if (!wnf) return iter_post_body(b, g, nunits, f, r, sc, o, spn, st, cus, dense, nullptr, nullptr, 0, 0, 0);
+  if (!wnf) return iter_post_body(b, g, nunits, f, r, sc, o, spn, st, cus, dense, nullptr, nullptr, WaveGeo{});
   // one wave per block, the Pike VM's lists in LDS (else global scratch)
   const size_t wb = nfa_wave_bytes(wnf->nleaves);
-  // Lists in LDS where 16 waves per CU fit, else in global scratch with 16
-  // waves per CU: the waves' work is latency-bound chains (global-table DFA
-  // steps, the Pike VM's list walks), and more waves in flight beat LDS
-  // lists (\b\w+n\b over 1 GiB of sherlock as it is, 2460 NFA leaves:
-  // 2 waves per CU in LDS 186 ms, 4 / 8 / 16 in scratch 134 / 112 / 102 ms,
-  // profiles/r06_wave_iter_bench.jsonl).  Knob wave_cu: waves per CU (A/B).
-  // ... and the stamps alone in the LDS where 16 waves' stamps fit (split;
-  // knob wave_split=0: all in scratch)
+  // Lists in LDS where 16 waves per CU fit (kWaveLds).  Else 8 waves per
+  // block share the NFA's tables in the LDS, each with its stamps there
+  // (kWaveTables), where that fits; else stamps alone in the LDS at 16 waves
+  // per CU (kWaveSplit), else all in scratch.  The waves' work is chains of
+  // dependent loads, so waves in flight and LDS latency both count
+  // (\b\w+n\b over 1 GiB of sherlock as it is, 2460 NFA leaves: 2 waves
+  // per CU in LDS 186 ms; in scratch at 4 / 8 / 16 waves per CU 134 / 112 /
+  // 102 ms; profiles/r06_wave_iter_bench.jsonl).  Knobs: wave_cu (waves per
+  // CU, all in scratch), wave_split (0: no LDS stamps), wave_tables (0).
   const long long kw = knob(Knob::WaveCu);
   const int lds_cu = (int)std::min<size_t>(32, (160u * 1024u) / wb);
-  const bool use_lds = wb <= kNfaLdsMax && kw <= 0 && lds_cu >= 16;
-  const int wcu = use_lds ? lds_cu : kw > 0 ? (int)std::min<long long>(kw, 32) : 16;
-  const size_t sb = ((size_t)wnf->nleaves * 4 + 255) & ~(size_t)255;
-  const uint32_t wsplit = !use_lds && knob(Knob::WaveSplit) != 0 && sb * (size_t)wcu <= 160u * 1024u ? 1u : 0u;
-  const int wgrid = grid_cap(nunits, 1, cus, wcu);
+  const size_t tb = wave_table_bytes(*wnf), sb = wave_stamp_bytes(*wnf);
+  constexpr int kWpb = 8;
+  uint32_t mode;
+  int wcu, wpb = 1;
+  if (wb <= kNfaLdsMax && kw <= 0 && lds_cu >= 16) {
+    mode = kWaveLds, wcu = lds_cu;
+  } else if (kw <= 0 && knob(Knob::WaveTables) != 0 && tb + kWpb * sb <= 160u * 1024u) {
+    mode = kWaveTables, wcu = kWpb, wpb = kWpb;
+  } else {
+    wcu = kw > 0 ? (int)std::min<long long>(kw, 32) : 16;
+    mode = knob(Knob::WaveSplit) != 0 && sb * (size_t)wcu <= 160u * 1024u ? kWaveSplit : kWaveScratch;
+  }
+  const int wgrid = mode == kWaveTables ? std::max<int>(1, std::min<int>(cus, (int)((nunits + wpb - 1) / wpb)))
+                                        : grid_cap(nunits, 1, cus, wcu);
   uint8_t *wscr = nullptr;
   hipError_t e = hipSuccess;
-  if (!use_lds && (e = scratch_malloc((void **)&wscr, wb * (size_t)wgrid, st)) != hipSuccess) return e;
-  const size_t wlds = use_lds ? wb : wsplit ? sb : 0;
+  if (mode != kWaveLds && (e = scratch_malloc((void **)&wscr, wb * (size_t)wgrid * wpb, st)) != hipSuccess) return e;
+  const size_t wlds = mode == kWaveLds ? wb : mode == kWaveSplit ? sb : mode == kWaveTables ? tb + wpb * sb : 0;
+  const size_t wlds1 = mode == kWaveTables ? tb + sb : wlds;  // the walker: one wave
   if (wlds > 64 * 1024 &&
       ((e = allow_lds(iter_wspec_kernel<false>, wlds)) != hipSuccess ||
        (e = allow_lds(iter_wspec_kernel<true>, wlds)) != hipSuccess || (e = allow_lds(iter_wfix_kernel, wlds)) != hipSuccess ||
@@ -2827,15 +2885,16 @@ static hipError_t iter_post(const BatchDev &b, const Geo &g, uint64_t nunits, co
     (void)scratch_free(wscr, st);
     return e;
   }
-  e = iter_post_body(b, g, nunits, f, r, sc, o, spn, st, cus, dense, wnf, wscr, wlds, wgrid, wsplit);
+  const WaveGeo wg{wgrid, wpb * 64, wlds, wlds1, mode};
+  e = iter_post_body(b, g, nunits, f, r, sc, o, spn, st, cus, dense, wnf, wscr, wg);
   const hipError_t e2 = scratch_free(wscr, st);
   return e != hipSuccess ? e : e2;
 }
 
 static hipError_t iter_post_body(const BatchDev &b, const Geo &g, uint64_t nunits, const FwdDfaDev &f,
                                  const RevDfaDev &r, const IterScratch &sc, const IterOut &o, const IterSpan *spn,
-                                 hipStream_t st, int cus, bool dense, const NfaDev *wnf, uint8_t *wscr, size_t wlds,
-                                 int wgrid, uint32_t wsplit) {
+                                 hipStream_t st, int cus, bool dense, const NfaDev *wnf, uint8_t *wscr,
+                                 const WaveGeo &wg) {
   hipError_t e;
   const int bs = iter_bs();
   const size_t lb = iter_lds_bytes(f, r);
@@ -2854,15 +2913,15 @@ static hipError_t iter_post_body(const BatchDev &b, const Geo &g, uint64_t nunit
     // what is still pending.
     if ((e = allow_lds(iter_spec_burst_kernel, lb)) != hipSuccess) return e;
     for (int k = 0; k < kWaveRounds; ++k) {
-      hipLaunchKernelGGL(iter_wspec_kernel<true>, dim3(wgrid), dim3(64), wlds, st, b, g, nunits, fw0, rw0, *wnf,
-                         sc.units, sc.slots, sc.counts, sc.dirty, wscr, wsplit);
+      hipLaunchKernelGGL(iter_wspec_kernel<true>, dim3(wg.grid), dim3(wg.threads), wg.lds, st, b, g, nunits, fw0, rw0, *wnf,
+                         sc.units, sc.slots, sc.counts, sc.dirty, wscr, wg.mode);
       if ((e = hipGetLastError()) != hipSuccess) return e;
       hipLaunchKernelGGL(iter_spec_burst_kernel, dim3(grid), dim3(bs), lb, st, b, g, nunits, f, r, sc.units, sc.slots,
                          sc.counts, sc.dirty, (uint32_t *)nullptr, 3u);
       if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(iter_wspec_kernel<false>, dim3(wgrid), dim3(64), wlds, st, b, g, nunits, fw0, rw0, *wnf,
-                       sc.units, sc.slots, sc.counts, sc.dirty, wscr, wsplit);
+    hipLaunchKernelGGL(iter_wspec_kernel<false>, dim3(wg.grid), dim3(wg.threads), wg.lds, st, b, g, nunits, fw0, rw0, *wnf,
+                       sc.units, sc.slots, sc.counts, sc.dirty, wscr, wg.mode);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   if (spn && spn->entry) {
@@ -2879,11 +2938,11 @@ static hipError_t iter_post_body(const BatchDev &b, const Geo &g, uint64_t nunit
                        (const uint64_t *)sc.slots, sc.queue, sc.qlen, (const uint32_t *)sc.dirty);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (wnf) {
-      hipLaunchKernelGGL(iter_wfix_kernel, dim3(wgrid), dim3(64), wlds, st, b, g, nunits, fw0, rw0, *wnf, sc.units,
-                         sc.counts, (const uint64_t *)sc.slots, sc.queue, sc.qlen, (const uint32_t *)sc.dirty, wscr, wsplit);
+      hipLaunchKernelGGL(iter_wfix_kernel, dim3(wg.grid), dim3(wg.threads), wg.lds, st, b, g, nunits, fw0, rw0, *wnf, sc.units,
+                         sc.counts, (const uint64_t *)sc.slots, sc.queue, sc.qlen, (const uint32_t *)sc.dirty, wscr, wg.mode);
       if ((e = hipGetLastError()) != hipSuccess) return e;
-      hipLaunchKernelGGL(iter_wwalk_kernel, dim3(1), dim3(64), wlds, st, b, g, nunits, fw0, rw0, *wnf, sc.units,
-                         sc.counts, (const uint64_t *)sc.slots, sc.queue, sc.qlen, wscr, wsplit);
+      hipLaunchKernelGGL(iter_wwalk_kernel, dim3(1), dim3(64), wg.lds1, st, b, g, nunits, fw0, rw0, *wnf, sc.units,
+                         sc.counts, (const uint64_t *)sc.slots, sc.queue, sc.qlen, wscr, wg.mode);
     } else {
       hipLaunchKernelGGL(iter_walk_kernel, dim3(1), dim3(64), 0, st, b, g, nunits, fw0, rw0, sc.units, sc.counts,
                          (const uint64_t *)sc.slots, sc.queue, sc.qlen);
@@ -2904,8 +2963,8 @@ static hipError_t iter_post_body(const BatchDev &b, const Geo &g, uint64_t nunit
                      o.matches, o.cap, dense ? 0 : 1);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if (wnf) {
-    hipLaunchKernelGGL(iter_wemit_kernel, dim3(wgrid), dim3(64), wlds, st, b, g, nunits, fw0, rw0, *wnf,
-                       (const Unit *)sc.units, (const uint64_t *)sc.off, o.matches, o.cap, wscr, wsplit);
+    hipLaunchKernelGGL(iter_wemit_kernel, dim3(wg.grid), dim3(wg.threads), wg.lds, st, b, g, nunits, fw0, rw0, *wnf,
+                       (const Unit *)sc.units, (const uint64_t *)sc.off, o.matches, o.cap, wscr, wg.mode);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   hipLaunchKernelGGL(iter_counts_kernel, dim3(grid_cap(b.count, 256, cus, 4)), dim3(256), 0, st, b.count, g.nk,
