@@ -123,8 +123,14 @@ struct Lists {
 
 // Appends closure `cid` (filtered by the assertions `holds`) to a thread
 // list in priority order, skipping leaves already in it (stamp == tag).
+// nb: the byte the list's threads will step on (0x100 at the end of the
+// text): a Bytes leaf that does not take it would die at that step, so it
+// is not added (Match leaves always are) -- the order of the survivors, and
+// so the leftmost-first priorities, are unchanged.  Inside a word of
+// Unicode \w+ this keeps one or two threads of the class's hundreds of
+// alternatives in the list instead of all of them.
 __device__ uint32_t append_closure(const NfaDev &nf, uint32_t cid, uint32_t holds, uint64_t stv, uint32_t *stamp,
-                                   uint32_t tag, uint32_t *lleaf, uint64_t *lst, uint32_t cnt) {
+                                   uint32_t tag, uint32_t *lleaf, uint64_t *lst, uint32_t cnt, uint32_t nb) {
   const uint32_t o0 = nf.cl_off[cid], o1 = nf.cl_off[cid + 1];
   const uint32_t lane = lane_id();
   for (uint32_t k0 = o0; k0 < o1; k0 += 64) {
@@ -140,6 +146,10 @@ __device__ uint32_t append_closure(const NfaDev &nf, uint32_t cid, uint32_t hold
         uint2 q = nf.entries[o0 + pv - 1];
         if (((q.y & 0xFF) & ~holds) == 0) pass = false;
         pv = q.y >> 8;
+      }
+      if (pass) {
+        const uint32_t w0 = nf.leaves[3 * leaf];
+        if ((w0 & 0xFF) == 0) pass = nb >= ((w0 >> 8) & 0xFF) && nb <= ((w0 >> 16) & 0xFF);
       }
       if (pass) pass = stamp[leaf] != tag;
     }
@@ -192,10 +202,12 @@ __device__ void pike_one(const NfaDev &nf, Lists &W, TagGen &tg, const uint8_t *
   while (true) {
     if (nc == 0 && ((matched && nf.single) || all_matched || (at != 0 && nf.anchored) || at >= cut)) break;
     if (at < cut && (nc == 0 || (!nf.anchored && !all_matched)))
-      nc = append_closure(nf, nf.root, look_holds(text, len, at, nf), at, W.stamp, ctag, W.leaf[c], W.st[c], nc);
+      nc = append_closure(nf, nf.root, look_holds(text, len, at, nf), at, W.stamp, ctag, W.leaf[c], W.st[c], nc,
+                          at < len ? text[at] : 0x100u);
     const uint32_t b = at < len ? text[at] : 0x100u;
     const uint32_t ntag = tg.next(W.stamp, nf.nleaves);
     const uint32_t hnx = at < len ? look_holds(text, len, at + 1, nf) : 0;
+    const uint32_t nbx = at + 1 < len ? text[at + 1] : 0x100u;  // the next list's byte
     uint32_t nn = 0;
     bool stop = false, quit_now = false;
     for (uint32_t j0 = 0; j0 < nc && !stop; j0 += 64) {
@@ -238,7 +250,7 @@ __device__ void pike_one(const NfaDev &nf, Lists &W, TagGen &tg, const uint8_t *
         const uint32_t t = (uint32_t)__builtin_ctzll(ab);
         ab &= ab - 1;
         const uint32_t cid = nf.leaves[3 * W.leaf[c][j0 + t] + 1];
-        nn = append_closure(nf, cid, hnx, W.st[c][j0 + t], W.stamp, ntag, W.leaf[c ^ 1], W.st[c ^ 1], nn);
+        nn = append_closure(nf, cid, hnx, W.st[c][j0 + t], W.stamp, ntag, W.leaf[c ^ 1], W.st[c ^ 1], nn, nbx);
       }
     }
     if (quit_now) break;
