@@ -425,6 +425,28 @@ NfaOffsets add_nfa(Blob &b, const NfaTables &nt) {
   o.perlw = b.add(U::kPairs + 2 * U::kPerlW.first, (size_t)U::kPerlW.count * 8);
   o.save_off = b.add(nt.save_off.data(), nt.save_off.size() * 4);
   o.save_slot = b.add(nt.save_slot.data(), nt.save_slot.size() * 2);
+  // per closure (NfaDev::cl_info, 9 words): the bytes its Bytes leaves take
+  // (256 bits), then the looks every entry requires | 0x100 if it holds a
+  // Match leaf -- append_closure skips a closure none of whose entries can
+  // pass (the Pike VM's root closure at a position inside a word of \bfox\b)
+  const size_t ncl = nt.cl_off.empty() ? 0 : nt.cl_off.size() - 1;
+  std::vector<uint32_t> ci(ncl * 9, 0);
+  for (size_t c = 0; c < ncl; ++c) {
+    uint32_t need = 0xFF, match = 0;
+    for (uint32_t k = nt.cl_off[c]; k < nt.cl_off[c + 1]; ++k) {
+      const NfaEntry &e = nt.entries[k];
+      need &= e.cond_prev & 0xFF;
+      const NfaLeaf &l = nt.leaves[e.leaf];
+      if (l.kind == 0) {
+        for (uint32_t x = l.lo; x <= l.hi; ++x) ci[c * 9 + (x >> 5)] |= 1u << (x & 31);
+      } else {
+        match = 0x100;
+      }
+    }
+    if (nt.cl_off[c] == nt.cl_off[c + 1]) need = 0;
+    ci[c * 9 + 8] = need | match;
+  }
+  o.cl_info = b.add(ci.data(), ci.size() * 4);
   return o;
 }
 
@@ -436,6 +458,7 @@ void fix_nfa(NfaDev *n, uint8_t *base, const NfaOffsets &o, const NfaTables &nt,
   n->perlw_n = rure_amd_unicode::kPerlW.count;
   n->save_off = (const uint32_t *)(base + o.save_off);
   n->save_slot = (const uint16_t *)(base + o.save_slot);
+  n->cl_info = (const uint32_t *)(base + o.cl_info);
   n->nleaves = (uint32_t)nt.leaves.size();
   n->root = nt.root;
   n->nmatch = nt.nmatch;

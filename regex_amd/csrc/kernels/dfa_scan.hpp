@@ -235,6 +235,7 @@ struct NfaDev {
   uint32_t nleaves, root, nmatch;
   uint32_t anchored, single, looks, unicode_wb;
   uint32_t ncl_off, nentries;  // cl_off's and entries' lengths (the wave kernels stage them in LDS)
+  const uint32_t *cl_info;     // per closure: its Bytes leaves' bytes (8 words), needed looks | Match << 8
   const uint32_t *save_off;   // per entry: CSR offsets into save_slot (Saves on its path)
   const uint16_t *save_slot;
 };

@@ -131,6 +131,12 @@ struct Lists {
 // alternatives in the list instead of all of them.
 __device__ uint32_t append_closure(const NfaDev &nf, uint32_t cid, uint32_t holds, uint64_t stv, uint32_t *stamp,
                                    uint32_t tag, uint32_t *lleaf, uint64_t *lst, uint32_t cnt, uint32_t nb) {
+  if (nf.cl_info) {  // no entry can pass: skip the scan (uniform)
+    const uint32_t *ci = nf.cl_info + (size_t)cid * 9;
+    const uint32_t w = ci[8];
+    const bool byte_ok = nb <= 0xFF && ((ci[nb >> 5] >> (nb & 31)) & 1u);
+    if (((w & 0xFF) & ~holds) != 0 || (!(w & 0x100) && !byte_ok)) return cnt;
+  }
   const uint32_t o0 = nf.cl_off[cid], o1 = nf.cl_off[cid + 1];
   const uint32_t lane = lane_id();
   for (uint32_t k0 = o0; k0 < o1; k0 += 64) {
