@@ -124,3 +124,22 @@ def test_wave_sherlock_one_gib(cuda):
     exp = OracleRegex(re).find_iter(t)[:e["count"] - 1]
     got = [tuple(x) for x in m[:len(exp)].cpu().numpy().tolist()]
     assert got == exp
+
+
+@pytest.mark.parametrize("pat", [r"\b\w+n\b", r"\b", r"\B[a-z]{2}", r"\w+\b"])
+def test_wave_ragged(cuda, pat):
+    """A ragged batch (one unit per haystack): 400 haystacks of 0-2000 bytes,
+    sparse and dense non-ASCII, empty ones included."""
+    import torch
+    rng = random.Random(zlib.crc32(pat.encode()))
+    texts = [_text(rng.randrange(1 << 30), rng.choice([0, 1, 5, 64, 300, 2000]), rng.choice([0, 40, 3000]))
+             for _ in range(400)]
+    offs = np.zeros(len(texts) + 1, dtype=np.int64)
+    offs[1:] = np.cumsum([len(x) for x in texts])
+    buf = torch.from_numpy(np.frombuffer(b"".join(texts) + bytes(16), dtype=np.uint8).copy()).to(cuda)
+    re = R.Regex(pat)
+    counts, m = re.find_iter_batch(buf, offsets=torch.from_numpy(offs).to(cuda))
+    o = OracleRegex(re)
+    exp = [o.find_iter(x) for x in texts]
+    assert counts.cpu().numpy().tolist() == [len(x) for x in exp]
+    assert [tuple(x) for x in m.cpu().numpy().tolist()] == [s for x in exp for s in x]
