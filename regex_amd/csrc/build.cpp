@@ -447,6 +447,44 @@ NfaOffsets add_nfa(Blob &b, const NfaTables &nt) {
     ci[c * 9 + 8] = need | match;
   }
   o.cl_info = b.add(ci.data(), ci.size() * 4);
+  // Closures of more than 64 entries, bucketed by the next byte
+  // (NfaDev::cl_big / cl_boff / cl_sub): bucket x (256 = the end of the
+  // text) holds, in order, the entries whose leaf is a Match or takes x, with
+  // their same-leaf links renumbered -- append_closure then scans the few
+  // entries that can pass instead of all (the loop closure of Unicode \w+
+  // holds every alternative of the class).
+  std::vector<uint32_t> big(ncl, 0xFFFFFFFFu), boff;
+  std::vector<NfaEntry> sub;
+  for (size_t c = 0; c < ncl; ++c) {
+    const uint32_t k0 = nt.cl_off[c], k1 = nt.cl_off[c + 1];
+    if (k1 - k0 <= 64) continue;
+    // (bounded: a closure of wide leaves -- `.` takes every byte -- would
+    // copy each entry into hundreds of buckets)
+    size_t want = 0;
+    for (uint32_t k = k0; k < k1; ++k) {
+      const NfaLeaf &l = nt.leaves[nt.entries[k].leaf];
+      want += l.kind == 0 ? (size_t)l.hi - l.lo + 1 : 257;
+    }
+    if (want > 16 * (size_t)(k1 - k0) || sub.size() + want > (1u << 22)) continue;
+    big[c] = (uint32_t)(boff.size() / 258);
+    for (uint32_t x = 0; x <= 256; ++x) {
+      boff.push_back((uint32_t)sub.size());
+      const size_t base = sub.size();
+      for (uint32_t k = k0; k < k1; ++k) {
+        const NfaEntry &e = nt.entries[k];
+        const NfaLeaf &l = nt.leaves[e.leaf];
+        if (l.kind == 0 && (x > 255 || x < l.lo || x > l.hi)) continue;
+        uint32_t prev = 0;
+        for (size_t q = sub.size(); q > base; --q)
+          if (sub[q - 1].leaf == e.leaf) { prev = (uint32_t)(q - base); break; }
+        sub.push_back(NfaEntry{e.leaf, (e.cond_prev & 0xFF) | (prev << 8)});
+      }
+    }
+    boff.push_back((uint32_t)sub.size());
+  }
+  o.cl_big = b.add(big.data(), big.size() * 4);
+  o.cl_boff = boff.empty() ? o.cl_big : b.add(boff.data(), boff.size() * 4);
+  o.cl_sub = sub.empty() ? o.cl_big : b.add(sub.data(), sub.size() * 8);
   return o;
 }
 
@@ -459,6 +497,9 @@ void fix_nfa(NfaDev *n, uint8_t *base, const NfaOffsets &o, const NfaTables &nt,
   n->save_off = (const uint32_t *)(base + o.save_off);
   n->save_slot = (const uint16_t *)(base + o.save_slot);
   n->cl_info = (const uint32_t *)(base + o.cl_info);
+  n->cl_big = (const uint32_t *)(base + o.cl_big);
+  n->cl_boff = (const uint32_t *)(base + o.cl_boff);
+  n->cl_sub = (const uint2 *)(base + o.cl_sub);
   n->nleaves = (uint32_t)nt.leaves.size();
   n->root = nt.root;
   n->nmatch = nt.nmatch;

@@ -236,6 +236,9 @@ struct NfaDev {
   uint32_t anchored, single, looks, unicode_wb;
   uint32_t ncl_off, nentries;  // cl_off's and entries' lengths (the wave kernels stage them in LDS)
   const uint32_t *cl_info;     // per closure: its Bytes leaves' bytes (8 words), needed looks | Match << 8
+  const uint32_t *cl_big;      // per closure: its bucket set (closures of > 64 entries), else ~0
+  const uint32_t *cl_boff;     // per bucket set: 258 offsets into cl_sub (bytes 0-255, the text end)
+  const uint2 *cl_sub;         // the buckets' entries (as `entries`, same-leaf links within the bucket)
   const uint32_t *save_off;   // per entry: CSR offsets into save_slot (Saves on its path)
   const uint16_t *save_slot;
 };

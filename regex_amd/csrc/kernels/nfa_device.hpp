@@ -137,19 +137,29 @@ __device__ uint32_t append_closure(const NfaDev &nf, uint32_t cid, uint32_t hold
     const bool byte_ok = nb <= 0xFF && ((ci[nb >> 5] >> (nb & 31)) & 1u);
     if (((w & 0xFF) & ~holds) != 0 || (!(w & 0x100) && !byte_ok)) return cnt;
   }
-  const uint32_t o0 = nf.cl_off[cid], o1 = nf.cl_off[cid + 1];
+  uint32_t o0 = nf.cl_off[cid], o1 = nf.cl_off[cid + 1];
+  const uint2 *E = nf.entries;
+  if (nf.cl_big && nb <= 0x100) {  // a big closure: only the next byte's bucket
+    const uint32_t bi = nf.cl_big[cid];
+    if (bi != 0xFFFFFFFFu) {
+      const uint32_t *bo = nf.cl_boff + (size_t)bi * 258;
+      o0 = bo[nb];
+      o1 = bo[nb + 1];
+      E = nf.cl_sub;
+    }
+  }
   const uint32_t lane = lane_id();
   for (uint32_t k0 = o0; k0 < o1; k0 += 64) {
     const uint32_t k = k0 + lane;
     bool pass = false;
     uint32_t leaf = 0;
     if (k < o1) {
-      uint2 e = nf.entries[k];
+      uint2 e = E[k];
       leaf = e.x;
       pass = ((e.y & 0xFF) & ~holds) == 0;
       uint32_t pv = e.y >> 8;
       while (pass && pv) {  // an earlier entry of the same leaf in this closure wins
-        uint2 q = nf.entries[o0 + pv - 1];
+        uint2 q = E[o0 + pv - 1];
         if (((q.y & 0xFF) & ~holds) == 0) pass = false;
         pv = q.y >> 8;
       }

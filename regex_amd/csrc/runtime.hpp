@@ -207,7 +207,7 @@ struct IterBufs {
   }
 };
 
-struct NfaOffsets { size_t leaves, cl_off, entries, perlw, save_off, save_slot, cl_info; };
+struct NfaOffsets { size_t leaves, cl_off, entries, perlw, save_off, save_slot, cl_info, cl_big, cl_boff, cl_sub; };
 struct LitOffsets { size_t bytes, off; uint32_t n; };
 
 }  // namespace rt
