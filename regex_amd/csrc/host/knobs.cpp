@@ -20,7 +20,7 @@ const char *const kNames[kN] = {
     "ascii_shadow", "fb",        "prefix",     "big",        "big_bytes",  "lazy",       "lazy_rows",
     "lines",      "split",       "suffix_long", "suffix_iter", "iter_looks", "iter_chunk", "iter_lanes",
     "iter_bs",    "long_lanes",  "core_bs",    "core_lds",   "core_prof",  "scratch_cap", "timing",
-    "replace_generic", "chain_seq", "shadow_sync", "iter_wave", "wave_cu", "wave_split", "wave_tables",
+    "replace_generic", "chain_seq", "shadow_sync", "iter_wave", "wave_cu", "wave_split", "wave_tables", "wave_lds",
 };
 
 std::atomic<long long> g_val[kN];

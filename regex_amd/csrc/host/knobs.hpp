@@ -44,6 +44,7 @@ enum class Knob : int {
   WaveCu,          // the wave-served units' waves per CU, their Pike VM lists in global scratch
   WaveSplit,       // 0: those waves' stamps in scratch too, not in the LDS
   WaveTables,      // 0: no NFA tables staged in the LDS for those waves
+  WaveLds,         // 1: those waves' whole working set in the LDS, however few waves fit
   kCount
 };
 

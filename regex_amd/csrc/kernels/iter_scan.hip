@@ -2863,7 +2863,7 @@ static hipError_t iter_post(const BatchDev &b, const Geo &g, uint64_t nunits, co
   constexpr int kWpb = 8;
   uint32_t mode;
   int wcu, wpb = 1;
-  if (wb <= kNfaLdsMax && kw <= 0 && lds_cu >= 16) {
+  if (wb <= kNfaLdsMax && kw <= 0 && (lds_cu >= 16 || knob(Knob::WaveLds) == 1)) {
     mode = kWaveLds, wcu = lds_cu;
   } else if (kw <= 0 && knob(Knob::WaveTables) != 0 && tb + kWpb * sb <= 160u * 1024u) {
     mode = kWaveTables, wcu = kWpb, wpb = kWpb;
