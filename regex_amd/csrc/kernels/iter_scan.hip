@@ -2070,11 +2070,11 @@ __device__ __forceinline__ void wave_setup(const NfaDev &nf0, uint8_t *lds_mem, 
 template <bool STEP>
 __global__ __launch_bounds__(512) void iter_wspec_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f,
                                                         RevDfaDev r, NfaDev nf, Unit *units, uint64_t *slots,
-                                                        uint32_t *counts, uint32_t *dirty, uint8_t *scratch, uint32_t split) {  // split: kWave*
+                                                        uint32_t *counts, uint32_t *dirty, uint8_t *scratch, uint32_t wmode) {  // wmode: kWave*
   if (gated_off(b) || !(__atomic_load_n(dirty, __ATOMIC_RELAXED) & 2u)) return;  // nothing pending
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_mem[];
   WaveSetup S;
-  wave_setup(nf, lds_mem, scratch, split, S);
+  wave_setup(nf, lds_mem, scratch, wmode, S);
   pike::TagGen tg;
   const WaveCtx wc{&S.nf, &S.W, &tg};
   const uint32_t lane = pike::lane_id();
@@ -2130,11 +2130,11 @@ __global__ __launch_bounds__(512) void iter_wspec_kernel(BatchDev b, Geo g, uint
 __global__ __launch_bounds__(512) void iter_wfix_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
                                                        NfaDev nf, Unit *units, uint32_t *counts, const uint64_t *slots,
                                                        uint64_t *queue, unsigned long long *qlen, const uint32_t *dirty,
-                                                       uint8_t *scratch, uint32_t split) {  // split: kWave*
+                                                       uint8_t *scratch, uint32_t wmode) {  // wmode: kWave*
   if (gated_off(b) || *dirty == 0) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_mem[];
   WaveSetup S;
-  wave_setup(nf, lds_mem, scratch, split, S);
+  wave_setup(nf, lds_mem, scratch, wmode, S);
   pike::TagGen tg;
   const WaveCtx wc{&S.nf, &S.W, &tg};
   for (uint64_t u = S.wave; u + 1 < nunits; u += S.nwaves) {
@@ -2153,11 +2153,11 @@ __global__ __launch_bounds__(512) void iter_wfix_kernel(BatchDev b, Geo g, uint6
 // The walker with the whole wave (one block of 64).
 __global__ __launch_bounds__(64) void iter_wwalk_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
                                                         NfaDev nf, Unit *units, uint32_t *counts, const uint64_t *slots,
-                                                        uint64_t *queue, unsigned long long *qlen, uint8_t *scratch, uint32_t split) {  // split: kWave*
+                                                        uint64_t *queue, unsigned long long *qlen, uint8_t *scratch, uint32_t wmode) {  // wmode: kWave*
   if (gated_off(b) || blockIdx.x != 0) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_mem[];
   WaveSetup S;
-  wave_setup(nf, lds_mem, scratch, split, S);
+  wave_setup(nf, lds_mem, scratch, wmode, S);
   pike::TagGen tg;
   const WaveCtx wc{&S.nf, &S.W, &tg};
   walk_body(b, g, nunits, f, r, units, counts, slots, queue, qlen, &wc);
@@ -2166,11 +2166,11 @@ __global__ __launch_bounds__(64) void iter_wwalk_kernel(BatchDev b, Geo g, uint6
 // emit_body's re-runs of U_QUIT units (from the unit's entry, cnt matches).
 __global__ __launch_bounds__(512) void iter_wemit_kernel(BatchDev b, Geo g, uint64_t nunits, FwdDfaDev f, RevDfaDev r,
                                                         NfaDev nf, const Unit *units, const uint64_t *off,
-                                                        uint64_t *out, uint64_t cap, uint8_t *scratch, uint32_t split) {  // split: kWave*
+                                                        uint64_t *out, uint64_t cap, uint8_t *scratch, uint32_t wmode) {  // wmode: kWave*
   if (gated_off(b)) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_mem[];
   WaveSetup S;
-  wave_setup(nf, lds_mem, scratch, split, S);
+  wave_setup(nf, lds_mem, scratch, wmode, S);
   pike::TagGen tg;
   const WaveCtx wc{&S.nf, &S.W, &tg};
   const uint64_t obase = off[0];
